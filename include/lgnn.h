@@ -1,0 +1,153 @@
+/*
+ * lgnn.h — C ABI of the MI355X (gfx950) lesion-graph message-passing library (liblgnn.so).
+ *
+ * This is the drop-in boundary for the reference's hot path: everything beneath
+ * `self.model(data.x, edge_index, data.batch)` (reference src/lesion_gnn/models/gin.py:64,
+ * src/lesion_gnn/models/gat.py:92), i.e. the work PyG 2.5.1 + torch_scatter + torch_sparse do for
+ * GINConv / GATConv / GCNConv / global_mean_pool (reference call sites gin.py:9,23,31,33 and
+ * gat.py:9,31,51,56). Each entry point names the reference interface it replaces.
+ *
+ * Conventions (all entry points):
+ *   - every pointer is a DEVICE pointer (hipMalloc / torch caching allocator) unless marked host;
+ *   - `stream` is a hipStream_t passed as void*; work is enqueued asynchronously on it;
+ *   - nothing is allocated inside; scratch comes from caller-provided workspaces;
+ *   - return 0 (LGNN_OK) or a negative LGNN_E* code / positive hipError_t; never throws;
+ *   - no host synchronisation inside any call, so every call is hipGraph-capturable;
+ *   - fp32 storage, fp32 accumulate; index arrays int32 (CSR) or int64 (edge_index / batch, as
+ *     PyG hands them over).
+ */
+#ifndef LGNN_H
+#define LGNN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LGNN_ABI_VERSION 1
+
+#define LGNN_OK 0
+#define LGNN_EINVAL (-22)
+#define LGNN_ENOSPC (-28)
+
+/* self-loop handling of the graph build (which PyG utility the conv applies to edge_index) */
+#define LGNN_LOOPS_KEEP 0      /* GINConv: edges used as given (KNN loop=True self pairs kept) */
+#define LGNN_LOOPS_REMAINING 1 /* GCNConv gcn_norm: add_remaining_self_loops (one loop/node, last) */
+#define LGNN_LOOPS_READD 2     /* GATConv: remove_self_loops + add_self_loops (one loop/node, last) */
+
+/* edge weights written by the graph build */
+#define LGNN_NORM_NONE 0 /* w = 1 */
+#define LGNN_NORM_GCN 1  /* w_ij = deg_j^-1/2 * deg_i^-1/2, deg = in-degree incl. loop, inf -> 0 */
+
+/* activation fused into the node-tile kernels */
+#define LGNN_ACT_NONE 0
+#define LGNN_ACT_ELU 1
+
+/* upstream-gradient source of lgnn_node_linear_bwd */
+#define LGNN_GRAD_DIRECT 0   /* dY[M,N] as given */
+#define LGNN_GRAD_POOL 1     /* dY[i] = dP[batch[i]] (/ count for mean pooling) */
+#define LGNN_GRAD_TRANSPOSE 2 /* dY[i] = tself*dS[i] + sum_{e in T(i)} tw_e dS[tidx_e] */
+
+int lgnn_abi_version(void);
+const char* lgnn_status_string(int status);
+
+/* ---------------------------------------------------------------------------------------------
+ * Graph structure.
+ * Replaces: PyG gcn_norm / add_remaining_self_loops (GCNConv), remove_self_loops+add_self_loops
+ * (GATConv, reference gat.py:31), torch_sparse ToSparseTensor CSR (reference
+ * datasets/datamodule.py:44-45) — i.e. the per-forward edge_index preprocessing.
+ *
+ * Builds, from edge_index int64 [2, E] (row 0 = source j, row 1 = target i, any order), a CSR
+ * grouped by TARGET (rowptr[N+1], col[cap] = source, w[cap]) and optionally its transpose grouped
+ * by SOURCE (tptr[N+1], tidx[cap] = target, tw[cap]), cap = E + N. Within a row entries keep
+ * edge_index order; with LOOPS_REMAINING / LOOPS_READD the node's single self loop is last (as
+ * PyG appends loops after the edge list). Invalid indices (<0 or >= N) are dropped and counted in
+ * *err_count (device int, may be NULL). Workspace size: lgnn_graph_workspace_bytes.
+ * ------------------------------------------------------------------------------------------- */
+size_t lgnn_graph_workspace_bytes(int64_t num_nodes, int64_t num_edges);
+int lgnn_graph_build(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes, int loops,
+                     int norm, int32_t* rowptr, int32_t* col, float* w, int32_t* tptr,
+                     int32_t* tidx, float* tw, int32_t* err_count, void* workspace,
+                     size_t workspace_bytes, void* stream);
+
+/* Graph offsets from a sorted PyG `batch` vector (Batch.ptr): ptr[g] = first node of graph g,
+ * ptr[B] = M. Replaces the count/offset half of PyG scatter(reduce='mean') over `batch`. */
+int lgnn_batch_ptr(const int64_t* batch, int64_t num_nodes, int64_t num_graphs, int32_t* ptr,
+                   void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Node-tile fused aggregate + linear (+bias, +activation), forward.
+ * Replaces: nn.Linear (reference gin.py:21 in_proj), GCNConv.lin + propagate + bias
+ * (A_hat (X W^T) == (A_hat X) W^T), GINConv aggregate + first MLP Linear (reference gin.py:23),
+ * with F.elu (gin.py:31) fused.
+ *
+ *   Y[M,N] = act( P(X) W^T + b ),  W [N,K] row-major (torch Linear layout), b [N] or NULL,
+ *   P(X) = X                                   if rowptr == NULL,
+ *   P(X)_i = sum_{e in row i} w_e X[col_e] + self_scale * X_i   otherwise (w == NULL: w_e = 1).
+ * ------------------------------------------------------------------------------------------- */
+int lgnn_node_linear_fwd(const float* X, int64_t M, int K, const int32_t* rowptr,
+                         const int32_t* col, const float* w, float self_scale, const float* W,
+                         const float* b, int N, int act, float* Y, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Node-tile fused backward of lgnn_node_linear_fwd.
+ * Replaces: autograd of nn.Linear / GCNConv / GINConv-first-Linear + F.elu + the scatter-add
+ * backward (index_select / index_add_) and the global_mean_pool backward (reference gin.py:33).
+ *
+ *   G   = upstream gradient by grad_mode (LGNN_GRAD_*):
+ *           DIRECT: dY[M,N];  POOL: dY[batch_i] (dY is [B,N]; mean: / (ptr[g+1]-ptr[g]));
+ *           TRANSPOSE: tself*dY[i] + sum_{e in tptr row i} tw_e dY[tidx_e] (tw NULL: 1)
+ *   dZ  = G ⊙ act'(H),  H = this layer's saved forward output [M,N] (ELU: H>0 ? 1 : H+1)
+ *   dW_partial[g] (+)= dZ^T P(X) over the row tiles owned by partial slot g  ([P][N][K])
+ *   db_partial[g] (+)= colsum(dZ)                                          ([P][N], may be NULL)
+ *   dXpre = dZ W  [M,K]  (may be NULL)
+ * The P partial slots are summed by lgnn_reduce_partials (deterministic order).
+ * num_partials: lgnn_bwd_num_partials(M, N, K) — pass that value and size slabs with it.
+ * ------------------------------------------------------------------------------------------- */
+int lgnn_bwd_num_partials(int64_t M, int N, int K);
+int lgnn_node_linear_bwd(int grad_mode, const float* dY, const int64_t* batch, const int32_t* gptr,
+                         int pool_mean, const int32_t* tptr, const int32_t* tidx, const float* tw,
+                         float tself, const float* H, int act, const float* X, int64_t M, int K,
+                         const int32_t* rowptr, const int32_t* col, const float* w,
+                         float self_scale, const float* W, int N, float* dXpre,
+                         float* dW_partial, float* db_partial, int num_partials, void* stream);
+
+/* out[i] = sum_{p < P} partial[p*len + i], fixed order (bitwise reproducible). */
+int lgnn_reduce_partials(const float* partial, int num_partials, int64_t len, float* out,
+                         void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Sparse aggregation alone (no linear): Y_i = self_scale*X_i + sum_{e in row i} w_e X[col_e].
+ * Replaces: torch_sparse spmm(adj_t, x, 'sum') / PyG propagate(aggr='add') (GINConv, and the
+ * transposed pass of every conv backward when called with the transpose CSR).
+ * ------------------------------------------------------------------------------------------- */
+int lgnn_spmm(const int32_t* rowptr, const int32_t* col, const float* w, float self_scale,
+              const float* X, int64_t M, int D, float* Y, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Readout: per-graph segmented pool fused with the out_proj Linear.
+ * Replaces: global_mean_pool / global_add_pool (reference gin.py:33, gat.py:56) + out_proj
+ * (gin.py:25, gat.py:46).
+ *   pooled[B,D] = sum_{i in graph g} H_i (/ count if mean; empty graph -> 0)
+ *   logits[B,C] = pooled Wout^T + bout        (Wout may be NULL: pool only, logits unused)
+ * ------------------------------------------------------------------------------------------- */
+int lgnn_pool_head_fwd(const float* H, const int32_t* gptr, int64_t B, int D, int pool_mean,
+                       const float* Wout, const float* bout, int C, float* pooled,
+                       float* logits, void* stream);
+
+/* Backward of lgnn_pool_head_fwd's Linear part:
+ *   dpooled = dlogits Wout;  dWout = dlogits^T pooled;  dbout = colsum(dlogits). */
+int lgnn_pool_head_bwd(const float* dlogits, const float* pooled, int64_t B, int D,
+                       const float* Wout, int C, float* dpooled, float* dWout, float* dbout,
+                       void* stream);
+
+/* Backward of a bare segmented pool: dH_i = dpooled[batch_i] (/ count if mean). */
+int lgnn_pool_bwd(const float* dpooled, const int64_t* batch, const int32_t* gptr, int64_t M,
+                  int D, int pool_mean, float* dH, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LGNN_H */

@@ -1,0 +1,97 @@
+"""ctypes binding of liblgnn.so (the C ABI declared in include/lgnn.h).
+
+The library is loaded from this package directory only (in-tree build, `make` or
+``__graft_entry__.build()``). There is no fallback: if the library or a GPU is missing, every
+product op raises. torch is imported first so that the HIP runtime torch ships
+(libamdhip64.so.7) is the one the library binds to — one runtime per process.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblgnn.so")
+
+LGNN_LOOPS_KEEP, LGNN_LOOPS_REMAINING, LGNN_LOOPS_READD = 0, 1, 2
+LGNN_NORM_NONE, LGNN_NORM_GCN = 0, 1
+LGNN_ACT_NONE, LGNN_ACT_ELU = 0, 1
+LGNN_GRAD_DIRECT, LGNN_GRAD_POOL, LGNN_GRAD_TRANSPOSE = 0, 1, 2
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int
+I64 = ctypes.c_int64
+F32 = ctypes.c_float
+SZ = ctypes.c_size_t
+
+# name -> (restype, argtypes); mirrors include/lgnn.h exactly
+SIGNATURES: dict[str, tuple] = {
+    "lgnn_abi_version": (I32, []),
+    "lgnn_status_string": (ctypes.c_char_p, [I32]),
+    "lgnn_graph_workspace_bytes": (SZ, [I64, I64]),
+    "lgnn_graph_build": (I32, [P, I64, I64, I32, I32, P, P, P, P, P, P, P, P, SZ, P]),
+    "lgnn_batch_ptr": (I32, [P, I64, I64, P, P]),
+    "lgnn_node_linear_fwd": (I32, [P, I64, I32, P, P, P, F32, P, P, I32, I32, P, P]),
+    "lgnn_bwd_num_partials": (I32, [I64, I32, I32]),
+    "lgnn_node_linear_bwd": (I32, [I32, P, P, P, I32, P, P, P, F32, P, I32, P, I64, I32,
+                                   P, P, P, F32, P, I32, P, P, P, I32, P]),
+    "lgnn_reduce_partials": (I32, [P, I32, I64, P, P]),
+    "lgnn_spmm": (I32, [P, P, P, F32, P, I64, I32, P, P]),
+    "lgnn_pool_head_fwd": (I32, [P, P, I64, I32, I32, P, P, I32, P, P, P]),
+    "lgnn_pool_head_bwd": (I32, [P, P, I64, I32, P, I32, P, P, P, P]),
+    "lgnn_pool_bwd": (I32, [P, P, P, I64, I32, I32, P, P]),
+}
+
+ABI_VERSION = 1
+
+_lib = None
+
+
+class LgnnError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load and type the library (no GPU needed to load)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise LgnnError(f"{LIB_PATH} is missing: build it with `make` or __graft_entry__.build()")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.lgnn_abi_version() != ABI_VERSION:
+        raise LgnnError("liblgnn.so ABI version mismatch; rebuild")
+    _lib = lib
+    return lib
+
+
+def check(status: int, what: str) -> None:
+    if status != 0:
+        msg = load().lgnn_status_string(status)
+        raise LgnnError(f"{what} failed: {status} ({msg.decode() if msg else '?'})")
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def stream(device: torch.device | None = None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_gpu(*tensors: torch.Tensor) -> None:
+    """The product path is HIP-only: refuse CPU tensors instead of silently falling back."""
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise LgnnError("lesion_gnn_amd ops run on the GPU only (HIP kernels); got a CPU "
+                            "tensor. There is no CPU fallback by design.")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(load(), name)(*args), name)

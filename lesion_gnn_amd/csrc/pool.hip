@@ -1,0 +1,160 @@
+// Readout kernels: per-graph segmented pool (global_mean_pool / global_add_pool) fused with the
+// out_proj Linear, and their backward.
+//
+// Replaces (reference): global_mean_pool(x, batch) gin.py:33 / gat.py:56 (PyG scatter mean =
+// sum / clamp(count, 1)), global_add_pool (NEW), out_proj nn.Linear gin.py:25.
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+// One wave per graph. Node rows of graph g are contiguous ([ptr[g], ptr[g+1])); lanes stride the
+// feature dimension; rows are summed in node order (PyG scatter_add_ order). Then each class logit
+// is a wave dot product.
+__global__ __launch_bounds__(NT) void k_pool_head_fwd(const float* __restrict__ H,
+                                                      const int32_t* __restrict__ gptr, int64_t B,
+                                                      int D, int pool_mean,
+                                                      const float* __restrict__ Wout,
+                                                      const float* __restrict__ bout, int C,
+                                                      float* __restrict__ pooled,
+                                                      float* __restrict__ logits) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t g = (int64_t)blockIdx.x * 4 + wave;
+  if (g >= B) return;
+  const int n0 = gptr[g], n1 = gptr[g + 1];
+  const int cnt = n1 - n0;
+  const float denom = (float)(cnt > 0 ? cnt : 1);
+  // up to 8 feature strips of 64 lanes in registers (D <= 512)
+  float p[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int d = q * 64 + lane;
+    float s = 0.f;
+    if (d < D) {
+      int i = n0;
+      for (; i + 4 <= n1; i += 4) {
+        const float v0 = H[(int64_t)i * D + d], v1 = H[(int64_t)(i + 1) * D + d];
+        const float v2 = H[(int64_t)(i + 2) * D + d], v3 = H[(int64_t)(i + 3) * D + d];
+        s += v0;
+        s += v1;
+        s += v2;
+        s += v3;
+      }
+      for (; i < n1; ++i) s += H[(int64_t)i * D + d];
+      if (pool_mean) s = s / denom;
+      pooled[g * D + d] = s;
+    }
+    p[q] = s;
+  }
+  if (!Wout) return;
+  for (int c = 0; c < C; ++c) {
+    float acc = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int d = q * 64 + lane;
+      if (d < D) acc = fmaf(p[q], Wout[(int64_t)c * D + d], acc);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (lane == 0) logits[g * C + c] = acc + (bout ? bout[c] : 0.f);
+  }
+}
+
+// dpooled[g][d] = sum_c dlogits[g][c] Wout[c][d]
+__global__ __launch_bounds__(NT) void k_head_bwd_dp(const float* __restrict__ dlogits, int64_t B,
+                                                    int D, const float* __restrict__ Wout, int C,
+                                                    float* __restrict__ dpooled) {
+  const int64_t idx = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (idx >= B * D) return;
+  const int64_t g = idx / D;
+  const int d = (int)(idx % D);
+  float acc = 0.f;
+  for (int c = 0; c < C; ++c) acc = fmaf(dlogits[g * C + c], Wout[(int64_t)c * D + d], acc);
+  dpooled[idx] = acc;
+}
+
+// dWout[c][d] = sum_g dlogits[g][c] pooled[g][d]; dbout[c] = sum_g dlogits[g][c].
+// block = (class c, 64-wide feature strip); 4 waves split g (w, w+4, ...), fixed-order combine.
+__global__ __launch_bounds__(NT) void k_head_bwd_dw(const float* __restrict__ dlogits,
+                                                    const float* __restrict__ pooled, int64_t B,
+                                                    int D, int C, float* __restrict__ dWout,
+                                                    float* __restrict__ dbout) {
+  __shared__ float red[4][65];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.y;
+  const int d = blockIdx.x * 64 + lane;
+  float s = 0.f, sb = 0.f;
+  for (int64_t g = wave; g < B; g += 4) {
+    const float dl = dlogits[g * C + c];
+    if (d < D) s = fmaf(dl, pooled[g * D + d], s);
+    sb += dl;
+  }
+  red[wave][lane] = s;
+  if (lane == 0) red[wave][64] = sb;
+  __syncthreads();
+  if (wave == 0) {
+    if (d < D) dWout[(int64_t)c * D + d] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    if (lane == 0 && blockIdx.x == 0 && dbout)
+      dbout[c] = ((red[0][64] + red[1][64]) + red[2][64]) + red[3][64];
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_pool_bwd(const float* __restrict__ dp,
+                                                 const int64_t* __restrict__ batch,
+                                                 const int32_t* __restrict__ gptr, int64_t M,
+                                                 int D, int pool_mean, float* __restrict__ dH) {
+  const int64_t idx = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (idx >= M * D) return;
+  const int64_t i = idx / D;
+  const int d = (int)(idx % D);
+  const int64_t g = batch[i];
+  float v = dp[g * D + d];
+  if (pool_mean) {
+    const int cnt = gptr[g + 1] - gptr[g];
+    v = v / (float)(cnt > 0 ? cnt : 1);
+  }
+  dH[idx] = v;
+}
+
+}  // namespace
+
+extern "C" int lgnn_pool_head_fwd(const float* H, const int32_t* gptr, int64_t B, int D,
+                                  int pool_mean, const float* Wout, const float* bout, int C,
+                                  float* pooled, float* logits, void* stream) {
+  if (B < 0 || D <= 0 || D > 512 || !gptr || !pooled) return LGNN_EINVAL;
+  if (Wout && (C <= 0 || !logits)) return LGNN_EINVAL;
+  if (B == 0) return LGNN_OK;
+  hipLaunchKernelGGL(k_pool_head_fwd, dim3((unsigned)((B + 3) / 4)), dim3(NT), 0,
+                     as_stream(stream), H, gptr, B, D, pool_mean, Wout, bout, C, pooled, logits);
+  LGNN_LAUNCH_CHECK();
+  return LGNN_OK;
+}
+
+extern "C" int lgnn_pool_head_bwd(const float* dlogits, const float* pooled, int64_t B, int D,
+                                  const float* Wout, int C, float* dpooled, float* dWout,
+                                  float* dbout, void* stream) {
+  if (B < 0 || D <= 0 || C <= 0 || !dlogits || !pooled || !Wout) return LGNN_EINVAL;
+  hipStream_t s = as_stream(stream);
+  if (dpooled && B > 0) {
+    hipLaunchKernelGGL(k_head_bwd_dp, dim3((unsigned)((B * D + NT - 1) / NT)), dim3(NT), 0, s,
+                       dlogits, B, D, Wout, C, dpooled);
+    LGNN_LAUNCH_CHECK();
+  }
+  if (dWout) {
+    hipLaunchKernelGGL(k_head_bwd_dw, dim3((unsigned)((D + 63) / 64), (unsigned)C), dim3(NT), 0, s,
+                       dlogits, pooled, B, D, C, dWout, dbout);
+    LGNN_LAUNCH_CHECK();
+  }
+  return LGNN_OK;
+}
+
+extern "C" int lgnn_pool_bwd(const float* dpooled, const int64_t* batch, const int32_t* gptr,
+                             int64_t M, int D, int pool_mean, float* dH, void* stream) {
+  if (M < 0 || D <= 0 || !dpooled || !batch || !gptr || !dH) return LGNN_EINVAL;
+  if (M == 0) return LGNN_OK;
+  hipLaunchKernelGGL(k_pool_bwd, dim3((unsigned)((M * D + NT - 1) / NT)), dim3(NT), 0,
+                     as_stream(stream), dpooled, batch, gptr, M, D, pool_mean, dH);
+  LGNN_LAUNCH_CHECK();
+  return LGNN_OK;
+}

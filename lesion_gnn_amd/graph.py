@@ -1,0 +1,107 @@
+"""Batched-graph structure on the GPU: CSR by target + CSR by source, Batch.ptr.
+
+Replaces the per-forward edge_index preprocessing PyG does inside each conv (gcn_norm for
+GCNConv, remove/add_self_loops for GATConv) and torch_sparse's adj_t CSR
+(reference src/lesion_gnn/datasets/datamodule.py:44-45). A `Graph` is built once per forward and
+shared by every conv of the model; it is also accepted in place of `edge_index` (the analogue of
+the reference's SparseTensor `adj_t` input, gin.py:59-62).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+
+KIND = {
+    # kind: (loops mode, norm mode, self_scale of the aggregation)
+    "gcn": (_lib.LGNN_LOOPS_REMAINING, _lib.LGNN_NORM_GCN),
+    "gin": (_lib.LGNN_LOOPS_KEEP, _lib.LGNN_NORM_NONE),
+    "gat": (_lib.LGNN_LOOPS_READD, _lib.LGNN_NORM_NONE),
+}
+
+
+@dataclass
+class Csr:
+    rowptr: torch.Tensor  # int32 [N+1]
+    col: torch.Tensor     # int32 [cap] source of each entry, grouped by target
+    w: torch.Tensor       # fp32 [cap]
+    tptr: torch.Tensor    # int32 [N+1]
+    tidx: torch.Tensor    # int32 [cap] target of each entry, grouped by source
+    tw: torch.Tensor      # fp32 [cap]
+    err: torch.Tensor     # int32 [1] count of dropped out-of-range edges
+
+
+class Graph:
+    """edge_index [2, E] int64 (source, target) + sorted `batch` [N] -> device CSR views."""
+
+    def __init__(self, edge_index: torch.Tensor, num_nodes: int, batch: torch.Tensor | None = None,
+                 num_graphs: int | None = None):
+        _lib.require_gpu(edge_index)
+        if edge_index.dim() != 2 or edge_index.size(0) != 2:
+            raise ValueError("edge_index must be [2, E]")
+        self.edge_index = edge_index.to(torch.int64).contiguous()
+        self.num_nodes = int(num_nodes)
+        self.device = edge_index.device
+        self._csr: dict[str, Csr] = {}
+        self.batch = None
+        self.gptr = None
+        self.num_graphs = None
+        if batch is not None:
+            self.set_batch(batch, num_graphs)
+
+    @property
+    def num_edges(self) -> int:
+        return self.edge_index.size(1)
+
+    def set_batch(self, batch: torch.Tensor, num_graphs: int | None = None) -> None:
+        _lib.require_gpu(batch)
+        if batch.numel() != self.num_nodes:
+            raise ValueError("batch must have one entry per node")
+        self.batch = batch.to(torch.int64).contiguous()
+        if num_graphs is None:
+            # PyG: int(batch.max()) + 1 (a device->host read; pass num_graphs to avoid it)
+            num_graphs = int(self.batch[-1].item()) + 1 if self.num_nodes > 0 else 0
+        self.num_graphs = int(num_graphs)
+        self.gptr = torch.empty(self.num_graphs + 1, dtype=torch.int32, device=self.device)
+        _lib.call("lgnn_batch_ptr", _lib.ptr(self.batch), self.num_nodes, self.num_graphs,
+                  _lib.ptr(self.gptr), _lib.stream(self.device))
+
+    def csr(self, kind: str) -> Csr:
+        if kind in self._csr:
+            return self._csr[kind]
+        loops, norm = KIND[kind]
+        n, e = self.num_nodes, self.num_edges
+        cap = e + n
+        dev = self.device
+        i32 = dict(dtype=torch.int32, device=dev)
+        c = Csr(
+            rowptr=torch.empty(n + 1, **i32), col=torch.empty(cap, **i32),
+            w=torch.empty(cap, dtype=torch.float32, device=dev),
+            tptr=torch.empty(n + 1, **i32), tidx=torch.empty(cap, **i32),
+            tw=torch.empty(cap, dtype=torch.float32, device=dev),
+            err=torch.zeros(1, **i32),
+        )
+        lib = _lib.load()
+        ws_bytes = lib.lgnn_graph_workspace_bytes(n, e)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        _lib.call("lgnn_graph_build", _lib.ptr(self.edge_index), e, n, loops, norm,
+                  _lib.ptr(c.rowptr), _lib.ptr(c.col), _lib.ptr(c.w), _lib.ptr(c.tptr),
+                  _lib.ptr(c.tidx), _lib.ptr(c.tw), _lib.ptr(c.err), _lib.ptr(ws), ws_bytes,
+                  _lib.stream(dev))
+        self._csr[kind] = c
+        return c
+
+    def dropped_edges(self, kind: str) -> int:
+        """Number of edges with an out-of-range index (synchronises)."""
+        return int(self.csr(kind).err.item())
+
+
+def as_graph(edge_index, num_nodes: int, batch=None, num_graphs=None) -> Graph:
+    if isinstance(edge_index, Graph):
+        g = edge_index
+        if batch is not None and g.batch is None:
+            g.set_batch(batch, num_graphs)
+        return g
+    return Graph(edge_index, num_nodes, batch, num_graphs)

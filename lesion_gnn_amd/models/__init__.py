@@ -1,0 +1,16 @@
+"""Model registry (reference src/lesion_gnn/models/__init__.py:10,22-35: isinstance dispatch on
+the config type), restricted to the message-passing families of the hot path."""
+from .base import (BaseModelConfig, BaseModule, LossType, LRSchedulerConfig, OptimizerAlgo,
+                   OptimizerConfig)
+from .gcn import GCN, GCNConfig, GCNModule
+
+ModelConfig = GCNConfig
+
+__all__ = ["GCN", "GCNConfig", "GCNModule", "BaseModule", "BaseModelConfig", "OptimizerConfig",
+           "OptimizerAlgo", "LossType", "LRSchedulerConfig", "ModelConfig", "get_model"]
+
+
+def get_model(config) -> BaseModule:
+    if isinstance(config, GCNConfig):
+        return GCNModule(config)
+    raise ValueError(f"Unknown model config type {type(config)}")

@@ -1,0 +1,111 @@
+"""The boundary caller: loss + step around `self.model(x, edge_index, batch)`.
+
+Mirrors the reference's BaseLightningModule contract (src/lesion_gnn/models/base.py:82-233) for
+the parts on the hot path — criterion selection (:88-96), the regression clamp of the
+XLightning.forward methods (gin.py:58-69, gat.py:86-97), training_step (:196-201) and
+configure_optimizers (:162-188) — as a plain nn.Module (Lightning, torchmetrics and W&B are not
+part of this build; metrics/logging are out of scope).
+"""
+from __future__ import annotations
+
+import dataclasses
+from enum import Enum
+from typing import Any, Literal
+
+import torch
+import torch.nn as nn
+
+from ..utils import ClassWeights
+from ..utils.placeholder import Placeholder
+
+
+class OptimizerAlgo(str, Enum):
+    ADAM = "adam"
+    ADAMW = "adamw"
+    SGD = "sgd"
+
+
+class LossType(str, Enum):
+    MSE = "MSE"
+    CE = "CE"
+    SMOOTH_L1 = "SmoothL1"
+
+
+@dataclasses.dataclass(kw_only=True)
+class LRSchedulerConfig:
+    name: str
+    kwargs: dict[str, Any]
+    monitor: str = "val_loss"
+    interval: Literal["epoch", "step"] = "epoch"
+    frequency: int = 1
+
+
+@dataclasses.dataclass(kw_only=True)
+class OptimizerConfig:
+    lr: float = 0.001
+    lr_scheduler: LRSchedulerConfig | None = None
+    weight_decay: float = 0.01
+    algo: OptimizerAlgo = OptimizerAlgo.ADAMW
+    loss_type: LossType = LossType.CE
+    class_weights_mode: ClassWeights = ClassWeights.UNIFORM
+    class_weights: Placeholder[torch.Tensor] = dataclasses.field(default_factory=Placeholder,
+                                                                 init=False)
+
+
+@dataclasses.dataclass(kw_only=True)
+class BaseModelConfig:
+    num_classes: Placeholder[int] = dataclasses.field(default_factory=Placeholder, init=False)
+    optimizer: OptimizerConfig
+    name: str
+
+
+def make_criterion(cfg: OptimizerConfig) -> nn.Module:
+    kind = LossType(cfg.loss_type)
+    if kind is LossType.CE:
+        weight = cfg.class_weights._value  # optional: uniform when unset
+        return nn.CrossEntropyLoss(weight=weight)
+    if kind is LossType.MSE:
+        return nn.MSELoss()
+    return nn.SmoothL1Loss()
+
+
+class BaseModule(nn.Module):
+    """Holds `self.model` (set by subclasses), the criterion and the step logic."""
+
+    model: nn.Module
+
+    def __init__(self, config: BaseModelConfig):
+        super().__init__()
+        opt = config.optimizer
+        self.loss_type = LossType(opt.loss_type)
+        self.num_classes = config.num_classes.value
+        self.criterion = make_criterion(opt)
+        self.lr, self.weight_decay = opt.lr, opt.weight_decay
+        self.optimizer_algo = OptimizerAlgo(opt.algo)
+
+    @property
+    def is_regression(self) -> bool:
+        return self.loss_type in (LossType.MSE, LossType.SMOOTH_L1)
+
+    def forward(self, data) -> torch.Tensor:
+        """data: object with x, edge_index (or adj_t / a Graph), batch [, num_graphs]."""
+        edge_index = getattr(data, "adj_t", None)
+        if edge_index is None:
+            edge_index = data.edge_index
+        logits = self.model(data.x, edge_index, data.batch, getattr(data, "num_graphs", None))
+        if self.is_regression:
+            logits = torch.clamp(logits.squeeze(1), min=0, max=self.num_classes - 1)
+        return logits
+
+    def training_step(self, batch, batch_idx: int = 0) -> torch.Tensor:
+        logits = self(batch)
+        y = batch.y.float() if self.is_regression else batch.y
+        return self.criterion(logits, y)
+
+    def configure_optimizers(self) -> torch.optim.Optimizer:
+        ctor = {
+            OptimizerAlgo.ADAM: torch.optim.Adam,
+            OptimizerAlgo.ADAMW: torch.optim.AdamW,
+            OptimizerAlgo.SGD: torch.optim.SGD,
+        }[self.optimizer_algo]
+        return ctor(self.parameters(), lr=self.lr, weight_decay=self.weight_decay)

@@ -1,0 +1,373 @@
+"""CPU oracle: plain-torch restatement of the PyG 2.5.1 op sequence on the lesion-gnn hot path.
+
+TEST INFRASTRUCTURE ONLY. Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may import this module, and only as the checker / the timed CPU baseline.
+The product path (``lesion_gnn_amd``) never imports it and has no CPU fallback.
+
+Parity status: **unpinned against PyG itself.** torch_geometric / torch_scatter / torch_sparse /
+torch_cluster are not installed in this image and the reference (zacharielegault/lesion-gnn @ v2)
+holds no test or fixture on the GNN path. This file restates the documented
+PyG 2.5.1 operator sequence (pinned in requirements.lock:407 of the reference) with the same ATen
+primitives PyG runs on CPU (index_select -> message -> scatter_add_ / scatter_reduce_), and is
+pinned by analytic known-answer tests (tests/test_oracle.py) plus the only reference fixture that
+exists (the GaussianDistance KATs, reference test/test_transforms.py:20,29,38).
+
+Reference call sites restated here (paths relative to the reference root):
+  * GIN:  src/lesion_gnn/models/gin.py:17-35  (GINConv(MLP([d1,d2,d2], act="ELU", dropout)) :23,
+          F.elu :31, dropout :32, global_mean_pool :33)
+  * GAT:  src/lesion_gnn/models/gat.py:17-59  (GATConv(d1, d2 // heads, heads, dropout) :31,
+          F.elu :51, global_mean_pool :56)
+  * GCN:  NEW: skeleton of gin.py:17-35 with PyG GCNConv semantics.
+  * Loss: src/lesion_gnn/models/base.py:88-96 (criterion), :196-201 (training_step).
+  * Graph: configs/config.py:47 (KNNGraph(k, loop=True)); PyG Batch collation
+          (src/lesion_gnn/datasets/datamodule.py:63-69).
+"""
+from __future__ import annotations
+
+import math
+from itertools import pairwise
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch import Tensor
+
+# ----------------------------------------------------------------------------------------------
+# scatter helpers (PyG 2.5.1 torch_geometric.utils.scatter on CPU == ATen scatter_add_/reduce_)
+# ----------------------------------------------------------------------------------------------
+
+
+def scatter_sum(src: Tensor, index: Tensor, dim_size: int) -> Tensor:
+    out = src.new_zeros((dim_size,) + tuple(src.shape[1:]))
+    idx = index.view((-1,) + (1,) * (src.dim() - 1)).expand_as(src)
+    return out.scatter_add_(0, idx, src)
+
+
+def scatter_max(src: Tensor, index: Tensor, dim_size: int) -> Tensor:
+    out = src.new_zeros((dim_size,) + tuple(src.shape[1:]))
+    idx = index.view((-1,) + (1,) * (src.dim() - 1)).expand_as(src)
+    return out.scatter_reduce_(0, idx, src, reduce="amax", include_self=False)
+
+
+def scatter_mean(src: Tensor, index: Tensor, dim_size: int) -> Tensor:
+    """PyG scatter(reduce='mean'): sum / count.clamp(min=1)."""
+    count = src.new_zeros(dim_size).scatter_add_(0, index, src.new_ones(src.size(0)))
+    count = count.clamp(min=1)
+    out = scatter_sum(src, index, dim_size)
+    return out / count.view((-1,) + (1,) * (src.dim() - 1))
+
+
+# ----------------------------------------------------------------------------------------------
+# graph construction: KNNGraph (configs/config.py:47) + Batch collation (datamodule.py:63-69)
+# ----------------------------------------------------------------------------------------------
+
+
+def knn_graph(pos: Tensor, k: int, loop: bool = True) -> Tensor:
+    """torch_cluster.knn_graph for ONE graph, flow='source_to_target'.
+
+    Returns edge_index [2, E] = [neighbor (source), query (target)], grouped by query in node
+    order, each query's neighbors ordered by (squared distance, index) ascending. With loop=True a
+    node is its own nearest neighbor (distance 0). k is clipped to the node count, as knn does.
+    loop=False asks for k+1 neighbours and drops the self pair (PyG knn_graph).
+    """
+    n = pos.size(0)
+    if n == 0:
+        return torch.empty(2, 0, dtype=torch.long)
+    kk = min(k if loop else k + 1, n)
+    d = ((pos[:, None, :] - pos[None, :, :]) ** 2).sum(-1)  # [query, cand]
+    rows, cols = [], []
+    for q in range(n):
+        order = sorted(range(n), key=lambda c: (d[q, c].item(), c))[:kk]
+        for c in order:
+            if not loop and c == q:
+                continue
+            rows.append(c)
+            cols.append(q)
+    return torch.tensor([rows, cols], dtype=torch.long).view(2, -1)
+
+
+def collate(graphs: list[dict]) -> dict:
+    """PyG Batch.from_data_list for graphs {'x', 'edge_index', 'y'}: concat x, offset edges,
+    build batch (graph id per node) and ptr."""
+    xs, eis, ys, batch, ptr = [], [], [], [], [0]
+    off = 0
+    for g, d in enumerate(graphs):
+        n = d["x"].size(0)
+        xs.append(d["x"])
+        eis.append(d["edge_index"] + off)
+        ys.append(d["y"].view(-1))
+        batch.append(torch.full((n,), g, dtype=torch.long))
+        off += n
+        ptr.append(off)
+    return {
+        "x": torch.cat(xs, 0),
+        "edge_index": torch.cat(eis, 1),
+        "y": torch.cat(ys, 0),
+        "batch": torch.cat(batch, 0),
+        "ptr": torch.tensor(ptr, dtype=torch.long),
+        "num_graphs": len(graphs),
+    }
+
+
+# ----------------------------------------------------------------------------------------------
+# self-loop utilities (torch_geometric.utils.loop, 2.5.1)
+# ----------------------------------------------------------------------------------------------
+
+
+def remove_self_loops(edge_index: Tensor) -> Tensor:
+    mask = edge_index[0] != edge_index[1]
+    return edge_index[:, mask]
+
+
+def add_self_loops(edge_index: Tensor, num_nodes: int) -> Tensor:
+    loop = torch.arange(num_nodes, dtype=edge_index.dtype).view(1, -1).repeat(2, 1)
+    return torch.cat([edge_index, loop], dim=1)
+
+
+def add_remaining_self_loops(edge_index: Tensor, edge_weight: Tensor, fill_value: float,
+                             num_nodes: int) -> tuple[Tensor, Tensor]:
+    """Drop existing loops from the list, append one loop per node at the end; a node that had a
+    loop keeps that loop's weight (the last one in edge order), others get fill_value."""
+    mask = edge_index[0] != edge_index[1]
+    loop_index = torch.arange(num_nodes, dtype=edge_index.dtype).view(1, -1).repeat(2, 1)
+    loop_attr = edge_weight.new_full((num_nodes,), fill_value)
+    inv = ~mask
+    loop_attr[edge_index[0][inv]] = edge_weight[inv]
+    edge_weight = torch.cat([edge_weight[mask], loop_attr], dim=0)
+    edge_index = torch.cat([edge_index[:, mask], loop_index], dim=1)
+    return edge_index, edge_weight
+
+
+def gcn_norm(edge_index: Tensor, num_nodes: int, improved: bool = False,
+             add_loops: bool = True) -> tuple[Tensor, Tensor]:
+    """torch_geometric.nn.conv.gcn_conv.gcn_norm, edge_index (COO) path, flow source_to_target."""
+    fill = 2.0 if improved else 1.0
+    edge_weight = torch.ones(edge_index.size(1), dtype=torch.float32)
+    if add_loops:
+        edge_index, edge_weight = add_remaining_self_loops(edge_index, edge_weight, fill, num_nodes)
+    row, col = edge_index[0], edge_index[1]
+    deg = scatter_sum(edge_weight, col, num_nodes)
+    dis = deg.pow(-0.5)
+    dis = dis.masked_fill(dis == float("inf"), 0.0)
+    edge_weight = dis[row] * edge_weight * dis[col]
+    return edge_index, edge_weight
+
+
+# ----------------------------------------------------------------------------------------------
+# message-passing layers
+# ----------------------------------------------------------------------------------------------
+
+
+def glorot_(t: Tensor) -> None:
+    a = math.sqrt(6.0 / (t.size(-2) + t.size(-1)))
+    with torch.no_grad():
+        t.uniform_(-a, a)
+
+
+class GCNConv(nn.Module):
+    """PyG GCNConv(in, out): lin (no bias, glorot) -> gcn_norm -> propagate(add) -> + bias."""
+
+    def __init__(self, in_channels: int, out_channels: int):
+        super().__init__()
+        self.lin = nn.Linear(in_channels, out_channels, bias=False)
+        self.bias = nn.Parameter(torch.zeros(out_channels))
+        glorot_(self.lin.weight)
+
+    def forward(self, x: Tensor, edge_index: Tensor) -> Tensor:
+        n = x.size(0)
+        ei, w = gcn_norm(edge_index, n)
+        x = self.lin(x)
+        x_j = x.index_select(0, ei[0])  # propagate: collect x_j
+        msg = w.view(-1, 1) * x_j  # message: edge_weight * x_j
+        out = scatter_sum(msg, ei[1], n)  # aggregate 'add' at target
+        return out + self.bias
+
+
+class BatchNorm(nn.Module):
+    """torch_geometric.nn.norm.BatchNorm: wraps torch.nn.BatchNorm1d as `.module`."""
+
+    def __init__(self, channels: int):
+        super().__init__()
+        self.module = nn.BatchNorm1d(channels)
+
+    def forward(self, x: Tensor) -> Tensor:
+        return self.module(x)
+
+
+class MLP(nn.Module):
+    """PyG MLP(channel_list, act='ELU', dropout=p): norm='batch_norm', plain_last=True,
+    act_first=False: Lin -> BN -> ELU -> Dropout for every layer but the last; last Lin plain."""
+
+    def __init__(self, channel_list: list[int], dropout: float = 0.0):
+        super().__init__()
+        self.lins = nn.ModuleList([nn.Linear(a, b) for a, b in pairwise(channel_list)])
+        self.norms = nn.ModuleList([BatchNorm(c) for c in channel_list[1:-1]])
+        self.dropout = dropout
+
+    def forward(self, x: Tensor) -> Tensor:
+        for lin, norm in zip(self.lins[:-1], self.norms):
+            x = lin(x)
+            x = norm(x)
+            x = F.elu(x)
+            x = F.dropout(x, p=self.dropout, training=self.training)
+        return self.lins[-1](x)
+
+
+class GINConv(nn.Module):
+    """PyG GINConv(nn, eps=0, train_eps=False): nn((1 + eps) * x_i + sum_{j->i} x_j)."""
+
+    def __init__(self, mlp: nn.Module):
+        super().__init__()
+        self.nn = mlp
+        self.register_buffer("eps", torch.zeros(1))
+
+    def forward(self, x: Tensor, edge_index: Tensor) -> Tensor:
+        x_j = x.index_select(0, edge_index[0])
+        out = scatter_sum(x_j, edge_index[1], x.size(0))
+        out = out + (1 + self.eps) * x
+        return self.nn(out)
+
+
+def edge_softmax(src: Tensor, index: Tensor, num_nodes: int) -> Tensor:
+    """torch_geometric.utils.softmax (index path): exp(e - max.detach()) / (sum + 1e-16)."""
+    src_max = scatter_max(src.detach(), index, num_nodes)
+    out = (src - src_max.index_select(0, index)).exp()
+    out_sum = scatter_sum(out, index, num_nodes) + 1e-16
+    return out / out_sum.index_select(0, index)
+
+
+class GATConv(nn.Module):
+    """PyG 2.5.1 GATConv(in, out, heads, dropout), concat=True, negative_slope=0.2,
+    add_self_loops=True, bias=True (state_dict: lin.weight, att_src, att_dst, bias)."""
+
+    def __init__(self, in_channels: int, out_channels: int, heads: int = 1, dropout: float = 0.0,
+                 negative_slope: float = 0.2):
+        super().__init__()
+        self.heads, self.out_channels = heads, out_channels
+        self.negative_slope, self.dropout = negative_slope, dropout
+        self.lin = nn.Linear(in_channels, heads * out_channels, bias=False)
+        self.att_src = nn.Parameter(torch.empty(1, heads, out_channels))
+        self.att_dst = nn.Parameter(torch.empty(1, heads, out_channels))
+        self.bias = nn.Parameter(torch.zeros(heads * out_channels))
+        glorot_(self.lin.weight)
+        glorot_(self.att_src)
+        glorot_(self.att_dst)
+
+    def forward(self, x: Tensor, edge_index: Tensor) -> Tensor:
+        H, C = self.heads, self.out_channels
+        n = x.size(0)
+        xs = self.lin(x).view(-1, H, C)
+        a_src = (xs * self.att_src).sum(-1)
+        a_dst = (xs * self.att_dst).sum(-1)
+        ei = add_self_loops(remove_self_loops(edge_index), n)
+        src, dst = ei[0], ei[1]
+        alpha = a_src.index_select(0, src) + a_dst.index_select(0, dst)  # alpha_j + alpha_i
+        alpha = F.leaky_relu(alpha, self.negative_slope)
+        alpha = edge_softmax(alpha, dst, n)
+        alpha = F.dropout(alpha, p=self.dropout, training=self.training)
+        msg = alpha.unsqueeze(-1) * xs.index_select(0, src)
+        out = scatter_sum(msg, dst, n)
+        return out.view(-1, H * C) + self.bias
+
+
+def global_mean_pool(x: Tensor, batch: Tensor, size: int | None = None) -> Tensor:
+    size = int(batch.max()) + 1 if size is None else size
+    return scatter_mean(x, batch, size)
+
+
+def global_add_pool(x: Tensor, batch: Tensor, size: int | None = None) -> Tensor:
+    size = int(batch.max()) + 1 if size is None else size
+    return scatter_sum(x, batch, size)
+
+
+# ----------------------------------------------------------------------------------------------
+# models (same constructor signatures and state_dict keys as the build's modules)
+# ----------------------------------------------------------------------------------------------
+
+
+def _pool(kind: str):
+    return {"mean": global_mean_pool, "add": global_add_pool}[kind]
+
+
+class GCN(nn.Module):
+    """NEW model: skeleton of reference gin.py:17-35 with GCNConv."""
+
+    def __init__(self, input_features: int, hidden_channels: list[int], num_classes: int,
+                 dropout: float, pool: str = "mean"):
+        super().__init__()
+        self.in_proj = nn.Linear(input_features, hidden_channels[0])
+        self.convs = nn.ModuleList([GCNConv(a, b) for a, b in pairwise(hidden_channels)])
+        self.out_proj = nn.Linear(hidden_channels[-1], num_classes)
+        self.dropout = nn.Dropout(dropout)
+        self.pool = pool
+
+    def forward(self, x, edge_index, batch, num_graphs=None):
+        x = self.in_proj(x)
+        for conv in self.convs:
+            x = F.elu(conv(x, edge_index))
+            x = self.dropout(x)
+        x = _pool(self.pool)(x, batch, num_graphs)
+        return self.out_proj(x)
+
+
+class GIN(nn.Module):
+    """Reference gin.py:17-35 (+ pool option, default 'mean')."""
+
+    def __init__(self, input_features: int, hidden_channels: list[int], num_classes: int,
+                 dropout: float, pool: str = "mean"):
+        super().__init__()
+        self.in_proj = nn.Linear(input_features, hidden_channels[0])
+        self.convs = nn.ModuleList(
+            [GINConv(MLP([a, b, b], dropout=dropout)) for a, b in pairwise(hidden_channels)])
+        self.out_proj = nn.Linear(hidden_channels[-1], num_classes)
+        self.dropout = nn.Dropout(dropout)
+        self.pool = pool
+
+    def forward(self, x, edge_index, batch, num_graphs=None):
+        x = self.in_proj(x)
+        for conv in self.convs:
+            x = F.elu(conv(x, edge_index))
+            x = self.dropout(x)
+        x = _pool(self.pool)(x, batch, num_graphs)
+        return self.out_proj(x)
+
+
+class GAT(nn.Module):
+    """Reference gat.py:17-59 (SetTransformer readout branch :33-43 out of scope)."""
+
+    def __init__(self, input_features: int, hiddden_channels: list[int], num_classes: int,
+                 heads: int, dropout: float, num_st_seed_points=None, pool: str = "mean"):
+        super().__init__()
+        assert num_st_seed_points is None
+        self.in_proj = nn.Linear(input_features, hiddden_channels[0])
+        self.convs = nn.ModuleList([GATConv(a, b // heads, heads=heads, dropout=dropout)
+                                    for a, b in pairwise(hiddden_channels)])
+        self.out_proj = nn.Linear(hiddden_channels[-1], num_classes)
+        self.pool = pool
+
+    def forward(self, x, edge_index, batch, num_graphs=None):
+        x = self.in_proj(x)
+        for conv in self.convs:
+            x = F.elu(conv(x, edge_index))
+        x = _pool(self.pool)(x, batch, num_graphs)
+        return self.out_proj(x)
+
+
+def criterion(kind: str, logits: Tensor, y: Tensor, num_classes: int,
+              class_weights: Tensor | None = None) -> Tensor:
+    """Reference base.py:88-96 + training_step :196-201 (+ regression clamp gin.py:66-67)."""
+    if kind == "CE":
+        return F.cross_entropy(logits, y, weight=class_weights)
+    pred = torch.clamp(logits.squeeze(1), min=0, max=num_classes - 1)
+    if kind == "MSE":
+        return F.mse_loss(pred, y.float())
+    if kind == "SmoothL1":
+        return F.smooth_l1_loss(pred, y.float())
+    raise ValueError(kind)
+
+
+def gaussian_distance(edge_index: Tensor, pos: Tensor, sigma: float) -> Tensor:
+    """Reference transforms.py:32-79 (EDGE_WEIGHT_REPLACE): exp(-d^2 / 2s^2) / sqrt(2 pi s^2)."""
+    row, col = edge_index
+    sq = (pos[row] - pos[col]).pow(2).sum(-1)
+    return torch.exp(-sq / (2 * sigma ** 2)) / math.sqrt(2 * math.pi * sigma ** 2)

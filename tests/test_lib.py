@@ -1,0 +1,69 @@
+"""CPU checks of the C-ABI library: it loads without a GPU, exports every symbol include/lgnn.h
+declares, and the ctypes signature table matches the header. No compute calls."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from lesion_gnn_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "lgnn.h")
+
+
+def declared_functions() -> dict[str, int]:
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    out = {}
+    for m in re.finditer(r"^\s*[a-zA-Z_][\w\s\*]*?\b(lgnn_\w+)\s*\(([^;]*?)\)\s*;", text,
+                         flags=re.M | re.S):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if args in ("", "void") else args.count(",") + 1
+    return out
+
+
+def test_header_parses():
+    fns = declared_functions()
+    assert "lgnn_node_linear_fwd" in fns and "lgnn_graph_build" in fns
+    assert len(fns) >= 12
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for name in declared_functions():
+        assert hasattr(lib, name), f"liblgnn.so does not export {name}"
+
+
+def test_ctypes_table_matches_header():
+    fns = declared_functions()
+    assert set(fns) == set(_lib.SIGNATURES), set(fns) ^ set(_lib.SIGNATURES)
+    for name, nargs in fns.items():
+        assert len(_lib.SIGNATURES[name][1]) == nargs, name
+
+
+def test_abi_version_and_status_strings():
+    lib = _lib.load()
+    assert lib.lgnn_abi_version() == _lib.ABI_VERSION
+    assert lib.lgnn_status_string(0) == b"ok"
+    assert lib.lgnn_status_string(-22) == b"invalid argument"
+
+
+def test_argument_validation_without_gpu():
+    lib = _lib.load()
+    # invalid shapes are rejected before any launch
+    assert lib.lgnn_node_linear_fwd(None, 10, 0, None, None, None, 0.0, None, None, 4, 0, None,
+                                    None) == -22
+    assert lib.lgnn_bwd_num_partials(100, 0, 128) == -22
+    assert lib.lgnn_bwd_num_partials(65536, 128, 128) > 0
+    assert lib.lgnn_graph_build(None, 0, -1, 1, 1, None, None, None, None, None, None, None,
+                                None, 0, None) == -22
+
+
+def test_product_path_refuses_cpu_tensors():
+    import torch
+
+    from lesion_gnn_amd.graph import Graph
+
+    with pytest.raises(_lib.LgnnError):
+        Graph(torch.zeros(2, 3, dtype=torch.long), 4)

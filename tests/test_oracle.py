@@ -1,0 +1,127 @@
+"""Pins the CPU oracle (oracle/pyg_ref.py) with known answers: analytic identities of the PyG
+operators and the only fixture the reference holds (GaussianDistance KATs, reference
+test/test_transforms.py:20,29,38, rtol = atol = 1e-3 as there). Also checks the synthetic
+generator's k-NN topology bit-exactly against the oracle's restatement."""
+import math
+
+import pytest
+import torch
+
+import oracle.pyg_ref as ref
+from lesion_gnn_amd import synth
+
+
+def small_graph(seed=0, n=12, k=4):
+    g = torch.Generator().manual_seed(seed)
+    pos = torch.rand(n, 2, generator=g, dtype=torch.float64)
+    return pos, ref.knn_graph(pos, k, loop=True)
+
+
+def test_knn_graph_structure():
+    pos, ei = small_graph()
+    n, k = 12, 4
+    assert ei.shape == (2, n * k)
+    assert torch.equal(ei[1], torch.arange(n).repeat_interleave(k))  # grouped by query
+    assert torch.equal(ei[0][::k], torch.arange(n))  # self is the nearest
+    d = ((pos[ei[0]] - pos[ei[1]]) ** 2).sum(-1).view(n, k)
+    assert (d[:, 1:] >= d[:, :-1]).all()
+
+
+def test_synth_knn_matches_oracle_bitexact():
+    b = synth.make_batch(6, n=20, k=8, d_in=4, seed=3, sizes=[20, 5, 1, 20, 9, 33])
+    for g in range(b.num_graphs):
+        lo, hi = int(b.ptr[g]), int(b.ptr[g + 1])
+        want = ref.knn_graph(b.pos[lo:hi], 8, loop=True) + lo
+        mask = (b.edge_index[1] >= lo) & (b.edge_index[1] < hi)
+        assert torch.equal(b.edge_index[:, mask], want)
+    b2 = synth.make_batch(3, n=15, k=5, d_in=4, seed=4, loop=False)
+    want = torch.cat([ref.knn_graph(b2.pos[15 * g:15 * (g + 1)], 5, loop=False) + 15 * g
+                      for g in range(3)], 1)
+    assert torch.equal(b2.edge_index, want)
+
+
+def test_gcn_norm_regular_knn_is_one_over_k():
+    _, ei = small_graph(k=6)
+    ei2, w = ref.gcn_norm(ei, 12)
+    assert ei2.size(1) == ei.size(1)  # loops already present: none added
+    torch.testing.assert_close(w, torch.full_like(w, 1 / 6), rtol=1e-6, atol=0)
+    # loops moved to the end
+    assert torch.equal(ei2[0, -12:], torch.arange(12)) and torch.equal(ei2[1, -12:],
+                                                                      torch.arange(12))
+
+
+def test_gcn_norm_isolated_node_and_missing_loops():
+    ei = torch.tensor([[0, 1], [1, 0]])
+    ei2, w = ref.gcn_norm(ei, 3)  # node 2 isolated: only its loop, deg 1
+    assert ei2.size(1) == 5
+    torch.testing.assert_close(w, torch.tensor([0.5, 0.5, 0.5, 0.5, 1.0]))
+
+
+def test_gat_softmax_rows_sum_to_one():
+    torch.manual_seed(0)
+    _, ei = small_graph(k=5)
+    conv = ref.GATConv(8, 4, heads=3)
+    x = torch.randn(12, 8)
+    xs = conv.lin(x).view(-1, 3, 4)
+    a_s, a_d = (xs * conv.att_src).sum(-1), (xs * conv.att_dst).sum(-1)
+    e = ref.add_self_loops(ref.remove_self_loops(ei), 12)
+    alpha = ref.edge_softmax(torch.nn.functional.leaky_relu(a_s[e[0]] + a_d[e[1]], 0.2), e[1], 12)
+    s = ref.scatter_sum(alpha, e[1], 12)
+    torch.testing.assert_close(s, torch.ones_like(s))
+
+
+def test_gin_self_loops_only_is_mlp_of_2x():
+    torch.manual_seed(0)
+    n = 7
+    ei = torch.stack([torch.arange(n), torch.arange(n)])
+    mlp = ref.MLP([5, 6, 6]).eval()
+    conv = ref.GINConv(mlp)
+    x = torch.randn(n, 5)
+    torch.testing.assert_close(conv(x, ei), mlp(2 * x))
+
+
+def test_pools():
+    x = torch.full((9, 3), 2.5)
+    batch = torch.tensor([0, 0, 0, 1, 1, 3, 3, 3, 3])
+    m = ref.global_mean_pool(x, batch)
+    assert m.shape == (4, 3)
+    torch.testing.assert_close(m[[0, 1, 3]], torch.full((3, 3), 2.5))
+    assert (m[2] == 0).all()  # empty graph -> 0 (count clamped to 1)
+    a = ref.global_add_pool(x, batch)
+    torch.testing.assert_close(a[:, 0], torch.tensor([7.5, 5.0, 0.0, 10.0]))
+
+
+@pytest.mark.parametrize("model", ["gcn", "gin", "gat"])
+def test_models_permutation_equivariant_within_graph(model):
+    torch.manual_seed(0)
+    b = synth.make_batch(3, n=10, k=4, d_in=16, seed=1)
+    if model == "gcn":
+        m = ref.GCN(16, [16, 16, 16], 5, 0.0)
+    elif model == "gin":
+        m = ref.GIN(16, [16, 16, 16], 5, 0.0)
+    else:
+        m = ref.GAT(16, [16, 16], 5, heads=2, dropout=0.0)
+    m.eval()
+    out = m(b.x, b.edge_index, b.batch)
+    perm = torch.cat([torch.randperm(10) + 10 * g for g in range(3)])
+    inv = torch.empty_like(perm)
+    inv[perm] = torch.arange(30)
+    out2 = m(b.x[perm], inv[b.edge_index], b.batch[perm])
+    torch.testing.assert_close(out, out2, atol=1e-5, rtol=1e-5)
+
+
+def test_gaussian_distance_reference_kats():
+    """Reference test/test_transforms.py:20,29,38 (sigma 1, 0.5, 2 at d = 1)."""
+    ei = torch.tensor([[0, 1], [1, 0]])
+    pos = torch.tensor([[0.0, 0.0], [1.0, 0.0]])
+    for sigma, want in [(1.0, 0.2420), (0.5, 0.1080), (2.0, 0.1760)]:
+        w = ref.gaussian_distance(ei, pos, sigma)
+        torch.testing.assert_close(w, torch.tensor([want, want]), rtol=1e-3, atol=1e-3)
+    assert math.isclose(ref.gaussian_distance(ei, pos, 1.0)[0].item(),
+                        math.exp(-0.5) / math.sqrt(2 * math.pi), rel_tol=1e-6)
+
+
+def test_criterion_regression_clamp():
+    logits = torch.tensor([[-1.0], [2.0], [9.0]])
+    y = torch.tensor([0, 2, 4])
+    assert ref.criterion("MSE", logits, y, 5).item() == 0.0
