@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 1
+#define LGNN_ABI_VERSION 2
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -86,10 +86,12 @@ int lgnn_batch_ptr(const int64_t* batch, int64_t num_nodes, int64_t num_graphs, 
  *   Y[M,N] = act( P(X) W^T + b ),  W [N,K] row-major (torch Linear layout), b [N] or NULL,
  *   P(X) = X                                   if rowptr == NULL,
  *   P(X)_i = sum_{e in row i} w_e X[col_e] + self_scale * X_i   otherwise (w == NULL: w_e = 1).
+ *   S_out [M,K] (may be NULL): also store P(X) — the backward then streams it instead of
+ *   re-aggregating (supported when K <= 128 and N <= 128, multiples of 4; else LGNN_EINVAL).
  * ------------------------------------------------------------------------------------------- */
 int lgnn_node_linear_fwd(const float* X, int64_t M, int K, const int32_t* rowptr,
                          const int32_t* col, const float* w, float self_scale, const float* W,
-                         const float* b, int N, int act, float* Y, void* stream);
+                         const float* b, int N, int act, float* Y, float* S_out, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Node-tile fused backward of lgnn_node_linear_fwd.
@@ -104,9 +106,10 @@ int lgnn_node_linear_fwd(const float* X, int64_t M, int K, const int32_t* rowptr
  *   db_partial[g] (+)= colsum(dZ)                                          ([P][N], may be NULL)
  *   dXpre = dZ W  [M,K]  (may be NULL)
  * The P partial slots are summed by lgnn_reduce_partials (deterministic order).
- * num_partials: lgnn_bwd_num_partials(M, N, K) — pass that value and size slabs with it.
+ * num_partials: lgnn_bwd_num_partials(M, N, K, rowptr != NULL) — pass that value and size the
+ * slabs with it.
  * ------------------------------------------------------------------------------------------- */
-int lgnn_bwd_num_partials(int64_t M, int N, int K);
+int lgnn_bwd_num_partials(int64_t M, int N, int K, int gather);
 int lgnn_node_linear_bwd(int grad_mode, const float* dY, const int64_t* batch, const int32_t* gptr,
                          int pool_mean, const int32_t* tptr, const int32_t* tidx, const float* tw,
                          float tself, const float* H, int act, const float* X, int64_t M, int K,

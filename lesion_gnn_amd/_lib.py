@@ -33,8 +33,8 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_graph_workspace_bytes": (SZ, [I64, I64]),
     "lgnn_graph_build": (I32, [P, I64, I64, I32, I32, P, P, P, P, P, P, P, P, SZ, P]),
     "lgnn_batch_ptr": (I32, [P, I64, I64, P, P]),
-    "lgnn_node_linear_fwd": (I32, [P, I64, I32, P, P, P, F32, P, P, I32, I32, P, P]),
-    "lgnn_bwd_num_partials": (I32, [I64, I32, I32]),
+    "lgnn_node_linear_fwd": (I32, [P, I64, I32, P, P, P, F32, P, P, I32, I32, P, P, P]),
+    "lgnn_bwd_num_partials": (I32, [I64, I32, I32, I32]),
     "lgnn_node_linear_bwd": (I32, [I32, P, P, P, I32, P, P, P, F32, P, I32, P, I64, I32,
                                    P, P, P, F32, P, I32, P, P, P, I32, P]),
     "lgnn_reduce_partials": (I32, [P, I32, I64, P, P]),
@@ -44,7 +44,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_pool_bwd": (I32, [P, P, P, I64, I32, I32, P, P]),
 }
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _lib = None
 

@@ -4,9 +4,15 @@
 // Replaces (reference call sites): gcn_norm inside GCNConv, GATConv's
 // remove_self_loops/add_self_loops (gat.py:31), ToSparseTensor (datasets/datamodule.py:44-45).
 //
-// Determinism: slots are claimed with integer atomics (order varies), then every row is sorted by
-// original edge id, so the final CSR is identical run to run and keeps edge_index order inside a
-// row — the order PyG's scatter_add_ visits a target's messages in.
+// Pipeline (one memset + 4 kernels + 2 scans, no host sync):
+//   k_count   per-edge in/out degree; runs of equal targets inside a wave (k-NN input is grouped by
+//             target) are folded into one atomic
+//   scan      rowptr / tptr = exclusive scan of (degree + appended loop)
+//   k_fill    claim slots (same run folding), write (source, edge id)
+//   k_finish  per 256-row block: stage the rows in LDS, append the self loop, sort each row by
+//             edge id (restores edge_index order: the order PyG's scatter_add_ visits a target's
+//             messages in), compute GCN weights, write back coalesced. Run for both CSRs.
+// The result is identical run to run.
 #include <hipcub/hipcub.hpp>
 
 #include "common.h"
@@ -14,26 +20,35 @@
 namespace {
 
 constexpr int kThreads = 256;
+constexpr int kFinishCap = 6144;  // staged CSR entries per 256-row block
 
 inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
+struct AddLoop {
+  int add;
+  __host__ __device__ int operator()(int v) const { return v + add; }
+};
+
+using CntIter = hipcub::TransformInputIterator<int, AddLoop, const int32_t*>;
+
+size_t scan_temp_bytes(int64_t n) {
+  size_t bytes = 0;
+  CntIter it(nullptr, AddLoop{0});
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, it, (int32_t*)nullptr, (int)n);
+  return bytes;
+}
+
 struct GraphWs {
-  int32_t* cnt;    // [N+1] non-loop in-degree, then scanned in place -> rowptr source
+  int32_t* cnt;    // [N+1] in-degree without loops
   int32_t* tcnt;   // [N+1]
   int32_t* fill;   // [N]
   int32_t* tfill;  // [N]
-  int32_t* loopc;  // [N] number of self pairs seen per node (LOOPS_KEEP ignores)
   int32_t* eid;    // [E+N]
   int32_t* teid;   // [E+N]
   void* scan_tmp;
   size_t scan_bytes;
+  size_t zero_bytes;
 };
-
-size_t scan_temp_bytes(int64_t n) {
-  size_t bytes = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (int32_t*)nullptr, (int32_t*)nullptr, (int)n);
-  return bytes;
-}
 
 GraphWs carve(void* base, int64_t N, int64_t E) {
   GraphWs ws;
@@ -47,7 +62,7 @@ GraphWs carve(void* base, int64_t N, int64_t E) {
   ws.tcnt = (int32_t*)take((N + 1) * 4);
   ws.fill = (int32_t*)take(N * 4);
   ws.tfill = (int32_t*)take(N * 4);
-  ws.loopc = (int32_t*)take(N * 4);
+  ws.zero_bytes = (size_t)(p - static_cast<char*>(base));
   ws.eid = (int32_t*)take((E + N) * 4);
   ws.teid = (int32_t*)take((E + N) * 4);
   ws.scan_bytes = scan_temp_bytes(N + 1);
@@ -56,124 +71,170 @@ GraphWs carve(void* base, int64_t N, int64_t E) {
 }
 
 size_t ws_total(int64_t N, int64_t E) {
-  return 2 * align_up((N + 1) * 4) + 3 * align_up(N * 4) + 2 * align_up((E + N) * 4) +
+  return 2 * align_up((N + 1) * 4) + 2 * align_up(N * 4) + 2 * align_up((E + N) * 4) +
          align_up(scan_temp_bytes(N + 1)) + 256;
 }
 
-__global__ void k_count(const int64_t* __restrict__ ei, int64_t E, int64_t N, int loops,
-                        int32_t* cnt, int32_t* tcnt, int32_t* loopc, int32_t* err) {
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t s = ei[e], d = ei[E + e];
-    if (s < 0 || s >= N || d < 0 || d >= N) {
-      if (err) atomicAdd(err, 1);
-      continue;
+// Wave-level run detection over consecutive edges: lanes whose target equals the previous
+// lane's form a run; the head lane acts for the run. Invalid/skipped lanes get unique keys.
+struct Run {
+  bool head;
+  int head_lane;
+  int len;  // valid on head lanes
+};
+
+__device__ __forceinline__ Run wave_run(int64_t key) {
+  const int lane = threadIdx.x & 63;
+  const int64_t prev = __shfl_up(key, 1, 64);
+  const bool head = lane == 0 || key != prev;
+  const unsigned long long hm = __ballot(head);
+  const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+  Run r;
+  r.head = head;
+  r.head_lane = 63 - __clzll(hm & upto);
+  const unsigned long long after = hm & ~upto;
+  const int next = after ? __ffsll((long long)after) - 1 : 64;
+  r.len = next - lane;
+  return r;
+}
+
+__device__ __forceinline__ bool edge_ok(int64_t s, int64_t d, int64_t N) {
+  return s >= 0 && s < N && d >= 0 && d < N;
+}
+
+// grid-stride over wave-aligned chunks so every wave sees 64 consecutive edges
+__global__ __launch_bounds__(kThreads) void k_count(const int64_t* __restrict__ ei, int64_t E,
+                                                    int64_t N, int loops, int32_t* cnt,
+                                                    int32_t* tcnt, int32_t* err) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t base = wave0 * 64; base < E; base += nwaves * 64) {
+    const int64_t e = base + lane;
+    int64_t s = -1, d = -1;
+    if (e < E) {
+      s = ei[e];
+      d = ei[E + e];
     }
-    if (loops != LGNN_LOOPS_KEEP && s == d) {
-      atomicAdd(&loopc[d], 1);
-      continue;
-    }
-    atomicAdd(&cnt[d], 1);
-    if (tcnt) atomicAdd(&tcnt[s], 1);
+    const bool valid = e < E && edge_ok(s, d, N);
+    if (e < E && !valid && err) atomicAdd(err, 1);
+    const bool use = valid && !(loops != LGNN_LOOPS_KEEP && s == d);
+    const Run r = wave_run(use ? d : -2 - lane);
+    if (use && r.head) atomicAdd(&cnt[d], r.len);
+    if (use && tcnt) atomicAdd(&tcnt[s], 1);
   }
 }
 
-// cnt[i] += add_loop (one appended loop per node); cnt[N] = 0 so the exclusive scan of N+1
-// entries ends with the total.
-__global__ void k_add_loops(int32_t* cnt, int32_t* tcnt, int64_t N, int add_loop) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= N;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    if (i == N) {
-      cnt[i] = 0;
-      if (tcnt) tcnt[i] = 0;
-    } else {
-      cnt[i] += add_loop;
-      if (tcnt) tcnt[i] += add_loop;
+__global__ __launch_bounds__(kThreads) void k_fill(const int64_t* __restrict__ ei, int64_t E,
+                                                   int64_t N, int loops,
+                                                   const int32_t* __restrict__ rowptr,
+                                                   int32_t* fill, int32_t* col, int32_t* eid,
+                                                   const int32_t* __restrict__ tptr,
+                                                   int32_t* tfill, int32_t* tidx, int32_t* teid) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t base = wave0 * 64; base < E; base += nwaves * 64) {
+    const int64_t e = base + lane;
+    int64_t s = -1, d = -1;
+    if (e < E) {
+      s = ei[e];
+      d = ei[E + e];
     }
-  }
-}
-
-__global__ void k_fill(const int64_t* __restrict__ ei, int64_t E, int64_t N, int loops,
-                       const int32_t* __restrict__ rowptr, int32_t* fill, int32_t* col,
-                       int32_t* eid, const int32_t* __restrict__ tptr, int32_t* tfill,
-                       int32_t* tidx, int32_t* teid) {
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t s = ei[e], d = ei[E + e];
-    if (s < 0 || s >= N || d < 0 || d >= N) continue;
-    if (loops != LGNN_LOOPS_KEEP && s == d) continue;
-    const int slot = atomicAdd(&fill[d], 1);
-    col[rowptr[d] + slot] = (int32_t)s;
-    eid[rowptr[d] + slot] = (int32_t)e;
-    if (tptr) {
-      const int ts = atomicAdd(&tfill[s], 1);
-      tidx[tptr[s] + ts] = (int32_t)d;
-      teid[tptr[s] + ts] = (int32_t)e;
-    }
-  }
-}
-
-// Per node: append the self loop (if the mode appends one), sort the row by edge id, write
-// weights. Rows are short (k-NN in-degree = k); insertion sort per thread.
-__device__ void sort_row(int32_t* idx, int32_t* key, int n) {
-  for (int a = 1; a < n; ++a) {
-    const int32_t kk = key[a], vv = idx[a];
-    int b = a - 1;
-    while (b >= 0 && key[b] > kk) {
-      key[b + 1] = key[b];
-      idx[b + 1] = idx[b];
-      --b;
-    }
-    key[b + 1] = kk;
-    idx[b + 1] = vv;
-  }
-}
-
-__global__ void k_finish(int64_t N, int64_t E, int add_loop, int norm,
-                         const int32_t* __restrict__ rowptr, int32_t* col, int32_t* eid, float* w,
-                         const int32_t* __restrict__ tptr, int32_t* tidx, int32_t* teid,
-                         float* tw) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < N;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int r0 = rowptr[i], r1 = rowptr[i + 1];
-    if (add_loop) {
-      col[r1 - 1] = (int32_t)i;
-      eid[r1 - 1] = (int32_t)(E + i);
-    }
-    sort_row(col + r0, eid + r0, r1 - r0);
-    if (tptr) {
-      const int t0 = tptr[i], t1 = tptr[i + 1];
-      if (add_loop) {
-        tidx[t1 - 1] = (int32_t)i;
-        teid[t1 - 1] = (int32_t)(E + i);
+    const bool use = e < E && edge_ok(s, d, N) && !(loops != LGNN_LOOPS_KEEP && s == d);
+    const Run r = wave_run(use ? d : -2 - lane);
+    int slot0 = 0;
+    if (use && r.head) slot0 = atomicAdd(&fill[d], r.len);
+    slot0 = __shfl(slot0, r.head_lane, 64);
+    if (use) {
+      const int pos = rowptr[d] + slot0 + (lane - r.head_lane);
+      col[pos] = (int32_t)s;
+      eid[pos] = (int32_t)e;
+      if (tptr) {
+        const int ts = atomicAdd(&tfill[s], 1);
+        tidx[tptr[s] + ts] = (int32_t)d;
+        teid[tptr[s] + ts] = (int32_t)e;
       }
-      sort_row(tidx + t0, teid + t0, t1 - t0);
     }
   }
 }
 
-// GCN weights: deg_i = row length of target i (all weights 1, loops included);
-// dis = deg^-1/2 (inf -> 0); w_e = dis[src] * dis[dst]  (PyG: dis[row] * 1 * dis[col]).
-__device__ __forceinline__ float gcn_dis(const int32_t* rowptr, int64_t j) {
+__device__ __forceinline__ float gcn_dis(const int32_t* __restrict__ rowptr, int64_t j) {
   const int deg = rowptr[j + 1] - rowptr[j];
   return deg > 0 ? 1.0f / sqrtf((float)deg) : 0.0f;
 }
 
-__global__ void k_weights(int64_t N, int norm, const int32_t* __restrict__ rowptr,
-                          const int32_t* __restrict__ col, float* w,
-                          const int32_t* __restrict__ tptr, const int32_t* __restrict__ tidx,
-                          float* tw) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < N;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const float di = norm == LGNN_NORM_GCN ? gcn_dis(rowptr, i) : 1.f;
-    if (w) {
-      for (int e = rowptr[i]; e < rowptr[i + 1]; ++e)
-        w[e] = norm == LGNN_NORM_GCN ? gcn_dis(rowptr, col[e]) * 1.0f * di : 1.0f;
+// insertion sort of n (key, val) pairs by key (keys distinct)
+template <typename KP, typename VP>
+__device__ __forceinline__ void sort_row(KP key, VP val, int n) {
+  for (int a = 1; a < n; ++a) {
+    const int32_t kk = key[a], vv = val[a];
+    int b = a - 1;
+    while (b >= 0 && key[b] > kk) {
+      key[b + 1] = key[b];
+      val[b + 1] = val[b];
+      --b;
     }
-    if (tptr && tw) {
-      // transposed entry (source i -> target t): weight dis[i] * dis[t]
-      for (int e = tptr[i]; e < tptr[i + 1]; ++e)
-        tw[e] = norm == LGNN_NORM_GCN ? di * 1.0f * gcn_dis(rowptr, tidx[e]) : 1.0f;
+    key[b + 1] = kk;
+    val[b + 1] = vv;
+  }
+}
+
+// blockIdx.y = 0: target CSR (rowptr/col/eid/w); 1: source CSR (tptr/tidx/teid/tw).
+// Weight of entry (row i, neighbour j): GCN (dis(src) * 1) * dis(dst) = dis(j) * dis(i).
+__global__ __launch_bounds__(kThreads) void k_finish(int64_t N, int64_t E, int add_loop, int norm,
+                                                     const int32_t* __restrict__ rowptr,
+                                                     int32_t* col, int32_t* eid, float* w,
+                                                     const int32_t* __restrict__ tptr,
+                                                     int32_t* tidx, int32_t* teid, float* tw) {
+  __shared__ int32_t s_key[kFinishCap];
+  __shared__ int32_t s_val[kFinishCap];
+  const bool tr = blockIdx.y == 1;
+  const int32_t* __restrict__ ptr = tr ? tptr : rowptr;
+  int32_t* idx = tr ? tidx : col;
+  int32_t* key = tr ? teid : eid;
+  float* wt = tr ? tw : w;
+  const int64_t i0 = (int64_t)blockIdx.x * kThreads;
+  const int64_t i = i0 + threadIdx.x;
+  const int64_t iend = i0 + kThreads < N ? i0 + kThreads : N;
+  const int eb = ptr[i0], ee = ptr[iend];
+  const bool staged = ee - eb <= kFinishCap;
+  if (staged) {
+    for (int j = eb + threadIdx.x; j < ee; j += kThreads) {
+      s_key[j - eb] = key[j];
+      s_val[j - eb] = idx[j];
+    }
+  }
+  __syncthreads();
+  if (i < N) {
+    const int r0 = ptr[i], r1 = ptr[i + 1];
+    if (staged) {
+      if (add_loop) {
+        s_val[r1 - 1 - eb] = (int32_t)i;
+        s_key[r1 - 1 - eb] = (int32_t)(E + i);
+      }
+      sort_row(s_key + (r0 - eb), s_val + (r0 - eb), r1 - r0);
+    } else {
+      if (add_loop) {
+        idx[r1 - 1] = (int32_t)i;
+        key[r1 - 1] = (int32_t)(E + i);
+      }
+      sort_row(key + r0, idx + r0, r1 - r0);
+    }
+  }
+  __syncthreads();
+  if (staged) {
+    for (int j = eb + threadIdx.x; j < ee; j += kThreads) idx[j] = s_val[j - eb];
+  }
+  if (wt) {
+    // row of each entry: binary search is avoided by a per-thread row walk (rows are short)
+    if (i < N) {
+      const int r0 = ptr[i], r1 = ptr[i + 1];
+      const float di = norm == LGNN_NORM_GCN ? gcn_dis(rowptr, i) : 1.f;
+      for (int j = r0; j < r1; ++j) {
+        const int nb = staged ? s_val[j - eb] : idx[j];
+        wt[j] = norm == LGNN_NORM_GCN ? (gcn_dis(rowptr, nb) * 1.0f) * di : 1.0f;
+      }
     }
   }
 }
@@ -191,10 +252,10 @@ __global__ void k_batch_ptr(const int64_t* __restrict__ batch, int64_t M, int64_
   }
 }
 
-inline int grid_for(int64_t n) {
+inline int grid_for(int64_t n, int64_t cap = 4096) {
   int64_t g = (n + kThreads - 1) / kThreads;
   if (g < 1) g = 1;
-  if (g > 4096) g = 4096;
+  if (g > cap) g = cap;
   return (int)g;
 }
 
@@ -227,45 +288,36 @@ extern "C" int lgnn_graph_build(const int64_t* edge_index, int64_t E, int64_t N,
   hipStream_t s = as_stream(stream);
   const int add_loop = loops == LGNN_LOOPS_KEEP ? 0 : 1;
   GraphWs ws = carve(workspace, N, E);
-  // zero the counters (one contiguous region: cnt .. loopc)
-  const size_t zero_bytes = (char*)ws.eid - (char*)ws.cnt;
-  if (hipMemsetAsync(ws.cnt, 0, zero_bytes, s) != hipSuccess) return (int)hipGetLastError();
+  if (hipMemsetAsync(ws.cnt, 0, ws.zero_bytes, s) != hipSuccess) return (int)hipGetLastError();
   if (N == 0) {
     if (hipMemsetAsync(rowptr, 0, 4, s) != hipSuccess) return (int)hipGetLastError();
     if (tptr && hipMemsetAsync(tptr, 0, 4, s) != hipSuccess) return (int)hipGetLastError();
     return LGNN_OK;
   }
   if (E > 0) {
-    hipLaunchKernelGGL(k_count, dim3(grid_for(E)), dim3(kThreads), 0, s, edge_index, E, N, loops,
-                       ws.cnt, tptr ? ws.tcnt : nullptr, ws.loopc, err_count);
+    hipLaunchKernelGGL(k_count, dim3(grid_for(E, 2048)), dim3(kThreads), 0, s, edge_index, E, N,
+                       loops, ws.cnt, tptr ? ws.tcnt : nullptr, err_count);
     LGNN_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(k_add_loops, dim3(grid_for(N + 1)), dim3(kThreads), 0, s, ws.cnt,
-                     tptr ? ws.tcnt : nullptr, N, add_loop);
-  LGNN_LAUNCH_CHECK();
   size_t tb = ws.scan_bytes;
-  if (hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, tb, ws.cnt, rowptr, (int)(N + 1), s) !=
-      hipSuccess)
+  if (hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, tb, CntIter(ws.cnt, AddLoop{add_loop}),
+                                       rowptr, (int)(N + 1), s) != hipSuccess)
     return (int)hipGetLastError();
   if (tptr) {
     tb = ws.scan_bytes;
-    if (hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, tb, ws.tcnt, tptr, (int)(N + 1), s) !=
-        hipSuccess)
+    if (hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, tb, CntIter(ws.tcnt, AddLoop{add_loop}),
+                                         tptr, (int)(N + 1), s) != hipSuccess)
       return (int)hipGetLastError();
   }
   if (E > 0) {
-    hipLaunchKernelGGL(k_fill, dim3(grid_for(E)), dim3(kThreads), 0, s, edge_index, E, N, loops,
-                       rowptr, ws.fill, col, ws.eid, tptr, ws.tfill, tidx, ws.teid);
+    hipLaunchKernelGGL(k_fill, dim3(grid_for(E, 2048)), dim3(kThreads), 0, s, edge_index, E, N,
+                       loops, rowptr, ws.fill, col, ws.eid, tptr, ws.tfill, tidx, ws.teid);
     LGNN_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(k_finish, dim3(grid_for(N)), dim3(kThreads), 0, s, N, E, add_loop, norm,
-                     rowptr, col, ws.eid, w, tptr, tidx, ws.teid, tw);
+  dim3 fg((unsigned)((N + kThreads - 1) / kThreads), tptr ? 2u : 1u);
+  hipLaunchKernelGGL(k_finish, fg, dim3(kThreads), 0, s, N, E, add_loop, norm, rowptr, col,
+                     ws.eid, w, tptr, tidx, ws.teid, tw);
   LGNN_LAUNCH_CHECK();
-  if (w || tw) {
-    hipLaunchKernelGGL(k_weights, dim3(grid_for(N)), dim3(kThreads), 0, s, N, norm, rowptr, col, w,
-                       tptr, tidx, tw);
-    LGNN_LAUNCH_CHECK();
-  }
   return LGNN_OK;
 }
 

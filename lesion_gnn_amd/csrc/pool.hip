@@ -75,28 +75,37 @@ __global__ __launch_bounds__(NT) void k_head_bwd_dp(const float* __restrict__ dl
 }
 
 // dWout[c][d] = sum_g dlogits[g][c] pooled[g][d]; dbout[c] = sum_g dlogits[g][c].
-// block = (class c, 64-wide feature strip); 4 waves split g (w, w+4, ...), fixed-order combine.
-__global__ __launch_bounds__(NT) void k_head_bwd_dw(const float* __restrict__ dlogits,
+// block = (class c, 64-wide feature strip), 16 waves split g (w, w+16, ...), unconditional
+// (clamped) loads so every iteration's loads are in flight; fixed-order combine.
+constexpr int HT = 1024;
+__global__ __launch_bounds__(HT) void k_head_bwd_dw(const float* __restrict__ dlogits,
                                                     const float* __restrict__ pooled, int64_t B,
                                                     int D, int C, float* __restrict__ dWout,
                                                     float* __restrict__ dbout) {
-  __shared__ float red[4][65];
+  __shared__ float red[16][65];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = blockIdx.y;
   const int d = blockIdx.x * 64 + lane;
+  const int dc = d < D ? d : D - 1;
   float s = 0.f, sb = 0.f;
-  for (int64_t g = wave; g < B; g += 4) {
+#pragma unroll 4
+  for (int64_t g = wave; g < B; g += 16) {
     const float dl = dlogits[g * C + c];
-    if (d < D) s = fmaf(dl, pooled[g * D + d], s);
+    s = fmaf(dl, pooled[g * D + dc], s);
     sb += dl;
   }
   red[wave][lane] = s;
   if (lane == 0) red[wave][64] = sb;
   __syncthreads();
   if (wave == 0) {
-    if (d < D) dWout[(int64_t)c * D + d] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
-    if (lane == 0 && blockIdx.x == 0 && dbout)
-      dbout[c] = ((red[0][64] + red[1][64]) + red[2][64]) + red[3][64];
+    float t = red[0][lane], tb = red[0][64];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) {
+      t += red[q][lane];
+      tb += red[q][64];
+    }
+    if (d < D) dWout[(int64_t)c * D + d] = t;
+    if (lane == 0 && blockIdx.x == 0 && dbout) dbout[c] = tb;
   }
 }
 
@@ -142,7 +151,7 @@ extern "C" int lgnn_pool_head_bwd(const float* dlogits, const float* pooled, int
     LGNN_LAUNCH_CHECK();
   }
   if (dWout) {
-    hipLaunchKernelGGL(k_head_bwd_dw, dim3((unsigned)((D + 63) / 64), (unsigned)C), dim3(NT), 0, s,
+    hipLaunchKernelGGL(k_head_bwd_dw, dim3((unsigned)((D + 63) / 64), (unsigned)C), dim3(HT), 0, s,
                        dlogits, pooled, B, D, C, dWout, dbout);
     LGNN_LAUNCH_CHECK();
   }

@@ -31,20 +31,27 @@ def _s(dev) -> int:
 # ----------------------------------------------------------------------------------------------
 
 
+def fast_shape(K: int, N: int) -> bool:
+    """Shapes served by the tile fast path (tile.hip): S can be saved in the forward."""
+    return K <= 128 and N <= 128 and K % 4 == 0 and N % 4 == 0
+
+
 def linear_fwd(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None, act: int,
-               csr: Csr | None = None, self_scale: float = 0.0) -> torch.Tensor:
+               csr: Csr | None = None, self_scale: float = 0.0, save_s: bool = False):
+    """Y = act(P(x) W^T + b). With save_s (aggregating fast-path shapes) also returns S = P(x)."""
     M, K = x.shape
     N = W.size(0)
     y = torch.empty(M, N, dtype=torch.float32, device=x.device)
+    s_out = torch.empty(M, K, dtype=torch.float32, device=x.device) if save_s else None
     _lib.call("lgnn_node_linear_fwd", _lib.ptr(x), M, K,
               _lib.ptr(csr.rowptr) if csr else None, _lib.ptr(csr.col) if csr else None,
               _lib.ptr(csr.w) if csr else None, float(self_scale), _lib.ptr(W), _lib.ptr(b), N,
-              act, _lib.ptr(y), _s(x.device))
-    return y
+              act, _lib.ptr(y), _lib.ptr(s_out), _s(x.device))
+    return (y, s_out) if save_s else y
 
 
-def num_partials(M: int, N: int, K: int) -> int:
-    p = _lib.load().lgnn_bwd_num_partials(M, N, K)
+def num_partials(M: int, N: int, K: int, gather: bool = False) -> int:
+    p = _lib.load().lgnn_bwd_num_partials(M, N, K, int(gather))
     _lib.check(0 if p > 0 else p, "lgnn_bwd_num_partials")
     return p
 
@@ -57,7 +64,7 @@ def linear_bwd(grad_mode: int, dY: torch.Tensor, *, H: torch.Tensor | None, act:
     M, K = X.shape
     N = W.size(0)
     dev = X.device
-    P = num_partials(M, N, K)
+    P = num_partials(M, N, K, csr is not None)
     slab = torch.empty(P * N * K + (P * N if want_db else 0), dtype=torch.float32, device=dev)
     dWp = slab[: P * N * K]
     dbp = slab[P * N * K:] if want_db else None
@@ -225,12 +232,21 @@ class _GCNStack(torch.autograd.Function):
         csr = graph.csr("gcn")
         W_in, b_in = params[0], params[1]
         hs = [linear_fwd(x, W_in, b_in, _lib.LGNN_ACT_NONE)]
+        ss = []  # aggregated conv inputs S_l = A_hat H_{l-1} (saved when the fast path applies)
+        ctx.saved_s = []
         for l in range(L):
             W, b = params[2 + 2 * l], params[3 + 2 * l]
-            hs.append(linear_fwd(hs[-1], W, b, _lib.LGNN_ACT_ELU, csr))
+            fast = fast_shape(W.size(1), W.size(0))
+            if fast:
+                h, s_ = linear_fwd(hs[-1], W, b, _lib.LGNN_ACT_ELU, csr, save_s=True)
+            else:
+                h, s_ = linear_fwd(hs[-1], W, b, _lib.LGNN_ACT_ELU, csr), hs[-1]
+            hs.append(h)
+            ss.append(s_)
+            ctx.saved_s.append(fast)
         W_out, b_out = params[2 + 2 * L], params[3 + 2 * L]
         pooled, logits = pool_head_fwd(hs[-1], graph, mean, W_out, b_out)
-        ctx.save_for_backward(x, pooled, *hs, *params)
+        ctx.save_for_backward(x, pooled, *hs, *ss, *params)
         ctx.graph, ctx.mean, ctx.L = graph, mean, L
         return logits
 
@@ -240,7 +256,8 @@ class _GCNStack(torch.autograd.Function):
         saved = ctx.saved_tensors
         x, pooled = saved[0], saved[1]
         hs = saved[2:3 + L]
-        params = saved[3 + L:]
+        ss = saved[3 + L:3 + 2 * L]
+        params = saved[3 + 2 * L:]
         graph = ctx.graph
         csr = graph.csr("gcn")
         W_out = params[2 + 2 * L]
@@ -254,8 +271,11 @@ class _GCNStack(torch.autograd.Function):
                 mode, dY, tc = _lib.LGNN_GRAD_POOL, dp, None
             else:
                 mode, dY, tc = _lib.LGNN_GRAD_TRANSPOSE, dS, csr
-            dS, dW, db = linear_bwd(mode, dY, H=hs[l + 1], act=_lib.LGNN_ACT_ELU, X=hs[l], W=W,
-                                    csr=csr, graph=graph, pool_mean=ctx.mean, tcsr=tc)
+            saved_s = ctx.saved_s[l]
+            dS, dW, db = linear_bwd(mode, dY, H=hs[l + 1], act=_lib.LGNN_ACT_ELU,
+                                    X=ss[l] if saved_s else hs[l], W=W,
+                                    csr=None if saved_s else csr, graph=graph,
+                                    pool_mean=ctx.mean, tcsr=tc)
             grads[2 + 2 * l], grads[3 + 2 * l] = dW, db
         # in_proj: dH0 = A^T dS_1 (transposed aggregation in the prologue); dx = dH0 W_in
         want_dx = ctx.needs_input_grad[0]

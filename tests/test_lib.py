@@ -53,9 +53,9 @@ def test_argument_validation_without_gpu():
     lib = _lib.load()
     # invalid shapes are rejected before any launch
     assert lib.lgnn_node_linear_fwd(None, 10, 0, None, None, None, 0.0, None, None, 4, 0, None,
-                                    None) == -22
-    assert lib.lgnn_bwd_num_partials(100, 0, 128) == -22
-    assert lib.lgnn_bwd_num_partials(65536, 128, 128) > 0
+                                    None, None) == -22
+    assert lib.lgnn_bwd_num_partials(100, 0, 128, 0) == -22
+    assert lib.lgnn_bwd_num_partials(65536, 128, 128, 0) > 0
     assert lib.lgnn_graph_build(None, 0, -1, 1, 1, None, None, None, None, None, None, None,
                                 None, 0, None) == -22
 
