@@ -60,18 +60,10 @@ def setup_dist(args):
     return world, rank, torch.device("cuda", local)
 
 
-def flat_allreduce(params, world):
-    grads = [p.grad for p in params]
-    flat = torch._utils._flatten_dense_tensors(grads)
-    dist.all_reduce(flat)
-    flat.div_(world)
-    for g, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
-        g.copy_(f)
-
-
 def time_dominant_kernel(model, b, dev, reps=20):
-    """Average duration of the dominant kernel (the fused conv backward: transposed aggregation
-    prologue + dW and dX fp32 MFMA GEMMs) with HIP events on the stream it is launched on."""
+    """Average duration of the dominant kernel — the fused GCN conv backward exactly as the step
+    launches it (transposed aggregation of dS + ELU' prologue, dW = dZ^T S and dX = dZ W fp32
+    MFMA GEMMs, S streamed from the forward) — with HIP events on the stream it runs on."""
     from lesion_gnn_amd import _lib, ops
     from lesion_gnn_amd.graph import Graph
 
@@ -80,12 +72,12 @@ def time_dominant_kernel(model, b, dev, reps=20):
     with torch.no_grad():
         h0 = ops.linear_fwd(b.x, model.in_proj.weight, model.in_proj.bias, _lib.LGNN_ACT_NONE)
         c0 = model.convs[0]
-        h1 = ops.linear_fwd(h0, c0.lin.weight, c0.bias, _lib.LGNN_ACT_ELU, csr)
-    M, K = h0.shape
+        h1, s1 = ops.linear_fwd(h0, c0.lin.weight, c0.bias, _lib.LGNN_ACT_ELU, csr, save_s=True)
+    M, K = s1.shape
     W = c0.lin.weight.detach().contiguous()
     N = W.size(0)
     dS = torch.randn(M, N, device=dev)
-    P = ops.num_partials(M, N, K)
+    P = ops.num_partials(M, N, K, False)
     dWp = torch.empty(P * N * K, device=dev)
     dbp = torch.empty(P * N, device=dev)
     dX = torch.empty(M, K, device=dev)
@@ -94,9 +86,9 @@ def time_dominant_kernel(model, b, dev, reps=20):
     def launch():
         _lib.call("lgnn_node_linear_bwd", _lib.LGNN_GRAD_TRANSPOSE, dS.data_ptr(), None, None, 1,
                   csr.tptr.data_ptr(), csr.tidx.data_ptr(), csr.tw.data_ptr(), 0.0,
-                  h1.data_ptr(), _lib.LGNN_ACT_ELU, h0.data_ptr(), M, K, csr.rowptr.data_ptr(),
-                  csr.col.data_ptr(), csr.w.data_ptr(), 0.0, W.data_ptr(), N, dX.data_ptr(),
-                  dWp.data_ptr(), dbp.data_ptr(), P, s.cuda_stream)
+                  h1.data_ptr(), _lib.LGNN_ACT_ELU, s1.data_ptr(), M, K, None, None, None, 0.0,
+                  W.data_ptr(), N, dX.data_ptr(), dWp.data_ptr(), dbp.data_ptr(), P,
+                  s.cuda_stream)
 
     for _ in range(3):
         launch()
@@ -109,7 +101,7 @@ def time_dominant_kernel(model, b, dev, reps=20):
     torch.cuda.synchronize(dev)
     ms = e0.elapsed_time(e1) / reps
     flops = 4.0 * M * N * K  # dW = dZ^T S (2MNK) + dX = dZ W (2MNK)
-    return {"kernel": "k_linear_bwd<GRAD_TRANSPOSE,ELU,GATHER,DX> (GCN conv backward)",
+    return {"kernel": "lgnn_tile::k_bwd<GRAD_TRANSPOSE,ELU,DX> (GCN conv backward)",
             "ms": ms, "flops": flops}
 
 
@@ -149,6 +141,7 @@ def cpu_baseline(args, seconds):
 def main():
     args = parse()
     world, rank, dev = setup_dist(args)
+    from lesion_gnn_amd import dist as ldist
     from lesion_gnn_amd import synth
     from lesion_gnn_amd.models.gcn import GCN
 
@@ -156,6 +149,8 @@ def main():
     b = synth.make_batch(B, n=args.nodes, k=args.k, d_in=128, seed=100 + rank).to(dev)
     torch.manual_seed(1234)
     model = GCN(128, [args.hidden] * (args.layers + 1), 5, dropout=0.0).to(dev)
+    if world > 1:
+        ldist.broadcast_params(model)
     params = list(model.parameters())
     opt = torch.optim.Adam(params, lr=1e-3, weight_decay=2e-6)
 
@@ -164,8 +159,8 @@ def main():
         logits = model(b.x, b.edge_index, b.batch, B)
         loss = torch.nn.functional.cross_entropy(logits, b.y)
         loss.backward()
-        if world > 1:
-            flat_allreduce(params, world)
+        if world > 1:  # one flat RCCL all-reduce; equal shards -> weights 1/world
+            ldist.allreduce_grads(params, B, B * world)
         opt.step()
 
     for _ in range(args.warmup):
