@@ -94,6 +94,9 @@ def time_dominant_kernel(model, b, dev, reps=20):
         launch()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
+    # park the stream on a spin kernel so every timed launch is queued before the GPU reaches
+    # the first event: the events then bracket back-to-back kernels, not host launch latency
+    torch.cuda._sleep(10_000_000)
     e0.record(s)
     for _ in range(reps):
         launch()
@@ -102,7 +105,20 @@ def time_dominant_kernel(model, b, dev, reps=20):
     ms = e0.elapsed_time(e1) / reps
     flops = 4.0 * M * N * K  # dW = dZ^T S (2MNK) + dX = dZ W (2MNK)
     return {"kernel": "lgnn_tile::k_bwd<GRAD_TRANSPOSE,ELU,DX> (GCN conv backward)",
-            "ms": ms, "flops": flops}
+            "ms": ms, "flops": flops, "trace_name": "void lgnn_tile::k_bwd<2, 1, true>"}
+
+
+def pmc_traffic(trace_name: str):
+    """HBM bytes per launch of `trace_name` from the committed rocprofv3 PMC passes
+    (profiles/traffic.json, written by tools/summarize_prof.py from separate FETCH_SIZE and
+    WRITE_SIZE passes of this same bench command: (2*FETCH_SIZE + WRITE_SIZE) * 1024)."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(path):
+        return None, None
+    for k, v in json.load(open(path)).items():
+        if k.startswith(trace_name):
+            return v["bytes_per_launch"], v["source"]
+    return None, None
 
 
 def cpu_baseline(args, seconds):
@@ -200,9 +216,12 @@ def main():
     if rank == 0 and not args.no_kernel_timing:
         kt = time_dominant_kernel(model, b, dev)
         achieved = kt["flops"] / (kt["ms"] * 1e-3) / 1e12
+        traffic, tsrc = pmc_traffic(kt["trace_name"])
         out["roofline"] = {"bound": "mfma", "achieved": round(achieved, 2),
                            "peak": MFMA_F32_PEAK_TF, "unit": "TFLOP/s",
-                           "frac": round(achieved / MFMA_F32_PEAK_TF, 4), "traffic": None,
+                           "frac": round(achieved / MFMA_F32_PEAK_TF, 4),
+                           "traffic": round(traffic) if traffic else None,
+                           "traffic_source": tsrc,
                            "kernel": kt["kernel"], "avg_launch_ms": round(kt["ms"], 5),
                            "flops_per_launch": kt["flops"]}
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
