@@ -150,6 +150,39 @@ int lgnn_pool_head_bwd(const float* dlogits, const float* pooled, int64_t B, int
 int lgnn_pool_bwd(const float* dpooled, const int64_t* batch, const int32_t* gptr, int64_t M,
                   int D, int pool_mean, float* dH, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * BatchNorm1d + ELU (+ dropout mask) of the GIN MLP.
+ * Replaces: PyG MLP([d1,d2,d2], act="ELU", norm="batch_norm") internals (reference gin.py:23):
+ * torch.nn.BatchNorm1d forward/backward (training: batch statistics, running stats updated with
+ * momentum and the unbiased variance; eval: running statistics), F.elu, F.dropout.
+ * Statistics in fp64, deterministic. `sums` is [2N] fp64: forward (sum z, sum z^2); backward
+ * (sum g, sum g*xhat) — caller-visible so a SyncBN all-reduce can run in between.
+ * mask (nullable): dropout keep-mask already scaled by 1/(1-p), [M,N].
+ * ------------------------------------------------------------------------------------------- */
+size_t lgnn_bn_workspace_bytes(int64_t num_rows, int N);
+int lgnn_bn_stats(const float* Z, int64_t M, int N, double* sums, void* workspace,
+                  size_t workspace_bytes, void* stream);
+/* mean/invstd/scale/shift [N] out; scale = gamma*invstd, shift = beta - mean*scale. training=0
+ * reads running_mean/var; training=1 updates them (if non-NULL) and num_batches_tracked. */
+int lgnn_bn_finalize(const double* sums, double count, const float* gamma, const float* beta,
+                     float eps, float momentum, int training, int N, float* running_mean,
+                     float* running_var, int64_t* num_batches_tracked, float* mean,
+                     float* invstd, float* scale, float* shift, void* stream);
+/* A = ELU(Z*scale + shift) [* mask] */
+int lgnn_bn_act(const float* Z, int64_t M, int N, const float* scale, const float* shift,
+                const float* mask, float* A, void* stream);
+/* sums = (sum g, sum g*xhat), g = dA * mask * ELU'(Z*scale+shift), xhat = (Z-mean)*invstd */
+int lgnn_bn_bwd_stats(const float* dA, const float* Z, const float* mask, int64_t M, int N,
+                      const float* scale, const float* shift, const float* mean,
+                      const float* invstd, double* sums, void* workspace, size_t workspace_bytes,
+                      void* stream);
+/* dZ = scale*(g - sum g/count - xhat * sum(g xhat)/count) (training) | scale*g (eval);
+ * dgamma = sum g*xhat, dbeta = sum g (each nullable) */
+int lgnn_bn_bwd_apply(const float* dA, const float* Z, const float* mask, int64_t M, int N,
+                      const float* scale, const float* shift, const float* mean,
+                      const float* invstd, const double* sums, double count, int training,
+                      float* dZ, float* dgamma, float* dbeta, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -24,6 +24,7 @@ P = ctypes.c_void_p
 I32 = ctypes.c_int
 I64 = ctypes.c_int64
 F32 = ctypes.c_float
+F64 = ctypes.c_double
 SZ = ctypes.c_size_t
 
 # name -> (restype, argtypes); mirrors include/lgnn.h exactly
@@ -42,6 +43,12 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_pool_head_fwd": (I32, [P, P, I64, I32, I32, P, P, I32, P, P, P]),
     "lgnn_pool_head_bwd": (I32, [P, P, I64, I32, P, I32, P, P, P, P]),
     "lgnn_pool_bwd": (I32, [P, P, P, I64, I32, I32, P, P]),
+    "lgnn_bn_workspace_bytes": (SZ, [I64, I32]),
+    "lgnn_bn_stats": (I32, [P, I64, I32, P, P, SZ, P]),
+    "lgnn_bn_finalize": (I32, [P, F64, P, P, F32, F32, I32, I32, P, P, P, P, P, P, P, P]),
+    "lgnn_bn_act": (I32, [P, I64, I32, P, P, P, P, P]),
+    "lgnn_bn_bwd_stats": (I32, [P, P, P, I64, I32, P, P, P, P, P, P, SZ, P]),
+    "lgnn_bn_bwd_apply": (I32, [P, P, P, I64, I32, P, P, P, P, P, F64, I32, P, P, P, P]),
 }
 
 ABI_VERSION = 2

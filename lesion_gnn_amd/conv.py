@@ -37,6 +37,55 @@ class GCNConv(nn.Module):
         return ops.node_linear(x, self.lin.weight, self.bias, g, "gcn", 0.0, act)
 
 
+class BatchNorm(nn.Module):
+    """torch_geometric.nn.norm.BatchNorm: torch.nn.BatchNorm1d wrapped as `.module` (state_dict
+    keys `module.{weight,bias,running_mean,running_var,num_batches_tracked}`)."""
+
+    def __init__(self, in_channels: int, eps: float = 1e-5, momentum: float = 0.1):
+        super().__init__()
+        self.module = nn.BatchNorm1d(in_channels, eps=eps, momentum=momentum)
+
+
+class MLP(nn.Module):
+    """Parameter container with PyG MLP(channel_list, act="ELU", dropout=p) structure
+    (norm="batch_norm", plain_last=True): `lins.{i}`, `norms.{i}.module`. The 3-entry form of the
+    reference GIN (gin.py:23) is computed by the fused GINConv kernel chain."""
+
+    def __init__(self, channel_list: list[int], dropout: float = 0.0):
+        super().__init__()
+        if len(channel_list) != 3:
+            raise ValueError("the fused GIN MLP supports channel_list [d1, d2, d3] (reference "
+                             "gin.py:23 uses [d1, d2, d2])")
+        self.channel_list = list(channel_list)
+        self.dropout = float(dropout)
+        self.lins = nn.ModuleList([nn.Linear(a, b) for a, b in
+                                   zip(channel_list[:-1], channel_list[1:])])
+        self.norms = nn.ModuleList([BatchNorm(channel_list[1])])
+
+
+class GINConv(nn.Module):
+    """PyG GINConv(nn, eps=0, train_eps=False): nn((1 + eps) x_i + sum_{j->i} x_j), with `nn` a
+    2-layer MLP with BatchNorm + ELU (reference gin.py:23); keys `nn.*` and the `eps` buffer."""
+
+    def __init__(self, mlp: MLP, eps: float = 0.0):
+        super().__init__()
+        self.nn = mlp
+        self.register_buffer("eps", torch.full((1,), float(eps)))
+        self.sync_group = None  # torch.distributed group for SyncBN (None: per-replica stats)
+
+    def forward(self, x: torch.Tensor, edge_index, act: int = _lib.LGNN_ACT_NONE) -> torch.Tensor:
+        g = as_graph(edge_index, x.size(0))
+        mlp = self.nn
+        bn = mlp.norms[0].module
+        mask = None
+        if mlp.dropout > 0.0 and self.training:
+            p = mlp.dropout
+            mask = (torch.rand(x.size(0), mlp.channel_list[1], device=x.device) >= p).float()
+            mask.mul_(1.0 / (1.0 - p))
+        return ops.gin_conv(x, mlp.lins[0].weight, mlp.lins[0].bias, bn, mlp.lins[1].weight,
+                            mlp.lins[1].bias, g, float(self.eps), mask, act, self.sync_group)
+
+
 def global_mean_pool(x: torch.Tensor, batch: torch.Tensor, size: int | None = None,
                      graph: Graph | None = None) -> torch.Tensor:
     g = graph if graph is not None else _pool_graph(x, batch, size)

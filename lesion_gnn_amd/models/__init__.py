@@ -3,14 +3,18 @@ the config type), restricted to the message-passing families of the hot path."""
 from .base import (BaseModelConfig, BaseModule, LossType, LRSchedulerConfig, OptimizerAlgo,
                    OptimizerConfig)
 from .gcn import GCN, GCNConfig, GCNModule
+from .gin import GIN, GINConfig, GINModule
 
-ModelConfig = GCNConfig
+ModelConfig = GCNConfig | GINConfig
 
-__all__ = ["GCN", "GCNConfig", "GCNModule", "BaseModule", "BaseModelConfig", "OptimizerConfig",
-           "OptimizerAlgo", "LossType", "LRSchedulerConfig", "ModelConfig", "get_model"]
+__all__ = ["GCN", "GCNConfig", "GCNModule", "GIN", "GINConfig", "GINModule", "BaseModule",
+           "BaseModelConfig", "OptimizerConfig", "OptimizerAlgo", "LossType", "LRSchedulerConfig",
+           "ModelConfig", "get_model"]
 
 
 def get_model(config) -> BaseModule:
     if isinstance(config, GCNConfig):
         return GCNModule(config)
+    if isinstance(config, GINConfig):
+        return GINModule(config)
     raise ValueError(f"Unknown model config type {type(config)}")

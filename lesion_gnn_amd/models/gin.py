@@ -1,0 +1,77 @@
+"""GIN graph classifier — reference src/lesion_gnn/models/gin.py:17-69 (GIN, GINConfig,
+GINLightning) with the `pool` option of SURVEY.md §0.3 ("mean" = reference behaviour, "add" =
+global_add_pool for BASELINE config C4).
+
+forward(x, edge_index | Graph, batch) is the drop-in boundary `self.model(data.x, edge_index,
+data.batch)` (reference gin.py:64). Each GINConv (aggregate -> Lin -> BatchNorm -> ELU -> Lin)
+plus the model's F.elu (gin.py:31) runs as one HIP autograd node (ops.gin_conv).
+"""
+from __future__ import annotations
+
+import dataclasses
+from itertools import pairwise
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import _lib, ops
+from ..conv import MLP, GINConv
+from ..graph import as_graph
+from ..utils.placeholder import Placeholder
+from .base import BaseModelConfig, BaseModule
+
+
+class GIN(nn.Module):
+    def __init__(self, input_features: int, hidden_channels: list[int], num_classes: int,
+                 dropout: float, pool: str = "mean"):
+        super().__init__()
+        assert all(d > 0 for d in hidden_channels)
+        if pool not in ("mean", "add"):
+            raise ValueError(f"pool must be 'mean' or 'add', got {pool!r}")
+        self.in_proj = nn.Linear(input_features, hidden_channels[0])
+        self.convs = nn.ModuleList([GINConv(MLP([d1, d2, d2], dropout=dropout))
+                                    for d1, d2 in pairwise(hidden_channels)])
+        self.out_proj = nn.Linear(hidden_channels[-1], num_classes)
+        self.dropout = nn.Dropout(dropout)
+        self.pool = pool
+
+    def set_sync_bn(self, group) -> None:
+        """SyncBatchNorm over a torch.distributed group (RCCL): BN statistics and their backward
+        sums are all-reduced, so N replicas compute exactly the single-device batch statistics."""
+        for c in self.convs:
+            c.sync_group = group
+
+    def forward(self, x: torch.Tensor, edge_index, batch: torch.Tensor,
+                num_graphs: int | None = None) -> torch.Tensor:
+        g = as_graph(edge_index, x.size(0), batch, num_graphs)
+        h = ops.node_linear(x, self.in_proj.weight, self.in_proj.bias)
+        for conv in self.convs:
+            h = conv(h, g, act=_lib.LGNN_ACT_ELU)
+            if self.dropout.p > 0.0 and self.training:
+                h = F.dropout(h, self.dropout.p, True)
+        return ops.pool_head(h, self.out_proj.weight, self.out_proj.bias, g, self.pool == "mean")
+
+
+@dataclasses.dataclass(kw_only=True)
+class GINConfig(BaseModelConfig):
+    input_features: Placeholder[int] = dataclasses.field(default_factory=Placeholder, init=False)
+    hidden_channels: list[int]
+    dropout: float
+    compile: bool
+    pool: str = "mean"
+    name: str = dataclasses.field(default="GIN", init=False)
+
+
+class GINModule(BaseModule):
+    """Reference GINLightning (gin.py:47-69)."""
+
+    def __init__(self, config: GINConfig):
+        super().__init__(config)
+        self.model = GIN(
+            input_features=config.input_features.value,
+            hidden_channels=config.hidden_channels,
+            num_classes=1 if self.is_regression else config.num_classes.value,
+            dropout=config.dropout,
+            pool=config.pool,
+        )

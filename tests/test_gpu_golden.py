@@ -1,0 +1,48 @@
+"""GPU parity against the committed golden vectors (tests/golden/*.npz): the HIP models through
+liblgnn.so's C ABI, loaded with the golden initial state_dict, run one training step on the
+regenerated batch; logits within 1e-4 (north_star), loss within 1e-5, gradients within
+atol = max(1e-4 * max|grad|, 5e-6) per tensor (fp32 sums in a different association order; vanishing
+gradients carry only rounding noise), BatchNorm running statistics within 1e-5."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import lesion_gnn_amd.models as models
+import oracle.pyg_ref as ref
+from tests.golden import make_golden as mg
+from tests.test_golden import golden_state, load
+
+pytestmark = pytest.mark.gpu
+
+OURS = {"gcn": models.GCN, "gin": models.GIN}
+CASES = [n for n, c in mg.CASES.items() if c[0] in OURS]
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_hip_matches_golden(cuda, name):
+    g = load(name)
+    kind, mkw, bkw, loss_kind, _ = mg.CASES[name]
+    m = OURS[kind](**mkw)
+    m.load_state_dict(golden_state(g))
+    m = m.to(cuda).train()
+    b = mg.make_batch(bkw)
+    logits = m(b.x.to(cuda), b.edge_index.to(cuda), b.batch.to(cuda), b.num_graphs)
+    classes = mkw["num_classes"] if loss_kind == "CE" else 5
+    loss = ref.criterion(loss_kind, logits, b.y.to(cuda), classes)
+    loss.backward()
+    # 1e-4 absolute (north_star); add-pool logits are sums over a graph: 1e-4 of their scale
+    atol = 1e-4 * max(1.0, float(np.abs(g["logits"]).max()))
+    np.testing.assert_allclose(logits.detach().cpu().numpy(), g["logits"], rtol=0, atol=atol)
+    np.testing.assert_allclose(loss.item(), float(g["loss"]), rtol=1e-5, atol=1e-6)
+    for k, p in m.named_parameters():
+        want = g[f"grads/{k}"]
+        # floor: gradients that vanish in exact arithmetic (a bias feeding BatchNorm) hold only
+        # fp32 rounding noise (~1e-6) in the golden file
+        atol = max(1e-4 * np.abs(want).max(), 5e-6)
+        np.testing.assert_allclose(p.grad.cpu().numpy(), want, rtol=0, atol=atol, err_msg=k)
+    for k, v in m.state_dict().items():
+        if f"after/{k}" in g:
+            np.testing.assert_allclose(v.cpu().numpy(), g[f"after/{k}"], rtol=1e-5, atol=1e-6,
+                                       err_msg=k)
