@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 2
+#define LGNN_ABI_VERSION 3
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -64,13 +64,15 @@ const char* lgnn_status_string(int status);
  * by SOURCE (tptr[N+1], tidx[cap] = target, tw[cap]), cap = E + N. Within a row entries keep
  * edge_index order; with LOOPS_REMAINING / LOOPS_READD the node's single self loop is last (as
  * PyG appends loops after the edge list). Invalid indices (<0 or >= N) are dropped and counted in
- * *err_count (device int, may be NULL). Workspace size: lgnn_graph_workspace_bytes.
+ * *err_count (device int, may be NULL). tmap (nullable, needs the transpose) [cap]: for each
+ * transpose entry, the position of the same edge in the target CSR (GAT backward reads per-edge
+ * attention saved in target order). Workspace size: lgnn_graph_workspace_bytes.
  * ------------------------------------------------------------------------------------------- */
 size_t lgnn_graph_workspace_bytes(int64_t num_nodes, int64_t num_edges);
 int lgnn_graph_build(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes, int loops,
                      int norm, int32_t* rowptr, int32_t* col, float* w, int32_t* tptr,
-                     int32_t* tidx, float* tw, int32_t* err_count, void* workspace,
-                     size_t workspace_bytes, void* stream);
+                     int32_t* tidx, float* tw, int32_t* tmap, int32_t* err_count,
+                     void* workspace, size_t workspace_bytes, void* stream);
 
 /* Graph offsets from a sorted PyG `batch` vector (Batch.ptr): ptr[g] = first node of graph g,
  * ptr[B] = M. Replaces the count/offset half of PyG scatter(reduce='mean') over `batch`. */
@@ -182,6 +184,38 @@ int lgnn_bn_bwd_apply(const float* dA, const float* Z, const float* mask, int64_
                       const float* scale, const float* shift, const float* mean,
                       const float* invstd, const double* sums, double count, int training,
                       float* dZ, float* dgamma, float* dbeta, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * GATConv attention (PyG 2.5.1 GATConv(d1, d2//H, heads=H, dropout=p), reference gat.py:31:
+ * concat=True, negative_slope, add_self_loops=True, bias=True) + the model's F.elu (gat.py:51).
+ * XP = lin(x) [M, H*C] (lgnn_node_linear_fwd without bias). Graph: the LGNN_LOOPS_READD CSR
+ * (remove_self_loops + add_self_loops). Per-edge arrays are [cap, H] in target-CSR order.
+ * Shapes: C in {4,8,16,32,64,128}, H*C <= 512. edge_mask (nullable): attention dropout keep-mask
+ * already scaled by 1/(1-p).
+ * ------------------------------------------------------------------------------------------- */
+/* a_s[i,h] = <XP[i,h,:], att_src[h,:]>, a_d likewise with att_dst (the alpha_src/alpha_dst sums) */
+int lgnn_gat_att(const float* XP, int64_t M, int H, int C, const float* att_src,
+                 const float* att_dst, float* a_s, float* a_d, void* stream);
+/* alpha = softmax_i(leaky_relu(a_s[j] + a_d[i])) (PyG utils.softmax, +1e-16; written if
+ * non-NULL), Y_i = act(sum_j alpha_ij mask_ij XP_j + bias) */
+int lgnn_gat_fwd(const int32_t* rowptr, const int32_t* col, const float* XP, const float* a_s,
+                 const float* a_d, int64_t M, int H, int C, float negative_slope,
+                 const float* edge_mask, const float* bias, int act, float* alpha, float* Y,
+                 void* stream);
+/* Backward, target rows: dZ = dY * act'(Y); da_e = d(logit) per edge; da_d = row sums. */
+int lgnn_gat_bwd_edge(const int32_t* rowptr, const int32_t* col, const float* XP,
+                      const float* a_s, const float* a_d, const float* alpha,
+                      const float* edge_mask, const float* dY, const float* Y, int act, int64_t M,
+                      int H, int C, float negative_slope, float* dZ, float* da_e, float* da_d,
+                      void* stream);
+/* Backward, source rows (transpose CSR + tmap from lgnn_graph_build): dXP, and per-block column
+ * partials [P][3][H*C] = (d att_src, d att_dst, d bias) for lgnn_reduce_partials. */
+int lgnn_gat_bwd_num_partials(int64_t M);
+int lgnn_gat_bwd_node(const int32_t* tptr, const int32_t* tidx, const int32_t* tmap,
+                      const float* alpha, const float* edge_mask, const float* da_e,
+                      const float* da_d, const float* dZ, const float* XP, const float* att_src,
+                      const float* att_dst, int64_t M, int H, int C, float* dXP,
+                      float* partials, int num_partials, void* stream);
 
 #ifdef __cplusplus
 }

@@ -86,6 +86,35 @@ class GINConv(nn.Module):
                             mlp.lins[1].bias, g, float(self.eps), mask, act, self.sync_group)
 
 
+class GATConv(nn.Module):
+    """PyG 2.5.1 GATConv(in, out, heads, dropout) with concat=True, negative_slope=0.2,
+    add_self_loops=True, bias=True (reference gat.py:31). state_dict: `lin.weight`, `att_src`,
+    `att_dst` [1, H, C], `bias` [H*C]."""
+
+    def __init__(self, in_channels: int, out_channels: int, heads: int = 1, dropout: float = 0.0,
+                 negative_slope: float = 0.2):
+        super().__init__()
+        self.in_channels, self.out_channels, self.heads = in_channels, out_channels, heads
+        self.negative_slope, self.dropout = negative_slope, dropout
+        self.lin = nn.Linear(in_channels, heads * out_channels, bias=False)
+        self.att_src = nn.Parameter(torch.empty(1, heads, out_channels))
+        self.att_dst = nn.Parameter(torch.empty(1, heads, out_channels))
+        self.bias = nn.Parameter(torch.zeros(heads * out_channels))
+        glorot_(self.lin.weight)
+        glorot_(self.att_src)
+        glorot_(self.att_dst)
+
+    def forward(self, x: torch.Tensor, edge_index, act: int = _lib.LGNN_ACT_NONE) -> torch.Tensor:
+        g = as_graph(edge_index, x.size(0))
+        mask = None
+        if self.dropout > 0.0 and self.training:
+            cap = g.csr("gat").col.numel()
+            mask = (torch.rand(cap, self.heads, device=x.device) >= self.dropout).float()
+            mask.mul_(1.0 / (1.0 - self.dropout))
+        return ops.gat_conv(x, self.lin.weight, self.att_src, self.att_dst, self.bias, g,
+                            self.heads, self.negative_slope, mask, act)
+
+
 def global_mean_pool(x: torch.Tensor, batch: torch.Tensor, size: int | None = None,
                      graph: Graph | None = None) -> torch.Tensor:
     g = graph if graph is not None else _pool_graph(x, batch, size)

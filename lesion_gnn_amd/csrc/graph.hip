@@ -45,6 +45,7 @@ struct GraphWs {
   int32_t* tfill;  // [N]
   int32_t* eid;    // [E+N]
   int32_t* teid;   // [E+N]
+  int32_t* inv;    // [E+N] edge id -> target-CSR position (for tmap)
   void* scan_tmp;
   size_t scan_bytes;
   size_t zero_bytes;
@@ -65,13 +66,14 @@ GraphWs carve(void* base, int64_t N, int64_t E) {
   ws.zero_bytes = (size_t)(p - static_cast<char*>(base));
   ws.eid = (int32_t*)take((E + N) * 4);
   ws.teid = (int32_t*)take((E + N) * 4);
+  ws.inv = (int32_t*)take((E + N) * 4);
   ws.scan_bytes = scan_temp_bytes(N + 1);
   ws.scan_tmp = take(ws.scan_bytes);
   return ws;
 }
 
 size_t ws_total(int64_t N, int64_t E) {
-  return 2 * align_up((N + 1) * 4) + 2 * align_up(N * 4) + 2 * align_up((E + N) * 4) +
+  return 2 * align_up((N + 1) * 4) + 2 * align_up(N * 4) + 3 * align_up((E + N) * 4) +
          align_up(scan_temp_bytes(N + 1)) + 256;
 }
 
@@ -224,7 +226,10 @@ __global__ __launch_bounds__(kThreads) void k_finish(int64_t N, int64_t E, int a
   }
   __syncthreads();
   if (staged) {
-    for (int j = eb + threadIdx.x; j < ee; j += kThreads) idx[j] = s_val[j - eb];
+    for (int j = eb + threadIdx.x; j < ee; j += kThreads) {
+      idx[j] = s_val[j - eb];
+      key[j] = s_key[j - eb];
+    }
   }
   if (wt) {
     // row of each entry: binary search is avoided by a per-thread row walk (rows are short)
@@ -237,6 +242,25 @@ __global__ __launch_bounds__(kThreads) void k_finish(int64_t N, int64_t E, int a
       }
     }
   }
+}
+
+// tmap[q] = position in the target CSR of the edge at source-CSR position q (both CSRs hold the
+// same entries; edge ids are unique: e for edges, E + i for appended loops).
+__global__ __launch_bounds__(kThreads) void k_tmap_inv(const int32_t* __restrict__ rowptr,
+                                                       int64_t N, const int32_t* __restrict__ eid,
+                                                       int32_t* __restrict__ inv) {
+  const int nnz = rowptr[N];
+  for (int p = blockIdx.x * kThreads + threadIdx.x; p < nnz; p += gridDim.x * kThreads)
+    inv[eid[p]] = p;
+}
+
+__global__ __launch_bounds__(kThreads) void k_tmap(const int32_t* __restrict__ tptr, int64_t N,
+                                                   const int32_t* __restrict__ teid,
+                                                   const int32_t* __restrict__ inv,
+                                                   int32_t* __restrict__ tmap) {
+  const int nnz = tptr[N];
+  for (int q = blockIdx.x * kThreads + threadIdx.x; q < nnz; q += gridDim.x * kThreads)
+    tmap[q] = inv[teid[q]];
 }
 
 __global__ void k_batch_ptr(const int64_t* __restrict__ batch, int64_t M, int64_t B,
@@ -278,12 +302,14 @@ extern "C" size_t lgnn_graph_workspace_bytes(int64_t num_nodes, int64_t num_edge
 
 extern "C" int lgnn_graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loops,
                                 int norm, int32_t* rowptr, int32_t* col, float* w, int32_t* tptr,
-                                int32_t* tidx, float* tw, int32_t* err_count, void* workspace,
+                                int32_t* tidx, float* tw, int32_t* tmap, int32_t* err_count,
+                                void* workspace,
                                 size_t workspace_bytes, void* stream) {
   if (N < 0 || E < 0 || loops < 0 || loops > 2 || norm < 0 || norm > 1) return LGNN_EINVAL;
   if (!rowptr || !col || (E > 0 && !edge_index)) return LGNN_EINVAL;
   if (N + E > INT32_MAX) return LGNN_EINVAL;
   if ((tptr == nullptr) != (tidx == nullptr)) return LGNN_EINVAL;
+  if (tmap && !tptr) return LGNN_EINVAL;
   if (workspace_bytes < ws_total(N, E) || !workspace) return LGNN_ENOSPC;
   hipStream_t s = as_stream(stream);
   const int add_loop = loops == LGNN_LOOPS_KEEP ? 0 : 1;
@@ -318,6 +344,13 @@ extern "C" int lgnn_graph_build(const int64_t* edge_index, int64_t E, int64_t N,
   hipLaunchKernelGGL(k_finish, fg, dim3(kThreads), 0, s, N, E, add_loop, norm, rowptr, col,
                      ws.eid, w, tptr, tidx, ws.teid, tw);
   LGNN_LAUNCH_CHECK();
+  if (tmap) {
+    const int g = grid_for(E + N, 2048);
+    hipLaunchKernelGGL(k_tmap_inv, dim3(g), dim3(kThreads), 0, s, rowptr, N, ws.eid, ws.inv);
+    LGNN_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_tmap, dim3(g), dim3(kThreads), 0, s, tptr, N, ws.teid, ws.inv, tmap);
+    LGNN_LAUNCH_CHECK();
+  }
   return LGNN_OK;
 }
 

@@ -30,6 +30,7 @@ class Csr:
     tptr: torch.Tensor    # int32 [N+1]
     tidx: torch.Tensor    # int32 [cap] target of each entry, grouped by source
     tw: torch.Tensor      # fp32 [cap]
+    tmap: torch.Tensor | None  # int32 [cap] target-CSR position of each transpose entry (GAT)
     err: torch.Tensor     # int32 [1] count of dropped out-of-range edges
 
 
@@ -81,6 +82,7 @@ class Graph:
             w=torch.empty(cap, dtype=torch.float32, device=dev),
             tptr=torch.empty(n + 1, **i32), tidx=torch.empty(cap, **i32),
             tw=torch.empty(cap, dtype=torch.float32, device=dev),
+            tmap=torch.empty(cap, **i32) if kind == "gat" else None,
             err=torch.zeros(1, **i32),
         )
         lib = _lib.load()
@@ -88,7 +90,8 @@ class Graph:
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         _lib.call("lgnn_graph_build", _lib.ptr(self.edge_index), e, n, loops, norm,
                   _lib.ptr(c.rowptr), _lib.ptr(c.col), _lib.ptr(c.w), _lib.ptr(c.tptr),
-                  _lib.ptr(c.tidx), _lib.ptr(c.tw), _lib.ptr(c.err), _lib.ptr(ws), ws_bytes,
+                  _lib.ptr(c.tidx), _lib.ptr(c.tw), _lib.ptr(c.tmap), _lib.ptr(c.err),
+                  _lib.ptr(ws), ws_bytes,
                   _lib.stream(dev))
         self._csr[kind] = c
         return c

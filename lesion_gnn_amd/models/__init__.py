@@ -3,11 +3,13 @@ the config type), restricted to the message-passing families of the hot path."""
 from .base import (BaseModelConfig, BaseModule, LossType, LRSchedulerConfig, OptimizerAlgo,
                    OptimizerConfig)
 from .gcn import GCN, GCNConfig, GCNModule
+from .gat import GAT, GATConfig, GATModule
 from .gin import GIN, GINConfig, GINModule
 
-ModelConfig = GCNConfig | GINConfig
+ModelConfig = GCNConfig | GINConfig | GATConfig
 
-__all__ = ["GCN", "GCNConfig", "GCNModule", "GIN", "GINConfig", "GINModule", "BaseModule",
+__all__ = ["GCN", "GCNConfig", "GCNModule", "GIN", "GINConfig", "GINModule", "GAT", "GATConfig",
+           "GATModule", "BaseModule",
            "BaseModelConfig", "OptimizerConfig", "OptimizerAlgo", "LossType", "LRSchedulerConfig",
            "ModelConfig", "get_model"]
 
@@ -17,4 +19,6 @@ def get_model(config) -> BaseModule:
         return GCNModule(config)
     if isinstance(config, GINConfig):
         return GINModule(config)
+    if isinstance(config, GATConfig):
+        return GATModule(config)
     raise ValueError(f"Unknown model config type {type(config)}")

@@ -1,0 +1,77 @@
+"""GAT graph classifier — reference src/lesion_gnn/models/gat.py:17-97 (GAT, GATConfig,
+GATLightning), including the config field typo `hiddden_channels` (gat.py:65, used by
+configs/config.py:61). The SetTransformer readout branch (gat.py:33-43, `num_st_seed_points`)
+is out of scope (no config enables it); passing it raises.
+
+forward(x, edge_index | Graph, batch) is the drop-in boundary `self.model(data.x, edge_index,
+data.batch)` (reference gat.py:92): in_proj -> L x ELU(GATConv) -> global_mean_pool -> out_proj,
+every conv one HIP autograd node (ops.gat_conv) with the ELU fused.
+"""
+from __future__ import annotations
+
+import dataclasses
+from itertools import pairwise
+
+import torch
+import torch.nn as nn
+
+from .. import _lib, ops
+from ..conv import GATConv
+from ..graph import as_graph
+from ..utils.placeholder import Placeholder
+from .base import BaseModelConfig, BaseModule
+
+
+class GAT(nn.Module):
+    def __init__(self, input_features: int, hiddden_channels: list[int], num_classes: int,
+                 heads: int, dropout: float, num_st_seed_points: int | None = None,
+                 pool: str = "mean"):
+        super().__init__()
+        assert all(d % heads == 0 for d in hiddden_channels)
+        if num_st_seed_points is not None:
+            raise NotImplementedError("SetTransformerAggregation readout (reference gat.py:33-43)"
+                                      " is out of scope for this build")
+        if pool not in ("mean", "add"):
+            raise ValueError(f"pool must be 'mean' or 'add', got {pool!r}")
+        self.in_proj = nn.Linear(input_features, hiddden_channels[0])
+        self.convs = nn.ModuleList([GATConv(d1, d2 // heads, heads=heads, dropout=dropout)
+                                    for d1, d2 in pairwise(hiddden_channels)])
+        self.st = None
+        self.out_proj = nn.Linear(hiddden_channels[-1], num_classes)
+        self.pool = pool
+
+    def forward(self, x: torch.Tensor, edge_index, batch: torch.Tensor,
+                num_graphs: int | None = None) -> torch.Tensor:
+        g = as_graph(edge_index, x.size(0), batch, num_graphs)
+        h = ops.node_linear(x, self.in_proj.weight, self.in_proj.bias)
+        for conv in self.convs:
+            h = conv(h, g, act=_lib.LGNN_ACT_ELU)
+        return ops.pool_head(h, self.out_proj.weight, self.out_proj.bias, g, self.pool == "mean")
+
+
+@dataclasses.dataclass(kw_only=True)
+class GATConfig(BaseModelConfig):
+    input_features: Placeholder[int] = dataclasses.field(default_factory=Placeholder, init=False)
+    hiddden_channels: list[int]
+    heads: int
+    dropout: float
+    compile: bool
+    num_st_seed_points: int | None = None
+    pool: str = "mean"
+    name: str = dataclasses.field(default="GAT", init=False)
+
+
+class GATModule(BaseModule):
+    """Reference GATLightning (gat.py:73-97)."""
+
+    def __init__(self, config: GATConfig):
+        super().__init__(config)
+        self.model = GAT(
+            input_features=config.input_features.value,
+            hiddden_channels=config.hiddden_channels,
+            num_classes=1 if self.is_regression else config.num_classes.value,
+            heads=config.heads,
+            dropout=config.dropout,
+            num_st_seed_points=config.num_st_seed_points,
+            pool=config.pool,
+        )

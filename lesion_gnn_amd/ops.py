@@ -454,3 +454,81 @@ def gin_conv(x, W1, b1, bn, W2, b2, graph: Graph, eps: float = 0.0, mask=None,
     beta = bn.bias if bn.affine else None
     return _GINConv.apply(x, W1, b1, gamma, beta, W2, b2, graph, bn, training, eps, mask, act,
                           group)
+
+
+# ----------------------------------------------------------------------------------------------
+# GATConv
+# ----------------------------------------------------------------------------------------------
+
+
+class _GATConv(torch.autograd.Function):
+    """PyG 2.5.1 GATConv (reference gat.py:31) + the model's F.elu (gat.py:51):
+        XP = x W^T (lin, no bias) viewed [M, H, C];  a_s = <XP, att_src>, a_d = <XP, att_dst>
+        alpha = softmax_dst(leaky_relu(a_s[j] + a_d[i]));  out_i = sum_j alpha_ij mask_ij XP_j
+        Y = act(out.view(M, H*C) + bias)
+    over remove_self_loops + add_self_loops of edge_index (graph kind "gat")."""
+
+    @staticmethod
+    def forward(ctx, x, W, att_src, att_dst, bias, graph, heads, slope, mask, act):
+        _lib.require_gpu(x, W, att_src, att_dst)
+        x, W = _f32c(x), _f32c(W)
+        att_src, att_dst = _f32c(att_src).view(-1), _f32c(att_dst).view(-1)
+        bias = _f32c(bias) if bias is not None else None
+        csr = graph.csr("gat")
+        M = x.size(0)
+        HC = W.size(0)
+        C = HC // heads
+        dev = x.device
+        XP = linear_fwd(x, W, None, _lib.LGNN_ACT_NONE)
+        a_s = torch.empty(M, heads, dtype=torch.float32, device=dev)
+        a_d = torch.empty(M, heads, dtype=torch.float32, device=dev)
+        _lib.call("lgnn_gat_att", _lib.ptr(XP), M, heads, C, _lib.ptr(att_src), _lib.ptr(att_dst),
+                  _lib.ptr(a_s), _lib.ptr(a_d), _s(dev))
+        cap = csr.col.numel()
+        alpha = torch.empty(cap, heads, dtype=torch.float32, device=dev)
+        Y = torch.empty(M, HC, dtype=torch.float32, device=dev)
+        _lib.call("lgnn_gat_fwd", _lib.ptr(csr.rowptr), _lib.ptr(csr.col), _lib.ptr(XP),
+                  _lib.ptr(a_s), _lib.ptr(a_d), M, heads, C, float(slope), _lib.ptr(mask),
+                  _lib.ptr(bias), act, _lib.ptr(alpha), _lib.ptr(Y), _s(dev))
+        ctx.save_for_backward(x, W, att_src, att_dst, XP, a_s, a_d, alpha, Y, mask)
+        ctx.graph, ctx.heads, ctx.slope, ctx.act = graph, heads, slope, act
+        ctx.has_bias = bias is not None
+        ctx.att_shape = (1, heads, C)
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        x, W, att_src, att_dst, XP, a_s, a_d, alpha, Y, mask = ctx.saved_tensors
+        csr = ctx.graph.csr("gat")
+        M, HC = Y.shape
+        H = ctx.heads
+        C = HC // H
+        dev = Y.device
+        dZ = torch.empty_like(Y)
+        da_e = torch.empty_like(alpha)
+        da_d = torch.empty(M, H, dtype=torch.float32, device=dev)
+        _lib.call("lgnn_gat_bwd_edge", _lib.ptr(csr.rowptr), _lib.ptr(csr.col), _lib.ptr(XP),
+                  _lib.ptr(a_s), _lib.ptr(a_d), _lib.ptr(alpha), _lib.ptr(mask),
+                  _lib.ptr(_f32c(dY)), _lib.ptr(Y), ctx.act, M, H, C, float(ctx.slope),
+                  _lib.ptr(dZ), _lib.ptr(da_e), _lib.ptr(da_d), _s(dev))
+        P = _lib.load().lgnn_gat_bwd_num_partials(M)
+        part = torch.empty(P * 3 * HC, dtype=torch.float32, device=dev)
+        dXP = torch.empty_like(XP)
+        _lib.call("lgnn_gat_bwd_node", _lib.ptr(csr.tptr), _lib.ptr(csr.tidx),
+                  _lib.ptr(csr.tmap), _lib.ptr(alpha), _lib.ptr(mask), _lib.ptr(da_e),
+                  _lib.ptr(da_d), _lib.ptr(dZ), _lib.ptr(XP), _lib.ptr(att_src),
+                  _lib.ptr(att_dst), M, H, C, _lib.ptr(dXP), _lib.ptr(part), P, _s(dev))
+        red = torch.empty(3 * HC, dtype=torch.float32, device=dev)
+        _lib.call("lgnn_reduce_partials", _lib.ptr(part), P, 3 * HC, _lib.ptr(red), _s(dev))
+        want_dx = ctx.needs_input_grad[0]
+        dx, dW, _ = linear_bwd(_lib.LGNN_GRAD_DIRECT, dXP, H=None, act=_lib.LGNN_ACT_NONE, X=x,
+                               W=W, want_dx=want_dx, want_db=False)
+        datt_s = red[:HC].view(ctx.att_shape)
+        datt_d = red[HC:2 * HC].view(ctx.att_shape)
+        dbias = red[2 * HC:] if ctx.has_bias else None
+        return dx, dW, datt_s, datt_d, dbias, None, None, None, None, None
+
+
+def gat_conv(x, W, att_src, att_dst, bias, graph: Graph, heads: int, slope: float = 0.2,
+             mask=None, act: int = _lib.LGNN_ACT_NONE):
+    return _GATConv.apply(x, W, att_src, att_dst, bias, graph, heads, slope, mask, act)

@@ -1,0 +1,122 @@
+"""GPU parity of the GAT path (reference gat.py:17-59: in_proj -> ELU(GATConv) x L -> mean pool
+-> out_proj; BASELINE config C3 shapes: d_in = 1025 (1024 encoder channels + lesion class),
+4 heads, h = 128, k = 6, log-normal graph sizes, MSE regression with clamp) vs the CPU oracle.
+fp32 tolerances as tests/test_gpu_gcn.py; attention rows checked to sum to 1."""
+import pytest
+import torch
+
+import oracle.pyg_ref as ref
+from lesion_gnn_amd import ops, synth
+from lesion_gnn_amd.graph import Graph
+from lesion_gnn_amd.models.gat import GAT
+
+pytestmark = pytest.mark.gpu
+
+
+def make_pair(d_in, hidden, classes, heads, seed=1234):
+    torch.manual_seed(seed)
+    ours = GAT(d_in, hidden, classes, heads=heads, dropout=0.0)
+    oref = ref.GAT(d_in, hidden, classes, heads=heads, dropout=0.0)
+    oref.load_state_dict(ours.state_dict())
+    return ours, oref
+
+
+def step(model, b, device, loss_kind, classes):
+    logits = model(b.x.to(device), b.edge_index.to(device), b.batch.to(device), b.num_graphs)
+    loss = ref.criterion(loss_kind, logits, b.y.to(device), classes)
+    model.zero_grad(set_to_none=True)
+    loss.backward()
+    return (logits.detach().cpu(), loss.detach().cpu(),
+            {k: p.grad.detach().cpu() for k, p in model.named_parameters()})
+
+
+def check(ours, oref, b, cuda, loss_kind="MSE", classes=5):
+    lo, losso, go = step(ours.to(cuda).train(), b, cuda, loss_kind, classes)
+    lr_, lossr, gr = step(oref.train(), b, "cpu", loss_kind, classes)
+    torch.testing.assert_close(lo, lr_, rtol=0, atol=1e-4)
+    torch.testing.assert_close(losso, lossr, rtol=1e-5, atol=1e-6)
+    for k in gr:
+        scale = gr[k].abs().max().item()
+        torch.testing.assert_close(go[k], gr[k], rtol=0, atol=max(1e-4 * scale, 1e-6),
+                                   msg=lambda m: f"{k}: {m}")
+
+
+def test_gat_c3_shape(cuda):
+    """C3: 3-layer GAT, 4 heads, d_in 1025, lognormal N, k = 6, MSE (256 graphs, fp32)."""
+    b = synth.make_batch(256, k=6, d_in=1025, seed=3, sizes="lognormal", last_channel_class=True)
+    ours, oref = make_pair(1025, [128] * 4, 1, heads=4)
+    check(ours, oref, b, cuda)
+
+
+def test_gat_reference_config(cuda):
+    """configs/config.py:47,59-64: hiddden_channels=[128]*4, heads=2 (C = 64), KNN k=6 loop."""
+    b = synth.make_batch(64, k=6, d_in=64, seed=10, sizes="lognormal")
+    ours, oref = make_pair(64, [128] * 4, 1, heads=2)
+    check(ours, oref, b, cuda)
+
+
+@pytest.mark.parametrize("heads,hidden", [(1, [128, 128]), (8, [128, 128]), (2, [64, 256, 32]),
+                                          (4, [48, 96, 48])])
+def test_gat_heads_and_widths(cuda, heads, hidden):
+    b = synth.make_batch(24, k=5, d_in=32, num_classes=3, seed=11, sizes="lognormal")
+    ours, oref = make_pair(32, hidden, 3, heads=heads)
+    check(ours, oref, b, cuda, "CE", 3)
+
+
+def test_gat_irregular_edges(cuda):
+    """loop=False input (self loops added by the conv), duplicated edges, explicit self loops,
+    shuffled edge order, 1-node graphs."""
+    sizes = [1, 3, 7, 64, 2, 130, 9]
+    b = synth.make_batch(len(sizes), k=6, d_in=16, seed=12, sizes=sizes, loop=False)
+    ei = b.edge_index
+    perm = torch.randperm(ei.size(1), generator=torch.Generator().manual_seed(0))
+    extra = torch.tensor([[5, 5, 5, 20, 20], [5, 5, 6, 21, 21]])
+    b.edge_index = torch.cat([ei[:, perm], extra], 1)
+    ours, oref = make_pair(16, [32, 32, 32], 1, heads=2)
+    check(ours, oref, b, cuda)
+
+
+def test_gat_alpha_rows_sum_to_one(cuda):
+    b = synth.make_batch(16, k=6, d_in=32, seed=13, sizes="lognormal")
+    torch.manual_seed(0)
+    m = GAT(32, [64, 64], 1, heads=4, dropout=0.0).to(cuda)
+    g = Graph(b.edge_index.to(cuda), b.num_nodes)
+    conv = m.convs[0]
+    x = torch.randn(b.num_nodes, 64, device=cuda)
+    ctxout = ops._GATConv.forward  # noqa: F841 (documented entry)
+    csr = g.csr("gat")
+    y = ops.gat_conv(x, conv.lin.weight, conv.att_src, conv.att_dst, conv.bias, g, 4)
+    assert torch.isfinite(y).all()
+    # recompute alpha through the C ABI and check row sums
+    from lesion_gnn_amd import _lib
+    XP = ops.linear_fwd(x, conv.lin.weight.detach(), None, _lib.LGNN_ACT_NONE)
+    a_s = torch.empty(b.num_nodes, 4, device=cuda)
+    a_d = torch.empty(b.num_nodes, 4, device=cuda)
+    _lib.call("lgnn_gat_att", XP.data_ptr(), b.num_nodes, 4, 16,
+              conv.att_src.detach().contiguous().data_ptr(),
+              conv.att_dst.detach().contiguous().data_ptr(), a_s.data_ptr(), a_d.data_ptr(),
+              _lib.stream())
+    alpha = torch.empty(csr.col.numel(), 4, device=cuda)
+    out = torch.empty(b.num_nodes, 64, device=cuda)
+    _lib.call("lgnn_gat_fwd", csr.rowptr.data_ptr(), csr.col.data_ptr(), XP.data_ptr(),
+              a_s.data_ptr(), a_d.data_ptr(), b.num_nodes, 4, 16, 0.2, None, None, 0,
+              alpha.data_ptr(), out.data_ptr(), _lib.stream())
+    nnz = int(csr.rowptr[-1])
+    rows = torch.repeat_interleave(torch.arange(b.num_nodes, device=cuda),
+                                   (csr.rowptr[1:] - csr.rowptr[:-1]).long())
+    s = torch.zeros(b.num_nodes, 4, device=cuda).index_add_(0, rows, alpha[:nnz])
+    torch.testing.assert_close(s, torch.ones_like(s), rtol=0, atol=1e-6)
+
+
+def test_gat_dropout_and_determinism(cuda):
+    b = synth.make_batch(32, k=6, d_in=64, seed=14, sizes="lognormal")
+    torch.manual_seed(0)
+    m = GAT(64, [128] * 4, 1, heads=2, dropout=0.35).to(cuda).train()
+    out = m(b.x.to(cuda), b.edge_index.to(cuda), b.batch.to(cuda))
+    out.sum().backward()
+    assert torch.isfinite(out).all()
+    assert all(torch.isfinite(p.grad).all() for p in m.parameters())
+    m.eval()
+    o1 = m(b.x.to(cuda), b.edge_index.to(cuda), b.batch.to(cuda))
+    o2 = m(b.x.to(cuda), b.edge_index.to(cuda), b.batch.to(cuda))
+    assert torch.equal(o1, o2)

@@ -16,7 +16,7 @@ from tests.test_golden import golden_state, load
 
 pytestmark = pytest.mark.gpu
 
-OURS = {"gcn": models.GCN, "gin": models.GIN}
+OURS = {"gcn": models.GCN, "gin": models.GIN, "gat": models.GAT}
 CASES = [n for n, c in mg.CASES.items() if c[0] in OURS]
 
 
