@@ -190,7 +190,7 @@ int lgnn_bn_bwd_apply(const float* dA, const float* Z, const float* mask, int64_
  * concat=True, negative_slope, add_self_loops=True, bias=True) + the model's F.elu (gat.py:51).
  * XP = lin(x) [M, H*C] (lgnn_node_linear_fwd without bias). Graph: the LGNN_LOOPS_READD CSR
  * (remove_self_loops + add_self_loops). Per-edge arrays are [cap, H] in target-CSR order.
- * Shapes: C in {4,8,16,32,64,128}, H*C <= 512. edge_mask (nullable): attention dropout keep-mask
+ * Shapes: C a power of two in [4, 512], H*C <= 512. edge_mask (nullable): attention dropout keep-mask
  * already scaled by 1/(1-p).
  * ------------------------------------------------------------------------------------------- */
 /* a_s[i,h] = <XP[i,h,:], att_src[h,:]>, a_d likewise with att_dst (the alpha_src/alpha_dst sums) */

@@ -48,28 +48,56 @@ __device__ __forceinline__ Lane lane_row() {
   return l;
 }
 
+// Feature passes. A half wave covers NS strips of 128 features per pass: NS = 1 when C <= 128
+// (a pass holds 128/C whole heads; head group = C/4 adjacent lanes), NS = C/128 when C > 128
+// (a pass is one head; its dot products add the NS strip partials, then all 32 lanes).
+template <int NS>
+struct Pass {
+  int f[NS];     // feature of sub-strip s for this lane
+  bool act[NS];  // f < HC
+  int fc[NS];    // clamped feature (loads stay in bounds)
+  int head, G;
+  bool leader;
+  __device__ __forceinline__ Pass(int p, int li, int HC, int C) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      f[s] = p * 128 * NS + s * 128 + 4 * li;
+      act[s] = f[s] < HC;
+      fc[s] = act[s] ? f[s] : HC - 4;
+    }
+    head = fc[0] / C;
+    G = NS == 1 ? C / 4 : 32;
+    leader = act[0] && (li % G) == 0;
+  }
+};
+
+__device__ __forceinline__ int num_passes(int HC, int NS) { return (HC + 128 * NS - 1) / (128 * NS); }
+
 // ------------------------------------------------------------------------------------------
 // a_s / a_d
 // ------------------------------------------------------------------------------------------
+template <int NS>
 __global__ __launch_bounds__(NT) void k_gat_att(const float* __restrict__ XP, int64_t M, int H,
                                                 int C, const float* __restrict__ att_src,
                                                 const float* __restrict__ att_dst,
                                                 float* __restrict__ a_s, float* __restrict__ a_d) {
   const Lane L = lane_row();
   if (L.row >= M) return;
-  const int HC = H * C, G = C / 4;
-  for (int s0 = 0; s0 < HC; s0 += 128) {
-    const int f = s0 + 4 * L.li;
-    const bool act = f < HC;
-    const int fc = act ? f : HC - 4;
-    const f32x4 v = ld4(XP + L.row * HC + fc);
-    float ps = act ? dot4(v, ld4(att_src + fc)) : 0.f;
-    float pd = act ? dot4(v, ld4(att_dst + fc)) : 0.f;
-    ps = group_sum(ps, G);
-    pd = group_sum(pd, G);
-    if (act && (L.li % G) == 0) {
-      a_s[L.row * H + f / C] = ps;
-      a_d[L.row * H + f / C] = pd;
+  const int HC = H * C;
+  for (int p = 0; p < num_passes(HC, NS); ++p) {
+    const Pass<NS> P(p, L.li, HC, C);
+    float ps = 0.f, pd = 0.f;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const f32x4 v = ld4(XP + L.row * HC + P.fc[s]);
+      ps += P.act[s] ? dot4(v, ld4(att_src + P.fc[s])) : 0.f;
+      pd += P.act[s] ? dot4(v, ld4(att_dst + P.fc[s])) : 0.f;
+    }
+    ps = group_sum(ps, P.G);
+    pd = group_sum(pd, P.G);
+    if (P.leader) {
+      a_s[L.row * H + P.head] = ps;
+      a_d[L.row * H + P.head] = pd;
     }
   }
 }
@@ -77,7 +105,7 @@ __global__ __launch_bounds__(NT) void k_gat_att(const float* __restrict__ XP, in
 // ------------------------------------------------------------------------------------------
 // forward: softmax over each target row + weighted sum of source rows (+ bias, ELU)
 // ------------------------------------------------------------------------------------------
-template <int ACT>
+template <int ACT, int NS>
 __global__ __launch_bounds__(NT) void k_gat_fwd(const int32_t* __restrict__ rowptr,
                                                 const int32_t* __restrict__ col,
                                                 const float* __restrict__ XP,
@@ -86,15 +114,14 @@ __global__ __launch_bounds__(NT) void k_gat_fwd(const int32_t* __restrict__ rowp
                                                 int C, float slope, const float* __restrict__ mask,
                                                 const float* __restrict__ bias,
                                                 float* __restrict__ alpha, float* __restrict__ Y) {
+  constexpr int EBN = EB / NS;
   const Lane L = lane_row();
   if (L.row >= M) return;
-  const int HC = H * C, G = C / 4;
+  const int HC = H * C;
   const int e0 = rowptr[L.row], e1 = rowptr[L.row + 1];
-  for (int s0 = 0; s0 < HC; s0 += 128) {
-    const int f = s0 + 4 * L.li;
-    const bool act = f < HC;
-    const int fc = act ? f : HC - 4;
-    const int head = fc / C;
+  for (int p = 0; p < num_passes(HC, NS); ++p) {
+    const Pass<NS> P(p, L.li, HC, C);
+    const int head = P.head;
     const float ad = a_d[L.row * H + head];
     // pass 1: row max of the logits (PyG: scatter max of the detached logits)
     float m = -INFINITY;
@@ -124,38 +151,45 @@ __global__ __launch_bounds__(NT) void k_gat_fwd(const int32_t* __restrict__ rowp
     }
     sum += EPS16;
     // pass 3: alpha, message sum
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    const bool leader = act && (L.li % G) == 0;
-    for (int e = e0; e < e1; e += EB) {
-      int c[EB];
-      float a[EB];
+    f32x4 acc[NS];
 #pragma unroll
-      for (int u = 0; u < EB; ++u) {
+    for (int s = 0; s < NS; ++s) acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int e = e0; e < e1; e += EBN) {
+      int c[EBN];
+      float a[EBN];
+#pragma unroll
+      for (int u = 0; u < EBN; ++u) {
         const int ee = e + u < e1 ? e + u : e0;
         c[u] = col[ee];
         a[u] = a_s[(int64_t)c[u] * H + head];
       }
-      f32x4 xv[EB];
+      f32x4 xv[EBN][NS];
 #pragma unroll
-      for (int u = 0; u < EB; ++u) xv[u] = ld4(XP + (int64_t)c[u] * HC + fc);
+      for (int u = 0; u < EBN; ++u)
 #pragma unroll
-      for (int u = 0; u < EB; ++u) {
+        for (int s = 0; s < NS; ++s) xv[u][s] = ld4(XP + (int64_t)c[u] * HC + P.fc[s]);
+#pragma unroll
+      for (int u = 0; u < EBN; ++u) {
         if (e + u < e1) {
           float al = expf(leaky(a[u] + ad, slope) - m) / sum;
-          if (leader && alpha) alpha[(int64_t)(e + u) * H + head] = al;
+          if (P.leader && alpha) alpha[(int64_t)(e + u) * H + head] = al;
           if (mask) al *= mask[(int64_t)(e + u) * H + head];
-          acc += al * xv[u];
+#pragma unroll
+          for (int s = 0; s < NS; ++s) acc[s] += al * xv[u][s];
         }
       }
     }
-    if (act) {
-      const f32x4 bv = bias ? ld4(bias + fc) : f32x4{0.f, 0.f, 0.f, 0.f};
-      f32x4 o = acc + bv;
-      if (ACT == LGNN_ACT_ELU) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = elu_f(o[j]);
+    for (int s = 0; s < NS; ++s) {
+      if (P.act[s]) {
+        const f32x4 bv = bias ? ld4(bias + P.fc[s]) : f32x4{0.f, 0.f, 0.f, 0.f};
+        f32x4 o = acc[s] + bv;
+        if (ACT == LGNN_ACT_ELU) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = elu_f(o[j]);
+        }
+        st4(Y + L.row * HC + P.f[s], o);
       }
-      st4(Y + L.row * HC + f, o);
     }
   }
 }
@@ -167,74 +201,70 @@ __global__ __launch_bounds__(NT) void k_gat_fwd(const int32_t* __restrict__ rowp
 //   de_ij = alpha_ij (dal_ij - s_i);  da_ij = de_ij * leaky'(a_s[j] + a_d[i])
 //   da_e[ij] = da_ij (per edge),  da_d[i] = sum_j da_ij
 // ------------------------------------------------------------------------------------------
-template <int ACT>
+template <int ACT, int NS>
 __global__ __launch_bounds__(NT) void k_gat_bwd_edge(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const float* __restrict__ XP, const float* __restrict__ a_s, const float* __restrict__ a_d,
     const float* __restrict__ alpha, const float* __restrict__ mask, const float* __restrict__ dY,
     const float* __restrict__ Y, int64_t M, int H, int C, float slope, float* __restrict__ dZ,
     float* __restrict__ da_e, float* __restrict__ da_d) {
+  constexpr int EBN = EB / NS;
   const Lane L = lane_row();
   if (L.row >= M) return;
-  const int HC = H * C, G = C / 4;
+  const int HC = H * C;
   const int e0 = rowptr[L.row], e1 = rowptr[L.row + 1];
-  for (int s0 = 0; s0 < HC; s0 += 128) {
-    const int f = s0 + 4 * L.li;
-    const bool act = f < HC;
-    const int fc = act ? f : HC - 4;
-    const int head = fc / C;
-    const bool leader = act && (L.li % G) == 0;
-    f32x4 dz = ld4(dY + L.row * HC + fc);
-    if (ACT == LGNN_ACT_ELU) {
-      const f32x4 y = ld4(Y + L.row * HC + fc);
+  for (int p = 0; p < num_passes(HC, NS); ++p) {
+    const Pass<NS> P(p, L.li, HC, C);
+    const int head = P.head;
+    f32x4 dz[NS];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) dz[j] *= elu_grad_from_out(y[j]);
-    }
-    if (!act) dz = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (act) st4(dZ + L.row * HC + f, dz);
-    const float ad = a_d[L.row * H + head];
-    // pass 1: s_i
-    float s = 0.f;
-    for (int e = e0; e < e1; e += EB) {
-      int c[EB];
+    for (int s = 0; s < NS; ++s) {
+      dz[s] = ld4(dY + L.row * HC + P.fc[s]);
+      if (ACT == LGNN_ACT_ELU) {
+        const f32x4 y = ld4(Y + L.row * HC + P.fc[s]);
 #pragma unroll
-      for (int u = 0; u < EB; ++u) c[u] = col[e + u < e1 ? e + u : e0];
-      f32x4 xv[EB];
-#pragma unroll
-      for (int u = 0; u < EB; ++u) xv[u] = ld4(XP + (int64_t)c[u] * HC + fc);
-#pragma unroll
-      for (int u = 0; u < EB; ++u) {
-        const int ee = e + u < e1 ? e + u : e0;
-        float d = group_sum(dot4(dz, xv[u]), G);
-        if (mask) d *= mask[(int64_t)ee * H + head];
-        const float al = alpha[(int64_t)ee * H + head];
-        if (e + u < e1) s += al * d;
+        for (int j = 0; j < 4; ++j) dz[s][j] *= elu_grad_from_out(y[j]);
       }
+      if (!P.act[s]) dz[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (P.act[s]) st4(dZ + L.row * HC + P.f[s], dz[s]);
     }
-    // pass 2: per-edge logit gradients
-    float dad = 0.f;
-    for (int e = e0; e < e1; e += EB) {
-      int c[EB];
+    const float ad = a_d[L.row * H + head];
+    // two sweeps over the row: sweep 0 accumulates s_i, sweep 1 emits the logit gradients
+    float s_i = 0.f, dad = 0.f;
+#pragma unroll 1
+    for (int sweep = 0; sweep < 2; ++sweep) {
+      for (int e = e0; e < e1; e += EBN) {
+        int c[EBN];
 #pragma unroll
-      for (int u = 0; u < EB; ++u) c[u] = col[e + u < e1 ? e + u : e0];
-      f32x4 xv[EB];
+        for (int u = 0; u < EBN; ++u) c[u] = col[e + u < e1 ? e + u : e0];
+        f32x4 xv[EBN][NS];
 #pragma unroll
-      for (int u = 0; u < EB; ++u) xv[u] = ld4(XP + (int64_t)c[u] * HC + fc);
+        for (int u = 0; u < EBN; ++u)
 #pragma unroll
-      for (int u = 0; u < EB; ++u) {
-        const int ee = e + u < e1 ? e + u : e0;
-        float d = group_sum(dot4(dz, xv[u]), G);
-        if (mask) d *= mask[(int64_t)ee * H + head];
-        const float al = alpha[(int64_t)ee * H + head];
-        const float pre = a_s[(int64_t)c[u] * H + head] + ad;
-        const float da = al * (d - s) * (pre > 0.f ? 1.f : slope);
-        if (e + u < e1) {
-          dad += da;
-          if (leader) da_e[(int64_t)ee * H + head] = da;
+          for (int s = 0; s < NS; ++s) xv[u][s] = ld4(XP + (int64_t)c[u] * HC + P.fc[s]);
+#pragma unroll
+        for (int u = 0; u < EBN; ++u) {
+          const int ee = e + u < e1 ? e + u : e0;
+          float part = 0.f;
+#pragma unroll
+          for (int s = 0; s < NS; ++s) part += dot4(dz[s], xv[u][s]);
+          float d = group_sum(part, P.G);
+          if (mask) d *= mask[(int64_t)ee * H + head];
+          const float al = alpha[(int64_t)ee * H + head];
+          if (sweep == 0) {
+            if (e + u < e1) s_i += al * d;
+          } else {
+            const float pre = a_s[(int64_t)c[u] * H + head] + ad;
+            const float da = al * (d - s_i) * (pre > 0.f ? 1.f : slope);
+            if (e + u < e1) {
+              dad += da;
+              if (P.leader) da_e[(int64_t)ee * H + head] = da;
+            }
+          }
         }
       }
     }
-    if (leader) da_d[L.row * H + head] = dad;
+    if (P.leader) da_d[L.row * H + head] = dad;
   }
 }
 
@@ -244,6 +274,7 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_edge(
 // plus per-block column partials: [0] datt_src = sum_j (sum_i da_ij) xp_j,
 //                                 [1] datt_dst = sum_j da_d[j] xp_j,  [2] dbias = sum_j dZ_j.
 // Persistent over rows (block b owns rows b*8 + hw + 8*P*t), fixed-order in-block combine.
+// Features are walked in strips of 128 (strip st = features [128 st, 128 st + 128)).
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(NT) void k_gat_bwd_node(
     const int32_t* __restrict__ tptr, const int32_t* __restrict__ tidx,
@@ -324,9 +355,12 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_node(
   }
 }
 
+// C a power of two in [4, 512] (the reference sweep: widths 32..512, heads 1/2/4/8), H*C <= 512
 inline bool shape_ok(int H, int C) {
-  return H > 0 && C >= 4 && C <= 128 && (128 % C) == 0 && H * C <= MAXS * 128;
+  return H > 0 && C >= 4 && C <= 512 && (C & (C - 1)) == 0 && H * C <= MAXS * 128;
 }
+
+inline int ns_of(int C) { return C <= 128 ? 1 : C / 128; }
 
 inline unsigned row_grid(int64_t M) { return (unsigned)((M + RB - 1) / RB); }
 
@@ -337,8 +371,15 @@ extern "C" int lgnn_gat_att(const float* XP, int64_t M, int H, int C, const floa
   if (M < 0 || !shape_ok(H, C) || !att_src || !att_dst || (M > 0 && (!XP || !a_s || !a_d)))
     return LGNN_EINVAL;
   if (M == 0) return LGNN_OK;
-  hipLaunchKernelGGL(k_gat_att, dim3(row_grid(M)), dim3(NT), 0, as_stream(stream), XP, M, H, C,
-                     att_src, att_dst, a_s, a_d);
+#define LGNN_ATT(NS_)                                                                       \
+  hipLaunchKernelGGL(k_gat_att<NS_>, dim3(row_grid(M)), dim3(NT), 0, as_stream(stream), XP, M, H, \
+                     C, att_src, att_dst, a_s, a_d)
+  switch (ns_of(C)) {
+    case 1: LGNN_ATT(1); break;
+    case 2: LGNN_ATT(2); break;
+    default: LGNN_ATT(4); break;
+  }
+#undef LGNN_ATT
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
 }
@@ -351,14 +392,22 @@ extern "C" int lgnn_gat_fwd(const int32_t* rowptr, const int32_t* col, const flo
     return LGNN_EINVAL;
   if (M > 0 && (!rowptr || !col || !XP || !a_s || !a_d || !Y)) return LGNN_EINVAL;
   if (M == 0) return LGNN_OK;
-  if (act == LGNN_ACT_ELU)
-    hipLaunchKernelGGL(k_gat_fwd<LGNN_ACT_ELU>, dim3(row_grid(M)), dim3(NT), 0, as_stream(stream),
-                       rowptr, col, XP, a_s, a_d, M, H, C, negative_slope, edge_mask, bias, alpha,
-                       Y);
-  else
-    hipLaunchKernelGGL(k_gat_fwd<LGNN_ACT_NONE>, dim3(row_grid(M)), dim3(NT), 0,
-                       as_stream(stream), rowptr, col, XP, a_s, a_d, M, H, C, negative_slope,
-                       edge_mask, bias, alpha, Y);
+#define LGNN_GF(A_, NS_)                                                                     \
+  hipLaunchKernelGGL((k_gat_fwd<A_, NS_>), dim3(row_grid(M)), dim3(NT), 0, as_stream(stream),    \
+                     rowptr, col, XP, a_s, a_d, M, H, C, negative_slope, edge_mask, bias, alpha, Y)
+#define LGNN_GF_NS(A_)                    \
+  switch (ns_of(C)) {                     \
+    case 1: LGNN_GF(A_, 1); break;        \
+    case 2: LGNN_GF(A_, 2); break;        \
+    default: LGNN_GF(A_, 4); break;       \
+  }
+  if (act == LGNN_ACT_ELU) {
+    LGNN_GF_NS(LGNN_ACT_ELU)
+  } else {
+    LGNN_GF_NS(LGNN_ACT_NONE)
+  }
+#undef LGNN_GF_NS
+#undef LGNN_GF
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
 }
@@ -374,14 +423,23 @@ extern "C" int lgnn_gat_bwd_edge(const int32_t* rowptr, const int32_t* col, cons
     return LGNN_EINVAL;
   if (act == LGNN_ACT_ELU && M > 0 && !Y) return LGNN_EINVAL;
   if (M == 0) return LGNN_OK;
-  if (act == LGNN_ACT_ELU)
-    hipLaunchKernelGGL(k_gat_bwd_edge<LGNN_ACT_ELU>, dim3(row_grid(M)), dim3(NT), 0,
-                       as_stream(stream), rowptr, col, XP, a_s, a_d, alpha, edge_mask, dY, Y, M,
-                       H, C, negative_slope, dZ, da_e, da_d);
-  else
-    hipLaunchKernelGGL(k_gat_bwd_edge<LGNN_ACT_NONE>, dim3(row_grid(M)), dim3(NT), 0,
-                       as_stream(stream), rowptr, col, XP, a_s, a_d, alpha, edge_mask, dY, Y, M,
-                       H, C, negative_slope, dZ, da_e, da_d);
+#define LGNN_GB(A_, NS_)                                                                   \
+  hipLaunchKernelGGL((k_gat_bwd_edge<A_, NS_>), dim3(row_grid(M)), dim3(NT), 0,               \
+                     as_stream(stream), rowptr, col, XP, a_s, a_d, alpha, edge_mask, dY, Y, M, \
+                     H, C, negative_slope, dZ, da_e, da_d)
+#define LGNN_GB_NS(A_)                    \
+  switch (ns_of(C)) {                     \
+    case 1: LGNN_GB(A_, 1); break;        \
+    case 2: LGNN_GB(A_, 2); break;        \
+    default: LGNN_GB(A_, 4); break;       \
+  }
+  if (act == LGNN_ACT_ELU) {
+    LGNN_GB_NS(LGNN_ACT_ELU)
+  } else {
+    LGNN_GB_NS(LGNN_ACT_NONE)
+  }
+#undef LGNN_GB_NS
+#undef LGNN_GB
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
 }

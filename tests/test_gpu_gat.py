@@ -56,11 +56,22 @@ def test_gat_reference_config(cuda):
 
 
 @pytest.mark.parametrize("heads,hidden", [(1, [128, 128]), (8, [128, 128]), (2, [64, 256, 32]),
-                                          (4, [48, 96, 48])])
+                                          (1, [64, 256, 64]), (1, [32, 512]), (2, [512, 512]),
+                                          (8, [32, 32])])
 def test_gat_heads_and_widths(cuda, heads, hidden):
     b = synth.make_batch(24, k=5, d_in=32, num_classes=3, seed=11, sizes="lognormal")
     ours, oref = make_pair(32, hidden, 3, heads=heads)
     check(ours, oref, b, cuda, "CE", 3)
+
+
+def test_gat_unsupported_head_width_raises(cuda):
+    """Head widths must be powers of two in [4, 512] (the reference sweep's space)."""
+    from lesion_gnn_amd import _lib
+
+    b = synth.make_batch(2, k=4, d_in=8, seed=1)
+    m = GAT(8, [48, 96], 1, heads=4, dropout=0.0).to(cuda)  # C = 24
+    with pytest.raises(_lib.LgnnError):
+        m(b.x.to(cuda), b.edge_index.to(cuda), b.batch.to(cuda))
 
 
 def test_gat_irregular_edges(cuda):
