@@ -101,7 +101,30 @@ class Graph:
         return int(self.csr(kind).err.item())
 
 
+def adj_t_to_edge_index(adj_t) -> torch.Tensor:
+    """The reference's `adj_t` input (ToSparseTensor, datasets/datamodule.py:44-45; selected at
+    gin.py:59-62 / gat.py:87-90): a transposed adjacency whose row is the TARGET and column the
+    SOURCE. Accepts a torch_sparse.SparseTensor (duck-typed: `.storage.row()/.col()`) or a torch
+    sparse COO/CSR tensor. Returns edge_index [2, E] = (source, target) in row-major order."""
+    if hasattr(adj_t, "storage") and hasattr(adj_t.storage, "row"):
+        row, col = adj_t.storage.row(), adj_t.storage.col()
+    elif isinstance(adj_t, torch.Tensor) and adj_t.layout == torch.sparse_csr:
+        crow = adj_t.crow_indices()
+        col = adj_t.col_indices()
+        row = torch.repeat_interleave(torch.arange(crow.numel() - 1, device=crow.device),
+                                      crow[1:] - crow[:-1])
+    elif isinstance(adj_t, torch.Tensor) and adj_t.layout == torch.sparse_coo:
+        idx = adj_t.coalesce().indices()
+        row, col = idx[0], idx[1]
+    else:
+        raise TypeError(f"unsupported adjacency input {type(adj_t)}")
+    return torch.stack([col.to(torch.int64), row.to(torch.int64)])
+
+
 def as_graph(edge_index, num_nodes: int, batch=None, num_graphs=None) -> Graph:
+    if not isinstance(edge_index, (Graph, torch.Tensor)) or (
+            isinstance(edge_index, torch.Tensor) and edge_index.layout != torch.strided):
+        edge_index = adj_t_to_edge_index(edge_index)
     if isinstance(edge_index, Graph):
         g = edge_index
         if batch is not None and g.batch is None:

@@ -62,8 +62,8 @@ class BaseModelConfig:
 def make_criterion(cfg: OptimizerConfig) -> nn.Module:
     kind = LossType(cfg.loss_type)
     if kind is LossType.CE:
-        weight = cfg.class_weights._value  # optional: uniform when unset
-        return nn.CrossEntropyLoss(weight=weight)
+        # reference base.py:93-94 reads the placeholder (unset -> ValueError, as there)
+        return nn.CrossEntropyLoss(weight=cfg.class_weights.value)
     if kind is LossType.MSE:
         return nn.MSELoss()
     return nn.SmoothL1Loss()
@@ -82,6 +82,7 @@ class BaseModule(nn.Module):
         self.criterion = make_criterion(opt)
         self.lr, self.weight_decay = opt.lr, opt.weight_decay
         self.optimizer_algo = OptimizerAlgo(opt.algo)
+        self.lr_scheduler_config = opt.lr_scheduler
 
     @property
     def is_regression(self) -> bool:
@@ -102,10 +103,21 @@ class BaseModule(nn.Module):
         y = batch.y.float() if self.is_regression else batch.y
         return self.criterion(logits, y)
 
-    def configure_optimizers(self) -> torch.optim.Optimizer:
+    def configure_optimizers(self):
+        """Reference base.py:162-188: the optimizer, plus a torch.optim.lr_scheduler by name
+        (the pl_bolts LinearWarmupCosineAnnealingLR is not available in this build)."""
         ctor = {
             OptimizerAlgo.ADAM: torch.optim.Adam,
             OptimizerAlgo.ADAMW: torch.optim.AdamW,
             OptimizerAlgo.SGD: torch.optim.SGD,
         }[self.optimizer_algo]
-        return ctor(self.parameters(), lr=self.lr, weight_decay=self.weight_decay)
+        optimizer = ctor(self.parameters(), lr=self.lr, weight_decay=self.weight_decay)
+        sc = self.lr_scheduler_config
+        if sc is None:
+            return optimizer
+        if sc.name == "LinearWarmupCosineAnnealingLR":
+            raise NotImplementedError("pl_bolts LinearWarmupCosineAnnealingLR is not available")
+        scheduler = getattr(torch.optim.lr_scheduler, sc.name)(optimizer, **sc.kwargs)
+        return {"optimizer": optimizer,
+                "lr_scheduler": {"scheduler": scheduler, "monitor": sc.monitor,
+                                 "interval": sc.interval, "frequency": sc.frequency}}

@@ -1,0 +1,99 @@
+"""Data-parallel HIP path on one GPU box: 2 ranks (processes) on cuda:0 over gloo (RCCL needs one
+GPU per rank; the collectives are the same torch.distributed calls bench.py makes on RCCL).
+
+* GCN: sharded batch + flat gradient all-reduce == single-process full-batch gradients.
+* GIN with SyncBN: all-reduced BatchNorm sums make 2 replicas reproduce the single-process
+  full-batch forward AND gradients.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+B, N, K = 16, 40, 6
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def build(kind):
+    from lesion_gnn_amd.models import GCN, GIN
+
+    torch.manual_seed(5)
+    if kind == "gcn":
+        return GCN(32, [64, 64, 64], 5, 0.0)
+    return GIN(32, [64, 64, 64], 5, 0.0, pool="add")
+
+
+def shard(b, g0, g1):
+    n0, n1 = int(b.ptr[g0]), int(b.ptr[g1])
+    m = (b.edge_index[1] >= n0) & (b.edge_index[1] < n1)
+    return b.x[n0:n1], b.edge_index[:, m] - n0, b.batch[n0:n1] - g0, b.y[g0:g1]
+
+
+def worker(rank, world, port, kind, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from lesion_gnn_amd import dist as ldist
+    from lesion_gnn_amd import synth
+
+    dev = torch.device("cuda:0")
+    b = synth.make_batch(B, n=N, k=K, d_in=32, seed=17)
+    m = build(kind).to(dev).train()
+    if kind == "gin":
+        m.set_sync_bn(dist.group.WORLD)
+    g0, g1 = rank * B // world, (rank + 1) * B // world
+    x, ei, bt, y = (t.to(dev) for t in shard(b, g0, g1))
+    logits = m(x, ei, bt, g1 - g0)
+    torch.nn.functional.cross_entropy(logits, y).backward()
+    ldist.allreduce_grads(list(m.parameters()), g1 - g0, B)
+    out = {"logits": logits.detach().cpu(),
+           "grads": {k: p.grad.detach().cpu() for k, p in m.named_parameters()}}
+    if kind == "gin":
+        out["state"] = {k: v.detach().cpu() for k, v in m.state_dict().items() if "running" in k}
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["gcn", "gin"])
+def test_two_ranks_match_full_batch(cuda, kind):
+    from lesion_gnn_amd import synth
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, 2, port, kind, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    b = synth.make_batch(B, n=N, k=K, d_in=32, seed=17)
+    m = build(kind).to(cuda).train()
+    logits = m(b.x.to(cuda), b.edge_index.to(cuda), b.batch.to(cuda), B)
+    torch.nn.functional.cross_entropy(logits, b.y.to(cuda)).backward()
+    full = logits.detach().cpu()
+    got = torch.cat([res[0]["logits"], res[1]["logits"]])
+    torch.testing.assert_close(got, full, rtol=0, atol=1e-4 * max(1.0, full.abs().max().item()))
+    for k, p in m.named_parameters():
+        want = p.grad.cpu()
+        for r in range(2):
+            torch.testing.assert_close(res[r]["grads"][k], want, rtol=0,
+                                       atol=max(1e-4 * want.abs().max().item(), 5e-6),
+                                       msg=lambda s: f"rank {r} {k}: {s}")
+    if kind == "gin":
+        for k, v in m.state_dict().items():
+            if "running" in k:
+                torch.testing.assert_close(res[0]["state"][k], v.cpu(), rtol=1e-5, atol=1e-6)

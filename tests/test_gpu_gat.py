@@ -131,3 +131,24 @@ def test_gat_dropout_and_determinism(cuda):
     o1 = m(b.x.to(cuda), b.edge_index.to(cuda), b.batch.to(cuda))
     o2 = m(b.x.to(cuda), b.edge_index.to(cuda), b.batch.to(cuda))
     assert torch.equal(o1, o2)
+
+
+def test_reference_config_training_step(cuda):
+    """configs/config.py model section through get_model + training_step (MSE + clamp), dropout
+    set to 0 for parity, vs the oracle criterion on the same weights."""
+    from lesion_gnn_amd.models import get_model
+    from tests.test_config import reference_model_section
+
+    cfg = reference_model_section()
+    cfg.dropout = 0.0
+    cfg.num_classes.value = 5
+    cfg.input_features.value = 64
+    cfg.optimizer.class_weights.value = torch.ones(5)
+    torch.manual_seed(0)
+    module = get_model(cfg).to(cuda).train()
+    oref = ref.GAT(64, [128] * 4, 1, heads=2, dropout=0.0)
+    oref.load_state_dict(module.model.state_dict())
+    b = synth.make_batch(32, k=6, d_in=64, seed=15, sizes="lognormal")
+    loss = module.training_step(b.to(cuda))
+    want = ref.criterion("MSE", oref(b.x, b.edge_index, b.batch, b.num_graphs), b.y, 5)
+    torch.testing.assert_close(loss.detach().cpu(), want.detach(), rtol=1e-5, atol=1e-6)

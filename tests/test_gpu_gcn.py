@@ -226,3 +226,41 @@ def test_cpu_tensors_rejected(cuda):
     m = GCN(128, [128, 128], 5, 0.0)
     with pytest.raises(_lib.LgnnError):
         m(b.x, b.edge_index, b.batch)
+
+
+class _FakeStorage:
+    def __init__(self, row, col):
+        self._row, self._col = row, col
+
+    def row(self):
+        return self._row
+
+    def col(self):
+        return self._col
+
+
+class FakeSparseTensor:
+    """Duck-typed torch_sparse.SparseTensor as ToSparseTensor builds it (row = target)."""
+
+    def __init__(self, edge_index):
+        o = torch.argsort(edge_index[1] * (edge_index.max() + 1) + edge_index[0])
+        self.storage = _FakeStorage(edge_index[1][o], edge_index[0][o])
+
+
+@pytest.mark.parametrize("form", ["torch_sparse", "sparse_csr"])
+def test_adj_t_input_matches_edge_index(cuda, form):
+    """Reference gin.py:59-62 / gat.py:87-90: the model accepts adj_t (compile=False path)."""
+    b = synth.make_batch(16, seed=21, sizes="lognormal")
+    ours, _ = make_pair([128, 128, 128])
+    ours = ours.to(cuda).eval()
+    ei = b.edge_index.to(cuda)
+    if form == "torch_sparse":
+        adj = FakeSparseTensor(ei)
+    else:
+        n = b.num_nodes
+        adj = torch.sparse_coo_tensor(torch.stack([ei[1], ei[0]]),
+                                      torch.ones(ei.size(1), device=cuda), (n, n)).coalesce()
+        adj = adj.to_sparse_csr()
+    want = ours(b.x.to(cuda), ei, b.batch.to(cuda))
+    got = ours(b.x.to(cuda), adj, b.batch.to(cuda))
+    torch.testing.assert_close(got, want, atol=1e-5, rtol=1e-5)
