@@ -50,7 +50,7 @@ def worker(rank, world, port, kind, out):
     loss.backward()
     ldist.allreduce_grads(list(m.parameters()), g1 - g0, b.num_graphs)
     if rank == 0:
-        out.put({k: p.grad.clone() for k, p in m.named_parameters()})
+        out.put({k: p.grad.numpy().copy() for k, p in m.named_parameters()})
     dist.barrier()
     dist.destroy_process_group()
 
@@ -71,7 +71,8 @@ def test_two_rank_gradients_match_full_batch(kind):
     m = make_model(kind)
     torch.nn.functional.cross_entropy(m(b.x, b.edge_index, b.batch, b.num_graphs), b.y).backward()
     for k, p in m.named_parameters():
-        torch.testing.assert_close(got[k], p.grad, atol=1e-6, rtol=1e-5, msg=lambda s: f"{k}: {s}")
+        torch.testing.assert_close(torch.from_numpy(got[k]), p.grad, atol=1e-6, rtol=1e-5,
+                                   msg=lambda s: f"{k}: {s}")
 
 
 def test_shard_bounds_balance_edges():

@@ -57,10 +57,13 @@ def worker(rank, world, port, kind, q):
     logits = m(x, ei, bt, g1 - g0)
     torch.nn.functional.cross_entropy(logits, y).backward()
     ldist.allreduce_grads(list(m.parameters()), g1 - g0, B)
-    out = {"logits": logits.detach().cpu(),
-           "grads": {k: p.grad.detach().cpu() for k, p in m.named_parameters()}}
+    # numpy arrays pickle by value (torch CPU tensors would travel through shared memory owned
+    # by this process, which may have exited before the parent reads the queue)
+    out = {"logits": logits.detach().cpu().numpy(),
+           "grads": {k: p.grad.detach().cpu().numpy() for k, p in m.named_parameters()}}
     if kind == "gin":
-        out["state"] = {k: v.detach().cpu() for k, v in m.state_dict().items() if "running" in k}
+        out["state"] = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()
+                        if "running" in k}
     q.put((rank, out))
     dist.barrier()
     dist.destroy_process_group()
@@ -85,15 +88,16 @@ def test_two_ranks_match_full_batch(cuda, kind):
     logits = m(b.x.to(cuda), b.edge_index.to(cuda), b.batch.to(cuda), B)
     torch.nn.functional.cross_entropy(logits, b.y.to(cuda)).backward()
     full = logits.detach().cpu()
-    got = torch.cat([res[0]["logits"], res[1]["logits"]])
+    got = torch.cat([torch.from_numpy(res[0]["logits"]), torch.from_numpy(res[1]["logits"])])
     torch.testing.assert_close(got, full, rtol=0, atol=1e-4 * max(1.0, full.abs().max().item()))
     for k, p in m.named_parameters():
         want = p.grad.cpu()
         for r in range(2):
-            torch.testing.assert_close(res[r]["grads"][k], want, rtol=0,
+            torch.testing.assert_close(torch.from_numpy(res[r]["grads"][k]), want, rtol=0,
                                        atol=max(1e-4 * want.abs().max().item(), 5e-6),
                                        msg=lambda s: f"rank {r} {k}: {s}")
     if kind == "gin":
         for k, v in m.state_dict().items():
             if "running" in k:
-                torch.testing.assert_close(res[0]["state"][k], v.cpu(), rtol=1e-5, atol=1e-6)
+                torch.testing.assert_close(torch.from_numpy(res[0]["state"][k]), v.cpu(),
+                                           rtol=1e-5, atol=1e-6)
