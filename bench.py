@@ -1,13 +1,22 @@
 """Benchmark: graphs/s of one training step of the lesion-graph GNN (BASELINE.json `metric`).
 
-Workload (BASELINE.json configs[1], "C2"): 2-layer GCN (in_proj -> 2 x GCNConv+ELU -> mean pool
--> out_proj), hidden 128, d_in 128, 5 classes, synthetic k-NN lesion graphs N=64, k=8, 1024
-graphs per GPU, fp32. One step = forward (incl. the per-forward graph build from edge_index) +
-cross-entropy + backward + (N>1: RCCL all-reduce of the flat gradient) + Adam step, inputs
-resident in HBM. Weak scaling: every rank processes its own 1024-graph shard.
+Default workload (BASELINE.json configs[1], "C2"): 2-layer GCN (in_proj -> 2 x GCNConv+ELU ->
+mean pool -> out_proj), hidden 128, d_in 128, 5 classes, synthetic k-NN lesion graphs N=64,
+k=8, 1024 graphs per GPU, fp32. One step = forward (incl. the per-forward graph build from
+edge_index) + cross-entropy + backward + (N>1: RCCL all-reduce of the flat gradient) + Adam
+step, inputs resident in HBM. Weak scaling: every rank processes its own 1024-graph shard.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]; N>1 under torch.distributed.run.
-Prints ONE JSON line on rank 0.
+Other workloads (--workload): c3 (3-layer GAT, 4 heads, d_in 1025, log-normal N, k=6, MSE;
+computed in fp32), c4 (GIN + global_add_pool, SyncBN over the ranks), c5k4 / c5k16 (GCN on
+power-law N in [16, 512], k = 4 / 16).
+
+Step launch (--graph 1, default): the forward+backward and the optimizer step are each captured
+once in a HIP graph and replayed — every kernel runs every step, only host launch overhead is
+removed; with N>1 the RCCL gradient all-reduce runs eagerly between the two graphs.
+--graph 0 runs everything eagerly.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2]; N>1 under
+torch.distributed.run. Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
@@ -24,14 +33,43 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+METRIC = "graphs/sec (fwd+bwd) on batched k-NN lesion graphs at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_F32_PEAK_TF = 157.3  # MI355X_MICROARCH.md: fp32 MFMA (= vector) peak
 
-# algorithmic bytes per graph for the whole fwd+bwd step:
-# B_graph = s*N*(2*d_in + h*(6L + 4 + 4*M*L)) + 2*L*(4E + 4(N+1)); GCN: M = 0
-def bytes_per_graph(n=64, k=8, d_in=128, h=128, L=2, s=4, m=0):
-    e = n * k
-    return s * n * (2 * d_in + h * (6 * L + 4 + 4 * m * L)) + 2 * L * (4 * e + 4 * (n + 1))
+WORKLOADS = {
+    "c2": dict(model="gcn", sizes="fixed", n=64, k=8, d_in=128, hidden=[128, 128, 128],
+               classes=5, loss="CE", pool="mean",
+               desc="C2: 2-layer GCN fwd+CE+bwd+Adam, graph build per forward"),
+    "c3": dict(model="gat", sizes="lognormal", n=64, k=6, d_in=1025, hidden=[128] * 4, heads=4,
+               classes=5, loss="MSE", pool="mean", last_channel_class=True,
+               desc="C3: 3-layer GAT (4 heads), d_in 1025, log-normal N, k=6, MSE (fp32)"),
+    "c4": dict(model="gin", sizes="fixed", n=64, k=8, d_in=128, hidden=[128, 128, 128],
+               classes=5, loss="CE", pool="add",
+               desc="C4: GIN + global_add_pool, SyncBN across ranks, fwd+CE+bwd+Adam"),
+    "c5k4": dict(model="gcn", sizes="powerlaw", n=64, k=4, d_in=128, hidden=[128, 128, 128],
+                 classes=5, loss="CE", pool="mean",
+                 desc="C5: GCN, power-law N in [16,512], k=4"),
+    "c5k16": dict(model="gcn", sizes="powerlaw", n=64, k=16, d_in=128, hidden=[128, 128, 128],
+                  classes=5, loss="CE", pool="mean",
+                  desc="C5: GCN, power-law N in [16,512], k=16"),
+}
+
+
+def step_bytes(b, wl) -> float:
+    """Algorithmic HBM bytes of one fwd+bwd step over batch b, summed per graph:
+    B_graph = s*N*(2*d_in + h*(6L + 4 + 4*M*L)) + 2*L*(4E + 4(N+1)) [+ GAT: 2*L*E*H*4 for alpha]
+    with s = 4 (fp32), M = 1 for GIN (MLP hidden), 0 otherwise; E = the edges of the batch's
+    k-NN graph (self loops included, as KNNGraph(loop=True) builds them)."""
+    h = wl["hidden"][1]
+    L = len(wl["hidden"]) - 1
+    m = 1 if wl["model"] == "gin" else 0
+    n = (b.ptr[1:] - b.ptr[:-1]).double().cpu()
+    e = torch.bincount(b.batch.cpu()[b.edge_index[1].cpu()], minlength=b.num_graphs).double()
+    tot = 4 * n * (2 * wl["d_in"] + h * (6 * L + 4 + 4 * m * L)) + 2 * L * (4 * e + 4 * (n + 1))
+    if wl["model"] == "gat":
+        tot = tot + 2 * L * e * wl["heads"] * 4
+    return float(tot.sum())
 
 
 def parse():
@@ -39,18 +77,19 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
     ap.add_argument("--graphs-per-gpu", type=int, default=1024)
-    ap.add_argument("--nodes", type=int, default=64)
-    ap.add_argument("--k", type=int, default=8)
-    ap.add_argument("--hidden", type=int, default=128)
-    ap.add_argument("--layers", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="bounded CPU-baseline sample (rank 0, N=1 only); 0 disables")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--opt", choices=["fused", "foreach"], default="fused",
+                    help="Adam implementation (runs inside the timed step either way)")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="1: replay the captured fwd+bwd and optimizer HIP graphs; 0: eager")
     return ap.parse_args()
 
 
-def setup_dist(args):
+def setup_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -58,6 +97,37 @@ def setup_dist(args):
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return world, rank, torch.device("cuda", local)
+
+
+def make_batch(wl, B, seed):
+    from lesion_gnn_amd import synth
+
+    return synth.make_batch(B, n=wl["n"], k=wl["k"], d_in=wl["d_in"], num_classes=wl["classes"],
+                            seed=seed, sizes=wl["sizes"],
+                            last_channel_class=wl.get("last_channel_class", False))
+
+
+def build_model(wl, oracle=False):
+    torch.manual_seed(1234)
+    if oracle:
+        import oracle.pyg_ref as ref
+
+        mods = {"gcn": ref.GCN, "gin": ref.GIN, "gat": ref.GAT}
+    else:
+        from lesion_gnn_amd import models
+
+        mods = {"gcn": models.GCN, "gin": models.GIN, "gat": models.GAT}
+    out = 1 if wl["loss"] == "MSE" else wl["classes"]
+    if wl["model"] == "gat":
+        return mods["gat"](wl["d_in"], wl["hidden"], out, heads=wl["heads"], dropout=0.0)
+    return mods[wl["model"]](wl["d_in"], wl["hidden"], out, 0.0, pool=wl["pool"])
+
+
+def loss_fn(wl, logits, y):
+    if wl["loss"] == "CE":
+        return torch.nn.functional.cross_entropy(logits, y)
+    # reference regression head: clamp(logits.squeeze(1), 0, C-1) then MSE (gat.py:94-95)
+    return torch.nn.functional.mse_loss(logits.squeeze(1).clamp(0, wl["classes"] - 1), y.float())
 
 
 def time_dominant_kernel(model, b, dev, reps=20):
@@ -121,24 +191,18 @@ def pmc_traffic(trace_name: str):
     return None, None
 
 
-def cpu_baseline(args, seconds):
+def cpu_baseline(wl, B, seconds):
     """Oracle (plain-torch CPU restatement of the PyG path) on the host cores: same model, same
-    step (fwd + CE + bwd + Adam), bounded sample of the same workload."""
-    import oracle.pyg_ref as ref
-    from lesion_gnn_amd import synth
-
+    step (fwd + loss + bwd + Adam), bounded sample of the same workload (same batch size)."""
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    B = args.graphs_per_gpu
-    b = synth.make_batch(B, n=args.nodes, k=args.k, d_in=128, seed=11)
-    torch.manual_seed(0)
-    m = ref.GCN(128, [args.hidden] * (args.layers + 1), 5, 0.0)
+    b = make_batch(wl, B, seed=11)
+    m = build_model(wl, oracle=True)
     opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=2e-6)
 
     def step():
         opt.zero_grad(set_to_none=True)
-        loss = torch.nn.functional.cross_entropy(m(b.x, b.edge_index, b.batch, B), b.y)
-        loss.backward()
+        loss_fn(wl, m(b.x, b.edge_index, b.batch, B), b.y).backward()
         opt.step()
 
     step()
@@ -150,34 +214,61 @@ def cpu_baseline(args, seconds):
         times.append(time.perf_counter() - t0)
     med = statistics.median(times)
     return {"value": round(B / med, 2), "unit": "graphs/s", "cores": threads, "kind": "port",
-            "sample": f"{len(times)} steps x {B} graphs (N={args.nodes}, k={args.k}), median "
+            "sample": f"{len(times)} steps x {B} graphs ({wl['desc']}), median "
                       f"{med * 1e3:.1f} ms/step, torch CPU fp32 with {threads} threads"}
 
 
 def main():
     args = parse()
-    world, rank, dev = setup_dist(args)
+    wl = WORKLOADS[args.workload]
+    world, rank, dev = setup_dist()
     from lesion_gnn_amd import dist as ldist
-    from lesion_gnn_amd import synth
-    from lesion_gnn_amd.models.gcn import GCN
 
     B = args.graphs_per_gpu
-    b = synth.make_batch(B, n=args.nodes, k=args.k, d_in=128, seed=100 + rank).to(dev)
-    torch.manual_seed(1234)
-    model = GCN(128, [args.hidden] * (args.layers + 1), 5, dropout=0.0).to(dev)
+    b = make_batch(wl, B, seed=100 + rank).to(dev)
+    model = build_model(wl).to(dev)
     if world > 1:
         ldist.broadcast_params(model)
+        if wl["model"] == "gin":  # SyncBN: full-batch statistics across the ranks
+            model.set_sync_bn(dist.group.WORLD, global_count=b.num_nodes * world)
     params = list(model.parameters())
-    opt = torch.optim.Adam(params, lr=1e-3, weight_decay=2e-6)
+    okw = {"fused": True} if args.opt == "fused" else {"foreach": True}
+    if args.graph:
+        okw["capturable"] = True
+    opt = torch.optim.Adam(params, lr=1e-3, weight_decay=2e-6, **okw)
 
-    def step():
-        opt.zero_grad(set_to_none=True)
-        logits = model(b.x, b.edge_index, b.batch, B)
-        loss = torch.nn.functional.cross_entropy(logits, b.y)
-        loss.backward()
+    def fwd_bwd():
+        loss_fn(wl, model(b.x, b.edge_index, b.batch, B), b.y).backward()
+
+    def exchange():
         if world > 1:  # one flat RCCL all-reduce; equal shards -> weights 1/world
             ldist.allreduce_grads(params, B, B * world)
+
+    def eager_step():
+        opt.zero_grad(set_to_none=True)
+        fwd_bwd()
+        exchange()
         opt.step()
+
+    step = eager_step
+    if args.graph:
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                eager_step()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        opt.zero_grad(set_to_none=True)
+        g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_fb):
+            fwd_bwd()
+        with torch.cuda.graph(g_opt):
+            opt.step()
+
+        def step():
+            g_fb.replay()
+            exchange()  # RCCL stays outside the captured graphs
+            g_opt.replay()
 
     for _ in range(args.warmup):
         step()
@@ -199,21 +290,22 @@ def main():
     value = B * world * args.steps / elapsed
 
     out = {
-        "metric": "graphs/sec (fwd+bwd) on batched k-NN lesion graphs at 1/2/4/8 MI355X",
-        "value": round(value, 1), "unit": "graphs/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "metric": METRIC, "value": round(value, 1), "unit": "graphs/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic k-NN lesion graphs (pos~U[0,1)^2, x~N(0,1)), random-init weights",
-        "config": {"workload": "C2: 2-layer GCN fwd+CE+bwd+Adam, graph build per forward",
-                   "model": "GCN(128,[128,128,128],5,dropout=0,pool=mean)",
-                   "graphs_per_gpu": B, "global_batch": B * world, "nodes_per_graph": args.nodes,
-                   "k": args.k, "d": 128, "parallelism": f"dp{world}"},
+        "config": {"workload": wl["desc"], "name": args.workload,
+                   "step_launch": "hip_graph_replay" if args.graph else "eager",
+                   "adam": args.opt, "graphs_per_gpu": B, "global_batch": B * world,
+                   "nodes": b.num_nodes, "edges": b.num_edges, "k": wl["k"], "d_in": wl["d_in"],
+                   "hidden": wl["hidden"], "parallelism": f"dp{world}"},
     }
-    bpg = bytes_per_graph(args.nodes, args.k, 128, args.hidden, args.layers)
+    bpb = step_bytes(b, wl)
     out["step_hbm_roofline"] = {
-        "bytes_per_graph": bpg, "achieved_GBps_per_gpu": round(value / world * bpg / 1e9, 1),
-        "frac_of_8TBps": round(value / world * bpg / (HBM_PEAK_GBS * 1e9), 4)}
-    if rank == 0 and not args.no_kernel_timing:
+        "bytes_per_graph": round(bpb / B, 1),
+        "achieved_GBps_per_gpu": round(value / world * bpb / B / 1e9, 1),
+        "frac_of_8TBps": round(value / world * bpb / B / (HBM_PEAK_GBS * 1e9), 4)}
+    if rank == 0 and not args.no_kernel_timing and args.workload == "c2":
         kt = time_dominant_kernel(model, b, dev)
         achieved = kt["flops"] / (kt["ms"] * 1e-3) / 1e12
         traffic, tsrc = pmc_traffic(kt["trace_name"])
@@ -225,7 +317,7 @@ def main():
                            "kernel": kt["kernel"], "avg_launch_ms": round(kt["ms"], 5),
                            "flops_per_launch": kt["flops"]}
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(wl, B, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -94,6 +94,14 @@ int lgnn_batch_ptr(const int64_t* batch, int64_t num_nodes, int64_t num_graphs, 
 int lgnn_node_linear_fwd(const float* X, int64_t M, int K, const int32_t* rowptr,
                          const int32_t* col, const float* w, float self_scale, const float* W,
                          const float* b, int N, int act, float* Y, float* S_out, void* stream);
+/* Same, restricted to the 64-node tiles t with (tile_open[t] != 0) == want_open (tile_open from
+ * lgnn_tile_open; NULL = every tile). Fast-path shapes only. Used to pair the layer-by-layer
+ * kernels with lgnn_gcn_stack_fwd, which takes the tiles no edge leaves. */
+int lgnn_node_linear_fwd_tiles(const float* X, int64_t M, int K, const int32_t* rowptr,
+                               const int32_t* col, const float* w, float self_scale,
+                               const float* W, const float* b, int N, int act, float* Y,
+                               float* S_out, const int32_t* tile_open, int want_open,
+                               void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Node-tile fused backward of lgnn_node_linear_fwd.
@@ -216,6 +224,29 @@ int lgnn_gat_bwd_node(const int32_t* tptr, const int32_t* tidx, const int32_t* t
                       const float* da_d, const float* dZ, const float* XP, const float* att_src,
                       const float* att_dst, int64_t M, int H, int C, float* dXP,
                       float* partials, int num_partials, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Fused GCN layer stack, forward (one launch for the whole model body below the readout).
+ * Replaces: in_proj nn.Linear (reference gin.py:21 skeleton) + L x (GCNConv + F.elu) — the
+ * layer-by-layer lgnn_node_linear_fwd chain — keeping each 64-node tile on chip across layers.
+ *   has_in_proj=1: H[0] = X W[0]^T + b[0] (X [M, d_in]); else H[0] is X itself (widths[0]=d_in)
+ *   for l = 1..L: S[l] = Â H[l-1] (CSR rowptr/col/w, self term via the CSR), H[l] = ELU(S[l]
+ *   W[l]^T + b[l]).  W, b, H, S: host arrays of L+1 device pointers (S[0] unused); widths[l] =
+ *   output width of layer l. All widths and d_in <= 128, multiples of 4; L + 1 <= 8.
+ *   tile_open (nullable): only tiles with tile_open[t] == 0 are computed (the others read
+ *   neighbours that another tile computes in the same layer: run them with
+ *   lgnn_node_linear_fwd_tiles(..., tile_open, 1)).
+ * ------------------------------------------------------------------------------------------- */
+int lgnn_gcn_stack_fwd(const float* X, int64_t M, int d_in, int has_in_proj,
+                       const int32_t* rowptr, const int32_t* col, const float* w, int L,
+                       const float* const* W, const float* const* b, const int* widths,
+                       float* const* H, float* const* S, const int32_t* tile_open,
+                       void* stream);
+/* Tiles: 64 consecutive node rows. open[t] = 1 when an edge joins tile t to another tile (its
+ * layers then depend on other tiles, so lgnn_gcn_stack_fwd skips it: tile_open non-NULL). */
+int lgnn_tile_count(int64_t num_nodes);
+int lgnn_tile_open(const int32_t* rowptr, const int32_t* col, int64_t num_nodes, int32_t* open,
+                   void* stream);
 
 #ifdef __cplusplus
 }

@@ -72,6 +72,7 @@ class GINConv(nn.Module):
         self.nn = mlp
         self.register_buffer("eps", torch.full((1,), float(eps)))
         self.sync_group = None  # torch.distributed group for SyncBN (None: per-replica stats)
+        self.sync_count = None  # fixed global node count under SyncBN (None: all-reduced)
 
     def forward(self, x: torch.Tensor, edge_index, act: int = _lib.LGNN_ACT_NONE) -> torch.Tensor:
         g = as_graph(edge_index, x.size(0))
@@ -83,7 +84,8 @@ class GINConv(nn.Module):
             mask = (torch.rand(x.size(0), mlp.channel_list[1], device=x.device) >= p).float()
             mask.mul_(1.0 / (1.0 - p))
         return ops.gin_conv(x, mlp.lins[0].weight, mlp.lins[0].bias, bn, mlp.lins[1].weight,
-                            mlp.lins[1].bias, g, float(self.eps), mask, act, self.sync_group)
+                            mlp.lins[1].bias, g, float(self.eps), mask, act, self.sync_group,
+                            self.sync_count)
 
 
 class GATConv(nn.Module):

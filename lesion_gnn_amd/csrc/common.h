@@ -5,6 +5,8 @@
 
 #include "../../include/lgnn.h"
 
+#define LGNN_MAX_STACK 8  // layers of one fused stack launch (in_proj + 7 convs)
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 

@@ -46,6 +46,7 @@ struct GraphWs {
   int32_t* eid;    // [E+N]
   int32_t* teid;   // [E+N]
   int32_t* inv;    // [E+N] edge id -> target-CSR position (for tmap)
+  float* dis;      // [N] deg^-1/2 (GCN normalisation), inf -> 0
   void* scan_tmp;
   size_t scan_bytes;
   size_t zero_bytes;
@@ -67,13 +68,14 @@ GraphWs carve(void* base, int64_t N, int64_t E) {
   ws.eid = (int32_t*)take((E + N) * 4);
   ws.teid = (int32_t*)take((E + N) * 4);
   ws.inv = (int32_t*)take((E + N) * 4);
+  ws.dis = (float*)take(N * 4);
   ws.scan_bytes = scan_temp_bytes(N + 1);
   ws.scan_tmp = take(ws.scan_bytes);
   return ws;
 }
 
 size_t ws_total(int64_t N, int64_t E) {
-  return 2 * align_up((N + 1) * 4) + 2 * align_up(N * 4) + 3 * align_up((E + N) * 4) +
+  return 2 * align_up((N + 1) * 4) + 3 * align_up(N * 4) + 3 * align_up((E + N) * 4) +
          align_up(scan_temp_bytes(N + 1)) + 256;
 }
 
@@ -161,6 +163,67 @@ __global__ __launch_bounds__(kThreads) void k_fill(const int64_t* __restrict__ e
   }
 }
 
+// Both degree scans in one launch (block 0: rowptr from cnt, block 1: tptr from tcnt), for
+// N + 1 <= kScanSmall: thread t scans a contiguous chunk, chunk totals are scanned across the
+// block. Block 0 also writes dis[i] = deg_i^-1/2 (GCN normalisation; deg 0 -> 0).
+constexpr int kScanThreads = 1024;
+constexpr int64_t kScanSmall = 1 << 18;
+
+__global__ __launch_bounds__(kScanThreads) void k_scan2(const int32_t* __restrict__ cnt,
+                                                        const int32_t* __restrict__ tcnt,
+                                                        int64_t N, int add,
+                                                        int32_t* __restrict__ rowptr,
+                                                        int32_t* __restrict__ tptr,
+                                                        float* __restrict__ dis) {
+  __shared__ int wsum[kScanThreads / 64];
+  const bool tr = blockIdx.x == 1;
+  const int32_t* __restrict__ c = tr ? tcnt : cnt;
+  int32_t* __restrict__ out = tr ? tptr : rowptr;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t n = N + 1;
+  const int64_t chunk = (n + kScanThreads - 1) / kScanThreads;
+  const int64_t b0 = tid * chunk, b1 = b0 + chunk < n ? b0 + chunk : n;
+  int sum = 0;
+  for (int64_t i = b0; i < b1; ++i) sum += i < N ? c[i] + add : 0;
+  // inclusive scan of the chunk sums: wave, then across waves
+  int x = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wave] = x;
+  __syncthreads();
+  if (wave == 0) {
+    int v = lane < kScanThreads / 64 ? wsum[lane] : 0;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const int y = __shfl_up(v, o, 64);
+      if (lane >= o) v += y;
+    }
+    if (lane < kScanThreads / 64) wsum[lane] = v;
+  }
+  __syncthreads();
+  int run = x - sum + (wave > 0 ? wsum[wave - 1] : 0);  // exclusive prefix of this chunk
+  for (int64_t i = b0; i < b1; ++i) {
+    out[i] = run;
+    if (i < N) {
+      const int deg = c[i] + add;
+      if (!tr && dis) dis[i] = deg > 0 ? 1.0f / sqrtf((float)deg) : 0.0f;
+      run += deg;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_dis(const int32_t* __restrict__ rowptr, int64_t N,
+                                                  float* __restrict__ dis) {
+  for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < N;
+       i += (int64_t)gridDim.x * kThreads) {
+    const int deg = rowptr[i + 1] - rowptr[i];
+    dis[i] = deg > 0 ? 1.0f / sqrtf((float)deg) : 0.0f;
+  }
+}
+
 __device__ __forceinline__ float gcn_dis(const int32_t* __restrict__ rowptr, int64_t j) {
   const int deg = rowptr[j + 1] - rowptr[j];
   return deg > 0 ? 1.0f / sqrtf((float)deg) : 0.0f;
@@ -188,7 +251,8 @@ __global__ __launch_bounds__(kThreads) void k_finish(int64_t N, int64_t E, int a
                                                      const int32_t* __restrict__ rowptr,
                                                      int32_t* col, int32_t* eid, float* w,
                                                      const int32_t* __restrict__ tptr,
-                                                     int32_t* tidx, int32_t* teid, float* tw) {
+                                                     int32_t* tidx, int32_t* teid, float* tw,
+                                                     const float* __restrict__ dis) {
   __shared__ int32_t s_key[kFinishCap];
   __shared__ int32_t s_val[kFinishCap];
   const bool tr = blockIdx.y == 1;
@@ -235,10 +299,10 @@ __global__ __launch_bounds__(kThreads) void k_finish(int64_t N, int64_t E, int a
     // row of each entry: binary search is avoided by a per-thread row walk (rows are short)
     if (i < N) {
       const int r0 = ptr[i], r1 = ptr[i + 1];
-      const float di = norm == LGNN_NORM_GCN ? gcn_dis(rowptr, i) : 1.f;
+      const float di = norm == LGNN_NORM_GCN ? dis[i] : 1.f;
       for (int j = r0; j < r1; ++j) {
         const int nb = staged ? s_val[j - eb] : idx[j];
-        wt[j] = norm == LGNN_NORM_GCN ? (gcn_dis(rowptr, nb) * 1.0f) * di : 1.0f;
+        wt[j] = norm == LGNN_NORM_GCN ? (dis[nb] * 1.0f) * di : 1.0f;
       }
     }
   }
@@ -325,15 +389,23 @@ extern "C" int lgnn_graph_build(const int64_t* edge_index, int64_t E, int64_t N,
                        loops, ws.cnt, tptr ? ws.tcnt : nullptr, err_count);
     LGNN_LAUNCH_CHECK();
   }
-  size_t tb = ws.scan_bytes;
-  if (hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, tb, CntIter(ws.cnt, AddLoop{add_loop}),
-                                       rowptr, (int)(N + 1), s) != hipSuccess)
-    return (int)hipGetLastError();
-  if (tptr) {
-    tb = ws.scan_bytes;
-    if (hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, tb, CntIter(ws.tcnt, AddLoop{add_loop}),
-                                         tptr, (int)(N + 1), s) != hipSuccess)
+  if (N + 1 <= kScanSmall) {
+    hipLaunchKernelGGL(k_scan2, dim3(tptr ? 2 : 1), dim3(kScanThreads), 0, s, ws.cnt, ws.tcnt, N,
+                       add_loop, rowptr, tptr, ws.dis);
+    LGNN_LAUNCH_CHECK();
+  } else {
+    size_t tb = ws.scan_bytes;
+    if (hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, tb, CntIter(ws.cnt, AddLoop{add_loop}),
+                                         rowptr, (int)(N + 1), s) != hipSuccess)
       return (int)hipGetLastError();
+    if (tptr) {
+      tb = ws.scan_bytes;
+      if (hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, tb, CntIter(ws.tcnt, AddLoop{add_loop}),
+                                           tptr, (int)(N + 1), s) != hipSuccess)
+        return (int)hipGetLastError();
+    }
+    hipLaunchKernelGGL(k_dis, dim3(grid_for(N)), dim3(kThreads), 0, s, rowptr, N, ws.dis);
+    LGNN_LAUNCH_CHECK();
   }
   if (E > 0) {
     hipLaunchKernelGGL(k_fill, dim3(grid_for(E, 2048)), dim3(kThreads), 0, s, edge_index, E, N,
@@ -342,7 +414,7 @@ extern "C" int lgnn_graph_build(const int64_t* edge_index, int64_t E, int64_t N,
   }
   dim3 fg((unsigned)((N + kThreads - 1) / kThreads), tptr ? 2u : 1u);
   hipLaunchKernelGGL(k_finish, fg, dim3(kThreads), 0, s, N, E, add_loop, norm, rowptr, col,
-                     ws.eid, w, tptr, tidx, ws.teid, tw);
+                     ws.eid, w, tptr, tidx, ws.teid, tw, ws.dis);
   LGNN_LAUNCH_CHECK();
   if (tmap) {
     const int g = grid_for(E + N, 2048);

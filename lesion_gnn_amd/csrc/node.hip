@@ -632,6 +632,16 @@ extern "C" int lgnn_node_linear_fwd(const float* X, int64_t M, int K, const int3
                                     const int32_t* col, const float* w, float self_scale,
                                     const float* W, const float* b, int N, int act, float* Y,
                                     float* S_out, void* stream) {
+  return lgnn_node_linear_fwd_tiles(X, M, K, rowptr, col, w, self_scale, W, b, N, act, Y, S_out,
+                                    nullptr, 0, stream);
+}
+
+extern "C" int lgnn_node_linear_fwd_tiles(const float* X, int64_t M, int K,
+                                          const int32_t* rowptr, const int32_t* col,
+                                          const float* w, float self_scale, const float* W,
+                                          const float* b, int N, int act, float* Y, float* S_out,
+                                          const int32_t* tile_open, int want_open,
+                                          void* stream) {
   if (M < 0 || K <= 0 || N <= 0 || !W || !Y || (M > 0 && !X)) return LGNN_EINVAL;
   if (act != LGNN_ACT_NONE && act != LGNN_ACT_ELU) return LGNN_EINVAL;
   const bool gather = rowptr != nullptr;
@@ -640,11 +650,12 @@ extern "C" int lgnn_node_linear_fwd(const float* X, int64_t M, int K, const int3
   const int64_t gx = (M + TM - 1) / TM;
   if (gx > INT32_MAX) return LGNN_EINVAL;
   hipStream_t s = as_stream(stream);
-  if (lgnn_tile_fits(K, N)) {
+  if (lgnn_tile_fits(M, K, N)) {
     const hipError_t e = lgnn_tile_fwd(s, X, M, K, rowptr, col, w, self_scale, W, b, N, act, Y,
-                                       gather ? S_out : nullptr);
+                                       gather ? S_out : nullptr, tile_open, want_open);
     return e == hipSuccess ? LGNN_OK : (int)e;
   }
+  if (tile_open) return LGNN_EINVAL;  // tile selection only on the fast path
   if (S_out) return LGNN_EINVAL;  // S_out only on the fast path (K, N <= 128)
   dim3 grid((unsigned)gx, (unsigned)((N + TN - 1) / TN));
   const bool vec = (K & 3) == 0;
@@ -668,11 +679,13 @@ extern "C" int lgnn_node_linear_fwd(const float* X, int64_t M, int K, const int3
 
 // The fast path applies when the prologue is direct (S streamed, not re-gathered).
 static hipStream_t s_(void* p) { return as_stream(p); }
-static bool bwd_fast(int N, int K, bool gather) { return !gather && lgnn_tile_fits(K, N); }
+static bool bwd_fast(int64_t M, int N, int K, bool gather) {
+  return !gather && lgnn_tile_fits(M, K, N);
+}
 
 extern "C" int lgnn_bwd_num_partials(int64_t M, int N, int K, int gather) {
   if (M < 0 || N <= 0 || K <= 0) return LGNN_EINVAL;
-  return bwd_fast(N, K, gather != 0) ? lgnn_tile_partials(M) : grid_partials(M, N, K);
+  return bwd_fast(M, N, K, gather != 0) ? lgnn_tile_partials(M) : grid_partials(M, N, K);
 }
 
 extern "C" int lgnn_node_linear_bwd(int grad_mode, const float* dY, const int64_t* batch,
@@ -684,7 +697,7 @@ extern "C" int lgnn_node_linear_bwd(int grad_mode, const float* dY, const int64_
                                     float* dW_partial, float* db_partial, int num_partials,
                                     void* stream) {
   if (M < 0 || K <= 0 || N <= 0 || (N & 3) || !W || !dW_partial) return LGNN_EINVAL;
-  const bool fast = bwd_fast(N, K, rowptr != nullptr);
+  const bool fast = bwd_fast(M, N, K, rowptr != nullptr);
   if (num_partials != (fast ? lgnn_tile_partials(M) : grid_partials(M, N, K))) return LGNN_EINVAL;
   if (act != LGNN_ACT_NONE && act != LGNN_ACT_ELU) return LGNN_EINVAL;
   if (act == LGNN_ACT_ELU && !H) return LGNN_EINVAL;

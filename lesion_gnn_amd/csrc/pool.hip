@@ -61,6 +61,58 @@ __global__ __launch_bounds__(NT) void k_pool_head_fwd(const float* __restrict__ 
   }
 }
 
+// D % 4 == 0 (every hidden width of the reference): one 256-thread block per graph; the 8 half
+// waves stride the graph's rows (float4 per lane, 128-feature strips, 2 rows in flight each),
+// partial sums combined in half-wave order; then one wave per class for the logits.
+__global__ __launch_bounds__(NT) void k_pool_head_fwd4(const float* __restrict__ H,
+                                                       const int32_t* __restrict__ gptr, int D,
+                                                       int pool_mean,
+                                                       const float* __restrict__ Wout,
+                                                       const float* __restrict__ bout, int C,
+                                                       float* __restrict__ pooled,
+                                                       float* __restrict__ logits) {
+  __shared__ __attribute__((aligned(16))) float red[8][512];
+  __shared__ float pl[512];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 31, hw = wave * 2 + (lane >> 5);
+  const int64_t g = blockIdx.x;
+  const int n0 = gptr[g], n1 = gptr[g + 1];
+  for (int s0 = 0; s0 < D; s0 += 128) {
+    const int f = s0 + 4 * li;
+    const int fc = f < D ? f : D - 4;
+    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+    int i = n0 + hw;
+    for (; i + 8 < n1; i += 16) {
+      const f32x4 v0 = ld4(H + (int64_t)i * D + fc);
+      const f32x4 v1 = ld4(H + (int64_t)(i + 8) * D + fc);
+      a0 += v0;
+      a1 += v1;
+    }
+    if (i < n1) a0 += ld4(H + (int64_t)i * D + fc);
+    if (f < D) st4(&red[hw][f], a0 + a1);
+  }
+  __syncthreads();
+  const int cnt = n1 - n0;
+  const float denom = (float)(cnt > 0 ? cnt : 1);
+  for (int d = threadIdx.x; d < D; d += NT) {
+    float t = red[0][d];
+#pragma unroll
+    for (int r = 1; r < 8; ++r) t += red[r][d];
+    if (pool_mean) t = t / denom;
+    pooled[g * D + d] = t;
+    pl[d] = t;
+  }
+  if (!Wout) return;
+  __syncthreads();
+  for (int c = wave; c < C; c += NT / 64) {
+    float acc = 0.f;
+    for (int d = lane; d < D; d += 64) acc = fmaf(pl[d], Wout[(int64_t)c * D + d], acc);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (lane == 0) logits[g * C + c] = acc + (bout ? bout[c] : 0.f);
+  }
+}
+
 // dpooled[g][d] = sum_c dlogits[g][c] Wout[c][d]
 __global__ __launch_bounds__(NT) void k_head_bwd_dp(const float* __restrict__ dlogits, int64_t B,
                                                     int D, const float* __restrict__ Wout, int C,
@@ -134,8 +186,13 @@ extern "C" int lgnn_pool_head_fwd(const float* H, const int32_t* gptr, int64_t B
   if (B < 0 || D <= 0 || D > 512 || !gptr || !pooled) return LGNN_EINVAL;
   if (Wout && (C <= 0 || !logits)) return LGNN_EINVAL;
   if (B == 0) return LGNN_OK;
-  hipLaunchKernelGGL(k_pool_head_fwd, dim3((unsigned)((B + 3) / 4)), dim3(NT), 0,
-                     as_stream(stream), H, gptr, B, D, pool_mean, Wout, bout, C, pooled, logits);
+  if ((D & 3) == 0)
+    hipLaunchKernelGGL(k_pool_head_fwd4, dim3((unsigned)B), dim3(NT), 0, as_stream(stream), H,
+                       gptr, D, pool_mean, Wout, bout, C, pooled, logits);
+  else
+    hipLaunchKernelGGL(k_pool_head_fwd, dim3((unsigned)((B + 3) / 4)), dim3(NT), 0,
+                       as_stream(stream), H, gptr, B, D, pool_mean, Wout, bout, C, pooled,
+                       logits);
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
 }

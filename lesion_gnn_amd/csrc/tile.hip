@@ -14,8 +14,34 @@
 #include "common.h"
 #include "tile.h"
 
+#include <type_traits>
+
+// Timing-only ablation builds (tools/ablate.py): -DLGNN_ABLATE=<mask> removes phases of the tile
+// kernels (1 MFMA, 2 aggregation, 4 global stores, 16 global row loads). The product build is
+// mask 0; ablated libraries are built outside the package and never loaded by it.
+#ifndef LGNN_ABLATE
+#define LGNN_ABLATE 0
+#endif
+
+// Diagnostic build only (-DLGNN_STAMPS, tools/stamps.py): thread 0 of each block records
+// s_memtime at phase boundaries of k_stack_fwd; never compiled into the product library.
+#ifdef LGNN_STAMPS
+__device__ unsigned long long lgnn_stamp_buf[1024 * 64];
+#define STAMP(k)                                                                   \
+  do {                                                                             \
+    const int _k = (k);                                                            \
+    if (threadIdx.x == 0 && _k < 64)                                               \
+      lgnn_stamp_buf[blockIdx.x * 64 + _k] = __builtin_amdgcn_s_memtime();         \
+  } while (0)
+#else
+#define STAMP(k) \
+  do {           \
+  } while (0)
+#endif
+
 namespace lgnn_tile {
 
+constexpr int ABL = LGNN_ABLATE;
 constexpr int TM = 64;
 constexpr int KC = 128;
 constexpr int LDS = KC + 4;
@@ -23,29 +49,53 @@ constexpr int NT = 256;
 constexpr int CAPE = 1024;
 constexpr int EB = 8;
 
+// A tile's CSR block in LDS. `local` (every entry's source row is in this tile — the k-NN
+// case with graphs aligned to tiles): ow[j] = (float offset of the source row in the A image,
+// weight bits), padded with EB zero-weight entries so a row's batch reads need no bounds logic.
+// Otherwise only rp is used and the rows are aggregated from global memory.
 struct TileIdx {
   int rp[TM + 1];
-  int col[CAPE];
-  float w[CAPE];
+  int local;
+  int2 ow[CAPE + EB];
 };
+
+// Tile selection by a per-tile mask (nullable = every tile): with `want` = 1 only tiles whose
+// mask is non-zero, with 0 only tiles whose mask is zero. Block-uniform scalar reads.
+__device__ __forceinline__ int64_t seek_tile(int64_t t, int64_t ntiles,
+                                             const int32_t* __restrict__ mask, int want) {
+  if (mask)
+    while (t < ntiles && ((mask[t] != 0) != (want != 0))) t += gridDim.x;
+  return t;
+}
+
+// Raw buffer access (SGPR descriptor + 32-bit byte offset): out-of-range loads return 0 and
+// out-of-range stores are dropped by the hardware range check, so row tails need no clamping
+// and addresses cost one VGPR. Tensors addressed this way are < 4 GiB (checked on the host).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t Buf;
+__device__ __forceinline__ Buf mkbuf(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)(uint32_t)bytes,
+                                           0x00020000);
+}
+__device__ __forceinline__ f32x4 bld4(Buf r, int off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ void bst4(Buf r, int off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
+}
 
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 __device__ __forceinline__ f32x4 sel4(bool c, f32x4 v) { return c ? v : zero4(); }
 
 // Coalesced raw tile load: thread owns rows hw + 8*it (it < 8), columns 4li..4li+3 — the same
 // (row, column) mapping as the half-wave-per-row aggregation, so register values can be reused.
-__device__ __forceinline__ void load_rows(f32x4 (&v)[8], const float* __restrict__ X, int64_t M,
-                                          int K, int64_t r0) {
+__device__ __forceinline__ void load_rows(f32x4 (&v)[8], Buf X, int K, int r0) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int hw = wave * 2 + (lane >> 5), li = lane & 31;
   const int k = 4 * li;
   const int kc = k < K ? k : K - 4;
 #pragma unroll
-  for (int it = 0; it < 8; ++it) {
-    const int64_t row = r0 + hw + 8 * it;
-    const int64_t rc = row < M ? row : M - 1;
-    v[it] = ld4(X + rc * K + kc);
-  }
+  for (int it = 0; it < 8; ++it) v[it] = bld4(X, ((r0 + hw + 8 * it) * K + kc) * 4);
 }
 
 __device__ __forceinline__ void store_rows_lds(float* A, const f32x4 (&v)[8], int64_t M, int K,
@@ -60,35 +110,99 @@ __device__ __forceinline__ void store_rows_lds(float* A, const f32x4 (&v)[8], in
   }
 }
 
-__device__ __forceinline__ void stage_idx(TileIdx& ti, bool& staged,
-                                          const int32_t* __restrict__ rowptr,
-                                          const int32_t* __restrict__ col,
-                                          const float* __restrict__ w, int64_t M, int64_t r0) {
+// One tile's CSR index block, loaded into registers ahead of use (software pipelining: the next
+// tile's block is in flight while the current tile aggregates and runs its MFMAs).
+//   head: rowptr[r0 .. r0+64] (one per thread, tid <= 64) + the uniform entry range (eb, ne)
+//   body: the ne <= CAPE entries (col, w), CAPE/NT per thread; issued once the head has landed
+struct IdxRegs {
+  int rp;
+  int eb, ne;
+  int c[CAPE / NT];
+  float w[CAPE / NT];
+};
+
+__device__ __forceinline__ void idx_load_head(IdxRegs& R, const int32_t* __restrict__ rowptr,
+                                              int64_t M, int64_t r0) {
   const int tid = threadIdx.x;
-  if (tid <= TM) {
-    const int64_t r = r0 + tid;
-    ti.rp[tid] = rowptr[r < M ? r : M];
-  }
-  __syncthreads();
-  const int eb = ti.rp[0], ne = ti.rp[TM] - eb;
-  staged = ne <= CAPE;
-  if (staged) {
-    for (int j = tid; j < ne; j += NT) {
-      ti.col[j] = col[eb + j];
-      ti.w[j] = w ? w[eb + j] : 1.f;
-    }
-  }
-  __syncthreads();
+  const int64_t r = r0 + (tid <= TM ? tid : 0);
+  R.rp = rowptr[r < M ? r : M];
+  const int64_t rl = r0 + TM < M ? r0 + TM : M;
+  R.eb = rowptr[r0];
+  R.ne = rowptr[rl] - R.eb;
 }
 
-// sum_{e in row rr} w_e * X[c_e][4li..], in CSR order; X rows of the tile come from the LDS image
-// A, others from global X (wave-uniform fallback).
-__device__ __forceinline__ f32x4 agg_row(const TileIdx& ti, bool staged, int rr, const float* A,
-                                         int64_t r0, const float* __restrict__ X, int K, int kc,
-                                         const int32_t* __restrict__ col,
-                                         const float* __restrict__ w) {
+__device__ __forceinline__ void idx_load_body(IdxRegs& R, const int32_t* __restrict__ col,
+                                              const float* __restrict__ w) {
+  if (R.ne > CAPE) return;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < CAPE / NT; ++u) {
+    const int j = tid + u * NT;
+    const int jc = j < R.ne ? j : 0;
+    R.c[u] = col[R.eb + jc];
+    R.w[u] = w ? w[R.eb + jc] : 1.f;
+  }
+}
+
+// Writes the prefetched block to LDS. Ends with a barrier (block-wide OR of "an entry leaves
+// the tile"); `staged` = the tile takes the local path.
+__device__ __forceinline__ void idx_store(TileIdx& ti, bool& staged, const IdxRegs& R,
+                                          int64_t r0) {
+  const int tid = threadIdx.x;
+  if (tid <= TM) ti.rp[tid] = R.rp;
+  bool fits = R.ne <= CAPE;
+  int out = 0;
+  if (fits) {
+#pragma unroll
+    for (int u = 0; u < CAPE / NT; ++u) {
+      const int j = tid + u * NT;
+      const int rel = R.c[u] - (int)r0;
+      if (j < R.ne && (unsigned)rel >= (unsigned)TM) out = 1;
+    }
+  }
+  const bool any_out = __syncthreads_or(out);
+  staged = fits && !any_out;
+  if (staged) {
+#pragma unroll
+    for (int u = 0; u < CAPE / NT; ++u) {
+      const int j = tid + u * NT;
+      if (j < R.ne) ti.ow[j] = make_int2((R.c[u] - (int)r0) * LDS, __float_as_int(R.w[u]));
+    }
+    if (tid < EB) ti.ow[R.ne + tid] = make_int2(0, 0);
+  }
+}
+
+// sum_{e in row rr} w_e * X[c_e][4li..], in CSR order.
+// Local path: every source row is in the LDS image A; per entry one ds_read_b64 (offset,
+// weight), one ds_read_b128 and two packed FMAs, no bounds logic and no global access (so no
+// vmcnt wait that would drain the prefetch loads and row stores in flight).
+__device__ __forceinline__ f32x4 agg_row_local(const TileIdx& ti, int rr, const float* A) {
   const int li = threadIdx.x & 31;
   const int eb = ti.rp[0];
+  const int e0 = ti.rp[rr] - eb, e1 = ti.rp[rr + 1] - eb;
+  f32x4 acc = zero4();
+  for (int e = e0; e < e1; e += EB) {
+    int2 p[EB];
+#pragma unroll
+    for (int u = 0; u < EB; ++u) p[u] = ti.ow[e + u];
+    f32x4 v[EB];
+#pragma unroll
+    for (int u = 0; u < EB; ++u) v[u] = ld4(A + p[u].x + 4 * li);
+#pragma unroll
+    for (int u = 0; u < EB; ++u) {
+      const float wv = e + u < e1 ? __int_as_float(p[u].y) : 0.f;
+      acc += wv * v[u];
+    }
+  }
+  return acc;
+}
+
+// Global path (graphs straddling tiles, or more than CAPE entries): CSR and source rows read
+// from global memory, same order and arithmetic as the local path (bitwise-identical sums).
+__device__ __forceinline__ f32x4 agg_row_global(const TileIdx& ti, int rr,
+                                                const float* __restrict__ X, int K, int kc,
+                                                const int32_t* __restrict__ col,
+                                                const float* __restrict__ w) {
   const int e0 = ti.rp[rr], e1 = ti.rp[rr + 1];
   f32x4 acc = zero4();
   for (int e = e0; e < e1; e += EB) {
@@ -98,33 +212,14 @@ __device__ __forceinline__ f32x4 agg_row(const TileIdx& ti, bool staged, int rr,
     for (int u = 0; u < EB; ++u) {
       const bool ok = e + u < e1;
       const int ee = ok ? e + u : e0;
-      c[u] = staged ? ti.col[ee - eb] : col[ee];
-      const float wv = staged ? ti.w[ee - eb] : (w ? w[ee] : 1.f);
-      ww[u] = ok ? wv : 0.f;
+      c[u] = col[ee];
+      ww[u] = ok ? (w ? w[ee] : 1.f) : 0.f;
     }
     f32x4 v[EB];
-    bool out = false;
 #pragma unroll
-    for (int u = 0; u < EB; ++u) {
-      const int64_t rel = (int64_t)c[u] - r0;
-      const bool in = rel >= 0 && rel < TM;
-      out |= (e + u < e1) && !in;
-      v[u] = ld4(A + (in ? (int)rel : 0) * LDS + 4 * li);
-    }
-    if (__any(out)) {
+    for (int u = 0; u < EB; ++u) v[u] = ld4(X + (int64_t)c[u] * K + kc);
 #pragma unroll
-      for (int u = 0; u < EB; ++u) {
-        const int64_t rel = (int64_t)c[u] - r0;
-        const bool in = rel >= 0 && rel < TM;
-        const f32x4 g = ld4(X + (int64_t)c[u] * K + kc);
-        v[u] = in ? v[u] : g;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < EB; ++u) {
-      const f32x4 t = ww[u] * v[u];
-      acc += (e + u < e1) ? t : zero4();
-    }
+    for (int u = 0; u < EB; ++u) acc += ww[u] * v[u];
   }
   return acc;
 }
@@ -139,7 +234,8 @@ __global__ __launch_bounds__(NT, 2) void k_fwd(const float* __restrict__ X, int6
                                                const float* __restrict__ w, float self_scale,
                                                const float* __restrict__ W,
                                                const float* __restrict__ b, int N,
-                                               float* __restrict__ Y, float* __restrict__ S_out) {
+                                               float* __restrict__ Y, float* __restrict__ S_out,
+                                               const int32_t* __restrict__ tmask, int want) {
   __shared__ __attribute__((aligned(16))) float A[TM * LDS];
   __shared__ __attribute__((aligned(16))) float S[GATHER ? TM * LDS : 4];
   __shared__ TileIdx ti;
@@ -149,6 +245,8 @@ __global__ __launch_bounds__(NT, 2) void k_fwd(const float* __restrict__ X, int6
   const int n = wave * 32 + li;
   const int ncl = n < N ? n : N - 1;
   const bool wave_active = wave * 32 < N;
+  int64_t t = seek_tile(blockIdx.x, ntiles, tmask, want);
+  if (t >= ntiles) return;
   float bf[64];
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
@@ -160,30 +258,66 @@ __global__ __launch_bounds__(NT, 2) void k_fwd(const float* __restrict__ X, int6
   }
   const float bias = b ? b[ncl] : 0.f;
   const int kc = 4 * li < K ? 4 * li : K - 4;
+  const Buf bX = mkbuf(X, M * K * 4), bY = mkbuf(Y, M * N * 4);
+  const Buf bS = mkbuf(S_out, S_out ? M * K * 4 : 0);
   float* Ain = GATHER ? S : A;  // MFMA A-operand image
 
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  if constexpr (ABL & 32) {  // desync experiment: odd blocks start half a tile late
+    if (blockIdx.x & 1) {
+      for (int i = 0; i < 4; ++i) __builtin_amdgcn_s_sleep(127);
+    }
+  }
+  // pipeline prologue: the first tile's rows and index block
+  f32x4 xr[8];
+  IdxRegs R;
+  if constexpr (!(ABL & 16)) load_rows(xr, bX, K, (int)(t * TM));
+  if constexpr (GATHER && !(ABL & 2)) {
+    idx_load_head(R, rowptr, M, t * TM);
+    idx_load_body(R, col, w);
+  }
+  for (; t < ntiles; t = seek_tile(t + gridDim.x, ntiles, tmask, want)) {
     const int64_t r0 = t * TM;
-    f32x4 xr[8];
-    load_rows(xr, X, M, K, r0);
+    const int64_t tn = seek_tile(t + gridDim.x, ntiles, tmask, want);
+    const bool has_next = tn < ntiles;
     bool staged = true;
-    if constexpr (GATHER) stage_idx(ti, staged, rowptr, col, w, M, r0);
+    if constexpr (ABL & 16) {
+#pragma unroll
+      for (int it = 0; it < 8; ++it) xr[it] = zero4();
+    }
     store_rows_lds(A, xr, M, K, r0);
+    if constexpr (GATHER && !(ABL & 2)) idx_store(ti, staged, R, r0);
     __syncthreads();
+    // prefetch: next tile's rows and index head fly during this tile's aggregation and MFMAs
+    if (has_next) {
+      if constexpr (!(ABL & 16)) load_rows(xr, bX, K, (int)(tn * TM));
+      if constexpr (GATHER && !(ABL & 2)) idx_load_head(R, rowptr, M, tn * TM);
+    }
     if constexpr (GATHER) {
-#pragma unroll 2
-      for (int it = 0; it < 8; ++it) {
-        const int rr = hw + 8 * it;
-        f32x4 a = agg_row(ti, staged, rr, A, r0, X, K, kc, col, w);
-        if (self_scale != 0.f) a += self_scale * xr[it];
-        a = sel4(4 * li < K && r0 + rr < M, a);
-        st4(S + rr * LDS + 4 * li, a);
-        if (S_out && r0 + rr < M && 4 * li < K) st4(S_out + (r0 + rr) * K + 4 * li, a);
+      auto agg_tile = [&](auto staged_tag) {
+        constexpr bool STG = decltype(staged_tag)::value;
+#pragma unroll 1
+        for (int it = 0; it < 8; ++it) {
+          const int rr = hw + 8 * it;
+          f32x4 a;
+          if constexpr (ABL & 2) a = ld4(A + rr * LDS + 4 * li);
+          else if constexpr (STG) a = agg_row_local(ti, rr, A);
+          else a = agg_row_global(ti, rr, X, K, kc, col, w);
+          if (self_scale != 0.f) a += self_scale * ld4(A + rr * LDS + 4 * li);
+          a = sel4(4 * li < K && r0 + rr < M, a);
+          st4(S + rr * LDS + 4 * li, a);
+          if (!(ABL & 4) && S_out && 4 * li < K)
+            bst4(bS, (int)((r0 + rr) * K + 4 * li) * 4, a);
+        }
+      };
+      if (staged) agg_tile(std::true_type{});
+      else agg_tile(std::false_type{});
+      if constexpr (!(ABL & 2)) {
+        if (has_next) idx_load_body(R, col, w);
       }
       __syncthreads();
     }
     f32x16 acc0 = {}, acc1 = {};
-    if (wave_active) {
+    if (wave_active && !(ABL & 1)) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const f32x4 a0 = ld4(Ain + li * LDS + 64 * h + 4 * q);
@@ -209,11 +343,11 @@ __global__ __launch_bounds__(NT, 2) void k_fwd(const float* __restrict__ X, int6
       A[(32 + rl) * LDS + n] = v1;
     }
     __syncthreads();
-    if (4 * li < N) {
+    if (4 * li < N && !(ABL & 4)) {
 #pragma unroll
       for (int it = 0; it < 8; ++it) {
         const int rr = hw + 8 * it;
-        if (r0 + rr < M) st4(Y + (r0 + rr) * N + 4 * li, ld4(A + rr * LDS + 4 * li));
+        bst4(bY, (int)((r0 + rr) * N + 4 * li) * 4, ld4(A + rr * LDS + 4 * li));
       }
     }
     __syncthreads();
@@ -240,36 +374,77 @@ __global__ __launch_bounds__(NT, 2) void k_bwd(
   const int oc = 4 * li < N ? 4 * li : N - 4;
   const bool oin = 4 * li < N;
 
+  const Buf bdY = mkbuf(dY, M * N * 4), bH = mkbuf(H, H ? M * N * 4 : 0);
+  const Buf bX = mkbuf(X, M * K * 4), bdX = mkbuf(dXpre, dXpre ? M * K * 4 : 0);
   f32x16 dw[4] = {{}, {}, {}, {}};
   float dbacc = 0.f;
   const int kx = 32 * wave + li;
   const int kxc = kx < K ? kx : K - 1;
 
+  // pipeline prologue (TRANSPOSE): the first tile's dY rows and transpose-CSR index block
+  f32x4 dr[8];
+  IdxRegs R;
+  if constexpr (GMODE == LGNN_GRAD_TRANSPOSE) {
+    const int64_t t0 = blockIdx.x;
+    if (t0 < ntiles) {
+      if constexpr (!(ABL & 16)) load_rows(dr, bdY, N, (int)(t0 * TM));
+      if constexpr (!(ABL & 2)) {
+        idx_load_head(R, tptr, M, t0 * TM);
+        idx_load_body(R, tidx, tw);
+      }
+    }
+  }
+
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int64_t r0 = t * TM;
+    const int64_t tn = t + gridDim.x;
+    const bool has_next = tn < ntiles;
     // ---- dZ tile -> C
     if constexpr (GMODE == LGNN_GRAD_TRANSPOSE) {
-      bool staged;
-      {
-        f32x4 dr[8];
-        load_rows(dr, dY, M, N, r0);
-        stage_idx(ti, staged, tptr, tidx, tw, M, r0);
-        store_rows_lds(A, dr, M, N, r0);
+      bool staged = true;
+      if constexpr (ABL & 16) {
+#pragma unroll
+        for (int it = 0; it < 8; ++it) dr[it] = zero4();
+      }
+      store_rows_lds(A, dr, M, N, r0);
+      if constexpr (!(ABL & 2)) idx_store(ti, staged, R, r0);
+      // this tile's H rows (ELU') are issued before the barrier so they land during it
+      f32x4 hv[8];
+      if constexpr (ACT == LGNN_ACT_ELU) {
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+          const int64_t row = r0 + hw + 8 * it, rc = row < M ? row : M - 1;
+          hv[it] = (ABL & 16) ? zero4() : bld4(bH, (int)(row * N + oc) * 4);
+        }
       }
       __syncthreads();
+      // prefetch: next tile's dY rows and index head
+      if (has_next) {
+        if constexpr (!(ABL & 16)) load_rows(dr, bdY, N, (int)(tn * TM));
+        if constexpr (!(ABL & 2)) idx_load_head(R, tptr, M, tn * TM);
+      }
+      auto agg_tile = [&](auto staged_tag) {
+        constexpr bool STG = decltype(staged_tag)::value;
 #pragma unroll 1
-      for (int it = 0; it < 8; ++it) {
-        const int rr = hw + 8 * it;
-        const int64_t row = r0 + rr, rc = row < M ? row : M - 1;
-        f32x4 hv = zero4();
-        if constexpr (ACT == LGNN_ACT_ELU) hv = ld4(H + rc * N + oc);
-        f32x4 g = agg_row(ti, staged, rr, A, r0, dY, N, oc, tidx, tw);
-        if (tself != 0.f) g += tself * ld4(A + rr * LDS + 4 * li);
-        if constexpr (ACT == LGNN_ACT_ELU) {
+        for (int it = 0; it < 8; ++it) {
+          const int rr = hw + 8 * it;
+          const int64_t row = r0 + rr;
+          f32x4 g;
+          if constexpr (ABL & 2) g = ld4(A + rr * LDS + 4 * li);
+          else if constexpr (STG) g = agg_row_local(ti, rr, A);
+          else g = agg_row_global(ti, rr, dY, N, oc, tidx, tw);
+          if (tself != 0.f) g += tself * ld4(A + rr * LDS + 4 * li);
+          if constexpr (ACT == LGNN_ACT_ELU) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) g[j] *= elu_grad_from_out(hv[j]);
+            for (int j = 0; j < 4; ++j) g[j] *= elu_grad_from_out(hv[it][j]);
+          }
+          st4(C + rr * LDS + 4 * li, sel4(oin && row < M, g));
         }
-        st4(C + rr * LDS + 4 * li, sel4(oin && row < M, g));
+      };
+      if (staged) agg_tile(std::true_type{});
+      else agg_tile(std::false_type{});
+      if constexpr (!(ABL & 2)) {
+        if (has_next) idx_load_body(R, tidx, tw);
       }
     } else {
       f32x4 g[8], hv[8];
@@ -302,7 +477,12 @@ __global__ __launch_bounds__(NT, 2) void k_bwd(
     }
     // ---- S tile -> A (A's raw dY image is dead once every wave has passed this barrier)
     f32x4 sr[8];
-    load_rows(sr, X, M, K, r0);
+    if constexpr (ABL & 16) {
+#pragma unroll
+      for (int it = 0; it < 8; ++it) sr[it] = zero4();
+    } else {
+      load_rows(sr, bX, K, (int)r0);
+    }
     __syncthreads();
     store_rows_lds(A, sr, M, K, r0);
     __syncthreads();
@@ -333,7 +513,7 @@ __global__ __launch_bounds__(NT, 2) void k_bwd(
     }
     // dW[o][k] += sum_m dZ[m][o] S[m][k]; wave owns o in [32w, 32w+32)
 #pragma unroll 4
-    for (int s = 0; s < TM / 2; ++s) {
+    for (int s = 0; s < (ABL & 1 ? 0 : TM / 2); ++s) {
       const int m = 2 * s + h;
       const float a = C[m * LDS + 32 * wave + li];
 #pragma unroll
@@ -342,7 +522,7 @@ __global__ __launch_bounds__(NT, 2) void k_bwd(
     if constexpr (DX) {
       f32x16 x0 = {}, x1 = {};
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
+      for (int q = 0; q < (ABL & 1 ? 0 : 16); ++q) {
         const f32x4 a0 = ld4(C + li * LDS + 64 * h + 4 * q);
         const f32x4 a1 = ld4(C + (32 + li) * LDS + 64 * h + 4 * q);
 #pragma unroll
@@ -359,11 +539,11 @@ __global__ __launch_bounds__(NT, 2) void k_bwd(
         A[(32 + rl) * LDS + kx] = x1[r];
       }
       __syncthreads();
-      if (4 * li < K) {
+      if (4 * li < K && !(ABL & 4)) {
 #pragma unroll
         for (int it = 0; it < 8; ++it) {
           const int rr = hw + 8 * it;
-          if (r0 + rr < M) st4(dXpre + (r0 + rr) * K + 4 * li, ld4(A + rr * LDS + 4 * li));
+          bst4(bdX, (int)((r0 + rr) * K + 4 * li) * 4, ld4(A + rr * LDS + 4 * li));
         }
       }
     }
@@ -382,11 +562,183 @@ __global__ __launch_bounds__(NT, 2) void k_bwd(
   if (dbp && tid < N) dbp[(int64_t)blockIdx.x * N + tid] = dbacc;
 }
 
+
+// ------------------------------------------------------------------------------------------
+// Fused layer stack, forward: a workgroup keeps one 64-node tile on chip through every layer
+//   H_0 = X W_0^T + b_0                      (in_proj; skipped when FIRST = false: X is H_0)
+//   S_l = Â H_{l-1},  H_l = ELU(S_l W_l^T + b_l),  l = 1..L   (GCNConv + the model's F.elu)
+// storing H_l and S_l for the backward. The tile's CSR block is staged once for all layers;
+// the next tile's rows and CSR block are prefetched into registers while this tile computes,
+// and each layer's weight fragment is fetched (L2) while the previous layer finishes its
+// epilogue and aggregation. Every k-NN neighbour of a graph aligned to the tile is in LDS.
+// All widths <= 128 (fast-path shapes).
+// ------------------------------------------------------------------------------------------
+struct StackArgs {
+  const float* W[LGNN_MAX_STACK];
+  const float* b[LGNN_MAX_STACK];
+  float* H[LGNN_MAX_STACK];
+  float* S[LGNN_MAX_STACK];
+  int width[LGNN_MAX_STACK + 1];  // width[0] = input width, width[l+1] = output of layer l
+};
+
+__device__ __forceinline__ void load_bfrag(float (&bf)[64], const float* __restrict__ W, int N,
+                                           int K) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h = lane >> 5, li = lane & 31;
+  const int n = wave * 32 + li;
+  const int ncl = n < N ? n : N - 1;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int k = 64 * h + 4 * q;
+    const f32x4 v = ld4(W + (int64_t)ncl * K + (k < K ? k : K - 4));
+    const bool ok = n < N && k < K;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[4 * q + j] = ok ? v[j] : 0.f;
+  }
+}
+
+template <bool FIRST>
+__global__ __launch_bounds__(NT, 2) void k_stack_fwd(const float* __restrict__ X, int64_t M,
+                                                     const int32_t* __restrict__ rowptr,
+                                                     const int32_t* __restrict__ col,
+                                                     const float* __restrict__ w, int L,
+                                                     StackArgs args,
+                                                     const int32_t* __restrict__ tmask) {
+  __shared__ __attribute__((aligned(16))) float A[TM * LDS];
+  __shared__ __attribute__((aligned(16))) float S[TM * LDS];
+  __shared__ TileIdx ti;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, li = lane & 31, hw = wave * 2 + h;
+  const int64_t ntiles = (M + TM - 1) / TM;
+  const int n = wave * 32 + li;
+  const int l0 = FIRST ? 0 : 1;
+  const int K0 = args.width[FIRST ? 0 : 1];
+
+  int stamp = 0;
+  STAMP(stamp++);
+  int64_t t = seek_tile(blockIdx.x, ntiles, tmask, 0);
+  if (t >= ntiles) return;
+  f32x4 xr[8];
+  IdxRegs R;
+  float bf[64];
+  const Buf bX = mkbuf(X, M * K0 * 4);
+  const bool any_conv = L >= 1;
+  load_rows(xr, bX, K0, (int)(t * TM));
+  if (any_conv) idx_load_head(R, rowptr, M, t * TM);
+  load_bfrag(bf, args.W[l0], args.width[l0 + 1], args.width[l0]);
+  if (any_conv) idx_load_body(R, col, w);
+  for (; t < ntiles; t = seek_tile(t + gridDim.x, ntiles, tmask, 0)) {
+    const int64_t r0 = t * TM;
+    const int64_t tn = seek_tile(t + gridDim.x, ntiles, tmask, 0);
+    const bool has_next = tn < ntiles;
+    bool staged = true;
+    store_rows_lds(A, xr, M, K0, r0);
+    if (any_conv) idx_store(ti, staged, R, r0);
+    __syncthreads();
+    STAMP(stamp++);
+    if (has_next) {
+      load_rows(xr, bX, K0, (int)(tn * TM));
+      if (any_conv) idx_load_head(R, rowptr, M, tn * TM);
+    }
+    for (int l = l0; l <= L; ++l) {
+      const int K = args.width[l], N = args.width[l + 1];
+      const bool conv = l > 0;
+      const float* Ain = conv ? S : A;
+      if (conv) {
+        const int kc = 4 * li < K ? 4 * li : K - 4;
+        auto agg_tile = [&](auto staged_tag) {
+          constexpr bool STG = decltype(staged_tag)::value;
+#pragma unroll 1
+          for (int it = 0; it < 8; ++it) {
+            const int rr = hw + 8 * it;
+            f32x4 a = STG ? agg_row_local(ti, rr, A)
+                          : agg_row_global(ti, rr, args.H[l - 1], K, kc, col, w);
+            a = sel4(4 * li < K && r0 + rr < M, a);
+            st4(S + rr * LDS + 4 * li, a);
+            if (4 * li < K) bst4(mkbuf(args.S[l], M * K * 4), (int)((r0 + rr) * K + 4 * li) * 4, a);
+          }
+        };
+        if (staged) agg_tile(std::true_type{});
+        else agg_tile(std::false_type{});
+        if (l == 1 && has_next) idx_load_body(R, col, w);  // the head has landed by now
+        __syncthreads();
+        STAMP(stamp++);
+      }
+      f32x16 acc0 = {}, acc1 = {};
+      if (wave * 32 < N) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const f32x4 a0 = ld4(Ain + li * LDS + 64 * h + 4 * q);
+          const f32x4 a1 = ld4(Ain + (32 + li) * LDS + 64 * h + 4 * q);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc0 = mfma32(a0[j], bf[4 * q + j], acc0);
+            acc1 = mfma32(a1[j], bf[4 * q + j], acc1);
+          }
+        }
+      }
+      STAMP(stamp++);
+      // next layer's weight fragment (or the first layer's, for the next tile)
+      const int lnext = l < L ? l + 1 : l0;
+      if (l < L || has_next)
+        load_bfrag(bf, args.W[lnext], args.width[lnext + 1], args.width[lnext]);
+      __syncthreads();  // every wave is done reading A / S
+      STAMP(stamp++);
+      const float bias = n < N ? args.b[l][n] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
+        float v0 = acc0[r] + bias, v1 = acc1[r] + bias;
+        if (conv) {
+          v0 = elu_f(v0);
+          v1 = elu_f(v1);
+        }
+        if (n < N) {
+          A[rl * LDS + n] = v0;
+          A[(32 + rl) * LDS + n] = v1;
+        }
+      }
+      __syncthreads();
+      if (4 * li < N) {
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+          const int rr = hw + 8 * it;
+          bst4(mkbuf(args.H[l], M * N * 4), (int)((r0 + rr) * N + 4 * li) * 4,
+               ld4(A + rr * LDS + 4 * li));
+        }
+      }
+      // A now holds H_l (zero beyond N) for the next layer's aggregation
+      if (l == L) __syncthreads();
+      STAMP(stamp++);
+    }
+  }
+}
+// open[t] = 1 if an edge joins a node of tile t with a node of another tile (target CSR).
+__global__ __launch_bounds__(NT) void k_tile_open(const int32_t* __restrict__ rowptr,
+                                                  const int32_t* __restrict__ col, int64_t M,
+                                                  int32_t* __restrict__ open) {
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < M; i += (int64_t)gridDim.x * NT) {
+    const int ti = (int)(i / TM);
+    const int e0 = rowptr[i], e1 = rowptr[i + 1];
+    for (int e = e0; e < e1; ++e) {
+      const int tj = col[e] / TM;
+      if (tj != ti) {
+        open[ti] = 1;  // benign race: every writer stores 1
+        open[tj] = 1;
+      }
+    }
+  }
+}
+
 }  // namespace lgnn_tile
 
 using namespace lgnn_tile;
 
-bool lgnn_tile_fits(int K, int N) { return K <= KC && N <= KC && K % 4 == 0 && N % 4 == 0; }
+// Fast-path shapes; buffer offsets are 32-bit signed byte offsets, so tensors stay < 2 GiB.
+bool lgnn_tile_fits(int64_t M, int K, int N) {
+  return K <= KC && N <= KC && K % 4 == 0 && N % 4 == 0 && K > 0 && N > 0 &&
+         (M + TM) * (int64_t)(K > N ? K : N) * 4 < (int64_t)INT32_MAX;
+}
 
 int lgnn_tile_partials(int64_t M) {
   const int64_t ntiles = (M + TM - 1) / TM;
@@ -396,12 +748,13 @@ int lgnn_tile_partials(int64_t M) {
 
 hipError_t lgnn_tile_fwd(hipStream_t s, const float* X, int64_t M, int K, const int32_t* rowptr,
                          const int32_t* col, const float* w, float self_scale, const float* W,
-                         const float* b, int N, int act, float* Y, float* S_out) {
+                         const float* b, int N, int act, float* Y, float* S_out,
+                         const int32_t* tile_mask, int want) {
   const int64_t ntiles = (M + TM - 1) / TM;
   dim3 grid((unsigned)(ntiles < 512 ? ntiles : 512));
 #define LGNN_TF(G, A)                                                                         \
   hipLaunchKernelGGL((k_fwd<G, A>), grid, dim3(NT), 0, s, X, M, K, rowptr, col, w, self_scale, \
-                     W, b, N, Y, S_out)
+                     W, b, N, Y, S_out, tile_mask, want)
   if (rowptr) {
     if (act == LGNN_ACT_ELU) LGNN_TF(true, LGNN_ACT_ELU);
     else LGNN_TF(true, LGNN_ACT_NONE);
@@ -437,3 +790,77 @@ hipError_t lgnn_tile_bwd(hipStream_t s, int grad_mode, const float* dY, const in
 #undef LGNN_TB
   return hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------------
+// C ABI: fused GCN stack forward
+// ------------------------------------------------------------------------------------------
+extern "C" int lgnn_tile_count(int64_t M) {
+  if (M < 0) return LGNN_EINVAL;
+  return (int)((M + lgnn_tile::TM - 1) / lgnn_tile::TM);
+}
+
+extern "C" int lgnn_tile_open(const int32_t* rowptr, const int32_t* col, int64_t M,
+                              int32_t* open, void* stream) {
+  if (M < 0 || !open || (M > 0 && (!rowptr || !col))) return LGNN_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t ntiles = (M + lgnn_tile::TM - 1) / lgnn_tile::TM;
+  if (ntiles == 0) return LGNN_OK;
+  if (hipMemsetAsync(open, 0, ntiles * sizeof(int32_t), s) != hipSuccess)
+    return (int)hipGetLastError();
+  int64_t g = (M + lgnn_tile::NT - 1) / lgnn_tile::NT;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(lgnn_tile::k_tile_open, dim3((unsigned)g), dim3(lgnn_tile::NT), 0, s, rowptr,
+                     col, M, open);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? LGNN_OK : (int)e;
+}
+
+extern "C" int lgnn_gcn_stack_fwd(const float* X, int64_t M, int d_in, int has_in_proj,
+                                  const int32_t* rowptr, const int32_t* col, const float* w,
+                                  int L, const float* const* W, const float* const* b,
+                                  const int* widths, float* const* H, float* const* S,
+                                  const int32_t* tile_open, void* stream) {
+  if (M < 0 || L < 0 || L + 1 > LGNN_MAX_STACK || !W || !b || !widths || !H || !S)
+    return LGNN_EINVAL;
+  if (L > 0 && (!rowptr || !col)) return LGNN_EINVAL;
+  lgnn_tile::StackArgs a = {};
+  const int l0 = has_in_proj ? 0 : 1;
+  if (l0 > L) return LGNN_EINVAL;
+  a.width[0] = d_in;
+  for (int l = 0; l <= L; ++l) {
+    a.width[l + 1] = widths[l];
+    if (l < l0) continue;
+    const int K = a.width[l], N = a.width[l + 1];
+    if (!lgnn_tile_fits(M, K, N) || !W[l] || !H[l]) return LGNN_EINVAL;
+    if (l > 0 && !S[l]) return LGNN_EINVAL;
+    a.W[l] = W[l];
+    a.b[l] = b[l];
+    a.H[l] = H[l];
+    a.S[l] = l > 0 ? S[l] : nullptr;
+  }
+  if (!has_in_proj) {
+    if (widths[0] != d_in) return LGNN_EINVAL;
+    a.H[0] = const_cast<float*>(X);  // the conv stack's input (first aggregation's fallback)
+  }
+  for (int l = l0; l <= L; ++l)
+    if (!a.b[l]) return LGNN_EINVAL;
+  if (M == 0) return LGNN_OK;
+  if (M > 0 && !X) return LGNN_EINVAL;
+  const int64_t ntiles = (M + lgnn_tile::TM - 1) / lgnn_tile::TM;
+  dim3 grid((unsigned)(ntiles < 512 ? ntiles : 512));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (has_in_proj)
+    hipLaunchKernelGGL(lgnn_tile::k_stack_fwd<true>, grid, dim3(lgnn_tile::NT), 0, s, X, M,
+                       rowptr, col, w, L, a, tile_open);
+  else
+    hipLaunchKernelGGL(lgnn_tile::k_stack_fwd<false>, grid, dim3(lgnn_tile::NT), 0, s, X, M,
+                       rowptr, col, w, L, a, tile_open);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? LGNN_OK : (int)e;
+}
+
+#ifdef LGNN_STAMPS
+extern "C" int lgnn_debug_stamps(unsigned long long* host_out) {
+  return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(lgnn_stamp_buf), sizeof(lgnn_stamp_buf));
+}
+#endif

@@ -46,6 +46,7 @@ class Graph:
         self.num_nodes = int(num_nodes)
         self.device = edge_index.device
         self._csr: dict[str, Csr] = {}
+        self._aux: dict[str, torch.Tensor] = {}
         self.batch = None
         self.gptr = None
         self.num_graphs = None
@@ -95,6 +96,18 @@ class Graph:
                   _lib.stream(dev))
         self._csr[kind] = c
         return c
+
+    def tile_open(self, kind: str) -> torch.Tensor:
+        """int32 [ceil(N/64)]: 1 for the 64-node tiles an edge leaves (lgnn_tile_open)."""
+        key = "open:" + kind
+        if key not in self._aux:
+            c = self.csr(kind)
+            n_t = _lib.load().lgnn_tile_count(self.num_nodes)
+            t = torch.empty(max(n_t, 1), dtype=torch.int32, device=self.device)
+            _lib.call("lgnn_tile_open", _lib.ptr(c.rowptr), _lib.ptr(c.col), self.num_nodes,
+                      _lib.ptr(t), _lib.stream(self.device))
+            self._aux[key] = t
+        return self._aux[key]
 
     def dropped_edges(self, kind: str) -> int:
         """Number of edges with an out-of-range index (synchronises)."""

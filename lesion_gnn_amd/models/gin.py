@@ -36,11 +36,15 @@ class GIN(nn.Module):
         self.dropout = nn.Dropout(dropout)
         self.pool = pool
 
-    def set_sync_bn(self, group) -> None:
+    def set_sync_bn(self, group, global_count: int | None = None) -> None:
         """SyncBatchNorm over a torch.distributed group (RCCL): BN statistics and their backward
-        sums are all-reduced, so N replicas compute exactly the single-device batch statistics."""
+        sums are all-reduced, so N replicas compute exactly the single-device batch statistics.
+        global_count: the total node count over the group when every step has the same one
+        (skips the per-step count all-reduce and its host read, so the step can be captured
+        in a HIP graph); None = all-reduce the count every step."""
         for c in self.convs:
             c.sync_group = group
+            c.sync_count = global_count
 
     def forward(self, x: torch.Tensor, edge_index, batch: torch.Tensor,
                 num_graphs: int | None = None) -> torch.Tensor:

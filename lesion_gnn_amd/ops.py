@@ -10,6 +10,8 @@
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -48,6 +50,42 @@ def linear_fwd(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None, act: in
               _lib.ptr(csr.w) if csr else None, float(self_scale), _lib.ptr(W), _lib.ptr(b), N,
               act, _lib.ptr(y), _lib.ptr(s_out), _s(x.device))
     return (y, s_out) if save_s else y
+
+
+STACK_MAX = 8  # LGNN_MAX_STACK
+
+
+def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list):
+    """in_proj + L x ELU(GCNConv) forward, every width <= 128: returns ([H_0..H_L],
+    [S_1..S_L]). Tiles no edge leaves run fused through every layer (lgnn_gcn_stack_fwd); the
+    rest (graphs straddling 64-node tiles) layer by layer (lgnn_node_linear_fwd_tiles), into the
+    same buffers. With graphs aligned to tiles (C2: N = 64) the second group is empty."""
+    csr = graph.csr("gcn")
+    open_ = graph.tile_open("gcn")
+    M = x.size(0)
+    L = len(Ws) - 1
+    dev = x.device
+    hs = [torch.empty(M, W.size(0), dtype=torch.float32, device=dev) for W in Ws]
+    ss = [torch.empty(M, Ws[l].size(1), dtype=torch.float32, device=dev) for l in range(1, L + 1)]
+    arr = ctypes.c_void_p * (L + 1)
+    Wp = arr(*[W.data_ptr() for W in Ws])
+    bp = arr(*[b.data_ptr() for b in bs])
+    Hp = arr(*[h.data_ptr() for h in hs])
+    Sp = arr(None, *[t.data_ptr() for t in ss])
+    widths = (ctypes.c_int * (L + 1))(*[W.size(0) for W in Ws])
+    _lib.call("lgnn_gcn_stack_fwd", _lib.ptr(x), M, x.size(1), 1, _lib.ptr(csr.rowptr),
+              _lib.ptr(csr.col), _lib.ptr(csr.w), L, Wp, bp, widths, Hp, Sp, _lib.ptr(open_),
+              _s(dev))
+    for l in range(L + 1):
+        inp = x if l == 0 else hs[l - 1]
+        c = csr if l > 0 else None
+        _lib.call("lgnn_node_linear_fwd_tiles", _lib.ptr(inp), M, inp.size(1),
+                  _lib.ptr(c.rowptr) if c else None, _lib.ptr(c.col) if c else None,
+                  _lib.ptr(c.w) if c else None, 0.0, _lib.ptr(Ws[l]), _lib.ptr(bs[l]),
+                  Ws[l].size(0), _lib.LGNN_ACT_ELU if l > 0 else _lib.LGNN_ACT_NONE,
+                  _lib.ptr(hs[l]), _lib.ptr(ss[l - 1]) if l > 0 else None, _lib.ptr(open_), 1,
+                  _s(dev))
+    return hs, ss
 
 
 def num_partials(M: int, N: int, K: int, gather: bool = False) -> int:
@@ -231,19 +269,25 @@ class _GCNStack(torch.autograd.Function):
         params = [_f32c(p) for p in params]
         csr = graph.csr("gcn")
         W_in, b_in = params[0], params[1]
-        hs = [linear_fwd(x, W_in, b_in, _lib.LGNN_ACT_NONE)]
-        ss = []  # aggregated conv inputs S_l = A_hat H_{l-1} (saved when the fast path applies)
-        ctx.saved_s = []
-        for l in range(L):
-            W, b = params[2 + 2 * l], params[3 + 2 * l]
-            fast = fast_shape(W.size(1), W.size(0))
-            if fast:
-                h, s_ = linear_fwd(hs[-1], W, b, _lib.LGNN_ACT_ELU, csr, save_s=True)
-            else:
-                h, s_ = linear_fwd(hs[-1], W, b, _lib.LGNN_ACT_ELU, csr), hs[-1]
-            hs.append(h)
-            ss.append(s_)
-            ctx.saved_s.append(fast)
+        Ws = [params[2 * l] for l in range(L + 1)]
+        fused = L + 1 <= STACK_MAX and all(fast_shape(W.size(1), W.size(0)) for W in Ws)
+        if fused:
+            hs, ss = stack_fwd(x, graph, Ws, [params[2 * l + 1] for l in range(L + 1)])
+            ctx.saved_s = [True] * L
+        else:
+            hs = [linear_fwd(x, W_in, b_in, _lib.LGNN_ACT_NONE)]
+            ss = []  # aggregated conv inputs S_l = A_hat H_{l-1} (saved on the fast path)
+            ctx.saved_s = []
+            for l in range(L):
+                W, b = params[2 + 2 * l], params[3 + 2 * l]
+                fast = fast_shape(W.size(1), W.size(0))
+                if fast:
+                    h, s_ = linear_fwd(hs[-1], W, b, _lib.LGNN_ACT_ELU, csr, save_s=True)
+                else:
+                    h, s_ = linear_fwd(hs[-1], W, b, _lib.LGNN_ACT_ELU, csr), hs[-1]
+                hs.append(h)
+                ss.append(s_)
+                ctx.saved_s.append(fast)
         W_out, b_out = params[2 + 2 * L], params[3 + 2 * L]
         pooled, logits = pool_head_fwd(hs[-1], graph, mean, W_out, b_out)
         ctx.save_for_backward(x, pooled, *hs, *ss, *params)
@@ -367,9 +411,11 @@ def bn_bwd_apply(dA, Z, mask, scale, shift, mean, invstd, sums, count, training,
     return dZ, dg, db
 
 
-def _global_count(M: int, group, dev) -> float:
+def _global_count(M: int, group, dev, fixed=None) -> float:
     if group is None:
         return float(M)
+    if fixed is not None:
+        return float(fixed)
     import torch.distributed as dist
 
     t = torch.tensor([float(M)], dtype=torch.float64, device=dev)
@@ -385,7 +431,8 @@ class _GINConv(torch.autograd.Function):
     statistics; SyncBN over `group` when given)."""
 
     @staticmethod
-    def forward(ctx, x, W1, b1, gamma, beta, W2, b2, graph, bn, training, eps, mask, act, group):
+    def forward(ctx, x, W1, b1, gamma, beta, W2, b2, graph, bn, training, eps, mask, act, group,
+                sync_count):
         _lib.require_gpu(x, W1, W2)
         x, W1, b1, W2, b2 = (_f32c(t) for t in (x, W1, b1, W2, b2))
         csr = graph.csr("gin")
@@ -401,7 +448,7 @@ class _GINConv(torch.autograd.Function):
         sums = None
         if training:
             sums = bn_stats(Z1)
-            count = _global_count(M, group, x.device)
+            count = _global_count(M, group, x.device, sync_count)
             if count <= 1:
                 raise ValueError("Expected more than 1 value per channel when training")
             if group is not None:
@@ -443,17 +490,18 @@ class _GINConv(torch.autograd.Function):
         dx = None
         if want_dx:
             dx = spmm_raw(csr.tptr, csr.tidx, csr.tw, ctx.self_scale, dxpre)
-        return (dx, dW1, db1, dg, dbt, dW2, db2, None, None, None, None, None, None, None)
+        return (dx, dW1, db1, dg, dbt, dW2, db2, None, None, None, None, None, None, None,
+                None)
 
 
 def gin_conv(x, W1, b1, bn, W2, b2, graph: Graph, eps: float = 0.0, mask=None,
-             act: int = _lib.LGNN_ACT_ELU, group=None):
+             act: int = _lib.LGNN_ACT_ELU, group=None, sync_count=None):
     """bn: the torch.nn.BatchNorm1d holding gamma/beta and the running statistics."""
     training = bn.training or not bn.track_running_stats
     gamma = bn.weight if bn.affine else None
     beta = bn.bias if bn.affine else None
     return _GINConv.apply(x, W1, b1, gamma, beta, W2, b2, graph, bn, training, eps, mask, act,
-                          group)
+                          group, sync_count)
 
 
 # ----------------------------------------------------------------------------------------------

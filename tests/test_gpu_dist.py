@@ -32,7 +32,7 @@ def build(kind):
     torch.manual_seed(5)
     if kind == "gcn":
         return GCN(32, [64, 64, 64], 5, 0.0)
-    return GIN(32, [64, 64, 64], 5, 0.0, pool="add")
+    return GIN(32, [64, 64, 64], 5, 0.0, pool="add")  # gin, gin_fixed
 
 
 def shard(b, g0, g1):
@@ -52,6 +52,8 @@ def worker(rank, world, port, kind, q):
     m = build(kind).to(dev).train()
     if kind == "gin":
         m.set_sync_bn(dist.group.WORLD)
+    elif kind == "gin_fixed":  # known global node count: no per-step count all-reduce
+        m.set_sync_bn(dist.group.WORLD, global_count=B * N)
     g0, g1 = rank * B // world, (rank + 1) * B // world
     x, ei, bt, y = (t.to(dev) for t in shard(b, g0, g1))
     logits = m(x, ei, bt, g1 - g0)
@@ -61,7 +63,7 @@ def worker(rank, world, port, kind, q):
     # by this process, which may have exited before the parent reads the queue)
     out = {"logits": logits.detach().cpu().numpy(),
            "grads": {k: p.grad.detach().cpu().numpy() for k, p in m.named_parameters()}}
-    if kind == "gin":
+    if kind != "gcn":
         out["state"] = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()
                         if "running" in k}
     q.put((rank, out))
@@ -69,7 +71,7 @@ def worker(rank, world, port, kind, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind", ["gcn", "gin"])
+@pytest.mark.parametrize("kind", ["gcn", "gin", "gin_fixed"])
 def test_two_ranks_match_full_batch(cuda, kind):
     from lesion_gnn_amd import synth
 
@@ -96,7 +98,7 @@ def test_two_ranks_match_full_batch(cuda, kind):
             torch.testing.assert_close(torch.from_numpy(res[r]["grads"][k]), want, rtol=0,
                                        atol=max(1e-4 * want.abs().max().item(), 5e-6),
                                        msg=lambda s: f"rank {r} {k}: {s}")
-    if kind == "gin":
+    if kind != "gcn":
         for k, v in m.state_dict().items():
             if "running" in k:
                 torch.testing.assert_close(torch.from_numpy(res[0]["state"][k]), v.cpu(),
