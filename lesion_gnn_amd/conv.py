@@ -70,6 +70,7 @@ class GINConv(nn.Module):
     def __init__(self, mlp: MLP, eps: float = 0.0):
         super().__init__()
         self.nn = mlp
+        self.initial_eps = float(eps)  # train_eps=False: eps stays at its initial value
         self.register_buffer("eps", torch.full((1,), float(eps)))
         self.sync_group = None  # torch.distributed group for SyncBN (None: per-replica stats)
         self.sync_count = None  # fixed global node count under SyncBN (None: all-reduced)
@@ -84,7 +85,7 @@ class GINConv(nn.Module):
             mask = (torch.rand(x.size(0), mlp.channel_list[1], device=x.device) >= p).float()
             mask.mul_(1.0 / (1.0 - p))
         return ops.gin_conv(x, mlp.lins[0].weight, mlp.lins[0].bias, bn, mlp.lins[1].weight,
-                            mlp.lins[1].bias, g, float(self.eps), mask, act, self.sync_group,
+                            mlp.lins[1].bias, g, self.initial_eps, mask, act, self.sync_group,
                             self.sync_count)
 
 

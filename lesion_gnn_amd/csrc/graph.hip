@@ -4,17 +4,16 @@
 // Replaces (reference call sites): gcn_norm inside GCNConv, GATConv's
 // remove_self_loops/add_self_loops (gat.py:31), ToSparseTensor (datasets/datamodule.py:44-45).
 //
-// Pipeline (one memset + 4 kernels + 2 scans, no host sync):
+// Pipeline (one memset + 5 kernels, no host sync):
 //   k_count   per-edge in/out degree; runs of equal targets inside a wave (k-NN input is grouped by
 //             target) are folded into one atomic
-//   scan      rowptr / tptr = exclusive scan of (degree + appended loop)
+//   k_scan_*  rowptr / tptr = exclusive scans of (degree + appended loop), both arrays per
+//             launch; dis = deg^-1/2 for the GCN weights
 //   k_fill    claim slots (same run folding), write (source, edge id)
 //   k_finish  per 256-row block: stage the rows in LDS, append the self loop, sort each row by
 //             edge id (restores edge_index order: the order PyG's scatter_add_ visits a target's
 //             messages in), compute GCN weights, write back coalesced. Run for both CSRs.
 // The result is identical run to run.
-#include <hipcub/hipcub.hpp>
-
 #include "common.h"
 
 namespace {
@@ -24,18 +23,8 @@ constexpr int kFinishCap = 6144;  // staged CSR entries per 256-row block
 
 inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
-struct AddLoop {
-  int add;
-  __host__ __device__ int operator()(int v) const { return v + add; }
-};
-
-using CntIter = hipcub::TransformInputIterator<int, AddLoop, const int32_t*>;
-
-size_t scan_temp_bytes(int64_t n) {
-  size_t bytes = 0;
-  CntIter it(nullptr, AddLoop{0});
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, it, (int32_t*)nullptr, (int)n);
-  return bytes;
+inline size_t scan_bsum_bytes(int64_t N) {
+  return (size_t)2 * 4 * ((N + 1 + 1023) / 1024);  // 2 arrays x blocks of 1024 elements
 }
 
 struct GraphWs {
@@ -47,8 +36,7 @@ struct GraphWs {
   int32_t* teid;   // [E+N]
   int32_t* inv;    // [E+N] edge id -> target-CSR position (for tmap)
   float* dis;      // [N] deg^-1/2 (GCN normalisation), inf -> 0
-  void* scan_tmp;
-  size_t scan_bytes;
+  int32_t* bsum;   // [2 * scan blocks] per-block degree sums
   size_t zero_bytes;
 };
 
@@ -69,14 +57,13 @@ GraphWs carve(void* base, int64_t N, int64_t E) {
   ws.teid = (int32_t*)take((E + N) * 4);
   ws.inv = (int32_t*)take((E + N) * 4);
   ws.dis = (float*)take(N * 4);
-  ws.scan_bytes = scan_temp_bytes(N + 1);
-  ws.scan_tmp = take(ws.scan_bytes);
+  ws.bsum = (int32_t*)take(scan_bsum_bytes(N));
   return ws;
 }
 
 size_t ws_total(int64_t N, int64_t E) {
   return 2 * align_up((N + 1) * 4) + 3 * align_up(N * 4) + 3 * align_up((E + N) * 4) +
-         align_up(scan_temp_bytes(N + 1)) + 256;
+         align_up(scan_bsum_bytes(N)) + 256;
 }
 
 // Wave-level run detection over consecutive edges: lanes whose target equals the previous
@@ -163,70 +150,86 @@ __global__ __launch_bounds__(kThreads) void k_fill(const int64_t* __restrict__ e
   }
 }
 
-// Both degree scans in one launch (block 0: rowptr from cnt, block 1: tptr from tcnt), for
-// N + 1 <= kScanSmall: thread t scans a contiguous chunk, chunk totals are scanned across the
-// block. Block 0 also writes dis[i] = deg_i^-1/2 (GCN normalisation; deg 0 -> 0).
-constexpr int kScanThreads = 1024;
-constexpr int64_t kScanSmall = 1 << 18;
+// Both degree scans (blockIdx.y = 0: rowptr from cnt, 1: tptr from tcnt) in two launches:
+//   k_scan_sums:  per 1024-element block, the sum of (count + add)
+//   k_scan_apply: each block adds up the sums of the blocks before it (in block order), scans its
+//                 own elements (4 per thread, coalesced) and writes the exclusive prefix; the
+//                 rowptr blocks also write dis[i] = deg_i^-1/2 (GCN normalisation; deg 0 -> 0).
+constexpr int kScanT = 256;
+constexpr int kScanPer = 4;
+constexpr int kScanBlk = kScanT * kScanPer;
 
-__global__ __launch_bounds__(kScanThreads) void k_scan2(const int32_t* __restrict__ cnt,
-                                                        const int32_t* __restrict__ tcnt,
-                                                        int64_t N, int add,
-                                                        int32_t* __restrict__ rowptr,
-                                                        int32_t* __restrict__ tptr,
-                                                        float* __restrict__ dis) {
-  __shared__ int wsum[kScanThreads / 64];
-  const bool tr = blockIdx.x == 1;
+__device__ __forceinline__ int scan_val(const int32_t* __restrict__ c, int64_t i, int64_t N,
+                                        int add) {
+  return i < N ? c[i] + add : 0;
+}
+
+__global__ __launch_bounds__(kScanT) void k_scan_sums(const int32_t* __restrict__ cnt,
+                                                      const int32_t* __restrict__ tcnt, int64_t N,
+                                                      int add, int32_t* __restrict__ bsum) {
+  __shared__ int red[kScanT / 64];
+  const int32_t* __restrict__ c = blockIdx.y ? tcnt : cnt;
+  const int64_t base = (int64_t)blockIdx.x * kScanBlk;
+  int s = 0;
+#pragma unroll
+  for (int j = 0; j < kScanPer; ++j) s += scan_val(c, base + j * kScanT + threadIdx.x, N, add);
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int w = 0; w < kScanT / 64; ++w) t += red[w];
+    bsum[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(kScanT) void k_scan_apply(const int32_t* __restrict__ cnt,
+                                                       const int32_t* __restrict__ tcnt,
+                                                       int64_t N, int add,
+                                                       const int32_t* __restrict__ bsum,
+                                                       int32_t* __restrict__ rowptr,
+                                                       int32_t* __restrict__ tptr,
+                                                       float* __restrict__ dis) {
+  __shared__ int red[kScanT / 64];
+  __shared__ int wsc[kScanT / 64];
+  const bool tr = blockIdx.y == 1;
   const int32_t* __restrict__ c = tr ? tcnt : cnt;
   int32_t* __restrict__ out = tr ? tptr : rowptr;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t n = N + 1;
-  const int64_t chunk = (n + kScanThreads - 1) / kScanThreads;
-  const int64_t b0 = tid * chunk, b1 = b0 + chunk < n ? b0 + chunk : n;
-  int sum = 0;
-  for (int64_t i = b0; i < b1; ++i) sum += i < N ? c[i] + add : 0;
-  // inclusive scan of the chunk sums: wave, then across waves
-  int x = sum;
+  // prefix of the preceding blocks
+  int pre = 0;
+  for (int b = tid; b < (int)blockIdx.x; b += kScanT) pre += bsum[(int64_t)blockIdx.y * gridDim.x + b];
+  for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
+  if (lane == 0) red[wave] = pre;
+  // this thread's 4 consecutive elements
+  const int64_t i0 = (int64_t)blockIdx.x * kScanBlk + (int64_t)tid * kScanPer;
+  int v[kScanPer];
+  int s = 0;
+#pragma unroll
+  for (int j = 0; j < kScanPer; ++j) {
+    v[j] = scan_val(c, i0 + j, N, add);
+    s += v[j];
+  }
+  int x = s;  // inclusive scan of the thread sums
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const int y = __shfl_up(x, o, 64);
     if (lane >= o) x += y;
   }
-  if (lane == 63) wsum[wave] = x;
+  if (lane == 63) wsc[wave] = x;
   __syncthreads();
-  if (wave == 0) {
-    int v = lane < kScanThreads / 64 ? wsum[lane] : 0;
+  int run = red[0] + red[1] + red[2] + red[3] + x - s;
+  for (int w = 0; w < wave; ++w) run += wsc[w];
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      const int y = __shfl_up(v, o, 64);
-      if (lane >= o) v += y;
+  for (int j = 0; j < kScanPer; ++j) {
+    const int64_t i = i0 + j;
+    if (i <= N) out[i] = run;
+    if (!tr && dis && i < N) {
+      const int deg = v[j];
+      dis[i] = deg > 0 ? 1.0f / sqrtf((float)deg) : 0.0f;
     }
-    if (lane < kScanThreads / 64) wsum[lane] = v;
+    run += v[j];
   }
-  __syncthreads();
-  int run = x - sum + (wave > 0 ? wsum[wave - 1] : 0);  // exclusive prefix of this chunk
-  for (int64_t i = b0; i < b1; ++i) {
-    out[i] = run;
-    if (i < N) {
-      const int deg = c[i] + add;
-      if (!tr && dis) dis[i] = deg > 0 ? 1.0f / sqrtf((float)deg) : 0.0f;
-      run += deg;
-    }
-  }
-}
-
-__global__ __launch_bounds__(kThreads) void k_dis(const int32_t* __restrict__ rowptr, int64_t N,
-                                                  float* __restrict__ dis) {
-  for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < N;
-       i += (int64_t)gridDim.x * kThreads) {
-    const int deg = rowptr[i + 1] - rowptr[i];
-    dis[i] = deg > 0 ? 1.0f / sqrtf((float)deg) : 0.0f;
-  }
-}
-
-__device__ __forceinline__ float gcn_dis(const int32_t* __restrict__ rowptr, int64_t j) {
-  const int deg = rowptr[j + 1] - rowptr[j];
-  return deg > 0 ? 1.0f / sqrtf((float)deg) : 0.0f;
 }
 
 // insertion sort of n (key, val) pairs by key (keys distinct)
@@ -389,22 +392,15 @@ extern "C" int lgnn_graph_build(const int64_t* edge_index, int64_t E, int64_t N,
                        loops, ws.cnt, tptr ? ws.tcnt : nullptr, err_count);
     LGNN_LAUNCH_CHECK();
   }
-  if (N + 1 <= kScanSmall) {
-    hipLaunchKernelGGL(k_scan2, dim3(tptr ? 2 : 1), dim3(kScanThreads), 0, s, ws.cnt, ws.tcnt, N,
-                       add_loop, rowptr, tptr, ws.dis);
+  {
+    const int64_t nblk = (N + 1 + kScanBlk - 1) / kScanBlk;
+    if (nblk > INT32_MAX / 2) return LGNN_EINVAL;
+    dim3 sg((unsigned)nblk, tptr ? 2u : 1u);
+    hipLaunchKernelGGL(k_scan_sums, sg, dim3(kScanT), 0, s, ws.cnt, ws.tcnt, N, add_loop,
+                       ws.bsum);
     LGNN_LAUNCH_CHECK();
-  } else {
-    size_t tb = ws.scan_bytes;
-    if (hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, tb, CntIter(ws.cnt, AddLoop{add_loop}),
-                                         rowptr, (int)(N + 1), s) != hipSuccess)
-      return (int)hipGetLastError();
-    if (tptr) {
-      tb = ws.scan_bytes;
-      if (hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, tb, CntIter(ws.tcnt, AddLoop{add_loop}),
-                                           tptr, (int)(N + 1), s) != hipSuccess)
-        return (int)hipGetLastError();
-    }
-    hipLaunchKernelGGL(k_dis, dim3(grid_for(N)), dim3(kThreads), 0, s, rowptr, N, ws.dis);
+    hipLaunchKernelGGL(k_scan_apply, sg, dim3(kScanT), 0, s, ws.cnt, ws.tcnt, N, add_loop,
+                       ws.bsum, rowptr, tptr, ws.dis);
     LGNN_LAUNCH_CHECK();
   }
   if (E > 0) {
