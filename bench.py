@@ -123,9 +123,13 @@ def build_model(wl, oracle=False):
     return mods[wl["model"]](wl["d_in"], wl["hidden"], out, 0.0, pool=wl["pool"])
 
 
-def loss_fn(wl, logits, y):
+def loss_fn(wl, logits, y, oracle=False):
     if wl["loss"] == "CE":
-        return torch.nn.functional.cross_entropy(logits, y)
+        if oracle:
+            return torch.nn.functional.cross_entropy(logits, y)
+        from lesion_gnn_amd import ops  # HIP criterion (reference nn.CrossEntropyLoss)
+
+        return ops.cross_entropy(logits, y)
     # reference regression head: clamp(logits.squeeze(1), 0, C-1) then MSE (gat.py:94-95)
     return torch.nn.functional.mse_loss(logits.squeeze(1).clamp(0, wl["classes"] - 1), y.float())
 
@@ -202,7 +206,7 @@ def cpu_baseline(wl, B, seconds):
 
     def step():
         opt.zero_grad(set_to_none=True)
-        loss_fn(wl, m(b.x, b.edge_index, b.batch, B), b.y).backward()
+        loss_fn(wl, m(b.x, b.edge_index, b.batch, B), b.y, oracle=True).backward()
         opt.step()
 
     step()

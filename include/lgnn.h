@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 3
+#define LGNN_ABI_VERSION 4
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -66,13 +66,15 @@ const char* lgnn_status_string(int status);
  * PyG appends loops after the edge list). Invalid indices (<0 or >= N) are dropped and counted in
  * *err_count (device int, may be NULL). tmap (nullable, needs the transpose) [cap]: for each
  * transpose entry, the position of the same edge in the target CSR (GAT backward reads per-edge
- * attention saved in target order). Workspace size: lgnn_graph_workspace_bytes.
+ * attention saved in target order). tile_open (nullable) [ceil(N/64)]: as lgnn_tile_open, in
+ * the same launches. *err_count is written (not accumulated). Workspace size:
+ * lgnn_graph_workspace_bytes.
  * ------------------------------------------------------------------------------------------- */
 size_t lgnn_graph_workspace_bytes(int64_t num_nodes, int64_t num_edges);
 int lgnn_graph_build(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes, int loops,
                      int norm, int32_t* rowptr, int32_t* col, float* w, int32_t* tptr,
-                     int32_t* tidx, float* tw, int32_t* tmap, int32_t* err_count,
-                     void* workspace, size_t workspace_bytes, void* stream);
+                     int32_t* tidx, float* tw, int32_t* tmap, int32_t* tile_open,
+                     int32_t* err_count, void* workspace, size_t workspace_bytes, void* stream);
 
 /* Graph offsets from a sorted PyG `batch` vector (Batch.ptr): ptr[g] = first node of graph g,
  * ptr[B] = M. Replaces the count/offset half of PyG scatter(reduce='mean') over `batch`. */
@@ -130,6 +132,9 @@ int lgnn_node_linear_bwd(int grad_mode, const float* dY, const int64_t* batch, c
 /* out[i] = sum_{p < P} partial[p*len + i], fixed order (bitwise reproducible). */
 int lgnn_reduce_partials(const float* partial, int num_partials, int64_t len, float* out,
                          void* stream);
+/* The same for n <= 16 independent slabs in one launch (host arrays of n entries). */
+int lgnn_reduce_partials_multi(int n, const float* const* partials, const int* num_partials,
+                               const int64_t* len, float* const* out, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Sparse aggregation alone (no linear): Y_i = self_scale*X_i + sum_{e in row i} w_e X[col_e].
@@ -247,6 +252,20 @@ int lgnn_gcn_stack_fwd(const float* X, int64_t M, int d_in, int has_in_proj,
 int lgnn_tile_count(int64_t num_nodes);
 int lgnn_tile_open(const int32_t* rowptr, const int32_t* col, int64_t num_nodes, int32_t* open,
                    void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Criterion. Replaces: nn.CrossEntropyLoss(weight=class_weights) of BaseLightningModule
+ * (reference models/base.py:93-94, training_step :196-201), mean reduction.
+ *   fwd: lse[B] = logsumexp(logits_i); loss[0] = sum w[y] (lse - z[y]) / sum w[y]; wsum[0] =
+ *        sum w[y] (weight NULL = 1); *bad = 1 if a target is outside [0, C) (such rows skipped).
+ *   bwd: dlogits = grad_loss[0] * w[y_i] / wsum * (softmax(z_i) - onehot(y_i)).
+ * Deterministic (one workgroup, fixed reduction order). All pointers device pointers.
+ * ------------------------------------------------------------------------------------------- */
+int lgnn_ce_fwd(const float* logits, const int64_t* target, const float* weight, int64_t B, int C,
+                float* lse, float* loss, float* wsum, int* bad, void* stream);
+int lgnn_ce_bwd(const float* logits, const int64_t* target, const float* weight, int64_t B, int C,
+                const float* lse, const float* wsum, const float* grad_loss, float* dlogits,
+                void* stream);
 
 #ifdef __cplusplus
 }

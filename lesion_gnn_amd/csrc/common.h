@@ -6,6 +6,7 @@
 #include "../../include/lgnn.h"
 
 #define LGNN_MAX_STACK 8  // layers of one fused stack launch (in_proj + 7 convs)
+#define LGNN_MAX_REDUCE 16  // slabs of one lgnn_reduce_partials_multi launch
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));

@@ -28,6 +28,7 @@ inline size_t scan_bsum_bytes(int64_t N) {
 }
 
 struct GraphWs {
+  int32_t* err;    // [1] dropped edges (zeroed with the counters, copied to err_count)
   int32_t* cnt;    // [N+1] in-degree without loops
   int32_t* tcnt;   // [N+1]
   int32_t* fill;   // [N]
@@ -48,6 +49,7 @@ GraphWs carve(void* base, int64_t N, int64_t E) {
     p += align_up(bytes);
     return q;
   };
+  ws.err = (int32_t*)take(4);
   ws.cnt = (int32_t*)take((N + 1) * 4);
   ws.tcnt = (int32_t*)take((N + 1) * 4);
   ws.fill = (int32_t*)take(N * 4);
@@ -62,7 +64,7 @@ GraphWs carve(void* base, int64_t N, int64_t E) {
 }
 
 size_t ws_total(int64_t N, int64_t E) {
-  return 2 * align_up((N + 1) * 4) + 3 * align_up(N * 4) + 3 * align_up((E + N) * 4) +
+  return align_up(4) + 2 * align_up((N + 1) * 4) + 3 * align_up(N * 4) + 3 * align_up((E + N) * 4) +
          align_up(scan_bsum_bytes(N)) + 256;
 }
 
@@ -96,8 +98,14 @@ __device__ __forceinline__ bool edge_ok(int64_t s, int64_t d, int64_t N) {
 // grid-stride over wave-aligned chunks so every wave sees 64 consecutive edges
 __global__ __launch_bounds__(kThreads) void k_count(const int64_t* __restrict__ ei, int64_t E,
                                                     int64_t N, int loops, int32_t* cnt,
-                                                    int32_t* tcnt, int32_t* err) {
+                                                    int32_t* tcnt, int32_t* err,
+                                                    int32_t* tile_open, int64_t ntiles) {
   const int lane = threadIdx.x & 63;
+  if (tile_open) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < ntiles;
+         t += (int64_t)gridDim.x * blockDim.x)
+      tile_open[t] = 0;
+  }
   const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t base = wave0 * 64; base < E; base += nwaves * 64) {
@@ -255,8 +263,11 @@ __global__ __launch_bounds__(kThreads) void k_finish(int64_t N, int64_t E, int a
                                                      int32_t* col, int32_t* eid, float* w,
                                                      const int32_t* __restrict__ tptr,
                                                      int32_t* tidx, int32_t* teid, float* tw,
-                                                     const float* __restrict__ dis) {
+                                                     const float* __restrict__ dis,
+                                                     const int32_t* __restrict__ ws_err,
+                                                     int32_t* err_out, int32_t* tile_open) {
   __shared__ int32_t s_key[kFinishCap];
+  if (err_out && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *err_out = *ws_err;
   __shared__ int32_t s_val[kFinishCap];
   const bool tr = blockIdx.y == 1;
   const int32_t* __restrict__ ptr = tr ? tptr : rowptr;
@@ -306,6 +317,18 @@ __global__ __launch_bounds__(kThreads) void k_finish(int64_t N, int64_t E, int a
       for (int j = r0; j < r1; ++j) {
         const int nb = staged ? s_val[j - eb] : idx[j];
         wt[j] = norm == LGNN_NORM_GCN ? (dis[nb] * 1.0f) * di : 1.0f;
+      }
+    }
+  }
+  // 64-node tiles an edge leaves (target CSR pass): the fused layer stack skips them
+  if (tile_open && !tr && i < N) {
+    const int r0 = ptr[i], r1 = ptr[i + 1];
+    const int64_t ti = i >> 6;
+    for (int j = r0; j < r1; ++j) {
+      const int nb = staged ? s_val[j - eb] : idx[j];
+      if ((nb >> 6) != ti) {
+        tile_open[ti] = 1;  // benign race: every writer stores 1
+        tile_open[nb >> 6] = 1;
       }
     }
   }
@@ -369,8 +392,8 @@ extern "C" size_t lgnn_graph_workspace_bytes(int64_t num_nodes, int64_t num_edge
 
 extern "C" int lgnn_graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loops,
                                 int norm, int32_t* rowptr, int32_t* col, float* w, int32_t* tptr,
-                                int32_t* tidx, float* tw, int32_t* tmap, int32_t* err_count,
-                                void* workspace,
+                                int32_t* tidx, float* tw, int32_t* tmap, int32_t* tile_open,
+                                int32_t* err_count, void* workspace,
                                 size_t workspace_bytes, void* stream) {
   if (N < 0 || E < 0 || loops < 0 || loops > 2 || norm < 0 || norm > 1) return LGNN_EINVAL;
   if (!rowptr || !col || (E > 0 && !edge_index)) return LGNN_EINVAL;
@@ -381,15 +404,19 @@ extern "C" int lgnn_graph_build(const int64_t* edge_index, int64_t E, int64_t N,
   hipStream_t s = as_stream(stream);
   const int add_loop = loops == LGNN_LOOPS_KEEP ? 0 : 1;
   GraphWs ws = carve(workspace, N, E);
-  if (hipMemsetAsync(ws.cnt, 0, ws.zero_bytes, s) != hipSuccess) return (int)hipGetLastError();
+  if (hipMemsetAsync(ws.err, 0, ws.zero_bytes, s) != hipSuccess) return (int)hipGetLastError();
   if (N == 0) {
     if (hipMemsetAsync(rowptr, 0, 4, s) != hipSuccess) return (int)hipGetLastError();
     if (tptr && hipMemsetAsync(tptr, 0, 4, s) != hipSuccess) return (int)hipGetLastError();
+    if (err_count && hipMemsetAsync(err_count, 0, 4, s) != hipSuccess)
+      return (int)hipGetLastError();
     return LGNN_OK;
   }
-  if (E > 0) {
-    hipLaunchKernelGGL(k_count, dim3(grid_for(E, 2048)), dim3(kThreads), 0, s, edge_index, E, N,
-                       loops, ws.cnt, tptr ? ws.tcnt : nullptr, err_count);
+  if (E > 0 || tile_open) {
+    hipLaunchKernelGGL(k_count, dim3(grid_for(E > N ? E : N, 2048)), dim3(kThreads), 0, s,
+                       edge_index, E, N,
+                       loops, ws.cnt, tptr ? ws.tcnt : nullptr, ws.err, tile_open,
+                       (N + 63) / 64);
     LGNN_LAUNCH_CHECK();
   }
   {
@@ -410,7 +437,7 @@ extern "C" int lgnn_graph_build(const int64_t* edge_index, int64_t E, int64_t N,
   }
   dim3 fg((unsigned)((N + kThreads - 1) / kThreads), tptr ? 2u : 1u);
   hipLaunchKernelGGL(k_finish, fg, dim3(kThreads), 0, s, N, E, add_loop, norm, rowptr, col,
-                     ws.eid, w, tptr, tidx, ws.teid, tw, ws.dis);
+                     ws.eid, w, tptr, tidx, ws.teid, tw, ws.dis, ws.err, err_count, tile_open);
   LGNN_LAUNCH_CHECK();
   if (tmap) {
     const int g = grid_for(E + N, 2048);

@@ -1,0 +1,167 @@
+// Cross-entropy criterion (reference models/base.py:93-94: nn.CrossEntropyLoss(weight=class
+// weights), mean reduction) and the batched deterministic reduction of per-workgroup partial
+// slabs, each in one launch.
+//
+//   loss = sum_i w[y_i] * (lse_i - z_i[y_i]) / sum_i w[y_i]       (w = 1 when weight == NULL)
+//   dz_i = g * w[y_i] / sum_j w[y_j] * (softmax(z_i) - onehot(y_i))
+// One workgroup; rows are summed in fixed order (per-thread strided partials, then a fixed
+// tree), so the loss is bitwise reproducible.
+#include "common.h"
+
+namespace {
+
+constexpr int CT = 1024;
+
+__device__ __forceinline__ float block_sum_fixed(float v, float* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  float t = 0.f;
+  if (threadIdx.x == 0) {
+    for (int w = 0; w < CT / 64; ++w) t += red[w];
+    red[CT / 64] = t;
+  }
+  __syncthreads();
+  return red[CT / 64];
+}
+
+// lse[i] = logsumexp(z_i) (saved for the backward); loss[0] = weighted mean NLL; wsum[0]
+__global__ __launch_bounds__(CT) void k_ce_fwd(const float* __restrict__ z,
+                                               const int64_t* __restrict__ y,
+                                               const float* __restrict__ weight, int64_t B, int C,
+                                               float* __restrict__ lse, float* __restrict__ loss,
+                                               float* __restrict__ wsum, int* __restrict__ bad) {
+  __shared__ float red[CT / 64 + 1];
+  if (threadIdx.x == 0) *bad = 0;
+  __syncthreads();
+  float num = 0.f, den = 0.f;
+  for (int64_t i = threadIdx.x; i < B; i += CT) {
+    const float* zi = z + i * C;
+    float m = -INFINITY;
+    for (int c = 0; c < C; ++c) m = fmaxf(m, zi[c]);
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s += expf(zi[c] - m);
+    const float l = m + logf(s);
+    lse[i] = l;
+    const int64_t t = y[i];
+    if (t < 0 || t >= C) {
+      atomicOr(bad, 1);
+      continue;
+    }
+    const float wt = weight ? weight[t] : 1.f;
+    num += wt * (l - zi[t]);
+    den += wt;
+  }
+  const float n = block_sum_fixed(num, red);
+  __syncthreads();
+  const float d = block_sum_fixed(den, red);
+  if (threadIdx.x == 0) {
+    loss[0] = n / d;
+    wsum[0] = d;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_ce_bwd(const float* __restrict__ z,
+                                                const int64_t* __restrict__ y,
+                                                const float* __restrict__ weight, int64_t B,
+                                                int C, const float* __restrict__ lse,
+                                                const float* __restrict__ wsum,
+                                                const float* __restrict__ gloss,
+                                                float* __restrict__ dz) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= B * C) return;
+  const int64_t i = idx / C;
+  const int c = (int)(idx % C);
+  const int64_t t = y[i];
+  const float wt = (t >= 0 && t < C) ? (weight ? weight[t] : 1.f) : 0.f;
+  const float p = expf(z[idx] - lse[i]);
+  dz[idx] = gloss[0] * wt / wsum[0] * (p - (c == t ? 1.f : 0.f));
+}
+
+// job j: out_j[i] = sum_{p < P_j} part_j[p * len_j + i] in slot order (as lgnn_reduce_partials)
+struct ReduceJobs {
+  const float* part[LGNN_MAX_REDUCE];
+  float* out[LGNN_MAX_REDUCE];
+  int64_t len[LGNN_MAX_REDUCE];
+  int P[LGNN_MAX_REDUCE];
+};
+
+constexpr int RT = 1024;
+__global__ __launch_bounds__(RT) void k_reduce_multi(ReduceJobs jobs) {
+  __shared__ float red[16][64];
+  const int j = blockIdx.y;
+  const int64_t len = jobs.len[j];
+  if ((int64_t)blockIdx.x * 64 >= len) return;
+  const float* __restrict__ part = jobs.part[j];
+  const int P = jobs.P[j];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t ic = i < len ? i : len - 1;
+  float s = 0.f;
+  int p = wave;
+  for (; p + 48 < P; p += 64) {
+    const float v0 = part[(int64_t)p * len + ic], v1 = part[(int64_t)(p + 16) * len + ic];
+    const float v2 = part[(int64_t)(p + 32) * len + ic], v3 = part[(int64_t)(p + 48) * len + ic];
+    s += v0;
+    s += v1;
+    s += v2;
+    s += v3;
+  }
+  for (; p < P; p += 16) s += part[(int64_t)p * len + ic];
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && i < len) {
+    float t = red[0][lane];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) t += red[q][lane];
+    jobs.out[j][i] = t;
+  }
+}
+
+}  // namespace
+
+extern "C" int lgnn_ce_fwd(const float* logits, const int64_t* target, const float* weight,
+                           int64_t B, int C, float* lse, float* loss, float* wsum, int* bad,
+                           void* stream) {
+  if (B <= 0 || C <= 0 || !logits || !target || !lse || !loss || !wsum || !bad)
+    return LGNN_EINVAL;
+  hipLaunchKernelGGL(k_ce_fwd, dim3(1), dim3(CT), 0, as_stream(stream), logits, target, weight, B,
+                     C, lse, loss, wsum, bad);
+  LGNN_LAUNCH_CHECK();
+  return LGNN_OK;
+}
+
+extern "C" int lgnn_ce_bwd(const float* logits, const int64_t* target, const float* weight,
+                           int64_t B, int C, const float* lse, const float* wsum,
+                           const float* grad_loss, float* dlogits, void* stream) {
+  if (B <= 0 || C <= 0 || !logits || !target || !lse || !wsum || !grad_loss || !dlogits)
+    return LGNN_EINVAL;
+  hipLaunchKernelGGL(k_ce_bwd, dim3((unsigned)((B * C + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), logits, target, weight, B, C, lse, wsum, grad_loss,
+                     dlogits);
+  LGNN_LAUNCH_CHECK();
+  return LGNN_OK;
+}
+
+extern "C" int lgnn_reduce_partials_multi(int n, const float* const* partials,
+                                          const int* num_partials, const int64_t* len,
+                                          float* const* out, void* stream) {
+  if (n <= 0 || n > LGNN_MAX_REDUCE || !partials || !num_partials || !len || !out)
+    return LGNN_EINVAL;
+  ReduceJobs jobs = {};
+  int64_t maxlen = 0;
+  for (int j = 0; j < n; ++j) {
+    if (!partials[j] || !out[j] || num_partials[j] <= 0 || len[j] < 0) return LGNN_EINVAL;
+    jobs.part[j] = partials[j];
+    jobs.out[j] = out[j];
+    jobs.len[j] = len[j];
+    jobs.P[j] = num_partials[j];
+    if (len[j] > maxlen) maxlen = len[j];
+  }
+  if (maxlen == 0) return LGNN_OK;
+  hipLaunchKernelGGL(k_reduce_multi, dim3((unsigned)((maxlen + 63) / 64), (unsigned)n), dim3(RT),
+                     0, as_stream(stream), jobs);
+  LGNN_LAUNCH_CHECK();
+  return LGNN_OK;
+}

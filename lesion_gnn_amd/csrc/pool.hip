@@ -113,31 +113,33 @@ __global__ __launch_bounds__(NT) void k_pool_head_fwd4(const float* __restrict__
   }
 }
 
-// dpooled[g][d] = sum_c dlogits[g][c] Wout[c][d]
-__global__ __launch_bounds__(NT) void k_head_bwd_dp(const float* __restrict__ dlogits, int64_t B,
-                                                    int D, const float* __restrict__ Wout, int C,
-                                                    float* __restrict__ dpooled) {
-  const int64_t idx = (int64_t)blockIdx.x * NT + threadIdx.x;
-  if (idx >= B * D) return;
-  const int64_t g = idx / D;
-  const int d = (int)(idx % D);
-  float acc = 0.f;
-  for (int c = 0; c < C; ++c) acc = fmaf(dlogits[g * C + c], Wout[(int64_t)c * D + d], acc);
-  dpooled[idx] = acc;
-}
-
-// dWout[c][d] = sum_g dlogits[g][c] pooled[g][d]; dbout[c] = sum_g dlogits[g][c].
-// block = (class c, 64-wide feature strip), 16 waves split g (w, w+16, ...), unconditional
-// (clamped) loads so every iteration's loads are in flight; fixed-order combine.
+// One launch for the out_proj backward: blocks [0, nb_dp) compute dpooled[g][d] = sum_c
+// dlogits[g][c] Wout[c][d] (one element per thread); the rest compute dWout[c][d] = sum_g
+// dlogits[g][c] pooled[g][d] and dbout[c] (block = (class c, 64-wide feature strip), 16 waves
+// split g, fixed-order combine).
 constexpr int HT = 1024;
-__global__ __launch_bounds__(HT) void k_head_bwd_dw(const float* __restrict__ dlogits,
-                                                    const float* __restrict__ pooled, int64_t B,
-                                                    int D, int C, float* __restrict__ dWout,
-                                                    float* __restrict__ dbout) {
+__global__ __launch_bounds__(HT) void k_head_bwd(const float* __restrict__ dlogits,
+                                                 const float* __restrict__ pooled, int64_t B,
+                                                 int D, const float* __restrict__ Wout, int C,
+                                                 float* __restrict__ dpooled,
+                                                 float* __restrict__ dWout,
+                                                 float* __restrict__ dbout, int nb_dp) {
   __shared__ float red[16][65];
+  if ((int)blockIdx.x < nb_dp) {
+    const int64_t idx = (int64_t)blockIdx.x * HT + threadIdx.x;
+    if (idx >= B * D) return;
+    const int64_t g = idx / D;
+    const int d = (int)(idx % D);
+    float acc = 0.f;
+    for (int c = 0; c < C; ++c) acc = fmaf(dlogits[g * C + c], Wout[(int64_t)c * D + d], acc);
+    dpooled[idx] = acc;
+    return;
+  }
+  const int b = (int)blockIdx.x - nb_dp;
+  const int nstrip = (D + 63) / 64;
+  const int c = b / nstrip, strip = b % nstrip;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = blockIdx.y;
-  const int d = blockIdx.x * 64 + lane;
+  const int d = strip * 64 + lane;
   const int dc = d < D ? d : D - 1;
   float s = 0.f, sb = 0.f;
 #pragma unroll 4
@@ -157,7 +159,7 @@ __global__ __launch_bounds__(HT) void k_head_bwd_dw(const float* __restrict__ dl
       tb += red[q][64];
     }
     if (d < D) dWout[(int64_t)c * D + d] = t;
-    if (lane == 0 && blockIdx.x == 0 && dbout) dbout[c] = tb;
+    if (lane == 0 && strip == 0 && dbout) dbout[c] = tb;
   }
 }
 
@@ -201,17 +203,12 @@ extern "C" int lgnn_pool_head_bwd(const float* dlogits, const float* pooled, int
                                   const float* Wout, int C, float* dpooled, float* dWout,
                                   float* dbout, void* stream) {
   if (B < 0 || D <= 0 || C <= 0 || !dlogits || !pooled || !Wout) return LGNN_EINVAL;
-  hipStream_t s = as_stream(stream);
-  if (dpooled && B > 0) {
-    hipLaunchKernelGGL(k_head_bwd_dp, dim3((unsigned)((B * D + NT - 1) / NT)), dim3(NT), 0, s,
-                       dlogits, B, D, Wout, C, dpooled);
-    LGNN_LAUNCH_CHECK();
-  }
-  if (dWout) {
-    hipLaunchKernelGGL(k_head_bwd_dw, dim3((unsigned)((D + 63) / 64), (unsigned)C), dim3(HT), 0, s,
-                       dlogits, pooled, B, D, C, dWout, dbout);
-    LGNN_LAUNCH_CHECK();
-  }
+  const int nb_dp = (dpooled && B > 0) ? (int)((B * D + HT - 1) / HT) : 0;
+  const int nb_dw = dWout ? C * ((D + 63) / 64) : 0;
+  if (nb_dp + nb_dw == 0) return LGNN_OK;
+  hipLaunchKernelGGL(k_head_bwd, dim3((unsigned)(nb_dp + nb_dw)), dim3(HT), 0, as_stream(stream),
+                     dlogits, pooled, B, D, Wout, C, dpooled, dWout, dbout, nb_dp);
+  LGNN_LAUNCH_CHECK();
   return LGNN_OK;
 }
 

@@ -14,6 +14,7 @@
 #include "common.h"
 #include "tile.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 // Timing-only ablation builds (tools/ablate.py): -DLGNN_ABLATE=<mask> removes phases of the tile
@@ -413,7 +414,7 @@ __global__ __launch_bounds__(NT, 2) void k_bwd(
       if constexpr (ACT == LGNN_ACT_ELU) {
 #pragma unroll
         for (int it = 0; it < 8; ++it) {
-          const int64_t row = r0 + hw + 8 * it, rc = row < M ? row : M - 1;
+          const int64_t row = r0 + hw + 8 * it;
           hv[it] = (ABL & 16) ? zero4() : bld4(bH, (int)(row * N + oc) * 4);
         }
       }
@@ -614,7 +615,7 @@ __global__ __launch_bounds__(NT, 2) void k_stack_fwd(const float* __restrict__ X
   const int l0 = FIRST ? 0 : 1;
   const int K0 = args.width[FIRST ? 0 : 1];
 
-  int stamp = 0;
+  [[maybe_unused]] int stamp = 0;
   STAMP(stamp++);
   int64_t t = seek_tile(blockIdx.x, ntiles, tmask, 0);
   if (t >= ntiles) return;
@@ -740,9 +741,16 @@ bool lgnn_tile_fits(int64_t M, int K, int N) {
          (M + TM) * (int64_t)(K > N ? K : N) * 4 < (int64_t)INT32_MAX;
 }
 
+// Workgroups of the backward kernels = dW partial slots (persistent over the tiles). Tuning knob
+// LGNN_BWD_WGS (read once; default 512 = 2 per CU).
 int lgnn_tile_partials(int64_t M) {
+  static const int64_t cap = [] {
+    const char* e = getenv("LGNN_BWD_WGS");
+    const long v = e ? atol(e) : 0;
+    return (int64_t)(v > 0 ? v : 512);
+  }();
   const int64_t ntiles = (M + TM - 1) / TM;
-  const int64_t p = ntiles < 512 ? ntiles : 512;
+  const int64_t p = ntiles < cap ? ntiles : cap;
   return (int)(p < 1 ? 1 : p);
 }
 

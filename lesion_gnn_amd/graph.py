@@ -31,6 +31,7 @@ class Csr:
     tidx: torch.Tensor    # int32 [cap] target of each entry, grouped by source
     tw: torch.Tensor      # fp32 [cap]
     tmap: torch.Tensor | None  # int32 [cap] target-CSR position of each transpose entry (GAT)
+    tile_open: torch.Tensor | None  # int32 [ceil(N/64)] tiles an edge leaves (GCN fused stack)
     err: torch.Tensor     # int32 [1] count of dropped out-of-range edges
 
 
@@ -84,24 +85,28 @@ class Graph:
             tptr=torch.empty(n + 1, **i32), tidx=torch.empty(cap, **i32),
             tw=torch.empty(cap, dtype=torch.float32, device=dev),
             tmap=torch.empty(cap, **i32) if kind == "gat" else None,
-            err=torch.zeros(1, **i32),
+            tile_open=torch.empty(max((n + 63) // 64, 1), **i32) if kind == "gcn" else None,
+            err=torch.empty(1, **i32),
         )
         lib = _lib.load()
         ws_bytes = lib.lgnn_graph_workspace_bytes(n, e)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         _lib.call("lgnn_graph_build", _lib.ptr(self.edge_index), e, n, loops, norm,
                   _lib.ptr(c.rowptr), _lib.ptr(c.col), _lib.ptr(c.w), _lib.ptr(c.tptr),
-                  _lib.ptr(c.tidx), _lib.ptr(c.tw), _lib.ptr(c.tmap), _lib.ptr(c.err),
-                  _lib.ptr(ws), ws_bytes,
+                  _lib.ptr(c.tidx), _lib.ptr(c.tw), _lib.ptr(c.tmap), _lib.ptr(c.tile_open),
+                  _lib.ptr(c.err), _lib.ptr(ws), ws_bytes,
                   _lib.stream(dev))
         self._csr[kind] = c
         return c
 
     def tile_open(self, kind: str) -> torch.Tensor:
-        """int32 [ceil(N/64)]: 1 for the 64-node tiles an edge leaves (lgnn_tile_open)."""
+        """int32 [ceil(N/64)]: 1 for the 64-node tiles an edge leaves (from the graph build for
+        kind "gcn"; lgnn_tile_open otherwise)."""
+        c = self.csr(kind)
+        if c.tile_open is not None:
+            return c.tile_open
         key = "open:" + kind
         if key not in self._aux:
-            c = self.csr(kind)
             n_t = _lib.load().lgnn_tile_count(self.num_nodes)
             t = torch.empty(max(n_t, 1), dtype=torch.int32, device=self.device)
             _lib.call("lgnn_tile_open", _lib.ptr(c.rowptr), _lib.ptr(c.col), self.num_nodes,

@@ -15,6 +15,7 @@ from typing import Any, Literal
 import torch
 import torch.nn as nn
 
+from .. import ops
 from ..utils import ClassWeights
 from ..utils.placeholder import Placeholder
 
@@ -59,11 +60,23 @@ class BaseModelConfig:
     name: str
 
 
+class CrossEntropyLoss(nn.Module):
+    """nn.CrossEntropyLoss(weight) (mean reduction) on the HIP criterion kernels
+    (ops.cross_entropy); `weight` is kept as a buffer so .to(device) moves it."""
+
+    def __init__(self, weight: torch.Tensor | None = None):
+        super().__init__()
+        self.register_buffer("weight", None if weight is None else weight.float().clone())
+
+    def forward(self, logits: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+        return ops.cross_entropy(logits, target, self.weight)
+
+
 def make_criterion(cfg: OptimizerConfig) -> nn.Module:
     kind = LossType(cfg.loss_type)
     if kind is LossType.CE:
         # reference base.py:93-94 reads the placeholder (unset -> ValueError, as there)
-        return nn.CrossEntropyLoss(weight=cfg.class_weights.value)
+        return CrossEntropyLoss(weight=cfg.class_weights.value)
     if kind is LossType.MSE:
         return nn.MSELoss()
     return nn.SmoothL1Loss()

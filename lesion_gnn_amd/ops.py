@@ -97,8 +97,11 @@ def num_partials(M: int, N: int, K: int, gather: bool = False) -> int:
 def linear_bwd(grad_mode: int, dY: torch.Tensor, *, H: torch.Tensor | None, act: int,
                X: torch.Tensor, W: torch.Tensor, csr: Csr | None = None, self_scale: float = 0.0,
                graph: Graph | None = None, pool_mean: bool = True, tcsr: Csr | None = None,
-               tself: float = 0.0, want_dx: bool = True, want_db: bool = True):
-    """Returns (dXpre or None, dW, db or None). dXpre = dZ W (pre-aggregation input grad)."""
+               tself: float = 0.0, want_dx: bool = True, want_db: bool = True,
+               reducer: list | None = None):
+    """Returns (dXpre or None, dW, db or None). dXpre = dZ W (pre-aggregation input grad).
+    With `reducer` (a list), the dW/db slab reductions are appended to it for one batched
+    launch (reduce_multi) instead of running here."""
     M, K = X.shape
     N = W.size(0)
     dev = X.device
@@ -117,12 +120,25 @@ def linear_bwd(grad_mode: int, dY: torch.Tensor, *, H: torch.Tensor | None, act:
         _lib.ptr(csr.col) if csr else None, _lib.ptr(csr.w) if csr else None, float(self_scale),
         _lib.ptr(W), N, _lib.ptr(dX), _lib.ptr(dWp), _lib.ptr(dbp), P, _s(dev))
     dW = torch.empty(N, K, dtype=torch.float32, device=dev)
-    _lib.call("lgnn_reduce_partials", _lib.ptr(dWp), P, N * K, _lib.ptr(dW), _s(dev))
-    db = None
-    if want_db:
-        db = torch.empty(N, dtype=torch.float32, device=dev)
-        _lib.call("lgnn_reduce_partials", _lib.ptr(dbp), P, N, _lib.ptr(db), _s(dev))
+    db = torch.empty(N, dtype=torch.float32, device=dev) if want_db else None
+    jobs = [(dWp, P, N * K, dW)] + ([(dbp, P, N, db)] if want_db else [])
+    if reducer is not None:  # caller batches the slab reductions of several layers
+        reducer.extend(jobs)
+    else:
+        reduce_multi(jobs, dev)
     return dX, dW, db
+
+
+def reduce_multi(jobs: list, dev) -> None:
+    """Deterministic slab reductions [(partials, P, len, out), ...] in one launch per 16."""
+    for i in range(0, len(jobs), 16):
+        chunk = jobs[i:i + 16]
+        n = len(chunk)
+        parts = (ctypes.c_void_p * n)(*[j[0].data_ptr() for j in chunk])
+        nps = (ctypes.c_int * n)(*[j[1] for j in chunk])
+        lens = (ctypes.c_int64 * n)(*[j[2] for j in chunk])
+        outs = (ctypes.c_void_p * n)(*[j[3].data_ptr() for j in chunk])
+        _lib.call("lgnn_reduce_partials_multi", n, parts, nps, lens, outs, _s(dev))
 
 
 def spmm_raw(rowptr, col, w, self_scale: float, x: torch.Tensor) -> torch.Tensor:
@@ -309,6 +325,7 @@ class _GCNStack(torch.autograd.Function):
         grads = [None] * len(params)
         grads[2 + 2 * L], grads[3 + 2 * L] = dWo, dbo
         dS = None
+        red: list = []
         for l in reversed(range(L)):
             W = params[2 + 2 * l]
             if l == L - 1:
@@ -319,7 +336,7 @@ class _GCNStack(torch.autograd.Function):
             dS, dW, db = linear_bwd(mode, dY, H=hs[l + 1], act=_lib.LGNN_ACT_ELU,
                                     X=ss[l] if saved_s else hs[l], W=W,
                                     csr=None if saved_s else csr, graph=graph,
-                                    pool_mean=ctx.mean, tcsr=tc)
+                                    pool_mean=ctx.mean, tcsr=tc, reducer=red)
             grads[2 + 2 * l], grads[3 + 2 * l] = dW, db
         # in_proj: dH0 = A^T dS_1 (transposed aggregation in the prologue); dx = dH0 W_in
         want_dx = ctx.needs_input_grad[0]
@@ -329,7 +346,8 @@ class _GCNStack(torch.autograd.Function):
             mode, dY, tc = _lib.LGNN_GRAD_POOL, dp, None
         dx, dW, db = linear_bwd(mode, dY, H=None, act=_lib.LGNN_ACT_NONE, X=x, W=params[0],
                                 graph=graph, pool_mean=ctx.mean, tcsr=tc,
-                                want_dx=want_dx)
+                                want_dx=want_dx, reducer=red)
+        reduce_multi(red, x.device)
         grads[0], grads[1] = dW, db
         return (dx, None, None, None, *grads)
 
@@ -580,3 +598,47 @@ class _GATConv(torch.autograd.Function):
 def gat_conv(x, W, att_src, att_dst, bias, graph: Graph, heads: int, slope: float = 0.2,
              mask=None, act: int = _lib.LGNN_ACT_NONE):
     return _GATConv.apply(x, W, att_src, att_dst, bias, graph, heads, slope, mask, act)
+
+
+# ----------------------------------------------------------------------------------------------
+# criterion
+# ----------------------------------------------------------------------------------------------
+
+
+class _CrossEntropy(torch.autograd.Function):
+    """nn.CrossEntropyLoss(weight) with mean reduction (reference models/base.py:93-94) in two
+    HIP kernels (lgnn_ce_fwd / lgnn_ce_bwd) instead of log_softmax + nll_loss + their backward."""
+
+    @staticmethod
+    def forward(ctx, logits, target, weight, validate):
+        _lib.require_gpu(logits, target)
+        z = _f32c(logits)
+        y = target.to(torch.int64).contiguous()
+        B, C = z.shape
+        dev = z.device
+        lse = torch.empty(B, dtype=torch.float32, device=dev)
+        out = torch.empty(2, dtype=torch.float32, device=dev)  # loss, sum of weights
+        bad = torch.empty(1, dtype=torch.int32, device=dev)
+        w = _f32c(weight) if weight is not None else None
+        _lib.call("lgnn_ce_fwd", _lib.ptr(z), _lib.ptr(y), _lib.ptr(w), B, C, _lib.ptr(lse),
+                  _lib.ptr(out), _lib.ptr(out) + 4, _lib.ptr(bad), _s(dev))
+        if validate and int(bad.item()):
+            raise ValueError("cross_entropy: a target is outside [0, num_classes)")
+        ctx.save_for_backward(z, y, w, lse, out)
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        z, y, w, lse, out = ctx.saved_tensors
+        B, C = z.shape
+        dz = torch.empty_like(z)
+        g = _f32c(g.reshape(1))
+        _lib.call("lgnn_ce_bwd", _lib.ptr(z), _lib.ptr(y), _lib.ptr(w), B, C, _lib.ptr(lse),
+                  _lib.ptr(out) + 4, _lib.ptr(g), _lib.ptr(dz), _s(z.device))
+        return dz, None, None, None
+
+
+def cross_entropy(logits, target, weight=None, validate: bool = False):
+    """Weighted-mean cross-entropy of [B, C] logits vs int64 targets. validate=True checks the
+    targets (one host read); otherwise out-of-range targets are skipped silently."""
+    return _CrossEntropy.apply(logits, target, weight, validate)

@@ -264,3 +264,23 @@ def test_adj_t_input_matches_edge_index(cuda, form):
     want = ours(b.x.to(cuda), ei, b.batch.to(cuda))
     got = ours(b.x.to(cuda), adj, b.batch.to(cuda))
     torch.testing.assert_close(got, want, atol=1e-5, rtol=1e-5)
+
+
+def test_tile_open_flags(cuda):
+    """Graph-build tile flags == the standalone lgnn_tile_open, and == a CPU recomputation."""
+    from lesion_gnn_amd import _lib
+    sizes = [64, 64, 30, 34, 64, 100, 28, 64, 1]
+    b = synth.make_batch(len(sizes), k=6, d_in=8, seed=22, sizes=sizes)
+    g = Graph(b.edge_index.to(cuda), b.num_nodes)
+    got = g.tile_open("gcn").cpu()
+    c = g.csr("gcn")
+    ref_t = torch.empty_like(got, device=cuda)
+    _lib.call("lgnn_tile_open", c.rowptr.data_ptr(), c.col.data_ptr(), b.num_nodes,
+              ref_t.data_ptr(), _lib.stream())
+    assert torch.equal(got, ref_t.cpu())
+    src, dst = b.edge_index
+    want = torch.zeros_like(got)
+    cross = (src // 64) != (dst // 64)
+    want[(src[cross] // 64)] = 1
+    want[(dst[cross] // 64)] = 1
+    assert torch.equal(got, want)
