@@ -43,6 +43,9 @@ __device__ unsigned long long lgnn_stamp_buf[1024 * 64];
 namespace lgnn_tile {
 
 constexpr int ABL = LGNN_ABLATE;
+#ifndef LGNN_AGG_UNROLL
+#define LGNN_AGG_UNROLL 2
+#endif
 constexpr int TM = 64;
 constexpr int KC = 128;
 constexpr int LDS = KC + 4;
@@ -649,7 +652,7 @@ __global__ __launch_bounds__(NT, 2) void k_stack_fwd(const float* __restrict__ X
         const int kc = 4 * li < K ? 4 * li : K - 4;
         auto agg_tile = [&](auto staged_tag) {
           constexpr bool STG = decltype(staged_tag)::value;
-#pragma unroll 1
+#pragma unroll LGNN_AGG_UNROLL
           for (int it = 0; it < 8; ++it) {
             const int rr = hw + 8 * it;
             f32x4 a = STG ? agg_row_local(ti, rr, A)

@@ -15,24 +15,35 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "tools", "_abl", "liblgnn_stamps.so")
+LIB = os.path.join(ROOT, "tools", "_abl", "liblgnn_stamps%s.so")
+
+
+VARIANTS = {"": [], "_u1": ["-DLGNN_AGG_UNROLL=1"], "_u4": ["-DLGNN_AGG_UNROLL=4"]}
 
 
 def build():
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(ROOT, "lesion_gnn_amd", "csrc", "*.hip")))
-    subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC",
-                           "--offload-arch=gfx950", "-shared", "-DLGNN_STAMPS", *srcs, "-o", LIB])
+    procs = [subprocess.Popen(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC",
+                               "--offload-arch=gfx950", "-shared", "-DLGNN_STAMPS", *flags, *srcs,
+                               "-o", LIB % v]) for v, flags in VARIANTS.items()]
+    assert all(p.wait() == 0 for p in procs)
 
 
 def run():
+    for v in VARIANTS:
+        print("== variant", v or "default")
+        run_one(LIB % v)
+
+
+def run_one(libpath):
     sys.path.insert(0, ROOT)
     import torch
 
     from lesion_gnn_amd import _lib, synth
     from lesion_gnn_amd.graph import Graph
 
-    lib = ctypes.CDLL(LIB)
+    lib = ctypes.CDLL(libpath)
     for name, (res, args) in _lib.SIGNATURES.items():
         f = getattr(lib, name)
         f.restype, f.argtypes = res, args
@@ -56,6 +67,15 @@ def run():
                                       csr.col.data_ptr(), csr.w.data_ptr(), L, Wp, bp, widths,
                                       Hp, Sp, None, s) == 0
     torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        lib.lgnn_gcn_stack_fwd(b.x.data_ptr(), M, 128, 1, csr.rowptr.data_ptr(),
+                               csr.col.data_ptr(), csr.w.data_ptr(), L, Wp, bp, widths, Hp, Sp,
+                               None, s)
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"stamped build: {e0.elapsed_time(e1) / 10 * 1e3:.1f} us per launch (shares only)")
     buf = (ctypes.c_ulonglong * (1024 * 64))()
     assert lib.lgnn_debug_stamps(buf) == 0
     a = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 64)[:512].astype(np.int64)
