@@ -8,7 +8,7 @@ LIB := lesion_gnn_amd/liblgnn.so
 
 all: $(LIB)
 
-build/%.o: lesion_gnn_amd/csrc/%.hip lesion_gnn_amd/csrc/common.h include/lgnn.h
+build/%.o: lesion_gnn_amd/csrc/%.hip $(wildcard lesion_gnn_amd/csrc/*.h) include/lgnn.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -129,6 +129,19 @@ int lgnn_node_linear_bwd(int grad_mode, const float* dY, const int64_t* batch, c
                          float self_scale, const float* W, int N, float* dXpre,
                          float* dW_partial, float* db_partial, int num_partials, void* stream);
 
+/* Same, restricted to the 64-node tiles t with (tile_open[t] != 0) == want_open; with
+ * accumulate = 1 a workgroup that processed a tile adds its dW/db into partial slot blockIdx.x
+ * (num_partials = lgnn_gcn_stack_bwd_partials, slots written by lgnn_gcn_stack_bwd) instead of
+ * overwriting it, and a workgroup that processed none leaves its slot alone. Fast path only. */
+int lgnn_node_linear_bwd_tiles(int grad_mode, const float* dY, const int64_t* batch,
+                               const int32_t* gptr, int pool_mean, const int32_t* tptr,
+                               const int32_t* tidx, const float* tw, float tself, const float* H,
+                               int act, const float* X, int64_t M, int K, const int32_t* rowptr,
+                               const int32_t* col, const float* w, float self_scale,
+                               const float* W, int N, float* dXpre, float* dW_partial,
+                               float* db_partial, int num_partials, const int32_t* tile_open,
+                               int want_open, int accumulate, void* stream);
+
 /* out[i] = sum_{p < P} partial[p*len + i], fixed order (bitwise reproducible). */
 int lgnn_reduce_partials(const float* partial, int num_partials, int64_t len, float* out,
                          void* stream);
@@ -266,6 +279,25 @@ int lgnn_ce_fwd(const float* logits, const int64_t* target, const float* weight,
 int lgnn_ce_bwd(const float* logits, const int64_t* target, const float* weight, int64_t B, int C,
                 const float* lse, const float* wsum, const float* grad_loss, float* dlogits,
                 void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Fused GCN layer stack, backward, for the tiles with tile_open[t] == 0 (L = 1 or 2 convs).
+ * Replaces: the autograd chain of lgnn_gcn_stack_fwd below the readout — pool broadcast of dP
+ * (global_mean/add_pool backward), per conv dZ = dH * ELU'(H), dW += dZ^T S, dS = dZ W, dH =
+ * Â^T dS, and dW_0 += dZ_0^T X for in_proj — with every intermediate on chip.
+ *   W, H, S: host arrays of L+1 device pointers (H[0] unused; S[0] = X, S[l] = saved Â H[l-1]);
+ *   widths[0..L+1] = d_in, h_0, ..., h_L; dWp/dbp: per-layer partial slabs with num_partials =
+ *   lgnn_gcn_stack_bwd_partials(M) slots (reduce with lgnn_reduce_partials[_multi]).
+ * Tiles with tile_open[t] != 0 are left to lgnn_node_linear_bwd_tiles(..., want_open = 1,
+ * accumulate = 1) on the same slabs. No input gradient (the model input needs none).
+ * ------------------------------------------------------------------------------------------- */
+int lgnn_gcn_stack_bwd_partials(int64_t num_nodes);
+int lgnn_gcn_stack_bwd(const float* dP, const int64_t* batch, const int32_t* gptr, int pool_mean,
+                       const int32_t* tptr, const int32_t* tidx, const float* tw, int64_t M,
+                       int L, const float* const* W, const float* const* H,
+                       const float* const* S, const int* widths, float* const* dWp,
+                       float* const* dbp, int num_partials, const int32_t* tile_open,
+                       void* stream);
 
 #ifdef __cplusplus
 }

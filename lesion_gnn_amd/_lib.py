@@ -39,6 +39,10 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_node_linear_bwd": (I32, [I32, P, P, P, I32, P, P, P, F32, P, I32, P, I64, I32,
                                    P, P, P, F32, P, I32, P, P, P, I32, P]),
     "lgnn_reduce_partials": (I32, [P, I32, I64, P, P]),
+    "lgnn_node_linear_bwd_tiles": (I32, [I32, P, P, P, I32, P, P, P, F32, P, I32, P, I64, I32,
+                                         P, P, P, F32, P, I32, P, P, P, I32, P, I32, I32, P]),
+    "lgnn_gcn_stack_bwd_partials": (I32, [I64]),
+    "lgnn_gcn_stack_bwd": (I32, [P, P, P, I32, P, P, P, I64, I32, P, P, P, P, P, P, I32, P, P]),
     "lgnn_spmm": (I32, [P, P, P, F32, P, I64, I32, P, P]),
     "lgnn_reduce_partials_multi": (I32, [I32, P, P, P, P, P]),
     "lgnn_ce_fwd": (I32, [P, P, P, I64, I32, P, P, P, P, P]),

@@ -320,7 +320,12 @@ __global__ __launch_bounds__(kThreads) void k_finish(int64_t N, int64_t E, int a
       }
     }
   }
-  // 64-node tiles an edge leaves (target CSR pass): the fused layer stack skips them
+  // 64-node tiles an edge leaves (source CSR pass) are open: the fused layer stacks skip them.
+  // So are tiles with more CSR entries than a tile stages in LDS (lgnn_tile CAPE = 1024).
+  if (tile_open && !tr && i < N && (i & 63) == 0) {
+    const int64_t iend64 = i + 64 < N ? i + 64 : N;
+    if (ptr[iend64] - ptr[i] > 1024) tile_open[i >> 6] = 1;
+  }
   if (tile_open && !tr && i < N) {
     const int r0 = ptr[i], r1 = ptr[i + 1];
     const int64_t ti = i >> 6;

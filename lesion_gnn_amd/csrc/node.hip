@@ -696,9 +696,27 @@ extern "C" int lgnn_node_linear_bwd(int grad_mode, const float* dY, const int64_
                                     float self_scale, const float* W, int N, float* dXpre,
                                     float* dW_partial, float* db_partial, int num_partials,
                                     void* stream) {
+  return lgnn_node_linear_bwd_tiles(grad_mode, dY, batch, gptr, pool_mean, tptr, tidx, tw, tself,
+                                    H, act, X, M, K, rowptr, col, w, self_scale, W, N, dXpre,
+                                    dW_partial, db_partial, num_partials, nullptr, 0, 0, stream);
+}
+
+extern "C" int lgnn_node_linear_bwd_tiles(int grad_mode, const float* dY, const int64_t* batch,
+                                          const int32_t* gptr, int pool_mean,
+                                          const int32_t* tptr, const int32_t* tidx,
+                                          const float* tw, float tself, const float* H, int act,
+                                          const float* X, int64_t M, int K,
+                                          const int32_t* rowptr, const int32_t* col,
+                                          const float* w, float self_scale, const float* W, int N,
+                                          float* dXpre, float* dW_partial, float* db_partial,
+                                          int num_partials, const int32_t* tile_open,
+                                          int want_open, int accumulate, void* stream) {
   if (M < 0 || K <= 0 || N <= 0 || (N & 3) || !W || !dW_partial) return LGNN_EINVAL;
   const bool fast = bwd_fast(M, N, K, rowptr != nullptr);
-  if (num_partials != (fast ? lgnn_tile_partials(M) : grid_partials(M, N, K))) return LGNN_EINVAL;
+  if (tile_open && !fast) return LGNN_EINVAL;  // tile selection only on the fast path
+  if (!tile_open && num_partials != (fast ? lgnn_tile_partials(M) : grid_partials(M, N, K)))
+    return LGNN_EINVAL;
+  if (num_partials <= 0) return LGNN_EINVAL;
   if (act != LGNN_ACT_NONE && act != LGNN_ACT_ELU) return LGNN_EINVAL;
   if (act == LGNN_ACT_ELU && !H) return LGNN_EINVAL;
   if (grad_mode == LGNN_GRAD_POOL && (!batch || !gptr)) return LGNN_EINVAL;
@@ -709,7 +727,8 @@ extern "C" int lgnn_node_linear_bwd(int grad_mode, const float* dY, const int64_
   if (fast && M > 0) {
     const hipError_t ef = lgnn_tile_bwd(s_(stream), grad_mode, dY, batch, gptr, pool_mean, tptr,
                                         tidx, tw, tself, H, act, X, M, K, W, N, dXpre, dW_partial,
-                                        db_partial, num_partials);
+                                        db_partial, num_partials, tile_open, want_open,
+                                        accumulate);
     return ef == hipSuccess ? LGNN_OK : (int)ef;
   }
   const bool dx_sep = dXpre != nullptr && N > TN;  // dZ W needs every output block: own kernel

@@ -13,4 +13,5 @@ hipError_t lgnn_tile_bwd(hipStream_t s, int grad_mode, const float* dY, const in
                          const int32_t* gptr, int pool_mean, const int32_t* tptr,
                          const int32_t* tidx, const float* tw, float tself, const float* H,
                          int act, const float* X, int64_t M, int K, const float* W, int N,
-                         float* dXpre, float* dWp, float* dbp, int P);
+                         float* dXpre, float* dWp, float* dbp, int P, const int32_t* tile_mask,
+                         int want, int accumulate);

@@ -91,25 +91,26 @@ __device__ __forceinline__ void bst4(Buf r, int off, f32x4 v) {
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 __device__ __forceinline__ f32x4 sel4(bool c, f32x4 v) { return c ? v : zero4(); }
 
-// Coalesced raw tile load: thread owns rows hw + 8*it (it < 8), columns 4li..4li+3 — the same
-// (row, column) mapping as the half-wave-per-row aggregation, so register values can be reused.
-__device__ __forceinline__ void load_rows(f32x4 (&v)[8], Buf X, int K, int r0) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int hw = wave * 2 + (lane >> 5), li = lane & 31;
+// Coalesced raw tile load: half-wave hw = tid / 32 owns rows hw + (64 / RPT) * it (it < RPT;
+// RPT = 8 for 256-thread blocks, 4 for 512), columns 4li..4li+3 — the same (row, column) mapping
+// as the half-wave-per-row aggregation, so register values can be reused.
+template <int RPT>
+__device__ __forceinline__ void load_rows(f32x4 (&v)[RPT], Buf X, int K, int r0) {
+  const int hw = threadIdx.x >> 5, li = threadIdx.x & 31;
   const int k = 4 * li;
   const int kc = k < K ? k : K - 4;
 #pragma unroll
-  for (int it = 0; it < 8; ++it) v[it] = bld4(X, ((r0 + hw + 8 * it) * K + kc) * 4);
+  for (int it = 0; it < RPT; ++it) v[it] = bld4(X, ((r0 + hw + (TM / RPT) * it) * K + kc) * 4);
 }
 
-__device__ __forceinline__ void store_rows_lds(float* A, const f32x4 (&v)[8], int64_t M, int K,
+template <int RPT>
+__device__ __forceinline__ void store_rows_lds(float* A, const f32x4 (&v)[RPT], int64_t M, int K,
                                                int64_t r0) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int hw = wave * 2 + (lane >> 5), li = lane & 31;
+  const int hw = threadIdx.x >> 5, li = threadIdx.x & 31;
   const bool kin = 4 * li < K;
 #pragma unroll
-  for (int it = 0; it < 8; ++it) {
-    const int rr = hw + 8 * it;
+  for (int it = 0; it < RPT; ++it) {
+    const int rr = hw + (TM / RPT) * it;
     st4(A + rr * LDS + 4 * li, sel4(kin && r0 + rr < M, v[it]));
   }
 }
@@ -118,14 +119,17 @@ __device__ __forceinline__ void store_rows_lds(float* A, const f32x4 (&v)[8], in
 // tile's block is in flight while the current tile aggregates and runs its MFMAs).
 //   head: rowptr[r0 .. r0+64] (one per thread, tid <= 64) + the uniform entry range (eb, ne)
 //   body: the ne <= CAPE entries (col, w), CAPE/NT per thread; issued once the head has landed
-struct IdxRegs {
+template <int NTH>
+struct IdxRegsT {
   int rp;
   int eb, ne;
-  int c[CAPE / NT];
-  float w[CAPE / NT];
+  int c[CAPE / NTH];
+  float w[CAPE / NTH];
 };
+using IdxRegs = IdxRegsT<NT>;
 
-__device__ __forceinline__ void idx_load_head(IdxRegs& R, const int32_t* __restrict__ rowptr,
+template <int NTH>
+__device__ __forceinline__ void idx_load_head(IdxRegsT<NTH>& R, const int32_t* __restrict__ rowptr,
                                               int64_t M, int64_t r0) {
   const int tid = threadIdx.x;
   const int64_t r = r0 + (tid <= TM ? tid : 0);
@@ -135,13 +139,14 @@ __device__ __forceinline__ void idx_load_head(IdxRegs& R, const int32_t* __restr
   R.ne = rowptr[rl] - R.eb;
 }
 
-__device__ __forceinline__ void idx_load_body(IdxRegs& R, const int32_t* __restrict__ col,
+template <int NTH>
+__device__ __forceinline__ void idx_load_body(IdxRegsT<NTH>& R, const int32_t* __restrict__ col,
                                               const float* __restrict__ w) {
   if (R.ne > CAPE) return;
   const int tid = threadIdx.x;
 #pragma unroll
-  for (int u = 0; u < CAPE / NT; ++u) {
-    const int j = tid + u * NT;
+  for (int u = 0; u < CAPE / NTH; ++u) {
+    const int j = tid + u * NTH;
     const int jc = j < R.ne ? j : 0;
     R.c[u] = col[R.eb + jc];
     R.w[u] = w ? w[R.eb + jc] : 1.f;
@@ -150,7 +155,8 @@ __device__ __forceinline__ void idx_load_body(IdxRegs& R, const int32_t* __restr
 
 // Writes the prefetched block to LDS. Ends with a barrier (block-wide OR of "an entry leaves
 // the tile"); `staged` = the tile takes the local path.
-__device__ __forceinline__ void idx_store(TileIdx& ti, bool& staged, const IdxRegs& R,
+template <int NTH>
+__device__ __forceinline__ void idx_store(TileIdx& ti, bool& staged, const IdxRegsT<NTH>& R,
                                           int64_t r0) {
   const int tid = threadIdx.x;
   if (tid <= TM) ti.rp[tid] = R.rp;
@@ -158,8 +164,8 @@ __device__ __forceinline__ void idx_store(TileIdx& ti, bool& staged, const IdxRe
   int out = 0;
   if (fits) {
 #pragma unroll
-    for (int u = 0; u < CAPE / NT; ++u) {
-      const int j = tid + u * NT;
+    for (int u = 0; u < CAPE / NTH; ++u) {
+      const int j = tid + u * NTH;
       const int rel = R.c[u] - (int)r0;
       if (j < R.ne && (unsigned)rel >= (unsigned)TM) out = 1;
     }
@@ -168,8 +174,8 @@ __device__ __forceinline__ void idx_store(TileIdx& ti, bool& staged, const IdxRe
   staged = fits && !any_out;
   if (staged) {
 #pragma unroll
-    for (int u = 0; u < CAPE / NT; ++u) {
-      const int j = tid + u * NT;
+    for (int u = 0; u < CAPE / NTH; ++u) {
+      const int j = tid + u * NTH;
       if (j < R.ne) ti.ow[j] = make_int2((R.c[u] - (int)r0) * LDS, __float_as_int(R.w[u]));
     }
     if (tid < EB) ti.ow[R.ne + tid] = make_int2(0, 0);
@@ -180,20 +186,22 @@ __device__ __forceinline__ void idx_store(TileIdx& ti, bool& staged, const IdxRe
 // Local path: every source row is in the LDS image A; per entry one ds_read_b64 (offset,
 // weight), one ds_read_b128 and two packed FMAs, no bounds logic and no global access (so no
 // vmcnt wait that would drain the prefetch loads and row stores in flight).
+template <int UB = EB>
 __device__ __forceinline__ f32x4 agg_row_local(const TileIdx& ti, int rr, const float* A) {
+  static_assert(UB <= EB, "row batches read at most EB padding entries");
   const int li = threadIdx.x & 31;
   const int eb = ti.rp[0];
   const int e0 = ti.rp[rr] - eb, e1 = ti.rp[rr + 1] - eb;
   f32x4 acc = zero4();
-  for (int e = e0; e < e1; e += EB) {
-    int2 p[EB];
+  for (int e = e0; e < e1; e += UB) {
+    int2 p[UB];
 #pragma unroll
-    for (int u = 0; u < EB; ++u) p[u] = ti.ow[e + u];
-    f32x4 v[EB];
+    for (int u = 0; u < UB; ++u) p[u] = ti.ow[e + u];
+    f32x4 v[UB];
 #pragma unroll
-    for (int u = 0; u < EB; ++u) v[u] = ld4(A + p[u].x + 4 * li);
+    for (int u = 0; u < UB; ++u) v[u] = ld4(A + p[u].x + 4 * li);
 #pragma unroll
-    for (int u = 0; u < EB; ++u) {
+    for (int u = 0; u < UB; ++u) {
       const float wv = e + u < e1 ? __int_as_float(p[u].y) : 0.f;
       acc += wv * v[u];
     }
@@ -368,7 +376,7 @@ __global__ __launch_bounds__(NT, 2) void k_bwd(
     const int32_t* __restrict__ tidx, const float* __restrict__ tw, float tself,
     const float* __restrict__ H, const float* __restrict__ X, int64_t M, int K,
     const float* __restrict__ W, int N, float* __restrict__ dXpre, float* __restrict__ dWp,
-    float* __restrict__ dbp) {
+    float* __restrict__ dbp, const int32_t* __restrict__ tmask, int want, int accumulate) {
   __shared__ __attribute__((aligned(16))) float A[TM * LDS];
   __shared__ __attribute__((aligned(16))) float C[TM * LDS];
   __shared__ TileIdx ti;
@@ -388,8 +396,9 @@ __global__ __launch_bounds__(NT, 2) void k_bwd(
   // pipeline prologue (TRANSPOSE): the first tile's dY rows and transpose-CSR index block
   f32x4 dr[8];
   IdxRegs R;
+  const int64_t tfirst = seek_tile(blockIdx.x, ntiles, tmask, want);
   if constexpr (GMODE == LGNN_GRAD_TRANSPOSE) {
-    const int64_t t0 = blockIdx.x;
+    const int64_t t0 = tfirst;
     if (t0 < ntiles) {
       if constexpr (!(ABL & 16)) load_rows(dr, bdY, N, (int)(t0 * TM));
       if constexpr (!(ABL & 2)) {
@@ -399,9 +408,9 @@ __global__ __launch_bounds__(NT, 2) void k_bwd(
     }
   }
 
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  for (int64_t t = tfirst; t < ntiles; t = seek_tile(t + gridDim.x, ntiles, tmask, want)) {
     const int64_t r0 = t * TM;
-    const int64_t tn = t + gridDim.x;
+    const int64_t tn = seek_tile(t + gridDim.x, ntiles, tmask, want);
     const bool has_next = tn < ntiles;
     // ---- dZ tile -> C
     if constexpr (GMODE == LGNN_GRAD_TRANSPOSE) {
@@ -553,6 +562,9 @@ __global__ __launch_bounds__(NT, 2) void k_bwd(
     }
     __syncthreads();
   }
+  // accumulate: add into slot blockIdx.x (written by the fused stack backward) if this
+  // workgroup processed any tile; otherwise leave the slot untouched
+  if (accumulate && tfirst >= ntiles) return;
   float* slab = dWp + (int64_t)blockIdx.x * N * K;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -560,10 +572,16 @@ __global__ __launch_bounds__(NT, 2) void k_bwd(
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int o = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (o < N && k < K) slab[(int64_t)o * K + k] = dw[j][r];
+      if (o < N && k < K) {
+        float* p = slab + (int64_t)o * K + k;
+        *p = accumulate ? *p + dw[j][r] : dw[j][r];
+      }
     }
   }
-  if (dbp && tid < N) dbp[(int64_t)blockIdx.x * N + tid] = dbacc;
+  if (dbp && tid < N) {
+    float* p = dbp + (int64_t)blockIdx.x * N + tid;
+    *p = accumulate ? *p + dbacc : dbacc;
+  }
 }
 
 
@@ -717,6 +735,339 @@ __global__ __launch_bounds__(NT, 2) void k_stack_fwd(const float* __restrict__ X
     }
   }
 }
+// ------------------------------------------------------------------------------------------
+// Fused layer stack, backward, for the tiles no edge leaves (the forward's k_stack_fwd tiles):
+// from the pooled-output gradient dP down to the in_proj weights in one launch, the tile on chip
+//   dZ_L = dP[g(i)] (/ count) * ELU'(H_L)
+//   for l = L..1:  dW_l += dZ_l^T S_l, db_l += colsum dZ_l, dS_l = dZ_l W_l,
+//                  dZ_{l-1} = (Â^T dS_l) * ELU'(H_{l-1})   (no ELU' below the first conv)
+//   dW_0 += dZ_0^T X, db_0 += colsum dZ_0
+// One workgroup per CU (4 waves, one per SIMD, up to 512 registers each): the NL layers' dW
+// accumulators stay in registers across the workgroup's tiles and are written once, as partial
+// slot blockIdx.x of each layer's slab. The next rows (S_{l-1}, H_{l-1}, or the next tile's
+// S_L, H_L, pool gradient and CSR block) are prefetched into registers while the MFMAs run.
+// ------------------------------------------------------------------------------------------
+struct StackBwdArgs {
+  const float* W[LGNN_MAX_STACK];
+  const float* H[LGNN_MAX_STACK];  // H[l], l >= 1: the conv's ELU output (for ELU')
+  const float* S[LGNN_MAX_STACK];  // dW operand: S[l] = Â H[l-1] (l >= 1), S[0] = X
+  float* dWp[LGNN_MAX_STACK];      // [P][N_l][K_l]
+  float* dbp[LGNN_MAX_STACK];      // [P][N_l]
+  int width[LGNN_MAX_STACK + 1];   // width[l] = input width of layer l, width[l+1] = output
+};
+
+// dH_L rows of a tile from the pooled-output gradient (global_mean/add_pool backward):
+// dH[m] = dP[batch[m]] (/ |graph|), in two steps so neither waits on the other: the graph ids
+// (pool_ids), then the dP rows and graph sizes (pool_rows); the division happens at use
+// (pool_scale). Same row mapping as load_rows.
+template <int RPT>
+__device__ __forceinline__ void pool_ids(int (&gi)[RPT], const int64_t* __restrict__ batch,
+                                         int64_t M, int64_t r0) {
+  const int hw = threadIdx.x >> 5;
+#pragma unroll
+  for (int it = 0; it < RPT; ++it) {
+    const int64_t row = r0 + hw + (TM / RPT) * it;
+    gi[it] = (int)batch[row < M ? row : M - 1];
+  }
+}
+
+template <int RPT>
+__device__ __forceinline__ void pool_rows(f32x4 (&gv)[RPT], int (&cnt)[RPT], const int (&gi)[RPT],
+                                          const float* __restrict__ dP,
+                                          const int32_t* __restrict__ gptr, int pool_mean, int N) {
+  const int li = threadIdx.x & 31;
+  const int oc = 4 * li < N ? 4 * li : N - 4;
+#pragma unroll
+  for (int it = 0; it < RPT; ++it) {
+    gv[it] = ld4(dP + (int64_t)gi[it] * N + oc);
+    cnt[it] = pool_mean ? gptr[gi[it] + 1] - gptr[gi[it]] : 1;
+  }
+}
+
+__device__ __forceinline__ f32x4 pool_scale(f32x4 v, int cnt) {
+  return cnt > 1 ? v / (float)cnt : v;
+}
+
+// ------------------------------------------------------------------------------------------
+// Fused GCN stack backward (closed tiles), 512 threads = 8 waves, one workgroup per CU (two
+// waves per SIMD hide each other's LDS / L2 latency). Per tile, all on chip:
+//   dZ_L = pool-broadcast(dP) * ELU'(H_L)
+//   for l = L..0:  dW_l += dZ_l^T S_l,  db_l += colsum(dZ_l)
+//                  (l >= 1) dS_l = dZ_l W_l;  dZ_{l-1} = (Â^T dS_l) [* ELU'(H_{l-1}) if l >= 2]
+// LDS: C = dZ_l, A = S_l then dS_l (padded rows), Wl = W_l (unpadded [o][k], filled by
+// direct-to-LDS buffer loads issued before the dW MFMAs, so the weight costs no registers),
+// ti = the tile's transposed CSR block.
+// Work split: dW_l — wave (wo = w & 3, wk = w >> 2) owns dW[32wo..+32][64wk..+64] (two 32x32
+// accumulators per layer, resident over all the workgroup's tiles); dS_l^T = W_l^T dZ_l^T —
+// wave (kb = w & 3, mb = w >> 2) owns the 32x32 block k in [32kb, +32), m in [32mb, +32).
+// db: per-thread column partials, reduced over the 16 row groups at the end.
+// ------------------------------------------------------------------------------------------
+#ifndef LGNN_BWD_EB
+#define LGNN_BWD_EB 2
+#endif
+#ifndef LGNN_AGG_ROWS
+#define LGNN_AGG_ROWS 1
+#endif
+constexpr int NTB = 512;
+constexpr int RPB = TM / (NTB / 32);  // rows per thread (4)
+
+// Register-lean row access for the 512-thread kernel: one buffer descriptor (SGPRs) per row
+// group, so the per-lane offset is a single VGPR per width instead of one per row (row offsets
+// held in VGPRs across the persistent tile loop would spill). Rows past M read as zeros.
+__device__ __forceinline__ Buf rows_buf(const float* X, int64_t M, int K, int64_t rb) {
+  const int64_t rem = M - rb;
+  return mkbuf(X + rb * K, rem > 0 ? rem * K * 4 : 0);
+}
+
+template <int RPT>
+__device__ __forceinline__ void load_rows_d(f32x4 (&v)[RPT], const float* X, int64_t M, int K,
+                                            int64_t r0) {
+  const int hw = threadIdx.x >> 5, li = threadIdx.x & 31;
+  const int kc = 4 * li < K ? 4 * li : K - 4;
+  const int off = (hw * K + kc) * 4;
+#pragma unroll
+  for (int it = 0; it < RPT; ++it) v[it] = bld4(rows_buf(X, M, K, r0 + (TM / RPT) * it), off);
+}
+
+// W [N][K] (row-major, global) -> Wl [N][KC] in LDS, zero-filled past N and K. 16 B per lane,
+// two 128-float rows per wave instruction; no registers, completion by vmcnt.
+__device__ __forceinline__ void stage_w_lds(float* Wl, const float* W, int N, int K) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = 4 * (lane & 31);
+  const int off = c < K ? ((lane >> 5) * K + c) * 4 : 0x7ffffff0;  // OOB -> zeros
+#pragma unroll
+  for (int u = 0; u < KC / (2 * (NTB / 64)); ++u) {  // 8 instructions per wave
+    const int o0 = 2 * (wave + (NTB / 64) * u);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        rows_buf(W, N, K, o0), (__attribute__((address_space(3))) void*)(Wl + o0 * KC), 16, off,
+        0, 0, 0);
+  }
+}
+
+// LDS image of k_stack_bwd. A and C first: every row access then fits the 16-bit immediate
+// offset of ds_read/ds_write (no per-access address VALU).
+template <int NL>
+struct BwdSmem {
+  float A[TM * LDS];
+  float C[TM * LDS];
+  TileIdx ti;
+  float Db[NL][NTB / 64][KC];  // db partials per wave, column
+  float Wl[KC * KC];
+};
+
+template <int NL>
+__global__ __launch_bounds__(NTB, 1) void k_stack_bwd(const float* __restrict__ dP,
+                                                      const int64_t* __restrict__ batch,
+                                                      const int32_t* __restrict__ gptr,
+                                                      int pool_mean,
+                                                      const int32_t* __restrict__ tptr,
+                                                      const int32_t* __restrict__ tidx,
+                                                      const float* __restrict__ tw, int64_t M,
+                                                      StackBwdArgs a,
+                                                      const int32_t* __restrict__ tmask) {
+  constexpr int L = NL - 1;
+  __shared__ __attribute__((aligned(16))) BwdSmem<NL> sm;
+  float* const A = sm.A;
+  float* const C = sm.C;
+  float* const Wl = sm.Wl;
+  TileIdx& ti = sm.ti;
+  auto& Db = sm.Db;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, li = lane & 31, hw = tid >> 5;
+  const int wq = wave & 3, wr2 = wave >> 2;  // (wo, wk) for dW; (kb, mb) for dS
+  const int64_t ntiles = (M + TM - 1) / TM;
+
+  f32x16 dw[NL][2];
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    dw[l][0] = f32x16{};
+    dw[l][1] = f32x16{};
+  }
+  for (int i = tid; i < NL * (NTB / 64) * KC; i += NTB) (&Db[0][0][0])[i] = 0.f;
+  // db partials: the two half-waves' column sums combined, added into the wave's LDS row by
+  // the lane that owns those 4 columns (no other thread touches them until the end)
+  auto db_flush = [&](int l, f32x4 v) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] += __shfl_xor(v[j], 32);
+    if (h == 0) {
+      float* d = &Db[l][wave][4 * li];
+      st4(d, ld4(d) + v);
+    }
+  };
+  f32x4 hv[RPB], sr[RPB], gv[RPB];
+  int gi[RPB], cnt[RPB];
+  IdxRegsT<NTB> R;
+  int64_t t = seek_tile(blockIdx.x, ntiles, tmask, 0);
+  if (t < ntiles) {
+    pool_ids(gi, batch, M, t * TM);
+    pool_rows(gv, cnt, gi, dP, gptr, pool_mean, a.width[L + 1]);
+    load_rows_d(hv, a.H[L], M, a.width[L + 1], t * TM);
+    load_rows_d(sr, a.S[L], M, a.width[L], t * TM);
+    idx_load_head(R, tptr, M, t * TM);
+    idx_load_body(R, tidx, tw);
+    stage_w_lds(Wl, a.W[L], a.width[L + 1], a.width[L]);
+  }
+  [[maybe_unused]] int stamp = 0;
+  STAMP(stamp++);
+  for (; t < ntiles;) {
+    const int64_t r0 = t * TM;
+    const int64_t tn = seek_tile(t + gridDim.x, ntiles, tmask, 0);
+    const bool has_next = tn < ntiles;
+    bool staged = true;
+    idx_store(ti, staged, R, r0);  // ends with a barrier; closed tiles are always local
+    {
+      const int N = a.width[L + 1];
+      f32x4 dsum = zero4();
+#pragma unroll
+      for (int it = 0; it < RPB; ++it) {
+        const int rr = hw + (TM / RPB) * it;
+        f32x4 v = pool_scale(gv[it], cnt[it]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] *= elu_grad_from_out(hv[it][j]);
+        v = sel4(4 * li < N && r0 + rr < M, v);
+        dsum += v;
+        st4(C + rr * LDS + 4 * li, v);
+      }
+      db_flush(L, dsum);
+    }
+#pragma unroll
+    for (int l = L; l >= 0; --l) {
+      const int K = a.width[l];
+      store_rows_lds(A, sr, M, K, r0);
+      // W_l was staged a phase earlier; this wave's share has landed once vmcnt drains (the
+      // row loads issued since have been consumed), the barrier publishes every wave's share
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      STAMP(stamp++);
+      // prefetch what the next phase needs. The next tile's loads are split over the last two
+      // phases so that no load waits on another in front of the MFMAs: graph ids and CSR
+      // head at l = 1, then the rows, the CSR body and W_L (Wl is free since l = 1's DX) at 0.
+      if (l >= 1) {
+        if (l >= 2)
+          load_rows_d(hv, a.H[l - 1], M, a.width[l], r0);
+        load_rows_d(sr, a.S[l - 1], M, a.width[l - 1], r0);
+        if (l == 1 && has_next) {
+          pool_ids(gi, batch, M, tn * TM);
+          idx_load_head(R, tptr, M, tn * TM);
+        }
+      } else if (has_next) {
+        pool_rows(gv, cnt, gi, dP, gptr, pool_mean, a.width[L + 1]);
+        load_rows_d(hv, a.H[L], M, a.width[L + 1], tn * TM);
+        load_rows_d(sr, a.S[L], M, a.width[L], tn * TM);
+        idx_load_body(R, tidx, tw);
+        stage_w_lds(Wl, a.W[L], a.width[L + 1], a.width[L]);
+      }
+      // dW_l[o][k] += sum_m dZ[m][o] S[m][k], m = 2 s2 + h. Accumulator j holds the columns
+      // k = 64 wk + 2 li + j, so a lane's two B operands are one ds_read_b64. Operands of step
+      // s2 + 1 are read before the MFMAs of step s2 are issued.
+      {
+        const float* cp = C + h * LDS + 32 * wq + li;
+        const float* ap = A + h * LDS + 64 * wr2 + 2 * li;
+        float a0 = cp[0];
+        float2 b = *reinterpret_cast<const float2*>(ap);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // step 0 operands
+#pragma unroll
+        for (int s2 = 0; s2 < TM / 2; ++s2) {
+          const int nx = (s2 + 1 < TM / 2 ? s2 + 1 : s2) * 2 * LDS;
+          const float a1 = cp[nx];
+          const float2 bn = *reinterpret_cast<const float2*>(ap + nx);
+          dw[l][0] = mfma32(a0, b.x, dw[l][0]);
+          dw[l][1] = mfma32(a0, b.y, dw[l][1]);
+          a0 = a1;
+          b = bn;
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS reads of step s2 + 1
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // MFMAs of step s2
+        }
+      }
+      if (l == 0) {
+        __syncthreads();  // A / C free for the next tile
+        STAMP(stamp++);
+        continue;
+      }
+      STAMP(stamp++);
+      // dS_l^T[k][m] = sum_o W_l[o][k] dZ[m][o]; half h contracts o in [64h, 64h + 64)
+      f32x16 x = {};
+      {
+        const float* wp = Wl + 64 * h * KC + 32 * wq + li;
+        const float* cp = C + (32 * wr2 + li) * LDS + 64 * h;
+        f32x4 cv = ld4(cp);
+        float wv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wv[j] = wp[j * KC];
+        __builtin_amdgcn_sched_group_barrier(0x100, 5, 0);
+#pragma unroll
+        for (int p4 = 0; p4 < 16; ++p4) {  // operands of group p4 + 1 read ahead
+          const int nx = p4 + 1 < 16 ? p4 + 1 : p4;
+          const f32x4 cn = ld4(cp + 4 * nx);
+          float wn[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) wn[j] = wp[(4 * nx + j) * KC];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) x = mfma32(wv[j], cv[j], x);
+          cv = cn;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) wv[j] = wn[j];
+          __builtin_amdgcn_sched_group_barrier(0x100, 5, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        }
+      }
+      __syncthreads();  // every wave is done reading A (S_l), C (dZ_l) and Wl
+      STAMP(stamp++);
+      if (l >= 2) stage_w_lds(Wl, a.W[l - 1], a.width[l], a.width[l - 1]);
+      {
+        float* ap = A + (32 * wr2 + li) * LDS + 32 * wq + 4 * h;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int k = 32 * wq + 8 * g + 4 * h;
+          st4(ap + 8 * g, sel4(k < K, f32x4{x[4 * g], x[4 * g + 1], x[4 * g + 2], x[4 * g + 3]}));
+        }
+      }
+      __syncthreads();
+      STAMP(stamp++);
+      // dZ_{l-1} = (Â^T dS_l) * ELU'(H_{l-1}); in_proj (l - 1 = 0) has no activation
+      f32x4 dsum = zero4();
+#pragma unroll LGNN_AGG_ROWS
+      for (int it = 0; it < RPB; ++it) {
+        const int rr = hw + (TM / RPB) * it;
+        f32x4 g = agg_row_local<LGNN_BWD_EB>(ti, rr, A);
+        if (l >= 2) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) g[j] *= elu_grad_from_out(hv[it][j]);
+        }
+        g = sel4(4 * li < K && r0 + rr < M, g);
+        dsum += g;
+        st4(C + rr * LDS + 4 * li, g);
+      }
+      db_flush(l - 1, dsum);
+      __syncthreads();
+      STAMP(stamp++);
+    }
+    t = tn;
+  }
+  __syncthreads();  // db: the 8 wave partials of each column, summed in a fixed order
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    const int N = a.width[l + 1], K = a.width[l];
+    if (tid < N) {
+      float acc = 0.f;
+#pragma unroll
+      for (int g = 0; g < NTB / 64; ++g) acc += Db[l][g][tid];
+      a.dbp[l][(int64_t)blockIdx.x * N + tid] = acc;
+    }
+    float* slab = a.dWp[l] + (int64_t)blockIdx.x * N * K;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = 64 * wr2 + 2 * li + j;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int o = 32 * wq + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (o < N && k < K) slab[(int64_t)o * K + k] = dw[l][j][r];
+      }
+    }
+  }
+}
+
 // open[t] = 1 if an edge joins a node of tile t with a node of another tile (target CSR).
 __global__ __launch_bounds__(NT) void k_tile_open(const int32_t* __restrict__ rowptr,
                                                   const int32_t* __restrict__ col, int64_t M,
@@ -781,11 +1132,13 @@ hipError_t lgnn_tile_bwd(hipStream_t s, int grad_mode, const float* dY, const in
                          const int32_t* gptr, int pool_mean, const int32_t* tptr,
                          const int32_t* tidx, const float* tw, float tself, const float* H,
                          int act, const float* X, int64_t M, int K, const float* W, int N,
-                         float* dXpre, float* dWp, float* dbp, int P) {
+                         float* dXpre, float* dWp, float* dbp, int P, const int32_t* tile_mask,
+                         int want, int accumulate) {
   dim3 grid((unsigned)P);
 #define LGNN_TB(GM, AC, D)                                                                     \
   hipLaunchKernelGGL((k_bwd<GM, AC, D>), grid, dim3(NT), 0, s, dY, batch, gptr, pool_mean, tptr, \
-                     tidx, tw, tself, H, X, M, K, W, N, dXpre, dWp, dbp)
+                     tidx, tw, tself, H, X, M, K, W, N, dXpre, dWp, dbp, tile_mask, want,        \
+                     accumulate)
 #define LGNN_TB_D(GM, AC) \
   if (dXpre) LGNN_TB(GM, AC, true); else LGNN_TB(GM, AC, false);
   if (act == LGNN_ACT_ELU) {
@@ -875,3 +1228,55 @@ extern "C" int lgnn_debug_stamps(unsigned long long* host_out) {
   return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(lgnn_stamp_buf), sizeof(lgnn_stamp_buf));
 }
 #endif
+
+// ------------------------------------------------------------------------------------------
+// C ABI: fused GCN stack backward (closed tiles)
+// ------------------------------------------------------------------------------------------
+extern "C" int lgnn_gcn_stack_bwd_partials(int64_t M) {
+  if (M < 0) return LGNN_EINVAL;
+  const int64_t ntiles = (M + lgnn_tile::TM - 1) / lgnn_tile::TM;
+  const int64_t p = ntiles < 256 ? ntiles : 256;
+  return (int)(p < 1 ? 1 : p);
+}
+
+extern "C" int lgnn_gcn_stack_bwd(const float* dP, const int64_t* batch, const int32_t* gptr,
+                                  int pool_mean, const int32_t* tptr, const int32_t* tidx,
+                                  const float* tw, int64_t M, int L, const float* const* W,
+                                  const float* const* H, const float* const* S,
+                                  const int* widths, float* const* dWp, float* const* dbp,
+                                  int num_partials, const int32_t* tile_open, void* stream) {
+  if (M < 0 || L < 1 || L > 2 || !dP || !batch || !gptr || !tptr || !tidx || !W || !H || !S ||
+      !widths || !dWp || !dbp || !tile_open)
+    return LGNN_EINVAL;
+  if (num_partials != lgnn_gcn_stack_bwd_partials(M)) return LGNN_EINVAL;
+  lgnn_tile::StackBwdArgs a = {};
+  for (int l = 0; l <= L + 1; ++l) a.width[l] = widths[l];
+  for (int l = 0; l <= L; ++l) {
+    const int K = a.width[l], N = a.width[l + 1];
+    if (!lgnn_tile_fits(M, K, N) || !W[l] || !S[l] || !dWp[l] || !dbp[l]) return LGNN_EINVAL;
+    if (l >= 1 && !H[l]) return LGNN_EINVAL;
+    a.W[l] = W[l];
+    a.H[l] = H[l];
+    a.S[l] = S[l];
+    a.dWp[l] = dWp[l];
+    a.dbp[l] = dbp[l];
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (M == 0) {  // one all-zero slot per layer
+    for (int l = 0; l <= L; ++l) {
+      if (hipMemsetAsync(a.dWp[l], 0, (size_t)a.width[l] * a.width[l + 1] * 4, s) != hipSuccess ||
+          hipMemsetAsync(a.dbp[l], 0, (size_t)a.width[l + 1] * 4, s) != hipSuccess)
+        return (int)hipGetLastError();
+    }
+    return LGNN_OK;
+  }
+  dim3 grid((unsigned)num_partials);
+  if (L == 1)
+    hipLaunchKernelGGL(lgnn_tile::k_stack_bwd<2>, grid, dim3(lgnn_tile::NTB), 0, s, dP, batch, gptr,
+                       pool_mean, tptr, tidx, tw, M, a, tile_open);
+  else
+    hipLaunchKernelGGL(lgnn_tile::k_stack_bwd<3>, grid, dim3(lgnn_tile::NTB), 0, s, dP, batch, gptr,
+                       pool_mean, tptr, tidx, tw, M, a, tile_open);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? LGNN_OK : (int)e;
+}

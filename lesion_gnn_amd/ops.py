@@ -11,6 +11,7 @@
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -55,6 +56,10 @@ def linear_fwd(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None, act: in
 STACK_MAX = 8  # LGNN_MAX_STACK
 
 
+# fused stack backward on/off (LGNN_FUSED_BWD=0 selects the layer-wise backward; diagnostics)
+FUSED_BWD = os.environ.get("LGNN_FUSED_BWD", "1") != "0"
+
+
 def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list):
     """in_proj + L x ELU(GCNConv) forward, every width <= 128: returns ([H_0..H_L],
     [S_1..S_L]). Tiles no edge leaves run fused through every layer (lgnn_gcn_stack_fwd); the
@@ -86,6 +91,63 @@ def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list):
                   _lib.ptr(hs[l]), _lib.ptr(ss[l - 1]) if l > 0 else None, _lib.ptr(open_), 1,
                   _s(dev))
     return hs, ss
+
+
+def stack_bwd(dp: torch.Tensor, x: torch.Tensor, graph: Graph, mean: bool, Ws: list,
+              hs: list, ss: list, reducer: list):
+    """Backward of stack_fwd from the pooled-output gradient dp down to in_proj, L = 1 or 2
+    convs, no input gradient. Closed tiles run fused (lgnn_gcn_stack_bwd, one launch); open
+    tiles layer by layer (lgnn_node_linear_bwd_tiles, want_open = 1, accumulate = 1) into the
+    same partial slots. Returns [(dW_l, db_l)] for l = 0..L; the slab reductions are appended
+    to `reducer`."""
+    csr = graph.csr("gcn")
+    open_ = graph.tile_open("gcn")
+    M = x.size(0)
+    L = len(Ws) - 1
+    dev = x.device
+    lib = _lib.load()
+    P = lib.lgnn_gcn_stack_bwd_partials(M)
+    _lib.check(0 if P > 0 else P, "lgnn_gcn_stack_bwd_partials")
+    widths = [x.size(1)] + [W.size(0) for W in Ws]
+    per = [widths[l + 1] * widths[l] + widths[l + 1] for l in range(L + 1)]
+    slab = torch.empty(P * sum(per), dtype=torch.float32, device=dev)
+    dWp, dbp, off = [], [], 0
+    for l in range(L + 1):
+        nk, n = widths[l + 1] * widths[l], widths[l + 1]
+        dWp.append(slab[off:off + P * nk])
+        dbp.append(slab[off + P * nk:off + P * (nk + n)])
+        off += P * (nk + n)
+    arr = ctypes.c_void_p * (L + 1)
+    Sx = [x] + list(ss)
+    _lib.call("lgnn_gcn_stack_bwd", _lib.ptr(dp), _lib.ptr(graph.batch), _lib.ptr(graph.gptr),
+              int(mean), _lib.ptr(csr.tptr), _lib.ptr(csr.tidx), _lib.ptr(csr.tw), M, L,
+              arr(*[W.data_ptr() for W in Ws]), arr(None, *[h.data_ptr() for h in hs[1:]]),
+              arr(*[t.data_ptr() for t in Sx]), (ctypes.c_int * (L + 2))(*widths),
+              arr(*[t.data_ptr() for t in dWp]), arr(*[t.data_ptr() for t in dbp]), P,
+              _lib.ptr(open_), _s(dev))
+    dS = None
+    for l in reversed(range(L + 1)):
+        K, N = widths[l], widths[l + 1]
+        if l == L:
+            mode, dY, tc = _lib.LGNN_GRAD_POOL, dp, None
+        else:
+            mode, dY, tc = _lib.LGNN_GRAD_TRANSPOSE, dS, csr
+        dX = torch.empty(M, K, dtype=torch.float32, device=dev) if l > 0 else None
+        _lib.call("lgnn_node_linear_bwd_tiles", mode, _lib.ptr(dY), _lib.ptr(graph.batch),
+                  _lib.ptr(graph.gptr), int(mean), _lib.ptr(tc.tptr) if tc else None,
+                  _lib.ptr(tc.tidx) if tc else None, _lib.ptr(tc.tw) if tc else None, 0.0,
+                  _lib.ptr(hs[l]) if l > 0 else None,
+                  _lib.LGNN_ACT_ELU if l > 0 else _lib.LGNN_ACT_NONE, _lib.ptr(Sx[l]), M, K,
+                  None, None, None, 0.0, _lib.ptr(Ws[l]), N, _lib.ptr(dX), _lib.ptr(dWp[l]),
+                  _lib.ptr(dbp[l]), P, _lib.ptr(open_), 1, 1, _s(dev))
+        dS = dX
+    out = []
+    for l in range(L + 1):
+        dW = torch.empty(widths[l + 1], widths[l], dtype=torch.float32, device=dev)
+        db = torch.empty(widths[l + 1], dtype=torch.float32, device=dev)
+        reducer.extend([(dWp[l], P, dW.numel(), dW), (dbp[l], P, db.numel(), db)])
+        out.append((dW, db))
+    return out
 
 
 def num_partials(M: int, N: int, K: int, gather: bool = False) -> int:
@@ -287,6 +349,7 @@ class _GCNStack(torch.autograd.Function):
         W_in, b_in = params[0], params[1]
         Ws = [params[2 * l] for l in range(L + 1)]
         fused = L + 1 <= STACK_MAX and all(fast_shape(W.size(1), W.size(0)) for W in Ws)
+        ctx.fused = fused
         if fused:
             hs, ss = stack_fwd(x, graph, Ws, [params[2 * l + 1] for l in range(L + 1)])
             ctx.saved_s = [True] * L
@@ -324,8 +387,14 @@ class _GCNStack(torch.autograd.Function):
         dp, dWo, dbo = pool_head_bwd(_f32c(dlogits), pooled, W_out)
         grads = [None] * len(params)
         grads[2 + 2 * L], grads[3 + 2 * L] = dWo, dbo
-        dS = None
         red: list = []
+        if ctx.fused and 1 <= L <= 2 and not ctx.needs_input_grad[0] and FUSED_BWD:
+            Ws = [params[2 * l] for l in range(L + 1)]
+            for l, (dW, db) in enumerate(stack_bwd(dp, x, graph, ctx.mean, Ws, hs, ss, red)):
+                grads[2 * l], grads[2 * l + 1] = dW, db
+            reduce_multi(red, x.device)
+            return (None, None, None, None, *grads)
+        dS = None
         for l in reversed(range(L)):
             W = params[2 + 2 * l]
             if l == L - 1:

@@ -284,3 +284,37 @@ def test_tile_open_flags(cuda):
     want[(src[cross] // 64)] = 1
     want[(dst[cross] // 64)] = 1
     assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("case", ["c2_L2", "irregular_L2", "irregular_L1_add", "dense_tiles"])
+def test_gcn_fused_backward(cuda, case, monkeypatch):
+    """lgnn_gcn_stack_bwd (closed tiles, fused) + masked accumulating layer-wise backward (open
+    tiles) vs the layer-wise backward and the oracle. dense_tiles: 64-node graphs with k = 20
+    (1344 CSR entries per tile > the 1024 a tile stages) are flagged open by the graph build."""
+    pool = "add" if case.endswith("add") else "mean"
+    hidden = [128, 128] if "L1" in case else [128, 128, 128]
+    if case == "c2_L2":
+        b = synth.make_batch(300, n=64, k=8, d_in=128, seed=31)
+    elif case == "dense_tiles":
+        b = synth.make_batch(6, n=64, k=20, d_in=128, seed=32, sizes=[64, 64, 30, 34, 64, 64])
+    else:
+        b = synth.make_batch(9, k=6, d_in=128, seed=33, sizes=[1, 5, 64, 200, 2, 33, 512, 17, 64])
+    ours, oref = make_pair(hidden, pool=pool)
+    ours = ours.to(cuda)
+    if case == "dense_tiles":
+        g = Graph(b.edge_index.to(cuda), b.num_nodes)
+        assert g.tile_open("gcn").cpu().tolist() == [1, 1, 1, 1, 1]
+    monkeypatch.setattr(ops, "FUSED_BWD", True)
+    lf, _, gf = run_step(ours, b, cuda)
+    monkeypatch.setattr(ops, "FUSED_BWD", False)
+    ll, _, gl = run_step(ours, b, cuda)
+    lr_, _, gr = run_step(oref, b, "cpu")
+    assert torch.equal(lf, ll)
+    torch.testing.assert_close(lf, lr_, atol=1e-4, rtol=0)
+    for k in gr:
+        torch.testing.assert_close(gf[k], gl[k], atol=1e-6, rtol=1e-5, msg=lambda m: f"{k}: {m}")
+        torch.testing.assert_close(gf[k], gr[k], atol=1e-5, rtol=1e-4, msg=lambda m: f"{k}: {m}")
+    monkeypatch.setattr(ops, "FUSED_BWD", True)
+    _, _, gf2 = run_step(ours, b, cuda)
+    for k in gf:
+        assert torch.equal(gf[k], gf2[k]), k
