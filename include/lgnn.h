@@ -247,21 +247,22 @@ int lgnn_gat_bwd_node(const int32_t* tptr, const int32_t* tidx, const int32_t* t
  * Fused GCN layer stack, forward (one launch for the whole model body below the readout).
  * Replaces: in_proj nn.Linear (reference gin.py:21 skeleton) + L x (GCNConv + F.elu) — the
  * layer-by-layer lgnn_node_linear_fwd chain — keeping each 64-node tile on chip across layers.
- *   has_in_proj=1: H[0] = X W[0]^T + b[0] (X [M, d_in]); else H[0] is X itself (widths[0]=d_in)
- *   for l = 1..L: S[l] = Â H[l-1] (CSR rowptr/col/w, self term via the CSR), H[l] = ELU(S[l]
- *   W[l]^T + b[l]).  W, b, H, S: host arrays of L+1 device pointers (S[0] unused); widths[l] =
- *   output width of layer l. All widths and d_in <= 128, multiples of 4; L + 1 <= 8.
- *   tile_open (nullable): only tiles with tile_open[t] == 0 are computed (the others read
- *   neighbours that another tile computes in the same layer: run them with
- *   lgnn_node_linear_fwd_tiles(..., tile_open, 1)).
+ *   has_in_proj=1: H[0] = X W[0]^T + b[0] (X [M, d_in]); else layer 1 reads X (widths[0]=d_in)
+ *   for l = 1..L: H[l] = ELU(Â (H[l-1] W[l]^T) + b[l]) (CSR rowptr/col/w, self loops in the
+ *   CSR; PyG 2.5.1 GCNConv order: lin, then propagate, then bias).  W, b, H: host arrays of
+ *   L+1 device pointers; widths[l] = output width of layer l. All widths and d_in <= 128,
+ *   multiples of 4; L + 1 <= 8.
+ *   tile_open (required when L >= 1): only tiles with tile_open[t] == 0 are computed — their
+ *   CSR entries stay inside the tile and number at most 1024 (lgnn_graph_build /
+ *   lgnn_tile_open flags); run the others with lgnn_node_linear_fwd_tiles(..., tile_open, 1).
  * ------------------------------------------------------------------------------------------- */
 int lgnn_gcn_stack_fwd(const float* X, int64_t M, int d_in, int has_in_proj,
                        const int32_t* rowptr, const int32_t* col, const float* w, int L,
                        const float* const* W, const float* const* b, const int* widths,
-                       float* const* H, float* const* S, const int32_t* tile_open,
-                       void* stream);
+                       float* const* H, const int32_t* tile_open, void* stream);
 /* Tiles: 64 consecutive node rows. open[t] = 1 when an edge joins tile t to another tile (its
- * layers then depend on other tiles, so lgnn_gcn_stack_fwd skips it: tile_open non-NULL). */
+ * layers then depend on other tiles) or when the tile holds more than 1024 CSR entries; the
+ * fused stacks skip open tiles. */
 int lgnn_tile_count(int64_t num_nodes);
 int lgnn_tile_open(const int32_t* rowptr, const int32_t* col, int64_t num_nodes, int32_t* open,
                    void* stream);
@@ -282,10 +283,13 @@ int lgnn_ce_bwd(const float* logits, const int64_t* target, const float* weight,
 
 /* ---------------------------------------------------------------------------------------------
  * Fused GCN layer stack, backward, for the tiles with tile_open[t] == 0 (L = 1 or 2 convs).
- * Replaces: the autograd chain of lgnn_gcn_stack_fwd below the readout — pool broadcast of dP
- * (global_mean/add_pool backward), per conv dZ = dH * ELU'(H), dW += dZ^T S, dS = dZ W, dH =
- * Â^T dS, and dW_0 += dZ_0^T X for in_proj — with every intermediate on chip.
- *   W, H, S: host arrays of L+1 device pointers (H[0] unused; S[0] = X, S[l] = saved Â H[l-1]);
+ * Replaces: the autograd chain below the readout of in_proj -> L x ELU(GCNConv) — pool broadcast
+ * of dP (global_mean/add_pool backward), per conv G = Â^T dZ, dW += G^T H_{l-1}, dH = G W,
+ * dZ = dH * ELU'(H) (PyG 2.5.1 GCNConv: out = propagate(lin(x)) + bias,
+ * torch_geometric/nn/conv/gcn_conv.py) and dW_0 += dZ_0^T X for in_proj — with every
+ * intermediate on chip.
+ *   rowptr/col/w: the forward (target-row) CSR of lgnn_graph_build;
+ *   W, H: host arrays of L+1 device pointers (H[l] = output of layer l, H[0] = in_proj output);
  *   widths[0..L+1] = d_in, h_0, ..., h_L; dWp/dbp: per-layer partial slabs with num_partials =
  *   lgnn_gcn_stack_bwd_partials(M) slots (reduce with lgnn_reduce_partials[_multi]).
  * Tiles with tile_open[t] != 0 are left to lgnn_node_linear_bwd_tiles(..., want_open = 1,
@@ -293,11 +297,10 @@ int lgnn_ce_bwd(const float* logits, const int64_t* target, const float* weight,
  * ------------------------------------------------------------------------------------------- */
 int lgnn_gcn_stack_bwd_partials(int64_t num_nodes);
 int lgnn_gcn_stack_bwd(const float* dP, const int64_t* batch, const int32_t* gptr, int pool_mean,
-                       const int32_t* tptr, const int32_t* tidx, const float* tw, int64_t M,
-                       int L, const float* const* W, const float* const* H,
-                       const float* const* S, const int* widths, float* const* dWp,
-                       float* const* dbp, int num_partials, const int32_t* tile_open,
-                       void* stream);
+                       const int32_t* rowptr, const int32_t* col, const float* w, const float* X,
+                       int64_t M, int L, const float* const* W, const float* const* H,
+                       const int* widths, float* const* dWp, float* const* dbp, int num_partials,
+                       const int32_t* tile_open, void* stream);
 
 #ifdef __cplusplus
 }

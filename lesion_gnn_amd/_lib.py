@@ -42,7 +42,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_node_linear_bwd_tiles": (I32, [I32, P, P, P, I32, P, P, P, F32, P, I32, P, I64, I32,
                                          P, P, P, F32, P, I32, P, P, P, I32, P, I32, I32, P]),
     "lgnn_gcn_stack_bwd_partials": (I32, [I64]),
-    "lgnn_gcn_stack_bwd": (I32, [P, P, P, I32, P, P, P, I64, I32, P, P, P, P, P, P, I32, P, P]),
+    "lgnn_gcn_stack_bwd": (I32, [P, P, P, I32, P, P, P, P, I64, I32, P, P, P, P, P, I32, P, P]),
     "lgnn_spmm": (I32, [P, P, P, F32, P, I64, I32, P, P]),
     "lgnn_reduce_partials_multi": (I32, [I32, P, P, P, P, P]),
     "lgnn_ce_fwd": (I32, [P, P, P, I64, I32, P, P, P, P, P]),
@@ -60,7 +60,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_gat_bwd_edge": (I32, [P, P, P, P, P, P, P, P, P, I32, I64, I32, I32, F32, P, P, P, P]),
     "lgnn_gat_bwd_num_partials": (I32, [I64]),
     "lgnn_gat_bwd_node": (I32, [P, P, P, P, P, P, P, P, P, P, P, I64, I32, I32, P, P, I32, P]),
-    "lgnn_gcn_stack_fwd": (I32, [P, I64, I32, I32, P, P, P, I32, P, P, P, P, P, P, P]),
+    "lgnn_gcn_stack_fwd": (I32, [P, I64, I32, I32, P, P, P, I32, P, P, P, P, P, P]),
     "lgnn_tile_count": (I32, [I64]),
     "lgnn_tile_open": (I32, [P, P, I64, P, P]),
     "lgnn_node_linear_fwd_tiles": (I32, [P, I64, I32, P, P, P, F32, P, P, I32, I32, P, P, P, I32,

@@ -17,9 +17,10 @@
 #include <cstdlib>
 #include <type_traits>
 
-// Timing-only ablation builds (tools/ablate.py): -DLGNN_ABLATE=<mask> removes phases of the tile
-// kernels (1 MFMA, 2 aggregation, 4 global stores, 16 global row loads). The product build is
-// mask 0; ablated libraries are built outside the package and never loaded by it.
+// Timing-only ablation builds (tools/ablate.py, tools/stamps.py): -DLGNN_ABLATE=<mask> removes
+// phases of the tile kernels (1 MFMA, 2 aggregation, 4 global stores, 8 ELU, 16 global row loads,
+// 64 dense-adjacency build). The product build is mask 0; ablated libraries are built outside
+// the package and never loaded by it.
 #ifndef LGNN_ABLATE
 #define LGNN_ABLATE 0
 #endif
@@ -31,8 +32,12 @@ __device__ unsigned long long lgnn_stamp_buf[1024 * 64];
 #define STAMP(k)                                                                   \
   do {                                                                             \
     const int _k = (k);                                                            \
-    if (threadIdx.x == 0 && _k < 64)                                               \
+    if (threadIdx.x == 0 && _k < 62)                                               \
       lgnn_stamp_buf[blockIdx.x * 64 + _k] = __builtin_amdgcn_s_memtime();         \
+    if (threadIdx.x == 0 && _k == 0) {  /* placement: HW_ID, XCC_ID */             \
+      lgnn_stamp_buf[blockIdx.x * 64 + 62] = __builtin_amdgcn_s_getreg(4 | (31 << 11));  \
+      lgnn_stamp_buf[blockIdx.x * 64 + 63] = __builtin_amdgcn_s_getreg(20 | (31 << 11)); \
+    }                                                                              \
   } while (0)
 #else
 #define STAMP(k) \
@@ -179,6 +184,31 @@ __device__ __forceinline__ void idx_store(TileIdx& ti, bool& staged, const IdxRe
       if (j < R.ne) ti.ow[j] = make_int2((R.c[u] - (int)r0) * LDS, __float_as_int(R.w[u]));
     }
     if (tid < EB) ti.ow[R.ne + tid] = make_int2(0, 0);
+  }
+}
+
+// Dense Â_tile from the tile's row-CSR block (entry j of R: source R.c, weight R.w; its target
+// row found by binary search over rp): Adj[target][source] (TRANS = false) or Adj[source][target]
+// (TRANS = true), row stride TM. Adj must be zero and rp visible. Duplicate (target, source)
+// pairs carry equal weights, so the LDS float adds are order independent.
+template <bool TRANS, int NTH>
+__device__ __forceinline__ void adj_scatter(float* Adj, const int* rp, const IdxRegsT<NTH>& R,
+                                            int64_t r0) {
+#pragma unroll
+  for (int u = 0; u < CAPE / NTH; ++u) {
+    const int j = threadIdx.x + u * NTH;
+    if (j < R.ne) {
+      const int e = R.eb + j;
+      int lo = 0, hi = TM;
+#pragma unroll
+      for (int it = 0; it < 6; ++it) {
+        const int mid = (lo + hi) >> 1;
+        if (rp[mid] <= e) lo = mid;
+        else hi = mid;
+      }
+      const int c = R.c[u] - (int)r0;
+      atomicAdd(&Adj[TRANS ? c * TM + lo : lo * TM + c], R.w[u]);
+    }
   }
 }
 
@@ -599,7 +629,6 @@ struct StackArgs {
   const float* W[LGNN_MAX_STACK];
   const float* b[LGNN_MAX_STACK];
   float* H[LGNN_MAX_STACK];
-  float* S[LGNN_MAX_STACK];
   int width[LGNN_MAX_STACK + 1];  // width[0] = input width, width[l+1] = output of layer l
 };
 
@@ -619,6 +648,24 @@ __device__ __forceinline__ void load_bfrag(float (&bf)[64], const float* __restr
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Fused GCN stack forward, for the tiles no edge leaves: in_proj + L x ELU(GCNConv) in one
+// launch, the tile on chip between layers. PyG's association (GCNConv: lin, then propagate):
+//   H_0 = X W_0^T + b_0;   H_l = ELU(Â_tile (H_{l-1} W_l^T) + b_l)
+// Â_tile is staged dense in LDS (transposed, 64 x 64, from the tile's CSR block), so the
+// aggregation is an MFMA product. 4 waves, 2 workgroups per CU (one's MFMAs overlap the
+// other's stores and barriers); wave w owns output columns [32w, 32w + 32) of all 64 rows (two
+// 32x32 accumulators). Per layer: P = A W^T (A = H_{l-1} image, W fragment in registers,
+// loaded a layer ahead) -> A; Z = Â P -> epilogue -> A (next layer's input) and HBM (H_l, rows
+// staged through LDS and written as whole rows). Only the H_l are written: the backward uses
+// G = Â^T dZ, dW = G^T H_{l-1} (k_stack_bwd), so no aggregated input is saved.
+// ------------------------------------------------------------------------------------------
+struct FwdSmem {
+  float A[TM * LDS];
+  float AdjT[TM * TM];  // Â_tile[source][target]
+  int rp[TM + 1];
+};
+
 template <bool FIRST>
 __global__ __launch_bounds__(NT, 2) void k_stack_fwd(const float* __restrict__ X, int64_t M,
                                                      const int32_t* __restrict__ rowptr,
@@ -626,20 +673,28 @@ __global__ __launch_bounds__(NT, 2) void k_stack_fwd(const float* __restrict__ X
                                                      const float* __restrict__ w, int L,
                                                      StackArgs args,
                                                      const int32_t* __restrict__ tmask) {
-  __shared__ __attribute__((aligned(16))) float A[TM * LDS];
-  __shared__ __attribute__((aligned(16))) float S[TM * LDS];
-  __shared__ TileIdx ti;
+  __shared__ __attribute__((aligned(16))) FwdSmem sm;
+  float* const A = sm.A;
+  float* const AdjT = sm.AdjT;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int h = lane >> 5, li = lane & 31, hw = wave * 2 + h;
+  const int h = lane >> 5, li = lane & 31, hw = tid >> 5;
   const int64_t ntiles = (M + TM - 1) / TM;
   const int n = wave * 32 + li;
   const int l0 = FIRST ? 0 : 1;
-  const int K0 = args.width[FIRST ? 0 : 1];
+  const int K0 = args.width[l0];
 
   [[maybe_unused]] int stamp = 0;
   STAMP(stamp++);
   int64_t t = seek_tile(blockIdx.x, ntiles, tmask, 0);
   if (t >= ntiles) return;
+#ifdef LGNN_DESYNC
+#ifndef LGNN_DESYNC_PRED
+#define LGNN_DESYNC_PRED (blockIdx.x & 1)
+#endif
+  // diagnostic: one workgroup of each CU pair starts late
+  if (LGNN_DESYNC_PRED)
+    for (int i = 0; i < LGNN_DESYNC; ++i) __builtin_amdgcn_s_sleep(1);
+#endif
   f32x4 xr[8];
   IdxRegs R;
   float bf[64];
@@ -648,109 +703,145 @@ __global__ __launch_bounds__(NT, 2) void k_stack_fwd(const float* __restrict__ X
   load_rows(xr, bX, K0, (int)(t * TM));
   if (any_conv) idx_load_head(R, rowptr, M, t * TM);
   load_bfrag(bf, args.W[l0], args.width[l0 + 1], args.width[l0]);
+  // bias of the layer whose fragment is in bf (loaded with it, a layer ahead of its use)
+  float bias = n < args.width[l0 + 1] ? args.b[l0][n] : 0.f;
   if (any_conv) idx_load_body(R, col, w);
-  for (; t < ntiles; t = seek_tile(t + gridDim.x, ntiles, tmask, 0)) {
+  for (; t < ntiles;) {
     const int64_t r0 = t * TM;
     const int64_t tn = seek_tile(t + gridDim.x, ntiles, tmask, 0);
     const bool has_next = tn < ntiles;
-    bool staged = true;
     store_rows_lds(A, xr, M, K0, r0);
-    if (any_conv) idx_store(ti, staged, R, r0);
+    if (any_conv) {
+      for (int i = tid; i < TM * TM / 4; i += NT) st4(AdjT + 4 * i, zero4());
+      if (tid <= TM) sm.rp[tid] = R.rp;
+    }
     __syncthreads();
     STAMP(stamp++);
+    if (any_conv && !(ABL & 64)) adj_scatter<true>(AdjT, sm.rp, R, r0);
     if (has_next) {
       load_rows(xr, bX, K0, (int)(tn * TM));
       if (any_conv) idx_load_head(R, rowptr, M, tn * TM);
     }
     for (int l = l0; l <= L; ++l) {
-      const int K = args.width[l], N = args.width[l + 1];
+      const int N = args.width[l + 1];
       const bool conv = l > 0;
-      const float* Ain = conv ? S : A;
-      if (conv) {
-        const int kc = 4 * li < K ? 4 * li : K - 4;
-        auto agg_tile = [&](auto staged_tag) {
-          constexpr bool STG = decltype(staged_tag)::value;
-#pragma unroll LGNN_AGG_UNROLL
-          for (int it = 0; it < 8; ++it) {
-            const int rr = hw + 8 * it;
-            f32x4 a = STG ? agg_row_local(ti, rr, A)
-                          : agg_row_global(ti, rr, args.H[l - 1], K, kc, col, w);
-            a = sel4(4 * li < K && r0 + rr < M, a);
-            st4(S + rr * LDS + 4 * li, a);
-            if (4 * li < K) bst4(mkbuf(args.S[l], M * K * 4), (int)((r0 + rr) * K + 4 * li) * 4, a);
-          }
-        };
-        if (staged) agg_tile(std::true_type{});
-        else agg_tile(std::false_type{});
-        if (l == 1 && has_next) idx_load_body(R, col, w);  // the head has landed by now
-        __syncthreads();
-        STAMP(stamp++);
-      }
+      // P = A W_l^T (A = X or H_{l-1} image); wave: columns n, rows li (acc0) and 32 + li (acc1)
       f32x16 acc0 = {}, acc1 = {};
-      if (wave * 32 < N) {
+      if (wave * 32 < N && !(ABL & 1)) {
+        const float* ap = A + li * LDS + 64 * h;
+        f32x4 a0 = ld4(ap), a1 = ld4(ap + 32 * LDS);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-          const f32x4 a0 = ld4(Ain + li * LDS + 64 * h + 4 * q);
-          const f32x4 a1 = ld4(Ain + (32 + li) * LDS + 64 * h + 4 * q);
+          const int nx = q + 1 < 16 ? q + 1 : q;
+          const f32x4 b0 = ld4(ap + 4 * nx), b1 = ld4(ap + 32 * LDS + 4 * nx);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             acc0 = mfma32(a0[j], bf[4 * q + j], acc0);
             acc1 = mfma32(a1[j], bf[4 * q + j], acc1);
           }
+          a0 = b0;
+          a1 = b1;
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
         }
       }
-      STAMP(stamp++);
       // next layer's weight fragment (or the first layer's, for the next tile)
       const int lnext = l < L ? l + 1 : l0;
-      if (l < L || has_next)
+      const float bias_l = bias;
+      if (l < L || has_next) {
         load_bfrag(bf, args.W[lnext], args.width[lnext + 1], args.width[lnext]);
-      __syncthreads();  // every wave is done reading A / S
+        bias = n < args.width[lnext + 1] ? args.b[lnext][n] : 0.f;
+      }
+      if (l == l0 && any_conv && has_next) idx_load_body(R, col, w);  // head has landed
+      __syncthreads();  // every wave is done reading A
       STAMP(stamp++);
-      const float bias = n < N ? args.b[l][n] : 0.f;
+      if (conv) {
+        // P -> A, then Z = Â P: Z[m][n] = sum_j AdjT[j][m] P[j][n]
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
+          A[rl * LDS + n] = n < N ? acc0[r] : 0.f;
+          A[(32 + rl) * LDS + n] = n < N ? acc1[r] : 0.f;
+        }
+        __syncthreads();
+        if (!(ABL & 2)) {
+          acc0 = f32x16{};
+          acc1 = f32x16{};
+        }
+        if (wave * 32 < N && !(ABL & 2)) {
+          const float* jp = AdjT + h * TM + li;
+          const float* pp = A + h * LDS + n;
+          float m0 = jp[0], m1 = jp[32], pv = pp[0];
+          __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+#pragma unroll
+          for (int s2 = 0; s2 < TM / 2; ++s2) {
+            const int nx = s2 + 1 < TM / 2 ? s2 + 1 : s2;
+            const float n0 = jp[2 * nx * TM], n1 = jp[2 * nx * TM + 32], pn = pp[2 * nx * LDS];
+            acc0 = mfma32(m0, pv, acc0);
+            acc1 = mfma32(m1, pv, acc1);
+            m0 = n0;
+            m1 = n1;
+            pv = pn;
+            __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+          }
+        }
+        __syncthreads();  // every wave is done reading P
+        STAMP(stamp++);
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
-        float v0 = acc0[r] + bias, v1 = acc1[r] + bias;
-        if (conv) {
+        float v0 = acc0[r] + bias_l, v1 = acc1[r] + bias_l;
+        if (conv && !(ABL & 8)) {
           v0 = elu_f(v0);
           v1 = elu_f(v1);
         }
-        if (n < N) {
-          A[rl * LDS + n] = v0;
-          A[(32 + rl) * LDS + n] = v1;
-        }
+        A[rl * LDS + n] = n < N ? v0 : 0.f;
+        A[(32 + rl) * LDS + n] = n < N ? v1 : 0.f;
       }
+      STAMP(stamp++);
       __syncthreads();
-      if (4 * li < N) {
+      STAMP(stamp++);
+      if (4 * li < N && !(ABL & 4)) {
+        const Buf hb = mkbuf(args.H[l], M * N * 4);
 #pragma unroll
         for (int it = 0; it < 8; ++it) {
           const int rr = hw + 8 * it;
-          bst4(mkbuf(args.H[l], M * N * 4), (int)((r0 + rr) * N + 4 * li) * 4,
-               ld4(A + rr * LDS + 4 * li));
+          bst4(hb, (int)((r0 + rr) * N + 4 * li) * 4, ld4(A + rr * LDS + 4 * li));
         }
       }
-      // A now holds H_l (zero beyond N) for the next layer's aggregation
-      if (l == L) __syncthreads();
       STAMP(stamp++);
+      // A now holds H_l (zero beyond N) for the next layer; its next writer comes after a
+      // barrier (the next layer's MFMA) or the tile-end barrier below
     }
+    __syncthreads();
+    t = tn;
   }
 }
 // ------------------------------------------------------------------------------------------
-// Fused layer stack, backward, for the tiles no edge leaves (the forward's k_stack_fwd tiles):
-// from the pooled-output gradient dP down to the in_proj weights in one launch, the tile on chip
+// Fused GCN stack backward, for the tiles no edge leaves (the forward's k_stack_fwd tiles): from
+// the pooled-output gradient dP down to the in_proj weights in one launch, the tile on chip.
+// Autograd's own association for GCNConv (out = Â (H W^T) + b, PyG order):
 //   dZ_L = dP[g(i)] (/ count) * ELU'(H_L)
-//   for l = L..1:  dW_l += dZ_l^T S_l, db_l += colsum dZ_l, dS_l = dZ_l W_l,
-//                  dZ_{l-1} = (Â^T dS_l) * ELU'(H_{l-1})   (no ELU' below the first conv)
+//   for l = L..1:  db_l += colsum dZ_l;  G = Â^T dZ_l;  dW_l += G^T H_{l-1};
+//                  dZ_{l-1} = (G W_l) * ELU'(H_{l-1})   (no ELU' below the first conv)
 //   dW_0 += dZ_0^T X, db_0 += colsum dZ_0
-// One workgroup per CU (4 waves, one per SIMD, up to 512 registers each): the NL layers' dW
-// accumulators stay in registers across the workgroup's tiles and are written once, as partial
-// slot blockIdx.x of each layer's slab. The next rows (S_{l-1}, H_{l-1}, or the next tile's
-// S_L, H_L, pool gradient and CSR block) are prefetched into registers while the MFMAs run.
+// 512 threads = 8 waves, one workgroup per CU (two waves per SIMD hide each other's latency).
+// Â of the tile is staged dense in LDS (64 x 64, built from the tile's CSR block by scattered
+// LDS adds), so the aggregation is an MFMA product instead of a latency-bound gather.
+// LDS: C = dZ_l / G, A = the H_{l-1} (or X) image, Wl = W_l (unpadded [o][k], filled by
+// direct-to-LDS buffer loads a phase ahead, so the weight costs no registers), Adj = Â_tile.
+// Work split per wave w (q = w & 3, r2 = w >> 2): dW_l block dW[32q..+32][64r2..+64] (two 32x32
+// accumulators per layer, resident over all the workgroup's tiles, written once as partial slot
+// blockIdx.x); G block rows 32r2.., columns 32q..; (G W_l)^T block k in [32q, +32), m in
+// [32r2, +32). db: per-wave column partials in LDS, reduced in a fixed order at the end.
 // ------------------------------------------------------------------------------------------
 struct StackBwdArgs {
   const float* W[LGNN_MAX_STACK];
-  const float* H[LGNN_MAX_STACK];  // H[l], l >= 1: the conv's ELU output (for ELU')
-  const float* S[LGNN_MAX_STACK];  // dW operand: S[l] = Â H[l-1] (l >= 1), S[0] = X
+  const float* H[LGNN_MAX_STACK];  // H[l]: output of layer l (H[0] = in_proj output)
+  const float* X;                  // model input (in_proj dW operand)
   float* dWp[LGNN_MAX_STACK];      // [P][N_l][K_l]
   float* dbp[LGNN_MAX_STACK];      // [P][N_l]
   int width[LGNN_MAX_STACK + 1];   // width[l] = input width of layer l, width[l+1] = output
@@ -788,26 +879,6 @@ __device__ __forceinline__ f32x4 pool_scale(f32x4 v, int cnt) {
   return cnt > 1 ? v / (float)cnt : v;
 }
 
-// ------------------------------------------------------------------------------------------
-// Fused GCN stack backward (closed tiles), 512 threads = 8 waves, one workgroup per CU (two
-// waves per SIMD hide each other's LDS / L2 latency). Per tile, all on chip:
-//   dZ_L = pool-broadcast(dP) * ELU'(H_L)
-//   for l = L..0:  dW_l += dZ_l^T S_l,  db_l += colsum(dZ_l)
-//                  (l >= 1) dS_l = dZ_l W_l;  dZ_{l-1} = (Â^T dS_l) [* ELU'(H_{l-1}) if l >= 2]
-// LDS: C = dZ_l, A = S_l then dS_l (padded rows), Wl = W_l (unpadded [o][k], filled by
-// direct-to-LDS buffer loads issued before the dW MFMAs, so the weight costs no registers),
-// ti = the tile's transposed CSR block.
-// Work split: dW_l — wave (wo = w & 3, wk = w >> 2) owns dW[32wo..+32][64wk..+64] (two 32x32
-// accumulators per layer, resident over all the workgroup's tiles); dS_l^T = W_l^T dZ_l^T —
-// wave (kb = w & 3, mb = w >> 2) owns the 32x32 block k in [32kb, +32), m in [32mb, +32).
-// db: per-thread column partials, reduced over the 16 row groups at the end.
-// ------------------------------------------------------------------------------------------
-#ifndef LGNN_BWD_EB
-#define LGNN_BWD_EB 2
-#endif
-#ifndef LGNN_AGG_ROWS
-#define LGNN_AGG_ROWS 1
-#endif
 constexpr int NTB = 512;
 constexpr int RPB = TM / (NTB / 32);  // rows per thread (4)
 
@@ -845,15 +916,16 @@ __device__ __forceinline__ void stage_w_lds(float* Wl, const float* W, int N, in
   }
 }
 
-// LDS image of k_stack_bwd. A and C first: every row access then fits the 16-bit immediate
-// offset of ds_read/ds_write (no per-access address VALU).
+// LDS image of k_stack_bwd (162 KB for three layers). A and C first: every row access then
+// fits the 16-bit immediate offset of ds_read/ds_write (no per-access address VALU).
 template <int NL>
 struct BwdSmem {
   float A[TM * LDS];
   float C[TM * LDS];
-  TileIdx ti;
-  float Db[NL][NTB / 64][KC];  // db partials per wave, column
   float Wl[KC * KC];
+  float Adj[TM * TM];          // Â_tile[target][source]
+  float Db[NL][NTB / 64][KC];  // db partials per wave, column
+  int rp[TM + 1];
 };
 
 template <int NL>
@@ -861,9 +933,9 @@ __global__ __launch_bounds__(NTB, 1) void k_stack_bwd(const float* __restrict__ 
                                                       const int64_t* __restrict__ batch,
                                                       const int32_t* __restrict__ gptr,
                                                       int pool_mean,
-                                                      const int32_t* __restrict__ tptr,
-                                                      const int32_t* __restrict__ tidx,
-                                                      const float* __restrict__ tw, int64_t M,
+                                                      const int32_t* __restrict__ rowptr,
+                                                      const int32_t* __restrict__ col,
+                                                      const float* __restrict__ w, int64_t M,
                                                       StackBwdArgs a,
                                                       const int32_t* __restrict__ tmask) {
   constexpr int L = NL - 1;
@@ -871,11 +943,11 @@ __global__ __launch_bounds__(NTB, 1) void k_stack_bwd(const float* __restrict__ 
   float* const A = sm.A;
   float* const C = sm.C;
   float* const Wl = sm.Wl;
-  TileIdx& ti = sm.ti;
+  float* const Adj = sm.Adj;
   auto& Db = sm.Db;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, li = lane & 31, hw = tid >> 5;
-  const int wq = wave & 3, wr2 = wave >> 2;  // (wo, wk) for dW; (kb, mb) for dS
+  const int wq = wave & 3, wr2 = wave >> 2;
   const int64_t ntiles = (M + TM - 1) / TM;
 
   f32x16 dw[NL][2];
@@ -885,6 +957,7 @@ __global__ __launch_bounds__(NTB, 1) void k_stack_bwd(const float* __restrict__ 
     dw[l][1] = f32x16{};
   }
   for (int i = tid; i < NL * (NTB / 64) * KC; i += NTB) (&Db[0][0][0])[i] = 0.f;
+  for (int i = tid; i < TM * TM / 4; i += NTB) st4(Adj + 4 * i, zero4());
   // db partials: the two half-waves' column sums combined, added into the wave's LDS row by
   // the lane that owns those 4 columns (no other thread touches them until the end)
   auto db_flush = [&](int l, f32x4 v) {
@@ -895,6 +968,16 @@ __global__ __launch_bounds__(NTB, 1) void k_stack_bwd(const float* __restrict__ 
       st4(d, ld4(d) + v);
     }
   };
+  // column sums of this thread's rows of C = dZ_l (row mapping of load_rows)
+  auto db_from_c = [&](int l) {
+    f32x4 v = zero4();
+#pragma unroll
+    for (int it = 0; it < RPB; ++it) v += ld4(C + (hw + (TM / RPB) * it) * LDS + 4 * li);
+    db_flush(l, v);
+  };
+  // image rows of layer l's dW operand: H_{l-1}, or X for in_proj
+  auto img_ptr = [&](int l) { return l >= 1 ? a.H[l - 1] : a.X; };
+
   f32x4 hv[RPB], sr[RPB], gv[RPB];
   int gi[RPB], cnt[RPB];
   IdxRegsT<NTB> R;
@@ -903,9 +986,9 @@ __global__ __launch_bounds__(NTB, 1) void k_stack_bwd(const float* __restrict__ 
     pool_ids(gi, batch, M, t * TM);
     pool_rows(gv, cnt, gi, dP, gptr, pool_mean, a.width[L + 1]);
     load_rows_d(hv, a.H[L], M, a.width[L + 1], t * TM);
-    load_rows_d(sr, a.S[L], M, a.width[L], t * TM);
-    idx_load_head(R, tptr, M, t * TM);
-    idx_load_body(R, tidx, tw);
+    load_rows_d(sr, img_ptr(L), M, a.width[L], t * TM);
+    idx_load_head(R, rowptr, M, t * TM);
+    idx_load_body(R, col, w);
     stage_w_lds(Wl, a.W[L], a.width[L + 1], a.width[L]);
   }
   [[maybe_unused]] int stamp = 0;
@@ -914,8 +997,9 @@ __global__ __launch_bounds__(NTB, 1) void k_stack_bwd(const float* __restrict__ 
     const int64_t r0 = t * TM;
     const int64_t tn = seek_tile(t + gridDim.x, ntiles, tmask, 0);
     const bool has_next = tn < ntiles;
-    bool staged = true;
-    idx_store(ti, staged, R, r0);  // ends with a barrier; closed tiles are always local
+    if (tid <= TM) sm.rp[tid] = R.rp;
+    __syncthreads();  // rp visible, Adj zero
+    adj_scatter<false>(Adj, sm.rp, R, r0);
     {
       const int N = a.width[L + 1];
       f32x4 dsum = zero4();
@@ -931,42 +1015,56 @@ __global__ __launch_bounds__(NTB, 1) void k_stack_bwd(const float* __restrict__ 
       }
       db_flush(L, dsum);
     }
+    store_rows_lds(A, sr, M, a.width[L], r0);
+    __builtin_amdgcn_s_waitcnt(0);  // W_L staged a phase ago
+    __syncthreads();
+    STAMP(stamp++);
 #pragma unroll
-    for (int l = L; l >= 0; --l) {
-      const int K = a.width[l];
-      store_rows_lds(A, sr, M, K, r0);
-      // W_l was staged a phase earlier; this wave's share has landed once vmcnt drains (the
-      // row loads issued since have been consumed), the barrier publishes every wave's share
-      __builtin_amdgcn_s_waitcnt(0);
+    for (int l = L; l >= 1; --l) {
+      const int N = a.width[l + 1], K = a.width[l];
+      if (l < L) db_from_c(l);
+      // prefetch: the next image (H_{l-2} or X); at l = 1 also the next tile's graph ids and
+      // CSR head (no load waits on another in front of the MFMAs)
+      load_rows_d(sr, img_ptr(l - 1), M, a.width[l - 1], r0);
+      if (l == 1 && has_next) {
+        pool_ids(gi, batch, M, tn * TM);
+        idx_load_head(R, rowptr, M, tn * TM);
+      }
+      // G[m][n] = sum_i Â[i][m] dZ[i][n]; wave block m in [32 r2, +32), n in [32q, +32)
+      f32x16 g = {};
+      {
+        const float* ap = Adj + h * TM + 32 * wr2 + li;
+        const float* cp = C + h * LDS + 32 * wq + li;
+        float av = ap[0], cv = cp[0];
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+        for (int s2 = 0; s2 < TM / 2; ++s2) {
+          const int nx = s2 + 1 < TM / 2 ? s2 + 1 : s2;
+          const float an = ap[2 * nx * TM], cn = cp[2 * nx * LDS];
+          g = mfma32(av, cv, g);
+          av = an;
+          cv = cn;
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
+      }
+      __syncthreads();  // every wave is done reading dZ_l
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = 32 * wr2 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        C[m * LDS + 32 * wq + li] = 32 * wq + li < N ? g[r] : 0.f;
+      }
+      __builtin_amdgcn_s_waitcnt(0);  // W_l (staged a phase ago) has landed
       __syncthreads();
       STAMP(stamp++);
-      // prefetch what the next phase needs. The next tile's loads are split over the last two
-      // phases so that no load waits on another in front of the MFMAs: graph ids and CSR
-      // head at l = 1, then the rows, the CSR body and W_L (Wl is free since l = 1's DX) at 0.
-      if (l >= 1) {
-        if (l >= 2)
-          load_rows_d(hv, a.H[l - 1], M, a.width[l], r0);
-        load_rows_d(sr, a.S[l - 1], M, a.width[l - 1], r0);
-        if (l == 1 && has_next) {
-          pool_ids(gi, batch, M, tn * TM);
-          idx_load_head(R, tptr, M, tn * TM);
-        }
-      } else if (has_next) {
-        pool_rows(gv, cnt, gi, dP, gptr, pool_mean, a.width[L + 1]);
-        load_rows_d(hv, a.H[L], M, a.width[L + 1], tn * TM);
-        load_rows_d(sr, a.S[L], M, a.width[L], tn * TM);
-        idx_load_body(R, tidx, tw);
-        stage_w_lds(Wl, a.W[L], a.width[L + 1], a.width[L]);
-      }
-      // dW_l[o][k] += sum_m dZ[m][o] S[m][k], m = 2 s2 + h. Accumulator j holds the columns
-      // k = 64 wk + 2 li + j, so a lane's two B operands are one ds_read_b64. Operands of step
-      // s2 + 1 are read before the MFMAs of step s2 are issued.
+      // dW_l[o][k] += sum_m G[m][o] H_{l-1}[m][k], m = 2 s2 + h. Accumulator j holds the
+      // columns k = 64 wk + 2 li + j, so a lane's two B operands are one ds_read_b64.
       {
         const float* cp = C + h * LDS + 32 * wq + li;
         const float* ap = A + h * LDS + 64 * wr2 + 2 * li;
         float a0 = cp[0];
         float2 b = *reinterpret_cast<const float2*>(ap);
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // step 0 operands
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
 #pragma unroll
         for (int s2 = 0; s2 < TM / 2; ++s2) {
           const int nx = (s2 + 1 < TM / 2 ? s2 + 1 : s2) * 2 * LDS;
@@ -976,17 +1074,11 @@ __global__ __launch_bounds__(NTB, 1) void k_stack_bwd(const float* __restrict__ 
           dw[l][1] = mfma32(a0, b.y, dw[l][1]);
           a0 = a1;
           b = bn;
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS reads of step s2 + 1
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // MFMAs of step s2
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
         }
       }
-      if (l == 0) {
-        __syncthreads();  // A / C free for the next tile
-        STAMP(stamp++);
-        continue;
-      }
-      STAMP(stamp++);
-      // dS_l^T[k][m] = sum_o W_l[o][k] dZ[m][o]; half h contracts o in [64h, 64h + 64)
+      // (G W_l)^T[k][m] = sum_o W_l[o][k] G[m][o]; half h contracts o in [64h, 64h + 64)
       f32x16 x = {};
       {
         const float* wp = Wl + 64 * h * KC + 32 * wq + li;
@@ -1012,37 +1104,65 @@ __global__ __launch_bounds__(NTB, 1) void k_stack_bwd(const float* __restrict__ 
           __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
         }
       }
-      __syncthreads();  // every wave is done reading A (S_l), C (dZ_l) and Wl
       STAMP(stamp++);
-      if (l >= 2) stage_w_lds(Wl, a.W[l - 1], a.width[l], a.width[l - 1]);
+      // dZ_{l-1} = (G W_l) * ELU'(H_{l-1}) at (m = 32 r2 + li, k = 32q + 8g + 4h + 0..3); the
+      // H_{l-1} values come from the A image
+      f32x4 dz[4];
       {
-        float* ap = A + (32 * wr2 + li) * LDS + 32 * wq + 4 * h;
+        const float* hp = A + (32 * wr2 + li) * LDS + 32 * wq + 4 * h;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int k = 32 * wq + 8 * g + 4 * h;
-          st4(ap + 8 * g, sel4(k < K, f32x4{x[4 * g], x[4 * g + 1], x[4 * g + 2], x[4 * g + 3]}));
+        for (int g4 = 0; g4 < 4; ++g4) {
+          f32x4 v = f32x4{x[4 * g4], x[4 * g4 + 1], x[4 * g4 + 2], x[4 * g4 + 3]};
+          if (l >= 2) {
+            const f32x4 hh = ld4(hp + 8 * g4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] *= elu_grad_from_out(hh[j]);
+          }
+          dz[g4] = sel4(32 * wq + 8 * g4 + 4 * h < K && r0 + 32 * wr2 + li < M, v);
         }
       }
-      __syncthreads();
-      STAMP(stamp++);
-      // dZ_{l-1} = (Â^T dS_l) * ELU'(H_{l-1}); in_proj (l - 1 = 0) has no activation
-      f32x4 dsum = zero4();
-#pragma unroll LGNN_AGG_ROWS
-      for (int it = 0; it < RPB; ++it) {
-        const int rr = hw + (TM / RPB) * it;
-        f32x4 g = agg_row_local<LGNN_BWD_EB>(ti, rr, A);
-        if (l >= 2) {
+      __syncthreads();  // every wave is done reading A (H_{l-1}), C (G) and Wl
+      {
+        float* cp = C + (32 * wr2 + li) * LDS + 32 * wq + 4 * h;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) g[j] *= elu_grad_from_out(hv[it][j]);
-        }
-        g = sel4(4 * li < K && r0 + rr < M, g);
-        dsum += g;
-        st4(C + rr * LDS + 4 * li, g);
+        for (int g4 = 0; g4 < 4; ++g4) st4(cp + 8 * g4, dz[g4]);
       }
-      db_flush(l - 1, dsum);
+      store_rows_lds(A, sr, M, a.width[l - 1], r0);
+      if (l >= 2) stage_w_lds(Wl, a.W[l - 1], a.width[l], a.width[l - 1]);
       __syncthreads();
       STAMP(stamp++);
     }
+    // in_proj: dW_0 += dZ_0^T X; the next tile's loads go out first
+    db_from_c(0);
+    if (has_next) {
+      pool_rows(gv, cnt, gi, dP, gptr, pool_mean, a.width[L + 1]);
+      load_rows_d(hv, a.H[L], M, a.width[L + 1], tn * TM);
+      load_rows_d(sr, img_ptr(L), M, a.width[L], tn * TM);
+      idx_load_body(R, col, w);
+      stage_w_lds(Wl, a.W[L], a.width[L + 1], a.width[L]);  // Wl is free since l = 1's DX
+    }
+    for (int i = tid; i < TM * TM / 4; i += NTB) st4(Adj + 4 * i, zero4());  // read at l = 1
+    {
+      const float* cp = C + h * LDS + 32 * wq + li;
+      const float* ap = A + h * LDS + 64 * wr2 + 2 * li;
+      float a0 = cp[0];
+      float2 b = *reinterpret_cast<const float2*>(ap);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+      for (int s2 = 0; s2 < TM / 2; ++s2) {
+        const int nx = (s2 + 1 < TM / 2 ? s2 + 1 : s2) * 2 * LDS;
+        const float a1 = cp[nx];
+        const float2 bn = *reinterpret_cast<const float2*>(ap + nx);
+        dw[0][0] = mfma32(a0, b.x, dw[0][0]);
+        dw[0][1] = mfma32(a0, b.y, dw[0][1]);
+        a0 = a1;
+        b = bn;
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      }
+    }
+    __syncthreads();  // A / C free for the next tile
+    STAMP(stamp++);
     t = tn;
   }
   __syncthreads();  // db: the 8 wave partials of each column, summed in a fixed order
@@ -1068,12 +1188,17 @@ __global__ __launch_bounds__(NTB, 1) void k_stack_bwd(const float* __restrict__ 
   }
 }
 
-// open[t] = 1 if an edge joins a node of tile t with a node of another tile (target CSR).
+// open[t] = 1 if an edge joins a node of tile t with a node of another tile (target CSR), or
+// if the tile holds more than CAPE CSR entries.
 __global__ __launch_bounds__(NT) void k_tile_open(const int32_t* __restrict__ rowptr,
                                                   const int32_t* __restrict__ col, int64_t M,
                                                   int32_t* __restrict__ open) {
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < M; i += (int64_t)gridDim.x * NT) {
     const int ti = (int)(i / TM);
+    if (i % TM == 0) {
+      const int64_t ie = i + TM < M ? i + TM : M;
+      if (rowptr[ie] - rowptr[i] > CAPE) open[ti] = 1;
+    }
     const int e0 = rowptr[i], e1 = rowptr[i + 1];
     for (int e = e0; e < e1; ++e) {
       const int tj = col[e] / TM;
@@ -1182,34 +1307,26 @@ extern "C" int lgnn_tile_open(const int32_t* rowptr, const int32_t* col, int64_t
 extern "C" int lgnn_gcn_stack_fwd(const float* X, int64_t M, int d_in, int has_in_proj,
                                   const int32_t* rowptr, const int32_t* col, const float* w,
                                   int L, const float* const* W, const float* const* b,
-                                  const int* widths, float* const* H, float* const* S,
-                                  const int32_t* tile_open, void* stream) {
-  if (M < 0 || L < 0 || L + 1 > LGNN_MAX_STACK || !W || !b || !widths || !H || !S)
-    return LGNN_EINVAL;
-  if (L > 0 && (!rowptr || !col)) return LGNN_EINVAL;
+                                  const int* widths, float* const* H, const int32_t* tile_open,
+                                  void* stream) {
+  if (M < 0 || L < 0 || L + 1 > LGNN_MAX_STACK || !W || !b || !widths || !H) return LGNN_EINVAL;
+  if (L > 0 && (!rowptr || !col || !tile_open)) return LGNN_EINVAL;
   lgnn_tile::StackArgs a = {};
   const int l0 = has_in_proj ? 0 : 1;
   if (l0 > L) return LGNN_EINVAL;
+  if (!has_in_proj && widths[0] != d_in) return LGNN_EINVAL;
   a.width[0] = d_in;
   for (int l = 0; l <= L; ++l) {
     a.width[l + 1] = widths[l];
     if (l < l0) continue;
     const int K = a.width[l], N = a.width[l + 1];
-    if (!lgnn_tile_fits(M, K, N) || !W[l] || !H[l]) return LGNN_EINVAL;
-    if (l > 0 && !S[l]) return LGNN_EINVAL;
+    if (!lgnn_tile_fits(M, K, N) || !W[l] || !b[l] || !H[l]) return LGNN_EINVAL;
     a.W[l] = W[l];
     a.b[l] = b[l];
     a.H[l] = H[l];
-    a.S[l] = l > 0 ? S[l] : nullptr;
   }
-  if (!has_in_proj) {
-    if (widths[0] != d_in) return LGNN_EINVAL;
-    a.H[0] = const_cast<float*>(X);  // the conv stack's input (first aggregation's fallback)
-  }
-  for (int l = l0; l <= L; ++l)
-    if (!a.b[l]) return LGNN_EINVAL;
   if (M == 0) return LGNN_OK;
-  if (M > 0 && !X) return LGNN_EINVAL;
+  if (!X) return LGNN_EINVAL;
   const int64_t ntiles = (M + lgnn_tile::TM - 1) / lgnn_tile::TM;
   dim3 grid((unsigned)(ntiles < 512 ? ntiles : 512));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -1240,24 +1357,23 @@ extern "C" int lgnn_gcn_stack_bwd_partials(int64_t M) {
 }
 
 extern "C" int lgnn_gcn_stack_bwd(const float* dP, const int64_t* batch, const int32_t* gptr,
-                                  int pool_mean, const int32_t* tptr, const int32_t* tidx,
-                                  const float* tw, int64_t M, int L, const float* const* W,
-                                  const float* const* H, const float* const* S,
-                                  const int* widths, float* const* dWp, float* const* dbp,
-                                  int num_partials, const int32_t* tile_open, void* stream) {
-  if (M < 0 || L < 1 || L > 2 || !dP || !batch || !gptr || !tptr || !tidx || !W || !H || !S ||
+                                  int pool_mean, const int32_t* rowptr, const int32_t* col,
+                                  const float* w, const float* X, int64_t M, int L,
+                                  const float* const* W, const float* const* H, const int* widths,
+                                  float* const* dWp, float* const* dbp, int num_partials,
+                                  const int32_t* tile_open, void* stream) {
+  if (M < 0 || L < 1 || L > 2 || !dP || !batch || !gptr || !rowptr || !col || !X || !W || !H ||
       !widths || !dWp || !dbp || !tile_open)
     return LGNN_EINVAL;
   if (num_partials != lgnn_gcn_stack_bwd_partials(M)) return LGNN_EINVAL;
   lgnn_tile::StackBwdArgs a = {};
   for (int l = 0; l <= L + 1; ++l) a.width[l] = widths[l];
+  a.X = X;
   for (int l = 0; l <= L; ++l) {
     const int K = a.width[l], N = a.width[l + 1];
-    if (!lgnn_tile_fits(M, K, N) || !W[l] || !S[l] || !dWp[l] || !dbp[l]) return LGNN_EINVAL;
-    if (l >= 1 && !H[l]) return LGNN_EINVAL;
+    if (!lgnn_tile_fits(M, K, N) || !W[l] || !H[l] || !dWp[l] || !dbp[l]) return LGNN_EINVAL;
     a.W[l] = W[l];
     a.H[l] = H[l];
-    a.S[l] = S[l];
     a.dWp[l] = dWp[l];
     a.dbp[l] = dbp[l];
   }
@@ -1273,10 +1389,10 @@ extern "C" int lgnn_gcn_stack_bwd(const float* dP, const int64_t* batch, const i
   dim3 grid((unsigned)num_partials);
   if (L == 1)
     hipLaunchKernelGGL(lgnn_tile::k_stack_bwd<2>, grid, dim3(lgnn_tile::NTB), 0, s, dP, batch, gptr,
-                       pool_mean, tptr, tidx, tw, M, a, tile_open);
+                       pool_mean, rowptr, col, w, M, a, tile_open);
   else
     hipLaunchKernelGGL(lgnn_tile::k_stack_bwd<3>, grid, dim3(lgnn_tile::NTB), 0, s, dP, batch, gptr,
-                       pool_mean, tptr, tidx, tw, M, a, tile_open);
+                       pool_mean, rowptr, col, w, M, a, tile_open);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? LGNN_OK : (int)e;
 }

@@ -76,10 +76,9 @@ def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list):
     Wp = arr(*[W.data_ptr() for W in Ws])
     bp = arr(*[b.data_ptr() for b in bs])
     Hp = arr(*[h.data_ptr() for h in hs])
-    Sp = arr(None, *[t.data_ptr() for t in ss])
     widths = (ctypes.c_int * (L + 1))(*[W.size(0) for W in Ws])
     _lib.call("lgnn_gcn_stack_fwd", _lib.ptr(x), M, x.size(1), 1, _lib.ptr(csr.rowptr),
-              _lib.ptr(csr.col), _lib.ptr(csr.w), L, Wp, bp, widths, Hp, Sp, _lib.ptr(open_),
+              _lib.ptr(csr.col), _lib.ptr(csr.w), L, Wp, bp, widths, Hp, _lib.ptr(open_),
               _s(dev))
     for l in range(L + 1):
         inp = x if l == 0 else hs[l - 1]
@@ -120,11 +119,10 @@ def stack_bwd(dp: torch.Tensor, x: torch.Tensor, graph: Graph, mean: bool, Ws: l
     arr = ctypes.c_void_p * (L + 1)
     Sx = [x] + list(ss)
     _lib.call("lgnn_gcn_stack_bwd", _lib.ptr(dp), _lib.ptr(graph.batch), _lib.ptr(graph.gptr),
-              int(mean), _lib.ptr(csr.tptr), _lib.ptr(csr.tidx), _lib.ptr(csr.tw), M, L,
-              arr(*[W.data_ptr() for W in Ws]), arr(None, *[h.data_ptr() for h in hs[1:]]),
-              arr(*[t.data_ptr() for t in Sx]), (ctypes.c_int * (L + 2))(*widths),
-              arr(*[t.data_ptr() for t in dWp]), arr(*[t.data_ptr() for t in dbp]), P,
-              _lib.ptr(open_), _s(dev))
+              int(mean), _lib.ptr(csr.rowptr), _lib.ptr(csr.col), _lib.ptr(csr.w), _lib.ptr(x),
+              M, L, arr(*[W.data_ptr() for W in Ws]), arr(*[h.data_ptr() for h in hs]),
+              (ctypes.c_int * (L + 2))(*widths), arr(*[t.data_ptr() for t in dWp]),
+              arr(*[t.data_ptr() for t in dbp]), P, _lib.ptr(open_), _s(dev))
     dS = None
     for l in reversed(range(L + 1)):
         K, N = widths[l], widths[l + 1]
@@ -394,6 +392,8 @@ class _GCNStack(torch.autograd.Function):
                 grads[2 * l], grads[2 * l + 1] = dW, db
             reduce_multi(red, x.device)
             return (None, None, None, None, *grads)
+        if ctx.fused:  # the fused forward saves no aggregated inputs: S_l = Â H_{l-1}
+            ss = [spmm_raw(csr.rowptr, csr.col, csr.w, 0.0, hs[l]) for l in range(L)]
         dS = None
         for l in reversed(range(L)):
             W = params[2 + 2 * l]

@@ -286,14 +286,16 @@ def test_tile_open_flags(cuda):
     assert torch.equal(got, want)
 
 
-@pytest.mark.parametrize("case", ["c2_L2", "irregular_L2", "irregular_L1_add", "dense_tiles"])
+@pytest.mark.parametrize("case", ["c2_L2", "irregular_L2", "irregular_L1_add", "dense_tiles",
+                                  "c2_L3"])
 def test_gcn_fused_backward(cuda, case, monkeypatch):
     """lgnn_gcn_stack_bwd (closed tiles, fused) + masked accumulating layer-wise backward (open
     tiles) vs the layer-wise backward and the oracle. dense_tiles: 64-node graphs with k = 20
-    (1344 CSR entries per tile > the 1024 a tile stages) are flagged open by the graph build."""
+    (1344 CSR entries per tile > the 1024 a tile stages) are flagged open by the graph build.
+    c2_L3: three convs (fused forward, layer-wise backward on recomputed aggregates either way)."""
     pool = "add" if case.endswith("add") else "mean"
-    hidden = [128, 128] if "L1" in case else [128, 128, 128]
-    if case == "c2_L2":
+    hidden = [128, 128] if "L1" in case else [128] * 4 if "L3" in case else [128, 128, 128]
+    if case.startswith("c2"):
         b = synth.make_batch(300, n=64, k=8, d_in=128, seed=31)
     elif case == "dense_tiles":
         b = synth.make_batch(6, n=64, k=20, d_in=128, seed=32, sizes=[64, 64, 30, 34, 64, 64])

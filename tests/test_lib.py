@@ -76,8 +76,11 @@ def test_stack_fwd_validation_without_gpu():
     arr = (ctypes.c_void_p * 2)(None, None)
     widths = (ctypes.c_int * 2)(128, 128)
     assert lib.lgnn_gcn_stack_fwd(None, -1, 128, 1, None, None, None, 1, arr, arr, widths, arr,
-                                  arr, None, None) == -22
+                                  None, None) == -22
     big = (ctypes.c_int * 2)(256, 128)  # widths beyond the tile fast path are refused
     assert lib.lgnn_gcn_stack_fwd(None, 10, 128, 1, None, None, None, 1, arr, arr, big, arr,
-                                  arr, None, None) == -22
+                                  None, None) == -22
+    # a conv stack needs the tile flags (closed tiles are aggregated on chip)
+    assert lib.lgnn_gcn_stack_fwd(None, 10, 128, 1, 1, 1, None, 1, arr, arr, widths, arr,
+                                  None, None) == -22
     assert lib.lgnn_tile_count(65) == 2 and lib.lgnn_tile_count(64) == 1

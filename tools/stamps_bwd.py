@@ -19,9 +19,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "tools", "_abl", "liblgnn_bwd_%s.so")
 VARIANTS = {
     "default": [],
-    "rows2": ["-DLGNN_AGG_ROWS=2"],
-    "rows4": ["-DLGNN_AGG_ROWS=4"],
-    "eb4": ["-DLGNN_BWD_EB=4"],
     "stamps": ["-DLGNN_STAMPS"],
 }
 
@@ -50,8 +47,7 @@ def run():
     M, L, D = b.num_nodes, 2, 128
     gen = torch.Generator(device=dev).manual_seed(0)
     Ws = [torch.randn(D, D, device=dev, generator=gen) / 11.3 for _ in range(L + 1)]
-    Hs = [None] + [torch.randn(M, D, device=dev, generator=gen) for _ in range(L)]
-    Ss = [b.x] + [torch.randn(M, D, device=dev, generator=gen) for _ in range(L)]
+    Hs = [torch.randn(M, D, device=dev, generator=gen) for _ in range(L + 1)]
     dP = torch.randn(b.num_graphs, D, device=dev, generator=gen)
     s = torch.cuda.current_stream().cuda_stream
     arr = ctypes.c_void_p * (L + 1)
@@ -64,9 +60,9 @@ def run():
         slabs = [torch.empty(P * (D * D + D), device=dev) for _ in range(L + 1)]
         dWp = arr(*[t.data_ptr() for t in slabs])
         dbp = arr(*[t.data_ptr() + P * D * D * 4 for t in slabs])
-        args = (dP.data_ptr(), g.batch.data_ptr(), g.gptr.data_ptr(), 1, csr.tptr.data_ptr(),
-                csr.tidx.data_ptr(), csr.tw.data_ptr(), M, L, arr(*[w.data_ptr() for w in Ws]),
-                arr(None, *[h.data_ptr() for h in Hs[1:]]), arr(*[x.data_ptr() for x in Ss]),
+        args = (dP.data_ptr(), g.batch.data_ptr(), g.gptr.data_ptr(), 1, csr.rowptr.data_ptr(),
+                csr.col.data_ptr(), csr.w.data_ptr(), b.x.data_ptr(), M, L,
+                arr(*[w.data_ptr() for w in Ws]), arr(*[h.data_ptr() for h in Hs]),
                 (ctypes.c_int * (L + 2))(D, D, D, D), dWp, dbp, P, open_.data_ptr(), s)
         for _ in range(3):
             assert lib.lgnn_gcn_stack_bwd(*args) == 0
@@ -85,12 +81,11 @@ def run():
             a = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 64)[:P].astype(np.int64)
             n = int((a[0] > 0).sum())
             d = np.diff(a[:, :n], axis=1)
-            names = ["tile start->l2 top", "l2 dW", "l2 DX+sync", "l2 dS write", "l2 agg",
-                     "l1 top", "l1 dW", "l1 DX+sync", "l1 dS write", "l1 agg", "l0 top",
-                     "l0 dW+sync"]
+            names = ["tile start (scatter, dZ_L)", "l2 G + write", "l2 dW + DX",
+                     "l2 dZ write", "l1 G + write", "l1 dW + DX", "l1 dZ write", "l0 dW + sync"]
             print(f"stamps per block: {n}; mean span {(a[:, n - 1] - a[:, 0]).mean():.0f} cycles")
             for i in range(min(n - 1, 24)):
-                print(f"{i:2d} {names[i % 12]:20s} mean {d[:, i].mean():8.0f}  "
+                print(f"{i:2d} {names[i % 8]:26s} mean {d[:, i].mean():8.0f}  "
                       f"p90 {np.percentile(d[:, i], 90):8.0f}")
 
 
