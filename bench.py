@@ -82,8 +82,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="bounded CPU-baseline sample (rank 0, N=1 only); 0 disables")
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--opt", choices=["fused", "foreach"], default="fused",
-                    help="Adam implementation (runs inside the timed step either way)")
+    ap.add_argument("--opt", choices=["lgnn", "fused", "foreach"], default="lgnn",
+                    help="Adam implementation, inside the timed step either way: lgnn = one "
+                         "HIP launch (lesion_gnn_amd.optim.Adam); fused / foreach = torch's")
     ap.add_argument("--graph", type=int, default=1,
                     help="1: replay the captured fwd+bwd and optimizer HIP graphs; 0: eager")
     return ap.parse_args()
@@ -152,50 +153,62 @@ def _time_launches(launch, dev, reps=20):
 
 
 def time_dominant_kernels(model, b, dev):
-    """The two largest kernels of the C2 step, launched exactly as the step launches them:
-    * lgnn_tile::k_stack_fwd — the fused forward (in_proj + 2 x (aggregation + GCN linear +
-      ELU)), 2*M*(d_in*h + L*h*h) FLOP per launch;
-    * lgnn_tile::k_bwd<GRAD_TRANSPOSE,ELU,DX> — the conv-1 backward (transposed aggregation of
-      dS + ELU' prologue, dW = dZ^T S and dX = dZ W), 4*M*h*h FLOP per launch."""
+    """The two largest kernels of the C2 step, each launched alone with the step's arguments:
+    * lgnn_tile::k_stack_bwd<3> — the fused backward of in_proj + 2 GCN convs (closed tiles),
+      useful FLOP per launch 2*M*(d_in*h + L*h*h) (dW) + 2*M*L*h*h (dH = G W) + 2*nnz*h*L (the
+      transposed aggregation);
+    * lgnn_tile::k_stack_fwd<true> — the fused forward, 2*M*(d_in*h + L*h*h) + 2*nnz*h*L.
+    The tile aggregation runs as a dense 64 x 64 MFMA product; its zeros are not counted."""
+    import ctypes
+
     from lesion_gnn_amd import _lib, ops
     from lesion_gnn_amd.graph import Graph
 
     g = Graph(b.edge_index, b.num_nodes, b.batch, b.num_graphs)
     csr = g.csr("gcn")
+    open_ = g.tile_open("gcn")
     Ws = [model.in_proj.weight.detach()] + [c.lin.weight.detach() for c in model.convs]
     bs = [model.in_proj.bias.detach()] + [c.bias.detach() for c in model.convs]
     with torch.no_grad():
-        hs, ss = ops.stack_fwd(b.x, g, Ws, bs)
+        hs, _ = ops.stack_fwd(b.x, g, Ws, bs)
     M, h = hs[1].shape
+    d_in = b.x.size(1)
     L = len(Ws) - 1
+    nnz = int(csr.rowptr[-1].item())
+    s = torch.cuda.current_stream(dev).cuda_stream
+    arr = ctypes.c_void_p * (L + 1)
+    Wp = arr(*[W.data_ptr() for W in Ws])
+    bp = arr(*[x.data_ptr() for x in bs])
+    Hp = arr(*[x.data_ptr() for x in hs])
+    widths = [d_in] + [W.size(0) for W in Ws]
+    lib = _lib.load()
+    P = lib.lgnn_gcn_stack_bwd_partials(M)
+    slabs = [torch.empty(P * (widths[l + 1] * widths[l] + widths[l + 1]), device=dev)
+             for l in range(L + 1)]
+    dWp = arr(*[t.data_ptr() for t in slabs])
+    dbp = arr(*[t.data_ptr() + P * widths[l + 1] * widths[l] * 4 for l, t in enumerate(slabs)])
+    dP = torch.randn(b.num_graphs, h, device=dev)
+    agg = 2.0 * nnz * h * L
+    lin = 2.0 * M * (d_in * h + L * h * h)
     out = []
 
-    def stack():
-        ops.stack_fwd(b.x, g, Ws, bs)
-
-    ms = _time_launches(stack, dev)
-    out.append({"kernel": "lgnn_tile::k_stack_fwd<true> (fused GCN forward, all layers)",
-                "ms": ms, "flops": 2.0 * M * (b.x.size(1) * h + L * h * h),
-                "trace_name": "void lgnn_tile::k_stack_fwd<true>"})
-    W = Ws[1].contiguous()
-    dS = torch.randn(M, h, device=dev)
-    P = ops.num_partials(M, h, h, False)
-    dWp = torch.empty(P * h * h, device=dev)
-    dbp = torch.empty(P * h, device=dev)
-    dX = torch.empty(M, h, device=dev)
-    s = torch.cuda.current_stream(dev)
-
     def bwd():
-        _lib.call("lgnn_node_linear_bwd", _lib.LGNN_GRAD_TRANSPOSE, dS.data_ptr(), None, None, 1,
-                  csr.tptr.data_ptr(), csr.tidx.data_ptr(), csr.tw.data_ptr(), 0.0,
-                  hs[1].data_ptr(), _lib.LGNN_ACT_ELU, ss[0].data_ptr(), M, h, None, None, None,
-                  0.0, W.data_ptr(), h, dX.data_ptr(), dWp.data_ptr(), dbp.data_ptr(), P,
-                  s.cuda_stream)
+        _lib.call("lgnn_gcn_stack_bwd", dP.data_ptr(), g.batch.data_ptr(), g.gptr.data_ptr(), 1,
+                  csr.rowptr.data_ptr(), csr.col.data_ptr(), csr.w.data_ptr(), b.x.data_ptr(), M,
+                  L, Wp, Hp, (ctypes.c_int * (L + 2))(*widths), dWp, dbp, P, open_.data_ptr(), s)
 
-    ms = _time_launches(bwd, dev)
-    out.append({"kernel": "lgnn_tile::k_bwd<GRAD_TRANSPOSE,ELU,DX> (GCN conv backward)",
-                "ms": ms, "flops": 4.0 * M * h * h,
-                "trace_name": "void lgnn_tile::k_bwd<2, 1, true>"})
+    out.append({"kernel": f"lgnn_tile::k_stack_bwd<{L + 1}> (fused GCN backward, all layers)",
+                "ms": _time_launches(bwd, dev), "flops": lin + 2.0 * M * L * h * h + agg,
+                "trace_name": f"void lgnn_tile::k_stack_bwd<{L + 1}>"})
+
+    def fwd():
+        _lib.call("lgnn_gcn_stack_fwd", b.x.data_ptr(), M, d_in, 1, csr.rowptr.data_ptr(),
+                  csr.col.data_ptr(), csr.w.data_ptr(), L, Wp, bp,
+                  (ctypes.c_int * (L + 1))(*widths[1:]), Hp, open_.data_ptr(), s)
+
+    out.append({"kernel": "lgnn_tile::k_stack_fwd<true> (fused GCN forward, all layers)",
+                "ms": _time_launches(fwd, dev), "flops": lin + agg,
+                "trace_name": "void lgnn_tile::k_stack_fwd<true>"})
     return out
 
 
@@ -253,13 +266,19 @@ def main():
         if wl["model"] == "gin":  # SyncBN: full-batch statistics across the ranks
             model.set_sync_bn(dist.group.WORLD, global_count=b.num_nodes * world)
     params = list(model.parameters())
-    okw = {"fused": True} if args.opt == "fused" else {"foreach": True}
-    if args.graph:
-        okw["capturable"] = True
-    opt = torch.optim.Adam(params, lr=1e-3, weight_decay=2e-6, **okw)
+    if args.opt == "lgnn":
+        from lesion_gnn_amd import optim as lgnn_optim
+        opt = lgnn_optim.Adam(params, lr=1e-3, weight_decay=2e-6)
+    else:
+        okw = {"fused": True} if args.opt == "fused" else {"foreach": True}
+        if args.graph:
+            okw["capturable"] = True
+        opt = torch.optim.Adam(params, lr=1e-3, weight_decay=2e-6, **okw)
+
+    one = torch.ones((), device=dev)  # the loss gradient, allocated once (no fill per step)
 
     def fwd_bwd():
-        loss_fn(wl, model(b.x, b.edge_index, b.batch, B), b.y).backward()
+        loss_fn(wl, model(b.x, b.edge_index, b.batch, B), b.y).backward(one)
 
     def exchange():
         if world > 1:  # one flat RCCL all-reduce; equal shards -> weights 1/world
@@ -337,7 +356,8 @@ def main():
                          "traffic": round(traffic) if traffic else None,
                          "traffic_source": tsrc, "kernel": kt["kernel"],
                          "avg_launch_ms": round(kt["ms"], 5), "flops_per_launch": kt["flops"]})
-        out["roofline"] = rows[0]  # the dominant kernel: the fused forward
+        rows.sort(key=lambda r: -r["avg_launch_ms"])
+        out["roofline"] = rows[0]  # the dominant kernel (longest launch)
         out["roofline_next"] = rows[1:]
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(wl, B, args.cpu_seconds)

@@ -66,8 +66,8 @@ const char* lgnn_status_string(int status);
  * PyG appends loops after the edge list). Invalid indices (<0 or >= N) are dropped and counted in
  * *err_count (device int, may be NULL). tmap (nullable, needs the transpose) [cap]: for each
  * transpose entry, the position of the same edge in the target CSR (GAT backward reads per-edge
- * attention saved in target order). tile_open (nullable) [ceil(N/64)]: as lgnn_tile_open, in
- * the same launches. *err_count is written (not accumulated). Workspace size:
+ * attention saved in target order). tile_open (nullable) [ceil(N/64) + 1]: as lgnn_tile_open,
+ * in the same launches. *err_count is written (not accumulated). Workspace size:
  * lgnn_graph_workspace_bytes.
  * ------------------------------------------------------------------------------------------- */
 size_t lgnn_graph_workspace_bytes(int64_t num_nodes, int64_t num_edges);
@@ -262,7 +262,8 @@ int lgnn_gcn_stack_fwd(const float* X, int64_t M, int d_in, int has_in_proj,
                        float* const* H, const int32_t* tile_open, void* stream);
 /* Tiles: 64 consecutive node rows. open[t] = 1 when an edge joins tile t to another tile (its
  * layers then depend on other tiles) or when the tile holds more than 1024 CSR entries; the
- * fused stacks skip open tiles. */
+ * fused stacks skip open tiles. open has lgnn_tile_count(N) + 1 entries: the last one counts the
+ * open tiles (the *_tiles kernels with want_open = 1 return at once when it is 0). */
 int lgnn_tile_count(int64_t num_nodes);
 int lgnn_tile_open(const int32_t* rowptr, const int32_t* col, int64_t num_nodes, int32_t* open,
                    void* stream);
@@ -301,6 +302,22 @@ int lgnn_gcn_stack_bwd(const float* dP, const int64_t* batch, const int32_t* gpt
                        int64_t M, int L, const float* const* W, const float* const* H,
                        const int* widths, float* const* dWp, float* const* dbp, int num_partials,
                        const int32_t* tile_open, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Optimizer step. Replaces: torch.optim.Adam / AdamW (amsgrad = False) as configured by the
+ * reference (models/base.py:162-188), in one launch over up to 16 fp32 tensors.
+ *   decoupled = 0: Adam (L2: g += weight_decay * p); 1: AdamW (p *= 1 - lr * weight_decay).
+ *   step: device float, the number of steps taken (read by every workgroup; with advance = 1
+ *   incremented once, by the last one); ticket: device uint32, zero before the first call
+ *   (re-armed by the call). Split a longer list over several calls with advance = 0 on all but
+ *   the last (every call of one step then uses the same step count).
+ *   Graph-capturable (lr and the betas are launch arguments: fixed in a captured graph).
+ * ------------------------------------------------------------------------------------------- */
+int lgnn_adam_step(int n, float* const* params, const float* const* grads, float* const* exp_avg,
+                   float* const* exp_avg_sq, const int64_t* numels, float* step,
+                   unsigned int* ticket, float lr, float beta1, float beta2, float eps,
+                   float weight_decay, int decoupled, int maximize, int advance,
+                   void* stream);
 
 #ifdef __cplusplus
 }

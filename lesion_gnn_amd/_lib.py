@@ -42,6 +42,8 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_node_linear_bwd_tiles": (I32, [I32, P, P, P, I32, P, P, P, F32, P, I32, P, I64, I32,
                                          P, P, P, F32, P, I32, P, P, P, I32, P, I32, I32, P]),
     "lgnn_gcn_stack_bwd_partials": (I32, [I64]),
+    "lgnn_adam_step": (I32, [I32, P, P, P, P, P, P, P, F32, F32, F32, F32, F32, I32, I32, I32,
+                             P]),
     "lgnn_gcn_stack_bwd": (I32, [P, P, P, I32, P, P, P, P, I64, I32, P, P, P, P, P, I32, P, P]),
     "lgnn_spmm": (I32, [P, P, P, F32, P, I64, I32, P, P]),
     "lgnn_reduce_partials_multi": (I32, [I32, P, P, P, P, P]),

@@ -7,6 +7,7 @@
 
 #define LGNN_MAX_STACK 8  // layers of one fused stack launch (in_proj + 7 convs)
 #define LGNN_MAX_REDUCE 16  // slabs of one lgnn_reduce_partials_multi launch
+#define LGNN_MAX_ADAM 16    // tensors of one lgnn_adam_step launch
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));

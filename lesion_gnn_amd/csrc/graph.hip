@@ -101,8 +101,8 @@ __global__ __launch_bounds__(kThreads) void k_count(const int64_t* __restrict__ 
                                                     int32_t* tcnt, int32_t* err,
                                                     int32_t* tile_open, int64_t ntiles) {
   const int lane = threadIdx.x & 63;
-  if (tile_open) {
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < ntiles;
+  if (tile_open) {  // ntiles flags + the open-tile count
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t <= ntiles;
          t += (int64_t)gridDim.x * blockDim.x)
       tile_open[t] = 0;
   }
@@ -322,9 +322,13 @@ __global__ __launch_bounds__(kThreads) void k_finish(int64_t N, int64_t E, int a
   }
   // 64-node tiles an edge leaves (source CSR pass) are open: the fused layer stacks skip them.
   // So are tiles with more CSR entries than a tile stages in LDS (lgnn_tile CAPE = 1024).
+  // flag setter: the first writer of a tile also counts it (tile_open[ntiles])
+  auto mark = [&](int64_t t) {
+    if (atomicCAS(&tile_open[t], 0, 1) == 0) atomicAdd(&tile_open[(N + 63) >> 6], 1);
+  };
   if (tile_open && !tr && i < N && (i & 63) == 0) {
     const int64_t iend64 = i + 64 < N ? i + 64 : N;
-    if (ptr[iend64] - ptr[i] > 1024) tile_open[i >> 6] = 1;
+    if (ptr[iend64] - ptr[i] > 1024) mark(i >> 6);
   }
   if (tile_open && !tr && i < N) {
     const int r0 = ptr[i], r1 = ptr[i + 1];
@@ -332,8 +336,8 @@ __global__ __launch_bounds__(kThreads) void k_finish(int64_t N, int64_t E, int a
     for (int j = r0; j < r1; ++j) {
       const int nb = staged ? s_val[j - eb] : idx[j];
       if ((nb >> 6) != ti) {
-        tile_open[ti] = 1;  // benign race: every writer stores 1
-        tile_open[nb >> 6] = 1;
+        if (tile_open[ti] == 0) mark(ti);
+        if (tile_open[nb >> 6] == 0) mark(nb >> 6);
       }
     }
   }

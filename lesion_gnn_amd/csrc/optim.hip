@@ -1,0 +1,97 @@
+// Fused Adam / AdamW step over a list of fp32 tensors in ONE launch (torch.optim.Adam /
+// AdamW semantics, amsgrad = False). Replaces the optimizer step of the reference's training
+// loop (models/base.py:162-188 configure_optimizers -> torch.optim.Adam/AdamW), which torch
+// runs as multi_tensor_apply launches plus a separate step-count update.
+//
+// Per element (t = step + 1, bc1 = 1 - beta1^t, bc2 = 1 - beta2^t):
+//   g = grad (negated if maximize); Adam: g += wd * p;  AdamW: p *= 1 - lr * wd
+//   m = beta1 m + (1 - beta1) g;  v = beta2 v + (1 - beta2) g^2
+//   p -= lr / bc1 * m / (sqrt(v) / sqrt(bc2) + eps)
+// The step count lives on the device (graph-capturable): every workgroup reads it, the last one
+// to finish (ticket counter) increments it and re-arms the ticket (advance = 1; a group of
+// more than LGNN_MAX_ADAM (16) tensors is stepped in several launches, the last one advancing).
+#include "common.h"
+
+namespace {
+
+constexpr int kT = 256;
+
+struct AdamJobs {
+  float* p[LGNN_MAX_ADAM];
+  const float* g[LGNN_MAX_ADAM];
+  float* m[LGNN_MAX_ADAM];
+  float* v[LGNN_MAX_ADAM];
+  int64_t off[LGNN_MAX_ADAM + 1];  // prefix of the element counts
+  int n;
+};
+
+__global__ __launch_bounds__(kT) void k_adam(AdamJobs J, float* __restrict__ step,
+                                             unsigned int* __restrict__ ticket, float lr,
+                                             float beta1, float beta2, float eps, float wd,
+                                             int decoupled, int maximize, int advance) {
+  const float t = step[0] + 1.f;
+  const float bc1 = 1.f - powf(beta1, t);
+  const float bc2s = sqrtf(1.f - powf(beta2, t));
+  const float step_size = lr / bc1;
+  const int64_t total = J.off[J.n];
+  int j = 0;
+  for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * kT) {
+    while (i >= J.off[j + 1]) ++j;
+    const int64_t k = i - J.off[j];
+    float p = J.p[j][k];
+    float g = J.g[j][k];
+    if (maximize) g = -g;
+    if (decoupled) p *= 1.f - lr * wd;
+    else g = fmaf(wd, p, g);
+    const float m = fmaf(beta1, J.m[j][k], (1.f - beta1) * g);
+    const float v = fmaf(beta2, J.v[j][k], (1.f - beta2) * g * g);
+    J.m[j][k] = m;
+    J.v[j][k] = v;
+    p -= step_size * m / (sqrtf(v) / bc2s + eps);
+    J.p[j][k] = p;
+  }
+  if (!advance) return;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
+      step[0] = t;
+      *ticket = 0u;
+      __threadfence();
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int lgnn_adam_step(int n, float* const* params, const float* const* grads,
+                              float* const* exp_avg, float* const* exp_avg_sq,
+                              const int64_t* numels, float* step, unsigned int* ticket, float lr,
+                              float beta1, float beta2, float eps, float weight_decay,
+                              int decoupled, int maximize, int advance, void* stream) {
+  if (n < 0 || n > LGNN_MAX_ADAM || !step || !ticket || (n > 0 && (!params || !grads ||
+      !exp_avg || !exp_avg_sq || !numels)))
+    return LGNN_EINVAL;
+  AdamJobs J = {};
+  J.n = n;
+  J.off[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    if (numels[i] < 0 || (numels[i] > 0 && (!params[i] || !grads[i] || !exp_avg[i] ||
+        !exp_avg_sq[i])))
+      return LGNN_EINVAL;
+    J.p[i] = params[i];
+    J.g[i] = grads[i];
+    J.m[i] = exp_avg[i];
+    J.v[i] = exp_avg_sq[i];
+    J.off[i + 1] = J.off[i] + numels[i];
+  }
+  const int64_t total = J.off[n];
+  int64_t g = (total + kT - 1) / kT;
+  if (g < 1) g = 1;
+  if (g > 1024) g = 1024;
+  hipLaunchKernelGGL(k_adam, dim3((unsigned)g), dim3(kT), 0, as_stream(stream), J, step, ticket,
+                     lr, beta1, beta2, eps, weight_decay, decoupled, maximize, advance);
+  LGNN_LAUNCH_CHECK();
+  return LGNN_OK;
+}

@@ -70,10 +70,13 @@ struct TileIdx {
 
 // Tile selection by a per-tile mask (nullable = every tile): with `want` = 1 only tiles whose
 // mask is non-zero, with 0 only tiles whose mask is zero. Block-uniform scalar reads.
+// mask[ntiles] counts the non-zero flags: a want = 1 launch with none returns after one load.
 __device__ __forceinline__ int64_t seek_tile(int64_t t, int64_t ntiles,
                                              const int32_t* __restrict__ mask, int want) {
-  if (mask)
+  if (mask) {
+    if (want && mask[ntiles] == 0) return ntiles;
     while (t < ntiles && ((mask[t] != 0) != (want != 0))) t += gridDim.x;
+  }
   return t;
 }
 
@@ -1195,16 +1198,20 @@ __global__ __launch_bounds__(NT) void k_tile_open(const int32_t* __restrict__ ro
                                                   int32_t* __restrict__ open) {
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < M; i += (int64_t)gridDim.x * NT) {
     const int ti = (int)(i / TM);
+    const int64_t ntiles = (M + TM - 1) / TM;
+    auto mark = [&](int64_t t) {  // the first writer of a tile also counts it
+      if (atomicCAS(&open[t], 0, 1) == 0) atomicAdd(&open[ntiles], 1);
+    };
     if (i % TM == 0) {
       const int64_t ie = i + TM < M ? i + TM : M;
-      if (rowptr[ie] - rowptr[i] > CAPE) open[ti] = 1;
+      if (rowptr[ie] - rowptr[i] > CAPE) mark(ti);
     }
     const int e0 = rowptr[i], e1 = rowptr[i + 1];
     for (int e = e0; e < e1; ++e) {
       const int tj = col[e] / TM;
       if (tj != ti) {
-        open[ti] = 1;  // benign race: every writer stores 1
-        open[tj] = 1;
+        if (open[ti] == 0) mark(ti);
+        if (open[tj] == 0) mark(tj);
       }
     }
   }
@@ -1293,9 +1300,9 @@ extern "C" int lgnn_tile_open(const int32_t* rowptr, const int32_t* col, int64_t
   if (M < 0 || !open || (M > 0 && (!rowptr || !col))) return LGNN_EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int64_t ntiles = (M + lgnn_tile::TM - 1) / lgnn_tile::TM;
-  if (ntiles == 0) return LGNN_OK;
-  if (hipMemsetAsync(open, 0, ntiles * sizeof(int32_t), s) != hipSuccess)
+  if (hipMemsetAsync(open, 0, (ntiles + 1) * sizeof(int32_t), s) != hipSuccess)
     return (int)hipGetLastError();
+  if (ntiles == 0) return LGNN_OK;
   int64_t g = (M + lgnn_tile::NT - 1) / lgnn_tile::NT;
   if (g > 4096) g = 4096;
   hipLaunchKernelGGL(lgnn_tile::k_tile_open, dim3((unsigned)g), dim3(lgnn_tile::NT), 0, s, rowptr,

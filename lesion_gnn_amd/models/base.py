@@ -118,10 +118,13 @@ class BaseModule(nn.Module):
 
     def configure_optimizers(self):
         """Reference base.py:162-188: the optimizer, plus a torch.optim.lr_scheduler by name
-        (the pl_bolts LinearWarmupCosineAnnealingLR is not available in this build)."""
+        (the pl_bolts LinearWarmupCosineAnnealingLR is not available in this build). Adam and
+        AdamW step in one HIP launch (lesion_gnn_amd.optim, same update as torch's)."""
+        from .. import optim as lgnn_optim
+
         ctor = {
-            OptimizerAlgo.ADAM: torch.optim.Adam,
-            OptimizerAlgo.ADAMW: torch.optim.AdamW,
+            OptimizerAlgo.ADAM: lgnn_optim.Adam,
+            OptimizerAlgo.ADAMW: lgnn_optim.AdamW,
             OptimizerAlgo.SGD: torch.optim.SGD,
         }[self.optimizer_algo]
         optimizer = ctor(self.parameters(), lr=self.lr, weight_decay=self.weight_decay)

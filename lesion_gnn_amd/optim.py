@@ -1,0 +1,84 @@
+"""Optimizers whose step is one HIP launch (lgnn_adam_step) — drop-ins for torch.optim.Adam /
+AdamW (amsgrad=False) as the reference's configure_optimizers builds them (models/base.py:
+162-188). torch runs the same update as multi_tensor_apply launches plus a step-count kernel.
+
+State per parameter mirrors torch's ('step', 'exp_avg', 'exp_avg_sq'); every parameter of a
+group shares one device step tensor. Graph-capturable: the launch reads only device pointers
+(lr / betas / eps / weight_decay are launch arguments, so fixed inside a captured graph).
+No CPU path: parameters and gradients must be contiguous fp32 GPU tensors.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+
+MAX_TENSORS = 16  # LGNN_MAX_ADAM
+
+
+class Adam(torch.optim.Optimizer):
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0, maximize: bool = False, amsgrad: bool = False,
+                 decoupled: bool = False):
+        if amsgrad:
+            raise NotImplementedError("lgnn Adam: amsgrad")
+        if not 0.0 <= lr or not 0.0 <= eps or not 0.0 <= weight_decay:
+            raise ValueError("lgnn Adam: lr, eps and weight_decay must be >= 0")
+        defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay,
+                        maximize=maximize)
+        super().__init__(params, defaults)
+        self._decoupled = decoupled
+        self._tickets: dict[int, torch.Tensor] = {}
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for gi, group in enumerate(self.param_groups):
+            ps = [p for p in group["params"] if p.grad is not None]
+            if not ps:
+                continue
+            _lib.require_gpu(*ps)
+            dev = ps[0].device
+            step_t = None
+            for p in ps:
+                if p.dtype != torch.float32 or not p.is_contiguous() or \
+                        p.grad.dtype != torch.float32 or not p.grad.is_contiguous():
+                    raise _lib.LgnnError("lgnn Adam: contiguous fp32 parameters and gradients")
+                st = self.state[p]
+                if not st:
+                    st["exp_avg"] = torch.zeros_like(p)
+                    st["exp_avg_sq"] = torch.zeros_like(p)
+                step_t = st.get("step", step_t)
+            if step_t is None:
+                step_t = torch.zeros((), dtype=torch.float32, device=dev)
+            for p in ps:
+                self.state[p]["step"] = step_t
+            ticket = self._tickets.get(gi)
+            if ticket is None:
+                ticket = self._tickets[gi] = torch.zeros(1, dtype=torch.int32, device=dev)
+            b1, b2 = group["betas"]
+            for c in range(0, len(ps), MAX_TENSORS):
+                chunk = ps[c:c + MAX_TENSORS]
+                n = len(chunk)
+                arr = ctypes.c_void_p * n
+                _lib.call("lgnn_adam_step", n, arr(*[p.data_ptr() for p in chunk]),
+                          arr(*[p.grad.data_ptr() for p in chunk]),
+                          arr(*[self.state[p]["exp_avg"].data_ptr() for p in chunk]),
+                          arr(*[self.state[p]["exp_avg_sq"].data_ptr() for p in chunk]),
+                          (ctypes.c_int64 * n)(*[p.numel() for p in chunk]),
+                          step_t.data_ptr(), ticket.data_ptr(), float(group["lr"]), float(b1),
+                          float(b2), float(group["eps"]), float(group["weight_decay"]),
+                          int(self._decoupled), int(group["maximize"]),
+                          int(c + MAX_TENSORS >= len(ps)), _lib.stream(dev))
+        return loss
+
+
+class AdamW(Adam):
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 1e-2, maximize: bool = False, amsgrad: bool = False):
+        super().__init__(params, lr, betas, eps, weight_decay, maximize, amsgrad, decoupled=True)

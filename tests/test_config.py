@@ -41,7 +41,8 @@ def test_reference_config_builds_gat():
     assert m.model.out_proj.out_features == 1  # regression -> 1 output (gat.py:79)
     assert len(m.model.convs) == 3 and m.model.convs[0].heads == 2
     opt = m.configure_optimizers()
-    assert isinstance(opt, torch.optim.Adam)
+    from lesion_gnn_amd import optim
+    assert isinstance(opt, optim.Adam) and isinstance(opt, torch.optim.Optimizer)
     want = ref.GAT(1025, [128] * 4, 1, heads=2, dropout=0.35).state_dict()
     assert {k: v.shape for k, v in m.model.state_dict().items()} == \
         {k: v.shape for k, v in want.items()}

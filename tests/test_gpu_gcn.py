@@ -283,7 +283,11 @@ def test_tile_open_flags(cuda):
     cross = (src // 64) != (dst // 64)
     want[(src[cross] // 64)] = 1
     want[(dst[cross] // 64)] = 1
+    want[-1] = int(want[:-1].sum())  # trailing entry: the number of open tiles
     assert torch.equal(got, want)
+    # all tiles closed: count 0 (the masked launches return at once)
+    b2 = synth.make_batch(4, n=64, k=6, d_in=8, seed=23)
+    assert Graph(b2.edge_index.to(cuda), b2.num_nodes).tile_open("gcn").cpu().tolist() == [0] * 5
 
 
 @pytest.mark.parametrize("case", ["c2_L2", "irregular_L2", "irregular_L1_add", "dense_tiles",
@@ -305,7 +309,7 @@ def test_gcn_fused_backward(cuda, case, monkeypatch):
     ours = ours.to(cuda)
     if case == "dense_tiles":
         g = Graph(b.edge_index.to(cuda), b.num_nodes)
-        assert g.tile_open("gcn").cpu().tolist() == [1, 1, 1, 1, 1]
+        assert g.tile_open("gcn").cpu().tolist() == [1, 1, 1, 1, 1, 5]
     monkeypatch.setattr(ops, "FUSED_BWD", True)
     lf, _, gf = run_step(ours, b, cuda)
     monkeypatch.setattr(ops, "FUSED_BWD", False)
