@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 4
+#define LGNN_ABI_VERSION 5
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -67,14 +67,16 @@ const char* lgnn_status_string(int status);
  * *err_count (device int, may be NULL). tmap (nullable, needs the transpose) [cap]: for each
  * transpose entry, the position of the same edge in the target CSR (GAT backward reads per-edge
  * attention saved in target order). tile_open (nullable) [ceil(N/64) + 1]: as lgnn_tile_open,
+ * in the same launches. gptr (nullable) [num_graphs + 1]: as lgnn_batch_ptr from batch [N],
  * in the same launches. *err_count is written (not accumulated). Workspace size:
- * lgnn_graph_workspace_bytes.
+ * lgnn_graph_workspace_bytes. N + E < 2^30. Five launches, no host synchronisation.
  * ------------------------------------------------------------------------------------------- */
 size_t lgnn_graph_workspace_bytes(int64_t num_nodes, int64_t num_edges);
 int lgnn_graph_build(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes, int loops,
                      int norm, int32_t* rowptr, int32_t* col, float* w, int32_t* tptr,
                      int32_t* tidx, float* tw, int32_t* tmap, int32_t* tile_open,
-                     int32_t* err_count, void* workspace, size_t workspace_bytes, void* stream);
+                     const int64_t* batch, int64_t num_graphs, int32_t* gptr, int32_t* err_count,
+                     void* workspace, size_t workspace_bytes, void* stream);
 
 /* Graph offsets from a sorted PyG `batch` vector (Batch.ptr): ptr[g] = first node of graph g,
  * ptr[B] = M. Replaces the count/offset half of PyG scatter(reduce='mean') over `batch`. */

@@ -32,7 +32,8 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_abi_version": (I32, []),
     "lgnn_status_string": (ctypes.c_char_p, [I32]),
     "lgnn_graph_workspace_bytes": (SZ, [I64, I64]),
-    "lgnn_graph_build": (I32, [P, I64, I64, I32, I32, P, P, P, P, P, P, P, P, P, P, SZ, P]),
+    "lgnn_graph_build": (I32, [P, I64, I64, I32, I32, P, P, P, P, P, P, P, P, P, I64, P, P, P,
+                               SZ, P]),
     "lgnn_batch_ptr": (I32, [P, I64, I64, P, P]),
     "lgnn_node_linear_fwd": (I32, [P, I64, I32, P, P, P, F32, P, P, I32, I32, P, P, P]),
     "lgnn_bwd_num_partials": (I32, [I64, I32, I32, I32]),
@@ -70,7 +71,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_bn_bwd_apply": (I32, [P, P, P, I64, I32, P, P, P, P, P, F64, I32, P, P, P, P]),
 }
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _lib = None
 

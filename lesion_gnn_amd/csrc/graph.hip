@@ -19,7 +19,8 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kFinishCap = 6144;  // staged CSR entries per 256-row block
+constexpr int kFinT = 64;          // k_finish: rows (threads) per block
+constexpr int kFinishCap = 1536;   // staged CSR entries per k_finish block
 
 inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -31,13 +32,13 @@ struct GraphWs {
   int32_t* err;    // [1] dropped edges (zeroed with the counters, copied to err_count)
   int32_t* cnt;    // [N+1] in-degree without loops
   int32_t* tcnt;   // [N+1]
-  int32_t* fill;   // [N]
+  int32_t* stat;   // [2 * scan blocks] chained-scan block prefixes, flagged (zeroed)
+  int32_t* fill;   // [N] next free slot of each row (set by the scan)
   int32_t* tfill;  // [N]
   int32_t* eid;    // [E+N]
   int32_t* teid;   // [E+N]
   int32_t* inv;    // [E+N] edge id -> target-CSR position (for tmap)
   float* dis;      // [N] deg^-1/2 (GCN normalisation), inf -> 0
-  int32_t* bsum;   // [2 * scan blocks] per-block degree sums
   size_t zero_bytes;
 };
 
@@ -52,20 +53,20 @@ GraphWs carve(void* base, int64_t N, int64_t E) {
   ws.err = (int32_t*)take(4);
   ws.cnt = (int32_t*)take((N + 1) * 4);
   ws.tcnt = (int32_t*)take((N + 1) * 4);
+  ws.stat = (int32_t*)take(scan_bsum_bytes(N));
+  ws.zero_bytes = (size_t)(p - static_cast<char*>(base));
   ws.fill = (int32_t*)take(N * 4);
   ws.tfill = (int32_t*)take(N * 4);
-  ws.zero_bytes = (size_t)(p - static_cast<char*>(base));
   ws.eid = (int32_t*)take((E + N) * 4);
   ws.teid = (int32_t*)take((E + N) * 4);
   ws.inv = (int32_t*)take((E + N) * 4);
   ws.dis = (float*)take(N * 4);
-  ws.bsum = (int32_t*)take(scan_bsum_bytes(N));
   return ws;
 }
 
 size_t ws_total(int64_t N, int64_t E) {
   return align_up(4) + 2 * align_up((N + 1) * 4) + 3 * align_up(N * 4) + 3 * align_up((E + N) * 4) +
-         align_up(scan_bsum_bytes(N)) + 256;
+         2 * align_up(scan_bsum_bytes(N)) + 256;
 }
 
 // Wave-level run detection over consecutive edges: lanes whose target equals the previous
@@ -95,21 +96,51 @@ __device__ __forceinline__ bool edge_ok(int64_t s, int64_t d, int64_t N) {
   return s >= 0 && s < N && d >= 0 && d < N;
 }
 
-// grid-stride over wave-aligned chunks so every wave sees 64 consecutive edges
-__global__ __launch_bounds__(kThreads) void k_count(const int64_t* __restrict__ ei, int64_t E,
-                                                    int64_t N, int loops, int32_t* cnt,
-                                                    int32_t* tcnt, int32_t* err,
-                                                    int32_t* tile_open, int64_t ntiles) {
-  const int lane = threadIdx.x & 63;
-  if (tile_open) {  // ntiles flags + the open-tile count
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t <= ntiles;
-         t += (int64_t)gridDim.x * blockDim.x)
-      tile_open[t] = 0;
+// First launch of a build: zero the counters, scan flags and tile flags (ntiles + the count),
+// and, when a batch vector is given, the graph offsets (as lgnn_batch_ptr).
+__global__ __launch_bounds__(kThreads) void k_prep(int32_t* __restrict__ zero, int64_t nzero,
+                                                   int32_t* __restrict__ tile_open,
+                                                   int64_t ntiles,
+                                                   const int64_t* __restrict__ batch, int64_t M,
+                                                   int64_t B, int32_t* __restrict__ gptr) {
+  const int64_t i0 = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const int64_t step = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = i0; i < nzero; i += step) zero[i] = 0;
+  if (tile_open)
+    for (int64_t t = i0; t <= ntiles; t += step) tile_open[t] = 0;
+  if (gptr) {
+    for (int64_t i = i0; i <= M; i += step) {
+      // graphs q with prev < q <= cur start at node i (prev = batch[i-1] or -1; cur = batch[i]
+      // or B)
+      int64_t prev = i == 0 ? -1 : batch[i - 1];
+      int64_t cur = i == M ? B : batch[i];
+      if (prev < -1) prev = -1;
+      if (cur > B) cur = B;
+      for (int64_t q = prev + 1; q <= cur; ++q) gptr[q] = (int32_t)i;
+    }
   }
-  const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t base = wave0 * 64; base < E; base += nwaves * 64) {
-    const int64_t e = base + lane;
+}
+
+// Edge passes. A block takes a chunk of kChunk consecutive edges, kPer per thread, so every
+// wave sees 64 consecutive edges per step (run detection on targets: one atomic per run of equal
+// targets). Sources are binned in LDS when the chunk's sources span fewer than kBins nodes (the
+// k-NN case: a chunk covers a few graphs), so the transpose needs one global atomic per distinct
+// source per chunk instead of one per edge; otherwise per-edge global atomics.
+constexpr int kPer = 8;
+constexpr int kChunk = kThreads * kPer;
+constexpr int kBins = 4096;
+
+struct EdgeChunk {
+  int64_t s[kPer], d[kPer];
+  bool use[kPer];
+};
+
+__device__ __forceinline__ void load_chunk(EdgeChunk& c, const int64_t* __restrict__ ei,
+                                           int64_t E, int64_t N, int loops, int64_t c0,
+                                           int32_t* err) {
+#pragma unroll
+  for (int it = 0; it < kPer; ++it) {
+    const int64_t e = c0 + (int64_t)it * kThreads + threadIdx.x;
     int64_t s = -1, d = -1;
     if (e < E) {
       s = ei[e];
@@ -117,99 +148,168 @@ __global__ __launch_bounds__(kThreads) void k_count(const int64_t* __restrict__ 
     }
     const bool valid = e < E && edge_ok(s, d, N);
     if (e < E && !valid && err) atomicAdd(err, 1);
-    const bool use = valid && !(loops != LGNN_LOOPS_KEEP && s == d);
-    const Run r = wave_run(use ? d : -2 - lane);
-    if (use && r.head) atomicAdd(&cnt[d], r.len);
-    if (use && tcnt) atomicAdd(&tcnt[s], 1);
+    c.s[it] = s;
+    c.d[it] = d;
+    c.use[it] = valid && !(loops != LGNN_LOOPS_KEEP && s == d);
   }
 }
 
+// block-uniform: the chunk's smallest used source and whether all used sources fit the bins
+__device__ __forceinline__ bool chunk_binned(const EdgeChunk& c, int64_t& smin, int* red) {
+  int64_t lo = INT64_MAX, hi = -1;
+#pragma unroll
+  for (int it = 0; it < kPer; ++it)
+    if (c.use[it]) {
+      lo = c.s[it] < lo ? c.s[it] : lo;
+      hi = c.s[it] > hi ? c.s[it] : hi;
+    }
+  int lo32 = lo == INT64_MAX ? INT32_MAX : (int)lo, hi32 = (int)hi;
+  for (int o = 32; o > 0; o >>= 1) {
+    const int a = __shfl_xor(lo32, o, 64), b = __shfl_xor(hi32, o, 64);
+    lo32 = a < lo32 ? a : lo32;
+    hi32 = b > hi32 ? b : hi32;
+  }
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[2 * wave] = lo32;
+    red[2 * wave + 1] = hi32;
+  }
+  __syncthreads();
+  int L = INT32_MAX, H = -1;
+  for (int w = 0; w < kThreads / 64; ++w) {
+    L = red[2 * w] < L ? red[2 * w] : L;
+    H = red[2 * w + 1] > H ? red[2 * w + 1] : H;
+  }
+  smin = L;
+  return H < 0 || H - L < kBins;
+}
+
+__global__ __launch_bounds__(kThreads) void k_count(const int64_t* __restrict__ ei, int64_t E,
+                                                    int64_t N, int loops, int32_t* cnt,
+                                                    int32_t* tcnt, int32_t* err) {
+  __shared__ int hist[kBins];
+  __shared__ int red[2 * kThreads / 64];
+  const int lane = threadIdx.x & 63;
+  const int64_t c0 = (int64_t)blockIdx.x * kChunk;
+  EdgeChunk c;
+  load_chunk(c, ei, E, N, loops, c0, err);
+#pragma unroll
+  for (int it = 0; it < kPer; ++it) {
+    const Run r = wave_run(c.use[it] ? c.d[it] : -2 - lane);
+    if (c.use[it] && r.head) atomicAdd(&cnt[c.d[it]], r.len);
+  }
+  if (!tcnt) return;
+  int64_t smin;
+  if (chunk_binned(c, smin, red)) {
+    for (int b = threadIdx.x; b < kBins; b += kThreads) hist[b] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kPer; ++it)
+      if (c.use[it]) atomicAdd(&hist[c.s[it] - smin], 1);
+    __syncthreads();
+    for (int b = threadIdx.x; b < kBins; b += kThreads)
+      if (hist[b]) atomicAdd(&tcnt[smin + b], hist[b]);
+  } else {
+#pragma unroll
+    for (int it = 0; it < kPer; ++it)
+      if (c.use[it]) atomicAdd(&tcnt[c.s[it]], 1);
+  }
+}
+
+// fill[d] / tfill[s] start at the row offsets (set by k_scan); slots come from atomics on them,
+// so the order inside a row is arbitrary here and restored by k_finish (sort by edge id).
 __global__ __launch_bounds__(kThreads) void k_fill(const int64_t* __restrict__ ei, int64_t E,
                                                    int64_t N, int loops,
                                                    const int32_t* __restrict__ rowptr,
                                                    int32_t* fill, int32_t* col, int32_t* eid,
                                                    const int32_t* __restrict__ tptr,
                                                    int32_t* tfill, int32_t* tidx, int32_t* teid) {
+  __shared__ int hist[kBins];
+  __shared__ int red[2 * kThreads / 64];
   const int lane = threadIdx.x & 63;
-  const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t base = wave0 * 64; base < E; base += nwaves * 64) {
-    const int64_t e = base + lane;
-    int64_t s = -1, d = -1;
-    if (e < E) {
-      s = ei[e];
-      d = ei[E + e];
-    }
-    const bool use = e < E && edge_ok(s, d, N) && !(loops != LGNN_LOOPS_KEEP && s == d);
-    const Run r = wave_run(use ? d : -2 - lane);
+  const int64_t c0 = (int64_t)blockIdx.x * kChunk;
+  EdgeChunk c;
+  load_chunk(c, ei, E, N, loops, c0, nullptr);
+#pragma unroll
+  for (int it = 0; it < kPer; ++it) {
+    const int64_t e = c0 + (int64_t)it * kThreads + threadIdx.x;
+    const Run r = wave_run(c.use[it] ? c.d[it] : -2 - lane);
     int slot0 = 0;
-    if (use && r.head) slot0 = atomicAdd(&fill[d], r.len);
+    if (c.use[it] && r.head) slot0 = atomicAdd(&fill[c.d[it]], r.len);
     slot0 = __shfl(slot0, r.head_lane, 64);
-    if (use) {
-      const int pos = rowptr[d] + slot0 + (lane - r.head_lane);
-      col[pos] = (int32_t)s;
+    if (c.use[it]) {
+      const int pos = slot0 + (lane - r.head_lane);
+      col[pos] = (int32_t)c.s[it];
       eid[pos] = (int32_t)e;
-      if (tptr) {
-        const int ts = atomicAdd(&tfill[s], 1);
-        tidx[tptr[s] + ts] = (int32_t)d;
-        teid[tptr[s] + ts] = (int32_t)e;
-      }
     }
+  }
+  if (!tptr) return;
+  int64_t smin;
+  if (chunk_binned(c, smin, red)) {
+    for (int b = threadIdx.x; b < kBins; b += kThreads) hist[b] = 0;
+    __syncthreads();
+    int rank[kPer];
+#pragma unroll
+    for (int it = 0; it < kPer; ++it)
+      rank[it] = c.use[it] ? atomicAdd(&hist[c.s[it] - smin], 1) : 0;
+    __syncthreads();
+    for (int b = threadIdx.x; b < kBins; b += kThreads) {
+      const int n = hist[b];
+      if (n) hist[b] = atomicAdd(&tfill[smin + b], n);  // the chunk's base slot for source b
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kPer; ++it)
+      if (c.use[it]) {
+        const int pos = hist[c.s[it] - smin] + rank[it];
+        tidx[pos] = (int32_t)c.d[it];
+        teid[pos] = (int32_t)(c0 + (int64_t)it * kThreads + threadIdx.x);
+      }
+  } else {
+#pragma unroll
+    for (int it = 0; it < kPer; ++it)
+      if (c.use[it]) {
+        const int pos = atomicAdd(&tfill[c.s[it]], 1);
+        tidx[pos] = (int32_t)c.d[it];
+        teid[pos] = (int32_t)(c0 + (int64_t)it * kThreads + threadIdx.x);
+      }
   }
 }
 
-// Both degree scans (blockIdx.y = 0: rowptr from cnt, 1: tptr from tcnt) in two launches:
-//   k_scan_sums:  per 1024-element block, the sum of (count + add)
-//   k_scan_apply: each block adds up the sums of the blocks before it (in block order), scans its
-//                 own elements (4 per thread, coalesced) and writes the exclusive prefix; the
-//                 rowptr blocks also write dis[i] = deg_i^-1/2 (GCN normalisation; deg 0 -> 0).
+// Both degree scans (blockIdx.y = 0: rowptr from cnt, 1: tptr from tcnt) in ONE launch over
+// 1024-element blocks: block b sums its elements and publishes the sum (flagged) in stat[b] at
+// once; its 256 threads then read the sums of blocks 0..b-1 in parallel (each spinning until its
+// entry is flagged — a block publishes before it waits, so the spin always ends) and add them
+// in a fixed order; then the block writes the exclusive prefix of its elements (4 per thread,
+// coalesced), the first free slot of each row (fill = rowptr) and, for rowptr,
+// dis[i] = deg_i^-1/2 (GCN normalisation; deg 0 -> 0). One round of cross-block latency instead
+// of a chain of them.
 constexpr int kScanT = 256;
 constexpr int kScanPer = 4;
 constexpr int kScanBlk = kScanT * kScanPer;
+constexpr int32_t kScanFlag = 0x40000000;  // prefix values stay below 2^30 (N + E <= INT32_MAX / 2)
 
 __device__ __forceinline__ int scan_val(const int32_t* __restrict__ c, int64_t i, int64_t N,
                                         int add) {
   return i < N ? c[i] + add : 0;
 }
 
-__global__ __launch_bounds__(kScanT) void k_scan_sums(const int32_t* __restrict__ cnt,
-                                                      const int32_t* __restrict__ tcnt, int64_t N,
-                                                      int add, int32_t* __restrict__ bsum) {
-  __shared__ int red[kScanT / 64];
-  const int32_t* __restrict__ c = blockIdx.y ? tcnt : cnt;
-  const int64_t base = (int64_t)blockIdx.x * kScanBlk;
-  int s = 0;
-#pragma unroll
-  for (int j = 0; j < kScanPer; ++j) s += scan_val(c, base + j * kScanT + threadIdx.x, N, add);
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int t = 0;
-    for (int w = 0; w < kScanT / 64; ++w) t += red[w];
-    bsum[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = t;
-  }
-}
-
-__global__ __launch_bounds__(kScanT) void k_scan_apply(const int32_t* __restrict__ cnt,
-                                                       const int32_t* __restrict__ tcnt,
-                                                       int64_t N, int add,
-                                                       const int32_t* __restrict__ bsum,
-                                                       int32_t* __restrict__ rowptr,
-                                                       int32_t* __restrict__ tptr,
-                                                       float* __restrict__ dis) {
-  __shared__ int red[kScanT / 64];
+__global__ __launch_bounds__(kScanT) void k_scan(const int32_t* __restrict__ cnt,
+                                                 const int32_t* __restrict__ tcnt, int64_t N,
+                                                 int add, int32_t* stat,
+                                                 int32_t* __restrict__ rowptr,
+                                                 int32_t* __restrict__ tptr,
+                                                 int32_t* __restrict__ fill,
+                                                 int32_t* __restrict__ tfill,
+                                                 float* __restrict__ dis) {
   __shared__ int wsc[kScanT / 64];
+  __shared__ int s_pre;
   const bool tr = blockIdx.y == 1;
   const int32_t* __restrict__ c = tr ? tcnt : cnt;
   int32_t* __restrict__ out = tr ? tptr : rowptr;
+  int32_t* __restrict__ fl = tr ? tfill : fill;
+  int32_t* st = stat + (int64_t)blockIdx.y * gridDim.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // prefix of the preceding blocks
-  int pre = 0;
-  for (int b = tid; b < (int)blockIdx.x; b += kScanT) pre += bsum[(int64_t)blockIdx.y * gridDim.x + b];
-  for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
-  if (lane == 0) red[wave] = pre;
-  // this thread's 4 consecutive elements
   const int64_t i0 = (int64_t)blockIdx.x * kScanBlk + (int64_t)tid * kScanPer;
   int v[kScanPer];
   int s = 0;
@@ -226,12 +326,30 @@ __global__ __launch_bounds__(kScanT) void k_scan_apply(const int32_t* __restrict
   }
   if (lane == 63) wsc[wave] = x;
   __syncthreads();
-  int run = red[0] + red[1] + red[2] + red[3] + x - s;
+  if (tid == 0)
+    __hip_atomic_store(&st[blockIdx.x], (wsc[0] + wsc[1] + wsc[2] + wsc[3]) | kScanFlag,
+                       __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  int pre = 0;  // sums of the preceding blocks, thread-strided, then combined in wave order
+  for (int j = tid; j < (int)blockIdx.x; j += kScanT) {
+    int f;
+    while (((f = __hip_atomic_load(&st[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) &
+            kScanFlag) == 0)
+      __builtin_amdgcn_s_sleep(1);
+    pre += f & (kScanFlag - 1);
+  }
+  for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
+  __shared__ int wpre[kScanT / 64];
+  if (lane == 0) wpre[wave] = pre;
+  __syncthreads();
+  if (tid == 0) s_pre = wpre[0] + wpre[1] + wpre[2] + wpre[3];
+  __syncthreads();
+  int run = s_pre + x - s;
   for (int w = 0; w < wave; ++w) run += wsc[w];
 #pragma unroll
   for (int j = 0; j < kScanPer; ++j) {
     const int64_t i = i0 + j;
     if (i <= N) out[i] = run;
+    if (i < N) fl[i] = run;
     if (!tr && dis && i < N) {
       const int deg = v[j];
       dis[i] = deg > 0 ? 1.0f / sqrtf((float)deg) : 0.0f;
@@ -258,7 +376,7 @@ __device__ __forceinline__ void sort_row(KP key, VP val, int n) {
 
 // blockIdx.y = 0: target CSR (rowptr/col/eid/w); 1: source CSR (tptr/tidx/teid/tw).
 // Weight of entry (row i, neighbour j): GCN (dis(src) * 1) * dis(dst) = dis(j) * dis(i).
-__global__ __launch_bounds__(kThreads) void k_finish(int64_t N, int64_t E, int add_loop, int norm,
+__global__ __launch_bounds__(kFinT) void k_finish(int64_t N, int64_t E, int add_loop, int norm,
                                                      const int32_t* __restrict__ rowptr,
                                                      int32_t* col, int32_t* eid, float* w,
                                                      const int32_t* __restrict__ tptr,
@@ -274,13 +392,13 @@ __global__ __launch_bounds__(kThreads) void k_finish(int64_t N, int64_t E, int a
   int32_t* idx = tr ? tidx : col;
   int32_t* key = tr ? teid : eid;
   float* wt = tr ? tw : w;
-  const int64_t i0 = (int64_t)blockIdx.x * kThreads;
+  const int64_t i0 = (int64_t)blockIdx.x * kFinT;
   const int64_t i = i0 + threadIdx.x;
-  const int64_t iend = i0 + kThreads < N ? i0 + kThreads : N;
+  const int64_t iend = i0 + kFinT < N ? i0 + kFinT : N;
   const int eb = ptr[i0], ee = ptr[iend];
   const bool staged = ee - eb <= kFinishCap;
   if (staged) {
-    for (int j = eb + threadIdx.x; j < ee; j += kThreads) {
+    for (int j = eb + threadIdx.x; j < ee; j += kFinT) {
       s_key[j - eb] = key[j];
       s_val[j - eb] = idx[j];
     }
@@ -304,7 +422,7 @@ __global__ __launch_bounds__(kThreads) void k_finish(int64_t N, int64_t E, int a
   }
   __syncthreads();
   if (staged) {
-    for (int j = eb + threadIdx.x; j < ee; j += kThreads) {
+    for (int j = eb + threadIdx.x; j < ee; j += kFinT) {
       idx[j] = s_val[j - eb];
       key[j] = s_key[j - eb];
     }
@@ -402,18 +520,27 @@ extern "C" size_t lgnn_graph_workspace_bytes(int64_t num_nodes, int64_t num_edge
 extern "C" int lgnn_graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loops,
                                 int norm, int32_t* rowptr, int32_t* col, float* w, int32_t* tptr,
                                 int32_t* tidx, float* tw, int32_t* tmap, int32_t* tile_open,
+                                const int64_t* batch, int64_t num_graphs, int32_t* gptr,
                                 int32_t* err_count, void* workspace,
                                 size_t workspace_bytes, void* stream) {
   if (N < 0 || E < 0 || loops < 0 || loops > 2 || norm < 0 || norm > 1) return LGNN_EINVAL;
   if (!rowptr || !col || (E > 0 && !edge_index)) return LGNN_EINVAL;
-  if (N + E > INT32_MAX) return LGNN_EINVAL;
+  if (N + E >= (int64_t)1 << 30) return LGNN_EINVAL;
+  if (gptr && (num_graphs < 0 || (N > 0 && !batch))) return LGNN_EINVAL;
   if ((tptr == nullptr) != (tidx == nullptr)) return LGNN_EINVAL;
   if (tmap && !tptr) return LGNN_EINVAL;
   if (workspace_bytes < ws_total(N, E) || !workspace) return LGNN_ENOSPC;
   hipStream_t s = as_stream(stream);
   const int add_loop = loops == LGNN_LOOPS_KEEP ? 0 : 1;
   GraphWs ws = carve(workspace, N, E);
-  if (hipMemsetAsync(ws.err, 0, ws.zero_bytes, s) != hipSuccess) return (int)hipGetLastError();
+  {
+    const int64_t nzero = (int64_t)(ws.zero_bytes / 4);
+    const int64_t ntiles = (N + 63) / 64;
+    hipLaunchKernelGGL(k_prep, dim3(grid_for(nzero > N + 1 ? nzero : N + 1, 1024)),
+                       dim3(kThreads), 0, s, ws.err, nzero, tile_open, ntiles, batch, N,
+                       num_graphs, gptr);
+    LGNN_LAUNCH_CHECK();
+  }
   if (N == 0) {
     if (hipMemsetAsync(rowptr, 0, 4, s) != hipSuccess) return (int)hipGetLastError();
     if (tptr && hipMemsetAsync(tptr, 0, 4, s) != hipSuccess) return (int)hipGetLastError();
@@ -421,31 +548,26 @@ extern "C" int lgnn_graph_build(const int64_t* edge_index, int64_t E, int64_t N,
       return (int)hipGetLastError();
     return LGNN_OK;
   }
-  if (E > 0 || tile_open) {
-    hipLaunchKernelGGL(k_count, dim3(grid_for(E > N ? E : N, 2048)), dim3(kThreads), 0, s,
-                       edge_index, E, N,
-                       loops, ws.cnt, tptr ? ws.tcnt : nullptr, ws.err, tile_open,
-                       (N + 63) / 64);
+  if (E > 0) {
+    hipLaunchKernelGGL(k_count, dim3((unsigned)((E + kChunk - 1) / kChunk)), dim3(kThreads), 0,
+                       s, edge_index, E, N, loops, ws.cnt, tptr ? ws.tcnt : nullptr, ws.err);
     LGNN_LAUNCH_CHECK();
   }
   {
     const int64_t nblk = (N + 1 + kScanBlk - 1) / kScanBlk;
-    if (nblk > INT32_MAX / 2) return LGNN_EINVAL;
     dim3 sg((unsigned)nblk, tptr ? 2u : 1u);
-    hipLaunchKernelGGL(k_scan_sums, sg, dim3(kScanT), 0, s, ws.cnt, ws.tcnt, N, add_loop,
-                       ws.bsum);
-    LGNN_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_scan_apply, sg, dim3(kScanT), 0, s, ws.cnt, ws.tcnt, N, add_loop,
-                       ws.bsum, rowptr, tptr, ws.dis);
+    hipLaunchKernelGGL(k_scan, sg, dim3(kScanT), 0, s, ws.cnt, ws.tcnt, N, add_loop, ws.stat,
+                       rowptr, tptr, ws.fill, ws.tfill, ws.dis);
     LGNN_LAUNCH_CHECK();
   }
   if (E > 0) {
-    hipLaunchKernelGGL(k_fill, dim3(grid_for(E, 2048)), dim3(kThreads), 0, s, edge_index, E, N,
-                       loops, rowptr, ws.fill, col, ws.eid, tptr, ws.tfill, tidx, ws.teid);
+    hipLaunchKernelGGL(k_fill, dim3((unsigned)((E + kChunk - 1) / kChunk)), dim3(kThreads), 0,
+                       s, edge_index, E, N, loops, rowptr, ws.fill, col, ws.eid, tptr, ws.tfill,
+                       tidx, ws.teid);
     LGNN_LAUNCH_CHECK();
   }
-  dim3 fg((unsigned)((N + kThreads - 1) / kThreads), tptr ? 2u : 1u);
-  hipLaunchKernelGGL(k_finish, fg, dim3(kThreads), 0, s, N, E, add_loop, norm, rowptr, col,
+  dim3 fg((unsigned)((N + kFinT - 1) / kFinT), tptr ? 2u : 1u);
+  hipLaunchKernelGGL(k_finish, fg, dim3(kFinT), 0, s, N, E, add_loop, norm, rowptr, col,
                      ws.eid, w, tptr, tidx, ws.teid, tw, ws.dis, ws.err, err_count, tile_open);
   LGNN_LAUNCH_CHECK();
   if (tmap) {

@@ -25,6 +25,7 @@ struct AdamJobs {
   int n;
 };
 
+// blockIdx.y = tensor (uniform: its pointers are scalar loads), blockIdx.x strides its elements
 __global__ __launch_bounds__(kT) void k_adam(AdamJobs J, float* __restrict__ step,
                                              unsigned int* __restrict__ ticket, float lr,
                                              float beta1, float beta2, float eps, float wd,
@@ -33,29 +34,30 @@ __global__ __launch_bounds__(kT) void k_adam(AdamJobs J, float* __restrict__ ste
   const float bc1 = 1.f - powf(beta1, t);
   const float bc2s = sqrtf(1.f - powf(beta2, t));
   const float step_size = lr / bc1;
-  const int64_t total = J.off[J.n];
-  int j = 0;
-  for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * kT) {
-    while (i >= J.off[j + 1]) ++j;
-    const int64_t k = i - J.off[j];
-    float p = J.p[j][k];
-    float g = J.g[j][k];
+  const int j = blockIdx.y;
+  const int64_t n = J.off[j + 1] - J.off[j];
+  float* __restrict__ P = J.p[j];
+  const float* __restrict__ G = J.g[j];
+  float* __restrict__ Mv = J.m[j];
+  float* __restrict__ Vv = J.v[j];
+  for (int64_t k = (int64_t)blockIdx.x * kT + threadIdx.x; k < n; k += (int64_t)gridDim.x * kT) {
+    float p = P[k];
+    float g = G[k];
     if (maximize) g = -g;
     if (decoupled) p *= 1.f - lr * wd;
     else g = fmaf(wd, p, g);
-    const float m = fmaf(beta1, J.m[j][k], (1.f - beta1) * g);
-    const float v = fmaf(beta2, J.v[j][k], (1.f - beta2) * g * g);
-    J.m[j][k] = m;
-    J.v[j][k] = v;
+    const float m = fmaf(beta1, Mv[k], (1.f - beta1) * g);
+    const float v = fmaf(beta2, Vv[k], (1.f - beta2) * g * g);
+    Mv[k] = m;
+    Vv[k] = v;
     p -= step_size * m / (sqrtf(v) / bc2s + eps);
-    J.p[j][k] = p;
+    P[k] = p;
   }
   if (!advance) return;
   __syncthreads();
   if (threadIdx.x == 0) {
     __threadfence();
-    if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
+    if (atomicAdd(ticket, 1u) == gridDim.x * gridDim.y - 1) {
       step[0] = t;
       *ticket = 0u;
       __threadfence();
@@ -86,12 +88,14 @@ extern "C" int lgnn_adam_step(int n, float* const* params, const float* const* g
     J.v[i] = exp_avg_sq[i];
     J.off[i + 1] = J.off[i] + numels[i];
   }
-  const int64_t total = J.off[n];
-  int64_t g = (total + kT - 1) / kT;
-  if (g < 1) g = 1;
-  if (g > 1024) g = 1024;
-  hipLaunchKernelGGL(k_adam, dim3((unsigned)g), dim3(kT), 0, as_stream(stream), J, step, ticket,
-                     lr, beta1, beta2, eps, weight_decay, decoupled, maximize, advance);
+  int64_t mx = 1;
+  for (int i = 0; i < n; ++i) mx = numels[i] > mx ? numels[i] : mx;
+  // few workgroups (the ticket is one contended atomic per workgroup): 8+ elements per thread
+  int64_t g = (mx + 8 * kT - 1) / (8 * kT);
+  if (g > 64) g = 64;
+  hipLaunchKernelGGL(k_adam, dim3((unsigned)g, (unsigned)(n > 0 ? n : 1)), dim3(kT), 0,
+                     as_stream(stream), J, step, ticket, lr, beta1, beta2, eps, weight_decay,
+                     decoupled, maximize, advance);
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
 }

@@ -49,7 +49,7 @@ class Graph:
         self._csr: dict[str, Csr] = {}
         self._aux: dict[str, torch.Tensor] = {}
         self.batch = None
-        self.gptr = None
+        self._gptr = None
         self.num_graphs = None
         if batch is not None:
             self.set_batch(batch, num_graphs)
@@ -67,9 +67,16 @@ class Graph:
             # PyG: int(batch.max()) + 1 (a device->host read; pass num_graphs to avoid it)
             num_graphs = int(self.batch[-1].item()) + 1 if self.num_nodes > 0 else 0
         self.num_graphs = int(num_graphs)
-        self.gptr = torch.empty(self.num_graphs + 1, dtype=torch.int32, device=self.device)
-        _lib.call("lgnn_batch_ptr", _lib.ptr(self.batch), self.num_nodes, self.num_graphs,
-                  _lib.ptr(self.gptr), _lib.stream(self.device))
+        self._gptr = None  # computed by the first CSR build, or on first use
+
+    @property
+    def gptr(self) -> torch.Tensor | None:
+        """int32 [num_graphs + 1] graph offsets (Batch.ptr)."""
+        if self._gptr is None and self.batch is not None:
+            self._gptr = torch.empty(self.num_graphs + 1, dtype=torch.int32, device=self.device)
+            _lib.call("lgnn_batch_ptr", _lib.ptr(self.batch), self.num_nodes, self.num_graphs,
+                      _lib.ptr(self._gptr), _lib.stream(self.device))
+        return self._gptr
 
     def csr(self, kind: str) -> Csr:
         if kind in self._csr:
@@ -91,11 +98,15 @@ class Graph:
         lib = _lib.load()
         ws_bytes = lib.lgnn_graph_workspace_bytes(n, e)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        gptr = None  # the graph offsets ride along with the first build
+        if self._gptr is None and self.batch is not None:
+            gptr = self._gptr = torch.empty(self.num_graphs + 1, dtype=torch.int32, device=dev)
         _lib.call("lgnn_graph_build", _lib.ptr(self.edge_index), e, n, loops, norm,
                   _lib.ptr(c.rowptr), _lib.ptr(c.col), _lib.ptr(c.w), _lib.ptr(c.tptr),
                   _lib.ptr(c.tidx), _lib.ptr(c.tw), _lib.ptr(c.tmap), _lib.ptr(c.tile_open),
-                  _lib.ptr(c.err), _lib.ptr(ws), ws_bytes,
-                  _lib.stream(dev))
+                  _lib.ptr(self.batch) if gptr is not None else None,
+                  self.num_graphs if gptr is not None else 0, _lib.ptr(gptr), _lib.ptr(c.err),
+                  _lib.ptr(ws), ws_bytes, _lib.stream(dev))
         self._csr[kind] = c
         return c
 

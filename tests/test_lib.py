@@ -57,7 +57,10 @@ def test_argument_validation_without_gpu():
     assert lib.lgnn_bwd_num_partials(100, 0, 128, 0) == -22
     assert lib.lgnn_bwd_num_partials(65536, 128, 128, 0) > 0
     assert lib.lgnn_graph_build(None, 0, -1, 1, 1, None, None, None, None, None, None, None,
-                                None, None, None, 0, None) == -22
+                                None, None, 0, None, None, None, 0, None) == -22
+    # too large for the 30-bit chained scan
+    assert lib.lgnn_graph_build(None, 1 << 30, 1, 1, 1, 1, 1, None, None, None, None, None,
+                                None, None, 0, None, None, None, 0, None) == -22
 
 
 def test_product_path_refuses_cpu_tensors():
