@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 5
+#define LGNN_ABI_VERSION 6
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -262,6 +262,22 @@ int lgnn_gcn_stack_fwd(const float* X, int64_t M, int d_in, int has_in_proj,
                        const int32_t* rowptr, const int32_t* col, const float* w, int L,
                        const float* const* W, const float* const* b, const int* widths,
                        float* const* H, const int32_t* tile_open, void* stream);
+/* Split-3 variant of lgnn_gcn_stack_fwd: the same math and arguments, the GEMMs on bf16 MFMA at
+ * fp32 accuracy — every operand held as three bf16 planes (x = hi + mid + lo to 2^-24) and each
+ * product taken as the six plane products that matter (liblgnn stack3.hip). `planes` holds the
+ * weights of layers 0..L as written by lgnn_weight_planes (in place of W). L >= 1. */
+int lgnn_gcn_stack_fwd_s3(const float* X, int64_t M, int d_in, int has_in_proj,
+                          const int32_t* rowptr, const int32_t* col, const float* w, int L,
+                          const uint16_t* planes, const float* const* b, const int* widths,
+                          float* const* H, const int32_t* tile_open, void* stream);
+/* Weight planes for the split-3 kernels: nl layers, W[l] [widths[l+1], widths[l]] fp32
+ * (torch Linear layout; widths <= 128, multiples of 4) -> planes[l][3][128][128] bf16 (zero
+ * padded, feature order perm16), lgnn_weight_planes_bytes(nl) bytes; planes_t (nullable, same
+ * size) also gets the transposed planes. One launch; rerun whenever the weights change. */
+size_t lgnn_weight_planes_bytes(int nl);
+int lgnn_weight_planes(int nl, const float* const* W, const int* widths, uint16_t* planes,
+                       uint16_t* planes_t, void* stream);
+
 /* Tiles: 64 consecutive node rows. open[t] = 1 when an edge joins tile t to another tile (its
  * layers then depend on other tiles) or when the tile holds more than 1024 CSR entries; the
  * fused stacks skip open tiles. open has lgnn_tile_count(N) + 1 entries: the last one counts the

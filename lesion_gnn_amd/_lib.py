@@ -64,6 +64,9 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_gat_bwd_num_partials": (I32, [I64]),
     "lgnn_gat_bwd_node": (I32, [P, P, P, P, P, P, P, P, P, P, P, I64, I32, I32, P, P, I32, P]),
     "lgnn_gcn_stack_fwd": (I32, [P, I64, I32, I32, P, P, P, I32, P, P, P, P, P, P]),
+    "lgnn_gcn_stack_fwd_s3": (I32, [P, I64, I32, I32, P, P, P, I32, P, P, P, P, P, P]),
+    "lgnn_weight_planes_bytes": (SZ, [I32]),
+    "lgnn_weight_planes": (I32, [I32, P, P, P, P, P]),
     "lgnn_tile_count": (I32, [I64]),
     "lgnn_tile_open": (I32, [P, P, I64, P, P]),
     "lgnn_node_linear_fwd_tiles": (I32, [P, I64, I32, P, P, P, F32, P, P, I32, I32, P, P, P, I32,
@@ -71,7 +74,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_bn_bwd_apply": (I32, [P, P, P, I64, I32, P, P, P, P, P, F64, I32, P, P, P, P]),
 }
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _lib = None
 

@@ -1,0 +1,567 @@
+// Fused GCN stack on bf16 MFMA at fp32 accuracy ("split-3"): every fp32 GEMM operand x is held as
+// three bf16 planes x = x_hi + x_mid + x_lo (+ r, |r| <= 2^-24 |x|; each plane is the RNE bf16 of
+// what the planes above it left over), and a product a.b is taken as the six plane products
+//   a_lo b_hi + a_mid b_mid + a_hi b_lo + a_mid b_hi + a_hi b_mid + a_hi b_hi
+// (the three dropped ones are below 2^-24 relative). Each bf16 x bf16 product is exact in fp32 and
+// the MFMA accumulates in fp32, so the result carries fp32-class error (a few ulp of the sum of
+// |a.b|), like the fp32 MFMA chain — at 16 / 6 = 2.7x its rate: gfx950 runs
+// v_mfma_f32_32x32x16_bf16 at 16x the FLOP rate of v_mfma_f32_32x32x2_f32 and has no xf32.
+//
+// k_s3_fwd is the split-3 twin of k_stack_fwd (tile.hip): in_proj + L x ELU(GCNConv) for the
+// tiles no edge leaves, PyG's association H_l = ELU(Â (H_{l-1} W_l^T) + b_l). Per layer:
+//   GEMM1  P = H W_l^T          A operand = H planes (LDS image), B operand = W_l planes
+//                               (registers, loaded a layer ahead, pre-split by k_wplanes)
+//   GEMM2  Z^T = P^T Â^T        A operand = P straight from GEMM1's accumulators (split in
+//                               registers; the accumulator's row order is the operand's k order),
+//                               B operand = Â_tile planes (LDS, built once per tile)
+//   epilogue  +b, ELU; H_l -> HBM (fp32, 16-B stores) and -> the LDS planes of the next layer
+// GEMM2's output has the node on the lane and four consecutive features per register group, so
+// the next layer's H planes are written with 8-byte stores and read back as whole MFMA fragments:
+// one LDS round trip per layer. When every weight of a tile's Â is exact in bf16 (k-regular
+// k-NN graphs: 1/k with k a power of two) GEMM2 takes three plane products instead of six.
+//
+// Feature index order: the planes store feature k at position perm16(k) (bits 2 and 3 of k
+// swapped), which is the k order an MFMA accumulator hands to the next MFMA; weights, images and
+// accumulators all use it, so every product pairs equal k.
+#include "common.h"
+#include "tile.h"
+#include "tile_util.h"
+
+// Timing-only ablation builds (tools/s3_probe.py): -DLGNN_S3_ABLATE=<mask> removes phases of
+// k_s3_fwd (1 GEMM1 MFMAs, 2 GEMM2 MFMAs, 4 H stores, 8 ELU, 16 epilogue plane split, 32 weight
+// reloads, 64 next-tile X loads). The product build is mask 0; ablated libraries are built
+// outside the package and never loaded by it.
+#ifndef LGNN_S3_ABLATE
+#define LGNN_S3_ABLATE 0
+#endif
+
+// Diagnostic build only (-DLGNN_S3_STAMPS, tools/s3_probe.py stamps): thread 0 of each block
+// records s_memtime at phase boundaries of k_s3_fwd; never compiled into the product library.
+#ifdef LGNN_S3_STAMPS
+__device__ unsigned long long lgnn_s3_stamp_buf[1024 * 64];
+#define S3STAMP()                                                                  \
+  do {                                                                             \
+    if (threadIdx.x == 0 && stamp_i < 64)                                          \
+      lgnn_s3_stamp_buf[blockIdx.x * 64 + stamp_i] = __builtin_amdgcn_s_memtime(); \
+    ++stamp_i;                                                                     \
+  } while (0)
+#else
+#define S3STAMP() \
+  do {            \
+  } while (0)
+#endif
+
+namespace lgnn_s3 {
+using namespace lgnn_tile;
+constexpr int S3ABL = LGNN_S3_ABLATE;
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int WP = 128;           // padded width of the weight planes and the H image
+constexpr int PLANE = WP * WP;    // bf16 elements per weight plane
+constexpr int AROW = WP * 2;      // bytes per H-image row (chunk-swizzled, no padding)
+constexpr int ADJ_LD = 72;        // Â plane row stride in bf16 (144 B: conflict-free b128 rows)
+constexpr int ADJ_PLANE = TM * ADJ_LD * 2;  // bytes per Â plane
+
+__device__ __forceinline__ constexpr int perm16(int k) {
+  return (k & ~12) | ((k & 4) << 1) | ((k & 8) >> 1);
+}
+
+// (a, b) -> three packed bf16 pairs (a in the low half), x = hi + mid + lo to 2^-24.
+struct Split2 {
+  uint32_t p[3];
+};
+__device__ __forceinline__ Split2 split2(float a, float b) {
+  Split2 s;
+  f32x2 v = {a, b};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const uint32_t q = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+    s.p[i] = q;
+    if (i < 2) {
+      const f32x2 back = {__uint_as_float(q << 16), __uint_as_float(q & 0xffff0000u)};
+      v -= back;
+    }
+  }
+  return s;
+}
+
+// four consecutive fp32 -> three planes of four bf16 (8 bytes each)
+__device__ __forceinline__ void split4(f32x4 v, u32x2 (&o)[3]) {
+  const Split2 a = split2(v[0], v[1]), b = split2(v[2], v[3]);
+#pragma unroll
+  for (int p = 0; p < 3; ++p) o[p] = u32x2{a.p[p], b.p[p]};
+}
+
+__device__ __forceinline__ f32x16 mfma16(u32x4 a, u32x4 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+// c += a.b at fp32 accuracy: the six plane products, smallest first.
+__device__ __forceinline__ f32x16 mfma_s3(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x16 c) {
+  c = mfma16(a[2], b[0], c);
+  c = mfma16(a[1], b[1], c);
+  c = mfma16(a[0], b[2], c);
+  c = mfma16(a[1], b[0], c);
+  c = mfma16(a[0], b[1], c);
+  return mfma16(a[0], b[0], c);
+}
+// b exact in bf16 (b_mid = b_lo = 0): three products.
+__device__ __forceinline__ f32x16 mfma_s3_bexact(const u32x4 (&a)[3], u32x4 b0, f32x16 c) {
+  c = mfma16(a[2], b0, c);
+  c = mfma16(a[1], b0, c);
+  return mfma16(a[0], b0, c);
+}
+
+// Byte offset of (row, 4-aligned feature k) in an H-image plane: position perm16(k), 16-B chunk
+// XOR-swizzled by row & 15 so a b128 read of one chunk by 16 rows is conflict-free.
+__device__ __forceinline__ int ap_off(int row, int k) {
+  const int p = perm16(k);
+  return row * AROW + ((((p >> 3) ^ (row & 15))) << 4) + ((p & 7) << 1);
+}
+__device__ __forceinline__ int ap_chunk(int row, int c) {
+  return row * AROW + ((c ^ (row & 15)) << 4);
+}
+
+__device__ __forceinline__ u32x4 lds16(const unsigned char* p) {
+  return *reinterpret_cast<const u32x4*>(p);
+}
+__device__ __forceinline__ void sts8(unsigned char* p, u32x2 v) {
+  *reinterpret_cast<u32x2*>(p) = v;
+}
+
+// ------------------------------------------------------------------------------------------
+// Weight planes: W_l [N][K] fp32 -> bf16 planes of W_l[n][perm16(k)], zero-padded to 128 x 128,
+// stored in MFMA fragment order so that one wave's load of a k-step fragment is 1 KiB contiguous:
+//   Wp[l][plane][n / 32][s][h][n % 32][8]  holds  phys positions 16 s + 8 h .. + 7 of row n
+// (lane h * 32 + n % 32 of wave n / 32 loads k-step s with one 16-B load). With WpT also the
+// transposed planes (rows k, positions perm16(n)) in the same order: the backward's dH = G W_l
+// operand. One thread per (layer, n, 4 consecutive k).
+// ------------------------------------------------------------------------------------------
+// element index of (row, phys position) within one fragment-ordered 128 x 128 plane
+__device__ __forceinline__ int frag_index(int row, int phys) {
+  return ((((row >> 5) * 8 + (phys >> 4)) * 2 + ((phys >> 3) & 1)) * 32 + (row & 31)) * 8 +
+         (phys & 7);
+}
+
+struct PlaneArgs {
+  const float* W[LGNN_MAX_STACK];
+  int N[LGNN_MAX_STACK];
+  int K[LGNN_MAX_STACK];
+};
+
+__global__ __launch_bounds__(256) void k_wplanes(PlaneArgs a, int nl, uint16_t* __restrict__ Wp,
+                                                 uint16_t* __restrict__ WpT) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int l = i / (WP * WP / 4);
+  if (l >= nl) return;
+  const int n = (i / (WP / 4)) % WP, k = 4 * (i % (WP / 4));
+  const int N = a.N[l], K = a.K[l];
+  const f32x4 v = (n < N && k < K) ? ld4(a.W[l] + (int64_t)n * K + k) : zero4();
+  u32x2 o[3];
+  split4(v, o);
+  uint16_t* base = Wp + (size_t)l * 3 * PLANE;
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+    *reinterpret_cast<u32x2*>(base + p * PLANE + frag_index(n, perm16(k))) = o[p];
+  if (WpT) {
+    uint16_t* bt = WpT + (size_t)l * 3 * PLANE;
+    const int pn = perm16(n);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      bt[p * PLANE + frag_index(k + 0, pn)] = (uint16_t)(o[p][0] & 0xffffu);
+      bt[p * PLANE + frag_index(k + 1, pn)] = (uint16_t)(o[p][0] >> 16);
+      bt[p * PLANE + frag_index(k + 2, pn)] = (uint16_t)(o[p][1] & 0xffffu);
+      bt[p * PLANE + frag_index(k + 3, pn)] = (uint16_t)(o[p][1] >> 16);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Fused forward
+// ------------------------------------------------------------------------------------------
+struct FwdSmem {
+  unsigned char Ap[3][TM * AROW];     // H_{l-1} (or X) planes, 48 KiB
+  unsigned char Adj[3][ADJ_PLANE];    // Â_tile planes [target][perm16(source)], 27 KiB; the first
+                                      // 16 KiB first hold Â in fp32 while it is summed
+  float bias[LGNN_MAX_STACK][WP];     // zero past each layer's width
+  int rp[TM + 1];
+  int flag;                           // some Â weight of the tile is not exact in bf16
+};
+
+// threadIdx.x through an empty asm: addresses derived from it cannot be hoisted out of the tile
+// loop or merged across phases (held over the whole loop they cost ~60 registers); each phase
+// recomputes its own in a few VALU ops.
+__device__ __forceinline__ int fresh_tid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
+// W_l planes fragment of this lane: row n = 32 * wave + li, chunk 2s + h of each plane.
+__device__ __forceinline__ void load_wf(u32x4 (&wf)[3][8], const uint16_t* __restrict__ Wp,
+                                        int l) {
+  const int t = fresh_tid(), lane = t & 63, wave = t >> 6;
+  // fragment order (k_wplanes): one contiguous 1-KiB wave load per plane and k-step
+  const uint16_t* base = Wp + (size_t)l * 3 * PLANE + wave * 8 * 512 + lane * 8;
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      wf[p][s] = *reinterpret_cast<const u32x4*>(base + p * PLANE + 512 * s);
+}
+
+// ELU(alpha = 1) as exp2-based exp(min(x, 0)) - 1: five VALU ops. Against PyTorch's expm1 form
+// the absolute difference is below 1e-7 (v_exp_f32 is ~1 ulp; the argument's rounding moves
+// exp(x) by at most |x| e^x 2^-24 ln 2 <= 2.3e-8), i.e. fp32 rounding level for |ELU| <= 1.
+__device__ __forceinline__ float elu_s3(float x) {
+  const float e = __builtin_amdgcn_exp2f(fminf(x, 0.f) * 1.44269504088896341f) - 1.f;
+  return x > 0.f ? x : e;
+}
+
+// Epilogue of one layer from the Z^T accumulators (z0: node li, z1: node 32 + li; register r:
+// feature 32 * wave + (r & 3) + 8 * (r >> 2) + 4h): + bias, ELU, H_l -> HBM, planes -> Ap.
+template <bool ELU, bool PLANES>
+__device__ __forceinline__ void epilogue(FwdSmem& sm, const f32x16& z0, const f32x16& z1,
+                                         const float* bias, Buf hb, int N, int64_t r0) {
+  const int t = fresh_tid(), lane = t & 63, wave = t >> 6;
+  const int h = lane >> 5, li = lane & 31;
+  f32x4 bv[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) bv[g] = ld4(bias + 32 * wave + 8 * g + 4 * h);
+  const int rowb = (int)(r0 * N * 4);  // byte offset of the tile's first row (< 2 GiB: host)
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const int m = 32 * a + li;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int n0 = 32 * wave + 8 * g + 4 * h;
+      const f32x16& z = a ? z1 : z0;
+      f32x4 v = f32x4{z[4 * g], z[4 * g + 1], z[4 * g + 2], z[4 * g + 3]} + bv[g];
+      if (ELU && !(S3ABL & 8)) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = elu_s3(v[j]);
+      }
+      // columns past N: an offset past the buffer's range, so the store is dropped (no branch)
+      if (!(S3ABL & 4)) bst4(hb, n0 < N ? rowb + (m * N + n0) * 4 : INT32_MAX - 15, v);
+      if (PLANES) {
+        u32x2 o[3];
+        if (S3ABL & 16)
+          o[0] = o[1] = o[2] = u32x2{__float_as_uint(v[0]), __float_as_uint(v[1])};
+        else
+          split4(v, o);
+        const int off = ap_off(m, n0);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) sts8(sm.Ap[p] + off, o[p]);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one (row block, group) at a time
+    }
+  }
+}
+
+// k-step s fragment (three planes) of image row `row` (chunk 2s + h of an H-image plane, or of
+// an Â plane when ADJ)
+template <bool ADJ = false>
+__device__ __forceinline__ void rd_half(u32x4 (&f)[3], const FwdSmem& sm, int h, int row, int s) {
+  const int off = ADJ ? row * ADJ_LD * 2 + 16 * (2 * s + h) : ap_chunk(row, 2 * s + h);
+#pragma unroll
+  for (int p = 0; p < 3; ++p) f[p] = lds16((ADJ ? sm.Adj[p] : sm.Ap[p]) + off);
+}
+
+// one k-step: six MFMAs on the first accumulator, then the first operand's next reads, six on
+// the second, its next reads (single-buffered operands: a read is issued once its last MFMA is)
+__device__ __forceinline__ void gemm_sched(bool reads) {
+  __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+  if (reads) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+  __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+  if (reads) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// GEMM over the 128 features of the H image with the W fragment: for the node blocks li and
+// 32 + li of the image, c0/c1 += (W-side) x (image-side). TRANS = false: the image is the A
+// operand (P = H W^T: feature on the lane); true: the B operand (H^T = W X^T: node on the lane).
+template <bool TRANS>
+__device__ __forceinline__ void gemm_feat(f32x16& c0, f32x16& c1, const u32x4 (&wf)[3][8],
+                                          const FwdSmem& sm) {
+  const int t = fresh_tid();
+  const int h = (t >> 5) & 1, li = t & 31;
+  u32x4 f0[3], f1[3];
+  rd_half(f0, sm, h, li, 0);
+  rd_half(f1, sm, h, 32 + li, 0);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    u32x4 w3[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) w3[p] = wf[p][s];
+    if (!(S3ABL & 1)) c0 = TRANS ? mfma_s3(w3, f0, c0) : mfma_s3(f0, w3, c0);
+    if (s + 1 < 8) rd_half(f0, sm, h, li, s + 1);
+    if (!(S3ABL & 1)) c1 = TRANS ? mfma_s3(w3, f1, c1) : mfma_s3(f1, w3, c1);
+    if (s + 1 < 8) rd_half(f1, sm, h, 32 + li, s + 1);
+    gemm_sched(s + 1 < 8);
+  }
+}
+
+template <bool FIRST>
+__global__ __launch_bounds__(NT, 2) void k_s3_fwd(const float* __restrict__ X, int64_t M,
+                                                  const int32_t* __restrict__ rowptr,
+                                                  const int32_t* __restrict__ col,
+                                                  const float* __restrict__ w, int L,
+                                                  StackArgs args, const uint16_t* __restrict__ Wp,
+                                                  const int32_t* __restrict__ tmask) {
+  __shared__ __attribute__((aligned(16))) FwdSmem sm;
+  const int64_t ntiles = (M + TM - 1) / TM;
+  const int l0 = FIRST ? 0 : 1;
+  const int K0 = args.width[l0];
+  float* const scr = reinterpret_cast<float*>(sm.Adj[0]);  // fp32 Â [target][source], 16 KiB
+
+  for (int i = threadIdx.x; i < (L + 1) * WP; i += NT) {
+    const int l = i / WP, n = i % WP;
+    sm.bias[l][n] = (l >= l0 && n < args.width[l + 1]) ? args.b[l][n] : 0.f;
+  }
+  int64_t t = seek_tile(blockIdx.x, ntiles, tmask, 0);
+  if (t >= ntiles) return;
+  [[maybe_unused]] int stamp_i = 0;
+  S3STAMP();
+
+  f32x4 xr[8];
+  IdxRegs R;
+  u32x4 wf[3][8];
+  const Buf bX = mkbuf(X, M * K0 * 4);
+  load_rows(xr, bX, K0, (int)(t * TM));
+  load_wf(wf, Wp, l0);
+  idx_load_head(R, rowptr, M, t * TM);
+  idx_load_body(R, col, w);
+  for (; t < ntiles;) {
+    const int64_t r0 = t * TM;
+    const int64_t tn = seek_tile(t + gridDim.x, ntiles, tmask, 0);
+    const bool has_next = tn < ntiles;
+    // X planes (zero past K0 and M), fp32 Â scratch zeroed, the tile's rowptr
+    {
+      const int tq = fresh_tid();
+      const int li = tq & 31, hw = tq >> 5;
+      const bool kin = 4 * li < K0;
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int rr = hw + 8 * it;
+        u32x2 o[3];
+        split4(sel4(kin && r0 + rr < M, xr[it]), o);
+        const int off = ap_off(rr, 4 * li);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) sts8(sm.Ap[p] + off, o[p]);
+      }
+#pragma unroll
+      for (int i = 0; i < TM * TM / 4 / NT; ++i) st4(scr + 4 * (tq + i * NT), zero4());
+      if (tq <= TM) sm.rp[tq] = R.rp;
+      if (tq == 0) sm.flag = 0;
+    }
+    lds_barrier();
+    S3STAMP();  // 1: prologue (X planes) + B1
+    adj_scatter<false>(scr, sm.rp, R, r0);
+    if (has_next) idx_load_head(R, rowptr, M, tn * TM);
+    f32x16 z0 = {}, z1 = {};
+    if (FIRST) {
+      // H_0^T = W_0 X^T: A = W_0 planes (registers), B = X planes; node on the lane
+      gemm_feat<true>(z0, z1, wf, sm);
+      if (!(S3ABL & 32)) load_wf(wf, Wp, 1);
+    }
+    S3STAMP();  // 2: scatter + in_proj GEMM
+    if (has_next) idx_load_body(R, col, w);
+    lds_barrier();  // Â summed; every read of the X planes done
+    S3STAMP();  // 3: B2
+    // this thread's 16 Â weights: target row tid / 4, sources 16 (tid & 3) ..
+    f32x4 av[4];
+    {
+      const int tq = fresh_tid();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) av[i] = ld4(scr + (tq >> 2) * TM + 16 * (tq & 3) + 4 * i);
+    }
+    if (FIRST)
+      epilogue<false, true>(sm, z0, z1, sm.bias[0], mkbuf(args.H[0], M * args.width[1] * 4),
+                            args.width[1], r0);
+    S3STAMP();  // 4: in_proj epilogue
+    lds_barrier();  // every scratch read done
+    int inexact = 0;
+    {
+      const int tq = fresh_tid();
+      const int am = tq >> 2, aq = tq & 3;
+      // phys position y of the 16-block holds source 16 aq + perm16(y)
+      float f[16];
+#pragma unroll
+      for (int y = 0; y < 16; ++y) {
+        const int src = perm16(y);
+        f[y] = av[src >> 2][src & 3];
+      }
+      uint32_t q[3][8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const Split2 s2 = split2(f[2 * i], f[2 * i + 1]);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) q[p][i] = s2.p[p];
+        inexact |= (s2.p[1] | s2.p[2]) != 0;
+      }
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        unsigned char* dst = sm.Adj[p] + am * ADJ_LD * 2 + 32 * aq;
+        *reinterpret_cast<u32x4*>(dst) = u32x4{q[p][0], q[p][1], q[p][2], q[p][3]};
+        *reinterpret_cast<u32x4*>(dst + 16) = u32x4{q[p][4], q[p][5], q[p][6], q[p][7]};
+      }
+    }
+    if (inexact) sm.flag = 1;
+    lds_barrier();
+    const bool exact = sm.flag == 0;
+    S3STAMP();  // 5: Â planes + B4
+    for (int l = 1; l <= L; ++l) {
+      const int N = args.width[l + 1];
+      // GEMM1: P = H W_l^T (A = H planes, B = W_l planes; feature on the lane)
+      f32x16 p0 = {}, p1 = {};
+      gemm_feat<false>(p0, p1, wf, sm);
+      S3STAMP();  // l: W load + GEMM1
+      // the next tile's rows, a GEMM2 and an epilogue ahead of their use (vmcnt is in order:
+      // they are issued after this layer's weight loads, before the next ones)
+      if (l == L && has_next && !(S3ABL & 64)) load_rows(xr, bX, K0, (int)(tn * TM));
+      // P (feature on the lane, node in the registers) -> A-operand fragments over nodes:
+      // k-step s uses registers 8 (s & 1) .. + 7 of p0 (s < 2) or p1
+      u32x4 pp[4][3];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const f32x16& pa = s < 2 ? p0 : p1;
+        const int rb = 8 * (s & 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const Split2 s2 = split2(pa[rb + 2 * i], pa[rb + 2 * i + 1]);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) pp[s][p][i] = s2.p[p];
+        }
+      }
+      S3STAMP();  // l: P split
+      // GEMM2: Z^T = P^T Â^T (B = Â planes, target node li / 32 + li)
+      z0 = f32x16{};
+      z1 = f32x16{};
+      {
+        const int tq = fresh_tid();
+        const int h = (tq >> 5) & 1, li = tq & 31;
+        if (exact) {
+          // Â_hi only: all eight operand reads up front, then 24 MFMAs
+          u32x4 b0[4], b1[4];
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            b0[s] = lds16(sm.Adj[0] + li * ADJ_LD * 2 + 16 * (2 * s + h));
+            b1[s] = lds16(sm.Adj[0] + (32 + li) * ADJ_LD * 2 + 16 * (2 * s + h));
+          }
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            if (!(S3ABL & 2)) {
+              z0 = mfma_s3_bexact(pp[s], b0[s], z0);
+              z1 = mfma_s3_bexact(pp[s], b1[s], z1);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            u32x4 b0[3], b1[3];
+            rd_half<true>(b0, sm, h, li, s);
+            rd_half<true>(b1, sm, h, 32 + li, s);
+            if (!(S3ABL & 2)) {
+              z0 = mfma_s3(pp[s], b0, z0);
+              z1 = mfma_s3(pp[s], b1, z1);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+      S3STAMP();  // l: GEMM2
+      // the next layer's weights (or the first layer's, for the next tile): issued before the
+      // epilogue's stores so that waiting for them never waits for the stores
+      if (!(S3ABL & 32)) load_wf(wf, Wp, l < L ? l + 1 : l0);
+      lds_barrier();  // every read of the H planes and Â done
+      S3STAMP();  // l: B5
+      const Buf hb = mkbuf(args.H[l], M * N * 4);
+      if (l < L) {
+        epilogue<true, true>(sm, z0, z1, sm.bias[l], hb, N, r0);
+        S3STAMP();  // l: epilogue
+        lds_barrier();
+        S3STAMP();  // l: B6
+      } else {
+        epilogue<true, false>(sm, z0, z1, sm.bias[l], hb, N, r0);
+        S3STAMP();  // L: epilogue
+      }
+    }
+    t = tn;
+  }
+}
+
+}  // namespace lgnn_s3
+
+// ------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------
+#ifdef LGNN_S3_STAMPS
+extern "C" int lgnn_s3_debug_stamps(unsigned long long* host_out) {
+  return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(lgnn_s3_stamp_buf),
+                                  sizeof(lgnn_s3_stamp_buf));
+}
+#endif
+
+extern "C" size_t lgnn_weight_planes_bytes(int nl) {
+  if (nl < 1 || nl > LGNN_MAX_STACK) return 0;
+  return (size_t)nl * 3 * lgnn_s3::PLANE * sizeof(uint16_t);
+}
+
+extern "C" int lgnn_weight_planes(int nl, const float* const* W, const int* widths,
+                                  uint16_t* planes, uint16_t* planes_t, void* stream) {
+  if (nl < 1 || nl > LGNN_MAX_STACK || !W || !widths || !planes) return LGNN_EINVAL;
+  lgnn_s3::PlaneArgs a = {};
+  for (int l = 0; l < nl; ++l) {
+    const int K = widths[l], N = widths[l + 1];
+    if (!W[l] || K < 4 || N < 4 || K > lgnn_s3::WP || N > lgnn_s3::WP || K % 4 || N % 4)
+      return LGNN_EINVAL;
+    a.W[l] = W[l];
+    a.N[l] = N;
+    a.K[l] = K;
+  }
+  const int threads = nl * lgnn_s3::WP * lgnn_s3::WP / 4;
+  hipLaunchKernelGGL(lgnn_s3::k_wplanes, dim3((threads + 255) / 256), dim3(256), 0,
+                     as_stream(stream), a, nl, planes, planes_t);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? LGNN_OK : (int)e;
+}
+
+extern "C" int lgnn_gcn_stack_fwd_s3(const float* X, int64_t M, int d_in, int has_in_proj,
+                                     const int32_t* rowptr, const int32_t* col, const float* w,
+                                     int L, const uint16_t* planes, const float* const* b,
+                                     const int* widths, float* const* H,
+                                     const int32_t* tile_open, void* stream) {
+  if (M < 0 || L < 1 || L + 1 > LGNN_MAX_STACK || !planes || !b || !widths || !H || !rowptr ||
+      !col || !tile_open)
+    return LGNN_EINVAL;
+  lgnn_tile::StackArgs a = {};
+  const int l0 = has_in_proj ? 0 : 1;
+  if (!has_in_proj && widths[0] != d_in) return LGNN_EINVAL;
+  a.width[0] = d_in;
+  for (int l = 0; l <= L; ++l) {
+    a.width[l + 1] = widths[l];
+    if (l < l0) continue;
+    const int K = a.width[l], N = a.width[l + 1];
+    if (!lgnn_tile_fits(M, K, N) || !b[l] || !H[l]) return LGNN_EINVAL;
+    a.b[l] = b[l];
+    a.H[l] = H[l];
+  }
+  if (M == 0) return LGNN_OK;
+  if (!X) return LGNN_EINVAL;
+  const int64_t ntiles = (M + lgnn_tile::TM - 1) / lgnn_tile::TM;
+  dim3 grid((unsigned)(ntiles < 512 ? ntiles : 512));
+  hipStream_t s = as_stream(stream);
+  if (has_in_proj)
+    hipLaunchKernelGGL(lgnn_s3::k_s3_fwd<true>, grid, dim3(lgnn_tile::NT), 0, s, X, M, rowptr,
+                       col, w, L, a, planes, tile_open);
+  else
+    hipLaunchKernelGGL(lgnn_s3::k_s3_fwd<false>, grid, dim3(lgnn_tile::NT), 0, s, X, M, rowptr,
+                       col, w, L, a, planes, tile_open);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? LGNN_OK : (int)e;
+}

@@ -1,0 +1,221 @@
+// Shared by the tile kernels (tile.hip, stack3.hip): tile constants, tile selection, raw
+// buffer access, coalesced row loads and the per-tile CSR block (registers, LDS, dense Â).
+#pragma once
+#include "common.h"
+
+// Timing-only ablation builds (tools/ablate.py, tools/stamps.py): -DLGNN_ABLATE=<mask> removes
+// phases of the tile kernels (1 MFMA, 2 aggregation, 4 global stores, 8 ELU, 16 global row loads,
+// 64 dense-adjacency build). The product build is mask 0; ablated libraries are built outside
+// the package and never loaded by it.
+#ifndef LGNN_ABLATE
+#define LGNN_ABLATE 0
+#endif
+
+// Diagnostic build only (-DLGNN_STAMPS, tools/stamps.py): thread 0 of each block records
+// s_memtime at phase boundaries of k_stack_fwd; never compiled into the product library.
+#ifdef LGNN_STAMPS
+__device__ unsigned long long lgnn_stamp_buf[1024 * 64];
+#define STAMP(k)                                                                   \
+  do {                                                                             \
+    const int _k = (k);                                                            \
+    if (threadIdx.x == 0 && _k < 62)                                               \
+      lgnn_stamp_buf[blockIdx.x * 64 + _k] = __builtin_amdgcn_s_memtime();         \
+    if (threadIdx.x == 0 && _k == 0) {  /* placement: HW_ID, XCC_ID */             \
+      lgnn_stamp_buf[blockIdx.x * 64 + 62] = __builtin_amdgcn_s_getreg(4 | (31 << 11));  \
+      lgnn_stamp_buf[blockIdx.x * 64 + 63] = __builtin_amdgcn_s_getreg(20 | (31 << 11)); \
+    }                                                                              \
+  } while (0)
+#else
+#define STAMP(k) \
+  do {           \
+  } while (0)
+#endif
+
+namespace lgnn_tile {
+
+constexpr int ABL = LGNN_ABLATE;
+#ifndef LGNN_AGG_UNROLL
+#define LGNN_AGG_UNROLL 2
+#endif
+constexpr int TM = 64;
+constexpr int KC = 128;
+constexpr int LDS = KC + 4;
+constexpr int NT = 256;
+constexpr int CAPE = 1024;
+constexpr int EB = 8;
+
+// A tile's CSR block in LDS. `local` (every entry's source row is in this tile — the k-NN
+// case with graphs aligned to tiles): ow[j] = (float offset of the source row in the A image,
+// weight bits), padded with EB zero-weight entries so a row's batch reads need no bounds logic.
+// Otherwise only rp is used and the rows are aggregated from global memory.
+struct TileIdx {
+  int rp[TM + 1];
+  int local;
+  int2 ow[CAPE + EB];
+};
+
+// Tile selection by a per-tile mask (nullable = every tile): with `want` = 1 only tiles whose
+// mask is non-zero, with 0 only tiles whose mask is zero. Block-uniform scalar reads.
+// mask[ntiles] counts the non-zero flags: a want = 1 launch with none returns after one load.
+__device__ __forceinline__ int64_t seek_tile(int64_t t, int64_t ntiles,
+                                             const int32_t* __restrict__ mask, int want) {
+  if (mask) {
+    if (want && mask[ntiles] == 0) return ntiles;
+    while (t < ntiles && ((mask[t] != 0) != (want != 0))) t += gridDim.x;
+  }
+  return t;
+}
+
+// Raw buffer access (SGPR descriptor + 32-bit byte offset): out-of-range loads return 0 and
+// out-of-range stores are dropped by the hardware range check, so row tails need no clamping
+// and addresses cost one VGPR. Tensors addressed this way are < 4 GiB (checked on the host).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t Buf;
+__device__ __forceinline__ Buf mkbuf(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)(uint32_t)bytes,
+                                           0x00020000);
+}
+__device__ __forceinline__ f32x4 bld4(Buf r, int off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ void bst4(Buf r, int off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
+}
+
+__device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+__device__ __forceinline__ f32x4 sel4(bool c, f32x4 v) { return c ? v : zero4(); }
+
+// Coalesced raw tile load: half-wave hw = tid / 32 owns rows hw + (64 / RPT) * it (it < RPT;
+// RPT = 8 for 256-thread blocks, 4 for 512), columns 4li..4li+3 — the same (row, column) mapping
+// as the half-wave-per-row aggregation, so register values can be reused.
+template <int RPT>
+__device__ __forceinline__ void load_rows(f32x4 (&v)[RPT], Buf X, int K, int r0) {
+  const int hw = threadIdx.x >> 5, li = threadIdx.x & 31;
+  const int k = 4 * li;
+  const int kc = k < K ? k : K - 4;
+#pragma unroll
+  for (int it = 0; it < RPT; ++it) v[it] = bld4(X, ((r0 + hw + (TM / RPT) * it) * K + kc) * 4);
+}
+
+template <int RPT>
+__device__ __forceinline__ void store_rows_lds(float* A, const f32x4 (&v)[RPT], int64_t M, int K,
+                                               int64_t r0) {
+  const int hw = threadIdx.x >> 5, li = threadIdx.x & 31;
+  const bool kin = 4 * li < K;
+#pragma unroll
+  for (int it = 0; it < RPT; ++it) {
+    const int rr = hw + (TM / RPT) * it;
+    st4(A + rr * LDS + 4 * li, sel4(kin && r0 + rr < M, v[it]));
+  }
+}
+
+// One tile's CSR index block, loaded into registers ahead of use (software pipelining: the next
+// tile's block is in flight while the current tile aggregates and runs its MFMAs).
+//   head: rowptr[r0 .. r0+64] (one per thread, tid <= 64) + the uniform entry range (eb, ne)
+//   body: the ne <= CAPE entries (col, w), CAPE/NT per thread; issued once the head has landed
+template <int NTH>
+struct IdxRegsT {
+  int rp;
+  int eb, ne;
+  int c[CAPE / NTH];
+  float w[CAPE / NTH];
+};
+using IdxRegs = IdxRegsT<NT>;
+
+template <int NTH>
+__device__ __forceinline__ void idx_load_head(IdxRegsT<NTH>& R, const int32_t* __restrict__ rowptr,
+                                              int64_t M, int64_t r0) {
+  const int tid = threadIdx.x;
+  const int64_t r = r0 + (tid <= TM ? tid : 0);
+  R.rp = rowptr[r < M ? r : M];
+  const int64_t rl = r0 + TM < M ? r0 + TM : M;
+  R.eb = rowptr[r0];
+  R.ne = rowptr[rl] - R.eb;
+}
+
+template <int NTH>
+__device__ __forceinline__ void idx_load_body(IdxRegsT<NTH>& R, const int32_t* __restrict__ col,
+                                              const float* __restrict__ w) {
+  if (R.ne > CAPE) return;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < CAPE / NTH; ++u) {
+    const int j = tid + u * NTH;
+    const int jc = j < R.ne ? j : 0;
+    R.c[u] = col[R.eb + jc];
+    R.w[u] = w ? w[R.eb + jc] : 1.f;
+  }
+}
+
+// Writes the prefetched block to LDS. Ends with a barrier (block-wide OR of "an entry leaves
+// the tile"); `staged` = the tile takes the local path.
+template <int NTH>
+__device__ __forceinline__ void idx_store(TileIdx& ti, bool& staged, const IdxRegsT<NTH>& R,
+                                          int64_t r0) {
+  const int tid = threadIdx.x;
+  if (tid <= TM) ti.rp[tid] = R.rp;
+  bool fits = R.ne <= CAPE;
+  int out = 0;
+  if (fits) {
+#pragma unroll
+    for (int u = 0; u < CAPE / NTH; ++u) {
+      const int j = tid + u * NTH;
+      const int rel = R.c[u] - (int)r0;
+      if (j < R.ne && (unsigned)rel >= (unsigned)TM) out = 1;
+    }
+  }
+  const bool any_out = __syncthreads_or(out);
+  staged = fits && !any_out;
+  if (staged) {
+#pragma unroll
+    for (int u = 0; u < CAPE / NTH; ++u) {
+      const int j = tid + u * NTH;
+      if (j < R.ne) ti.ow[j] = make_int2((R.c[u] - (int)r0) * LDS, __float_as_int(R.w[u]));
+    }
+    if (tid < EB) ti.ow[R.ne + tid] = make_int2(0, 0);
+  }
+}
+
+// Dense Â_tile from the tile's row-CSR block (entry j of R: source R.c, weight R.w; its target
+// row found by binary search over rp): Adj[target][source] (TRANS = false) or Adj[source][target]
+// (TRANS = true), row stride TM. Adj must be zero and rp visible. Duplicate (target, source)
+// pairs carry equal weights, so the LDS float adds are order independent.
+template <bool TRANS, int NTH>
+__device__ __forceinline__ void adj_scatter(float* Adj, const int* rp, const IdxRegsT<NTH>& R,
+                                            int64_t r0) {
+#pragma unroll
+  for (int u = 0; u < CAPE / NTH; ++u) {
+    const int j = threadIdx.x + u * NTH;
+    if (j < R.ne) {
+      const int e = R.eb + j;
+      int lo = 0, hi = TM;
+#pragma unroll
+      for (int it = 0; it < 6; ++it) {
+        const int mid = (lo + hi) >> 1;
+        if (rp[mid] <= e) lo = mid;
+        else hi = mid;
+      }
+      const int c = R.c[u] - (int)r0;
+      atomicAdd(&Adj[TRANS ? c * TM + lo : lo * TM + c], R.w[u]);
+    }
+  }
+}
+
+// Workgroup barrier ordering LDS only: unlike __syncthreads it does not wait for outstanding
+// global loads and stores (s_waitcnt vmcnt(0)), so loads issued a phase ahead stay in flight
+// across it. For kernels whose threads exchange data through LDS only.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Arguments of the fused GCN stack forward kernels (tile.hip, stack3.hip).
+struct StackArgs {
+  const float* W[LGNN_MAX_STACK];
+  const float* b[LGNN_MAX_STACK];
+  float* H[LGNN_MAX_STACK];
+  int width[LGNN_MAX_STACK + 1];  // width[0] = input width, width[l+1] = output of layer l
+};
+
+}  // namespace lgnn_tile

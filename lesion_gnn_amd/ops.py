@@ -60,6 +60,25 @@ STACK_MAX = 8  # LGNN_MAX_STACK
 FUSED_BWD = os.environ.get("LGNN_FUSED_BWD", "1") != "0"
 
 
+# GEMM arithmetic of the fused GCN stack: "s3" = bf16 MFMA on three-plane split operands (fp32
+# accuracy, stack3.hip), "f32" = fp32 MFMA (tile.hip). LGNN_MFMA=f32 selects the latter.
+MFMA_MODE = os.environ.get("LGNN_MFMA", "s3")
+
+
+def weight_planes(Ws: list, d_in: int, transposed: bool = False):
+    """bf16 three-plane images of the stack weights for the split-3 kernels (one launch):
+    returns (planes, planes_t or None), each [L+1, 3, 128, 128] int16."""
+    nl = len(Ws)
+    dev = Ws[0].device
+    planes = torch.empty(nl, 3, 128, 128, dtype=torch.int16, device=dev)
+    planes_t = torch.empty_like(planes) if transposed else None
+    widths = (ctypes.c_int * (nl + 1))(*([d_in] + [W.size(0) for W in Ws]))
+    arr = ctypes.c_void_p * nl
+    _lib.call("lgnn_weight_planes", nl, arr(*[W.data_ptr() for W in Ws]), widths,
+              _lib.ptr(planes), _lib.ptr(planes_t), _s(dev))
+    return planes, planes_t
+
+
 def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list):
     """in_proj + L x ELU(GCNConv) forward, every width <= 128: returns ([H_0..H_L],
     [S_1..S_L]). Tiles no edge leaves run fused through every layer (lgnn_gcn_stack_fwd); the
@@ -77,9 +96,15 @@ def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list):
     bp = arr(*[b.data_ptr() for b in bs])
     Hp = arr(*[h.data_ptr() for h in hs])
     widths = (ctypes.c_int * (L + 1))(*[W.size(0) for W in Ws])
-    _lib.call("lgnn_gcn_stack_fwd", _lib.ptr(x), M, x.size(1), 1, _lib.ptr(csr.rowptr),
-              _lib.ptr(csr.col), _lib.ptr(csr.w), L, Wp, bp, widths, Hp, _lib.ptr(open_),
-              _s(dev))
+    if MFMA_MODE == "s3" and L >= 1:
+        planes, _ = weight_planes(Ws, x.size(1))
+        _lib.call("lgnn_gcn_stack_fwd_s3", _lib.ptr(x), M, x.size(1), 1, _lib.ptr(csr.rowptr),
+                  _lib.ptr(csr.col), _lib.ptr(csr.w), L, _lib.ptr(planes), bp, widths, Hp,
+                  _lib.ptr(open_), _s(dev))
+    else:
+        _lib.call("lgnn_gcn_stack_fwd", _lib.ptr(x), M, x.size(1), 1, _lib.ptr(csr.rowptr),
+                  _lib.ptr(csr.col), _lib.ptr(csr.w), L, Wp, bp, widths, Hp, _lib.ptr(open_),
+                  _s(dev))
     for l in range(L + 1):
         inp = x if l == 0 else hs[l - 1]
         c = csr if l > 0 else None
