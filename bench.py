@@ -230,6 +230,42 @@ def time_dominant_kernels(model, b, dev):
     return out
 
 
+def time_knn(b, wl, dev):
+    """The data-side k-NN graph build of this batch (KNNGraph(k, loop=True), reference
+    configs/config.py:47): GPU (lgnn_knn_graph, one launch for the whole batch, HIP events) vs
+    the vectorised CPU restatement (synth.knn_edges per size group, one thread). Not part of the
+    timed step; reported beside it."""
+    from lesion_gnn_amd import synth
+    from lesion_gnn_amd.knn import knn_graph
+
+    k = wl["k"]
+    knn_graph(b.pos, k, b.batch, loop=True, num_graphs=b.num_graphs)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    reps = 10
+    for _ in range(reps):
+        ei = knn_graph(b.pos, k, b.batch, loop=True, num_graphs=b.num_graphs)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    gpu_ms = e0.elapsed_time(e1) / reps
+    same = bool(torch.equal(ei, b.edge_index))
+    pos, ptr = b.pos.cpu(), b.ptr.cpu().tolist()
+    sizes = [ptr[i + 1] - ptr[i] for i in range(len(ptr) - 1)]
+    nthreads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    t0 = time.perf_counter()
+    by_size: dict[int, list[int]] = {}
+    for g, n in enumerate(sizes):
+        by_size.setdefault(n, []).append(g)
+    for n, gs in by_size.items():
+        synth.knn_edges(torch.stack([pos[ptr[g]:ptr[g] + n] for g in gs]), k, True)
+    cpu_ms = (time.perf_counter() - t0) * 1e3
+    torch.set_num_threads(nthreads)
+    return {"graphs": b.num_graphs, "nodes": b.num_nodes, "k": k,
+            "gpu_ms_incl_host_sizing": round(gpu_ms, 4), "cpu_ms_1thread": round(cpu_ms, 2),
+            "bitexact_vs_batch_edge_index": same}
+
+
 def pmc_traffic(trace_name: str):
     """HBM bytes per launch of `trace_name` from the committed rocprofv3 PMC passes
     (profiles/traffic.json, written by tools/summarize_prof.py from separate FETCH_SIZE and
@@ -378,6 +414,8 @@ def main():
         rows.sort(key=lambda r: -r["avg_launch_ms"])
         out["roofline"] = rows[0]  # the dominant kernel (longest launch)
         out["roofline_next"] = rows[1:]
+    if rank == 0 and not args.no_kernel_timing:
+        out["knn_graph"] = time_knn(b, wl, dev)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(wl, B, args.cpu_seconds)
     if rank == 0:

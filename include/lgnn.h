@@ -84,6 +84,22 @@ int lgnn_batch_ptr(const int64_t* batch, int64_t num_nodes, int64_t num_graphs, 
                    void* stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * k-NN graph of a batch of point sets. Replaces: torch_cluster.knn_graph(pos, k, batch, loop,
+ * flow='source_to_target') behind PyG's KNNGraph transform (reference configs/config.py:47
+ * KNNGraph(k=6, loop=True); per graph in datasets/datamodule.py:43-48; sweep.py:105-120 k in
+ * [2, 32]). pos [N][dims] fp64 (dims 2 or 3); batch [N] int64 sorted graph ids; ptr [B+1] int32
+ * graph offsets (lgnn_batch_ptr). For every node q: its kk = min(k, n_g) (loop) or
+ * min(k + 1, n_g) - 1 (!loop, q itself excluded) nearest nodes of its graph, ordered by (fp64
+ * squared distance, index); edge_index [2][num_edges] int64 = (neighbour, q), grouped by q in node
+ * order. num_edges = sum_g n_g * kk_g (the caller computes it to size edge_index). 1 <= k <= 32.
+ * workspace: lgnn_knn_workspace_bytes(B) bytes. Deterministic, bit-exact vs the fp64 restatement.
+ * ------------------------------------------------------------------------------------------- */
+size_t lgnn_knn_workspace_bytes(int64_t num_graphs);
+int lgnn_knn_graph(const double* pos, int64_t num_nodes, int dims, const int64_t* batch,
+                   const int32_t* ptr, int64_t num_graphs, int k, int loop, int64_t* edge_index,
+                   int64_t num_edges, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
  * Node-tile fused aggregate + linear (+bias, +activation), forward.
  * Replaces: nn.Linear (reference gin.py:21 in_proj), GCNConv.lin + propagate + bias
  * (A_hat (X W^T) == (A_hat X) W^T), GINConv aggregate + first MLP Linear (reference gin.py:23),

@@ -8,10 +8,11 @@ include/lgnn.h). GPU only — there is no CPU fallback.
 from . import _lib
 from .conv import GCNConv, global_add_pool, global_mean_pool
 from .graph import Graph
+from .knn import KNNGraph, knn_graph
 from .models import GCN, GCNConfig, get_model
 
-__all__ = ["GCN", "GCNConfig", "GCNConv", "Graph", "get_model", "global_mean_pool",
-           "global_add_pool", "load_library"]
+__all__ = ["GCN", "GCNConfig", "GCNConv", "Graph", "KNNGraph", "get_model", "global_mean_pool",
+           "global_add_pool", "knn_graph", "load_library"]
 
 
 def load_library():

@@ -1,0 +1,185 @@
+// k-NN graph construction on the GPU for a batch of graphs: torch_cluster.knn_graph(pos, k,
+// batch, loop, flow='source_to_target') as PyG's KNNGraph transform calls it (reference
+// configs/config.py:47 KNNGraph(k=6, loop=True), applied per graph in datasets/datamodule.py:43-48,
+// sweep.py:105-120 for k in [2, 32]). For every node (the query) of every graph: its k nearest
+// nodes of the same graph, itself included when `loop` (excluded otherwise), ordered by
+// (squared distance, node index); edge_index = [neighbour, query], grouped by query in node
+// order — already the target-grouped COO the graph build consumes.
+//
+// Squared distances are fp64 dx*dx + dy*dy (+ dz*dz) with explicit round-to-nearest operations
+// (no FMA contraction), the arithmetic of the CPU restatement (synth.knn_edges: ((p_q - p_c)**2)
+// .sum(-1)), so neighbour lists and their order are bit-exact.
+//
+// Layout: pos [N][D] fp64 (D = 2 or 3), graph offsets ptr [B+1] (int32, Batch.ptr), graph id
+// batch [N] (int64, sorted). One thread per query; a block's queries are consecutive nodes, so
+// the candidates of its graphs form one contiguous node range, staged through LDS in chunks.
+// Each thread keeps its best KMAX (k rounded up to a power of two) in registers as a sorted
+// list; candidates arrive in index order, so strict comparisons keep ties in index order.
+#include "common.h"
+
+namespace {
+
+constexpr int QT = 256;      // queries (threads) per block
+constexpr int CHUNK = 1024;  // candidates staged per round
+
+__device__ __forceinline__ double sqd(const double* a, const double* b, int D) {
+  const double dx = a[0] - b[0], dy = a[1] - b[1];
+  double s = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
+  if (D == 3) {
+    const double dz = a[2] - b[2];
+    s = __dadd_rn(s, __dmul_rn(dz, dz));
+  }
+  return s;
+}
+
+// eoff[g] = first edge of graph g (exclusive scan of n_g * kk_g), eoff[B] = total. One block,
+// each thread a contiguous range of graphs (fixed order).
+__global__ __launch_bounds__(1024) void k_knn_offsets(const int32_t* __restrict__ ptr, int64_t B,
+                                                      int k, int loop,
+                                                      int64_t* __restrict__ eoff) {
+  __shared__ int64_t part[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (B + 1023) / 1024;
+  const int64_t g0 = t * per, g1 = g0 + per < B ? g0 + per : B;
+  auto edges = [&](int64_t g) -> int64_t {
+    const int64_t n = ptr[g + 1] - ptr[g];
+    int64_t kk = loop ? (k < n ? k : n) : ((k + 1 < n ? k + 1 : n) - 1);
+    if (kk < 0) kk = 0;
+    return n * kk;
+  };
+  int64_t s = 0;
+  for (int64_t g = g0; g < g1; ++g) s += edges(g);
+  part[t] = s;
+  __syncthreads();
+  if (t == 0) {
+    int64_t run = 0;
+    for (int i = 0; i < 1024; ++i) {
+      const int64_t v = part[i];
+      part[i] = run;
+      run += v;
+    }
+    eoff[B] = run;
+  }
+  __syncthreads();
+  int64_t run = part[t];
+  for (int64_t g = g0; g < g1; ++g) {
+    eoff[g] = run;
+    run += edges(g);
+  }
+}
+
+template <int KMAX, int D>
+__global__ __launch_bounds__(QT) void k_knn(const double* __restrict__ pos, int64_t N,
+                                            const int64_t* __restrict__ batch,
+                                            const int32_t* __restrict__ ptr, int k, int loop,
+                                            const int64_t* __restrict__ eoff, int64_t E,
+                                            int64_t* __restrict__ ei) {
+  __shared__ double cp[CHUNK * D];
+  const int64_t q0 = (int64_t)blockIdx.x * QT;
+  const int64_t q = q0 + threadIdx.x;
+  const int64_t qlast = q0 + QT - 1 < N - 1 ? q0 + QT - 1 : N - 1;
+  // the block's candidate range: the graphs of its first and last query
+  const int64_t cbeg = ptr[batch[q0]], cend = ptr[batch[qlast] + 1];
+  const bool active = q < N;
+  int64_t g = 0, gs = 0, ge = 0;
+  double pq[D];
+  if (active) {
+    g = batch[q];
+    gs = ptr[g];
+    ge = ptr[g + 1];
+#pragma unroll
+    for (int d = 0; d < D; ++d) pq[d] = pos[q * D + d];
+  }
+  double bd[KMAX];
+  int bi[KMAX];
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j) {
+    bd[j] = __longlong_as_double(0x7ff0000000000000ll);  // +inf
+    bi[j] = -1;
+  }
+  for (int64_t c0 = cbeg; c0 < cend; c0 += CHUNK) {
+    const int64_t c1 = c0 + CHUNK < cend ? c0 + CHUNK : cend;
+    __syncthreads();
+    for (int64_t i = c0 * D + threadIdx.x; i < c1 * D; i += QT) cp[i - c0 * D] = pos[i];
+    __syncthreads();
+    if (!active) continue;
+    const int64_t lo = gs > c0 ? gs : c0, hi = ge < c1 ? ge : c1;
+    for (int64_t c = lo; c < hi; ++c) {
+      if (!loop && c == q) continue;
+      const double dc = sqd(pq, cp + (c - c0) * D, D);
+      if (dc < bd[KMAX - 1]) {
+        bd[KMAX - 1] = dc;
+        bi[KMAX - 1] = (int)(c - gs);
+#pragma unroll
+        for (int j = KMAX - 1; j > 0; --j) {
+          if (bd[j] < bd[j - 1]) {
+            const double td = bd[j];
+            bd[j] = bd[j - 1];
+            bd[j - 1] = td;
+            const int ti = bi[j];
+            bi[j] = bi[j - 1];
+            bi[j - 1] = ti;
+          }
+        }
+      }
+    }
+  }
+  if (!active) return;
+  const int64_t n = ge - gs;
+  int64_t kk = loop ? (k < n ? k : n) : ((k + 1 < n ? k + 1 : n) - 1);
+  if (kk < 0) kk = 0;
+  const int64_t base = eoff[g] + (q - gs) * kk;
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j) {
+    if (j < kk) {
+      ei[base + j] = gs + bi[j];
+      ei[E + base + j] = q;
+    }
+  }
+}
+
+template <int D>
+hipError_t launch_knn(int kmax, dim3 grid, hipStream_t s, const double* pos, int64_t N,
+                      const int64_t* batch, const int32_t* ptr, int k, int loop,
+                      const int64_t* eoff, int64_t E, int64_t* ei) {
+#define LGNN_KNN(KM) \
+  hipLaunchKernelGGL((k_knn<KM, D>), grid, dim3(QT), 0, s, pos, N, batch, ptr, k, loop, eoff, E, ei)
+  switch (kmax) {
+    case 4: LGNN_KNN(4); break;
+    case 8: LGNN_KNN(8); break;
+    case 16: LGNN_KNN(16); break;
+    default: LGNN_KNN(32); break;
+  }
+#undef LGNN_KNN
+  return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" size_t lgnn_knn_workspace_bytes(int64_t num_graphs) {
+  return num_graphs < 0 ? 0 : (size_t)(num_graphs + 1) * sizeof(int64_t);
+}
+
+extern "C" int lgnn_knn_graph(const double* pos, int64_t N, int dims, const int64_t* batch,
+                              const int32_t* ptr, int64_t B, int k, int loop, int64_t* edge_index,
+                              int64_t num_edges, void* workspace, size_t workspace_bytes,
+                              void* stream) {
+  if (N < 0 || B < 0 || k < 1 || k > 32 || (dims != 2 && dims != 3)) return LGNN_EINVAL;
+  if (N > 0 && (!pos || !batch || !ptr || !edge_index)) return LGNN_EINVAL;
+  if (N > INT32_MAX || num_edges < 0) return LGNN_EINVAL;
+  if (!workspace || workspace_bytes < lgnn_knn_workspace_bytes(B)) return LGNN_ENOSPC;
+  if (N == 0 || B == 0) return LGNN_OK;
+  hipStream_t s = as_stream(stream);
+  int64_t* eoff = static_cast<int64_t*>(workspace);
+  hipLaunchKernelGGL(k_knn_offsets, dim3(1), dim3(1024), 0, s, ptr, B, k, loop, eoff);
+  LGNN_LAUNCH_CHECK();
+  const int kmax = k <= 4 ? 4 : k <= 8 ? 8 : k <= 16 ? 16 : 32;  // the self loop is skipped, not
+                                                                   // kept, when !loop
+  const dim3 grid((unsigned)((N + QT - 1) / QT));
+  const hipError_t e =
+      dims == 2 ? launch_knn<2>(kmax, grid, s, pos, N, batch, ptr, k, loop, eoff, num_edges,
+                                edge_index)
+                : launch_knn<3>(kmax, grid, s, pos, N, batch, ptr, k, loop, eoff, num_edges,
+                                edge_index);
+  return e == hipSuccess ? LGNN_OK : (int)e;
+}
