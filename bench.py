@@ -45,8 +45,11 @@ WORKLOADS = {
                classes=5, loss="CE", pool="mean",
                desc="C2: 2-layer GCN fwd+CE+bwd+Adam, graph build per forward"),
     "c3": dict(model="gat", sizes="lognormal", n=64, k=6, d_in=1025, hidden=[128] * 4, heads=4,
-               classes=5, loss="MSE", pool="mean", last_channel_class=True,
-               desc="C3: 3-layer GAT (4 heads), d_in 1025, log-normal N, k=6, MSE (fp32)"),
+               classes=5, loss="MSE", pool="mean", last_channel_class=True, precision="bf16",
+               desc="C3: 3-layer GAT (4 heads), d_in 1025, log-normal N, k=6, MSE, bf16 GEMMs"),
+    "c3f32": dict(model="gat", sizes="lognormal", n=64, k=6, d_in=1025, hidden=[128] * 4,
+                  heads=4, classes=5, loss="MSE", pool="mean", last_channel_class=True,
+                  desc="C3 in fp32: 3-layer GAT (4 heads), d_in 1025, log-normal N, k=6, MSE"),
     "c4": dict(model="gin", sizes="fixed", n=64, k=8, d_in=128, hidden=[128, 128, 128],
                classes=5, loss="CE", pool="add",
                desc="C4: GIN + global_add_pool, SyncBN across ranks, fwd+CE+bwd+Adam"),
@@ -123,7 +126,8 @@ def build_model(wl, oracle=False):
         mods = {"gcn": models.GCN, "gin": models.GIN, "gat": models.GAT}
     out = 1 if wl["loss"] == "MSE" else wl["classes"]
     if wl["model"] == "gat":
-        return mods["gat"](wl["d_in"], wl["hidden"], out, heads=wl["heads"], dropout=0.0)
+        return mods["gat"](wl["d_in"], wl["hidden"], out, heads=wl["heads"], dropout=0.0,
+                           precision=wl.get("precision", "fp32"))
     return mods[wl["model"]](wl["d_in"], wl["hidden"], out, 0.0, pool=wl["pool"])
 
 
@@ -386,7 +390,8 @@ def main():
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "graphs/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "bf16 GEMM operands, f32 accumulate" if wl.get("precision") == "bf16" else "f32",
         "data": "synthetic k-NN lesion graphs (pos~U[0,1)^2, x~N(0,1)), random-init weights",
         "config": {"workload": wl["desc"], "name": args.workload,
                    "step_launch": "hip_graph_replay" if args.graph else "eager",

@@ -107,7 +107,8 @@ class GATConv(nn.Module):
         glorot_(self.att_src)
         glorot_(self.att_dst)
 
-    def forward(self, x: torch.Tensor, edge_index, act: int = _lib.LGNN_ACT_NONE) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, edge_index, act: int = _lib.LGNN_ACT_NONE,
+                bf16: bool = False) -> torch.Tensor:
         g = as_graph(edge_index, x.size(0))
         mask = None
         if self.dropout > 0.0 and self.training:
@@ -115,7 +116,7 @@ class GATConv(nn.Module):
             mask = (torch.rand(cap, self.heads, device=x.device) >= self.dropout).float()
             mask.mul_(1.0 / (1.0 - self.dropout))
         return ops.gat_conv(x, self.lin.weight, self.att_src, self.att_dst, self.bias, g,
-                            self.heads, self.negative_slope, mask, act)
+                            self.heads, self.negative_slope, mask, act, bf16)
 
 
 def global_mean_pool(x: torch.Tensor, batch: torch.Tensor, size: int | None = None,

@@ -25,8 +25,13 @@ from .base import BaseModelConfig, BaseModule
 class GAT(nn.Module):
     def __init__(self, input_features: int, hiddden_channels: list[int], num_classes: int,
                  heads: int, dropout: float, num_st_seed_points: int | None = None,
-                 pool: str = "mean"):
+                 pool: str = "mean", precision: str = "fp32"):
         super().__init__()
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
+        # bf16 (BASELINE config C3): in_proj and every GATConv.lin on bf16-rounded operands with
+        # fp32 accumulation and fp32 activations; attention, softmax, pool and out_proj in fp32
+        self.bf16 = precision == "bf16"
         assert all(d % heads == 0 for d in hiddden_channels)
         if num_st_seed_points is not None:
             raise NotImplementedError("SetTransformerAggregation readout (reference gat.py:33-43)"
@@ -43,9 +48,9 @@ class GAT(nn.Module):
     def forward(self, x: torch.Tensor, edge_index, batch: torch.Tensor,
                 num_graphs: int | None = None) -> torch.Tensor:
         g = as_graph(edge_index, x.size(0), batch, num_graphs)
-        h = ops.node_linear(x, self.in_proj.weight, self.in_proj.bias)
+        h = ops.linear_auto(x, self.in_proj.weight, self.in_proj.bias, self.bf16)
         for conv in self.convs:
-            h = conv(h, g, act=_lib.LGNN_ACT_ELU)
+            h = conv(h, g, act=_lib.LGNN_ACT_ELU, bf16=self.bf16)
         return ops.pool_head(h, self.out_proj.weight, self.out_proj.bias, g, self.pool == "mean")
 
 
@@ -58,6 +63,7 @@ class GATConfig(BaseModelConfig):
     compile: bool
     num_st_seed_points: int | None = None
     pool: str = "mean"
+    precision: str = "fp32"
     name: str = dataclasses.field(default="GAT", init=False)
 
 
@@ -74,4 +80,5 @@ class GATModule(BaseModule):
             dropout=config.dropout,
             num_st_seed_points=config.num_st_seed_points,
             pool=config.pool,
+            precision=config.precision,
         )

@@ -303,6 +303,78 @@ def node_linear(x, W, b=None, graph: Graph | None = None, kind: str = "gcn",
     return _NodeLinear.apply(x, W, b, graph, kind, self_scale, act)
 
 
+def mm_dense(a: torch.Tensor, b: torch.Tensor, bf16: bool) -> torch.Tensor:
+    """a @ b in fp32 out: a plain library GEMM (hipBLASLt through torch) — fp32 operands, or
+    bf16-rounded operands with fp32 accumulation and fp32 output (aten::mm.dtype)."""
+    if bf16:
+        return torch.mm(a.to(torch.bfloat16), b.to(torch.bfloat16), out_dtype=torch.float32)
+    return torch.mm(a, b)
+
+
+def dw_dense(dy: torch.Tensor, x: torch.Tensor, bf16: bool) -> torch.Tensor:
+    """dW = dy^T x over M rows (M >> N, K): split-K — S row chunks as one batched GEMM, then a
+    fixed-order sum over the chunks (deterministic). The library's single GEMM parallelises
+    over the small N x K output only (C3 in_proj, M = 40k: 252 -> 112 us fp32, 181 -> 51 us
+    bf16 on MI355X, tools/gemm_probe.py)."""
+    M = x.size(0)
+    S = 32 if bf16 else 16
+    m = M // S
+    if m < 256:
+        return mm_dense(dy.t(), x, bf16)
+    head = S * m
+    xs, ds = x[:head].view(S, m, -1), dy[:head].view(S, m, -1)
+    if bf16:
+        part = torch.bmm(ds.to(torch.bfloat16).transpose(1, 2), xs.to(torch.bfloat16),
+                         out_dtype=torch.float32)
+    else:
+        part = torch.bmm(ds.transpose(1, 2), xs)
+    dW = part.sum(0)
+    if head < M:
+        dW += mm_dense(dy[head:].t(), x[head:], bf16)
+    return dW
+
+
+class _DenseLinear(torch.autograd.Function):
+    """y = x W^T + b for shapes outside the tile kernels (K > 128, K % 4 != 0: the reference's
+    in_proj with 1025 input channels, gat.py:29 / lesions.py:142,169) or in bf16 mode. A plain
+    GEMM, so it goes to the vendor library (hipBLASLt) rather than a hand-written kernel; the
+    backward is dW = dy^T x, db = colsum dy, dx = dy W in the same precision."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, bf16):
+        _lib.require_gpu(x, W)
+        x, W = _f32c(x), _f32c(W)
+        if bf16:  # rounded once; the backward's dW reuses the bf16 copy
+            x = x.to(torch.bfloat16)
+        y = mm_dense(x, W.t(), bf16)
+        if b is not None:
+            y += b
+        ctx.save_for_backward(x, W)
+        ctx.bf16, ctx.has_b = bf16, b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W = ctx.saved_tensors
+        dy = _f32c(dy)
+        dW = dw_dense(dy, x, ctx.bf16)
+        db = dy.sum(0) if ctx.has_b else None
+        dx = mm_dense(dy, W, ctx.bf16) if ctx.needs_input_grad[0] else None
+        return dx, dW, db, None
+
+
+def dense_linear(x, W, b=None, bf16: bool = False):
+    return _DenseLinear.apply(x, W, b, bf16)
+
+
+def linear_auto(x, W, b=None, bf16: bool = False):
+    """node_linear (tile kernels) where the shape allows and fp32 is asked for; else the library
+    GEMM (dense_linear)."""
+    if not bf16 and fast_shape(W.size(1), W.size(0)):
+        return node_linear(x, W, b)
+    return dense_linear(x, W, b, bf16)
+
+
 class _Spmm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, graph, kind, self_scale):
@@ -629,7 +701,7 @@ class _GATConv(torch.autograd.Function):
     over remove_self_loops + add_self_loops of edge_index (graph kind "gat")."""
 
     @staticmethod
-    def forward(ctx, x, W, att_src, att_dst, bias, graph, heads, slope, mask, act):
+    def forward(ctx, x, W, att_src, att_dst, bias, graph, heads, slope, mask, act, bf16=False):
         _lib.require_gpu(x, W, att_src, att_dst)
         x, W = _f32c(x), _f32c(W)
         att_src, att_dst = _f32c(att_src).view(-1), _f32c(att_dst).view(-1)
@@ -639,7 +711,8 @@ class _GATConv(torch.autograd.Function):
         HC = W.size(0)
         C = HC // heads
         dev = x.device
-        XP = linear_fwd(x, W, None, _lib.LGNN_ACT_NONE)
+        dense = bf16 or not fast_shape(W.size(1), HC)
+        XP = mm_dense(x, W.t(), bf16) if dense else linear_fwd(x, W, None, _lib.LGNN_ACT_NONE)
         a_s = torch.empty(M, heads, dtype=torch.float32, device=dev)
         a_d = torch.empty(M, heads, dtype=torch.float32, device=dev)
         _lib.call("lgnn_gat_att", _lib.ptr(XP), M, heads, C, _lib.ptr(att_src), _lib.ptr(att_dst),
@@ -652,6 +725,7 @@ class _GATConv(torch.autograd.Function):
                   _lib.ptr(bias), act, _lib.ptr(alpha), _lib.ptr(Y), _s(dev))
         ctx.save_for_backward(x, W, att_src, att_dst, XP, a_s, a_d, alpha, Y, mask)
         ctx.graph, ctx.heads, ctx.slope, ctx.act = graph, heads, slope, act
+        ctx.bf16, ctx.dense = bf16, dense
         ctx.has_bias = bias is not None
         ctx.att_shape = (1, heads, C)
         return Y
@@ -681,17 +755,23 @@ class _GATConv(torch.autograd.Function):
         red = torch.empty(3 * HC, dtype=torch.float32, device=dev)
         _lib.call("lgnn_reduce_partials", _lib.ptr(part), P, 3 * HC, _lib.ptr(red), _s(dev))
         want_dx = ctx.needs_input_grad[0]
-        dx, dW, _ = linear_bwd(_lib.LGNN_GRAD_DIRECT, dXP, H=None, act=_lib.LGNN_ACT_NONE, X=x,
-                               W=W, want_dx=want_dx, want_db=False)
+        if ctx.dense:
+            dW = dw_dense(dXP, x, ctx.bf16)
+            dx = mm_dense(dXP, W, ctx.bf16) if want_dx else None
+        else:
+            dx, dW, _ = linear_bwd(_lib.LGNN_GRAD_DIRECT, dXP, H=None, act=_lib.LGNN_ACT_NONE,
+                                   X=x, W=W, want_dx=want_dx, want_db=False)
         datt_s = red[:HC].view(ctx.att_shape)
         datt_d = red[HC:2 * HC].view(ctx.att_shape)
         dbias = red[2 * HC:] if ctx.has_bias else None
-        return dx, dW, datt_s, datt_d, dbias, None, None, None, None, None
+        return dx, dW, datt_s, datt_d, dbias, None, None, None, None, None, None
 
 
 def gat_conv(x, W, att_src, att_dst, bias, graph: Graph, heads: int, slope: float = 0.2,
-             mask=None, act: int = _lib.LGNN_ACT_NONE):
-    return _GATConv.apply(x, W, att_src, att_dst, bias, graph, heads, slope, mask, act)
+             mask=None, act: int = _lib.LGNN_ACT_NONE, bf16: bool = False):
+    """bf16: the lin GEMM (and its backward) on bf16-rounded operands, fp32 accumulate/out;
+    attention, softmax and aggregation stay fp32."""
+    return _GATConv.apply(x, W, att_src, att_dst, bias, graph, heads, slope, mask, act, bf16)
 
 
 # ----------------------------------------------------------------------------------------------

@@ -236,6 +236,34 @@ def edge_softmax(src: Tensor, index: Tensor, num_nodes: int) -> Tensor:
     return out / out_sum.index_select(0, index)
 
 
+def _r16(t: Tensor) -> Tensor:
+    return t.to(torch.bfloat16).float()
+
+
+class _Bf16Linear(torch.autograd.Function):
+    """bf16 GEMM semantics of BASELINE config C3 (the GPU path's lesion_gnn_amd.ops.mm_dense):
+    every GEMM — forward y = x W^T, and backward dW = dy^T x, dx = dy W — takes bf16-rounded
+    operands and accumulates / returns fp32; bias and its gradient stay fp32."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        ctx.save_for_backward(x, W)
+        ctx.has_b = b is not None
+        return F.linear(_r16(x), _r16(W), b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W = ctx.saved_tensors
+        dW = _r16(dy).t() @ _r16(x)
+        dx = _r16(dy) @ _r16(W)
+        return dx, dW, dy.sum(0) if ctx.has_b else None
+
+
+def linear(x: Tensor, W: Tensor, b: Tensor | None, bf16: bool) -> Tensor:
+    """nn.Linear, or with bf16 the bf16-operand GEMMs of _Bf16Linear."""
+    return _Bf16Linear.apply(x, W, b) if bf16 else F.linear(x, W, b)
+
+
 class GATConv(nn.Module):
     """PyG 2.5.1 GATConv(in, out, heads, dropout), concat=True, negative_slope=0.2,
     add_self_loops=True, bias=True (state_dict: lin.weight, att_src, att_dst, bias)."""
@@ -256,7 +284,7 @@ class GATConv(nn.Module):
     def forward(self, x: Tensor, edge_index: Tensor) -> Tensor:
         H, C = self.heads, self.out_channels
         n = x.size(0)
-        xs = self.lin(x).view(-1, H, C)
+        xs = linear(x, self.lin.weight, None, getattr(self, "bf16", False)).view(-1, H, C)
         a_src = (xs * self.att_src).sum(-1)
         a_dst = (xs * self.att_dst).sum(-1)
         ei = add_self_loops(remove_self_loops(edge_index), n)
@@ -336,9 +364,11 @@ class GAT(nn.Module):
     """Reference gat.py:17-59 (SetTransformer readout branch :33-43 out of scope)."""
 
     def __init__(self, input_features: int, hiddden_channels: list[int], num_classes: int,
-                 heads: int, dropout: float, num_st_seed_points=None, pool: str = "mean"):
+                 heads: int, dropout: float, num_st_seed_points=None, pool: str = "mean",
+                 precision: str = "fp32"):
         super().__init__()
         assert num_st_seed_points is None
+        self.bf16 = precision == "bf16"
         self.in_proj = nn.Linear(input_features, hiddden_channels[0])
         self.convs = nn.ModuleList([GATConv(a, b // heads, heads=heads, dropout=dropout)
                                     for a, b in pairwise(hiddden_channels)])
@@ -346,8 +376,9 @@ class GAT(nn.Module):
         self.pool = pool
 
     def forward(self, x, edge_index, batch, num_graphs=None):
-        x = self.in_proj(x)
+        x = linear(x, self.in_proj.weight, self.in_proj.bias, self.bf16)
         for conv in self.convs:
+            conv.bf16 = self.bf16
             x = F.elu(conv(x, edge_index))
         x = _pool(self.pool)(x, batch, num_graphs)
         return self.out_proj(x)
