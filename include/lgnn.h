@@ -294,6 +294,19 @@ size_t lgnn_weight_planes_bytes(int nl);
 int lgnn_weight_planes(int nl, const float* const* W, const int* widths, uint16_t* planes,
                        uint16_t* planes_t, void* stream);
 
+/* Split-3 backward of the fused GCN stack for the closed tiles (tile_open[t] == 0), one launch per
+ * layer (stack3_bwd.hip), the same math and outputs as lgnn_gcn_stack_bwd with any L >= 1 (L + 1 <=
+ * 8): the GEMMs on bf16 MFMA at fp32 accuracy. planes_t: the transposed weight planes of layers
+ * 0..L (lgnn_weight_planes(..., planes_t)); dP [num_graphs][widths[L+1]] the pooled-output
+ * gradient; dz_ws: 2 * M * 128 floats of scratch (dZ between the layer launches); dWp/dbp slabs
+ * with num_partials = lgnn_gcn_stack_bwd_s3_partials(M) slots, every slot written. */
+int lgnn_gcn_stack_bwd_s3_partials(int64_t num_nodes);
+int lgnn_gcn_stack_bwd_s3(const float* dP, const int64_t* batch, const int32_t* gptr,
+                          int pool_mean, int64_t num_graphs, const int32_t* rowptr,
+                          const int32_t* col, const float* w, const float* X, int64_t M, int L,
+                          const uint16_t* planes_t, const float* const* H, const int* widths,
+                          float* const* dWp, float* const* dbp, int num_partials, float* dz_ws,
+                          const int32_t* tile_open, void* stream);
 /* Tiles: 64 consecutive node rows. open[t] = 1 when an edge joins tile t to another tile (its
  * layers then depend on other tiles) or when the tile holds more than 1024 CSR entries; the
  * fused stacks skip open tiles. open has lgnn_tile_count(N) + 1 entries: the last one counts the

@@ -67,6 +67,9 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_gcn_stack_fwd_s3": (I32, [P, I64, I32, I32, P, P, P, I32, P, P, P, P, P, P]),
     "lgnn_weight_planes_bytes": (SZ, [I32]),
     "lgnn_weight_planes": (I32, [I32, P, P, P, P, P]),
+    "lgnn_gcn_stack_bwd_s3_partials": (I32, [I64]),
+    "lgnn_gcn_stack_bwd_s3": (I32, [P, P, P, I32, I64, P, P, P, P, I64, I32, P, P, P, P, P, I32,
+                                    P, P, P]),
     "lgnn_knn_workspace_bytes": (SZ, [I64]),
     "lgnn_knn_graph": (I32, [P, I64, I32, P, P, I64, I32, I32, P, I64, P, SZ, P]),
     "lgnn_tile_count": (I32, [I64]),

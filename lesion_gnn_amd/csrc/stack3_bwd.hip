@@ -1,0 +1,445 @@
+// Split-3 backward of the fused GCN stack (closed tiles), one launch per layer ("layer-major"):
+// the GEMMs on bf16 MFMA at fp32 accuracy exactly as the forward (stack3.hip: three-plane
+// operands, six products, three when Â is exact in bf16). Autograd of PyG's GCNConv
+// (out = Â (H W^T) + b, torch_geometric/nn/conv/gcn_conv.py) + the model's F.elu, per layer l:
+//   G = Â^T dZ_l,   dW_l += G^T H_{l-1},   db_l += colsum dZ_l,
+//   dZ_{l-1} = (G W_l) ⊙ ELU'(H_{l-1})        (no ELU' below the first conv: in_proj has none)
+// and for in_proj (mode LIN) dW_0 += dZ_0^T X, db_0 += colsum dZ_0.
+//
+// Layouts (4 waves; wave w owns features [32w, 32w + 32) of dZ / G / dW rows and of dH columns):
+//   P layout   accumulator with the feature on the lane and 32 nodes in its 16 registers (two
+//              accumulators per 64-node tile): dZ_l is loaded straight into it; as an MFMA operand
+//              it contracts over nodes with no LDS round trip (perm16 node order)
+//   Z^T layout the node on the lane, four consecutive features per register group
+// Per tile: G (P layout) = Â^T dZ and G^T (Z^T layout) = dZ^T Â both from the dZ registers and the
+// tile's Â^T planes (LDS); H_{l-1} is staged feature-major in LDS ([k][perm16 m]) so that dW_l =
+// G^T H_{l-1} takes G from registers and H from the image, for all 128 k, into dW accumulators that
+// stay in registers over the workgroup's tiles (64 VGPRs) and are written once as partial slot
+// blockIdx.x; G^T is then written node-major ([m][perm16 n]) and dH = G W_l runs like the
+// forward's GEMM1 with the transposed weight planes (k_wplanes WpT). dZ_{l-1} goes to HBM in P
+// layout (feature on the lane: 128-B row segments) for the next launch.
+#include "common.h"
+#include "tile.h"
+#include "tile_util.h"
+#include "s3_util.h"
+
+namespace lgnn_s3 {
+
+constexpr int BM_POOL = 0;  // top conv: dZ_L = pool broadcast of dP (/ |graph|), times ELU'(H_L)
+constexpr int BM_CONV = 1;  // lower conv: dZ_l from HBM (the previous launch applied ELU')
+constexpr int BM_LIN = 2;   // in_proj: dW_0 = dZ_0^T X, db_0 only
+
+struct BwdLayerArgs {
+  const float* dZin;      // dZ_l [M][N] (CONV, LIN) or dP [B][N] (POOL)
+  const int64_t* batch;   // POOL
+  const int32_t* gptr;    // POOL
+  int pool_mean;          // POOL
+  int64_t num_graphs;     // POOL
+  const float* Hout;      // H_l [M][N] (POOL: ELU'(H_L))
+  const float* Hin;       // H_{l-1} [M][K], or X for LIN
+  const uint16_t* WpT;    // transposed planes of W_l, fragment order (POOL, CONV)
+  float* dZout;           // dZ_{l-1} [M][K] (POOL, CONV)
+  float* dWp;             // [P][N][K]
+  float* dbp;             // [P][N]
+  int N, K;               // out / in width of layer l (<= 128)
+  int elu_prev;           // dZ_{l-1} = dH * ELU'(H_{l-1})
+};
+
+struct BwdSmem {
+  unsigned char Img[3][TM * AROW];  // 48 KiB: H_{l-1} feature-major [k][perm16 m] (128 rows of
+                                    // 128 B), then G node-major [m][perm16 n] (64 rows of 256 B)
+  unsigned char Adj[3][ADJ_PLANE];  // 27 KiB: Â^T planes [source m][perm16 target]; the first
+                                    // 16 KiB hold it in fp32 while it is summed
+  float pscale[TM];                 // POOL: 1 / |graph| (mean) or 1, per tile row (0 past M)
+  int pg[TM];                       // POOL: graph id per tile row
+  int rp[TM + 1];
+  int flag;
+};
+
+// Feature-major image: row k (128 B = 64 nodes), 16-B chunk XOR-swizzled by (k >> 1) & 7 (a b128
+// read of one chunk by 16 consecutive rows is conflict-free).
+__device__ __forceinline__ int hf_chunk(int k, int c) { return k * 128 + ((c ^ ((k >> 1) & 7)) << 4); }
+__device__ __forceinline__ int hf_off(int k, int m4) {
+  const int p = perm16(m4 & 15) + (m4 & ~15);
+  return hf_chunk(k, p >> 3) + ((p & 7) << 1);
+}
+
+// A tile of a [rows][ld] fp32 matrix in P layout: lane column `colv` (< ncols, else 0), node rows
+// m = 32 a + (r & 3) + 8 (r >> 2) + 4h of the tile (rows past the buffer read 0).
+__device__ __forceinline__ void load_p(f32x16 (&v)[2], Buf b, int64_t r0, int ld, int colv,
+                                       int ncols, int h) {
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int off = colv < ncols ? (int)(((r0 + m) * ld + colv) * 4) : INT32_MAX - 3;
+      v[a][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(b, off, 0, 0));
+    }
+}
+
+// P-layout pair -> node-step operand fragments (s = 0, 1 from v[0], 2, 3 from v[1])
+__device__ __forceinline__ void split_p(const f32x16 (&v)[2], u32x4 (&o)[4][3]) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const f32x16& pa = v[s >> 1];
+    const int rb = 8 * (s & 1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const Split2 s2 = split2(pa[rb + 2 * i], pa[rb + 2 * i + 1]);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) o[s][p][i] = s2.p[p];
+    }
+  }
+}
+
+// Two workgroups per CU (77 KB LDS, 256 VGPRs each). Tried: one 512-thread workgroup whose
+// two 4-wave halves take a tile each and combine their dW at the end (half the partial slots):
+// the halves' lockstep barriers cost more (+30 %) than the slab traffic saved.
+template <int MODE>
+__global__ __launch_bounds__(NT, 2) void k_s3_bwd(const int32_t* __restrict__ rowptr,
+                                                  const int32_t* __restrict__ col,
+                                                  const float* __restrict__ w, int64_t M,
+                                                  BwdLayerArgs a, const int32_t* __restrict__ tmask) {
+  constexpr bool AGG = MODE != BM_LIN;
+  __shared__ __attribute__((aligned(16))) BwdSmem sm;
+  const int64_t ntiles = (M + TM - 1) / TM;
+  float* const scr = reinterpret_cast<float*>(sm.Adj[0]);  // fp32 Â^T [source][target]
+  const int N = a.N, K = a.K;
+  const Buf bZ = mkbuf(a.dZin, MODE == BM_POOL ? a.num_graphs * N * 4 : M * N * 4);
+  const Buf bHo = mkbuf(a.Hout, MODE == BM_POOL ? M * N * 4 : 0);
+  const Buf bHi = mkbuf(a.Hin, M * K * 4);
+  const Buf bZo = mkbuf(a.dZout, AGG ? M * K * 4 : 0);
+
+  f32x16 dw[4];
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) dw[kb] = f32x16{};
+  float dbacc = 0.f;
+  IdxRegs R;
+  int64_t t = seek_tile(blockIdx.x, ntiles, tmask, 0);
+  if (AGG && t < ntiles) {
+    idx_load_head(R, rowptr, M, t * TM);
+    idx_load_body(R, col, w);
+  }
+  for (; t < ntiles;) {
+    const int64_t r0 = t * TM;
+    const int64_t tn = seek_tile(t + gridDim.x, ntiles, tmask, 0);
+    const bool has_next = tn < ntiles;
+    {
+      const int tq = fresh_tid();
+      if (AGG) {
+#pragma unroll
+        for (int i = 0; i < TM * TM / 4 / NT; ++i) st4(scr + 4 * (tq + i * NT), zero4());
+        if (tq <= TM) sm.rp[tq] = R.rp;
+        if (tq == 0) sm.flag = 0;
+      }
+      if (MODE == BM_POOL && tq < TM) {
+        const int64_t row = r0 + tq;
+        const int64_t g = row < M ? a.batch[row] : 0;
+        const int cnt = a.gptr[g + 1] - a.gptr[g];
+        sm.pg[tq] = (int)g;
+        sm.pscale[tq] = row >= M ? 0.f : (a.pool_mean && cnt > 1 ? 1.f / (float)cnt : 1.f);
+      }
+    }
+    lds_barrier();
+    if (AGG) {
+      adj_scatter<true>(scr, sm.rp, R, r0);
+      if (has_next) idx_load_head(R, rowptr, M, tn * TM);
+    }
+    // dZ_l in P layout (feature n = 32 wave + li on the lane)
+    f32x16 dz[2];
+    {
+      const int tq = fresh_tid();
+      const int h = (tq >> 5) & 1, n = 32 * (tq >> 6) + (tq & 31);
+      if (MODE == BM_POOL) {
+        f32x16 hv[2];
+        load_p(hv, bHo, r0, N, n, N, h);
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int off = n < N ? (sm.pg[m] * N + n) * 4 : INT32_MAX - 3;
+            const float gv =
+                __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(bZ, off, 0, 0));
+            dz[q][r] = gv * sm.pscale[m] * elu_grad_from_out(hv[q][r]);
+          }
+      } else {
+        load_p(dz, bZ, r0, N, n, N, h);
+      }
+      // db_l: this lane's 32 nodes, then the partner half's
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s += dz[q][r];
+      s += __shfl_xor(s, 32, 64);
+      dbacc += s;
+    }
+    u32x4 dzp[4][3];
+    split_p(dz, dzp);
+    f32x16 g[2], gt[2];
+    if (AGG) {
+      lds_barrier();  // Â^T summed
+      f32x4 av[4];
+      {
+        const int tq = fresh_tid();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) av[i] = ld4(scr + (tq >> 2) * TM + 16 * (tq & 3) + 4 * i);
+      }
+      lds_barrier();  // every scratch read done
+      int inexact = 0;
+      {
+        const int tq = fresh_tid();
+        const int am = tq >> 2, aq = tq & 3;
+        float f[16];
+#pragma unroll
+        for (int y = 0; y < 16; ++y) {
+          const int src = perm16(y);
+          f[y] = av[src >> 2][src & 3];
+        }
+        uint32_t q[3][8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const Split2 s2 = split2(f[2 * i], f[2 * i + 1]);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) q[p][i] = s2.p[p];
+          inexact |= (s2.p[1] | s2.p[2]) != 0;
+        }
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          unsigned char* dst = sm.Adj[p] + am * ADJ_LD * 2 + 32 * aq;
+          *reinterpret_cast<u32x4*>(dst) = u32x4{q[p][0], q[p][1], q[p][2], q[p][3]};
+          *reinterpret_cast<u32x4*>(dst + 16) = u32x4{q[p][4], q[p][5], q[p][6], q[p][7]};
+        }
+      }
+      if (inexact) sm.flag = 1;
+      lds_barrier();
+      const bool exact = sm.flag == 0;
+      if (has_next) idx_load_body(R, col, w);
+      // G = Â^T dZ (P layout: A = Â^T rows m, B = dZ) and G^T = dZ^T Â (Z^T layout: A = dZ,
+      // B = Â^T rows m as columns), both over the 64 target nodes i (four k-steps)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        g[q] = f32x16{};
+        gt[q] = f32x16{};
+      }
+      {
+        const int tq = fresh_tid();
+        const int h = (tq >> 5) & 1, li = tq & 31;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int off = (32 * q + li) * ADJ_LD * 2 + 16 * (2 * s + h);
+            if (exact) {
+              const u32x4 at0 = lds16(sm.Adj[0] + off);
+              g[q] = mfma_s3_aexact(at0, dzp[s], g[q]);
+              gt[q] = mfma_s3_bexact(dzp[s], at0, gt[q]);
+            } else {
+              u32x4 at[3];
+#pragma unroll
+              for (int p = 0; p < 3; ++p) at[p] = lds16(sm.Adj[p] + off);
+              g[q] = mfma_s3(at, dzp[s], g[q]);
+              gt[q] = mfma_s3(dzp[s], at, gt[q]);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    } else {
+      g[0] = dz[0];
+      g[1] = dz[1];
+    }
+    // H_{l-1} (X for in_proj) in P layout, feature k = 32 wave + li: -> feature-major image
+    f32x16 hp[2];
+    {
+      const int tq = fresh_tid();
+      const int h = (tq >> 5) & 1, li = tq & 31, k = 32 * (tq >> 6) + li;
+      load_p(hp, bHi, r0, K, k, K, h);
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          u32x2 o[3];
+          split4(f32x4{hp[q][4 * gq], hp[q][4 * gq + 1], hp[q][4 * gq + 2], hp[q][4 * gq + 3]}, o);
+          const int off = hf_off(k, 32 * q + 8 * gq + 4 * h);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) sts8(sm.Img[p] + off, o[p]);
+        }
+    }
+    lds_barrier();  // H image complete (and, LIN, nothing else)
+    // dW_l += G^T H: A = G (P layout, node steps), B = H image rows k = 32 kb + li
+    {
+      u32x4 gp[4][3];
+      split_p(g, gp);
+      const int tq = fresh_tid();
+      const int h = (tq >> 5) & 1, li = tq & 31;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          u32x4 hb[3];
+          const int off = hf_chunk(32 * kb + li, 2 * s + h);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) hb[p] = lds16(sm.Img[p] + off);
+          dw[kb] = mfma_s3(gp[s], hb, dw[kb]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if (AGG) {
+      lds_barrier();  // every read of the H image done
+      // G^T (Z^T layout: node m on the lane, features 32 wave + 8 gq + 4h + 0..3) -> node-major
+      {
+        const int tq = fresh_tid();
+        const int h = (tq >> 5) & 1, li = tq & 31, wv = tq >> 6;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq) {
+            u32x2 o[3];
+            split4(f32x4{gt[q][4 * gq], gt[q][4 * gq + 1], gt[q][4 * gq + 2], gt[q][4 * gq + 3]},
+                   o);
+            const int off = ap_off(32 * q + li, 32 * wv + 8 * gq + 4 * h);
+#pragma unroll
+            for (int p = 0; p < 3; ++p) sts8(sm.Img[p] + off, o[p]);
+          }
+      }
+      lds_barrier();
+      // dH = G W_l (P layout: feature k on the lane): A = G image rows m, B = W_l^T planes
+      f32x16 dh[2] = {f32x16{}, f32x16{}};
+      {
+        u32x4 wf[3][8];
+        const int tq = fresh_tid();
+        const int lane = tq & 63, wv = tq >> 6, h = lane >> 5, li = lane & 31;
+        const uint16_t* base = a.WpT + wv * 8 * 512 + lane * 8;
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+          for (int s = 0; s < 8; ++s)
+            wf[p][s] = *reinterpret_cast<const u32x4*>(base + p * PLANE + 512 * s);
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            u32x4 f[3];
+            const int off = ap_chunk(32 * q + li, 2 * s + h);
+#pragma unroll
+            for (int p = 0; p < 3; ++p) f[p] = lds16(sm.Img[p] + off);
+            u32x4 b[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) b[p] = wf[p][s];
+            dh[q] = mfma_s3(f, b, dh[q]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      // dZ_{l-1} = dH * ELU'(H_{l-1}) -> HBM (P layout: feature k on the lane)
+      {
+        const int tq = fresh_tid();
+        const int h = (tq >> 5) & 1, k = 32 * (tq >> 6) + (tq & 31);
+        if (a.elu_prev) load_p(hp, bHi, r0, K, k, K, h);
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const float v = a.elu_prev ? dh[q][r] * elu_grad_from_out(hp[q][r]) : dh[q][r];
+            const int off = k < K ? (int)(((r0 + m) * K + k) * 4) : INT32_MAX - 3;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), bZo, off, 0, 0);
+          }
+      }
+    }
+    t = tn;
+  }
+  // partial slot blockIdx.x: dW rows n = 32 wave + (r & 3) + 8 (r >> 2) + 4h, columns
+  // k = 32 kb + li; db from the h = 0 lanes (both halves' sums)
+  {
+    const int tq = threadIdx.x;
+    const int h = (tq >> 5) & 1, li = tq & 31, wv = tq >> 6;
+    float* slab = a.dWp + (int64_t)blockIdx.x * N * K;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      const int k = 32 * kb + li;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = 32 * wv + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (n < N && k < K) slab[(int64_t)n * K + k] = dw[kb][r];
+      }
+    }
+    const int n = 32 * wv + li;
+    if (h == 0 && n < N) a.dbp[(int64_t)blockIdx.x * N + n] = dbacc;
+  }
+}
+
+}  // namespace lgnn_s3
+
+extern "C" int lgnn_gcn_stack_bwd_s3_partials(int64_t M) {
+  if (M < 0) return LGNN_EINVAL;
+  const int64_t ntiles = (M + lgnn_tile::TM - 1) / lgnn_tile::TM;
+  const int64_t p = ntiles < 512 ? ntiles : 512;
+  return (int)(p < 1 ? 1 : p);
+}
+
+extern "C" int lgnn_gcn_stack_bwd_s3(const float* dP, const int64_t* batch, const int32_t* gptr,
+                                     int pool_mean, int64_t num_graphs, const int32_t* rowptr,
+                                     const int32_t* col, const float* w, const float* X,
+                                     int64_t M, int L, const uint16_t* planes_t,
+                                     const float* const* H, const int* widths,
+                                     float* const* dWp, float* const* dbp, int num_partials,
+                                     float* dz_ws, const int32_t* tile_open, void* stream) {
+  if (M < 0 || L < 1 || L + 1 > LGNN_MAX_STACK || !dP || !batch || !gptr || !rowptr || !col ||
+      !X || !planes_t || !H || !widths || !dWp || !dbp || !dz_ws || !tile_open || num_graphs < 0)
+    return LGNN_EINVAL;
+  if (num_partials != lgnn_gcn_stack_bwd_s3_partials(M)) return LGNN_EINVAL;
+  for (int l = 0; l <= L; ++l) {
+    if (!lgnn_tile_fits(M, widths[l], widths[l + 1]) || !H[l] || !dWp[l] || !dbp[l])
+      return LGNN_EINVAL;
+  }
+  hipStream_t s = as_stream(stream);
+  if (M == 0) {
+    for (int l = 0; l <= L; ++l)
+      if (hipMemsetAsync(dWp[l], 0, (size_t)widths[l] * widths[l + 1] * 4, s) != hipSuccess ||
+          hipMemsetAsync(dbp[l], 0, (size_t)widths[l + 1] * 4, s) != hipSuccess)
+        return (int)hipGetLastError();
+    return LGNN_OK;
+  }
+  float* dz[2] = {dz_ws, dz_ws + M * lgnn_s3::WP};
+  const dim3 grid((unsigned)num_partials), blk(lgnn_tile::NT);
+  for (int l = L; l >= 0; --l) {
+    lgnn_s3::BwdLayerArgs a = {};
+    a.N = widths[l + 1];
+    a.K = widths[l];
+    a.dWp = dWp[l];
+    a.dbp = dbp[l];
+    a.Hin = l >= 1 ? H[l - 1] : X;
+    if (l == L) {
+      a.dZin = dP;
+      a.batch = batch;
+      a.gptr = gptr;
+      a.pool_mean = pool_mean;
+      a.num_graphs = num_graphs;
+      a.Hout = H[L];
+    } else {
+      a.dZin = dz[(L - 1 - l) & 1];
+    }
+    if (l >= 1) {
+      a.WpT = planes_t + (size_t)l * 3 * lgnn_s3::PLANE;
+      a.dZout = dz[(L - l) & 1];
+      a.elu_prev = l >= 2;
+    }
+    if (l == L)
+      hipLaunchKernelGGL(lgnn_s3::k_s3_bwd<lgnn_s3::BM_POOL>, grid, blk, 0, s, rowptr, col, w, M,
+                         a, tile_open);
+    else if (l >= 1)
+      hipLaunchKernelGGL(lgnn_s3::k_s3_bwd<lgnn_s3::BM_CONV>, grid, blk, 0, s, rowptr, col, w, M,
+                         a, tile_open);
+    else
+      hipLaunchKernelGGL(lgnn_s3::k_s3_bwd<lgnn_s3::BM_LIN>, grid, blk, 0, s, rowptr, col, w, M,
+                         a, tile_open);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
+  return LGNN_OK;
+}

@@ -124,8 +124,8 @@ using IdxRegs = IdxRegsT<NT>;
 
 template <int NTH>
 __device__ __forceinline__ void idx_load_head(IdxRegsT<NTH>& R, const int32_t* __restrict__ rowptr,
-                                              int64_t M, int64_t r0) {
-  const int tid = threadIdx.x;
+                                              int64_t M, int64_t r0, int tid_ = -1) {
+  const int tid = tid_ < 0 ? (int)threadIdx.x : tid_;
   const int64_t r = r0 + (tid <= TM ? tid : 0);
   R.rp = rowptr[r < M ? r : M];
   const int64_t rl = r0 + TM < M ? r0 + TM : M;
@@ -135,9 +135,9 @@ __device__ __forceinline__ void idx_load_head(IdxRegsT<NTH>& R, const int32_t* _
 
 template <int NTH>
 __device__ __forceinline__ void idx_load_body(IdxRegsT<NTH>& R, const int32_t* __restrict__ col,
-                                              const float* __restrict__ w) {
+                                              const float* __restrict__ w, int tid_ = -1) {
   if (R.ne > CAPE) return;
-  const int tid = threadIdx.x;
+  const int tid = tid_ < 0 ? (int)threadIdx.x : tid_;
 #pragma unroll
   for (int u = 0; u < CAPE / NTH; ++u) {
     const int j = tid + u * NTH;
@@ -182,10 +182,11 @@ __device__ __forceinline__ void idx_store(TileIdx& ti, bool& staged, const IdxRe
 // pairs carry equal weights, so the LDS float adds are order independent.
 template <bool TRANS, int NTH>
 __device__ __forceinline__ void adj_scatter(float* Adj, const int* rp, const IdxRegsT<NTH>& R,
-                                            int64_t r0) {
+                                            int64_t r0, int tid_ = -1) {
+  const int tid = tid_ < 0 ? (int)threadIdx.x : tid_;
 #pragma unroll
   for (int u = 0; u < CAPE / NTH; ++u) {
-    const int j = threadIdx.x + u * NTH;
+    const int j = tid + u * NTH;
     if (j < R.ne) {
       const int e = R.eb + j;
       int lo = 0, hi = TM;

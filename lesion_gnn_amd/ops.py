@@ -63,6 +63,11 @@ FUSED_BWD = os.environ.get("LGNN_FUSED_BWD", "1") != "0"
 # GEMM arithmetic of the fused GCN stack: "s3" = bf16 MFMA on three-plane split operands (fp32
 # accuracy, stack3.hip), "f32" = fp32 MFMA (tile.hip). LGNN_MFMA=f32 selects the latter.
 MFMA_MODE = os.environ.get("LGNN_MFMA", "s3")
+# Backward of the fused stack: the fp32 fused kernel (tile.hip k_stack_bwd, one launch) by default;
+# LGNN_BWD_S3=1 selects the split-3 layer-major kernels (stack3_bwd.hip: 3 launches, 125 us of
+# kernels vs 150 us, but 512 partial slots double the slab reduction and the step measured 1 %
+# slower on MI355X — DESIGN.md §4.3)
+BWD_S3 = os.environ.get("LGNN_BWD_S3", "0") == "1"
 
 
 def weight_planes(Ws: list, d_in: int, transposed: bool = False):
@@ -79,7 +84,7 @@ def weight_planes(Ws: list, d_in: int, transposed: bool = False):
     return planes, planes_t
 
 
-def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list):
+def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list, keep: dict | None = None):
     """in_proj + L x ELU(GCNConv) forward, every width <= 128: returns ([H_0..H_L],
     [S_1..S_L]). Tiles no edge leaves run fused through every layer (lgnn_gcn_stack_fwd); the
     rest (graphs straddling 64-node tiles) layer by layer (lgnn_node_linear_fwd_tiles), into the
@@ -97,7 +102,11 @@ def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list):
     Hp = arr(*[h.data_ptr() for h in hs])
     widths = (ctypes.c_int * (L + 1))(*[W.size(0) for W in Ws])
     if MFMA_MODE == "s3" and L >= 1:
-        planes, _ = weight_planes(Ws, x.size(1))
+        # the transposed planes (the split-3 backward's dH = G W_l operand) come from the same
+        # launch when the caller keeps them
+        planes, planes_t = weight_planes(Ws, x.size(1), transposed=keep is not None)
+        if keep is not None:
+            keep["planes_t"] = planes_t
         _lib.call("lgnn_gcn_stack_fwd_s3", _lib.ptr(x), M, x.size(1), 1, _lib.ptr(csr.rowptr),
                   _lib.ptr(csr.col), _lib.ptr(csr.w), L, _lib.ptr(planes), bp, widths, Hp,
                   _lib.ptr(open_), _s(dev))
@@ -118,7 +127,7 @@ def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list):
 
 
 def stack_bwd(dp: torch.Tensor, x: torch.Tensor, graph: Graph, mean: bool, Ws: list,
-              hs: list, ss: list, reducer: list):
+              hs: list, ss: list, reducer: list, planes_t: torch.Tensor | None = None):
     """Backward of stack_fwd from the pooled-output gradient dp down to in_proj, L = 1 or 2
     convs, no input gradient. Closed tiles run fused (lgnn_gcn_stack_bwd, one launch); open
     tiles layer by layer (lgnn_node_linear_bwd_tiles, want_open = 1, accumulate = 1) into the
@@ -130,7 +139,8 @@ def stack_bwd(dp: torch.Tensor, x: torch.Tensor, graph: Graph, mean: bool, Ws: l
     L = len(Ws) - 1
     dev = x.device
     lib = _lib.load()
-    P = lib.lgnn_gcn_stack_bwd_partials(M)
+    s3 = planes_t is not None
+    P = lib.lgnn_gcn_stack_bwd_s3_partials(M) if s3 else lib.lgnn_gcn_stack_bwd_partials(M)
     _lib.check(0 if P > 0 else P, "lgnn_gcn_stack_bwd_partials")
     widths = [x.size(1)] + [W.size(0) for W in Ws]
     per = [widths[l + 1] * widths[l] + widths[l + 1] for l in range(L + 1)]
@@ -143,11 +153,21 @@ def stack_bwd(dp: torch.Tensor, x: torch.Tensor, graph: Graph, mean: bool, Ws: l
         off += P * (nk + n)
     arr = ctypes.c_void_p * (L + 1)
     Sx = [x] + list(ss)
-    _lib.call("lgnn_gcn_stack_bwd", _lib.ptr(dp), _lib.ptr(graph.batch), _lib.ptr(graph.gptr),
-              int(mean), _lib.ptr(csr.rowptr), _lib.ptr(csr.col), _lib.ptr(csr.w), _lib.ptr(x),
-              M, L, arr(*[W.data_ptr() for W in Ws]), arr(*[h.data_ptr() for h in hs]),
-              (ctypes.c_int * (L + 2))(*widths), arr(*[t.data_ptr() for t in dWp]),
-              arr(*[t.data_ptr() for t in dbp]), P, _lib.ptr(open_), _s(dev))
+    if s3:  # one split-3 launch per layer (stack3_bwd.hip); dZ between them in dz_ws
+        dz_ws = torch.empty(2 * M * 128, dtype=torch.float32, device=dev)
+        _lib.call("lgnn_gcn_stack_bwd_s3", _lib.ptr(dp), _lib.ptr(graph.batch),
+                  _lib.ptr(graph.gptr), int(mean), dp.size(0), _lib.ptr(csr.rowptr),
+                  _lib.ptr(csr.col), _lib.ptr(csr.w), _lib.ptr(x), M, L, _lib.ptr(planes_t),
+                  arr(*[h.data_ptr() for h in hs]), (ctypes.c_int * (L + 2))(*widths),
+                  arr(*[t.data_ptr() for t in dWp]), arr(*[t.data_ptr() for t in dbp]), P,
+                  _lib.ptr(dz_ws), _lib.ptr(open_), _s(dev))
+    else:
+        _lib.call("lgnn_gcn_stack_bwd", _lib.ptr(dp), _lib.ptr(graph.batch),
+                  _lib.ptr(graph.gptr), int(mean), _lib.ptr(csr.rowptr), _lib.ptr(csr.col),
+                  _lib.ptr(csr.w), _lib.ptr(x), M, L, arr(*[W.data_ptr() for W in Ws]),
+                  arr(*[h.data_ptr() for h in hs]), (ctypes.c_int * (L + 2))(*widths),
+                  arr(*[t.data_ptr() for t in dWp]), arr(*[t.data_ptr() for t in dbp]), P,
+                  _lib.ptr(open_), _s(dev))
     dS = None
     for l in reversed(range(L + 1)):
         K, N = widths[l], widths[l + 1]
@@ -445,8 +465,11 @@ class _GCNStack(torch.autograd.Function):
         Ws = [params[2 * l] for l in range(L + 1)]
         fused = L + 1 <= STACK_MAX and all(fast_shape(W.size(1), W.size(0)) for W in Ws)
         ctx.fused = fused
+        ctx.planes_t = None
         if fused:
-            hs, ss = stack_fwd(x, graph, Ws, [params[2 * l + 1] for l in range(L + 1)])
+            keep = {} if MFMA_MODE == "s3" and BWD_S3 and L >= 1 else None
+            hs, ss = stack_fwd(x, graph, Ws, [params[2 * l + 1] for l in range(L + 1)], keep)
+            ctx.planes_t = keep.get("planes_t") if keep else None
             ctx.saved_s = [True] * L
         else:
             hs = [linear_fwd(x, W_in, b_in, _lib.LGNN_ACT_NONE)]
@@ -483,9 +506,11 @@ class _GCNStack(torch.autograd.Function):
         grads = [None] * len(params)
         grads[2 + 2 * L], grads[3 + 2 * L] = dWo, dbo
         red: list = []
-        if ctx.fused and 1 <= L <= 2 and not ctx.needs_input_grad[0] and FUSED_BWD:
+        s3 = ctx.planes_t is not None
+        if ctx.fused and (1 <= L <= 2 or s3) and not ctx.needs_input_grad[0] and FUSED_BWD:
             Ws = [params[2 * l] for l in range(L + 1)]
-            for l, (dW, db) in enumerate(stack_bwd(dp, x, graph, ctx.mean, Ws, hs, ss, red)):
+            for l, (dW, db) in enumerate(stack_bwd(dp, x, graph, ctx.mean, Ws, hs, ss, red,
+                                                   ctx.planes_t)):
                 grads[2 * l], grads[2 * l + 1] = dW, db
             reduce_multi(red, x.device)
             return (None, None, None, None, *grads)
