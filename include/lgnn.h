@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 6
+#define LGNN_ABI_VERSION 7
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -98,6 +98,20 @@ size_t lgnn_knn_workspace_bytes(int64_t num_graphs);
 int lgnn_knn_graph(const double* pos, int64_t num_nodes, int dims, const int64_t* batch,
                    const int32_t* ptr, int64_t num_graphs, int k, int loop, int64_t* edge_index,
                    int64_t num_edges, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Gaussian edge weights. Replaces lesion_gnn.transforms.GaussianDistance.__call__ (reference
+ * src/lesion_gnn/transforms.py:49-58; known answers test/test_transforms.py:8-77), the
+ * edge_weight producer of DRGNet's GraphConv stack (models/drgnet.py:55, :103):
+ *   out[e] = exp(-|pos[row_e] - pos[col_e]|^2 / (2 sigma^2)) / sqrt(2 pi sigma^2)
+ * evaluated in pos's precision (pos_f64: 0 = fp32, 1 = fp64; pos [num_nodes][dims], dims <= 16),
+ * stored as fp32 (out_f64 = 0, the reference's default dtype) or fp64. edge_index [2][num_edges]
+ * int64 (row, col). err [1] (device) = number of edges with an out-of-range index (their weight
+ * is 0). num_edges == 0 is a no-op (the reference warns and leaves the graph unchanged).
+ * ------------------------------------------------------------------------------------------- */
+int lgnn_gaussian_distance(const void* pos, int pos_f64, int64_t num_nodes, int dims,
+                           const int64_t* edge_index, int64_t num_edges, double sigma, void* out,
+                           int out_f64, int32_t* err, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Node-tile fused aggregate + linear (+bias, +activation), forward.

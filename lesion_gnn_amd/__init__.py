@@ -6,13 +6,15 @@ state_dict keys; forward/backward run on the hand-written kernels of liblgnn.so 
 include/lgnn.h). GPU only — there is no CPU fallback.
 """
 from . import _lib
-from .conv import GCNConv, global_add_pool, global_mean_pool
+from .conv import GCNConv, GraphConv, global_add_pool, global_mean_pool
 from .graph import Graph
 from .knn import KNNGraph, knn_graph
+from .transforms import GaussianDistance, SaveAs, gaussian_distance
 from .models import GCN, GCNConfig, get_model
 
-__all__ = ["GCN", "GCNConfig", "GCNConv", "Graph", "KNNGraph", "get_model", "global_mean_pool",
-           "global_add_pool", "knn_graph", "load_library"]
+__all__ = ["GCN", "GCNConfig", "GCNConv", "GaussianDistance", "Graph", "GraphConv", "KNNGraph",
+           "SaveAs", "gaussian_distance", "get_model", "global_mean_pool", "global_add_pool",
+           "knn_graph", "load_library"]
 
 
 def load_library():

@@ -72,6 +72,7 @@ SIGNATURES: dict[str, tuple] = {
                                     P, P, P]),
     "lgnn_knn_workspace_bytes": (SZ, [I64]),
     "lgnn_knn_graph": (I32, [P, I64, I32, P, P, I64, I32, I32, P, I64, P, SZ, P]),
+    "lgnn_gaussian_distance": (I32, [P, I32, I64, I32, P, I64, F64, P, I32, P, P]),
     "lgnn_tile_count": (I32, [I64]),
     "lgnn_tile_open": (I32, [P, P, I64, P, P]),
     "lgnn_node_linear_fwd_tiles": (I32, [P, I64, I32, P, P, P, F32, P, P, I32, I32, P, P, P, I32,
@@ -79,7 +80,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_bn_bwd_apply": (I32, [P, P, P, I64, I32, P, P, P, P, P, F64, I32, P, P, P, P]),
 }
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _lib = None
 

@@ -3,6 +3,8 @@ the HIP kernels of liblgnn.so.
 
 GCNConv  — PyG GCNConv(in, out): keys `lin.weight`, `bias` (added conv)
 GINConv  — PyG GINConv(nn, eps=0): keys `nn.*`, `eps` (reference gin.py:23)
+GraphConv — PyG GraphConv(in, out): keys `lin_rel.*`, `lin_root.weight` (DRGNet,
+           reference models/drgnet.py:30-33,55)
 global_mean_pool / global_add_pool — reference gin.py:33 / gat.py:56 (+ add)
 """
 from __future__ import annotations
@@ -35,6 +37,40 @@ class GCNConv(nn.Module):
     def forward(self, x: torch.Tensor, edge_index, act: int = _lib.LGNN_ACT_NONE) -> torch.Tensor:
         g = as_graph(edge_index, x.size(0))
         return ops.node_linear(x, self.lin.weight, self.bias, g, "gcn", 0.0, act)
+
+
+class GraphConv(nn.Module):
+    """out_i = lin_rel(sum_{j->i} w_ji x_j) + lin_root(x_i) (aggr 'add', no self loops), with the
+    optional per-edge weight of the reference's GaussianDistance transform (drgnet.py:55, :103).
+
+    The weighted aggregation runs in the HIP segmented-sum kernel (lgnn_spmm, transpose CSR in
+    the backward) on whichever side of lin_rel has a width divisible by 4 — A(X) W^T == A(X W^T)
+    — so DRGNet's wide input layer (d_in 1025) aggregates its `hidden` outputs and the final
+    GraphConv(hidden, 1) its inputs; the two Linears run on the tile kernels or the library GEMM
+    (ops.linear_auto)."""
+
+    def __init__(self, in_channels: int, out_channels: int):
+        super().__init__()
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.lin_rel = nn.Linear(in_channels, out_channels, bias=True)
+        self.lin_root = nn.Linear(in_channels, out_channels, bias=False)
+
+    def forward(self, x: torch.Tensor, edge_index, edge_weight: torch.Tensor | None = None
+                ) -> torch.Tensor:
+        _lib.require_gpu(x)
+        g = as_graph(edge_index, x.size(0))
+        kind = g.weighted(edge_weight) if edge_weight is not None else "gin"
+        K, N = self.in_channels, self.out_channels
+        root = ops.linear_auto(x, self.lin_root.weight)
+        if K % 4 == 0 and (N % 4 != 0 or K <= N):
+            rel = ops.linear_auto(ops.spmm(x, g, kind), self.lin_rel.weight, self.lin_rel.bias)
+        elif N % 4 == 0:
+            rel = ops.spmm(ops.linear_auto(x, self.lin_rel.weight), g, kind) + self.lin_rel.bias
+        else:  # neither width divisible by 4: zero-pad the input columns for the aggregation
+            pad = (-K) % 4
+            agg = ops.spmm(torch.nn.functional.pad(x, (0, pad)), g, kind)[:, :K]
+            rel = ops.linear_auto(agg, self.lin_rel.weight, self.lin_rel.bias)
+        return rel + root
 
 
 class BatchNorm(nn.Module):

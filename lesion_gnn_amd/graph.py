@@ -110,6 +110,30 @@ class Graph:
         self._csr[kind] = c
         return c
 
+    def weighted(self, edge_weight: torch.Tensor) -> str:
+        """Register the CSR pair carrying per-edge weights `edge_weight` [E] (edge order, e.g.
+        GaussianDistance output) for GraphConv (reference models/drgnet.py:55); returns its kind
+        key for csr(). The structure is the "gin" build (edges as given, no loops, rows in
+        edge-id order), so the weights are gathered by the stable (target | source, edge id)
+        order on the device; cached per weight tensor (and its version)."""
+        _lib.require_gpu(edge_weight)
+        if edge_weight.dim() != 1 or edge_weight.numel() != self.num_edges:
+            raise ValueError("edge_weight must be [E]")
+        key = f"w:{id(edge_weight)}:{edge_weight._version}"
+        if key in self._csr:
+            return key
+        base = self.csr("gin")
+        w = edge_weight.detach().to(torch.float32)
+        if "perm" not in self._aux:
+            self._aux["perm"] = torch.argsort(self.edge_index[1], stable=True)
+            self._aux["tperm"] = torch.argsort(self.edge_index[0], stable=True)
+        cw, ctw = torch.zeros_like(base.w), torch.zeros_like(base.tw)
+        cw[: self.num_edges] = w[self._aux["perm"]]
+        ctw[: self.num_edges] = w[self._aux["tperm"]]
+        self._csr[key] = Csr(rowptr=base.rowptr, col=base.col, w=cw, tptr=base.tptr,
+                             tidx=base.tidx, tw=ctw, tmap=None, tile_open=None, err=base.err)
+        return key
+
     def tile_open(self, kind: str) -> torch.Tensor:
         """int32 [ceil(N/64) + 1]: 1 for the 64-node tiles an edge leaves or that exceed the
         on-chip CSR capacity, then the number of such tiles (from the graph build for kind

@@ -402,3 +402,22 @@ def gaussian_distance(edge_index: Tensor, pos: Tensor, sigma: float) -> Tensor:
     row, col = edge_index
     sq = (pos[row] - pos[col]).pow(2).sum(-1)
     return torch.exp(-sq / (2 * sigma ** 2)) / math.sqrt(2 * math.pi * sigma ** 2)
+
+
+class GraphConv(nn.Module):
+    """PyG 2.5.1 GraphConv(in, out) as DRGNet stacks it (reference models/drgnet.py:30-33,
+    called with edge_weight at :55): out_i = lin_rel(sum_{j->i} w_ji x_j) + lin_root(x_i);
+    aggr='add' via scatter_add_ by target, no self loops; lin_rel has the bias, lin_root none."""
+
+    def __init__(self, in_channels: int, out_channels: int):
+        super().__init__()
+        self.lin_rel = nn.Linear(in_channels, out_channels, bias=True)
+        self.lin_root = nn.Linear(in_channels, out_channels, bias=False)
+
+    def forward(self, x: Tensor, edge_index: Tensor, edge_weight: Tensor | None = None) -> Tensor:
+        src, dst = edge_index
+        msg = x.index_select(0, src)
+        if edge_weight is not None:
+            msg = msg * edge_weight.view(-1, 1)
+        agg = scatter_sum(msg, dst, x.size(0))
+        return self.lin_rel(agg) + self.lin_root(x)

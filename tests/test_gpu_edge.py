@@ -1,0 +1,142 @@
+"""GaussianDistance edge weights (liblgnn lgnn_gaussian_distance via lesion_gnn_amd.transforms)
+and DRGNet's GraphConv (lesion_gnn_amd.conv.GraphConv) on the GPU.
+
+Pinned by the reference's own known answers: test/test_transforms.py:8-77 (sigma 1 / 0.5 / 2 on
+a two-node graph -> 0.2420 / 0.1080 / 0.1760 at rtol = atol = 1e-3, the three SaveAs modes, the
+warning on graphs without edges), restated below with the reference's inputs and tolerances.
+Random batches are checked against oracle.pyg_ref.gaussian_distance (itself pinned by the same
+KATs in tests/test_oracle.py): fp32 pos within 2 ulp-scale (rtol 1e-6: the GPU's expf and the
+CPU's may differ in the last bit), fp64 within rtol 1e-14. GraphConv forward and backward vs
+oracle.pyg_ref.GraphConv (PyG 2.5.1 semantics, parity unpinned against PyG itself) at
+rtol 1e-4 / atol 1e-5 (fp32; the aggregation side and summation order differ).
+"""
+import types
+
+import pytest
+import torch
+
+import oracle.pyg_ref as ref
+from lesion_gnn_amd import synth
+from lesion_gnn_amd.conv import GraphConv
+from lesion_gnn_amd.knn import knn_graph
+from lesion_gnn_amd.transforms import GaussianDistance, SaveAs, gaussian_distance
+
+pytestmark = pytest.mark.gpu
+
+
+def two_node(cuda):
+    return types.SimpleNamespace(
+        edge_index=torch.tensor([[0, 1], [1, 0]], device=cuda),
+        pos=torch.tensor([[0, 0], [1, 0]], dtype=torch.float, device=cuda),
+        edge_weight=torch.tensor([1, 1], dtype=torch.float, device=cuda),
+        edge_attr=torch.tensor([1, 1], dtype=torch.float, device=cuda))
+
+
+@pytest.mark.parametrize("sigma,expected", [(1, 0.2420), (0.5, 0.1080), (2, 0.1760)])
+def test_reference_kats_edge_weight(cuda, sigma, expected):
+    data = GaussianDistance(sigma=sigma, save_as=SaveAs.EDGE_WEIGHT_REPLACE)(two_node(cuda))
+    torch.testing.assert_close(data.edge_weight.cpu(), torch.tensor([expected, expected]),
+                               rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(data.edge_attr.cpu(), torch.tensor([1.0, 1.0]), rtol=1e-3,
+                               atol=1e-3)
+
+
+def test_reference_kats_edge_attr_modes(cuda):
+    data = GaussianDistance(sigma=1, save_as=SaveAs.EDGE_ATTR_CAT)(two_node(cuda))
+    torch.testing.assert_close(data.edge_attr.cpu(), torch.tensor([[1, 0.2420], [1, 0.2420]]),
+                               rtol=1e-3, atol=1e-3)
+    data = GaussianDistance(sigma=1, save_as=SaveAs.EDGE_ATTR_REPLACE)(two_node(cuda))
+    torch.testing.assert_close(data.edge_attr.cpu(), torch.tensor([[0.2420], [0.2420]]),
+                               rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("n", [2, 1])
+def test_reference_kats_no_edges_warns(cuda, n):
+    data = types.SimpleNamespace(
+        edge_index=torch.tensor([], dtype=torch.long, device=cuda),
+        pos=torch.zeros(n, 2, device=cuda),
+        edge_weight=torch.tensor([], dtype=torch.float, device=cuda),
+        edge_attr=torch.tensor([], dtype=torch.float, device=cuda))
+    with pytest.warns(UserWarning):
+        data = GaussianDistance(sigma=1)(data)
+    assert data.edge_weight.numel() == 0
+
+
+@pytest.mark.parametrize("dtype,dims,rtol", [(torch.float32, 2, 1e-6), (torch.float64, 2, 1e-14),
+                                             (torch.float64, 3, 1e-14)])
+def test_gaussian_batch_vs_oracle(cuda, dtype, dims, rtol):
+    b = synth.make_batch(200, n=64, k=6, d_in=4, seed=5, sizes="lognormal")
+    gen = torch.Generator().manual_seed(3)
+    pos = torch.rand(b.pos.size(0), dims, generator=gen, dtype=torch.float64).to(dtype)
+    for sigma in (0.05, 0.3, 1.0):
+        want = ref.gaussian_distance(b.edge_index, pos, sigma).to(torch.float32)
+        got = gaussian_distance(b.edge_index.to(cuda), pos.to(cuda), sigma).cpu()
+        torch.testing.assert_close(got, want, rtol=rtol, atol=0)
+        if dtype == torch.float64:  # fp64 output keeps the full precision
+            want64 = ref.gaussian_distance(b.edge_index, pos, sigma)
+            got64 = gaussian_distance(b.edge_index.to(cuda), pos.to(cuda), sigma,
+                                      torch.float64).cpu()
+            torch.testing.assert_close(got64, want64, rtol=rtol, atol=0)
+
+
+def test_gaussian_out_of_range_raises(cuda):
+    ei = torch.tensor([[0, 5], [1, 0]], device=cuda)
+    with pytest.raises(IndexError):
+        gaussian_distance(ei, torch.zeros(2, 2, device=cuda), 1.0)
+
+
+def _graphconv_case(cuda, K, N, weighted, seed):
+    b = synth.make_batch(24, n=40, k=6, d_in=K, seed=seed, sizes="lognormal")
+    torch.manual_seed(seed)
+    want_m = ref.GraphConv(K, N)
+    got_m = GraphConv(K, N)
+    got_m.load_state_dict(want_m.state_dict())
+    got_m = got_m.to(cuda)
+    ew = ref.gaussian_distance(b.edge_index, b.pos, 0.2).float() if weighted else None
+    x = b.x.clone().requires_grad_(True)
+    xg = b.x.to(cuda).requires_grad_(True)
+    want = want_m(x, b.edge_index, ew)
+    got = got_m(xg, b.edge_index.to(cuda), None if ew is None else ew.to(cuda))
+    gy = torch.randn(want.shape, generator=torch.Generator().manual_seed(seed + 1))
+    want.backward(gy)
+    got.backward(gy.to(cuda))
+    tol = dict(rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(got.detach().cpu(), want.detach(), **tol)
+    torch.testing.assert_close(xg.grad.cpu(), x.grad, **tol)
+    for (n1, p1), (n2, p2) in zip(want_m.named_parameters(), got_m.named_parameters()):
+        assert n1 == n2
+        torch.testing.assert_close(p2.grad.cpu(), p1.grad, **tol, msg=n1)
+
+
+@pytest.mark.parametrize("K,N", [(32, 32), (1025, 32), (32, 1), (6, 3)])
+@pytest.mark.parametrize("weighted", [True, False])
+def test_graphconv_vs_oracle(cuda, K, N, weighted):
+    _graphconv_case(cuda, K, N, weighted, seed=K + N)
+
+
+def test_drgnet_graph_stack_pipeline(cuda):
+    """kNN -> GaussianDistance -> GraphConv+ELU stack on one collated batch, all on the GPU,
+    against the oracle's op sequence (drgnet.py:52-57: x = elu(conv(x, ei, w)) per layer, cat)."""
+    b = synth.make_batch(64, n=48, k=6, d_in=16, seed=9, sizes="lognormal")
+    sizes = (b.ptr[1:] - b.ptr[:-1]).tolist()
+    batch = torch.repeat_interleave(torch.arange(len(sizes)), torch.tensor(sizes))
+    ei = knn_graph(b.pos.to(cuda), 6, batch.to(cuda), loop=True, num_graphs=len(sizes))
+    assert torch.equal(ei.cpu(), b.edge_index)
+    w = gaussian_distance(ei, b.pos.to(cuda), 0.1)
+    dims = [16, 32, 32, 1]
+    torch.manual_seed(0)
+    refs = [ref.GraphConv(a, c) for a, c in zip(dims[:-1], dims[1:])]
+    mods = []
+    for r in refs:
+        m = GraphConv(r.lin_rel.in_features, r.lin_rel.out_features)
+        m.load_state_dict(r.state_dict())
+        mods.append(m.to(cuda))
+    wr = ref.gaussian_distance(b.edge_index, b.pos, 0.1).float()
+    xr, xg, outs_r, outs_g = b.x, b.x.to(cuda), [], []
+    for r, m in zip(refs, mods):
+        xr = torch.nn.functional.elu(r(xr, b.edge_index, wr))
+        xg = torch.nn.functional.elu(m(xg, ei, w))
+        outs_r.append(xr)
+        outs_g.append(xg)
+    torch.testing.assert_close(torch.cat(outs_g, 1).detach().cpu(),
+                               torch.cat(outs_r, 1).detach(), rtol=1e-4, atol=1e-5)

@@ -125,3 +125,24 @@ def test_criterion_regression_clamp():
     logits = torch.tensor([[-1.0], [2.0], [9.0]])
     y = torch.tensor([0, 2, 4])
     assert ref.criterion("MSE", logits, y, 5).item() == 0.0
+
+
+def test_graphconv_oracle_dense_form():
+    """oracle GraphConv == dense A_w X W_rel^T + b_rel + X W_root^T (A_w[i, j] = sum of the
+    weights of edges j -> i, duplicates and self loops included as given)."""
+    torch.manual_seed(0)
+    n, K, N = 7, 5, 3
+    ei = torch.tensor([[0, 1, 2, 3, 3, 6, 5, 4, 4], [1, 0, 0, 2, 2, 6, 4, 5, 0]])
+    w = torch.rand(ei.size(1), dtype=torch.float64)
+    x = torch.randn(n, K, dtype=torch.float64)
+    conv = ref.GraphConv(K, N).double()
+    A = torch.zeros(n, n, dtype=torch.float64)
+    for e in range(ei.size(1)):
+        A[ei[1, e], ei[0, e]] += w[e]
+    want = A @ x @ conv.lin_rel.weight.T + conv.lin_rel.bias + x @ conv.lin_root.weight.T
+    torch.testing.assert_close(conv(x, ei, w), want)
+    A1 = (A > 0).double() * 0
+    for e in range(ei.size(1)):
+        A1[ei[1, e], ei[0, e]] += 1
+    want1 = A1 @ x @ conv.lin_rel.weight.T + conv.lin_rel.bias + x @ conv.lin_root.weight.T
+    torch.testing.assert_close(conv(x, ei), want1)
