@@ -93,17 +93,56 @@ def parse():
                          "HIP launch (lesion_gnn_amd.optim.Adam); fused / foreach = torch's")
     ap.add_argument("--graph", type=int, default=1,
                     help="1: replay the captured fwd+bwd and optimizer HIP graphs; 0: eager")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process-group backend for N > 1 (nccl = RCCL over xGMI on ROCm)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher/rank plumbing only: set up the process group, all-reduce a "
+                         "gradient-sized buffer once, print the JSON line with value null; "
+                         "touches no GPU (CPU tests drive this over gloo)")
     return ap.parse_args()
 
 
-def setup_dist():
+def launch_ranks(args) -> int:
+    """`--gpus N` with N > 1 and no torch.distributed environment: start N ranks on this node
+    as ONE child `torch.distributed.run` process (rendezvous on 127.0.0.1, a free port) and
+    return its exit code. Runs before anything touches the GPU, and never replaces this
+    process (no exec)."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get(
+        "HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
+
+
+def setup_dist(args):
+    """One process per GPU (LOCAL_RANK = device). Refuses a rank count that differs from
+    --gpus, so a run cannot report fewer GPUs than it was asked for."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    return world, rank, torch.device("cuda", local)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group(args.backend)
+    else:
+        dev = torch.device("cuda", local)
+        if world > 1:
+            torch.cuda.set_device(local)
+            kw = {"device_id": dev} if args.backend == "nccl" else {}
+            dist.init_process_group(args.backend, **kw)
+    if world > 1 and dist.get_world_size() != args.gpus:
+        raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, "
+                         f"--gpus {args.gpus}")
+    return world, rank, dev
 
 
 def make_batch(wl, B, seed):
@@ -283,37 +322,103 @@ def pmc_traffic(trace_name: str):
     return None, None
 
 
+def cpu_share() -> int:
+    """CPUs this process may actually use: its affinity mask, capped by the cgroup CPU quota
+    (cgroup v2 cpu.max) and by OMP_NUM_THREADS when the environment sets it. On the GPU box the affinity mask lists every host CPU (256) while the
+    job's quota is 16 CPUs; torch with 256 threads under a 16-CPU quota runs ~500x slower
+    (measured r02c: 23 s per 1024-graph step)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(float(quota) / float(period))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:  # the box exports its CPU share here (16 per GPU)
+        n = min(n, int(omp))
+    return n
+
+
 def cpu_baseline(wl, B, seconds):
-    """Oracle (plain-torch CPU restatement of the PyG path) on the host cores: same model, same
-    step (fwd + loss + bwd + Adam), bounded sample of the same workload (same batch size)."""
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
-    b = make_batch(wl, B, seed=11)
-    m = build_model(wl, oracle=True)
-    opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=2e-6)
+    """Oracle (plain-torch CPU restatement of the PyG path) on the host cores:
+    same model, same step (fwd + loss + bwd + Adam), same per-graph shapes. Two legs, each 3
+    warmup steps then the median of up to 10 timed steps (fewer if a leg passes `seconds`):
+      * all cores this process may run on (cpu_share: affinity capped by the cgroup quota),
+        B graphs per step;
+      * 1 thread, on a B/8-graph sample of the same workload (a 1024-graph step takes seconds
+        on one core; the per-graph cost does not depend on the batch size at these sizes).
+    `value` / `cores` are the all-cores leg; the host's os.cpu_count() and OMP_NUM_THREADS are
+    reported beside them."""
+    host = os.cpu_count() or 1
+    avail = cpu_share()
+    legs = []
+    for threads, nb in ((avail, B), (1, max(1, B // 8))):
+        torch.set_num_threads(threads)
+        b = make_batch(wl, nb, seed=11)
+        m = build_model(wl, oracle=True)
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=2e-6)
 
-    def step():
-        opt.zero_grad(set_to_none=True)
-        loss_fn(wl, m(b.x, b.edge_index, b.batch, B), b.y, oracle=True).backward()
-        opt.step()
+        def step():
+            opt.zero_grad(set_to_none=True)
+            loss_fn(wl, m(b.x, b.edge_index, b.batch, nb), b.y, oracle=True).backward()
+            opt.step()
 
-    step()
-    times = []
-    t_end = time.perf_counter() + seconds
-    while time.perf_counter() < t_end or len(times) < 3:
-        t0 = time.perf_counter()
-        step()
-        times.append(time.perf_counter() - t0)
-    med = statistics.median(times)
-    return {"value": round(B / med, 2), "unit": "graphs/s", "cores": threads, "kind": "port",
-            "sample": f"{len(times)} steps x {B} graphs ({wl['desc']}), median "
-                      f"{med * 1e3:.1f} ms/step, torch CPU fp32 with {threads} threads"}
+        for _ in range(3):
+            step()
+        times = []
+        t_end = time.perf_counter() + seconds / 2
+        while len(times) < 10 and (time.perf_counter() < t_end or len(times) < 3):
+            t0 = time.perf_counter()
+            step()
+            times.append(time.perf_counter() - t0)
+        med = statistics.median(times)
+        legs.append({"threads": threads, "graphs_per_step": nb, "steps": len(times),
+                     "median_ms": round(med * 1e3, 2), "value": round(nb / med, 2)})
+    main_leg = legs[0]
+    return {"value": main_leg["value"], "unit": "graphs/s", "cores": main_leg["threads"],
+            "kind": "port", "host_cpu_count": host, "cpu_share": avail,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "one_thread_value": legs[1]["value"], "legs": legs,
+            "sample": f"{wl['desc']}; all-cores leg {main_leg['steps']} steps x "
+                      f"{main_leg['graphs_per_step']} graphs, 1-thread leg {legs[1]['steps']} "
+                      f"steps x {legs[1]['graphs_per_step']} graphs; median step time after 3 "
+                      f"warmups; torch CPU fp32"}
+
+
+def dry_run(args, wl, world, rank):
+    """Plumbing check for the launcher (no GPU, no measurement): every rank all-reduces a
+    buffer the size of the model's flat gradient once; rank 0 prints the JSON line."""
+    n = sum(p.numel() for p in build_model(wl).parameters())  # module init only, on CPU
+    flat = torch.full((n,), float(rank + 1))
+    if world > 1:
+        dist.all_reduce(flat)
+        dist.barrier()
+    ok = bool(torch.all(flat == world * (world + 1) / 2))
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "graphs/s", "n_gpus": world,
+                          "dry_run": True, "allreduce_ok": ok,
+                          "dist": {"backend": args.backend if world > 1 else None,
+                                   "world_size": world},
+                          "config": {"workload": wl["desc"], "name": args.workload,
+                                     "parallelism": f"dp{world}"}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    if not ok:
+        raise SystemExit("bench.py --dry-run: all-reduce result wrong")
 
 
 def main():
     args = parse()
     wl = WORKLOADS[args.workload]
-    world, rank, dev = setup_dist()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    world, rank, dev = setup_dist(args)
+    if args.dry_run:
+        return dry_run(args, wl, world, rank)
     from lesion_gnn_amd import dist as ldist
 
     B = args.graphs_per_gpu
@@ -398,6 +503,7 @@ def main():
                    "adam": args.opt, "graphs_per_gpu": B, "global_batch": B * world,
                    "nodes": b.num_nodes, "edges": b.num_edges, "k": wl["k"], "d_in": wl["d_in"],
                    "hidden": wl["hidden"], "parallelism": f"dp{world}"},
+        "dist": {"backend": args.backend if world > 1 else None, "world_size": world},
     }
     bpb = step_bytes(b, wl)
     out["step_hbm_roofline"] = {

@@ -16,23 +16,37 @@
 
 namespace {
 
+// Each operation rounds on its own, as torch's CPU ops do. HIP's __fmul_rn / __dadd_rn are
+// plain operators carrying the `contract` flag of the header they come from, so under the
+// default -ffp-contract=fast a product feeding a sum still fuses into an FMA (an ulp of the
+// squared distance is |arg| ulps of the weight: up to ~350 at sigma = 0.05). Plain operators in
+// a contract(off) scope carry no flag and stay separate instructions.
 template <typename T>
-struct Ops;
-template <>
-struct Ops<float> {
-  static __device__ __forceinline__ float sub(float a, float b) { return __fsub_rn(a, b); }
-  static __device__ __forceinline__ float mul(float a, float b) { return __fmul_rn(a, b); }
-  static __device__ __forceinline__ float add(float a, float b) { return __fadd_rn(a, b); }
-  static __device__ __forceinline__ float div(float a, float b) { return __fdiv_rn(a, b); }
-  static __device__ __forceinline__ float ex(float a) { return expf(a); }
-};
-template <>
-struct Ops<double> {
-  static __device__ __forceinline__ double sub(double a, double b) { return __dsub_rn(a, b); }
-  static __device__ __forceinline__ double mul(double a, double b) { return __dmul_rn(a, b); }
-  static __device__ __forceinline__ double add(double a, double b) { return __dadd_rn(a, b); }
-  static __device__ __forceinline__ double div(double a, double b) { return __ddiv_rn(a, b); }
-  static __device__ __forceinline__ double ex(double a) { return exp(a); }
+struct Ops {
+  static __device__ __forceinline__ T sub(T a, T b) {
+#pragma clang fp contract(off)
+    return a - b;
+  }
+  static __device__ __forceinline__ T mul(T a, T b) {
+#pragma clang fp contract(off)
+    return a * b;
+  }
+  static __device__ __forceinline__ T add(T a, T b) {
+#pragma clang fp contract(off)
+    return a + b;
+  }
+  static __device__ __forceinline__ T div(T a, T b) {
+#pragma clang fp contract(off)
+    return a / b;  // IEEE division (div_scale / div_fmas / div_fixup), correctly rounded
+  }
+  // fp32: exp evaluated in fp64 and rounded once — the correctly rounded fp32 exp (double
+  // rounding needs a tie within 2^-29 relative), graceful in the subnormal band (exp(x) for
+  // x in [-103.9, -87.3] is subnormal in fp32 and feeds the division by the norm constant,
+  // which can bring it back into the normal range). torch's CPU expf is a <= 1-ulp
+  // approximation of the same value, so the two agree to within 2 ulp after the division in
+  // the normal range (tests/test_gpu_edge.py); in the subnormal band the CPU result itself
+  // depends on the host ISA (some vectorised expf flush it), so the test bounds it absolutely.
+  static __device__ __forceinline__ T ex(T a) { return (T)exp((double)a); }
 };
 
 template <typename T, typename O>
@@ -65,8 +79,14 @@ __global__ __launch_bounds__(256) void k_gauss(const T* __restrict__ pos, int64_
 template <typename T>
 int launch(const T* pos, int64_t n, int dims, const int64_t* ei, int64_t E, double sigma,
            void* out, int out_f64, int32_t* err, hipStream_t s) {
-  const T two_s2 = T(2.0 * sigma * sigma);  // 2 * self.sigma**2 (Python float), as T
-  const T norm = T(std::sqrt(2.0 * M_PI * sigma * sigma));  // self._norm_const (:45), as T
+  // The two constants are rounded exactly as Python evaluates the reference's expressions in
+  // double and torch then rounds the scalar operand to T: `2 * self.sigma**2` (:57) is
+  // 2 * (sigma * sigma), and `math.sqrt(2 * math.pi * sigma**2)` (:45) is
+  // sqrt((2 * pi) * (sigma * sigma)). A different association moves the constant by an ulp,
+  // which the exponent turns into |arg| ulps of the result (up to ~350 at sigma = 0.05).
+  const double s2 = sigma * sigma;
+  const T two_s2 = T(2.0 * s2);
+  const T norm = T(std::sqrt((2.0 * M_PI) * s2));
   const int64_t want = (E + 255) / 256;
   const int grid = (int)(want < 8192 ? want : 8192);
   if (out_f64)

@@ -23,11 +23,15 @@ constexpr int QT = 256;      // queries (threads) per block
 constexpr int CHUNK = 1024;  // candidates staged per round
 
 __device__ __forceinline__ double sqd(const double* a, const double* b, int D) {
+  // Plain operators in a contract(off) scope: each product and sum rounds on its own. (HIP's
+  // __dmul_rn / __dadd_rn carry their header's `contract` flag and still fuse into an FMA
+  // under the default -ffp-contract=fast.)
+#pragma clang fp contract(off)
   const double dx = a[0] - b[0], dy = a[1] - b[1];
-  double s = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
+  double s = dx * dx + dy * dy;
   if (D == 3) {
     const double dz = a[2] - b[2];
-    s = __dadd_rn(s, __dmul_rn(dz, dz));
+    s = s + dz * dz;
   }
   return s;
 }

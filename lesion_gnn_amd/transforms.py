@@ -9,9 +9,11 @@ precision of `pos`, then cast to `dtype`). The weights feed DRGNet's GraphConv s
 """
 from __future__ import annotations
 
+import dataclasses
 import math
 import warnings
 from enum import Enum
+from typing import Any
 
 import torch
 
@@ -84,3 +86,32 @@ class GaussianDistance:
 
     def __repr__(self) -> str:
         return f"{self.__class__.__name__}(sigma={self.sigma})"
+
+
+@dataclasses.dataclass(kw_only=True)
+class TransformConfig:
+    """Reference transforms.py:13-16: a transform by name plus its keyword arguments."""
+
+    name: str
+    kwargs: dict[str, Any] = dataclasses.field(default_factory=dict)
+
+
+def get_transform(config: TransformConfig):
+    """Reference transforms.py:19-23: GaussianDistance by name, otherwise the
+    torch_geometric.transforms class of that name. The graph-building transforms the reference
+    configs use run on the GPU here (KNNGraph, GaussianDistance); ToSparseTensor is accepted
+    (the models take either input form); any other PyG transform is outside the hot path and
+    raises."""
+    kw = dict(config.kwargs)
+    if config.name == "GaussianDistance":
+        return GaussianDistance(**kw)
+    if config.name == "KNNGraph":
+        from .knn import KNNGraph
+
+        return KNNGraph(**kw)
+    if config.name == "ToSparseTensor":
+        from .datasets.datamodule import ToSparseTensor
+
+        return ToSparseTensor()
+    raise NotImplementedError(f"transform {config.name!r} is not part of this package (the "
+                              "reference configs use KNNGraph and GaussianDistance)")

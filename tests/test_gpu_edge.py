@@ -5,11 +5,13 @@ Pinned by the reference's own known answers: test/test_transforms.py:8-77 (sigma
 a two-node graph -> 0.2420 / 0.1080 / 0.1760 at rtol = atol = 1e-3, the three SaveAs modes, the
 warning on graphs without edges), restated below with the reference's inputs and tolerances.
 Random batches are checked against oracle.pyg_ref.gaussian_distance (itself pinned by the same
-KATs in tests/test_oracle.py): fp32 pos within 2 ulp-scale (rtol 1e-6: the GPU's expf and the
-CPU's may differ in the last bit), fp64 within rtol 1e-14. GraphConv forward and backward vs
-oracle.pyg_ref.GraphConv (PyG 2.5.1 semantics, parity unpinned against PyG itself) at
-rtol 1e-4 / atol 1e-5 (fp32; the aggregation side and summation order differ).
+KATs in tests/test_oracle.py): fp32 pos within 2 ulp element by element (see
+test_gaussian_batch_vs_oracle), fp64 within rtol 1e-14. GraphConv forward and backward vs
+oracle.pyg_ref.GraphConv (PyG 2.5.1 semantics, parity unpinned against PyG itself): within
+1e-4 x max|tensor| of the float64 oracle, or no further from it than 2x the fp32 oracle's own
+error (assert_vs_f64; the aggregation side and summation order differ).
 """
+import math
 import types
 
 import pytest
@@ -62,16 +64,50 @@ def test_reference_kats_no_edges_warns(cuda, n):
     assert data.edge_weight.numel() == 0
 
 
-@pytest.mark.parametrize("dtype,dims,rtol", [(torch.float32, 2, 1e-6), (torch.float64, 2, 1e-14),
+def ulp_distance32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """|a - b| in units in the last place of fp32, counted through the ordered integer image
+    (so subnormals count one 2^-149 step per ulp, and +0 / a subnormal are 1 apart)."""
+    def key(t):
+        i = t.contiguous().view(torch.int32).to(torch.int64)
+        return torch.where(i < 0, -(i & 0x7FFFFFFF), i)
+    return (key(a) - key(b)).abs()
+
+
+@pytest.mark.parametrize("dtype,dims,rtol", [(torch.float32, 2, None), (torch.float32, 3, None),
+                                             (torch.float64, 2, 1e-14),
                                              (torch.float64, 3, 1e-14)])
 def test_gaussian_batch_vs_oracle(cuda, dtype, dims, rtol):
+    """fp32 pos, normal range (exp argument >= ln FLT_MIN = -87.34): within 2 ulp of torch's
+    CPU result, element by element — torch's CPU expf is a <= 1-ulp approximation (measured
+    against the correctly rounded exp on these inputs: 1-2 ulp apart after the division by the
+    norm constant), the kernel's exp is the correctly rounded one, and the squared distance
+    and the division are the same round-to-nearest operations on both sides.
+    Subnormal band (argument < -87.34; sigma = 0.05 puts 2.4k edges there and 7.7k further
+    below, where both sides are 0): what torch's CPU exp returns there depends on the host's
+    vector ISA (one vectorised expf keeps subnormals, another flushes them: GPUTEST_r01 /
+    r02a saw 0 against values of up to 128 subnormal steps), so the bar there is absolute: at
+    most FLT_MIN / norm, the size of the whole band after the division. Both bars are far
+    inside the reference's own rtol = atol = 1e-3 (test/test_transforms.py:22)."""
     b = synth.make_batch(200, n=64, k=6, d_in=4, seed=5, sizes="lognormal")
     gen = torch.Generator().manual_seed(3)
     pos = torch.rand(b.pos.size(0), dims, generator=gen, dtype=torch.float64).to(dtype)
+    row, col = b.edge_index
     for sigma in (0.05, 0.3, 1.0):
         want = ref.gaussian_distance(b.edge_index, pos, sigma).to(torch.float32)
         got = gaussian_distance(b.edge_index.to(cuda), pos.to(cuda), sigma).cpu()
-        torch.testing.assert_close(got, want, rtol=rtol, atol=0)
+        if rtol is None:
+            assert bool((got >= 0).all())
+            arg = -(pos[row] - pos[col]).pow(2).sum(-1) / (2 * sigma ** 2)
+            sub = arg < math.log(torch.finfo(torch.float32).tiny)
+            ulps = ulp_distance32(got, want)
+            bad = ulps.masked_fill(sub, 0)
+            assert int(bad.max()) <= 2, (sigma, int(bad.max()), int(bad.argmax()))
+            norm = torch.tensor(math.sqrt(2 * math.pi * sigma ** 2), dtype=torch.float32)
+            floor = float(torch.finfo(torch.float32).tiny / norm)
+            band = (got - want).abs().masked_fill(~sub, 0)
+            assert float(band.max()) <= floor, (sigma, float(band.max()), floor)
+        else:
+            torch.testing.assert_close(got, want, rtol=rtol, atol=0)
         if dtype == torch.float64:  # fp64 output keeps the full precision
             want64 = ref.gaussian_distance(b.edge_index, pos, sigma)
             got64 = gaussian_distance(b.edge_index.to(cuda), pos.to(cuda), sigma,
@@ -85,27 +121,56 @@ def test_gaussian_out_of_range_raises(cuda):
         gaussian_distance(ei, torch.zeros(2, 2, device=cuda), 1.0)
 
 
+def assert_scaled(got, want, name, tol=1e-4):
+    """Within tol x max|want| of the tensor (floor 1e-6), the suite's bar for fp32 results that
+    sum many terms in a different order (a weight gradient sums ~1000 node rows)."""
+    scale = want.abs().max().item()
+    torch.testing.assert_close(got, want, rtol=0, atol=max(tol * scale, 1e-6),
+                               msg=lambda m: f"{name}: {m}")
+
+
+def assert_vs_f64(got, want32, want64, name, tol=1e-4):
+    """The GPU result is at most 2x as far from the float64 oracle as the fp32 oracle is, or
+    within tol x max|want| of it. A reduction whose result is far smaller than its terms (a
+    bias gradient: ~1000 rows of N(0,1) summing to ~10) carries fp32 rounding noise set by
+    the terms, not by the result, on the CPU path too; this bar admits that noise and no
+    more."""
+    ref_err = (want32.double() - want64).abs()
+    err = (got.double() - want64).abs()
+    bound = torch.maximum(2 * ref_err, torch.full_like(ref_err, tol * want64.abs().max().item()))
+    bound = bound.clamp_min(1e-6)
+    bad = err > bound
+    assert not bool(bad.any()), (name, float(err.max()), float(ref_err.max()),
+                                 int(bad.sum()), err.numel())
+
+
 def _graphconv_case(cuda, K, N, weighted, seed):
     b = synth.make_batch(24, n=40, k=6, d_in=K, seed=seed, sizes="lognormal")
     torch.manual_seed(seed)
     want_m = ref.GraphConv(K, N)
+    ref64 = ref.GraphConv(K, N).double()
+    ref64.load_state_dict(want_m.state_dict())
     got_m = GraphConv(K, N)
     got_m.load_state_dict(want_m.state_dict())
     got_m = got_m.to(cuda)
-    ew = ref.gaussian_distance(b.edge_index, b.pos, 0.2).float() if weighted else None
+    ew64 = ref.gaussian_distance(b.edge_index, b.pos, 0.2) if weighted else None
+    ew = ew64.float() if weighted else None
     x = b.x.clone().requires_grad_(True)
+    x64 = b.x.double().requires_grad_(True)
     xg = b.x.to(cuda).requires_grad_(True)
     want = want_m(x, b.edge_index, ew)
+    want64 = ref64(x64, b.edge_index, ew64)
     got = got_m(xg, b.edge_index.to(cuda), None if ew is None else ew.to(cuda))
     gy = torch.randn(want.shape, generator=torch.Generator().manual_seed(seed + 1))
     want.backward(gy)
+    want64.backward(gy.double())
     got.backward(gy.to(cuda))
-    tol = dict(rtol=1e-4, atol=1e-5)
-    torch.testing.assert_close(got.detach().cpu(), want.detach(), **tol)
-    torch.testing.assert_close(xg.grad.cpu(), x.grad, **tol)
-    for (n1, p1), (n2, p2) in zip(want_m.named_parameters(), got_m.named_parameters()):
+    assert_vs_f64(got.detach().cpu(), want.detach(), want64.detach(), "out")
+    assert_vs_f64(xg.grad.cpu(), x.grad, x64.grad, "x.grad")
+    for (n1, p1), (n2, p2), (_, p3) in zip(want_m.named_parameters(), got_m.named_parameters(),
+                                            ref64.named_parameters()):
         assert n1 == n2
-        torch.testing.assert_close(p2.grad.cpu(), p1.grad, **tol, msg=n1)
+        assert_vs_f64(p2.grad.cpu(), p1.grad, p3.grad, n1)
 
 
 @pytest.mark.parametrize("K,N", [(32, 32), (1025, 32), (32, 1), (6, 3)])
@@ -138,5 +203,5 @@ def test_drgnet_graph_stack_pipeline(cuda):
         xg = torch.nn.functional.elu(m(xg, ei, w))
         outs_r.append(xr)
         outs_g.append(xg)
-    torch.testing.assert_close(torch.cat(outs_g, 1).detach().cpu(),
-                               torch.cat(outs_r, 1).detach(), rtol=1e-4, atol=1e-5)
+    for i, (og, orf) in enumerate(zip(outs_g, outs_r)):
+        assert_scaled(og.detach().cpu(), orf.detach(), f"layer {i}")
