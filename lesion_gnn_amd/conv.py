@@ -59,6 +59,8 @@ class GraphConv(nn.Module):
                 ) -> torch.Tensor:
         _lib.require_gpu(x)
         g = as_graph(edge_index, x.size(0))
+        if edge_weight is None and g.adj_values is not None:  # weighted adj_t (ToSparseTensor)
+            edge_weight = g.adj_values
         kind = g.weighted(edge_weight) if edge_weight is not None else "gin"
         K, N = self.in_channels, self.out_channels
         root = ops.linear_auto(x, self.lin_root.weight)

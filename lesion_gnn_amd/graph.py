@@ -48,6 +48,7 @@ class Graph:
         self.device = edge_index.device
         self._csr: dict[str, Csr] = {}
         self._aux: dict[str, torch.Tensor] = {}
+        self.adj_values: torch.Tensor | None = None  # values of an adj_t input (as_graph)
         self.batch = None
         self._gptr = None
         self.num_graphs = None
@@ -115,23 +116,31 @@ class Graph:
         GaussianDistance output) for GraphConv (reference models/drgnet.py:55); returns its kind
         key for csr(). The structure is the "gin" build (edges as given, no loops, rows in
         edge-id order), so the weights are gathered by the stable (target | source, edge id)
-        order on the device; cached per weight tensor (and its version)."""
+        order on the device. Edges the build drops (an index outside [0, N)) sort after every
+        valid one, so they never shift a valid edge's weight. One weighted entry per Graph,
+        reused only for the same tensor object at the same version."""
         _lib.require_gpu(edge_weight)
         if edge_weight.dim() != 1 or edge_weight.numel() != self.num_edges:
             raise ValueError("edge_weight must be [E]")
-        key = f"w:{id(edge_weight)}:{edge_weight._version}"
-        if key in self._csr:
+        key = "weighted"
+        src = self._aux.get("w_src")
+        if key in self._csr and src is not None and src[0] is edge_weight \
+                and src[1] == edge_weight._version:
             return key
         base = self.csr("gin")
         w = edge_weight.detach().to(torch.float32)
         if "perm" not in self._aux:
-            self._aux["perm"] = torch.argsort(self.edge_index[1], stable=True)
-            self._aux["tperm"] = torch.argsort(self.edge_index[0], stable=True)
+            n = self.num_nodes
+            ei = self.edge_index
+            bad = ((ei < 0) | (ei >= n)).any(0)
+            self._aux["perm"] = torch.argsort(ei[1].masked_fill(bad, n), stable=True)
+            self._aux["tperm"] = torch.argsort(ei[0].masked_fill(bad, n), stable=True)
         cw, ctw = torch.zeros_like(base.w), torch.zeros_like(base.tw)
         cw[: self.num_edges] = w[self._aux["perm"]]
         ctw[: self.num_edges] = w[self._aux["tperm"]]
         self._csr[key] = Csr(rowptr=base.rowptr, col=base.col, w=cw, tptr=base.tptr,
                              tidx=base.tidx, tw=ctw, tmap=None, tile_open=None, err=base.err)
+        self._aux["w_src"] = (edge_weight, edge_weight._version)  # holds the tensor: id stays
         return key
 
     def tile_open(self, kind: str) -> torch.Tensor:
@@ -155,33 +164,47 @@ class Graph:
         return int(self.csr(kind).err.item())
 
 
-def adj_t_to_edge_index(adj_t) -> torch.Tensor:
+def adj_t_to_edge_index(adj_t, with_values: bool = False):
     """The reference's `adj_t` input (ToSparseTensor, datasets/datamodule.py:44-45; selected at
     gin.py:59-62 / gat.py:87-90): a transposed adjacency whose row is the TARGET and column the
-    SOURCE. Accepts a torch_sparse.SparseTensor (duck-typed: `.storage.row()/.col()`) or a torch
-    sparse COO/CSR tensor. Returns edge_index [2, E] = (source, target) in row-major order."""
+    SOURCE. Accepts a torch_sparse.SparseTensor (duck-typed: `.storage.row()/.col()/.value()`) or
+    a torch sparse COO/CSR tensor. Returns edge_index [2, E] = (source, target) in row-major
+    order; with `with_values`, also the stored values [E] (ToSparseTensor moves `edge_weight`
+    there; PyG GraphConv's spmm(adj_t, x) aggregates with them) or None."""
+    vals = None
     if hasattr(adj_t, "storage") and hasattr(adj_t.storage, "row"):
         row, col = adj_t.storage.row(), adj_t.storage.col()
+        if hasattr(adj_t.storage, "value"):
+            vals = adj_t.storage.value()
     elif isinstance(adj_t, torch.Tensor) and adj_t.layout == torch.sparse_csr:
         crow = adj_t.crow_indices()
         col = adj_t.col_indices()
         row = torch.repeat_interleave(torch.arange(crow.numel() - 1, device=crow.device),
                                       crow[1:] - crow[:-1])
+        vals = adj_t.values()
     elif isinstance(adj_t, torch.Tensor) and adj_t.layout == torch.sparse_coo:
-        idx = adj_t.coalesce().indices()
+        adj_t = adj_t.coalesce()
+        idx = adj_t.indices()
         row, col = idx[0], idx[1]
+        vals = adj_t.values()
     else:
         raise TypeError(f"unsupported adjacency input {type(adj_t)}")
-    return torch.stack([col.to(torch.int64), row.to(torch.int64)])
+    ei = torch.stack([col.to(torch.int64), row.to(torch.int64)])
+    return (ei, vals) if with_values else ei
 
 
 def as_graph(edge_index, num_nodes: int, batch=None, num_graphs=None) -> Graph:
+    """edge_index [2, E] | Graph | adj_t -> Graph. An adj_t's stored values ride along as
+    `Graph.adj_values` (the edge weights of a weighted conv given no explicit edge_weight)."""
+    vals = None
     if not isinstance(edge_index, (Graph, torch.Tensor)) or (
             isinstance(edge_index, torch.Tensor) and edge_index.layout != torch.strided):
-        edge_index = adj_t_to_edge_index(edge_index)
+        edge_index, vals = adj_t_to_edge_index(edge_index, with_values=True)
     if isinstance(edge_index, Graph):
         g = edge_index
         if batch is not None and g.batch is None:
             g.set_batch(batch, num_graphs)
         return g
-    return Graph(edge_index, num_nodes, batch, num_graphs)
+    g = Graph(edge_index, num_nodes, batch, num_graphs)
+    g.adj_values = vals
+    return g

@@ -400,12 +400,13 @@ class _Spmm(torch.autograd.Function):
     def forward(ctx, x, graph, kind, self_scale):
         _lib.require_gpu(x)
         c = graph.csr(kind)
-        ctx.graph, ctx.kind, ctx.self_scale = graph, kind, self_scale
+        # the Csr itself, not its key: a later weighted() call may replace the "weighted" entry
+        ctx.c, ctx.self_scale = c, self_scale
         return spmm_raw(c.rowptr, c.col, c.w, self_scale, _f32c(x))
 
     @staticmethod
     def backward(ctx, dy):
-        c = ctx.graph.csr(ctx.kind)
+        c = ctx.c
         return spmm_raw(c.tptr, c.tidx, c.tw, ctx.self_scale, _f32c(dy)), None, None, None
 
 

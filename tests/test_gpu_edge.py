@@ -205,3 +205,82 @@ def test_drgnet_graph_stack_pipeline(cuda):
         outs_g.append(xg)
     for i, (og, orf) in enumerate(zip(outs_g, outs_r)):
         assert_scaled(og.detach().cpu(), orf.detach(), f"layer {i}")
+
+
+class _Storage:
+    """torch_sparse SparseTensor storage stand-in (duck-typed: row / col / value)."""
+
+    def __init__(self, row, col, value):
+        self._r, self._c, self._v = row, col, value
+
+    def row(self):
+        return self._r
+
+    def col(self):
+        return self._c
+
+    def value(self):
+        return self._v
+
+
+def test_graphconv_weighted_adj_t_uses_values(cuda):
+    """ToSparseTensor moves edge_weight into adj_t's values; PyG GraphConv's spmm(adj_t, x)
+    aggregates with them: adj_t input == edge_index + edge_weight input."""
+    b = synth.make_batch(16, n=30, k=5, d_in=32, seed=21)
+    w = ref.gaussian_distance(b.edge_index, b.pos, 0.2).float()
+    torch.manual_seed(0)
+    m = GraphConv(32, 16).to(cuda)
+    ei, x, wg = b.edge_index.to(cuda), b.x.to(cuda), w.to(cuda)
+    order = torch.argsort(ei[1] * b.num_nodes + ei[0])  # adj_t rows = targets
+    adj = types.SimpleNamespace(storage=_Storage(ei[1][order], ei[0][order], wg[order]))
+    want = m(x, ei, wg)
+    got = m(x, adj)
+    torch.testing.assert_close(got, want, rtol=0, atol=1e-6)
+
+
+def test_graphconv_new_weights_same_graph(cuda):
+    """One Graph reused with two weight tensors: each forward and backward uses its own weights
+    (the weighted CSR is keyed by tensor identity + version, never by id() alone)."""
+    from lesion_gnn_amd.graph import Graph
+
+    b = synth.make_batch(8, n=24, k=4, d_in=8, seed=22)
+    g = Graph(b.edge_index.to(cuda), b.num_nodes)
+    torch.manual_seed(1)
+    m = GraphConv(8, 8).to(cuda)
+    r = ref.GraphConv(8, 8)
+    r.load_state_dict({k: v.cpu() for k, v in m.state_dict().items()})
+    x = b.x.to(cuda).requires_grad_(True)
+    xr = b.x.clone().requires_grad_(True)
+    outs, refs = [], []
+    for s in (0.1, 0.5):
+        w = ref.gaussian_distance(b.edge_index, b.pos, s).float()
+        outs.append(m(x, g, w.to(cuda)))
+        refs.append(r(xr, b.edge_index, w))
+    (outs[0].sum() + 2 * outs[1].sum()).backward()
+    (refs[0].sum() + 2 * refs[1].sum()).backward()
+    for o, rr in zip(outs, refs):
+        assert_scaled(o.detach().cpu(), rr.detach(), "out")
+    assert_scaled(x.grad.cpu(), xr.grad, "x.grad")
+    w = ref.gaussian_distance(b.edge_index, b.pos, 0.1).float().to(cuda)
+    a = m(x, g, w).detach()
+    w.mul_(3.0)  # in-place change bumps the version: the CSR weights follow
+    torch.testing.assert_close(m(x, g, w).detach() - m.lin_root(x).detach(),
+                               3.0 * (a - m.lin_root(x).detach() - m.lin_rel.bias.detach())
+                               + m.lin_rel.bias.detach(), rtol=0, atol=1e-5)
+
+
+def test_graphconv_weights_skip_dropped_edges(cuda):
+    """An out-of-range edge is dropped by the graph build; the weights of the valid edges stay
+    on their own CSR slots (the weight gather sorts dropped edges last)."""
+    b = synth.make_batch(6, n=20, k=4, d_in=8, seed=23)
+    w = ref.gaussian_distance(b.edge_index, b.pos, 0.3).float()
+    n = b.num_nodes
+    bad = torch.tensor([[n + 5, 0], [0, n + 7]])  # (source out of range, target out of range)
+    ei_bad = torch.cat([bad, b.edge_index], 1)
+    w_bad = torch.cat([torch.tensor([9.0, 9.0]), w])
+    torch.manual_seed(2)
+    m = GraphConv(8, 4).to(cuda)
+    x = b.x.to(cuda)
+    want = m(x, b.edge_index.to(cuda), w.to(cuda))
+    got = m(x, ei_bad.to(cuda), w_bad.to(cuda))
+    torch.testing.assert_close(got, want, rtol=0, atol=0)
