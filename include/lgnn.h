@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 7
+#define LGNN_ABI_VERSION 8
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -379,6 +379,43 @@ int lgnn_adam_step(int n, float* const* params, const float* const* grads, float
                    unsigned int* ticket, float lr, float beta1, float beta2, float eps,
                    float weight_decay, int decoupled, int maximize, int advance,
                    void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Sort pooling (DGCNN). Replaces: PyG 2.5.1 SortAggregation(k) as DRGNet applies it to the
+ * concatenated GraphConv outputs (reference src/lesion_gnn/models/drgnet.py:37, called at :59).
+ *   x [M, D] fp32 (rows of one graph contiguous, PyG Batch order), gptr [B+1] int32 (Batch.ptr);
+ *   out [B, k*D]: per graph the rows sorted by the LAST channel descending (ties: node order,
+ *   i.e. a stable sort), the first k kept, missing rows 0; fill = min(x) - 1 and every element
+ *   equal to fill is 0 (PyG's masked_fill). rank [M] int32: each node's output row, or -1;
+ *   fill [1]: device float, written (read by the backward). Workspace:
+ *   lgnn_sort_pool_workspace_bytes(). 1 <= k <= 4096. Two launches.
+ * lgnn_sort_pool_bwd: dx [M, D] = dout[batch[i], rank[i], :] where rank[i] >= 0 and
+ *   x[i, d] != fill, else 0. One launch.
+ * ------------------------------------------------------------------------------------------- */
+size_t lgnn_sort_pool_workspace_bytes(void);
+int lgnn_sort_pool_fwd(const float* x, int64_t num_nodes, int dims, const int32_t* gptr,
+                       int64_t num_graphs, int k, float* out, int32_t* rank, float* fill,
+                       void* workspace, size_t workspace_bytes, void* stream);
+int lgnn_sort_pool_bwd(const float* dout, const float* x, const int32_t* rank,
+                       const int64_t* batch, const float* fill, int64_t num_nodes, int dims,
+                       int k, float* dx, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Lesion-node feature pooling. Replaces: extract_features_by_cc (reference
+ * src/lesion_gnn/datasets/nodes/lesions.py:88-93, called at :172) — torch_scatter
+ * scatter(features.view(C, H*W).T, cc.flatten(), 0, reduce) with reduce "mean" or "max"
+ * (FeaturesReduction, lesions.py:62-64).
+ *   features [C, num_pixels] fp32 channel-major (the encoder's (1, C, H, W), contiguous);
+ *   cc [num_pixels] int64 component labels; out [num_segments, C] fp32 (num_segments =
+ *   max(cc) + 1 as PyG sizes it): mean = sum / max(count, 1); max of an empty segment = 0.
+ *   Labels outside [0, num_segments) are skipped and counted in *err (written). counts_out
+ *   [num_segments] int32 (nullable): pixels per label. 1 <= num_segments <= 4032. Workspace:
+ *   lgnn_cc_pool_workspace_bytes. Two launches + two memsets, no host synchronisation.
+ * ------------------------------------------------------------------------------------------- */
+size_t lgnn_cc_pool_workspace_bytes(int64_t num_pixels, int channels, int num_segments);
+int lgnn_cc_pool(const float* features, int channels, int64_t num_pixels, const int64_t* cc,
+                 int num_segments, int reduce_max, float* out, int32_t* counts_out, int32_t* err,
+                 void* workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -173,3 +173,27 @@ def _pool_graph(x: torch.Tensor, batch: torch.Tensor, size: int | None) -> Graph
     _lib.require_gpu(x, batch)
     empty = torch.empty(2, 0, dtype=torch.int64, device=x.device)
     return Graph(empty, x.size(0), batch, size)
+
+
+class SortAggregation(nn.Module):
+    """PyG 2.5.1 SortAggregation(k) (reference models/drgnet.py:37, :59): per graph, rows sorted
+    by the last channel (descending, stable), top k kept (zero rows when fewer), elements equal
+    to min(x) - 1 zeroed; [ΣN, D] -> [B, k * D]. HIP: lgnn_sort_pool_fwd / _bwd."""
+
+    def __init__(self, k: int):
+        super().__init__()
+        self.k = int(k)
+
+    def forward(self, x: torch.Tensor, index: torch.Tensor | None = None,
+                ptr: torch.Tensor | None = None, dim_size: int | None = None, dim: int = -2,
+                graph: Graph | None = None) -> torch.Tensor:
+        if dim not in (-2, 0) or x.dim() != 2:
+            raise ValueError("SortAggregation: x must be [num_nodes, channels], dim=-2")
+        if graph is None:
+            if index is None:
+                raise ValueError("SortAggregation needs the batch index (or a Graph)")
+            graph = _pool_graph(x, index, dim_size)
+        return ops.sort_pool(x, graph, self.k)
+
+    def __repr__(self) -> str:
+        return f"{self.__class__.__name__}(k={self.k})"

@@ -5,16 +5,19 @@ from .base import (BaseModelConfig, BaseModule, LossType, LRSchedulerConfig, Opt
 from .gcn import GCN, GCNConfig, GCNModule
 from .gat import GAT, GATConfig, GATModule
 from .gin import GIN, GINConfig, GINModule
+from .drgnet import DRGNet, DRGNetModelConfig, DRGNetModule
 
-ModelConfig = GCNConfig | GINConfig | GATConfig
+ModelConfig = DRGNetModelConfig | GCNConfig | GINConfig | GATConfig
 
 __all__ = ["GCN", "GCNConfig", "GCNModule", "GIN", "GINConfig", "GINModule", "GAT", "GATConfig",
-           "GATModule", "BaseModule",
+           "GATModule", "DRGNet", "DRGNetModelConfig", "DRGNetModule", "BaseModule",
            "BaseModelConfig", "OptimizerConfig", "OptimizerAlgo", "LossType", "LRSchedulerConfig",
            "ModelConfig", "get_model"]
 
 
 def get_model(config) -> BaseModule:
+    if isinstance(config, DRGNetModelConfig):
+        return DRGNetModule(config)
     if isinstance(config, GCNConfig):
         return GCNModule(config)
     if isinstance(config, GINConfig):

@@ -842,3 +842,70 @@ def cross_entropy(logits, target, weight=None, validate: bool = False):
     """Weighted-mean cross-entropy of [B, C] logits vs int64 targets. validate=True checks the
     targets (one host read); otherwise out-of-range targets are skipped silently."""
     return _CrossEntropy.apply(logits, target, weight, validate)
+
+
+# ----------------------------------------------------------------------------------------------
+# SortAggregation (DRGNet) and per-component feature pooling
+# ----------------------------------------------------------------------------------------------
+
+
+class _SortPool(torch.autograd.Function):
+    """PyG 2.5.1 SortAggregation(k) (reference drgnet.py:37,59) on lgnn_sort_pool_fwd/_bwd."""
+
+    @staticmethod
+    def forward(ctx, x, graph, k):
+        _lib.require_gpu(x)
+        x = _f32c(x)
+        M, D = x.shape
+        B = graph.num_graphs
+        dev = x.device
+        out = torch.empty(B, k * D, dtype=torch.float32, device=dev)
+        rank = torch.empty(M, dtype=torch.int32, device=dev)
+        fill = torch.empty(1, dtype=torch.float32, device=dev)
+        nws = _lib.load().lgnn_sort_pool_workspace_bytes()
+        ws = torch.empty(nws, dtype=torch.uint8, device=dev)
+        _lib.call("lgnn_sort_pool_fwd", _lib.ptr(x), M, D, _lib.ptr(graph.gptr), B, int(k),
+                  _lib.ptr(out), _lib.ptr(rank), _lib.ptr(fill), _lib.ptr(ws), nws, _s(dev))
+        ctx.save_for_backward(x, rank, fill)
+        ctx.graph, ctx.k = graph, int(k)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, rank, fill = ctx.saved_tensors
+        M, D = x.shape
+        dx = torch.empty_like(x)
+        _lib.call("lgnn_sort_pool_bwd", _lib.ptr(_f32c(dout)), _lib.ptr(x), _lib.ptr(rank),
+                  _lib.ptr(ctx.graph.batch), _lib.ptr(fill), M, D, ctx.k, _lib.ptr(dx),
+                  _s(x.device))
+        return dx, None, None
+
+
+def sort_pool(x, graph: Graph, k: int):
+    """x [ΣN, D] -> [B, k * D]; graph carries batch / Batch.ptr."""
+    if graph.batch is None:
+        raise ValueError("sort_pool needs the graph's batch vector")
+    return _SortPool.apply(x, graph, k)
+
+
+def cc_pool(features: torch.Tensor, cc: torch.Tensor, num_segments: int, reduce_max: bool,
+            validate: bool = True) -> torch.Tensor:
+    """features (C, P) fp32 channel-major, cc (P,) int64 -> (num_segments, C): per-label mean or
+    max (lgnn_cc_pool). validate: raise if a label falls outside [0, num_segments) (one host
+    read)."""
+    _lib.require_gpu(features, cc)
+    f = _f32c(features)
+    C, P = f.shape
+    lab = cc.reshape(-1).to(torch.int64).contiguous()
+    if lab.numel() != P:
+        raise ValueError("cc must hold one label per pixel")
+    dev = f.device
+    out = torch.empty(num_segments, C, dtype=torch.float32, device=dev)
+    err = torch.empty(1, dtype=torch.int32, device=dev)
+    nws = _lib.load().lgnn_cc_pool_workspace_bytes(P, C, num_segments)
+    ws = torch.empty(nws, dtype=torch.uint8, device=dev)
+    _lib.call("lgnn_cc_pool", _lib.ptr(f), C, P, _lib.ptr(lab), int(num_segments),
+              int(reduce_max), _lib.ptr(out), None, _lib.ptr(err), _lib.ptr(ws), nws, _s(dev))
+    if validate and int(err.item()):
+        raise IndexError(f"cc_pool: {int(err.item())} labels outside [0, {num_segments})")
+    return out

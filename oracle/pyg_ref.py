@@ -421,3 +421,110 @@ class GraphConv(nn.Module):
             msg = msg * edge_weight.view(-1, 1)
         agg = scatter_sum(msg, dst, x.size(0))
         return self.lin_rel(agg) + self.lin_root(x)
+
+
+def to_dense_batch(x: Tensor, batch: Tensor, fill_value: float | Tensor,
+                   batch_size: int | None = None) -> tuple[Tensor, Tensor]:
+    """PyG 2.5.1 torch_geometric.utils.to_dense_batch (called by SortAggregation): [ΣN, D] ->
+    [B, Nmax, D] with fill_value padding, rows in node order within each graph."""
+    if batch_size is None:
+        batch_size = int(batch.max()) + 1 if batch.numel() else 0
+    counts = torch.bincount(batch, minlength=batch_size)
+    cum = torch.cat([counts.new_zeros(1), counts.cumsum(0)])
+    nmax = int(counts.max()) if counts.numel() else 0
+    idx = torch.arange(batch.numel()) - cum[batch] + batch * nmax
+    out = x.new_full((batch_size * nmax, x.size(1)), 0.0) + fill_value
+    out = out.index_put((idx,), x)  # out-of-place so autograd reaches x
+    mask = torch.zeros(batch_size * nmax, dtype=torch.bool)
+    mask[idx] = True
+    return out.view(batch_size, nmax, x.size(1)), mask.view(batch_size, nmax)
+
+
+def sort_aggregation(x: Tensor, batch: Tensor, k: int, batch_size: int | None = None) -> Tensor:
+    """PyG 2.5.1 SortAggregation(k) (reference models/drgnet.py:37, called at :59): pad each
+    graph with fill = min(x) - 1, sort its rows by the last channel (descending; ties by node
+    order — torch's CPU sort is stable), keep the first k rows (pad with fill rows when the
+    graph has fewer), zero every element equal to fill, flatten to [B, k * D]."""
+    fill_value = x.detach().min() - 1
+    bx, _ = to_dense_batch(x, batch, fill_value, batch_size)
+    B, N, D = bx.size()
+    _, perm = bx[:, :, -1].sort(dim=-1, descending=True, stable=True)
+    perm = perm + (torch.arange(B) * N).view(-1, 1)
+    bx = bx.reshape(B * N, D)[perm].view(B, N, D)
+    if N >= k:
+        bx = bx[:, :k].contiguous()
+    else:
+        bx = torch.cat([bx, bx.new_full((B, k - N, D), 0.0) + fill_value], dim=1)
+    bx = bx.masked_fill(bx == fill_value, 0.0)
+    return bx.view(B, k * D)
+
+
+class MLPPlain(nn.Module):
+    """PyG 2.5.1 MLP(channel_list, dropout, norm=None, act=F.elu), plain_last=True (reference
+    drgnet.py:48): Lin -> act -> dropout ... -> Lin; state_dict keys lins.{i}.*."""
+
+    def __init__(self, channel_list: list[int], dropout: float = 0.0):
+        super().__init__()
+        self.lins = nn.ModuleList([nn.Linear(a, b) for a, b in pairwise(channel_list)])
+        self.dropout = dropout
+
+    def forward(self, x: Tensor) -> Tensor:
+        for lin in self.lins[:-1]:
+            x = F.dropout(F.elu(lin(x)), self.dropout, self.training)
+        return self.lins[-1](x)
+
+
+class DRGNet(nn.Module):
+    """Reference models/drgnet.py:16-69: GraphConv stack (ELU after each, outputs concatenated),
+    SortAggregation(k), Conv1d(1, c0, D, stride D) -> ELU -> MaxPool1d(2, 2) -> Conv1d(c0, c1, 5)
+    -> ELU -> flatten -> MLP([dense, 128, C], dropout 0.5)."""
+
+    def __init__(self, input_features: int, gnn_hidden_dim: int, num_layers: int,
+                 sortpool_k: int, num_classes: int, conv_hidden_dims: tuple[int, int] = (16, 32),
+                 dropout: float = 0.5):
+        super().__init__()
+        dims = [input_features] + [gnn_hidden_dim] * num_layers
+        self.graph_convs = nn.ModuleList([GraphConv(a, b) for a, b in pairwise(dims)])
+        self.graph_convs.append(GraphConv(gnn_hidden_dim, 1))
+        total = gnn_hidden_dim * num_layers + 1
+        self.k = sortpool_k
+        self.conv1 = nn.Conv1d(1, conv_hidden_dims[0], kernel_size=total, stride=total)
+        self.max_pool = nn.MaxPool1d(2, 2)
+        self.conv2 = nn.Conv1d(conv_hidden_dims[0], conv_hidden_dims[1], kernel_size=5, stride=1)
+        dense = int((sortpool_k - 2) / 2 + 1)
+        dense = (dense - 5 + 1) * conv_hidden_dims[1]
+        self.mlp = MLPPlain([dense, 128, num_classes], dropout=dropout)
+
+    def forward(self, x: Tensor, edge_index: Tensor, batch: Tensor,
+                edge_weight: Tensor | None = None, num_graphs: int | None = None) -> Tensor:
+        xs = []
+        for conv in self.graph_convs:
+            x = F.elu(conv(x, edge_index, edge_weight))
+            xs.append(x)
+        x = sort_aggregation(torch.cat(xs, dim=1), batch, self.k, num_graphs).unsqueeze(1)
+        x = self.max_pool(F.elu(self.conv1(x)))
+        x = F.elu(self.conv2(x))
+        return self.mlp(x.view(x.size(0), -1))
+
+
+def extract_features_by_cc(cc: Tensor, features: Tensor, nlabel: int,
+                           reduce: str = "mean") -> Tensor:
+    """Reference datasets/nodes/lesions.py:88-93: features (1, C, H, W), cc (H, W) int64
+    component labels -> per-label mean (or sum) of the pixel features, [max(cc) + 1, C]
+    (torch_scatter.scatter along dim 0: sum, then / clamp(count, 1) for mean). nlabel == 1
+    returns the global average (1, C)."""
+    if nlabel == 1:
+        return features.mean((2, 3))
+    f = features.squeeze(0).flatten(1, 2).transpose(0, 1)  # (H*W, C)
+    idx = cc.flatten()
+    size = int(idx.max()) + 1
+    if reduce == "max":  # PyG scatter(reduce="max"): scatter_reduce_ amax, include_self=False
+        ix = idx.view(-1, 1).expand_as(f)
+        return f.new_zeros(size, f.size(1)).scatter_reduce_(0, ix, f, "amax", include_self=False)
+    if reduce not in ("sum", "add", "mean"):
+        raise ValueError(reduce)
+    out = f.new_zeros(size, f.size(1)).index_add_(0, idx, f)
+    if reduce == "mean":
+        cnt = torch.bincount(idx, minlength=size).clamp_min(1).to(f.dtype)
+        out = out / cnt.view(-1, 1)
+    return out

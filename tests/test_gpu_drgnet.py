@@ -1,0 +1,181 @@
+"""DRGNet path on the GPU and the lesion-node feature pooling (§8f rank 4).
+
+* SortAggregation (reference models/drgnet.py:37,59; PyG 2.5.1 semantics in
+  oracle.pyg_ref.sort_aggregation): pure data movement, so forward and backward are compared
+  BIT-EXACT with the oracle — graphs smaller and larger than k, an empty graph, ties in the sort
+  key (stable: node order), k larger than every graph.
+* DRGNet (drgnet.py:16-69) end to end: kNN -> GaussianDistance -> GraphConv x (L + 1) ->
+  SortAggregation -> Conv1d/MaxPool/Conv1d/MLP, forward + backward vs oracle.pyg_ref.DRGNet with
+  the same weights (eval mode: the MLP's dropout 0.5 off); fp32 bar 1e-4 (logits absolute,
+  gradients × max|grad| per tensor, floor 1e-6).
+* extract_features_by_cc (datasets/nodes/lesions.py:88-93) vs oracle.pyg_ref.extract_features_by_cc:
+  max bit-exact; mean within 2× the fp32 oracle's own error against a float64 restatement (or
+  1e-6 relative to the largest mean) — sums of up to 262k pixels in a different order.
+"""
+import pytest
+import torch
+
+import oracle.pyg_ref as ref
+from lesion_gnn_amd import synth
+from lesion_gnn_amd.conv import SortAggregation
+from lesion_gnn_amd.datasets.nodes.lesions import extract_features_by_cc
+from lesion_gnn_amd.graph import Graph
+from lesion_gnn_amd.knn import knn_graph
+from lesion_gnn_amd.models.drgnet import DRGNet
+from lesion_gnn_amd.transforms import gaussian_distance
+
+pytestmark = pytest.mark.gpu
+
+
+def _sort_case(sizes, D, k, seed, ties=False):
+    gen = torch.Generator().manual_seed(seed)
+    batch = torch.repeat_interleave(torch.arange(len(sizes)), torch.tensor(sizes))
+    x = torch.randn(int(sum(sizes)), D, generator=gen)
+    if ties:  # few distinct keys -> long runs of equal keys (stable order decides)
+        x[:, -1] = torch.randint(0, 3, (x.size(0),), generator=gen).float()
+    return x, batch
+
+
+@pytest.mark.parametrize("sizes,D,k,ties", [
+    ([5, 40, 1, 30, 12], 7, 10, False),
+    ([64] * 32, 97, 30, False),
+    ([3, 0, 17, 9], 4, 8, True),      # an empty graph in the middle
+    ([200, 513, 31], 33, 30, True),   # a graph larger than the kernel's thread count
+    ([4, 6], 5, 50, False),           # k above every graph size
+])
+def test_sort_aggregation_bitexact(cuda, sizes, D, k, ties):
+    x, batch = _sort_case(sizes, D, k, seed=sum(sizes) + D, ties=ties)
+    B = len(sizes)
+    xr = x.clone().requires_grad_(True)
+    want = ref.sort_aggregation(xr, batch, k, batch_size=B)
+    gy = torch.randn(want.shape, generator=torch.Generator().manual_seed(k))
+    want.backward(gy)
+    xg = x.to(cuda).requires_grad_(True)
+    g = Graph(torch.empty(2, 0, dtype=torch.int64, device=cuda), x.size(0), batch.to(cuda), B)
+    got = SortAggregation(k)(xg, graph=g)
+    got.backward(gy.to(cuda))
+    assert got.shape == (B, k * D)
+    assert torch.equal(got.detach().cpu(), want.detach())
+    assert torch.equal(xg.grad.cpu(), xr.grad)
+
+
+def test_sort_aggregation_index_api(cuda):
+    """PyG call form: sort_pool(x_cat, batch) (drgnet.py:59)."""
+    x, batch = _sort_case([10, 3, 25], 6, 12, seed=5)
+    want = ref.sort_aggregation(x, batch, 12)
+    got = SortAggregation(12)(x.to(cuda), batch.to(cuda))
+    assert torch.equal(got.cpu(), want)
+
+
+def _drgnet_pair(d_in, hidden, layers, k, classes, scale, seed=1234):
+    torch.manual_seed(seed)
+    ours = DRGNet(d_in, hidden, layers, k, classes)
+    with torch.no_grad():  # keep the GraphConv outputs out of ELU saturation (see below)
+        for c in ours.graph_convs:
+            c.lin_rel.weight.mul_(scale)
+            c.lin_root.weight.mul_(scale)
+    oref = ref.DRGNet(d_in, hidden, layers, k, classes)
+    missing = oref.load_state_dict(ours.state_dict())
+    assert not missing.missing_keys and not missing.unexpected_keys
+    return ours, oref
+
+
+def _key_margin(oref, b, ew, k):
+    """Smallest gap between consecutive sort keys (last channel of the concatenated GraphConv
+    outputs) among each graph's top k + 1 in the oracle."""
+    x, xs = b.x, []
+    for c in oref.graph_convs:
+        x = torch.nn.functional.elu(c(x, b.edge_index, ew))
+        xs.append(x)
+    key = torch.cat(xs, 1)[:, -1].detach()
+    ptr, m = b.ptr.tolist(), float("inf")
+    for g in range(len(ptr) - 1):
+        kk = key[ptr[g]:ptr[g + 1]].sort(descending=True).values[:k + 1]
+        if kk.numel() > 1:
+            m = min(m, float((kk[:-1] - kk[1:]).min()))
+    return m
+
+
+@pytest.mark.parametrize("d_in,hidden,layers,k,B,seed", [(1025, 32, 3, 30, 64, 95),
+                                                         (16, 8, 2, 10, 20, 32)])
+def test_drgnet_step_vs_oracle(cuda, d_in, hidden, layers, k, B, seed):
+    """Sort pooling is discontinuous in its keys: two keys closer than the fp32 difference of
+    the GPU and CPU GraphConv outputs (~1e-6 here) can swap, which changes a graph's whole
+    pooled row. With the reference init and GaussianDistance(0.1) weights the last GraphConv's
+    outputs sit deep in ELU saturation (keys -0.99999x, spaced 1e-7 apart), so every graph
+    has such near-ties — on PyG's own CPU-vs-GPU runs too. The case therefore scales the
+    GraphConv weights (same weights both sides) and asserts its own conditioning: every key gap
+    in the top k + 1 >= 1e-5, 10x the key error."""
+    b = synth.make_batch(B, n=24, k=6, d_in=d_in, seed=seed, sizes="lognormal",
+                         last_channel_class=d_in > 64)
+    ew = ref.gaussian_distance(b.edge_index, b.pos, 0.1).float()
+    ours, oref = _drgnet_pair(d_in, hidden, layers, k, 5, scale=0.25)
+    ours = ours.to(cuda).eval()
+    oref.eval()
+    assert _key_margin(oref, b, ew, k) >= 1e-5
+    # the data side on the GPU too: kNN graph + GaussianDistance, checked against the batch
+    ei = knn_graph(b.pos.to(cuda), 6, b.batch.to(cuda), loop=True, num_graphs=b.num_graphs)
+    assert torch.equal(ei.cpu(), b.edge_index)
+    w = gaussian_distance(ei, b.pos.to(cuda), 0.1)
+    lo = ours(b.x.to(cuda), ei, b.batch.to(cuda), w, b.num_graphs)
+    lr_ = oref(b.x, b.edge_index, b.batch, ew, b.num_graphs)
+    torch.testing.assert_close(lo.detach().cpu(), lr_.detach(), rtol=0, atol=1e-4)
+    y = b.y % 5
+    torch.nn.functional.cross_entropy(lo, y.to(cuda)).backward()
+    torch.nn.functional.cross_entropy(lr_, y).backward()
+    for (n1, p1), (n2, p2) in zip(oref.named_parameters(), ours.named_parameters()):
+        assert n1 == n2
+        s = p1.grad.abs().max().item()
+        torch.testing.assert_close(p2.grad.cpu(), p1.grad, rtol=0, atol=max(1e-4 * s, 1e-6),
+                                   msg=lambda m: f"{n1}: {m}")
+
+
+def _components(H, W, n, gen):
+    """Background 0 + n axis-aligned blobs (overlaps: later blob wins), labels 1..n."""
+    cc = torch.zeros(H, W, dtype=torch.int64)
+    for i in range(1, n + 1):
+        h = int(torch.randint(1, max(2, H // 8), (1,), generator=gen))
+        w = int(torch.randint(1, max(2, W // 8), (1,), generator=gen))
+        y0 = int(torch.randint(0, H - h + 1, (1,), generator=gen))
+        x0 = int(torch.randint(0, W - w + 1, (1,), generator=gen))
+        cc[y0:y0 + h, x0:x0 + w] = i
+    # relabel so every label 0..m-1 is present (as connectedComponents returns them)
+    _, cc = torch.unique(cc, return_inverse=True)
+    return cc.view(H, W)
+
+
+@pytest.mark.parametrize("C,H,W,n", [(1025, 64, 64, 40), (64, 512, 512, 300), (3, 16, 16, 5)])
+@pytest.mark.parametrize("reduce", ["mean", "max"])
+def test_extract_features_by_cc(cuda, C, H, W, n, reduce):
+    gen = torch.Generator().manual_seed(C + H + n)
+    cc = _components(H, W, n, gen)
+    feats = torch.randn(1, C, H, W, generator=gen)
+    nlabel = int(cc.max()) + 1
+    got = extract_features_by_cc(cc.to(cuda), feats.to(cuda), nlabel, reduce).cpu()
+    want = ref.extract_features_by_cc(cc, feats, nlabel, reduce)
+    assert got.shape == want.shape == (nlabel, C)
+    if reduce == "max":
+        assert torch.equal(got, want)
+        return
+    want64 = ref.extract_features_by_cc(cc, feats.double(), nlabel, reduce)
+    ref_err = (want.double() - want64).abs()
+    err = (got.double() - want64).abs()
+    bound = torch.maximum(2 * ref_err, torch.full_like(ref_err, 1e-6 * want64.abs().max().item()))
+    assert bool((err <= bound).all()), (float(err.max()), float(ref_err.max()))
+    again = extract_features_by_cc(cc.to(cuda), feats.to(cuda), nlabel, reduce).cpu()
+    assert torch.equal(got, again)  # deterministic
+
+
+def test_extract_features_single_label_is_global_mean(cuda):
+    feats = torch.randn(1, 8, 32, 32, generator=torch.Generator().manual_seed(3))
+    cc = torch.zeros(32, 32, dtype=torch.int64)
+    got = extract_features_by_cc(cc.to(cuda), feats.to(cuda), 1).cpu()
+    torch.testing.assert_close(got, feats.mean((2, 3)), rtol=1e-6, atol=1e-7)
+
+
+def test_cc_pool_out_of_range_raises(cuda):
+    from lesion_gnn_amd import ops
+
+    cc = torch.tensor([0, 1, 5], device=cuda)
+    with pytest.raises(IndexError):
+        ops.cc_pool(torch.ones(2, 3, device=cuda), cc, 2, reduce_max=False)

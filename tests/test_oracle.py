@@ -146,3 +146,26 @@ def test_graphconv_oracle_dense_form():
         A1[ei[1, e], ei[0, e]] += 1
     want1 = A1 @ x @ conv.lin_rel.weight.T + conv.lin_rel.bias + x @ conv.lin_root.weight.T
     torch.testing.assert_close(conv(x, ei), want1)
+
+
+def test_sort_aggregation_known_answer():
+    """PyG SortAggregation semantics (reference drgnet.py:37,59): rows by last channel
+    descending, ties in node order, top k, short graphs zero-padded, x.min()-1 fill zeroed."""
+    x = torch.tensor([[1., 5.], [2., 7.], [3., 5.], [4., -1.], [9., 0.]])
+    batch = torch.tensor([0, 0, 0, 1, 1])
+    out = ref.sort_aggregation(x, batch, 3).view(2, 3, 2)
+    assert torch.equal(out[0], torch.tensor([[2., 7.], [1., 5.], [3., 5.]]))
+    assert torch.equal(out[1], torch.tensor([[9., 0.], [4., -1.], [0., 0.]]))
+    out2 = ref.sort_aggregation(x, batch, 2).view(2, 2, 2)
+    assert torch.equal(out2[0], torch.tensor([[2., 7.], [1., 5.]]))
+
+
+def test_extract_features_by_cc_known_answer():
+    """lesions.py:88-93: per-label mean / max over the (H*W, C) view of (1, C, H, W)."""
+    feats = torch.arange(8, dtype=torch.float32).view(1, 2, 2, 2)  # c0: 0..3, c1: 4..7
+    cc = torch.tensor([[0, 1], [1, 0]])
+    mean = ref.extract_features_by_cc(cc, feats, 2, "mean")
+    assert torch.equal(mean, torch.tensor([[1.5, 5.5], [1.5, 5.5]]))
+    mx = ref.extract_features_by_cc(cc, feats, 2, "max")
+    assert torch.equal(mx, torch.tensor([[3., 7.], [2., 6.]]))
+    assert torch.equal(ref.extract_features_by_cc(cc, feats, 1), feats.mean((2, 3)))
