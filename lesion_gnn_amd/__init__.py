@@ -6,6 +6,7 @@ state_dict keys; forward/backward run on the hand-written kernels of liblgnn.so 
 include/lgnn.h). GPU only — there is no CPU fallback.
 """
 from . import _lib
+from . import library  # noqa: F401  (registers the lgnn:: custom ops for torch.compile)
 from .conv import GCNConv, GraphConv, global_add_pool, global_mean_pool
 from .graph import Graph
 from .knn import KNNGraph, knn_graph

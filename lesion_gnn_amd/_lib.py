@@ -129,7 +129,9 @@ def stream(device: torch.device | None = None) -> int:
 def require_gpu(*tensors: torch.Tensor) -> None:
     """The product path is HIP-only: refuse CPU tensors instead of silently falling back."""
     for t in tensors:
-        if t is not None and not t.is_cuda:
+        # meta tensors only while torch.compile / torch.export traces (shape propagation
+        # through the fake kernels of library.py; nothing is launched)
+        if t is not None and not t.is_cuda and not (t.is_meta and torch.compiler.is_compiling()):
             raise LgnnError("lesion_gnn_amd ops run on the GPU only (HIP kernels); got a CPU "
                             "tensor. There is no CPU fallback by design.")
 

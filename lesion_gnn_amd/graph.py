@@ -73,6 +73,8 @@ class Graph:
     @property
     def gptr(self) -> torch.Tensor | None:
         """int32 [num_graphs + 1] graph offsets (Batch.ptr)."""
+        if self._gptr is None and self.batch is not None and torch.compiler.is_compiling():
+            self._gptr = torch.ops.lgnn.batch_ptr(self.batch, self.num_graphs)
         if self._gptr is None and self.batch is not None:
             self._gptr = torch.empty(self.num_graphs + 1, dtype=torch.int32, device=self.device)
             _lib.call("lgnn_batch_ptr", _lib.ptr(self.batch), self.num_nodes, self.num_graphs,
@@ -82,6 +84,14 @@ class Graph:
     def csr(self, kind: str) -> Csr:
         if kind in self._csr:
             return self._csr[kind]
+        if torch.compiler.is_compiling():  # traced: the graph build is one opaque lgnn op
+            rp, col, w, tp, ti, tw, tmap, topen, err = torch.ops.lgnn.graph_build(
+                self.edge_index, self.num_nodes, kind)
+            c = Csr(rowptr=rp, col=col, w=w, tptr=tp, tidx=ti, tw=tw,
+                    tmap=tmap if kind == "gat" else None,
+                    tile_open=topen if kind == "gcn" else None, err=err)
+            self._csr[kind] = c
+            return c
         loops, norm = KIND[kind]
         n, e = self.num_nodes, self.num_edges
         cap = e + n
@@ -123,6 +133,13 @@ class Graph:
         if edge_weight.dim() != 1 or edge_weight.numel() != self.num_edges:
             raise ValueError("edge_weight must be [E]")
         key = "weighted"
+        if torch.compiler.is_compiling():
+            base = self.csr("gin")
+            cw, ctw = torch.ops.lgnn.weighted_csr(self.edge_index, edge_weight, self.num_nodes,
+                                                  base.w)
+            self._csr[key] = Csr(rowptr=base.rowptr, col=base.col, w=cw, tptr=base.tptr,
+                                 tidx=base.tidx, tw=ctw, tmap=None, tile_open=None, err=base.err)
+            return key
         src = self._aux.get("w_src")
         if key in self._csr and src is not None and src[0] is edge_weight \
                 and src[1] == edge_weight._version:

@@ -95,7 +95,7 @@ class DRGNetModule(BaseModule):
 
     def __init__(self, config: DRGNetModelConfig):
         super().__init__(config)
-        self.model = DRGNet(
+        model = DRGNet(
             input_features=config.input_features.value,
             gnn_hidden_dim=config.gnn_hidden_dim,
             num_layers=config.num_layers,
@@ -103,6 +103,9 @@ class DRGNetModule(BaseModule):
             num_classes=1 if self.is_regression else config.num_classes.value,
             conv_hidden_dims=config.conv_hidden_dims,
         )
+        # reference drgnet.py:103: the model is compiled when the config asks (library.py holds the
+        # lgnn:: custom ops + fake kernels Dynamo traces)
+        self.model = torch.compile(model, dynamic=True) if config.compile else model
 
     def forward(self, data) -> torch.Tensor:
         edge_index = getattr(data, "adj_t", None)

@@ -72,7 +72,7 @@ class GATModule(BaseModule):
 
     def __init__(self, config: GATConfig):
         super().__init__(config)
-        self.model = GAT(
+        model = GAT(
             input_features=config.input_features.value,
             hiddden_channels=config.hiddden_channels,
             num_classes=1 if self.is_regression else config.num_classes.value,
@@ -82,3 +82,6 @@ class GATModule(BaseModule):
             pool=config.pool,
             precision=config.precision,
         )
+        # reference gat.py:84: the model is compiled when the config asks (library.py holds the
+        # lgnn:: custom ops + fake kernels Dynamo traces)
+        self.model = torch.compile(model, dynamic=True) if config.compile else model

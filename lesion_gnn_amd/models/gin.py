@@ -72,10 +72,13 @@ class GINModule(BaseModule):
 
     def __init__(self, config: GINConfig):
         super().__init__(config)
-        self.model = GIN(
+        model = GIN(
             input_features=config.input_features.value,
             hidden_channels=config.hidden_channels,
             num_classes=1 if self.is_regression else config.num_classes.value,
             dropout=config.dropout,
             pool=config.pool,
         )
+        # reference gin.py:56: the model is compiled when the config asks (library.py holds the
+        # lgnn:: custom ops + fake kernels Dynamo traces)
+        self.model = torch.compile(model, dynamic=True) if config.compile else model

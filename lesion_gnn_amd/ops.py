@@ -19,6 +19,18 @@ from . import _lib
 from .graph import Csr, Graph
 
 
+def _compiling() -> bool:
+    """True while torch.compile / torch.export traces: the ops then dispatch to their
+    torch.library custom ops (library.py) instead of the eager autograd.Functions."""
+    return torch.compiler.is_compiling()
+
+
+def _lgnn():
+    from . import library
+
+    return library
+
+
 def _f32c(t: torch.Tensor) -> torch.Tensor:
     if t.dtype != torch.float32:
         raise TypeError(f"expected float32, got {t.dtype}")
@@ -320,6 +332,11 @@ class _NodeLinear(torch.autograd.Function):
 
 def node_linear(x, W, b=None, graph: Graph | None = None, kind: str = "gcn",
                 self_scale: float = 0.0, act: int = _lib.LGNN_ACT_NONE):
+    if _compiling():
+        lib = _lgnn()
+        g = lib.gparts(graph, kind) if graph is not None else lib.gparts_empty(x.device)
+        return torch.ops.lgnn.node_linear(x, W, b, g, kind if graph is not None else "",
+                                          float(self_scale), int(act))
     return _NodeLinear.apply(x, W, b, graph, kind, self_scale, act)
 
 
@@ -384,6 +401,8 @@ class _DenseLinear(torch.autograd.Function):
 
 
 def dense_linear(x, W, b=None, bf16: bool = False):
+    if _compiling():
+        return torch.ops.lgnn.dense_linear(x, W, b, bool(bf16))
     return _DenseLinear.apply(x, W, b, bf16)
 
 
@@ -411,6 +430,8 @@ class _Spmm(torch.autograd.Function):
 
 
 def spmm(x, graph: Graph, kind: str = "gin", self_scale: float = 0.0):
+    if _compiling():
+        return torch.ops.lgnn.spmm(x, _lgnn().gparts(graph, kind), float(self_scale), False)
     return _Spmm.apply(x, graph, kind, self_scale)
 
 
@@ -428,6 +449,8 @@ class _Pool(torch.autograd.Function):
 
 
 def segment_pool(x, graph: Graph, mean: bool = True):
+    if _compiling():
+        return torch.ops.lgnn.segment_pool(x, _lgnn().gparts(graph, None), bool(mean))
     return _Pool.apply(x, graph, mean)
 
 
@@ -449,6 +472,9 @@ class _PoolHead(torch.autograd.Function):
 
 
 def pool_head(x, Wout, bout, graph: Graph, mean: bool = True):
+    if _compiling():
+        return torch.ops.lgnn.pool_head(x, Wout, bout, _lgnn().gparts(graph, None),
+                                        bool(mean))[0]
     return _PoolHead.apply(x, Wout, bout, graph, mean)
 
 
@@ -545,6 +571,9 @@ class _GCNStack(torch.autograd.Function):
 
 
 def gcn_stack(x, graph: Graph, params: list[torch.Tensor], L: int, mean: bool = True):
+    if _compiling():
+        return torch.ops.lgnn.gcn_stack(x, _lgnn().gparts(graph, "gcn"), bool(mean), int(L),
+                                        list(params))[0]
     return _GCNStack.apply(x, graph, mean, L, *params)
 
 
@@ -672,6 +701,7 @@ class _GINConv(torch.autograd.Function):
                               shift, mask)
         ctx.graph, ctx.self_scale, ctx.gathered = graph, self_scale, S is None
         ctx.training, ctx.count, ctx.group, ctx.act = training, count, group, act
+        ctx.bn_sums = sums  # the batch statistics' sums (library.py: running-stat update op)
         ctx.affine = gamma is not None
         return H
 
@@ -710,6 +740,21 @@ def gin_conv(x, W1, b1, bn, W2, b2, graph: Graph, eps: float = 0.0, mask=None,
     training = bn.training or not bn.track_running_stats
     gamma = bn.weight if bn.affine else None
     beta = bn.bias if bn.affine else None
+    if _compiling():
+        if group is not None:
+            raise NotImplementedError("SyncBatchNorm (GIN.set_sync_bn) is not supported under "
+                                      "torch.compile")
+        track = bn.track_running_stats and bn.running_mean is not None
+        out = torch.ops.lgnn.gin_conv(x, W1, b1, gamma, beta, W2, b2,
+                                      bn.running_mean if track else None,
+                                      bn.running_var if track else None,
+                                      _lgnn().gparts(graph, "gin"), bool(training), float(eps),
+                                      float(bn.eps), mask, int(act))
+        if training and track:
+            torch.ops.lgnn.bn_running_update(
+                bn.running_mean, bn.running_var, bn.num_batches_tracked, out[8], x.size(0),
+                float(bn.eps), -1.0 if bn.momentum is None else float(bn.momentum))
+        return out[0]
     return _GINConv.apply(x, W1, b1, gamma, beta, W2, b2, graph, bn, training, eps, mask, act,
                           group, sync_count)
 
@@ -797,6 +842,9 @@ def gat_conv(x, W, att_src, att_dst, bias, graph: Graph, heads: int, slope: floa
              mask=None, act: int = _lib.LGNN_ACT_NONE, bf16: bool = False):
     """bf16: the lin GEMM (and its backward) on bf16-rounded operands, fp32 accumulate/out;
     attention, softmax and aggregation stay fp32."""
+    if _compiling():
+        return torch.ops.lgnn.gat_conv(x, W, att_src, att_dst, bias, _lgnn().gparts(graph, "gat"),
+                                       int(heads), float(slope), mask, int(act), bool(bf16))[0]
     return _GATConv.apply(x, W, att_src, att_dst, bias, graph, heads, slope, mask, act, bf16)
 
 
@@ -885,6 +933,8 @@ def sort_pool(x, graph: Graph, k: int):
     """x [ΣN, D] -> [B, k * D]; graph carries batch / Batch.ptr."""
     if graph.batch is None:
         raise ValueError("sort_pool needs the graph's batch vector")
+    if _compiling():
+        return torch.ops.lgnn.sort_pool(x, _lgnn().gparts(graph, None), int(k))[0]
     return _SortPool.apply(x, graph, k)
 
 
