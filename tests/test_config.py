@@ -44,8 +44,10 @@ def test_reference_config_builds_gat():
     from lesion_gnn_amd import optim
     assert isinstance(opt, optim.Adam) and isinstance(opt, torch.optim.Optimizer)
     want = ref.GAT(1025, [128] * 4, 1, heads=2, dropout=0.35).state_dict()
+    # compile=True: the model is torch.compile'd as in the reference (gat.py:84), so its keys
+    # carry the `_orig_mod.` prefix exactly as the reference's compiled module's do
     assert {k: v.shape for k, v in m.model.state_dict().items()} == \
-        {k: v.shape for k, v in want.items()}
+        {"_orig_mod." + k: v.shape for k, v in want.items()}
 
 
 def test_gin_and_gcn_configs():
@@ -58,8 +60,10 @@ def test_gin_and_gcn_configs():
     m = get_model(gin)
     assert isinstance(m, GINModule) and m.model.pool == "add"
     want = ref.GIN(128, [128, 128, 128], 5, 0.0).state_dict()
+    # compile=True: the model is torch.compile'd as in the reference (gat.py:84), so its keys
+    # carry the `_orig_mod.` prefix exactly as the reference's compiled module's do
     assert {k: v.shape for k, v in m.model.state_dict().items()} == \
-        {k: v.shape for k, v in want.items()}
+        {"_orig_mod." + k: v.shape for k, v in want.items()}
     gcn = GCNConfig(optimizer=OptimizerConfig(), hidden_channels=[64, 64], dropout=0.1,
                     compile=False)
     gcn.num_classes.value, gcn.input_features.value = 3, 32
@@ -160,8 +164,10 @@ def test_reference_config_file_loads_unchanged():
     m = _fill_and_build(cfg)
     assert isinstance(m, GATModule) and m.is_regression
     want = ref.GAT(1025, [128] * 4, 1, heads=2, dropout=0.35).state_dict()
+    # compile=True: the model is torch.compile'd as in the reference (gat.py:84), so its keys
+    # carry the `_orig_mod.` prefix exactly as the reference's compiled module's do
     assert {k: v.shape for k, v in m.model.state_dict().items()} == \
-        {k: v.shape for k, v in want.items()}
+        {"_orig_mod." + k: v.shape for k, v in want.items()}
 
 
 def test_parse_args_requires_config(tmp_path):
