@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 8
+#define LGNN_ABI_VERSION 9
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -379,6 +379,24 @@ int lgnn_adam_step(int n, float* const* params, const float* const* grads, float
                    unsigned int* ticket, float lr, float beta1, float beta2, float eps,
                    float weight_decay, int decoupled, int maximize, int advance,
                    void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Fused GCN stack backward on split-3 bf16 MFMA (fp32 accuracy), every layer of a tile in one
+ * pass, one launch. Replaces the same autograd chain as lgnn_gcn_stack_bwd (reference path:
+ * global_mean/add_pool backward, per conv G = Â^T dZ, dW += G^T H, dH = G W, ELU', and in_proj
+ * dW) for tiles with tile_open[t] == 0, L = 1 or 2 convs, every width <= 128 and % 4 == 0.
+ *   planes_t: the transposed weight planes of lgnn_weight_planes (all L + 1 layers);
+ *   H[0..L]: layer outputs (H[0] = in_proj output); X: model input; widths[0..L+1];
+ *   dWp / dbp: per-layer partial slabs with num_partials = lgnn_gcn_stack_bwd_partials(M)
+ *   slots, every slot written (zeros for a workgroup without tiles), so open tiles can be
+ *   accumulated afterwards by lgnn_node_linear_bwd_tiles(..., accumulate = 1).
+ * ------------------------------------------------------------------------------------------- */
+int lgnn_gcn_stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* gptr,
+                           int pool_mean, int64_t num_graphs, const int32_t* rowptr,
+                           const int32_t* col, const float* w, const float* X, int64_t M, int L,
+                           const uint16_t* planes_t, const float* const* H, const int* widths,
+                           float* const* dWp, float* const* dbp, int num_partials,
+                           const int32_t* tile_open, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Sort pooling (DGCNN). Replaces: PyG 2.5.1 SortAggregation(k) as DRGNet applies it to the

@@ -78,6 +78,8 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_node_linear_fwd_tiles": (I32, [P, I64, I32, P, P, P, F32, P, P, I32, I32, P, P, P, I32,
                                          P]),
     "lgnn_bn_bwd_apply": (I32, [P, P, P, I64, I32, P, P, P, P, P, F64, I32, P, P, P, P]),
+    "lgnn_gcn_stack_bwd_s3f": (I32, [P, P, P, I32, I64, P, P, P, P, I64, I32, P, P, P, P, P,
+                                     I32, P, P]),
     "lgnn_sort_pool_workspace_bytes": (SZ, []),
     "lgnn_sort_pool_fwd": (I32, [P, I64, I32, P, I64, I32, P, P, P, P, SZ, P]),
     "lgnn_sort_pool_bwd": (I32, [P, P, P, P, P, I64, I32, I32, P, P]),
@@ -85,7 +87,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _lib = None
 

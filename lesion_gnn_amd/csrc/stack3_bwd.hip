@@ -78,6 +78,25 @@ __device__ __forceinline__ void load_p(f32x16 (&v)[2], Buf b, int64_t r0, int ld
     }
 }
 
+// load_p with the descriptor based at the tile's first row: one lane-base VGPR, and each of the
+// 32 loads adds a wave-uniform row offset (one VALU add instead of 64-bit address arithmetic).
+// Rows past M fall outside the descriptor's range and read 0.
+__device__ __forceinline__ void load_pt(f32x16 (&v)[2], const float* base, int64_t M, int64_t r0,
+                                        int ld, int colv, int ncols, int h) {
+  const int64_t rem = M - r0;
+  const Buf b = mkbuf(base + r0 * ld, rem > 0 ? rem * ld * 4 : 0);
+  const int vb = colv < ncols ? (4 * h * ld + colv) * 4 : 0x7fff0000;
+  const int rs = __builtin_amdgcn_readfirstlane(ld * 4);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int mc = 32 * a + (r & 3) + 8 * (r >> 2);
+      v[a][r] = __builtin_bit_cast(
+          float, __builtin_amdgcn_raw_buffer_load_b32(b, vb + mc * rs, 0, 0));
+    }
+}
+
 // P-layout pair -> node-step operand fragments (s = 0, 1 from v[0], 2, 3 from v[1])
 __device__ __forceinline__ void split_p(const f32x16 (&v)[2], u32x4 (&o)[4][3]) {
 #pragma unroll
@@ -443,3 +462,465 @@ extern "C" int lgnn_gcn_stack_bwd_s3(const float* dP, const int64_t* batch, cons
   }
   return LGNN_OK;
 }
+
+namespace lgnn_s3 {
+
+// ==============================================================================================
+// Fused split-3 backward: every layer of a tile in one pass (tile-major), one launch.
+//
+// Same arithmetic and layouts as k_s3_bwd above, with the layer loop inside the tile loop:
+//   * the tile's Â^T planes are built once and serve every conv layer;
+//   * dZ stays in registers (P layout) from one layer to the next: dH = G W_l comes out of its
+//     MFMAs in exactly the layout the next layer's dZ is consumed in, so no HBM round trip;
+//   * the dW accumulators of ALL layers stay in registers over the workgroup's tiles (64 per
+//     layer per lane; the MFMA accumulators live in AGPRs at one wave per SIMD) and are written
+//     once as partial slot blockIdx.x — one workgroup per CU, the fp32 kernel's 256 slots;
+//   * G^T has its own LDS image, so the H image of the dW product and the G^T image of the dH
+//     product coexist (two barriers per conv layer);
+//   * the next tile's CSR block is prefetched during the current tile (idx head/body), and the
+//     next layer's H_{l-1} rows are issued before the current layer's G products.
+// Per tile HBM traffic: H_L, H_{L-1}, ..., H_0, X read once (the algorithmic bytes).
+// ==============================================================================================
+
+// scheduling fence between MFMA groups (-DLGNN_S3F_NOSB: none, the compiler interleaves freely)
+#ifdef LGNN_S3F_NOSB
+#define S3F_SB() \
+  do {           \
+  } while (0)
+#else
+#define S3F_SB() __builtin_amdgcn_sched_barrier(0)
+#endif
+
+struct FBwdArgs {
+  const float* dP;                // [B][N_L] pooled-output gradient
+  const int64_t* batch;
+  const int32_t* gptr;
+  int pool_mean;
+  int64_t num_graphs;
+  const float* X;                 // model input (in_proj dW operand)
+  const float* H[LGNN_MAX_STACK];  // H[l] = output of layer l
+  const uint16_t* WpT;            // transposed weight planes, [l][3][PLANE] fragment order
+  float* dWp[LGNN_MAX_STACK];     // [P][N_l][K_l]
+  float* dbp[LGNN_MAX_STACK];     // [P][N_l]
+  int width[LGNN_MAX_STACK + 1];
+};
+
+struct FBwdSmem {
+  unsigned char Img[3][TM * AROW];  // 48 KiB: H_{l-1} (or X) feature-major [k][perm16 m]
+  unsigned char Gt[3][TM * AROW];   // 48 KiB: G node-major [m][perm16 n]
+  unsigned char Adj[3][ADJ_PLANE];  // 27 KiB: Â^T planes; first 16 KiB fp32 while summed
+  float pscale[TM];
+  int pg[TM];
+  int rp[TM + 1];
+  int flag;
+};
+
+template <int NL>
+__global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ rowptr,
+                                                   const int32_t* __restrict__ col,
+                                                   const float* __restrict__ w, int64_t M,
+                                                   FBwdArgs a, const int32_t* __restrict__ tmask) {
+  constexpr int L = NL - 1;
+  __shared__ __attribute__((aligned(16))) FBwdSmem sm;
+  const int64_t ntiles = (M + TM - 1) / TM;
+  float* const scr = reinterpret_cast<float*>(sm.Adj[0]);  // fp32 Â^T [source][target]
+  const int NLast = a.width[L + 1];
+  const Buf bP = mkbuf(a.dP, a.num_graphs * NLast * 4);
+
+  f32x16 dw[NL][4];
+#pragma unroll
+  for (int l = 0; l < NL; ++l)
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) dw[l][kb] = f32x16{};
+  float dbacc[NL];
+#pragma unroll
+  for (int l = 0; l < NL; ++l) dbacc[l] = 0.f;
+
+  IdxRegs R;
+  [[maybe_unused]] int stamp = 0;
+  int64_t t = seek_tile(blockIdx.x, ntiles, tmask, 0);
+  if (t < ntiles) {
+    idx_load_head(R, rowptr, M, t * TM);
+    idx_load_body(R, col, w);
+  }
+  for (; t < ntiles;) {
+    STAMP(stamp++);
+    const int64_t r0 = t * TM;
+    const int64_t tn = seek_tile(t + gridDim.x, ntiles, tmask, 0);
+    const bool has_next = tn < ntiles;
+    {
+      const int tq = fresh_tid();
+#pragma unroll
+      for (int i = 0; i < TM * TM / 4 / NT; ++i) st4(scr + 4 * (tq + i * NT), zero4());
+      if (tq <= TM) sm.rp[tq] = R.rp;
+      if (tq == 0) sm.flag = 0;
+      if (tq < TM) {
+        const int64_t row = r0 + tq;
+        const int64_t g = row < M ? a.batch[row] : 0;
+        const int cnt = a.gptr[g + 1] - a.gptr[g];
+        sm.pg[tq] = (int)g;
+        sm.pscale[tq] = row >= M ? 0.f : (a.pool_mean && cnt > 1 ? 1.f / (float)cnt : 1.f);
+      }
+    }
+    lds_barrier();
+    adj_scatter<true>(scr, sm.rp, R, r0);
+    if (has_next) idx_load_head(R, rowptr, M, tn * TM);
+    // dZ_L = pool broadcast of dP (/ |graph|) * ELU'(H_L), P layout (feature n on the lane)
+    f32x16 dz[2];
+    {
+      const int tq = fresh_tid();
+      const int h = (tq >> 5) & 1, n = 32 * (tq >> 6) + (tq & 31);
+      f32x16 hv[2];
+      load_pt(hv, a.H[L], M, r0, NLast, n, NLast, h);
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const int off = n < NLast ? (sm.pg[m] * NLast + n) * 4 : INT32_MAX - 3;
+          const float gv =
+              __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(bP, off, 0, 0));
+          dz[q][r] = gv * sm.pscale[m] * elu_grad_from_out(hv[q][r]);
+        }
+    }
+    lds_barrier();  // Â^T summed
+    {
+      f32x4 av[4];
+      {
+        const int tq = fresh_tid();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) av[i] = ld4(scr + (tq >> 2) * TM + 16 * (tq & 3) + 4 * i);
+      }
+      lds_barrier();  // every scratch read done
+      int inexact = 0;
+      {
+        const int tq = fresh_tid();
+        const int am = tq >> 2, aq = tq & 3;
+        float f[16];
+#pragma unroll
+        for (int y = 0; y < 16; ++y) {
+          const int src = perm16(y);
+          f[y] = av[src >> 2][src & 3];
+        }
+        uint32_t q[3][8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const Split2 s2 = split2(f[2 * i], f[2 * i + 1]);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) q[p][i] = s2.p[p];
+          inexact |= (s2.p[1] | s2.p[2]) != 0;
+        }
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          unsigned char* dst = sm.Adj[p] + am * ADJ_LD * 2 + 32 * aq;
+          *reinterpret_cast<u32x4*>(dst) = u32x4{q[p][0], q[p][1], q[p][2], q[p][3]};
+          *reinterpret_cast<u32x4*>(dst + 16) = u32x4{q[p][4], q[p][5], q[p][6], q[p][7]};
+        }
+      }
+      (void)inexact;  // the fused kernel always takes the six products (no per-tile branch)
+      lds_barrier();
+    }
+    if (has_next) idx_load_body(R, col, w);
+    STAMP(stamp++);
+
+    f32x16 xp[2];  // X rows of the in_proj phase (issued during the last conv's dH)
+#pragma unroll
+    for (int l = L; l >= 1; --l) {
+      const int K = a.width[l];
+      const bool elu_prev = l >= 2;
+      // H_{l-1} rows (P layout, feature k on the lane): issued first, consumed by the image
+      // write after the G products and by ELU' at the end of the layer
+      f32x16 hp[2];
+      {
+        const int tq = fresh_tid();
+        const int h = (tq >> 5) & 1, k = 32 * (tq >> 6) + (tq & 31);
+        load_pt(hp, a.H[l - 1], (ABL & 16) ? 0 : M, r0, K, k, K, h);
+      }
+      // db_l: this lane's 32 nodes, then the partner half's
+      {
+        float sacc = 0.f;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sacc += dz[q][r];
+        sacc += __shfl_xor(sacc, 32, 64);
+        dbacc[l] += sacc;
+      }
+      u32x4 dzp[4][3];
+      split_p(dz, dzp);
+      // G^T = dZ^T Â (node on the lane) -> node-major image right away (keeps one pair of
+      // accumulators live at a time); the previous layer's dH readers of the image passed the
+      // barrier that closed that layer
+      {
+        f32x16 gt[2] = {f32x16{}, f32x16{}};
+        const int tq = fresh_tid();
+        const int h = (tq >> 5) & 1, li = tq & 31, wv = tq >> 6;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int off = (32 * q + li) * ADJ_LD * 2 + 16 * (2 * s + h);
+            u32x4 at[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) at[p] = lds16(sm.Adj[p] + off);
+            if constexpr (!(ABL & 1)) gt[q] = mfma_s3(dzp[s], at, gt[q]);
+          }
+          S3F_SB();
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq) {
+            u32x2 o[3];
+            split4(f32x4{gt[q][4 * gq], gt[q][4 * gq + 1], gt[q][4 * gq + 2], gt[q][4 * gq + 3]},
+                   o);
+            const int off = ap_off(32 * q + li, 32 * wv + 8 * gq + 4 * h);
+#pragma unroll
+            for (int p = 0; p < 3; ++p) sts8(sm.Gt[p] + off, o[p]);
+          }
+      }
+      // G = Â^T dZ (P layout)
+      f32x16 g[2] = {f32x16{}, f32x16{}};
+      {
+        const int tq = fresh_tid();
+        const int h = (tq >> 5) & 1, li = tq & 31;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int off = (32 * q + li) * ADJ_LD * 2 + 16 * (2 * s + h);
+            u32x4 at[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) at[p] = lds16(sm.Adj[p] + off);
+            if constexpr (!(ABL & 1)) g[q] = mfma_s3(at, dzp[s], g[q]);
+          }
+          S3F_SB();
+        }
+      }
+      STAMP(stamp++);
+      // H_{l-1} -> feature-major image (the previous layer's dW readers passed its barrier)
+      {
+        const int tq = fresh_tid();
+        const int h = (tq >> 5) & 1, li = tq & 31, k = 32 * (tq >> 6) + li;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq) {
+            u32x2 o[3];
+            split4(f32x4{hp[q][4 * gq], hp[q][4 * gq + 1], hp[q][4 * gq + 2], hp[q][4 * gq + 3]},
+                   o);
+            const int off = hf_off(k, 32 * q + 8 * gq + 4 * h);
+#pragma unroll
+            for (int p = 0; p < 3; ++p) sts8(sm.Img[p] + off, o[p]);
+          }
+      }
+      // W_l^T planes for dH (L2-resident, 1 KiB per wave-load): the first four k-steps fly
+      // during the dW products, the last four during the first half of dH
+      const uint16_t* wbase;
+      {
+        const int tq = fresh_tid();
+        const int lane = tq & 63, wv = tq >> 6;
+        wbase = a.WpT + (size_t)l * 3 * PLANE + wv * 8 * 512 + lane * 8;
+      }
+      auto load_w = [&](u32x4 (&wf)[3][4], int half) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4)
+            wf[p][s4] = (ABL & 16) ? u32x4{}
+                                   : *reinterpret_cast<const u32x4*>(wbase + p * PLANE +
+                                                                     512 * (4 * half + s4));
+      };
+      u32x4 wf0[3][4], wf1[3][4];
+      load_w(wf0, 0);
+      lds_barrier();  // both images complete
+      STAMP(stamp++);
+      // dW_l += G^T H: A = G (P layout, node steps), B = H image rows k = 32 kb + li
+      {
+        u32x4 gp[4][3];
+        split_p(g, gp);
+        const int tq = fresh_tid();
+        const int h = (tq >> 5) & 1, li = tq & 31;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            u32x4 hb[3];
+            const int off = hf_chunk(32 * kb + li, 2 * s + h);
+#pragma unroll
+            for (int p = 0; p < 3; ++p) hb[p] = lds16(sm.Img[p] + off);
+            if constexpr (!(ABL & 1)) dw[l][kb] = mfma_s3(gp[s], hb, dw[l][kb]);
+          }
+          S3F_SB();
+        }
+      }
+      STAMP(stamp++);
+      // dH = G W_l (P layout: feature k on the lane): A = G^T image rows m, B = W_l^T planes
+      f32x16 dh[2] = {f32x16{}, f32x16{}};
+      {
+        const int tq = fresh_tid();
+        const int h = (tq >> 5) & 1, li = tq & 31;
+        auto dh_half = [&](const u32x4 (&wf)[3][4], int half) {
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              u32x4 f[3];
+              const int off = ap_chunk(32 * q + li, 2 * (4 * half + s4) + h);
+#pragma unroll
+              for (int p = 0; p < 3; ++p) f[p] = lds16(sm.Gt[p] + off);
+              u32x4 bw[3];
+#pragma unroll
+              for (int p = 0; p < 3; ++p) bw[p] = wf[p][s4];
+              if constexpr (!(ABL & 1)) dh[q] = mfma_s3(f, bw, dh[q]);
+            }
+            S3F_SB();
+          }
+        };
+        load_w(wf1, 1);
+        dh_half(wf0, 0);
+        dh_half(wf1, 1);
+      }
+      // dZ_{l-1} = dH * ELU'(H_{l-1}) (no ELU below the first conv: in_proj has none); rows past
+      // M and features past K are zero
+      {
+        const int tq = fresh_tid();
+        const int h = (tq >> 5) & 1, k = 32 * (tq >> 6) + (tq & 31);
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const float v = elu_prev ? dh[q][r] * elu_grad_from_out(hp[q][r]) : dh[q][r];
+            dz[q][r] = (k < K && r0 + m < M) ? v : 0.f;
+          }
+      }
+      lds_barrier();  // every read of both images done
+      STAMP(stamp++);
+    }
+    // in_proj: db_0, dW_0 += dZ_0^T X
+    {
+      const int K = a.width[0];
+      {
+        const int tq = fresh_tid();
+        const int h = (tq >> 5) & 1, li = tq & 31, k = 32 * (tq >> 6) + li;
+        load_pt(xp, a.X, (ABL & 16) ? 0 : M, r0, K, k, K, h);
+        float sacc = 0.f;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sacc += dz[q][r];
+        sacc += __shfl_xor(sacc, 32, 64);
+        dbacc[0] += sacc;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq) {
+            u32x2 o[3];
+            split4(f32x4{xp[q][4 * gq], xp[q][4 * gq + 1], xp[q][4 * gq + 2], xp[q][4 * gq + 3]},
+                   o);
+            const int off = hf_off(k, 32 * q + 8 * gq + 4 * h);
+#pragma unroll
+            for (int p = 0; p < 3; ++p) sts8(sm.Img[p] + off, o[p]);
+          }
+        (void)K;
+      }
+      lds_barrier();
+      {
+        u32x4 gp[4][3];
+        split_p(dz, gp);
+        const int tq = fresh_tid();
+        const int h = (tq >> 5) & 1, li = tq & 31;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            u32x4 hb[3];
+            const int off = hf_chunk(32 * kb + li, 2 * s + h);
+#pragma unroll
+            for (int p = 0; p < 3; ++p) hb[p] = lds16(sm.Img[p] + off);
+            if constexpr (!(ABL & 1)) dw[0][kb] = mfma_s3(gp[s], hb, dw[0][kb]);
+          }
+          S3F_SB();
+        }
+      }
+      lds_barrier();  // X image read; the next tile may overwrite LDS
+      STAMP(stamp++);
+    }
+    t = tn;
+  }
+  // partial slot blockIdx.x of every layer: dW rows n = 32 wave + (r & 3) + 8 (r >> 2) + 4h,
+  // columns k = 32 kb + li; db from the h = 0 lanes
+  {
+    const int tq = threadIdx.x;
+    const int h = (tq >> 5) & 1, li = tq & 31, wv = tq >> 6;
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int N = a.width[l + 1], K = a.width[l];
+      float* slab = a.dWp[l] + (int64_t)blockIdx.x * N * K;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        const int k = 32 * kb + li;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int n = 32 * wv + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (n < N && k < K) slab[(int64_t)n * K + k] = dw[l][kb][r];
+        }
+      }
+      const int n = 32 * wv + li;
+      if (h == 0 && n < N) a.dbp[l][(int64_t)blockIdx.x * N + n] = dbacc[l];
+    }
+  }
+}
+
+}  // namespace lgnn_s3
+
+extern "C" int lgnn_gcn_stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* gptr,
+                                      int pool_mean, int64_t num_graphs, const int32_t* rowptr,
+                                      const int32_t* col, const float* w, const float* X,
+                                      int64_t M, int L, const uint16_t* planes_t,
+                                      const float* const* H, const int* widths,
+                                      float* const* dWp, float* const* dbp, int num_partials,
+                                      const int32_t* tile_open, void* stream) {
+  if (M < 0 || L < 1 || L > 2 || !dP || !batch || !gptr || !rowptr || !col || !X || !planes_t ||
+      !H || !widths || !dWp || !dbp || !tile_open || num_graphs < 0)
+    return LGNN_EINVAL;
+  if (num_partials != lgnn_gcn_stack_bwd_partials(M)) return LGNN_EINVAL;
+  lgnn_s3::FBwdArgs a = {};
+  a.dP = dP;
+  a.batch = batch;
+  a.gptr = gptr;
+  a.pool_mean = pool_mean;
+  a.num_graphs = num_graphs;
+  a.X = X;
+  a.WpT = planes_t;
+  for (int l = 0; l <= L + 1; ++l) a.width[l] = widths[l];
+  for (int l = 0; l <= L; ++l) {
+    if (!lgnn_tile_fits(M, widths[l], widths[l + 1]) || !H[l] || !dWp[l] || !dbp[l])
+      return LGNN_EINVAL;
+    a.H[l] = H[l];
+    a.dWp[l] = dWp[l];
+    a.dbp[l] = dbp[l];
+  }
+  hipStream_t s = as_stream(stream);
+  if (M == 0) {
+    for (int l = 0; l <= L; ++l)
+      if (hipMemsetAsync(dWp[l], 0, (size_t)widths[l] * widths[l + 1] * 4, s) != hipSuccess ||
+          hipMemsetAsync(dbp[l], 0, (size_t)widths[l + 1] * 4, s) != hipSuccess)
+        return (int)hipGetLastError();
+    return LGNN_OK;
+  }
+  const dim3 grid((unsigned)num_partials), blk(lgnn_tile::NT);
+  if (L == 1)
+    hipLaunchKernelGGL(lgnn_s3::k_s3_fbwd<2>, grid, blk, 0, s, rowptr, col, w, M, a, tile_open);
+  else
+    hipLaunchKernelGGL(lgnn_s3::k_s3_fbwd<3>, grid, blk, 0, s, rowptr, col, w, M, a, tile_open);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? LGNN_OK : (int)e;
+}
+
+#ifdef LGNN_STAMPS
+extern "C" int lgnn_debug_stamps_s3b(unsigned long long* host_out) {
+  return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(lgnn_stamp_buf), sizeof(lgnn_stamp_buf));
+}
+#endif

@@ -75,11 +75,13 @@ FUSED_BWD = os.environ.get("LGNN_FUSED_BWD", "1") != "0"
 # GEMM arithmetic of the fused GCN stack: "s3" = bf16 MFMA on three-plane split operands (fp32
 # accuracy, stack3.hip), "f32" = fp32 MFMA (tile.hip). LGNN_MFMA=f32 selects the latter.
 MFMA_MODE = os.environ.get("LGNN_MFMA", "s3")
-# Backward of the fused stack: the fp32 fused kernel (tile.hip k_stack_bwd, one launch) by default;
-# LGNN_BWD_S3=1 selects the split-3 layer-major kernels (stack3_bwd.hip: 3 launches, 125 us of
-# kernels vs 150 us, but 512 partial slots double the slab reduction and the step measured 1 %
-# slower on MI355X — DESIGN.md §4.3)
-BWD_S3 = os.environ.get("LGNN_BWD_S3", "0") == "1"
+# Backward of the fused stack (LGNN_BWD): "f32" = the fp32 fused kernel (tile.hip k_stack_bwd, one
+# launch); "s3" = the split-3 layer-major kernels (stack3_bwd.hip k_s3_bwd: one launch per layer,
+# dZ through HBM, 512 partial slots); "s3f" = the fused split-3 kernel (stack3_bwd.hip
+# k_s3_fbwd: every layer of a tile in one pass, one launch, 256 slots). s3 / s3f need the
+# split-3 forward (their transposed weight planes come out of its weight-plane launch).
+BWD_MODE = os.environ.get("LGNN_BWD", "s3" if os.environ.get("LGNN_BWD_S3", "0") == "1" else "f32")
+BWD_S3 = BWD_MODE in ("s3", "s3f")
 
 
 def weight_planes(Ws: list, d_in: int, transposed: bool = False):
@@ -152,7 +154,9 @@ def stack_bwd(dp: torch.Tensor, x: torch.Tensor, graph: Graph, mean: bool, Ws: l
     dev = x.device
     lib = _lib.load()
     s3 = planes_t is not None
-    P = lib.lgnn_gcn_stack_bwd_s3_partials(M) if s3 else lib.lgnn_gcn_stack_bwd_partials(M)
+    s3f = s3 and BWD_MODE == "s3f" and L <= 2
+    P = lib.lgnn_gcn_stack_bwd_s3_partials(M) if s3 and not s3f else \
+        lib.lgnn_gcn_stack_bwd_partials(M)
     _lib.check(0 if P > 0 else P, "lgnn_gcn_stack_bwd_partials")
     widths = [x.size(1)] + [W.size(0) for W in Ws]
     per = [widths[l + 1] * widths[l] + widths[l + 1] for l in range(L + 1)]
@@ -165,7 +169,14 @@ def stack_bwd(dp: torch.Tensor, x: torch.Tensor, graph: Graph, mean: bool, Ws: l
         off += P * (nk + n)
     arr = ctypes.c_void_p * (L + 1)
     Sx = [x] + list(ss)
-    if s3:  # one split-3 launch per layer (stack3_bwd.hip); dZ between them in dz_ws
+    if s3f:  # one fused split-3 launch, every layer of a tile in one pass (stack3_bwd.hip)
+        _lib.call("lgnn_gcn_stack_bwd_s3f", _lib.ptr(dp), _lib.ptr(graph.batch),
+                  _lib.ptr(graph.gptr), int(mean), dp.size(0), _lib.ptr(csr.rowptr),
+                  _lib.ptr(csr.col), _lib.ptr(csr.w), _lib.ptr(x), M, L, _lib.ptr(planes_t),
+                  arr(*[h.data_ptr() for h in hs]), (ctypes.c_int * (L + 2))(*widths),
+                  arr(*[t.data_ptr() for t in dWp]), arr(*[t.data_ptr() for t in dbp]), P,
+                  _lib.ptr(open_), _s(dev))
+    elif s3:  # one split-3 launch per layer (stack3_bwd.hip); dZ between them in dz_ws
         dz_ws = torch.empty(2 * M * 128, dtype=torch.float32, device=dev)
         _lib.call("lgnn_gcn_stack_bwd_s3", _lib.ptr(dp), _lib.ptr(graph.batch),
                   _lib.ptr(graph.gptr), int(mean), dp.size(0), _lib.ptr(csr.rowptr),

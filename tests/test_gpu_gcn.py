@@ -290,15 +290,17 @@ def test_tile_open_flags(cuda):
     assert Graph(b2.edge_index.to(cuda), b2.num_nodes).tile_open("gcn").cpu().tolist() == [0] * 5
 
 
-@pytest.mark.parametrize("bwd_s3", [False, True])
+@pytest.mark.parametrize("bwd", ["f32", "s3", "s3f"])
 @pytest.mark.parametrize("case", ["c2_L2", "irregular_L2", "irregular_L1_add", "dense_tiles",
                                   "c2_L3"])
-def test_gcn_fused_backward(cuda, case, bwd_s3, monkeypatch):
+def test_gcn_fused_backward(cuda, case, bwd, monkeypatch):
     """lgnn_gcn_stack_bwd (closed tiles, fused) + masked accumulating layer-wise backward (open
     tiles) vs the layer-wise backward and the oracle. dense_tiles: 64-node graphs with k = 20
     (1344 CSR entries per tile > the 1024 a tile stages) are flagged open by the graph build.
     c2_L3: three convs (fp32: layer-wise backward on recomputed aggregates; split-3: fused).
-    bwd_s3: the split-3 layer-major backward (lgnn_gcn_stack_bwd_s3) instead of the fp32 one."""
+    bwd: the fp32 fused kernel (lgnn_gcn_stack_bwd), the split-3 layer-major kernels
+    (lgnn_gcn_stack_bwd_s3) or the fused split-3 kernel (lgnn_gcn_stack_bwd_s3f; L <= 2, so c2_L3
+    takes the layer-major one)."""
     pool = "add" if case.endswith("add") else "mean"
     hidden = [128, 128] if "L1" in case else [128] * 4 if "L3" in case else [128, 128, 128]
     if case.startswith("c2"):
@@ -309,7 +311,8 @@ def test_gcn_fused_backward(cuda, case, bwd_s3, monkeypatch):
         b = synth.make_batch(9, k=6, d_in=128, seed=33, sizes=[1, 5, 64, 200, 2, 33, 512, 17, 64])
     ours, oref = make_pair(hidden, pool=pool)
     ours = ours.to(cuda)
-    monkeypatch.setattr(ops, "BWD_S3", bwd_s3)  # split-3 layer-major backward (stack3_bwd.hip)
+    monkeypatch.setattr(ops, "BWD_MODE", bwd)
+    monkeypatch.setattr(ops, "BWD_S3", bwd != "f32")
     if case == "dense_tiles":
         g = Graph(b.edge_index.to(cuda), b.num_nodes)
         assert g.tile_open("gcn").cpu().tolist() == [1, 1, 1, 1, 1, 5]
