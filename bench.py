@@ -243,9 +243,28 @@ def time_dominant_kernels(model, b, dev):
                   csr.rowptr.data_ptr(), csr.col.data_ptr(), csr.w.data_ptr(), b.x.data_ptr(), M,
                   L, Wp, Hp, (ctypes.c_int * (L + 2))(*widths), dWp, dbp, P, open_.data_ptr(), s)
 
-    out.append({"kernel": f"lgnn_tile::k_stack_bwd<{L + 1}> (fused GCN backward, all layers)",
-                "ms": _time_launches(bwd, dev), "flops": lin + 2.0 * M * L * h * h + agg,
-                "trace_name": f"void lgnn_tile::k_stack_bwd<{L + 1}>"})
+    bwd_flops = lin + 2.0 * M * L * h * h + agg
+    if ops.MFMA_MODE == "s3" and ops.BWD_MODE == "s3f" and L <= 2:
+        # the step's backward: the fused split-3 kernel (stack3_bwd.hip), priced against the
+        # split-3 peak like the forward
+        _, planes_t = ops.weight_planes(Ws, d_in, transposed=True)
+
+        def bwd_s3f():
+            _lib.call("lgnn_gcn_stack_bwd_s3f", dP.data_ptr(), g.batch.data_ptr(),
+                      g.gptr.data_ptr(), 1, b.num_graphs, csr.rowptr.data_ptr(),
+                      csr.col.data_ptr(), csr.w.data_ptr(), b.x.data_ptr(), M, L,
+                      planes_t.data_ptr(), Hp, (ctypes.c_int * (L + 2))(*widths), dWp, dbp, P,
+                      open_.data_ptr(), s)
+
+        out.append({"kernel": f"lgnn_s3::k_s3_fbwd<{L + 1}> (fused GCN backward, all layers, "
+                              "split-3 bf16 MFMA)",
+                    "ms": _time_launches(bwd_s3f, dev), "flops": bwd_flops,
+                    "peak": MFMA_S3_PEAK_TF, "trace_name": f"void lgnn_s3::k_s3_fbwd<{L + 1}>"})
+    else:
+        out.append({"kernel": f"lgnn_tile::k_stack_bwd<{L + 1}> (fused GCN backward, all "
+                              "layers)",
+                    "ms": _time_launches(bwd, dev), "flops": bwd_flops,
+                    "trace_name": f"void lgnn_tile::k_stack_bwd<{L + 1}>"})
 
     if ops.MFMA_MODE == "s3":
         planes, _ = ops.weight_planes(Ws, d_in)

@@ -78,9 +78,10 @@ MFMA_MODE = os.environ.get("LGNN_MFMA", "s3")
 # Backward of the fused stack (LGNN_BWD): "f32" = the fp32 fused kernel (tile.hip k_stack_bwd, one
 # launch); "s3" = the split-3 layer-major kernels (stack3_bwd.hip k_s3_bwd: one launch per layer,
 # dZ through HBM, 512 partial slots); "s3f" = the fused split-3 kernel (stack3_bwd.hip
-# k_s3_fbwd: every layer of a tile in one pass, one launch, 256 slots). s3 / s3f need the
-# split-3 forward (their transposed weight planes come out of its weight-plane launch).
-BWD_MODE = os.environ.get("LGNN_BWD", "s3" if os.environ.get("LGNN_BWD_S3", "0") == "1" else "f32")
+# k_s3_fbwd: every layer of a tile in one pass, one launch, 256 slots; the default: 121 us vs
+# 154 us for f32 at C2 on MI355X). s3 / s3f need the split-3 forward (their transposed weight
+# planes come out of its weight-plane launch); otherwise the f32 kernel runs.
+BWD_MODE = os.environ.get("LGNN_BWD", "s3f")
 BWD_S3 = BWD_MODE in ("s3", "s3f")
 
 

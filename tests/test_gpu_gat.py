@@ -166,7 +166,9 @@ def test_reference_config_training_step(cuda):
     torch.manual_seed(0)
     module = get_model(cfg).to(cuda).train()
     oref = ref.GAT(64, [128] * 4, 1, heads=2, dropout=0.0)
-    oref.load_state_dict(module.model.state_dict())
+    # compile=True in the reference section: the model is torch.compile'd (gat.py:84), so the
+    # training step below runs the compiled lgnn:: graph
+    oref.load_state_dict(getattr(module.model, "_orig_mod", module.model).state_dict())
     b = synth.make_batch(32, k=6, d_in=64, seed=15, sizes="lognormal")
     loss = module.training_step(b.to(cuda))
     want = ref.criterion("MSE", oref(b.x, b.edge_index, b.batch, b.num_graphs), b.y, 5)

@@ -26,6 +26,9 @@ NAMES = ["prologue (adj, dZ_L)", "l2 G^T,G", "l2 images", "l2 dW", "l2 dH+dZ", "
          "l1 images", "l1 dW", "l1 dH+dZ", "l0 X + dW", "tile tail"]
 
 
+PREBUILT = ["v2"]  # variant libraries built by hand from an earlier source (not rebuilt here)
+
+
 def build():
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(ROOT, "lesion_gnn_amd", "csrc", "*.hip")))
@@ -55,7 +58,7 @@ def run():
     _, planes_t = ops.weight_planes(Ws, D, transposed=True)
     s = torch.cuda.current_stream().cuda_stream
     arr = ctypes.c_void_p * (L + 1)
-    for v in VARIANTS:
+    for v in [*VARIANTS, *[p for p in PREBUILT if os.path.exists(LIB % p)]]:
         lib = ctypes.CDLL(LIB % v)
         for name, (res, args) in _lib.SIGNATURES.items():
             f = getattr(lib, name)
