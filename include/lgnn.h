@@ -26,11 +26,16 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 9
+#define LGNN_ABI_VERSION 10
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
 #define LGNN_ENOSPC (-28)
+
+/* tile flag arrays (tile_open) hold ceil(N/64) + LGNN_TILE_OPEN_EXTRA int32: one flag per 64-node
+ * tile, the number of flagged tiles, then six words the fused GCN stack kernels use as grid-barrier
+ * counters for their open-tile phase (zeroed by whoever writes the flags, re-armed by the kernels) */
+#define LGNN_TILE_OPEN_EXTRA 7
 
 /* self-loop handling of the graph build (which PyG utility the conv applies to edge_index) */
 #define LGNN_LOOPS_KEEP 0      /* GINConv: edges used as given (KNN loop=True self pairs kept) */
@@ -66,7 +71,7 @@ const char* lgnn_status_string(int status);
  * PyG appends loops after the edge list). Invalid indices (<0 or >= N) are dropped and counted in
  * *err_count (device int, may be NULL). tmap (nullable, needs the transpose) [cap]: for each
  * transpose entry, the position of the same edge in the target CSR (GAT backward reads per-edge
- * attention saved in target order). tile_open (nullable) [ceil(N/64) + 1]: as lgnn_tile_open,
+ * attention saved in target order). tile_open (nullable) [ceil(N/64) + LGNN_TILE_OPEN_EXTRA]: as lgnn_tile_open,
  * in the same launches. gptr (nullable) [num_graphs + 1]: as lgnn_batch_ptr from batch [N],
  * in the same launches. *err_count is written (not accumulated). Workspace size:
  * lgnn_graph_workspace_bytes. N + E < 2^30. Five launches, no host synchronisation.
@@ -397,6 +402,33 @@ int lgnn_gcn_stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t*
                            const uint16_t* planes_t, const float* const* H, const int* widths,
                            float* const* dWp, float* const* dbp, int num_partials,
                            const int32_t* tile_open, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * The fused GCN stack with its open-tile phase in the same launch (no separate layer-by-layer
+ * launches). Tiles flagged open (an edge leaves them, or > 1024 CSR entries) share no edge with
+ * closed tiles, so after the closed tiles the kernel runs them layer by layer in fp32 (the bodies
+ * of lgnn_node_linear_fwd_tiles / _bwd_tiles) with a grid barrier between layers; with no open
+ * tile (the count word of tile_open is 0) that phase is skipped. tile_open: the graph build's
+ * [ceil(M/64) + LGNN_TILE_OPEN_EXTRA] array (its barrier words are used and re-armed).
+ * lgnn_gcn_stack_fwd_s3_all = lgnn_gcn_stack_fwd_s3 + W (fp32 weights, host array of L + 1
+ *   device pointers) + S (host array of L pointers: S[l - 1] [M][K_l] receives Â H_{l-1} of the
+ *   open tiles, read by the backward's open phase).
+ * lgnn_gcn_stack_bwd_s3f_all = lgnn_gcn_stack_bwd_s3f + the transpose CSR (tptr / tidx / tw),
+ *   W, S (as above) and dS_ws (2 * M * 128 floats of workspace).
+ * ------------------------------------------------------------------------------------------- */
+int lgnn_gcn_stack_fwd_s3_all(const float* X, int64_t M, int d_in, int has_in_proj,
+                              const int32_t* rowptr, const int32_t* col, const float* w, int L,
+                              const uint16_t* planes, const float* const* W,
+                              const float* const* b, const int* widths, float* const* H,
+                              float* const* S, int32_t* tile_open, void* stream);
+int lgnn_gcn_stack_bwd_s3f_all(const float* dP, const int64_t* batch, const int32_t* gptr,
+                               int pool_mean, int64_t num_graphs, const int32_t* rowptr,
+                               const int32_t* col, const float* w, const int32_t* tptr,
+                               const int32_t* tidx, const float* tw, const float* X, int64_t M,
+                               int L, const uint16_t* planes_t, const float* const* W,
+                               const float* const* H, const float* const* S, const int* widths,
+                               float* const* dWp, float* const* dbp, int num_partials,
+                               float* dS_ws, int32_t* tile_open, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Sort pooling (DGCNN). Replaces: PyG 2.5.1 SortAggregation(k) as DRGNet applies it to the

@@ -19,6 +19,7 @@ LGNN_LOOPS_KEEP, LGNN_LOOPS_REMAINING, LGNN_LOOPS_READD = 0, 1, 2
 LGNN_NORM_NONE, LGNN_NORM_GCN = 0, 1
 LGNN_ACT_NONE, LGNN_ACT_ELU = 0, 1
 LGNN_GRAD_DIRECT, LGNN_GRAD_POOL, LGNN_GRAD_TRANSPOSE = 0, 1, 2
+LGNN_TILE_OPEN_EXTRA = 7  # tile_open words after the per-tile flags (count + barrier words)
 
 P = ctypes.c_void_p
 I32 = ctypes.c_int
@@ -80,6 +81,9 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_bn_bwd_apply": (I32, [P, P, P, I64, I32, P, P, P, P, P, F64, I32, P, P, P, P]),
     "lgnn_gcn_stack_bwd_s3f": (I32, [P, P, P, I32, I64, P, P, P, P, I64, I32, P, P, P, P, P,
                                      I32, P, P]),
+    "lgnn_gcn_stack_fwd_s3_all": (I32, [P, I64, I32, I32, P, P, P, I32, P, P, P, P, P, P, P, P]),
+    "lgnn_gcn_stack_bwd_s3f_all": (I32, [P, P, P, I32, I64, P, P, P, P, P, P, P, I64, I32, P, P, P,
+                                         P, P, P, P, I32, P, P, P]),
     "lgnn_sort_pool_workspace_bytes": (SZ, []),
     "lgnn_sort_pool_fwd": (I32, [P, I64, I32, P, I64, I32, P, P, P, P, SZ, P]),
     "lgnn_sort_pool_bwd": (I32, [P, P, P, P, P, I64, I32, I32, P, P]),
@@ -87,7 +91,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _lib = None
 

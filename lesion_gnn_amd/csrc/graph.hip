@@ -106,8 +106,8 @@ __global__ __launch_bounds__(kThreads) void k_prep(int32_t* __restrict__ zero, i
   const int64_t i0 = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   const int64_t step = (int64_t)gridDim.x * kThreads;
   for (int64_t i = i0; i < nzero; i += step) zero[i] = 0;
-  if (tile_open)
-    for (int64_t t = i0; t <= ntiles; t += step) tile_open[t] = 0;
+  if (tile_open)  // flags, their count, and the fused kernels' grid-barrier words
+    for (int64_t t = i0; t < ntiles + LGNN_TILE_OPEN_EXTRA; t += step) tile_open[t] = 0;
   if (gptr) {
     for (int64_t i = i0; i <= M; i += step) {
       // graphs q with prev < q <= cur start at node i (prev = batch[i-1] or -1; cur = batch[i]

@@ -27,6 +27,7 @@
 #include "tile.h"
 #include "tile_util.h"
 #include "s3_util.h"
+#include "tile_lw.h"
 
 // Timing-only ablation builds (tools/s3_probe.py): -DLGNN_S3_ABLATE=<mask> removes phases of
 // k_s3_fwd (1 GEMM1 MFMAs, 2 GEMM2 MFMAs, 4 H stores, 8 ELU, 16 epilogue plane split, 32 weight
@@ -205,13 +206,25 @@ __device__ __forceinline__ void gemm_feat(f32x16& c0, f32x16& c1, const u32x4 (&
   }
 }
 
+// Open-tile phase of the fused forward (optional): after the closed tiles, the tiles an edge
+// leaves run layer by layer on the fp32 layer-wise bodies (tile_lw.h, fp32 weights W, aggregated
+// inputs saved to S[l - 1] for the backward), a grid barrier between layers. Closed and open tiles
+// share no edge (the graph build flags both ends of a crossing edge), so the two phases are
+// independent; with no open tile (k-NN graphs aligned to tiles) the phase is skipped.
+struct OpenFwdArgs {
+  const float* W[LGNN_MAX_STACK];  // fp32 weights [N_l][K_l]
+  float* S[LGNN_MAX_STACK];        // S[l - 1] = Â H_{l-1} of the open tiles (conv l)
+  int32_t* sync;                   // grid-barrier words (nullptr: no open phase)
+};
+
 template <bool FIRST>
 __global__ __launch_bounds__(NT, 2) void k_s3_fwd(const float* __restrict__ X, int64_t M,
                                                   const int32_t* __restrict__ rowptr,
                                                   const int32_t* __restrict__ col,
                                                   const float* __restrict__ w, int L,
                                                   StackArgs args, const uint16_t* __restrict__ Wp,
-                                                  const int32_t* __restrict__ tmask) {
+                                                  const int32_t* __restrict__ tmask,
+                                                  OpenFwdArgs o) {
   __shared__ __attribute__((aligned(16))) FwdSmem sm;
   const int64_t ntiles = (M + TM - 1) / TM;
   const int l0 = FIRST ? 0 : 1;
@@ -223,7 +236,7 @@ __global__ __launch_bounds__(NT, 2) void k_s3_fwd(const float* __restrict__ X, i
     sm.bias[l][n] = (l >= l0 && n < args.width[l + 1]) ? args.b[l][n] : 0.f;
   }
   int64_t t = seek_tile(blockIdx.x, ntiles, tmask, 0);
-  if (t >= ntiles) return;
+  if (t < ntiles) {
   [[maybe_unused]] int stamp_i = 0;
   S3STAMP();
 
@@ -392,6 +405,24 @@ __global__ __launch_bounds__(NT, 2) void k_s3_fwd(const float* __restrict__ X, i
     }
     t = tn;
   }
+  }
+  if (o.sync && tmask[ntiles] > 0) {
+    static_assert(sizeof(LwSmem) <= sizeof(FwdSmem), "open-tile LDS aliases the fused LDS");
+    __syncthreads();  // the closed phase's LDS is free
+    LwSmem& lw = *reinterpret_cast<LwSmem*>(&sm);
+    for (int l = l0; l <= L; ++l) {
+      if (l > l0) grid_sync(o.sync, l - l0);  // layer l reads other open tiles' H_{l-1}
+      const int K = args.width[l], N = args.width[l + 1];
+      if (l == 0)
+        fwd_tiles<false, LGNN_ACT_NONE>(lw.A, lw.C, lw.ti, X, M, K, nullptr, nullptr, nullptr,
+                                        0.f, o.W[0], args.b[0], N, args.H[0], nullptr, tmask, 1);
+      else
+        fwd_tiles<true, LGNN_ACT_ELU>(lw.A, lw.C, lw.ti, l == 1 && !FIRST ? X : args.H[l - 1], M,
+                                      K, rowptr, col, w, 0.f, o.W[l], args.b[l], N, args.H[l],
+                                      o.S[l - 1], tmask, 1);
+    }
+    grid_exit(o.sync);
+  }
 }
 
 }  // namespace lgnn_s3
@@ -430,11 +461,38 @@ extern "C" int lgnn_weight_planes(int nl, const float* const* W, const int* widt
   return e == hipSuccess ? LGNN_OK : (int)e;
 }
 
+static int stack_fwd_s3(const float* X, int64_t M, int d_in, int has_in_proj,
+                        const int32_t* rowptr, const int32_t* col, const float* w, int L,
+                        const uint16_t* planes, const float* const* b, const int* widths,
+                        float* const* H, const int32_t* tile_open, const float* const* Wf,
+                        float* const* S, int32_t* sync, void* stream);
+
 extern "C" int lgnn_gcn_stack_fwd_s3(const float* X, int64_t M, int d_in, int has_in_proj,
                                      const int32_t* rowptr, const int32_t* col, const float* w,
                                      int L, const uint16_t* planes, const float* const* b,
                                      const int* widths, float* const* H,
                                      const int32_t* tile_open, void* stream) {
+  return stack_fwd_s3(X, M, d_in, has_in_proj, rowptr, col, w, L, planes, b, widths, H, tile_open,
+                      nullptr, nullptr, nullptr, stream);
+}
+
+extern "C" int lgnn_gcn_stack_fwd_s3_all(const float* X, int64_t M, int d_in, int has_in_proj,
+                                         const int32_t* rowptr, const int32_t* col,
+                                         const float* w, int L, const uint16_t* planes,
+                                         const float* const* W, const float* const* b,
+                                         const int* widths, float* const* H, float* const* S,
+                                         int32_t* tile_open, void* stream) {
+  if (!W || !S || !tile_open || M < 0) return LGNN_EINVAL;
+  const int64_t ntiles = (M + lgnn_tile::TM - 1) / lgnn_tile::TM;
+  return stack_fwd_s3(X, M, d_in, has_in_proj, rowptr, col, w, L, planes, b, widths, H, tile_open,
+                      W, S, tile_open + ntiles + 1, stream);
+}
+
+static int stack_fwd_s3(const float* X, int64_t M, int d_in, int has_in_proj,
+                        const int32_t* rowptr, const int32_t* col, const float* w, int L,
+                        const uint16_t* planes, const float* const* b, const int* widths,
+                        float* const* H, const int32_t* tile_open, const float* const* Wf,
+                        float* const* S, int32_t* sync, void* stream) {
   if (M < 0 || L < 1 || L + 1 > LGNN_MAX_STACK || !planes || !b || !widths || !H || !rowptr ||
       !col || !tile_open)
     return LGNN_EINVAL;
@@ -450,6 +508,15 @@ extern "C" int lgnn_gcn_stack_fwd_s3(const float* X, int64_t M, int d_in, int ha
     a.b[l] = b[l];
     a.H[l] = H[l];
   }
+  lgnn_s3::OpenFwdArgs o = {};
+  if (sync) {
+    for (int l = l0; l <= L; ++l) {
+      if (!Wf[l] || (l >= 1 && !S[l - 1])) return LGNN_EINVAL;
+      o.W[l] = Wf[l];
+      if (l >= 1) o.S[l - 1] = S[l - 1];
+    }
+    o.sync = sync;
+  }
   if (M == 0) return LGNN_OK;
   if (!X) return LGNN_EINVAL;
   const int64_t ntiles = (M + lgnn_tile::TM - 1) / lgnn_tile::TM;
@@ -457,10 +524,10 @@ extern "C" int lgnn_gcn_stack_fwd_s3(const float* X, int64_t M, int d_in, int ha
   hipStream_t s = as_stream(stream);
   if (has_in_proj)
     hipLaunchKernelGGL(lgnn_s3::k_s3_fwd<true>, grid, dim3(lgnn_tile::NT), 0, s, X, M, rowptr,
-                       col, w, L, a, planes, tile_open);
+                       col, w, L, a, planes, tile_open, o);
   else
     hipLaunchKernelGGL(lgnn_s3::k_s3_fwd<false>, grid, dim3(lgnn_tile::NT), 0, s, X, M, rowptr,
-                       col, w, L, a, planes, tile_open);
+                       col, w, L, a, planes, tile_open, o);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? LGNN_OK : (int)e;
 }

@@ -22,6 +22,7 @@
 #include "tile.h"
 #include "tile_util.h"
 #include "s3_util.h"
+#include "tile_lw.h"
 
 namespace lgnn_s3 {
 
@@ -505,6 +506,20 @@ struct FBwdArgs {
   int width[LGNN_MAX_STACK + 1];
 };
 
+// Open-tile phase of the fused backward (optional): after this workgroup wrote its partial
+// slots, the open tiles run layer by layer on the fp32 layer-wise bodies (tile_lw.h), adding into
+// the same slots (program order: no race), a grid barrier between layers (layer l - 1 gathers
+// layer l's pre-aggregation gradient dS through the transposed CSR).
+struct OpenBwdArgs {
+  const float* W[LGNN_MAX_STACK];  // fp32 weights
+  const float* S[LGNN_MAX_STACK];  // S[l - 1]: the forward's saved aggregated inputs (open tiles)
+  float* dS[2];                    // ping-pong [M][128] pre-aggregation gradients
+  const int32_t* tptr;             // transpose CSR
+  const int32_t* tidx;
+  const float* tw;
+  int32_t* sync;                   // grid-barrier words (nullptr: no open phase)
+};
+
 struct FBwdSmem {
   unsigned char Img[3][TM * AROW];  // 48 KiB: H_{l-1} (or X) feature-major [k][perm16 m]
   unsigned char Gt[3][TM * AROW];   // 48 KiB: G node-major [m][perm16 n]
@@ -519,7 +534,8 @@ template <int NL>
 __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ rowptr,
                                                    const int32_t* __restrict__ col,
                                                    const float* __restrict__ w, int64_t M,
-                                                   FBwdArgs a, const int32_t* __restrict__ tmask) {
+                                                   FBwdArgs a, const int32_t* __restrict__ tmask,
+                                                   OpenBwdArgs o) {
   constexpr int L = NL - 1;
   __shared__ __attribute__((aligned(16))) FBwdSmem sm;
   const int64_t ntiles = (M + TM - 1) / TM;
@@ -871,9 +887,40 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
       if (h == 0 && n < N) a.dbp[l][(int64_t)blockIdx.x * N + n] = dbacc[l];
     }
   }
+  if (o.sync && tmask[ntiles] > 0) {
+    static_assert(sizeof(LwSmem) <= sizeof(FBwdSmem), "open-tile LDS aliases the fused LDS");
+    __syncthreads();  // the closed phase's LDS is free; this workgroup's slots are written
+    LwSmem& lw = *reinterpret_cast<LwSmem*>(&sm);
+    for (int l = L; l >= 0; --l) {
+      if (l < L) grid_sync(o.sync, L - l);  // dS of layer l + 1 complete for every open tile
+      const int K = a.width[l], N = a.width[l + 1];
+      const float* Sx = l == 0 ? a.X : o.S[l - 1];
+      if (l == L)
+        bwd_tiles<LGNN_GRAD_POOL, LGNN_ACT_ELU, true>(
+            lw.A, lw.C, lw.ti, a.dP, a.batch, a.gptr, a.pool_mean, nullptr, nullptr, nullptr, 0.f,
+            a.H[l], Sx, M, K, o.W[l], N, o.dS[l & 1], a.dWp[l], a.dbp[l], tmask, 1, 1);
+      else if (l >= 1)
+        bwd_tiles<LGNN_GRAD_TRANSPOSE, LGNN_ACT_ELU, true>(
+            lw.A, lw.C, lw.ti, o.dS[(l + 1) & 1], a.batch, a.gptr, a.pool_mean, o.tptr, o.tidx,
+            o.tw, 0.f, a.H[l], Sx, M, K, o.W[l], N, o.dS[l & 1], a.dWp[l], a.dbp[l], tmask, 1,
+            1);
+      else
+        bwd_tiles<LGNN_GRAD_TRANSPOSE, LGNN_ACT_NONE, false>(
+            lw.A, lw.C, lw.ti, o.dS[1], a.batch, a.gptr, a.pool_mean, o.tptr, o.tidx, o.tw, 0.f,
+            nullptr, Sx, M, K, o.W[0], N, nullptr, a.dWp[0], a.dbp[0], tmask, 1, 1);
+    }
+    grid_exit(o.sync);
+  }
 }
 
 }  // namespace lgnn_s3
+
+static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* gptr,
+                         int pool_mean, int64_t num_graphs, const int32_t* rowptr,
+                         const int32_t* col, const float* w, const float* X, int64_t M, int L,
+                         const uint16_t* planes_t, const float* const* H, const int* widths,
+                         float* const* dWp, float* const* dbp, int num_partials,
+                         const int32_t* tile_open, const lgnn_s3::OpenBwdArgs& o, void* stream);
 
 extern "C" int lgnn_gcn_stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* gptr,
                                       int pool_mean, int64_t num_graphs, const int32_t* rowptr,
@@ -882,6 +929,43 @@ extern "C" int lgnn_gcn_stack_bwd_s3f(const float* dP, const int64_t* batch, con
                                       const float* const* H, const int* widths,
                                       float* const* dWp, float* const* dbp, int num_partials,
                                       const int32_t* tile_open, void* stream) {
+  const lgnn_s3::OpenBwdArgs o = {};
+  return stack_bwd_s3f(dP, batch, gptr, pool_mean, num_graphs, rowptr, col, w, X, M, L, planes_t,
+                       H, widths, dWp, dbp, num_partials, tile_open, o, stream);
+}
+
+extern "C" int lgnn_gcn_stack_bwd_s3f_all(
+    const float* dP, const int64_t* batch, const int32_t* gptr, int pool_mean,
+    int64_t num_graphs, const int32_t* rowptr, const int32_t* col, const float* w,
+    const int32_t* tptr, const int32_t* tidx, const float* tw, const float* X, int64_t M, int L,
+    const uint16_t* planes_t, const float* const* W, const float* const* H,
+    const float* const* S, const int* widths, float* const* dWp, float* const* dbp,
+    int num_partials, float* dS_ws, int32_t* tile_open, void* stream) {
+  if (M < 0 || L < 1 || L > 2 || !W || !S || !tptr || !tidx || !tw || !dS_ws || !tile_open)
+    return LGNN_EINVAL;
+  lgnn_s3::OpenBwdArgs o = {};
+  for (int l = 0; l <= L; ++l) {
+    if (!W[l] || (l >= 1 && !S[l - 1])) return LGNN_EINVAL;
+    o.W[l] = W[l];
+    if (l >= 1) o.S[l - 1] = S[l - 1];
+  }
+  o.dS[0] = dS_ws;
+  o.dS[1] = dS_ws + M * lgnn_s3::WP;
+  o.tptr = tptr;
+  o.tidx = tidx;
+  o.tw = tw;
+  const int64_t ntiles = (M + lgnn_tile::TM - 1) / lgnn_tile::TM;
+  o.sync = tile_open + ntiles + 4;
+  return stack_bwd_s3f(dP, batch, gptr, pool_mean, num_graphs, rowptr, col, w, X, M, L, planes_t,
+                       H, widths, dWp, dbp, num_partials, tile_open, o, stream);
+}
+
+static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* gptr,
+                         int pool_mean, int64_t num_graphs, const int32_t* rowptr,
+                         const int32_t* col, const float* w, const float* X, int64_t M, int L,
+                         const uint16_t* planes_t, const float* const* H, const int* widths,
+                         float* const* dWp, float* const* dbp, int num_partials,
+                         const int32_t* tile_open, const lgnn_s3::OpenBwdArgs& o, void* stream) {
   if (M < 0 || L < 1 || L > 2 || !dP || !batch || !gptr || !rowptr || !col || !X || !planes_t ||
       !H || !widths || !dWp || !dbp || !tile_open || num_graphs < 0)
     return LGNN_EINVAL;
@@ -912,9 +996,11 @@ extern "C" int lgnn_gcn_stack_bwd_s3f(const float* dP, const int64_t* batch, con
   }
   const dim3 grid((unsigned)num_partials), blk(lgnn_tile::NT);
   if (L == 1)
-    hipLaunchKernelGGL(lgnn_s3::k_s3_fbwd<2>, grid, blk, 0, s, rowptr, col, w, M, a, tile_open);
+    hipLaunchKernelGGL(lgnn_s3::k_s3_fbwd<2>, grid, blk, 0, s, rowptr, col, w, M, a, tile_open,
+                       o);
   else
-    hipLaunchKernelGGL(lgnn_s3::k_s3_fbwd<3>, grid, blk, 0, s, rowptr, col, w, M, a, tile_open);
+    hipLaunchKernelGGL(lgnn_s3::k_s3_fbwd<3>, grid, blk, 0, s, rowptr, col, w, M, a, tile_open,
+                       o);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? LGNN_OK : (int)e;
 }

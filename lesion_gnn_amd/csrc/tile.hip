@@ -14,6 +14,7 @@
 #include "common.h"
 #include "tile.h"
 #include "tile_util.h"
+#include "tile_lw.h"
 
 #include <cstdlib>
 #include <type_traits>
@@ -21,63 +22,7 @@
 namespace lgnn_tile {
 
 
-// sum_{e in row rr} w_e * X[c_e][4li..], in CSR order.
-// Local path: every source row is in the LDS image A; per entry one ds_read_b64 (offset,
-// weight), one ds_read_b128 and two packed FMAs, no bounds logic and no global access (so no
-// vmcnt wait that would drain the prefetch loads and row stores in flight).
-template <int UB = EB>
-__device__ __forceinline__ f32x4 agg_row_local(const TileIdx& ti, int rr, const float* A) {
-  static_assert(UB <= EB, "row batches read at most EB padding entries");
-  const int li = threadIdx.x & 31;
-  const int eb = ti.rp[0];
-  const int e0 = ti.rp[rr] - eb, e1 = ti.rp[rr + 1] - eb;
-  f32x4 acc = zero4();
-  for (int e = e0; e < e1; e += UB) {
-    int2 p[UB];
-#pragma unroll
-    for (int u = 0; u < UB; ++u) p[u] = ti.ow[e + u];
-    f32x4 v[UB];
-#pragma unroll
-    for (int u = 0; u < UB; ++u) v[u] = ld4(A + p[u].x + 4 * li);
-#pragma unroll
-    for (int u = 0; u < UB; ++u) {
-      const float wv = e + u < e1 ? __int_as_float(p[u].y) : 0.f;
-      acc += wv * v[u];
-    }
-  }
-  return acc;
-}
-
-// Global path (graphs straddling tiles, or more than CAPE entries): CSR and source rows read
-// from global memory, same order and arithmetic as the local path (bitwise-identical sums).
-__device__ __forceinline__ f32x4 agg_row_global(const TileIdx& ti, int rr,
-                                                const float* __restrict__ X, int K, int kc,
-                                                const int32_t* __restrict__ col,
-                                                const float* __restrict__ w) {
-  const int e0 = ti.rp[rr], e1 = ti.rp[rr + 1];
-  f32x4 acc = zero4();
-  for (int e = e0; e < e1; e += EB) {
-    int c[EB];
-    float ww[EB];
-#pragma unroll
-    for (int u = 0; u < EB; ++u) {
-      const bool ok = e + u < e1;
-      const int ee = ok ? e + u : e0;
-      c[u] = col[ee];
-      ww[u] = ok ? (w ? w[ee] : 1.f) : 0.f;
-    }
-    f32x4 v[EB];
-#pragma unroll
-    for (int u = 0; u < EB; ++u) v[u] = ld4(X + (int64_t)c[u] * K + kc);
-#pragma unroll
-    for (int u = 0; u < EB; ++u) acc += ww[u] * v[u];
-  }
-  return acc;
-}
-
-// ------------------------------------------------------------------------------------------
-// forward: Y = act(P(X) W^T + b); optional S_out = P(X)
-// ------------------------------------------------------------------------------------------
+// The layer-wise kernels: the bodies in tile_lw.h on their own LDS.
 template <bool GATHER, int ACT>
 __global__ __launch_bounds__(NT, 2) void k_fwd(const float* __restrict__ X, int64_t M, int K,
                                                const int32_t* __restrict__ rowptr,
@@ -90,124 +35,10 @@ __global__ __launch_bounds__(NT, 2) void k_fwd(const float* __restrict__ X, int6
   __shared__ __attribute__((aligned(16))) float A[TM * LDS];
   __shared__ __attribute__((aligned(16))) float S[GATHER ? TM * LDS : 4];
   __shared__ TileIdx ti;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int h = lane >> 5, li = lane & 31, hw = wave * 2 + h;
-  const int64_t ntiles = (M + TM - 1) / TM;
-  const int n = wave * 32 + li;
-  const int ncl = n < N ? n : N - 1;
-  const bool wave_active = wave * 32 < N;
-  int64_t t = seek_tile(blockIdx.x, ntiles, tmask, want);
-  if (t >= ntiles) return;
-  float bf[64];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int k = 64 * h + 4 * q;
-    const f32x4 v = ld4(W + (int64_t)ncl * K + (k < K ? k : K - 4));
-    const bool ok = n < N && k < K;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bf[4 * q + j] = ok ? v[j] : 0.f;
-  }
-  const float bias = b ? b[ncl] : 0.f;
-  const int kc = 4 * li < K ? 4 * li : K - 4;
-  const Buf bX = mkbuf(X, M * K * 4), bY = mkbuf(Y, M * N * 4);
-  const Buf bS = mkbuf(S_out, S_out ? M * K * 4 : 0);
-  float* Ain = GATHER ? S : A;  // MFMA A-operand image
-
-  if constexpr (ABL & 32) {  // desync experiment: odd blocks start half a tile late
-    if (blockIdx.x & 1) {
-      for (int i = 0; i < 4; ++i) __builtin_amdgcn_s_sleep(127);
-    }
-  }
-  // pipeline prologue: the first tile's rows and index block
-  f32x4 xr[8];
-  IdxRegs R;
-  if constexpr (!(ABL & 16)) load_rows(xr, bX, K, (int)(t * TM));
-  if constexpr (GATHER && !(ABL & 2)) {
-    idx_load_head(R, rowptr, M, t * TM);
-    idx_load_body(R, col, w);
-  }
-  for (; t < ntiles; t = seek_tile(t + gridDim.x, ntiles, tmask, want)) {
-    const int64_t r0 = t * TM;
-    const int64_t tn = seek_tile(t + gridDim.x, ntiles, tmask, want);
-    const bool has_next = tn < ntiles;
-    bool staged = true;
-    if constexpr (ABL & 16) {
-#pragma unroll
-      for (int it = 0; it < 8; ++it) xr[it] = zero4();
-    }
-    store_rows_lds(A, xr, M, K, r0);
-    if constexpr (GATHER && !(ABL & 2)) idx_store(ti, staged, R, r0);
-    __syncthreads();
-    // prefetch: next tile's rows and index head fly during this tile's aggregation and MFMAs
-    if (has_next) {
-      if constexpr (!(ABL & 16)) load_rows(xr, bX, K, (int)(tn * TM));
-      if constexpr (GATHER && !(ABL & 2)) idx_load_head(R, rowptr, M, tn * TM);
-    }
-    if constexpr (GATHER) {
-      auto agg_tile = [&](auto staged_tag) {
-        constexpr bool STG = decltype(staged_tag)::value;
-#pragma unroll 1
-        for (int it = 0; it < 8; ++it) {
-          const int rr = hw + 8 * it;
-          f32x4 a;
-          if constexpr (ABL & 2) a = ld4(A + rr * LDS + 4 * li);
-          else if constexpr (STG) a = agg_row_local(ti, rr, A);
-          else a = agg_row_global(ti, rr, X, K, kc, col, w);
-          if (self_scale != 0.f) a += self_scale * ld4(A + rr * LDS + 4 * li);
-          a = sel4(4 * li < K && r0 + rr < M, a);
-          st4(S + rr * LDS + 4 * li, a);
-          if (!(ABL & 4) && S_out && 4 * li < K)
-            bst4(bS, (int)((r0 + rr) * K + 4 * li) * 4, a);
-        }
-      };
-      if (staged) agg_tile(std::true_type{});
-      else agg_tile(std::false_type{});
-      if constexpr (!(ABL & 2)) {
-        if (has_next) idx_load_body(R, col, w);
-      }
-      __syncthreads();
-    }
-    f32x16 acc0 = {}, acc1 = {};
-    if (wave_active && !(ABL & 1)) {
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const f32x4 a0 = ld4(Ain + li * LDS + 64 * h + 4 * q);
-        const f32x4 a1 = ld4(Ain + (32 + li) * LDS + 64 * h + 4 * q);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc0 = mfma32(a0[j], bf[4 * q + j], acc0);
-          acc1 = mfma32(a1[j], bf[4 * q + j], acc1);
-        }
-      }
-    }
-    __syncthreads();  // every wave is done reading A / S
-    // epilogue staged in A as [row][col], then whole-row stores
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
-      float v0 = acc0[r] + bias, v1 = acc1[r] + bias;
-      if (ACT == LGNN_ACT_ELU) {
-        v0 = elu_f(v0);
-        v1 = elu_f(v1);
-      }
-      A[rl * LDS + n] = v0;
-      A[(32 + rl) * LDS + n] = v1;
-    }
-    __syncthreads();
-    if (4 * li < N && !(ABL & 4)) {
-#pragma unroll
-      for (int it = 0; it < 8; ++it) {
-        const int rr = hw + 8 * it;
-        bst4(bY, (int)((r0 + rr) * N + 4 * li) * 4, ld4(A + rr * LDS + 4 * li));
-      }
-    }
-    __syncthreads();
-  }
+  fwd_tiles<GATHER, ACT>(A, S, ti, X, M, K, rowptr, col, w, self_scale, W, b, N, Y, S_out, tmask,
+                         want);
 }
 
-// ------------------------------------------------------------------------------------------
-// backward: dZ = G ⊙ act'(H); dW += dZ^T S (S = X, direct); db += colsum dZ; dXpre = dZ W
-// ------------------------------------------------------------------------------------------
 template <int GMODE, int ACT, bool DX>
 __global__ __launch_bounds__(NT, 2) void k_bwd(
     const float* __restrict__ dY, const int64_t* __restrict__ batch,
@@ -219,208 +50,8 @@ __global__ __launch_bounds__(NT, 2) void k_bwd(
   __shared__ __attribute__((aligned(16))) float A[TM * LDS];
   __shared__ __attribute__((aligned(16))) float C[TM * LDS];
   __shared__ TileIdx ti;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int h = lane >> 5, li = lane & 31, hw = wave * 2 + h;
-  const int64_t ntiles = (M + TM - 1) / TM;
-  const int oc = 4 * li < N ? 4 * li : N - 4;
-  const bool oin = 4 * li < N;
-
-  const Buf bdY = mkbuf(dY, M * N * 4), bH = mkbuf(H, H ? M * N * 4 : 0);
-  const Buf bX = mkbuf(X, M * K * 4), bdX = mkbuf(dXpre, dXpre ? M * K * 4 : 0);
-  f32x16 dw[4] = {{}, {}, {}, {}};
-  float dbacc = 0.f;
-  const int kx = 32 * wave + li;
-  const int kxc = kx < K ? kx : K - 1;
-
-  // pipeline prologue (TRANSPOSE): the first tile's dY rows and transpose-CSR index block
-  f32x4 dr[8];
-  IdxRegs R;
-  const int64_t tfirst = seek_tile(blockIdx.x, ntiles, tmask, want);
-  if constexpr (GMODE == LGNN_GRAD_TRANSPOSE) {
-    const int64_t t0 = tfirst;
-    if (t0 < ntiles) {
-      if constexpr (!(ABL & 16)) load_rows(dr, bdY, N, (int)(t0 * TM));
-      if constexpr (!(ABL & 2)) {
-        idx_load_head(R, tptr, M, t0 * TM);
-        idx_load_body(R, tidx, tw);
-      }
-    }
-  }
-
-  for (int64_t t = tfirst; t < ntiles; t = seek_tile(t + gridDim.x, ntiles, tmask, want)) {
-    const int64_t r0 = t * TM;
-    const int64_t tn = seek_tile(t + gridDim.x, ntiles, tmask, want);
-    const bool has_next = tn < ntiles;
-    // ---- dZ tile -> C
-    if constexpr (GMODE == LGNN_GRAD_TRANSPOSE) {
-      bool staged = true;
-      if constexpr (ABL & 16) {
-#pragma unroll
-        for (int it = 0; it < 8; ++it) dr[it] = zero4();
-      }
-      store_rows_lds(A, dr, M, N, r0);
-      if constexpr (!(ABL & 2)) idx_store(ti, staged, R, r0);
-      // this tile's H rows (ELU') are issued before the barrier so they land during it
-      f32x4 hv[8];
-      if constexpr (ACT == LGNN_ACT_ELU) {
-#pragma unroll
-        for (int it = 0; it < 8; ++it) {
-          const int64_t row = r0 + hw + 8 * it;
-          hv[it] = (ABL & 16) ? zero4() : bld4(bH, (int)(row * N + oc) * 4);
-        }
-      }
-      __syncthreads();
-      // prefetch: next tile's dY rows and index head
-      if (has_next) {
-        if constexpr (!(ABL & 16)) load_rows(dr, bdY, N, (int)(tn * TM));
-        if constexpr (!(ABL & 2)) idx_load_head(R, tptr, M, tn * TM);
-      }
-      auto agg_tile = [&](auto staged_tag) {
-        constexpr bool STG = decltype(staged_tag)::value;
-#pragma unroll 1
-        for (int it = 0; it < 8; ++it) {
-          const int rr = hw + 8 * it;
-          const int64_t row = r0 + rr;
-          f32x4 g;
-          if constexpr (ABL & 2) g = ld4(A + rr * LDS + 4 * li);
-          else if constexpr (STG) g = agg_row_local(ti, rr, A);
-          else g = agg_row_global(ti, rr, dY, N, oc, tidx, tw);
-          if (tself != 0.f) g += tself * ld4(A + rr * LDS + 4 * li);
-          if constexpr (ACT == LGNN_ACT_ELU) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) g[j] *= elu_grad_from_out(hv[it][j]);
-          }
-          st4(C + rr * LDS + 4 * li, sel4(oin && row < M, g));
-        }
-      };
-      if (staged) agg_tile(std::true_type{});
-      else agg_tile(std::false_type{});
-      if constexpr (!(ABL & 2)) {
-        if (has_next) idx_load_body(R, tidx, tw);
-      }
-    } else {
-      f32x4 g[8], hv[8];
-#pragma unroll
-      for (int it = 0; it < 8; ++it) {
-        const int64_t row = r0 + hw + 8 * it;
-        const int64_t rc = row < M ? row : M - 1;
-        if constexpr (GMODE == LGNN_GRAD_DIRECT) {
-          g[it] = ld4(dY + rc * N + oc);
-        } else {
-          const int64_t gi = batch[rc];
-          g[it] = ld4(dY + gi * N + oc);
-          if (pool_mean) {
-            const int cnt = gptr[gi + 1] - gptr[gi];
-            g[it] = g[it] / (float)(cnt > 0 ? cnt : 1);
-          }
-        }
-        if constexpr (ACT == LGNN_ACT_ELU) hv[it] = ld4(H + rc * N + oc);
-      }
-#pragma unroll
-      for (int it = 0; it < 8; ++it) {
-        const int rr = hw + 8 * it;
-        f32x4 v = g[it];
-        if constexpr (ACT == LGNN_ACT_ELU) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] *= elu_grad_from_out(hv[it][j]);
-        }
-        st4(C + rr * LDS + 4 * li, sel4(oin && r0 + rr < M, v));
-      }
-    }
-    // ---- S tile -> A (A's raw dY image is dead once every wave has passed this barrier)
-    f32x4 sr[8];
-    if constexpr (ABL & 16) {
-#pragma unroll
-      for (int it = 0; it < 8; ++it) sr[it] = zero4();
-    } else {
-      load_rows(sr, bX, K, (int)r0);
-    }
-    __syncthreads();
-    store_rows_lds(A, sr, M, K, r0);
-    __syncthreads();
-    if (tid < 128) {
-      float s0 = 0.f, s1 = 0.f;
-#pragma unroll 8
-      for (int r = 0; r < TM; r += 2) {
-        s0 += C[r * LDS + tid];
-        s1 += C[(r + 1) * LDS + tid];
-      }
-      dbacc += s0 + s1;
-    }
-    // DX B-fragment W[o = 64h + s][kx], re-read per tile (L2) so it is not live during the
-    // aggregation phase; its latency hides under the dW MFMAs.
-    // Buffer loads: per-lane voffset (column kx, half-wave row block 64h) + uniform soffset
-    // (row s); rows o >= N fall outside the descriptor's range and read 0.
-    float wt[64];
-    if constexpr (DX) {
-      const __amdgpu_buffer_rsrc_t wr =
-          __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, N * K * 4, 0x00020000);
-      const int voff = (64 * h * K + kxc) * 4;
-#pragma unroll
-      for (int s = 0; s < 64; ++s) {
-        const float v = __builtin_bit_cast(
-            float, __builtin_amdgcn_raw_buffer_load_b32(wr, voff, s * K * 4, 0));
-        wt[s] = kx < K ? v : 0.f;
-      }
-    }
-    // dW[o][k] += sum_m dZ[m][o] S[m][k]; wave owns o in [32w, 32w+32)
-#pragma unroll 4
-    for (int s = 0; s < (ABL & 1 ? 0 : TM / 2); ++s) {
-      const int m = 2 * s + h;
-      const float a = C[m * LDS + 32 * wave + li];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) dw[j] = mfma32(a, A[m * LDS + 32 * j + li], dw[j]);
-    }
-    if constexpr (DX) {
-      f32x16 x0 = {}, x1 = {};
-#pragma unroll
-      for (int q = 0; q < (ABL & 1 ? 0 : 16); ++q) {
-        const f32x4 a0 = ld4(C + li * LDS + 64 * h + 4 * q);
-        const f32x4 a1 = ld4(C + (32 + li) * LDS + 64 * h + 4 * q);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          x0 = mfma32(a0[j], wt[4 * q + j], x0);
-          x1 = mfma32(a1[j], wt[4 * q + j], x1);
-        }
-      }
-      __syncthreads();  // dW reads of A are done
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
-        A[rl * LDS + kx] = x0[r];
-        A[(32 + rl) * LDS + kx] = x1[r];
-      }
-      __syncthreads();
-      if (4 * li < K && !(ABL & 4)) {
-#pragma unroll
-        for (int it = 0; it < 8; ++it) {
-          const int rr = hw + 8 * it;
-          bst4(bdX, (int)((r0 + rr) * K + 4 * li) * 4, ld4(A + rr * LDS + 4 * li));
-        }
-      }
-    }
-    __syncthreads();
-  }
-  // accumulate: add into slot blockIdx.x (written by the fused stack backward) if this
-  // workgroup processed any tile; otherwise leave the slot untouched
-  if (accumulate && tfirst >= ntiles) return;
-  float* slab = dWp + (int64_t)blockIdx.x * N * K;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int k = 32 * j + li;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int o = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (o < N && k < K) {
-        float* p = slab + (int64_t)o * K + k;
-        *p = accumulate ? *p + dw[j][r] : dw[j][r];
-      }
-    }
-  }
-  if (dbp && tid < N) {
-    float* p = dbp + (int64_t)blockIdx.x * N + tid;
-    *p = accumulate ? *p + dbacc : dbacc;
-  }
+  bwd_tiles<GMODE, ACT, DX>(A, C, ti, dY, batch, gptr, pool_mean, tptr, tidx, tw, tself, H, X, M,
+                            K, W, N, dXpre, dWp, dbp, tmask, want, accumulate);
 }
 
 
@@ -1100,7 +731,7 @@ extern "C" int lgnn_tile_open(const int32_t* rowptr, const int32_t* col, int64_t
   if (M < 0 || !open || (M > 0 && (!rowptr || !col))) return LGNN_EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int64_t ntiles = (M + lgnn_tile::TM - 1) / lgnn_tile::TM;
-  if (hipMemsetAsync(open, 0, (ntiles + 1) * sizeof(int32_t), s) != hipSuccess)
+  if (hipMemsetAsync(open, 0, (ntiles + LGNN_TILE_OPEN_EXTRA) * sizeof(int32_t), s) != hipSuccess)
     return (int)hipGetLastError();
   if (ntiles == 0) return LGNN_OK;
   int64_t g = (M + lgnn_tile::NT - 1) / lgnn_tile::NT;

@@ -211,6 +211,51 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// Grid-wide barrier of a persistent launch whose workgroups are all co-resident (the fused
+// stack kernels: 2 per CU forward, 1 per CU backward, grid <= that). sync[0] counts arrivals
+// (barrier `gen` = 1, 2, ... waits for gen * gridDim.x), sync[1] counts exits; both start at 0
+// (zeroed by the graph build) and grid_exit() re-arms them for the next launch: the workgroup
+// that completes the exit count resets both, when no other workgroup reads them any more.
+// Producer side: __syncthreads drains every wave's stores (vmcnt(0)), then one lane releases at
+// agent scope (L2 write-back for the other XCDs); consumer: agent-scope acquire (L1/L2
+// invalidate), then __syncthreads before any wave reads (MI355X_MICROARCH.md, correctness
+// boundaries). The spin is bounded (~0.5 s): a barrier that cannot complete yields wrong
+// results, never a hang; it counts itself in sync[2].
+__device__ __forceinline__ void grid_sync(int32_t* sync, int gen) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(sync, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    const int target = gen * (int)gridDim.x;
+    int spins = 0;
+    while (__hip_atomic_load(sync, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(8);
+      if (++spins > (1 << 20)) {
+        __hip_atomic_fetch_add(sync + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void grid_exit(int32_t* sync) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int n = __hip_atomic_fetch_add(sync + 1, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (n == (int)gridDim.x - 1) {
+      __hip_atomic_store(sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sync + 1, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Layer-wise (open-tile) LDS of tile_lw.h's bodies, aliased onto a fused kernel's LDS.
+struct LwSmem {
+  float A[TM * LDS];
+  float C[TM * LDS];
+  TileIdx ti;
+};
+
 // Arguments of the fused GCN stack forward kernels (tile.hip, stack3.hip).
 struct StackArgs {
   const float* W[LGNN_MAX_STACK];

@@ -31,7 +31,8 @@ class Csr:
     tidx: torch.Tensor    # int32 [cap] target of each entry, grouped by source
     tw: torch.Tensor      # fp32 [cap]
     tmap: torch.Tensor | None  # int32 [cap] target-CSR position of each transpose entry (GAT)
-    tile_open: torch.Tensor | None  # int32 [ceil(N/64) + 1] tiles an edge leaves, + their count
+    tile_open: torch.Tensor | None  # int32 [ceil(N/64) + 7] tiles an edge leaves, their count,
+    # and the fused stack kernels' grid-barrier words (LGNN_TILE_OPEN_EXTRA)
     err: torch.Tensor     # int32 [1] count of dropped out-of-range edges
 
 
@@ -103,7 +104,8 @@ class Graph:
             tptr=torch.empty(n + 1, **i32), tidx=torch.empty(cap, **i32),
             tw=torch.empty(cap, dtype=torch.float32, device=dev),
             tmap=torch.empty(cap, **i32) if kind == "gat" else None,
-            tile_open=torch.empty((n + 63) // 64 + 1, **i32) if kind == "gcn" else None,
+            tile_open=torch.empty((n + 63) // 64 + _lib.LGNN_TILE_OPEN_EXTRA, **i32)
+            if kind == "gcn" else None,
             err=torch.empty(1, **i32),
         )
         lib = _lib.load()
@@ -161,7 +163,7 @@ class Graph:
         return key
 
     def tile_open(self, kind: str) -> torch.Tensor:
-        """int32 [ceil(N/64) + 1]: 1 for the 64-node tiles an edge leaves or that exceed the
+        """int32 [ceil(N/64) + 7]: 1 for the 64-node tiles an edge leaves or that exceed the
         on-chip CSR capacity, then the number of such tiles (from the graph build for kind
         "gcn"; lgnn_tile_open otherwise)."""
         c = self.csr(kind)
@@ -170,7 +172,8 @@ class Graph:
         key = "open:" + kind
         if key not in self._aux:
             n_t = _lib.load().lgnn_tile_count(self.num_nodes)
-            t = torch.empty(n_t + 1, dtype=torch.int32, device=self.device)
+            t = torch.empty(n_t + _lib.LGNN_TILE_OPEN_EXTRA, dtype=torch.int32,
+                            device=self.device)
             _lib.call("lgnn_tile_open", _lib.ptr(c.rowptr), _lib.ptr(c.col), self.num_nodes,
                       _lib.ptr(t), _lib.stream(self.device))
             self._aux[key] = t

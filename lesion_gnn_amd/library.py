@@ -126,7 +126,7 @@ def _(edge_index, num_nodes, kind):
             e.new_empty(n + 1, **i32), e.new_empty(cap, **i32), e.new_empty(cap, **f32),
             e.new_empty(cap if kind == "gat" else 0, **(i32 if kind == "gat" else
                                                        dict(dtype=torch.uint8))),
-            e.new_empty((n + 63) // 64 + 1 if kind == "gcn" else 0,
+            e.new_empty((n + 63) // 64 + 7 if kind == "gcn" else 0,
                         **(i32 if kind == "gcn" else dict(dtype=torch.uint8))),
             e.new_empty(1, **i32)]
 

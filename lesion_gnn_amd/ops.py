@@ -83,6 +83,30 @@ MFMA_MODE = os.environ.get("LGNN_MFMA", "s3")
 # planes come out of its weight-plane launch); otherwise the f32 kernel runs.
 BWD_MODE = os.environ.get("LGNN_BWD", "s3f")
 BWD_S3 = BWD_MODE in ("s3", "s3f")
+# open tiles (an edge leaves them) inside the fused split-3 launches, layer by layer behind grid
+# barriers, instead of three layer-wise launches per direction (LGNN_OPEN_IN_FUSED=0: separate)
+# The fused kernels' open phase saves the six layer-wise launches (~4.5 us each), but runs the
+# open tiles ~1.5x slower than the standalone layer-wise kernels (measured C5, r02j). So it is
+# taken when open tiles are expected to be rare: "auto" (default) = when every graph could sit
+# whole in 64-node tiles (all graphs of one size that divides or is a multiple of 64: the
+# batch's node count is B * n with 64 % n == 0 or n % 64 == 0). Either choice is exact; "1" /
+# "0" force it (also "fwd" / "bwd" for one direction).
+OPEN_IN_FUSED = os.environ.get("LGNN_OPEN_IN_FUSED", "auto")
+OPEN_IN_FUSED_BWD = OPEN_IN_FUSED
+
+
+def _open_in_fused(mode, graph: Graph, direction: str) -> bool:
+    if mode in ("1", True):
+        return True
+    if mode in ("0", False):
+        return False
+    if mode in ("fwd", "bwd"):
+        return mode == direction
+    M, B = graph.num_nodes, graph.num_graphs
+    if not B or M % B:
+        return False
+    n = M // B
+    return n > 0 and (64 % n == 0 or n % 64 == 0)
 
 
 def weight_planes(Ws: list, d_in: int, transposed: bool = False):
@@ -122,6 +146,13 @@ def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list, keep: dict | No
         planes, planes_t = weight_planes(Ws, x.size(1), transposed=keep is not None)
         if keep is not None:
             keep["planes_t"] = planes_t
+        if _open_in_fused(OPEN_IN_FUSED, graph, "fwd"):  # open tiles in the same launch
+            _lib.call("lgnn_gcn_stack_fwd_s3_all", _lib.ptr(x), M, x.size(1), 1,
+                      _lib.ptr(csr.rowptr), _lib.ptr(csr.col), _lib.ptr(csr.w), L,
+                      _lib.ptr(planes), Wp, bp, widths, Hp,
+                      (ctypes.c_void_p * L)(*[t.data_ptr() for t in ss]), _lib.ptr(open_),
+                      _s(dev))
+            return hs, ss
         _lib.call("lgnn_gcn_stack_fwd_s3", _lib.ptr(x), M, x.size(1), 1, _lib.ptr(csr.rowptr),
                   _lib.ptr(csr.col), _lib.ptr(csr.w), L, _lib.ptr(planes), bp, widths, Hp,
                   _lib.ptr(open_), _s(dev))
@@ -170,6 +201,18 @@ def stack_bwd(dp: torch.Tensor, x: torch.Tensor, graph: Graph, mean: bool, Ws: l
         off += P * (nk + n)
     arr = ctypes.c_void_p * (L + 1)
     Sx = [x] + list(ss)
+    if s3f and _open_in_fused(OPEN_IN_FUSED_BWD, graph, "bwd"):  # one launch, open tiles last
+        dS_ws = torch.empty(2 * M * 128, dtype=torch.float32, device=dev)
+        _lib.call("lgnn_gcn_stack_bwd_s3f_all", _lib.ptr(dp), _lib.ptr(graph.batch),
+                  _lib.ptr(graph.gptr), int(mean), dp.size(0), _lib.ptr(csr.rowptr),
+                  _lib.ptr(csr.col), _lib.ptr(csr.w), _lib.ptr(csr.tptr), _lib.ptr(csr.tidx),
+                  _lib.ptr(csr.tw), _lib.ptr(x), M, L, _lib.ptr(planes_t),
+                  arr(*[W.data_ptr() for W in Ws]), arr(*[h.data_ptr() for h in hs]),
+                  (ctypes.c_void_p * L)(*[t.data_ptr() for t in ss]),
+                  (ctypes.c_int * (L + 2))(*widths), arr(*[t.data_ptr() for t in dWp]),
+                  arr(*[t.data_ptr() for t in dbp]), P, _lib.ptr(dS_ws), _lib.ptr(open_),
+                  _s(dev))
+        return _stack_bwd_outputs(L, widths, dWp, dbp, P, dev, reducer)
     if s3f:  # one fused split-3 launch, every layer of a tile in one pass (stack3_bwd.hip)
         _lib.call("lgnn_gcn_stack_bwd_s3f", _lib.ptr(dp), _lib.ptr(graph.batch),
                   _lib.ptr(graph.gptr), int(mean), dp.size(0), _lib.ptr(csr.rowptr),
@@ -208,6 +251,10 @@ def stack_bwd(dp: torch.Tensor, x: torch.Tensor, graph: Graph, mean: bool, Ws: l
                   None, None, None, 0.0, _lib.ptr(Ws[l]), N, _lib.ptr(dX), _lib.ptr(dWp[l]),
                   _lib.ptr(dbp[l]), P, _lib.ptr(open_), 1, 1, _s(dev))
         dS = dX
+    return _stack_bwd_outputs(L, widths, dWp, dbp, P, dev, reducer)
+
+
+def _stack_bwd_outputs(L, widths, dWp, dbp, P, dev, reducer):
     out = []
     for l in range(L + 1):
         dW = torch.empty(widths[l + 1], widths[l], dtype=torch.float32, device=dev)

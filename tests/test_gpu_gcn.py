@@ -272,12 +272,15 @@ def test_tile_open_flags(cuda):
     sizes = [64, 64, 30, 34, 64, 100, 28, 64, 1]
     b = synth.make_batch(len(sizes), k=6, d_in=8, seed=22, sizes=sizes)
     g = Graph(b.edge_index.to(cuda), b.num_nodes)
-    got = g.tile_open("gcn").cpu()
+    nt = (b.num_nodes + 63) // 64
+    got_all = g.tile_open("gcn").cpu()
+    assert got_all.numel() == nt + 7 and got_all[nt + 1:].tolist() == [0] * 6  # barrier words
+    got = got_all[:nt + 1]
     c = g.csr("gcn")
-    ref_t = torch.empty_like(got, device=cuda)
+    ref_t = torch.empty_like(got_all, device=cuda)
     _lib.call("lgnn_tile_open", c.rowptr.data_ptr(), c.col.data_ptr(), b.num_nodes,
               ref_t.data_ptr(), _lib.stream())
-    assert torch.equal(got, ref_t.cpu())
+    assert torch.equal(got_all, ref_t.cpu())
     src, dst = b.edge_index
     want = torch.zeros_like(got)
     cross = (src // 64) != (dst // 64)
@@ -287,7 +290,7 @@ def test_tile_open_flags(cuda):
     assert torch.equal(got, want)
     # all tiles closed: count 0 (the masked launches return at once)
     b2 = synth.make_batch(4, n=64, k=6, d_in=8, seed=23)
-    assert Graph(b2.edge_index.to(cuda), b2.num_nodes).tile_open("gcn").cpu().tolist() == [0] * 5
+    assert Graph(b2.edge_index.to(cuda), b2.num_nodes).tile_open("gcn").cpu().tolist()[:5] == [0] * 5
 
 
 @pytest.mark.parametrize("bwd", ["f32", "s3", "s3f"])
@@ -315,7 +318,7 @@ def test_gcn_fused_backward(cuda, case, bwd, monkeypatch):
     monkeypatch.setattr(ops, "BWD_S3", bwd != "f32")
     if case == "dense_tiles":
         g = Graph(b.edge_index.to(cuda), b.num_nodes)
-        assert g.tile_open("gcn").cpu().tolist() == [1, 1, 1, 1, 1, 5]
+        assert g.tile_open("gcn").cpu().tolist()[:6] == [1, 1, 1, 1, 1, 5]
     monkeypatch.setattr(ops, "FUSED_BWD", True)
     lf, _, gf = run_step(ours, b, cuda)
     monkeypatch.setattr(ops, "FUSED_BWD", False)
@@ -330,3 +333,39 @@ def test_gcn_fused_backward(cuda, case, bwd, monkeypatch):
     _, _, gf2 = run_step(ours, b, cuda)
     for k in gf:
         assert torch.equal(gf[k], gf2[k]), k
+
+
+@pytest.mark.parametrize("open_in_fused", [True, False])
+def test_open_tiles_in_fused_launch(cuda, open_in_fused, monkeypatch):
+    """Open tiles (graphs straddling 64-node tiles, an over-capacity tile) processed inside the
+    fused split-3 launches (layer by layer behind grid barriers) == the separate layer-wise
+    launches == the oracle; the same Graph reused for a second step (the barrier words re-arm
+    themselves: every word back to 0, no barrier gave up)."""
+    from lesion_gnn_amd.graph import Graph
+
+    monkeypatch.setattr(ops, "OPEN_IN_FUSED", open_in_fused)
+    monkeypatch.setattr(ops, "OPEN_IN_FUSED_BWD", open_in_fused)
+    sizes = [1, 5, 64, 200, 2, 33, 512, 17, 64, 64, 30, 34]
+    b = synth.make_batch(len(sizes), k=6, d_in=128, seed=41, sizes=sizes)
+    ours, oref = make_pair([128, 128, 128])
+    ours = ours.to(cuda)
+    g = Graph(b.edge_index.to(cuda), b.num_nodes, b.batch.to(cuda), b.num_graphs)
+    nt = (b.num_nodes + 63) // 64
+    results = []
+    for _ in range(2):
+        logits = ours(b.x.to(cuda), g, b.batch.to(cuda), b.num_graphs)
+        loss = torch.nn.functional.cross_entropy(logits, b.y.to(cuda))
+        ours.zero_grad(set_to_none=True)
+        loss.backward()
+        results.append((logits.detach().cpu(),
+                        {k: p.grad.detach().cpu() for k, p in ours.named_parameters()}))
+        words = g.tile_open("gcn").cpu().tolist()
+        assert words[nt] > 0  # this batch has open tiles
+        assert words[nt + 1:] == [0] * 6, words[nt:]
+    lr_, _, gr = run_step(oref, b, "cpu")
+    for lo, go in results:
+        torch.testing.assert_close(lo, lr_, atol=1e-4, rtol=0)
+        for k in gr:
+            torch.testing.assert_close(go[k], gr[k], atol=1e-5, rtol=1e-4,
+                                       msg=lambda m: f"{k}: {m}")
+    assert torch.equal(results[0][0], results[1][0])
