@@ -7,24 +7,32 @@
 // left in a caller-visible fp64 buffer so a SyncBN all-reduce (RCCL) can run between
 // lgnn_bn_stats and lgnn_bn_finalize.
 //
-// Column mapping (all kernels): blockIdx.y = 64-column chunk, lane = column, the block's 4 waves
-// stride rows. One fp32 load per lane and row = 256 contiguous bytes per wave instruction.
+// Thread mapping (all kernels): a row of up to 128 columns is covered by 32 lanes holding 4
+// consecutive columns each (blockIdx.y = 128-column chunk); the block's 8 half-wave row groups
+// stride rows, so per-column constants stay in registers and every row access is one 16-B load
+// per lane (512 contiguous bytes per half-wave). Sums: four rows in flight per thread.
 #include "common.h"
 
 namespace {
 
 constexpr int NT = 256;
-constexpr int ROWS_PER_BLOCK = 512;  // rows summed by one block into one partial
+constexpr int RG = NT / 32;           // row groups per block
+constexpr int ROWS_PER_BLOCK = 256;   // rows summed by one block into one partial
+constexpr int RED_SPLIT = 8;          // k_colsum_reduce: partial groups per output
 
 inline int row_blocks(int64_t M) {
   const int64_t b = (M + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
   return (int)(b < 1 ? 1 : b);
 }
 
-// xhat-side helpers -------------------------------------------------------------------------
+// ELU'(zn) for zn = z * scale + shift: 1 above 0, exp(zn) below (exp2 form)
 __device__ __forceinline__ float bn_elu_grad(float z, float sc, float sh) {
   const float zn = fmaf(z, sc, sh);
-  return zn > 0.f ? 1.f : expf(zn);
+  return zn > 0.f ? 1.f : __builtin_amdgcn_exp2f(zn * 1.44269504088896341f);
+}
+
+__device__ __forceinline__ f32x4 ld4c(const float* p, int c, int N) {
+  return c < N ? ld4(p + c) : f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
 // MODE 0: sums of z and z^2                        (forward statistics)
@@ -38,52 +46,94 @@ __global__ __launch_bounds__(NT) void k_colsum(const float* __restrict__ Z,
                                                const float* __restrict__ mean,
                                                const float* __restrict__ invstd,
                                                double* __restrict__ part) {
-  __shared__ double red[2][4][64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = blockIdx.y * 64 + lane;
-  const int cc = c < N ? c : N - 1;
+  __shared__ double red[2][RG][128];
+  const int li = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int c = blockIdx.y * 128 + 4 * li;
+  const bool cin = c < N;
   const int64_t r0 = (int64_t)blockIdx.x * ROWS_PER_BLOCK;
   const int64_t r1 = r0 + ROWS_PER_BLOCK < M ? r0 + ROWS_PER_BLOCK : M;
-  float sc = 0.f, sh = 0.f, mu = 0.f, is = 0.f;
+  f32x4 sc = {}, sh = {}, mu = {}, is = {};
   if constexpr (MODE == 1) {
-    sc = scale[cc];
-    sh = shift[cc];
-    mu = mean[cc];
-    is = invstd[cc];
+    sc = ld4c(scale, c, N);
+    sh = ld4c(shift, c, N);
+    mu = ld4c(mean, c, N);
+    is = ld4c(invstd, c, N);
   }
-  double s0 = 0.0, s1 = 0.0;
-  for (int64_t r = r0 + wave; r < r1; r += 4) {
-    const float z = Z[r * N + cc];
+  double s0[4] = {0.0, 0.0, 0.0, 0.0}, s1[4] = {0.0, 0.0, 0.0, 0.0};
+  auto term = [&](int64_t r) {
+    const f32x4 z = ld4(Z + r * N + c);
     if constexpr (MODE == 0) {
-      s0 += (double)z;
-      s1 += (double)z * (double)z;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s0[j] += (double)z[j];
+        s1[j] += (double)z[j] * (double)z[j];
+      }
     } else {
-      float g = dA[r * N + cc] * bn_elu_grad(z, sc, sh);
-      if (mask) g *= mask[r * N + cc];
-      const float xh = (z - mu) * is;
-      s0 += (double)g;
-      s1 += (double)g * (double)xh;
+      const f32x4 da = ld4(dA + r * N + c);
+      const f32x4 m = mask ? ld4(mask + r * N + c) : f32x4{1.f, 1.f, 1.f, 1.f};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float g = da[j] * bn_elu_grad(z[j], sc[j], sh[j]) * m[j];
+        const float xh = (z[j] - mu[j]) * is[j];
+        s0[j] += (double)g;
+        s1[j] += (double)g * (double)xh;
+      }
     }
+  };
+  if (cin) {
+    int64_t r = r0 + rg;
+    for (; r + 3 * RG < r1; r += 4 * RG) {
+      term(r);
+      term(r + RG);
+      term(r + 2 * RG);
+      term(r + 3 * RG);
+    }
+    for (; r < r1; r += RG) term(r);
   }
-  red[0][wave][lane] = s0;
-  red[1][wave][lane] = s1;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    red[0][rg][4 * li + j] = s0[j];
+    red[1][rg][4 * li + j] = s1[j];
+  }
   __syncthreads();
-  if (wave == 0 && c < N) {
-    const double t0 = ((red[0][0][lane] + red[0][1][lane]) + red[0][2][lane]) + red[0][3][lane];
-    const double t1 = ((red[1][0][lane] + red[1][1][lane]) + red[1][2][lane]) + red[1][3][lane];
-    part[(int64_t)blockIdx.x * 2 * N + c] = t0;
-    part[(int64_t)blockIdx.x * 2 * N + N + c] = t1;
+  if (threadIdx.x < 256) {  // 2 x 128 outputs: (sum kind, column), row groups in fixed order
+    const int k = threadIdx.x >> 7, cl = threadIdx.x & 127;
+    const int cc = blockIdx.y * 128 + cl;
+    double t = red[k][0][cl];
+#pragma unroll
+    for (int g = 1; g < RG; ++g) t += red[k][g][cl];
+    if (cc < N) part[(int64_t)blockIdx.x * 2 * N + k * N + cc] = t;
   }
 }
 
-// sums[2N] = sum over P partials in block order
+// sums[2N] = sum over P partials: RED_SPLIT strided groups per output (four loads in flight
+// each), combined in group order
 __global__ __launch_bounds__(NT) void k_colsum_reduce(const double* __restrict__ part, int P,
                                                       int N2, double* __restrict__ sums) {
-  const int i = blockIdx.x * NT + threadIdx.x;
-  if (i >= N2) return;
+  __shared__ double red[RED_SPLIT][NT / RED_SPLIT];
+  const int o = blockIdx.x * (NT / RED_SPLIT) + (threadIdx.x % (NT / RED_SPLIT));
+  const int g = threadIdx.x / (NT / RED_SPLIT);
   double s = 0.0;
-  for (int p = 0; p < P; ++p) s += part[(int64_t)p * N2 + i];
-  sums[i] = s;
+  if (o < N2) {
+    int p = g;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    for (; p + 3 * RED_SPLIT < P; p += 4 * RED_SPLIT) {
+      a0 += part[(int64_t)p * N2 + o];
+      a1 += part[(int64_t)(p + RED_SPLIT) * N2 + o];
+      a2 += part[(int64_t)(p + 2 * RED_SPLIT) * N2 + o];
+      a3 += part[(int64_t)(p + 3 * RED_SPLIT) * N2 + o];
+    }
+    for (; p < P; p += RED_SPLIT) a0 += part[(int64_t)p * N2 + o];
+    s = (a0 + a1) + (a2 + a3);
+  }
+  red[g][threadIdx.x % (NT / RED_SPLIT)] = s;
+  __syncthreads();
+  if (g == 0 && o < N2) {
+    double t = red[0][threadIdx.x];
+#pragma unroll
+    for (int k = 1; k < RED_SPLIT; ++k) t += red[k][threadIdx.x];
+    sums[o] = t;
+  }
 }
 
 // Per-column constants. training: batch mean / biased var from sums (count rows), running stats
@@ -128,22 +178,23 @@ __global__ __launch_bounds__(NT) void k_bn_finalize(const double* __restrict__ s
   shift[c] = (beta ? beta[c] : 0.f) - m * sc;
 }
 
-// A = ELU(Z * scale + shift) [* mask]
+// A = ELU(Z * scale + shift) [* mask]; per-column constants in registers (thread mapping above)
 __global__ __launch_bounds__(NT) void k_bn_act(const float* __restrict__ Z, int64_t M, int N,
                                                const float* __restrict__ scale,
                                                const float* __restrict__ shift,
                                                const float* __restrict__ mask,
                                                float* __restrict__ A) {
-  const int64_t n4 = M * N / 4;
-  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n4;
-       i += (int64_t)gridDim.x * NT) {
-    const int c = (int)((i * 4) % N);
-    f32x4 z = ld4(Z + 4 * i);
+  const int li = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int c = blockIdx.y * 128 + 4 * li;
+  if (c >= N) return;
+  const f32x4 sc = ld4(scale + c), sh = ld4(shift + c);
+  for (int64_t r = (int64_t)blockIdx.x * RG + rg; r < M; r += (int64_t)gridDim.x * RG) {
+    const f32x4 z = ld4(Z + r * N + c);
     f32x4 o;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = elu_f(fmaf(z[j], scale[c + j], shift[c + j]));
-    if (mask) o *= ld4(mask + 4 * i);
-    st4(A + 4 * i, o);
+    for (int j = 0; j < 4; ++j) o[j] = elu_f(fmaf(z[j], sc[j], sh[j]));
+    if (mask) o *= ld4(mask + r * N + c);
+    st4(A + r * N + c, o);
   }
 }
 
@@ -160,29 +211,34 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply(const float* __restrict__ d
                                                      const double* __restrict__ sums,
                                                      double count, int training,
                                                      float* __restrict__ dZ) {
-  const int64_t n4 = M * N / 4;
-  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n4;
-       i += (int64_t)gridDim.x * NT) {
-    const int c = (int)((i * 4) % N);
-    const f32x4 z = ld4(Z + 4 * i);
-    const f32x4 da = ld4(dA + 4 * i);
-    f32x4 m = {1.f, 1.f, 1.f, 1.f};
-    if (mask) m = ld4(mask + 4 * i);
+  const int li = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int c = blockIdx.y * 128 + 4 * li;
+  if (c >= N) return;
+  const f32x4 sc = ld4(scale + c), sh = ld4(shift + c), mu = ld4(mean + c), is = ld4(invstd + c);
+  f32x4 mg = {}, mgx = {};
+  if (training) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      mg[j] = (float)(sums[c + j] / count);
+      mgx[j] = (float)(sums[N + c + j] / count);
+    }
+  }
+  for (int64_t r = (int64_t)blockIdx.x * RG + rg; r < M; r += (int64_t)gridDim.x * RG) {
+    const f32x4 z = ld4(Z + r * N + c);
+    const f32x4 da = ld4(dA + r * N + c);
+    const f32x4 m = mask ? ld4(mask + r * N + c) : f32x4{1.f, 1.f, 1.f, 1.f};
     f32x4 o;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int cj = c + j;
-      const float g = da[j] * bn_elu_grad(z[j], scale[cj], shift[cj]) * m[j];
+      const float g = da[j] * bn_elu_grad(z[j], sc[j], sh[j]) * m[j];
       if (training) {
-        const float mg = (float)(sums[cj] / count);
-        const float mgx = (float)(sums[N + cj] / count);
-        const float xh = (z[j] - mean[cj]) * invstd[cj];
-        o[j] = scale[cj] * (g - mg - xh * mgx);
+        const float xh = (z[j] - mu[j]) * is[j];
+        o[j] = sc[j] * (g - mg[j] - xh * mgx[j]);
       } else {
-        o[j] = scale[cj] * g;
+        o[j] = sc[j] * g;
       }
     }
-    st4(dZ + 4 * i, o);
+    st4(dZ + r * N + c, o);
   }
 }
 
@@ -195,10 +251,11 @@ __global__ void k_bn_param_grads(const double* __restrict__ sums, int N, float* 
   if (db) db[c] = (float)sums[c];
 }
 
-inline unsigned ew_grid(int64_t n4) {
-  int64_t g = (n4 + NT - 1) / NT;
-  if (g > 4096) g = 4096;
-  return (unsigned)(g < 1 ? 1 : g);
+// elementwise grid: row blocks of RG rows (capped), x 128-column chunks
+inline dim3 ew_grid(int64_t M, int N) {
+  int64_t g = (M + RG - 1) / RG;
+  if (g > 2048) g = 2048;
+  return dim3((unsigned)(g < 1 ? 1 : g), (unsigned)((N + 127) / 128));
 }
 
 }  // namespace
@@ -209,16 +266,16 @@ extern "C" size_t lgnn_bn_workspace_bytes(int64_t M, int N) {
 
 extern "C" int lgnn_bn_stats(const float* Z, int64_t M, int N, double* sums, void* workspace,
                              size_t workspace_bytes, void* stream) {
-  if (M < 0 || N <= 0 || !sums || (M > 0 && !Z)) return LGNN_EINVAL;
+  if (M < 0 || N <= 0 || (N & 3) || !sums || (M > 0 && !Z)) return LGNN_EINVAL;
   if (!workspace || workspace_bytes < lgnn_bn_workspace_bytes(M, N)) return LGNN_ENOSPC;
   hipStream_t s = as_stream(stream);
   const int P = row_blocks(M);
   double* part = static_cast<double*>(workspace);
-  hipLaunchKernelGGL(k_colsum<0>, dim3(P, (N + 63) / 64), dim3(NT), 0, s, Z, nullptr, nullptr, M,
-                     N, nullptr, nullptr, nullptr, nullptr, part);
+  hipLaunchKernelGGL(k_colsum<0>, dim3(P, (N + 127) / 128), dim3(NT), 0, s, Z, nullptr, nullptr,
+                     M, N, nullptr, nullptr, nullptr, nullptr, part);
   LGNN_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_colsum_reduce, dim3((2 * N + NT - 1) / NT), dim3(NT), 0, s, part, P, 2 * N,
-                     sums);
+  hipLaunchKernelGGL(k_colsum_reduce, dim3((2 * N + NT / RED_SPLIT - 1) / (NT / RED_SPLIT)),
+                     dim3(NT), 0, s, part, P, 2 * N, sums);
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
 }
@@ -244,8 +301,8 @@ extern "C" int lgnn_bn_act(const float* Z, int64_t M, int N, const float* scale,
   if (M < 0 || N <= 0 || (N & 3) || !scale || !shift || (M > 0 && (!Z || !A)))
     return LGNN_EINVAL;
   if (M == 0) return LGNN_OK;
-  hipLaunchKernelGGL(k_bn_act, dim3(ew_grid(M * N / 4)), dim3(NT), 0, as_stream(stream), Z, M, N,
-                     scale, shift, mask, A);
+  hipLaunchKernelGGL(k_bn_act, ew_grid(M, N), dim3(NT), 0, as_stream(stream), Z, M, N, scale,
+                     shift, mask, A);
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
 }
@@ -254,17 +311,18 @@ extern "C" int lgnn_bn_bwd_stats(const float* dA, const float* Z, const float* m
                                  int N, const float* scale, const float* shift, const float* mean,
                                  const float* invstd, double* sums, void* workspace,
                                  size_t workspace_bytes, void* stream) {
-  if (M < 0 || N <= 0 || !sums || !scale || !shift || !mean || !invstd) return LGNN_EINVAL;
+  if (M < 0 || N <= 0 || (N & 3) || !sums || !scale || !shift || !mean || !invstd)
+    return LGNN_EINVAL;
   if (M > 0 && (!dA || !Z)) return LGNN_EINVAL;
   if (!workspace || workspace_bytes < lgnn_bn_workspace_bytes(M, N)) return LGNN_ENOSPC;
   hipStream_t s = as_stream(stream);
   const int P = row_blocks(M);
   double* part = static_cast<double*>(workspace);
-  hipLaunchKernelGGL(k_colsum<1>, dim3(P, (N + 63) / 64), dim3(NT), 0, s, Z, dA, mask, M, N,
+  hipLaunchKernelGGL(k_colsum<1>, dim3(P, (N + 127) / 128), dim3(NT), 0, s, Z, dA, mask, M, N,
                      scale, shift, mean, invstd, part);
   LGNN_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_colsum_reduce, dim3((2 * N + NT - 1) / NT), dim3(NT), 0, s, part, P, 2 * N,
-                     sums);
+  hipLaunchKernelGGL(k_colsum_reduce, dim3((2 * N + NT / RED_SPLIT - 1) / (NT / RED_SPLIT)),
+                     dim3(NT), 0, s, part, P, 2 * N, sums);
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
 }
@@ -280,8 +338,8 @@ extern "C" int lgnn_bn_bwd_apply(const float* dA, const float* Z, const float* m
   hipStream_t s = as_stream(stream);
   if (M > 0) {
     if (!dA || !Z || !dZ) return LGNN_EINVAL;
-    hipLaunchKernelGGL(k_bn_bwd_apply, dim3(ew_grid(M * N / 4)), dim3(NT), 0, s, dA, Z, mask, M,
-                       N, scale, shift, mean, invstd, sums, count, training, dZ);
+    hipLaunchKernelGGL(k_bn_bwd_apply, ew_grid(M, N), dim3(NT), 0, s, dA, Z, mask, M, N, scale,
+                       shift, mean, invstd, sums, count, training, dZ);
     LGNN_LAUNCH_CHECK();
   }
   if (dgamma || dbeta) {
