@@ -440,8 +440,8 @@ class _DenseLinear(torch.autograd.Function):
     def forward(ctx, x, W, b, bf16):
         _lib.require_gpu(x, W)
         x, W = _f32c(x), _f32c(W)
-        if bf16:  # rounded once; the backward's dW reuses the bf16 copy
-            x = x.to(torch.bfloat16)
+        if bf16:  # each operand rounded once; the backward reuses the bf16 copies
+            x, W = x.to(torch.bfloat16), W.to(torch.bfloat16)
         y = mm_dense(x, W.t(), bf16)
         if b is not None:
             y += b
@@ -453,8 +453,10 @@ class _DenseLinear(torch.autograd.Function):
     def backward(ctx, dy):
         x, W = ctx.saved_tensors
         dy = _f32c(dy)
-        dW = dw_dense(dy, x, ctx.bf16)
         db = dy.sum(0) if ctx.has_b else None
+        if ctx.bf16:  # dy rounded once for both products
+            dy = dy.to(torch.bfloat16)
+        dW = dw_dense(dy, x, ctx.bf16)
         dx = mm_dense(dy, W, ctx.bf16) if ctx.needs_input_grad[0] else None
         return dx, dW, db, None
 
@@ -842,7 +844,11 @@ class _GATConv(torch.autograd.Function):
         C = HC // heads
         dev = x.device
         dense = bf16 or not fast_shape(W.size(1), HC)
-        XP = mm_dense(x, W.t(), bf16) if dense else linear_fwd(x, W, None, _lib.LGNN_ACT_NONE)
+        if bf16:  # GEMM operands rounded once; the backward reuses the bf16 copies
+            xg, Wg = x.to(torch.bfloat16), W.to(torch.bfloat16)
+        else:
+            xg, Wg = x, W
+        XP = mm_dense(xg, Wg.t(), bf16) if dense else linear_fwd(x, W, None, _lib.LGNN_ACT_NONE)
         a_s = torch.empty(M, heads, dtype=torch.float32, device=dev)
         a_d = torch.empty(M, heads, dtype=torch.float32, device=dev)
         _lib.call("lgnn_gat_att", _lib.ptr(XP), M, heads, C, _lib.ptr(att_src), _lib.ptr(att_dst),
@@ -853,7 +859,7 @@ class _GATConv(torch.autograd.Function):
         _lib.call("lgnn_gat_fwd", _lib.ptr(csr.rowptr), _lib.ptr(csr.col), _lib.ptr(XP),
                   _lib.ptr(a_s), _lib.ptr(a_d), M, heads, C, float(slope), _lib.ptr(mask),
                   _lib.ptr(bias), act, _lib.ptr(alpha), _lib.ptr(Y), _s(dev))
-        ctx.save_for_backward(x, W, att_src, att_dst, XP, a_s, a_d, alpha, Y, mask)
+        ctx.save_for_backward(xg, Wg, att_src, att_dst, XP, a_s, a_d, alpha, Y, mask)
         ctx.graph, ctx.heads, ctx.slope, ctx.act = graph, heads, slope, act
         ctx.bf16, ctx.dense = bf16, dense
         ctx.has_bias = bias is not None
@@ -886,8 +892,9 @@ class _GATConv(torch.autograd.Function):
         _lib.call("lgnn_reduce_partials", _lib.ptr(part), P, 3 * HC, _lib.ptr(red), _s(dev))
         want_dx = ctx.needs_input_grad[0]
         if ctx.dense:
-            dW = dw_dense(dXP, x, ctx.bf16)
-            dx = mm_dense(dXP, W, ctx.bf16) if want_dx else None
+            dg = dXP.to(torch.bfloat16) if ctx.bf16 else dXP  # rounded once for both
+            dW = dw_dense(dg, x, ctx.bf16)
+            dx = mm_dense(dg, W, ctx.bf16) if want_dx else None
         else:
             dx, dW, _ = linear_bwd(_lib.LGNN_GRAD_DIRECT, dXP, H=None, act=_lib.LGNN_ACT_NONE,
                                    X=x, W=W, want_dx=want_dx, want_db=False)
