@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 10
+#define LGNN_ABI_VERSION 11
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -185,6 +185,13 @@ int lgnn_reduce_partials(const float* partial, int num_partials, int64_t len, fl
 /* The same for n <= 16 independent slabs in one launch (host arrays of n entries). */
 int lgnn_reduce_partials_multi(int n, const float* const* partials, const int* num_partials,
                                const int64_t* len, float* const* out, void* stream);
+/* lgnn_reduce_partials_multi + outer-product jobs: where factor[j] is set (factor / width may be
+ * NULL for none), out_j[c * width_j + d] = sum_{p < P_j} partials_j[p * (len_j / width_j) + c] *
+ * factor_j[p * width_j + d] (fixed order). One such job is out_proj's weight gradient
+ * dW_out = dlogits^T pooled, queued with the stack's slab reductions. */
+int lgnn_reduce_jobs(int n, const float* const* partials, const float* const* factor,
+                     const int* width, const int* num_partials, const int64_t* len,
+                     float* const* out, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Sparse aggregation alone (no linear): Y_i = self_scale*X_i + sum_{e in row i} w_e X[col_e].
@@ -414,7 +421,10 @@ int lgnn_gcn_stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t*
  *   device pointers) + S (host array of L pointers: S[l - 1] [M][K_l] receives Â H_{l-1} of the
  *   open tiles, read by the backward's open phase).
  * lgnn_gcn_stack_bwd_s3f_all = lgnn_gcn_stack_bwd_s3f + the transpose CSR (tptr / tidx / tw),
- *   W, S (as above) and dS_ws (2 * M * 128 floats of workspace).
+ *   W, S (as above) and dS_ws (2 * M * 128 floats of workspace); with dlogits [B][C] and Wout
+ *   [C][N_L] (C <= 8) the pooled-output gradient dP = dlogits Wout (out_proj backward) is formed
+ *   inside the kernel and dP may be NULL (lgnn_pool_head_bwd then only needs dWout / dbout, and
+ *   can run concurrently).
  * ------------------------------------------------------------------------------------------- */
 int lgnn_gcn_stack_fwd_s3_all(const float* X, int64_t M, int d_in, int has_in_proj,
                               const int32_t* rowptr, const int32_t* col, const float* w, int L,
@@ -428,7 +438,8 @@ int lgnn_gcn_stack_bwd_s3f_all(const float* dP, const int64_t* batch, const int3
                                int L, const uint16_t* planes_t, const float* const* W,
                                const float* const* H, const float* const* S, const int* widths,
                                float* const* dWp, float* const* dbp, int num_partials,
-                               float* dS_ws, int32_t* tile_open, void* stream);
+                               float* dS_ws, int32_t* tile_open, const float* dlogits,
+                               const float* Wout, int num_classes, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Sort pooling (DGCNN). Replaces: PyG 2.5.1 SortAggregation(k) as DRGNet applies it to the

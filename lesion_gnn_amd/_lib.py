@@ -49,6 +49,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_gcn_stack_bwd": (I32, [P, P, P, I32, P, P, P, P, I64, I32, P, P, P, P, P, I32, P, P]),
     "lgnn_spmm": (I32, [P, P, P, F32, P, I64, I32, P, P]),
     "lgnn_reduce_partials_multi": (I32, [I32, P, P, P, P, P]),
+    "lgnn_reduce_jobs": (I32, [I32, P, P, P, P, P, P, P]),
     "lgnn_ce_fwd": (I32, [P, P, P, I64, I32, P, P, P, P, P]),
     "lgnn_ce_bwd": (I32, [P, P, P, I64, I32, P, P, P, P, P]),
     "lgnn_pool_head_fwd": (I32, [P, P, I64, I32, I32, P, P, I32, P, P, P]),
@@ -83,7 +84,7 @@ SIGNATURES: dict[str, tuple] = {
                                      I32, P, P]),
     "lgnn_gcn_stack_fwd_s3_all": (I32, [P, I64, I32, I32, P, P, P, I32, P, P, P, P, P, P, P, P]),
     "lgnn_gcn_stack_bwd_s3f_all": (I32, [P, P, P, I32, I64, P, P, P, P, P, P, P, I64, I32, P, P, P,
-                                         P, P, P, P, I32, P, P, P]),
+                                         P, P, P, P, I32, P, P, P, P, I32, P]),
     "lgnn_sort_pool_workspace_bytes": (SZ, []),
     "lgnn_sort_pool_fwd": (I32, [P, I64, I32, P, I64, I32, P, P, P, P, SZ, P]),
     "lgnn_sort_pool_bwd": (I32, [P, P, P, P, P, I64, I32, I32, P, P]),
@@ -91,7 +92,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 _lib = None
 

@@ -79,12 +79,16 @@ __global__ __launch_bounds__(256) void k_ce_bwd(const float* __restrict__ z,
   dz[idx] = gloss[0] * wt / wsum[0] * (p - (c == t ? 1.f : 0.f));
 }
 
-// job j: out_j[i] = sum_{p < P_j} part_j[p * len_j + i] in slot order (as lgnn_reduce_partials)
+// job j: out_j[i] = sum_{p < P_j} part_j[p * len_j + i] in slot order (as lgnn_reduce_partials);
+// with a factor (outer-product job): out_j[c * width_j + d] =
+//   sum_p part_j[p * (len_j / width_j) + c] * factor_j[p * width_j + d]
 struct ReduceJobs {
   const float* part[LGNN_MAX_REDUCE];
+  const float* factor[LGNN_MAX_REDUCE];
   float* out[LGNN_MAX_REDUCE];
   int64_t len[LGNN_MAX_REDUCE];
   int P[LGNN_MAX_REDUCE];
+  int width[LGNN_MAX_REDUCE];
 };
 
 constexpr int RT = 1024;
@@ -94,12 +98,28 @@ __global__ __launch_bounds__(RT) void k_reduce_multi(ReduceJobs jobs) {
   const int64_t len = jobs.len[j];
   if ((int64_t)blockIdx.x * 64 >= len) return;
   const float* __restrict__ part = jobs.part[j];
-  const int P = jobs.P[j];
+  int P = jobs.P[j];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t i = (int64_t)blockIdx.x * 64 + lane;
   const int64_t ic = i < len ? i : len - 1;
   float s = 0.f;
   int p = wave;
+  if (const float* __restrict__ f = jobs.factor[j]) {  // sum_p part[p][c] * f[p][d]
+    const int width = jobs.width[j];
+    const int64_t rows = len / width, c = ic / width, d = ic % width;
+    for (; p + 16 * 15 < P; p += 16 * 16) {  // 32 loads in flight per lane (latency bound)
+      float av[16], fv[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        av[u] = part[(int64_t)(p + 16 * u) * rows + c];
+        fv[u] = f[(int64_t)(p + 16 * u) * width + d];
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s = fmaf(av[u], fv[u], s);
+    }
+    for (; p < P; p += 16) s = fmaf(part[(int64_t)p * rows + c], f[(int64_t)p * width + d], s);
+    P = 0;  // fall through to the fixed-order wave fold
+  }
   for (; p + 48 < P; p += 64) {
     const float v0 = part[(int64_t)p * len + ic], v1 = part[(int64_t)(p + 16) * len + ic];
     const float v2 = part[(int64_t)(p + 32) * len + ic], v3 = part[(int64_t)(p + 48) * len + ic];
@@ -147,12 +167,23 @@ extern "C" int lgnn_ce_bwd(const float* logits, const int64_t* target, const flo
 extern "C" int lgnn_reduce_partials_multi(int n, const float* const* partials,
                                           const int* num_partials, const int64_t* len,
                                           float* const* out, void* stream) {
+  return lgnn_reduce_jobs(n, partials, nullptr, nullptr, num_partials, len, out, stream);
+}
+
+extern "C" int lgnn_reduce_jobs(int n, const float* const* partials, const float* const* factor,
+                                const int* width, const int* num_partials, const int64_t* len,
+                                float* const* out, void* stream) {
   if (n <= 0 || n > LGNN_MAX_REDUCE || !partials || !num_partials || !len || !out)
     return LGNN_EINVAL;
   ReduceJobs jobs = {};
   int64_t maxlen = 0;
   for (int j = 0; j < n; ++j) {
     if (!partials[j] || !out[j] || num_partials[j] <= 0 || len[j] < 0) return LGNN_EINVAL;
+    if (factor && factor[j]) {
+      if (!width || width[j] <= 0 || len[j] % width[j] != 0) return LGNN_EINVAL;
+      jobs.factor[j] = factor[j];
+      jobs.width[j] = width[j];
+    }
     jobs.part[j] = partials[j];
     jobs.out[j] = out[j];
     jobs.len[j] = len[j];

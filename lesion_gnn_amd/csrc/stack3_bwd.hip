@@ -493,7 +493,10 @@ namespace lgnn_s3 {
 #endif
 
 struct FBwdArgs {
-  const float* dP;                // [B][N_L] pooled-output gradient
+  const float* dP;                // [B][N_L] pooled-output gradient (or formed from dlog / Wout)
+  const float* dlog;              // [B][C] logits gradient (nullable): dP = dlog Wout on the fly
+  const float* Wout;              // [C][N_L]
+  int C;
   const int64_t* batch;
   const int32_t* gptr;
   int pool_mean;
@@ -520,6 +523,8 @@ struct OpenBwdArgs {
   int32_t* sync;                   // grid-barrier words (nullptr: no open phase)
 };
 
+constexpr int kMaxHeadC = 8;  // classes for which dP is formed in the kernel
+
 struct FBwdSmem {
   unsigned char Img[3][TM * AROW];  // 48 KiB: H_{l-1} (or X) feature-major [k][perm16 m]
   unsigned char Gt[3][TM * AROW];   // 48 KiB: G node-major [m][perm16 n]
@@ -528,6 +533,7 @@ struct FBwdSmem {
   int pg[TM];
   int rp[TM + 1];
   int flag;
+  __attribute__((aligned(16))) float dl[TM][kMaxHeadC];  // dlog rows of the tile's graphs, pre-scaled by pscale
 };
 
 template <int NL>
@@ -574,8 +580,16 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
         const int64_t row = r0 + tq;
         const int64_t g = row < M ? a.batch[row] : 0;
         const int cnt = a.gptr[g + 1] - a.gptr[g];
+        const float ps = row >= M ? 0.f : (a.pool_mean && cnt > 1 ? 1.f / (float)cnt : 1.f);
         sm.pg[tq] = (int)g;
-        sm.pscale[tq] = row >= M ? 0.f : (a.pool_mean && cnt > 1 ? 1.f / (float)cnt : 1.f);
+        sm.pscale[tq] = ps;
+        if (a.dlog) {  // zero-padded to kMaxHeadC: the dZ_L loop below runs without branches
+          float v[kMaxHeadC];
+#pragma unroll
+          for (int c = 0; c < kMaxHeadC; ++c) v[c] = c < a.C ? a.dlog[g * a.C + c] * ps : 0.f;
+          st4(&sm.dl[tq][0], f32x4{v[0], v[1], v[2], v[3]});
+          st4(&sm.dl[tq][4], f32x4{v[4], v[5], v[6], v[7]});
+        }
       }
     }
     lds_barrier();
@@ -588,16 +602,36 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
       const int h = (tq >> 5) & 1, n = 32 * (tq >> 6) + (tq & 31);
       f32x16 hv[2];
       load_pt(hv, a.H[L], M, r0, NLast, n, NLast, h);
+      if (a.dlog) {  // dP[g][n] = sum_c dlog[g][c] Wout[c][n], dlog rows staged (scaled) in LDS
+        float wo[kMaxHeadC];
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
+        for (int c = 0; c < kMaxHeadC; ++c)
+          wo[c] = (c < a.C && n < NLast) ? a.Wout[c * NLast + n] : 0.f;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
-          const int off = n < NLast ? (sm.pg[m] * NLast + n) * 4 : INT32_MAX - 3;
-          const float gv =
-              __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(bP, off, 0, 0));
-          dz[q][r] = gv * sm.pscale[m] * elu_grad_from_out(hv[q][r]);
-        }
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const f32x4 d0 = ld4(&sm.dl[m][0]), d1 = ld4(&sm.dl[m][4]);
+            float gv = d0[0] * wo[0];
+#pragma unroll
+            for (int c = 1; c < 4; ++c) gv = fmaf(d0[c], wo[c], gv);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) gv = fmaf(d1[c], wo[4 + c], gv);
+            dz[q][r] = gv * elu_grad_from_out(hv[q][r]);
+          }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int off = n < NLast ? (sm.pg[m] * NLast + n) * 4 : INT32_MAX - 3;
+            const float gv =
+                __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(bP, off, 0, 0));
+            dz[q][r] = gv * sm.pscale[m] * elu_grad_from_out(hv[q][r]);
+          }
+      }
     }
     lds_barrier();  // Â^T summed
     {
@@ -898,7 +932,8 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
       if (l == L)
         bwd_tiles<LGNN_GRAD_POOL, LGNN_ACT_ELU, true>(
             lw.A, lw.C, lw.ti, a.dP, a.batch, a.gptr, a.pool_mean, nullptr, nullptr, nullptr, 0.f,
-            a.H[l], Sx, M, K, o.W[l], N, o.dS[l & 1], a.dWp[l], a.dbp[l], tmask, 1, 1);
+            a.H[l], Sx, M, K, o.W[l], N, o.dS[l & 1], a.dWp[l], a.dbp[l], tmask, 1, 1, a.dlog,
+            a.Wout, a.C);
       else if (l >= 1)
         bwd_tiles<LGNN_GRAD_TRANSPOSE, LGNN_ACT_ELU, true>(
             lw.A, lw.C, lw.ti, o.dS[(l + 1) & 1], a.batch, a.gptr, a.pool_mean, o.tptr, o.tidx,
@@ -920,7 +955,9 @@ static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* g
                          const int32_t* col, const float* w, const float* X, int64_t M, int L,
                          const uint16_t* planes_t, const float* const* H, const int* widths,
                          float* const* dWp, float* const* dbp, int num_partials,
-                         const int32_t* tile_open, const lgnn_s3::OpenBwdArgs& o, void* stream);
+                         const int32_t* tile_open, const lgnn_s3::OpenBwdArgs& o, void* stream,
+                         const float* dlogits = nullptr, const float* Wout = nullptr,
+                         int num_classes = 0);
 
 extern "C" int lgnn_gcn_stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* gptr,
                                       int pool_mean, int64_t num_graphs, const int32_t* rowptr,
@@ -940,8 +977,11 @@ extern "C" int lgnn_gcn_stack_bwd_s3f_all(
     const int32_t* tptr, const int32_t* tidx, const float* tw, const float* X, int64_t M, int L,
     const uint16_t* planes_t, const float* const* W, const float* const* H,
     const float* const* S, const int* widths, float* const* dWp, float* const* dbp,
-    int num_partials, float* dS_ws, int32_t* tile_open, void* stream) {
+    int num_partials, float* dS_ws, int32_t* tile_open, const float* dlogits, const float* Wout,
+    int num_classes, void* stream) {
   if (M < 0 || L < 1 || L > 2 || !W || !S || !tptr || !tidx || !tw || !dS_ws || !tile_open)
+    return LGNN_EINVAL;
+  if (dlogits && (!Wout || num_classes < 1 || num_classes > lgnn_s3::kMaxHeadC))
     return LGNN_EINVAL;
   lgnn_s3::OpenBwdArgs o = {};
   for (int l = 0; l <= L; ++l) {
@@ -957,7 +997,8 @@ extern "C" int lgnn_gcn_stack_bwd_s3f_all(
   const int64_t ntiles = (M + lgnn_tile::TM - 1) / lgnn_tile::TM;
   o.sync = tile_open + ntiles + 4;
   return stack_bwd_s3f(dP, batch, gptr, pool_mean, num_graphs, rowptr, col, w, X, M, L, planes_t,
-                       H, widths, dWp, dbp, num_partials, tile_open, o, stream);
+                       H, widths, dWp, dbp, num_partials, tile_open, o, stream, dlogits, Wout,
+                       num_classes);
 }
 
 static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* gptr,
@@ -965,13 +1006,17 @@ static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* g
                          const int32_t* col, const float* w, const float* X, int64_t M, int L,
                          const uint16_t* planes_t, const float* const* H, const int* widths,
                          float* const* dWp, float* const* dbp, int num_partials,
-                         const int32_t* tile_open, const lgnn_s3::OpenBwdArgs& o, void* stream) {
-  if (M < 0 || L < 1 || L > 2 || !dP || !batch || !gptr || !rowptr || !col || !X || !planes_t ||
-      !H || !widths || !dWp || !dbp || !tile_open || num_graphs < 0)
+                         const int32_t* tile_open, const lgnn_s3::OpenBwdArgs& o, void* stream,
+                         const float* dlogits, const float* Wout, int num_classes) {
+  if (M < 0 || L < 1 || L > 2 || !(dP || dlogits) || !batch || !gptr || !rowptr || !col || !X ||
+      !planes_t || !H || !widths || !dWp || !dbp || !tile_open || num_graphs < 0)
     return LGNN_EINVAL;
   if (num_partials != lgnn_gcn_stack_bwd_partials(M)) return LGNN_EINVAL;
   lgnn_s3::FBwdArgs a = {};
   a.dP = dP;
+  a.dlog = dlogits;
+  a.Wout = Wout;
+  a.C = num_classes;
   a.batch = batch;
   a.gptr = gptr;
   a.pool_mean = pool_mean;

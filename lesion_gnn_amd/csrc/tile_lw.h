@@ -202,7 +202,11 @@ __device__ __forceinline__ void bwd_tiles(
     const int32_t* __restrict__ tidx, const float* __restrict__ tw, float tself,
     const float* __restrict__ H, const float* __restrict__ X, int64_t M, int K,
     const float* __restrict__ W, int N, float* __restrict__ dXpre, float* __restrict__ dWp,
-    float* __restrict__ dbp, const int32_t* __restrict__ tmask, int want, int accumulate) {
+    float* __restrict__ dbp, const int32_t* __restrict__ tmask, int want, int accumulate,
+    const float* __restrict__ dlog = nullptr, const float* __restrict__ Wout = nullptr,
+    int nclass = 0) {
+  // GRAD_POOL with dlog: the pooled-output gradient is formed on the fly from the logits'
+  // gradient, dP[g][n] = sum_c dlog[g][c] Wout[c][n] (out_proj backward, nclass classes)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, li = lane & 31, hw = wave * 2 + h;
   const int64_t ntiles = (M + TM - 1) / TM;
@@ -292,7 +296,14 @@ __device__ __forceinline__ void bwd_tiles(
           g[it] = ld4(dY + rc * N + oc);
         } else {
           const int64_t gi = batch[rc];
-          g[it] = ld4(dY + gi * N + oc);
+          if (dlog) {
+            f32x4 acc = zero4();
+            for (int c = 0; c < nclass; ++c)
+              acc += dlog[gi * nclass + c] * ld4(Wout + (int64_t)c * N + oc);
+            g[it] = acc;
+          } else {
+            g[it] = ld4(dY + gi * N + oc);
+          }
           if (pool_mean) {
             const int cnt = gptr[gi + 1] - gptr[gi];
             g[it] = g[it] / (float)(cnt > 0 ? cnt : 1);

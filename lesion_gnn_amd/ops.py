@@ -93,6 +93,9 @@ BWD_S3 = BWD_MODE in ("s3", "s3f")
 # "0" force it (also "fwd" / "bwd" for one direction).
 OPEN_IN_FUSED = os.environ.get("LGNN_OPEN_IN_FUSED", "auto")
 OPEN_IN_FUSED_BWD = OPEN_IN_FUSED
+# dP = dlogits W_out formed inside the single-launch split-3 backward (LGNN_HEAD_FOLD=0: by
+# lgnn_pool_head_bwd before it)
+HEAD_FOLD = os.environ.get("LGNN_HEAD_FOLD", "1") != "0"
 
 
 def _open_in_fused(mode, graph: Graph, direction: str) -> bool:
@@ -172,13 +175,21 @@ def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list, keep: dict | No
     return hs, ss
 
 
-def stack_bwd(dp: torch.Tensor, x: torch.Tensor, graph: Graph, mean: bool, Ws: list,
-              hs: list, ss: list, reducer: list, planes_t: torch.Tensor | None = None):
+def head_in_stack_bwd(graph: Graph, L: int, C: int, s3: bool) -> bool:
+    """True when stack_bwd's single split-3 launch forms dP = dlogits W_out itself (out_proj
+    backward folded into the kernel's pool prologue, <= 8 classes)."""
+    return (HEAD_FOLD and s3 and BWD_MODE == "s3f" and L <= 2 and C <= 8 and
+            _open_in_fused(OPEN_IN_FUSED_BWD, graph, "bwd"))
+
+
+def stack_bwd(dp: torch.Tensor | None, x: torch.Tensor, graph: Graph, mean: bool, Ws: list,
+              hs: list, ss: list, reducer: list, planes_t: torch.Tensor | None = None,
+              head: tuple | None = None):
     """Backward of stack_fwd from the pooled-output gradient dp down to in_proj, L = 1 or 2
     convs, no input gradient. Closed tiles run fused (lgnn_gcn_stack_bwd, one launch); open
     tiles layer by layer (lgnn_node_linear_bwd_tiles, want_open = 1, accumulate = 1) into the
     same partial slots. Returns [(dW_l, db_l)] for l = 0..L; the slab reductions are appended
-    to `reducer`."""
+    to `reducer`. head = (dlogits, W_out) replaces dp where head_in_stack_bwd() allows."""
     csr = graph.csr("gcn")
     open_ = graph.tile_open("gcn")
     M = x.size(0)
@@ -201,18 +212,21 @@ def stack_bwd(dp: torch.Tensor, x: torch.Tensor, graph: Graph, mean: bool, Ws: l
         off += P * (nk + n)
     arr = ctypes.c_void_p * (L + 1)
     Sx = [x] + list(ss)
+    dlog, W_out = head if head is not None else (None, None)
+    B = dp.size(0) if dp is not None else dlog.size(0)
     if s3f and _open_in_fused(OPEN_IN_FUSED_BWD, graph, "bwd"):  # one launch, open tiles last
         dS_ws = torch.empty(2 * M * 128, dtype=torch.float32, device=dev)
         _lib.call("lgnn_gcn_stack_bwd_s3f_all", _lib.ptr(dp), _lib.ptr(graph.batch),
-                  _lib.ptr(graph.gptr), int(mean), dp.size(0), _lib.ptr(csr.rowptr),
+                  _lib.ptr(graph.gptr), int(mean), B, _lib.ptr(csr.rowptr),
                   _lib.ptr(csr.col), _lib.ptr(csr.w), _lib.ptr(csr.tptr), _lib.ptr(csr.tidx),
                   _lib.ptr(csr.tw), _lib.ptr(x), M, L, _lib.ptr(planes_t),
                   arr(*[W.data_ptr() for W in Ws]), arr(*[h.data_ptr() for h in hs]),
                   (ctypes.c_void_p * L)(*[t.data_ptr() for t in ss]),
                   (ctypes.c_int * (L + 2))(*widths), arr(*[t.data_ptr() for t in dWp]),
                   arr(*[t.data_ptr() for t in dbp]), P, _lib.ptr(dS_ws), _lib.ptr(open_),
-                  _s(dev))
+                  _lib.ptr(dlog), _lib.ptr(W_out), W_out.size(0) if head else 0, _s(dev))
         return _stack_bwd_outputs(L, widths, dWp, dbp, P, dev, reducer)
+    assert head is None, "dP from the logits gradient only in the single-launch split-3 path"
     if s3f:  # one fused split-3 launch, every layer of a tile in one pass (stack3_bwd.hip)
         _lib.call("lgnn_gcn_stack_bwd_s3f", _lib.ptr(dp), _lib.ptr(graph.batch),
                   _lib.ptr(graph.gptr), int(mean), dp.size(0), _lib.ptr(csr.rowptr),
@@ -306,7 +320,8 @@ def linear_bwd(grad_mode: int, dY: torch.Tensor, *, H: torch.Tensor | None, act:
 
 
 def reduce_multi(jobs: list, dev) -> None:
-    """Deterministic slab reductions [(partials, P, len, out), ...] in one launch per 16."""
+    """Deterministic slab reductions [(partials, P, len, out), ...] in one launch per 16; a job
+    (a, P, len, out, f, width) is the outer-product sum out[c, d] = sum_p a[p, c] f[p, d]."""
     for i in range(0, len(jobs), 16):
         chunk = jobs[i:i + 16]
         n = len(chunk)
@@ -314,7 +329,12 @@ def reduce_multi(jobs: list, dev) -> None:
         nps = (ctypes.c_int * n)(*[j[1] for j in chunk])
         lens = (ctypes.c_int64 * n)(*[j[2] for j in chunk])
         outs = (ctypes.c_void_p * n)(*[j[3].data_ptr() for j in chunk])
-        _lib.call("lgnn_reduce_partials_multi", n, parts, nps, lens, outs, _s(dev))
+        if any(len(j) > 4 for j in chunk):
+            fac = (ctypes.c_void_p * n)(*[j[4].data_ptr() if len(j) > 4 else None for j in chunk])
+            wid = (ctypes.c_int * n)(*[j[5] if len(j) > 4 else 0 for j in chunk])
+            _lib.call("lgnn_reduce_jobs", n, parts, fac, wid, nps, lens, outs, _s(dev))
+        else:
+            _lib.call("lgnn_reduce_partials_multi", n, parts, nps, lens, outs, _s(dev))
 
 
 def spmm_raw(rowptr, col, w, self_scale: float, x: torch.Tensor) -> torch.Tensor:
@@ -590,18 +610,32 @@ class _GCNStack(torch.autograd.Function):
         graph = ctx.graph
         csr = graph.csr("gcn")
         W_out = params[2 + 2 * L]
-        dp, dWo, dbo = pool_head_bwd(_f32c(dlogits), pooled, W_out)
+        dlogits = _f32c(dlogits)
         grads = [None] * len(params)
-        grads[2 + 2 * L], grads[3 + 2 * L] = dWo, dbo
         red: list = []
         s3 = ctx.planes_t is not None
         if ctx.fused and (1 <= L <= 2 or s3) and not ctx.needs_input_grad[0] and FUSED_BWD:
             Ws = [params[2 * l] for l in range(L + 1)]
-            for l, (dW, db) in enumerate(stack_bwd(dp, x, graph, ctx.mean, Ws, hs, ss, red,
-                                                   ctx.planes_t)):
+            if head_in_stack_bwd(graph, L, W_out.size(0), s3):
+                # dP is formed inside the stack kernel; out_proj's gradients (dlogits^T pooled,
+                # column sums of dlogits) join the stack's slab reductions: no head launch
+                C, D = W_out.shape
+                dWo = torch.empty_like(W_out)
+                dbo = torch.empty(C, dtype=torch.float32, device=x.device)
+                red += [(dlogits, dlogits.size(0), C * D, dWo, pooled, D),
+                        (dlogits, dlogits.size(0), C, dbo)]
+                outs = stack_bwd(None, x, graph, ctx.mean, Ws, hs, ss, red, ctx.planes_t,
+                                 head=(dlogits, W_out))
+            else:
+                dp, dWo, dbo = pool_head_bwd(dlogits, pooled, W_out)
+                outs = stack_bwd(dp, x, graph, ctx.mean, Ws, hs, ss, red, ctx.planes_t)
+            grads[2 + 2 * L], grads[3 + 2 * L] = dWo, dbo
+            for l, (dW, db) in enumerate(outs):
                 grads[2 * l], grads[2 * l + 1] = dW, db
             reduce_multi(red, x.device)
             return (None, None, None, None, *grads)
+        dp, dWo, dbo = pool_head_bwd(dlogits, pooled, W_out)
+        grads[2 + 2 * L], grads[3 + 2 * L] = dWo, dbo
         if ctx.fused:  # the fused forward saves no aggregated inputs: S_l = Â H_{l-1}
             ss = [spmm_raw(csr.rowptr, csr.col, csr.w, 0.0, hs[l]) for l in range(L)]
         dS = None

@@ -369,3 +369,33 @@ def test_open_tiles_in_fused_launch(cuda, open_in_fused, monkeypatch):
             torch.testing.assert_close(go[k], gr[k], atol=1e-5, rtol=1e-4,
                                        msg=lambda m: f"{k}: {m}")
     assert torch.equal(results[0][0], results[1][0])
+
+
+@pytest.mark.parametrize("classes,pool", [(5, "mean"), (8, "add"), (12, "mean")])
+def test_head_backward_folded_into_stack(cuda, classes, pool, monkeypatch):
+    """out_proj backward folded into the single split-3 backward launch (dP = dlogits W_out
+    formed in the pool prologue of closed tiles and in the open-tile phase, dW_out / db_out as
+    jobs of the slab reduction; <= 8 classes, 12 falls back to lgnn_pool_head_bwd) and the same
+    step with the fold off: both == the oracle."""
+    from lesion_gnn_amd.graph import Graph
+
+    monkeypatch.setattr(ops, "OPEN_IN_FUSED", "1")
+    monkeypatch.setattr(ops, "OPEN_IN_FUSED_BWD", "1")
+    sizes = [1, 5, 64, 200, 2, 33, 512, 17, 64, 64, 30, 34] * 3
+    b = synth.make_batch(len(sizes), k=6, d_in=128, seed=43, sizes=sizes)
+    b.y = b.y % classes
+    ours, oref = make_pair([128, 128, 128], classes=classes, pool=pool)
+    ours = ours.to(cuda)
+    if ops.BWD_S3:
+        g = Graph(b.edge_index.to(cuda), b.num_nodes, b.batch.to(cuda), b.num_graphs)
+        assert ops.head_in_stack_bwd(g, 2, classes, True) == (classes <= 8)
+    results = []
+    for fold in (True, False):
+        monkeypatch.setattr(ops, "HEAD_FOLD", fold)
+        results.append(run_step(ours, b, cuda, b.num_graphs))
+    lr_, _, gr = run_step(oref, b, "cpu", b.num_graphs)
+    for lo, _, go in results:
+        torch.testing.assert_close(lo, lr_, atol=1e-4, rtol=0)
+        for k in gr:
+            torch.testing.assert_close(go[k], gr[k], atol=1e-5, rtol=1e-4,
+                                       msg=lambda m: f"{k}: {m}")
