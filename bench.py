@@ -248,13 +248,19 @@ def time_dominant_kernels(model, b, dev):
         # the step's backward: the fused split-3 kernel (stack3_bwd.hip), priced against the
         # split-3 peak like the forward
         _, planes_t = ops.weight_planes(Ws, d_in, transposed=True)
+        # the Â^T planes the step's forward hands over (as the step: the backward loads them)
+        adjt = torch.empty(ops.adjt_numel(M), dtype=torch.int16, device=dev) if ops.ADJT else None
+        planes_f, _ = ops.weight_planes(Ws, d_in)
+        _lib.call("lgnn_gcn_stack_fwd_s3", b.x.data_ptr(), M, d_in, 1, csr.rowptr.data_ptr(),
+                  csr.col.data_ptr(), csr.w.data_ptr(), L, planes_f.data_ptr(), bp,
+                  (ctypes.c_int * (L + 1))(*widths[1:]), Hp, open_.data_ptr(), _lib.ptr(adjt), s)
 
         def bwd_s3f():
             _lib.call("lgnn_gcn_stack_bwd_s3f", dP.data_ptr(), g.batch.data_ptr(),
                       g.gptr.data_ptr(), 1, b.num_graphs, csr.rowptr.data_ptr(),
                       csr.col.data_ptr(), csr.w.data_ptr(), b.x.data_ptr(), M, L,
                       planes_t.data_ptr(), Hp, (ctypes.c_int * (L + 2))(*widths), dWp, dbp, P,
-                      open_.data_ptr(), s)
+                      open_.data_ptr(), _lib.ptr(adjt), s)
 
         out.append({"kernel": f"lgnn_s3::k_s3_fbwd<{L + 1}> (fused GCN backward, all layers, "
                               "split-3 bf16 MFMA)",
@@ -268,12 +274,14 @@ def time_dominant_kernels(model, b, dev):
 
     if ops.MFMA_MODE == "s3":
         planes, _ = ops.weight_planes(Ws, d_in)
+        adjt_f = torch.empty(ops.adjt_numel(M), dtype=torch.int16, device=dev) \
+            if ops.BWD_MODE == "s3f" and L <= 2 and ops.ADJT else None
 
-        def fwd():
+        def fwd():  # as in the step: with the Â^T planes for the fused backward when it runs
             _lib.call("lgnn_gcn_stack_fwd_s3", b.x.data_ptr(), M, d_in, 1,
                       csr.rowptr.data_ptr(), csr.col.data_ptr(), csr.w.data_ptr(), L,
                       planes.data_ptr(), bp, (ctypes.c_int * (L + 1))(*widths[1:]), Hp,
-                      open_.data_ptr(), s)
+                      open_.data_ptr(), _lib.ptr(adjt_f), s)
 
         out.append({"kernel": "lgnn_s3::k_s3_fwd<true> (fused GCN forward, all layers, "
                               "split-3 bf16 MFMA)",
@@ -481,16 +489,25 @@ def main():
                 eager_step()
         torch.cuda.current_stream(dev).wait_stream(side)
         opt.zero_grad(set_to_none=True)
-        g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g_fb):
-            fwd_bwd()
-        with torch.cuda.graph(g_opt):
-            opt.step()
+        if world == 1:  # nothing between backward and optimizer: one graph for the whole step
+            g_step = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_step):
+                fwd_bwd()
+                opt.step()
 
-        def step():
-            g_fb.replay()
-            exchange()  # RCCL stays outside the captured graphs
-            g_opt.replay()
+            def step():
+                g_step.replay()
+        else:
+            g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_fb):
+                fwd_bwd()
+            with torch.cuda.graph(g_opt):
+                opt.step()
+
+            def step():
+                g_fb.replay()
+                exchange()  # RCCL stays outside the captured graphs
+                g_opt.replay()
 
     for _ in range(args.warmup):
         step()

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 11
+#define LGNN_ABI_VERSION 12
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -307,11 +307,15 @@ int lgnn_gcn_stack_fwd(const float* X, int64_t M, int d_in, int has_in_proj,
 /* Split-3 variant of lgnn_gcn_stack_fwd: the same math and arguments, the GEMMs on bf16 MFMA at
  * fp32 accuracy — every operand held as three bf16 planes (x = hi + mid + lo to 2^-24) and each
  * product taken as the six plane products that matter (liblgnn stack3.hip). `planes` holds the
- * weights of layers 0..L as written by lgnn_weight_planes (in place of W). L >= 1. */
+ * weights of layers 0..L as written by lgnn_weight_planes (in place of W). L >= 1.
+ * adjt (nullable): ceil(M/64) * LGNN_S3_ADJT_TILE_BYTES bytes; receives, for every closed tile,
+ * the tile's dense fp32 Â (64 x 64, as summed from the CSR block), which
+ * lgnn_gcn_stack_bwd_s3f(_all) then loads instead of rebuilding it (same graph, same tile_open). */
+#define LGNN_S3_ADJT_TILE_BYTES 16384
 int lgnn_gcn_stack_fwd_s3(const float* X, int64_t M, int d_in, int has_in_proj,
                           const int32_t* rowptr, const int32_t* col, const float* w, int L,
                           const uint16_t* planes, const float* const* b, const int* widths,
-                          float* const* H, const int32_t* tile_open, void* stream);
+                          float* const* H, const int32_t* tile_open, void* adjt, void* stream);
 /* Weight planes for the split-3 kernels: nl layers, W[l] [widths[l+1], widths[l]] fp32
  * (torch Linear layout; widths <= 128, multiples of 4) -> planes[l][3][128][128] bf16 (zero
  * padded, feature order perm16), lgnn_weight_planes_bytes(nl) bytes; planes_t (nullable, same
@@ -402,13 +406,16 @@ int lgnn_adam_step(int n, float* const* params, const float* const* grads, float
  *   dWp / dbp: per-layer partial slabs with num_partials = lgnn_gcn_stack_bwd_partials(M)
  *   slots, every slot written (zeros for a workgroup without tiles), so open tiles can be
  *   accumulated afterwards by lgnn_node_linear_bwd_tiles(..., accumulate = 1).
+ *   adjt (nullable): the tile adjacencies the split-3 forward wrote for this graph (its adjt);
+ *   each tile's goes straight into LDS (prefetched during the previous tile) instead of being
+ *   rebuilt from the CSR.
  * ------------------------------------------------------------------------------------------- */
 int lgnn_gcn_stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* gptr,
                            int pool_mean, int64_t num_graphs, const int32_t* rowptr,
                            const int32_t* col, const float* w, const float* X, int64_t M, int L,
                            const uint16_t* planes_t, const float* const* H, const int* widths,
                            float* const* dWp, float* const* dbp, int num_partials,
-                           const int32_t* tile_open, void* stream);
+                           const int32_t* tile_open, const void* adjt, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * The fused GCN stack with its open-tile phase in the same launch (no separate layer-by-layer
@@ -430,7 +437,7 @@ int lgnn_gcn_stack_fwd_s3_all(const float* X, int64_t M, int d_in, int has_in_pr
                               const int32_t* rowptr, const int32_t* col, const float* w, int L,
                               const uint16_t* planes, const float* const* W,
                               const float* const* b, const int* widths, float* const* H,
-                              float* const* S, int32_t* tile_open, void* stream);
+                              float* const* S, int32_t* tile_open, void* adjt, void* stream);
 int lgnn_gcn_stack_bwd_s3f_all(const float* dP, const int64_t* batch, const int32_t* gptr,
                                int pool_mean, int64_t num_graphs, const int32_t* rowptr,
                                const int32_t* col, const float* w, const int32_t* tptr,
@@ -439,7 +446,8 @@ int lgnn_gcn_stack_bwd_s3f_all(const float* dP, const int64_t* batch, const int3
                                const float* const* H, const float* const* S, const int* widths,
                                float* const* dWp, float* const* dbp, int num_partials,
                                float* dS_ws, int32_t* tile_open, const float* dlogits,
-                               const float* Wout, int num_classes, void* stream);
+                               const float* Wout, int num_classes, const void* adjt,
+                               void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Sort pooling (DGCNN). Replaces: PyG 2.5.1 SortAggregation(k) as DRGNet applies it to the

@@ -20,6 +20,7 @@ LGNN_NORM_NONE, LGNN_NORM_GCN = 0, 1
 LGNN_ACT_NONE, LGNN_ACT_ELU = 0, 1
 LGNN_GRAD_DIRECT, LGNN_GRAD_POOL, LGNN_GRAD_TRANSPOSE = 0, 1, 2
 LGNN_TILE_OPEN_EXTRA = 7  # tile_open words after the per-tile flags (count + barrier words)
+LGNN_S3_ADJT_TILE_BYTES = 16384  # lgnn.h: fp32 Â per tile, split-3 forward -> fused backward
 
 P = ctypes.c_void_p
 I32 = ctypes.c_int
@@ -66,7 +67,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_gat_bwd_num_partials": (I32, [I64]),
     "lgnn_gat_bwd_node": (I32, [P, P, P, P, P, P, P, P, P, P, P, I64, I32, I32, P, P, I32, P]),
     "lgnn_gcn_stack_fwd": (I32, [P, I64, I32, I32, P, P, P, I32, P, P, P, P, P, P]),
-    "lgnn_gcn_stack_fwd_s3": (I32, [P, I64, I32, I32, P, P, P, I32, P, P, P, P, P, P]),
+    "lgnn_gcn_stack_fwd_s3": (I32, [P, I64, I32, I32, P, P, P, I32, P, P, P, P, P, P, P]),
     "lgnn_weight_planes_bytes": (SZ, [I32]),
     "lgnn_weight_planes": (I32, [I32, P, P, P, P, P]),
     "lgnn_gcn_stack_bwd_s3_partials": (I32, [I64]),
@@ -81,10 +82,10 @@ SIGNATURES: dict[str, tuple] = {
                                          P]),
     "lgnn_bn_bwd_apply": (I32, [P, P, P, I64, I32, P, P, P, P, P, F64, I32, P, P, P, P]),
     "lgnn_gcn_stack_bwd_s3f": (I32, [P, P, P, I32, I64, P, P, P, P, I64, I32, P, P, P, P, P,
-                                     I32, P, P]),
-    "lgnn_gcn_stack_fwd_s3_all": (I32, [P, I64, I32, I32, P, P, P, I32, P, P, P, P, P, P, P, P]),
+                                     I32, P, P, P]),
+    "lgnn_gcn_stack_fwd_s3_all": (I32, [P, I64, I32, I32, P, P, P, I32, P, P, P, P, P, P, P, P, P]),
     "lgnn_gcn_stack_bwd_s3f_all": (I32, [P, P, P, I32, I64, P, P, P, P, P, P, P, I64, I32, P, P, P,
-                                         P, P, P, P, I32, P, P, P, P, I32, P]),
+                                         P, P, P, P, I32, P, P, P, P, I32, P, P]),
     "lgnn_sort_pool_workspace_bytes": (SZ, []),
     "lgnn_sort_pool_fwd": (I32, [P, I64, I32, P, I64, I32, P, P, P, P, SZ, P]),
     "lgnn_sort_pool_bwd": (I32, [P, P, P, P, P, I64, I32, I32, P, P]),
@@ -92,7 +93,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 _lib = None
 

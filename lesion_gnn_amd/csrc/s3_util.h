@@ -18,6 +18,10 @@ constexpr int PLANE = WP * WP;    // bf16 elements per weight plane
 constexpr int AROW = WP * 2;      // bytes per H-image row (chunk-swizzled, no padding)
 constexpr int ADJ_LD = 72;        // Â plane row stride in bf16 (144 B: conflict-free b128 rows)
 constexpr int ADJ_PLANE = TM * ADJ_LD * 2;  // bytes per Â plane
+// one tile's fp32 Â [target][source] as the split-3 forward hands it to the fused backward (the
+// forward's LDS sum, row-major: 16 chunks of 1 KiB, one direct-to-LDS wave load each)
+constexpr int ADJT_TILE_BYTES = TM * TM * 4;
+static_assert(ADJT_TILE_BYTES == LGNN_S3_ADJT_TILE_BYTES && ADJT_TILE_BYTES % 1024 == 0, "");
 
 __device__ __forceinline__ constexpr int perm16(int k) {
   return (k & ~12) | ((k & 4) << 1) | ((k & 8) >> 1);

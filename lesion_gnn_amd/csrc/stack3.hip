@@ -215,6 +215,8 @@ struct OpenFwdArgs {
   const float* W[LGNN_MAX_STACK];  // fp32 weights [N_l][K_l]
   float* S[LGNN_MAX_STACK];        // S[l - 1] = Â H_{l-1} of the open tiles (conv l)
   int32_t* sync;                   // grid-barrier words (nullptr: no open phase)
+  unsigned char* adjt;             // nullable: fp32 Â of every closed tile for the fused backward,
+                                   // ADJT_TILE_BYTES per tile
 };
 
 template <bool FIRST>
@@ -291,6 +293,12 @@ __global__ __launch_bounds__(NT, 2) void k_s3_fwd(const float* __restrict__ X, i
       const int tq = fresh_tid();
 #pragma unroll
       for (int i = 0; i < 4; ++i) av[i] = ld4(scr + (tq >> 2) * TM + 16 * (tq & 3) + 4 * i);
+    }
+    if (o.adjt) {  // the summed fp32 Â for the backward: this thread's 64 B, the tile coalesced
+      const Buf ba = mkbuf(o.adjt + t * ADJT_TILE_BYTES, ADJT_TILE_BYTES);
+      const int tq = fresh_tid();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bst4(ba, 64 * tq + 16 * i, av[i]);
     }
     if (FIRST)
       epilogue<false, true>(sm, z0, z1, sm.bias[0], mkbuf(args.H[0], M * args.width[1] * 4),
@@ -465,15 +473,15 @@ static int stack_fwd_s3(const float* X, int64_t M, int d_in, int has_in_proj,
                         const int32_t* rowptr, const int32_t* col, const float* w, int L,
                         const uint16_t* planes, const float* const* b, const int* widths,
                         float* const* H, const int32_t* tile_open, const float* const* Wf,
-                        float* const* S, int32_t* sync, void* stream);
+                        float* const* S, int32_t* sync, void* adjt, void* stream);
 
 extern "C" int lgnn_gcn_stack_fwd_s3(const float* X, int64_t M, int d_in, int has_in_proj,
                                      const int32_t* rowptr, const int32_t* col, const float* w,
                                      int L, const uint16_t* planes, const float* const* b,
                                      const int* widths, float* const* H,
-                                     const int32_t* tile_open, void* stream) {
+                                     const int32_t* tile_open, void* adjt, void* stream) {
   return stack_fwd_s3(X, M, d_in, has_in_proj, rowptr, col, w, L, planes, b, widths, H, tile_open,
-                      nullptr, nullptr, nullptr, stream);
+                      nullptr, nullptr, nullptr, adjt, stream);
 }
 
 extern "C" int lgnn_gcn_stack_fwd_s3_all(const float* X, int64_t M, int d_in, int has_in_proj,
@@ -481,18 +489,18 @@ extern "C" int lgnn_gcn_stack_fwd_s3_all(const float* X, int64_t M, int d_in, in
                                          const float* w, int L, const uint16_t* planes,
                                          const float* const* W, const float* const* b,
                                          const int* widths, float* const* H, float* const* S,
-                                         int32_t* tile_open, void* stream) {
+                                         int32_t* tile_open, void* adjt, void* stream) {
   if (!W || !S || !tile_open || M < 0) return LGNN_EINVAL;
   const int64_t ntiles = (M + lgnn_tile::TM - 1) / lgnn_tile::TM;
   return stack_fwd_s3(X, M, d_in, has_in_proj, rowptr, col, w, L, planes, b, widths, H, tile_open,
-                      W, S, tile_open + ntiles + 1, stream);
+                      W, S, tile_open + ntiles + 1, adjt, stream);
 }
 
 static int stack_fwd_s3(const float* X, int64_t M, int d_in, int has_in_proj,
                         const int32_t* rowptr, const int32_t* col, const float* w, int L,
                         const uint16_t* planes, const float* const* b, const int* widths,
                         float* const* H, const int32_t* tile_open, const float* const* Wf,
-                        float* const* S, int32_t* sync, void* stream) {
+                        float* const* S, int32_t* sync, void* adjt, void* stream) {
   if (M < 0 || L < 1 || L + 1 > LGNN_MAX_STACK || !planes || !b || !widths || !H || !rowptr ||
       !col || !tile_open)
     return LGNN_EINVAL;
@@ -517,6 +525,7 @@ static int stack_fwd_s3(const float* X, int64_t M, int d_in, int has_in_proj,
     }
     o.sync = sync;
   }
+  o.adjt = static_cast<unsigned char*>(adjt);
   if (M == 0) return LGNN_OK;
   if (!X) return LGNN_EINVAL;
   const int64_t ntiles = (M + lgnn_tile::TM - 1) / lgnn_tile::TM;

@@ -483,13 +483,15 @@ namespace lgnn_s3 {
 // Per tile HBM traffic: H_L, H_{L-1}, ..., H_0, X read once (the algorithmic bytes).
 // ==============================================================================================
 
-// scheduling fence between MFMA groups (-DLGNN_S3F_NOSB: none, the compiler interleaves freely)
-#ifdef LGNN_S3F_NOSB
+// scheduling fence between MFMA groups: none by default (the compiler interleaves the groups'
+// LDS reads and MFMAs freely: 122 -> 113 us at C2, tools/stamps_s3f.py); -DLGNN_S3F_SB restores
+// a sched_barrier after each group
+#ifdef LGNN_S3F_SB
+#define S3F_SB() __builtin_amdgcn_sched_barrier(0)
+#else
 #define S3F_SB() \
   do {           \
   } while (0)
-#else
-#define S3F_SB() __builtin_amdgcn_sched_barrier(0)
 #endif
 
 struct FBwdArgs {
@@ -497,6 +499,7 @@ struct FBwdArgs {
   const float* dlog;              // [B][C] logits gradient (nullable): dP = dlog Wout on the fly
   const float* Wout;              // [C][N_L]
   int C;
+  const unsigned char* adjt;      // Â^T planes per tile from the forward (AG), or nullptr
   const int64_t* batch;
   const int32_t* gptr;
   int pool_mean;
@@ -536,7 +539,19 @@ struct FBwdSmem {
   __attribute__((aligned(16))) float dl[TM][kMaxHeadC];  // dlog rows of the tile's graphs, pre-scaled by pscale
 };
 
-template <int NL>
+// the tile's fp32 Â [target][source] (the forward's sum) straight into the scratch: 16 wave loads
+// of 1 KiB, no registers, completion by vmcnt
+__device__ __forceinline__ void adj_issue(FBwdSmem& sm, const unsigned char* adjt, int64_t t) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const Buf rs = mkbuf(adjt + t * ADJT_TILE_BYTES, ADJT_TILE_BYTES);
+  for (int c = wave; c < ADJT_TILE_BYTES / 1024; c += NT / 64)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        rs, (__attribute__((address_space(3))) void*)(&sm.Adj[0][0] + c * 1024), 16,
+        c * 1024 + lane * 16, 0, 0, 0);
+}
+
+template <int NL, bool AG>
 __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ rowptr,
                                                    const int32_t* __restrict__ col,
                                                    const float* __restrict__ w, int64_t M,
@@ -561,25 +576,49 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
   IdxRegs R;
   [[maybe_unused]] int stamp = 0;
   int64_t t = seek_tile(blockIdx.x, ntiles, tmask, 0);
+  // graph of row tq of the tile and its size (tq < TM), loaded a tile ahead
+  int64_t pre_g = 0;
+  int pre_cnt = 0;
   if (t < ntiles) {
-    idx_load_head(R, rowptr, M, t * TM);
-    idx_load_body(R, col, w);
+    {
+      const int tq = fresh_tid();
+      const int64_t row = t * TM + tq;
+      if (tq < TM && row < M) {
+        pre_g = a.batch[row];
+        pre_cnt = a.gptr[pre_g + 1] - a.gptr[pre_g];
+      }
+    }
+    if constexpr (AG) {
+      adj_issue(sm, a.adjt, t);
+    } else {
+      idx_load_head(R, rowptr, M, t * TM);
+      idx_load_body(R, col, w);
+    }
   }
   for (; t < ntiles;) {
     STAMP(stamp++);
     const int64_t r0 = t * TM;
     const int64_t tn = seek_tile(t + gridDim.x, ntiles, tmask, 0);
     const bool has_next = tn < ntiles;
+    // H_L rows first: their latency overlaps the staging below
+    f32x16 hv[2];
     {
       const int tq = fresh_tid();
+      const int h = (tq >> 5) & 1, n = 32 * (tq >> 6) + (tq & 31);
+      load_pt(hv, a.H[L], M, r0, NLast, n, NLast, h);
+    }
+    {
+      const int tq = fresh_tid();
+      if constexpr (!AG) {
 #pragma unroll
-      for (int i = 0; i < TM * TM / 4 / NT; ++i) st4(scr + 4 * (tq + i * NT), zero4());
-      if (tq <= TM) sm.rp[tq] = R.rp;
-      if (tq == 0) sm.flag = 0;
+        for (int i = 0; i < TM * TM / 4 / NT; ++i) st4(scr + 4 * (tq + i * NT), zero4());
+        if (tq <= TM) sm.rp[tq] = R.rp;
+        if (tq == 0) sm.flag = 0;
+      }
       if (tq < TM) {
         const int64_t row = r0 + tq;
-        const int64_t g = row < M ? a.batch[row] : 0;
-        const int cnt = a.gptr[g + 1] - a.gptr[g];
+        const int64_t g = pre_g;
+        const int cnt = pre_cnt;
         const float ps = row >= M ? 0.f : (a.pool_mean && cnt > 1 ? 1.f / (float)cnt : 1.f);
         sm.pg[tq] = (int)g;
         sm.pscale[tq] = ps;
@@ -593,15 +632,15 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
       }
     }
     lds_barrier();
-    adj_scatter<true>(scr, sm.rp, R, r0);
-    if (has_next) idx_load_head(R, rowptr, M, tn * TM);
+    if constexpr (!AG) {
+      adj_scatter<true>(scr, sm.rp, R, r0);
+      if (has_next) idx_load_head(R, rowptr, M, tn * TM);
+    }
     // dZ_L = pool broadcast of dP (/ |graph|) * ELU'(H_L), P layout (feature n on the lane)
     f32x16 dz[2];
     {
       const int tq = fresh_tid();
       const int h = (tq >> 5) & 1, n = 32 * (tq >> 6) + (tq & 31);
-      f32x16 hv[2];
-      load_pt(hv, a.H[L], M, r0, NLast, n, NLast, h);
       if (a.dlog) {  // dP[g][n] = sum_c dlog[g][c] Wout[c][n], dlog rows staged (scaled) in LDS
         float wo[kMaxHeadC];
 #pragma unroll
@@ -633,6 +672,32 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
           }
       }
     }
+    if constexpr (AG) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's Â loads landed
+      lds_barrier();  // ... and every wave's
+      // Â^T planes: row am = source, positions perm16 of targets 16 aq .. (a wave reads 64
+      // different banks)
+      const int tq = fresh_tid();
+      const int am = tq & 63, aq = tq >> 6;
+      float f[16];
+#pragma unroll
+      for (int y = 0; y < 16; ++y) f[y] = scr[(16 * aq + perm16(y)) * TM + am];
+      uint32_t q[3][8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const Split2 s2 = split2(f[2 * i], f[2 * i + 1]);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) q[p][i] = s2.p[p];
+      }
+      lds_barrier();  // every scratch read done (the planes overwrite it)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        unsigned char* dst = sm.Adj[p] + am * ADJ_LD * 2 + 32 * aq;
+        *reinterpret_cast<u32x4*>(dst) = u32x4{q[p][0], q[p][1], q[p][2], q[p][3]};
+        *reinterpret_cast<u32x4*>(dst + 16) = u32x4{q[p][4], q[p][5], q[p][6], q[p][7]};
+      }
+      lds_barrier();
+    } else {
     lds_barrier();  // Â^T summed
     {
       f32x4 av[4];
@@ -671,6 +736,7 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
       lds_barrier();
     }
     if (has_next) idx_load_body(R, col, w);
+    }
     STAMP(stamp++);
 
     f32x16 xp[2];  // X rows of the in_proj phase (issued during the last conv's dH)
@@ -784,6 +850,16 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
       u32x4 wf0[3][4], wf1[3][4];
       load_w(wf0, 0);
       lds_barrier();  // both images complete
+      // the last conv's Â^T reads are done: the next tile's planes load into LDS behind the
+      // remaining phases of this tile
+      if constexpr (AG) {
+        if (l == 1 && has_next) adj_issue(sm, a.adjt, tn);
+      }
+      if (l == 1) {  // the next tile's graph ids (their sizes follow in the in_proj phase)
+        const int tq = fresh_tid();
+        const int64_t row = tn * TM + tq;
+        pre_g = (has_next && tq < TM && row < M) ? a.batch[row] : 0;
+      }
       STAMP(stamp++);
       // dW_l += G^T H: A = G (P layout, node steps), B = H image rows k = 32 kb + li
       {
@@ -874,6 +950,7 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
             for (int p = 0; p < 3; ++p) sts8(sm.Img[p] + off, o[p]);
           }
         (void)K;
+        pre_cnt = (has_next && tq < TM) ? a.gptr[pre_g + 1] - a.gptr[pre_g] : 0;
       }
       lds_barrier();
       {
@@ -957,7 +1034,7 @@ static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* g
                          float* const* dWp, float* const* dbp, int num_partials,
                          const int32_t* tile_open, const lgnn_s3::OpenBwdArgs& o, void* stream,
                          const float* dlogits = nullptr, const float* Wout = nullptr,
-                         int num_classes = 0);
+                         int num_classes = 0, const void* adjt = nullptr);
 
 extern "C" int lgnn_gcn_stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* gptr,
                                       int pool_mean, int64_t num_graphs, const int32_t* rowptr,
@@ -965,10 +1042,11 @@ extern "C" int lgnn_gcn_stack_bwd_s3f(const float* dP, const int64_t* batch, con
                                       int64_t M, int L, const uint16_t* planes_t,
                                       const float* const* H, const int* widths,
                                       float* const* dWp, float* const* dbp, int num_partials,
-                                      const int32_t* tile_open, void* stream) {
+                                      const int32_t* tile_open, const void* adjt, void* stream) {
   const lgnn_s3::OpenBwdArgs o = {};
   return stack_bwd_s3f(dP, batch, gptr, pool_mean, num_graphs, rowptr, col, w, X, M, L, planes_t,
-                       H, widths, dWp, dbp, num_partials, tile_open, o, stream);
+                       H, widths, dWp, dbp, num_partials, tile_open, o, stream, nullptr, nullptr,
+                       0, adjt);
 }
 
 extern "C" int lgnn_gcn_stack_bwd_s3f_all(
@@ -978,7 +1056,7 @@ extern "C" int lgnn_gcn_stack_bwd_s3f_all(
     const uint16_t* planes_t, const float* const* W, const float* const* H,
     const float* const* S, const int* widths, float* const* dWp, float* const* dbp,
     int num_partials, float* dS_ws, int32_t* tile_open, const float* dlogits, const float* Wout,
-    int num_classes, void* stream) {
+    int num_classes, const void* adjt, void* stream) {
   if (M < 0 || L < 1 || L > 2 || !W || !S || !tptr || !tidx || !tw || !dS_ws || !tile_open)
     return LGNN_EINVAL;
   if (dlogits && (!Wout || num_classes < 1 || num_classes > lgnn_s3::kMaxHeadC))
@@ -998,7 +1076,7 @@ extern "C" int lgnn_gcn_stack_bwd_s3f_all(
   o.sync = tile_open + ntiles + 4;
   return stack_bwd_s3f(dP, batch, gptr, pool_mean, num_graphs, rowptr, col, w, X, M, L, planes_t,
                        H, widths, dWp, dbp, num_partials, tile_open, o, stream, dlogits, Wout,
-                       num_classes);
+                       num_classes, adjt);
 }
 
 static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* gptr,
@@ -1007,7 +1085,8 @@ static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* g
                          const uint16_t* planes_t, const float* const* H, const int* widths,
                          float* const* dWp, float* const* dbp, int num_partials,
                          const int32_t* tile_open, const lgnn_s3::OpenBwdArgs& o, void* stream,
-                         const float* dlogits, const float* Wout, int num_classes) {
+                         const float* dlogits, const float* Wout, int num_classes,
+                         const void* adjt) {
   if (M < 0 || L < 1 || L > 2 || !(dP || dlogits) || !batch || !gptr || !rowptr || !col || !X ||
       !planes_t || !H || !widths || !dWp || !dbp || !tile_open || num_graphs < 0)
     return LGNN_EINVAL;
@@ -1017,6 +1096,7 @@ static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* g
   a.dlog = dlogits;
   a.Wout = Wout;
   a.C = num_classes;
+  a.adjt = static_cast<const unsigned char*>(adjt);
   a.batch = batch;
   a.gptr = gptr;
   a.pool_mean = pool_mean;
@@ -1040,12 +1120,18 @@ static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* g
     return LGNN_OK;
   }
   const dim3 grid((unsigned)num_partials), blk(lgnn_tile::NT);
-  if (L == 1)
-    hipLaunchKernelGGL(lgnn_s3::k_s3_fbwd<2>, grid, blk, 0, s, rowptr, col, w, M, a, tile_open,
-                       o);
+  if (L == 1 && adjt)
+    hipLaunchKernelGGL((lgnn_s3::k_s3_fbwd<2, true>), grid, blk, 0, s, rowptr, col, w, M, a,
+                       tile_open, o);
+  else if (L == 1)
+    hipLaunchKernelGGL((lgnn_s3::k_s3_fbwd<2, false>), grid, blk, 0, s, rowptr, col, w, M, a,
+                       tile_open, o);
+  else if (adjt)
+    hipLaunchKernelGGL((lgnn_s3::k_s3_fbwd<3, true>), grid, blk, 0, s, rowptr, col, w, M, a,
+                       tile_open, o);
   else
-    hipLaunchKernelGGL(lgnn_s3::k_s3_fbwd<3>, grid, blk, 0, s, rowptr, col, w, M, a, tile_open,
-                       o);
+    hipLaunchKernelGGL((lgnn_s3::k_s3_fbwd<3, false>), grid, blk, 0, s, rowptr, col, w, M, a,
+                       tile_open, o);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? LGNN_OK : (int)e;
 }

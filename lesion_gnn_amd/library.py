@@ -631,7 +631,9 @@ def _(x, g, mean, L, params):
     fused, saved_s = _gcn_layout(params, L)
     hs = [x.new_empty(M, W.shape[0]) for W in Ws]
     ss = [x.new_empty(M, Ws[l + 1].shape[1]) for l in range(L)]
-    planes = (x.new_empty(L + 1, 3, 128, 128, dtype=torch.int16)
+    from .ops import bwd_planes_numel
+
+    planes = (x.new_empty(bwd_planes_numel(L, M), dtype=torch.int16)
               if fused and MFMA_MODE == "s3" and BWD_S3 and L >= 1 else _none(x.device))
     return [x.new_empty(B, params[2 + 2 * L].shape[0]), x.new_empty(B, Ws[-1].shape[0])] + hs + \
         ss + [planes]

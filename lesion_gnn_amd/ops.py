@@ -112,18 +112,46 @@ def _open_in_fused(mode, graph: Graph, direction: str) -> bool:
     return n > 0 and (64 % n == 0 or n % 64 == 0)
 
 
-def weight_planes(Ws: list, d_in: int, transposed: bool = False):
+def weight_planes(Ws: list, d_in: int, transposed: bool = False, extra: int = 0):
     """bf16 three-plane images of the stack weights for the split-3 kernels (one launch):
-    returns (planes, planes_t or None), each [L+1, 3, 128, 128] int16."""
+    returns (planes [L+1, 3, 128, 128] int16, planes_t or None). planes_t is flat: the
+    transposed planes, then `extra` int16 of room (the forward's Â^T planes, bwd_planes_numel)."""
     nl = len(Ws)
     dev = Ws[0].device
     planes = torch.empty(nl, 3, 128, 128, dtype=torch.int16, device=dev)
-    planes_t = torch.empty_like(planes) if transposed else None
+    planes_t = torch.empty(nl * 3 * 128 * 128 + extra, dtype=torch.int16, device=dev) \
+        if transposed else None
     widths = (ctypes.c_int * (nl + 1))(*([d_in] + [W.size(0) for W in Ws]))
     arr = ctypes.c_void_p * nl
     _lib.call("lgnn_weight_planes", nl, arr(*[W.data_ptr() for W in Ws]), widths,
               _lib.ptr(planes), _lib.ptr(planes_t), _s(dev))
     return planes, planes_t
+
+
+def adjt_numel(M) -> int:
+    """int16 elements of the Â^T planes the split-3 forward hands to the fused backward."""
+    return (M + 63) // 64 * (_lib.LGNN_S3_ADJT_TILE_BYTES // 2)
+
+
+def bwd_planes_numel(L: int, M) -> int:
+    """Size of the buffer the fused GCN forward keeps for its backward (ctx.planes_t): the
+    transposed weight planes, plus the Â^T planes when the single-launch split-3 backward runs."""
+    return (L + 1) * 3 * 128 * 128 + (adjt_numel(M) if _s3f(L) and ADJT else 0)
+
+
+def _s3f(L: int) -> bool:
+    return BWD_MODE == "s3f" and L <= 2
+
+
+# the split-3 forward hands each closed tile's Â^T planes to the fused backward (LGNN_ADJT=0: the
+# backward rebuilds them from the CSR)
+ADJT = os.environ.get("LGNN_ADJT", "1") != "0"
+
+
+def _adjt_ptr(planes_t: torch.Tensor, L: int):
+    """Device address of the Â^T planes inside planes_t, or None."""
+    base = (L + 1) * 3 * 128 * 128
+    return planes_t.data_ptr() + 2 * base if planes_t.numel() > base else None
 
 
 def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list, keep: dict | None = None):
@@ -146,7 +174,9 @@ def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list, keep: dict | No
     if MFMA_MODE == "s3" and L >= 1:
         # the transposed planes (the split-3 backward's dH = G W_l operand) come from the same
         # launch when the caller keeps them
-        planes, planes_t = weight_planes(Ws, x.size(1), transposed=keep is not None)
+        extra = adjt_numel(M) if keep is not None and _s3f(L) and ADJT else 0
+        planes, planes_t = weight_planes(Ws, x.size(1), transposed=keep is not None, extra=extra)
+        adjt = _adjt_ptr(planes_t, L) if extra else None
         if keep is not None:
             keep["planes_t"] = planes_t
         if _open_in_fused(OPEN_IN_FUSED, graph, "fwd"):  # open tiles in the same launch
@@ -154,11 +184,11 @@ def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list, keep: dict | No
                       _lib.ptr(csr.rowptr), _lib.ptr(csr.col), _lib.ptr(csr.w), L,
                       _lib.ptr(planes), Wp, bp, widths, Hp,
                       (ctypes.c_void_p * L)(*[t.data_ptr() for t in ss]), _lib.ptr(open_),
-                      _s(dev))
+                      adjt, _s(dev))
             return hs, ss
         _lib.call("lgnn_gcn_stack_fwd_s3", _lib.ptr(x), M, x.size(1), 1, _lib.ptr(csr.rowptr),
                   _lib.ptr(csr.col), _lib.ptr(csr.w), L, _lib.ptr(planes), bp, widths, Hp,
-                  _lib.ptr(open_), _s(dev))
+                  _lib.ptr(open_), adjt, _s(dev))
     else:
         _lib.call("lgnn_gcn_stack_fwd", _lib.ptr(x), M, x.size(1), 1, _lib.ptr(csr.rowptr),
                   _lib.ptr(csr.col), _lib.ptr(csr.w), L, Wp, bp, widths, Hp, _lib.ptr(open_),
@@ -197,7 +227,8 @@ def stack_bwd(dp: torch.Tensor | None, x: torch.Tensor, graph: Graph, mean: bool
     dev = x.device
     lib = _lib.load()
     s3 = planes_t is not None
-    s3f = s3 and BWD_MODE == "s3f" and L <= 2
+    s3f = s3 and _s3f(L)
+    adjt = _adjt_ptr(planes_t, L) if s3f else None
     P = lib.lgnn_gcn_stack_bwd_s3_partials(M) if s3 and not s3f else \
         lib.lgnn_gcn_stack_bwd_partials(M)
     _lib.check(0 if P > 0 else P, "lgnn_gcn_stack_bwd_partials")
@@ -224,7 +255,7 @@ def stack_bwd(dp: torch.Tensor | None, x: torch.Tensor, graph: Graph, mean: bool
                   (ctypes.c_void_p * L)(*[t.data_ptr() for t in ss]),
                   (ctypes.c_int * (L + 2))(*widths), arr(*[t.data_ptr() for t in dWp]),
                   arr(*[t.data_ptr() for t in dbp]), P, _lib.ptr(dS_ws), _lib.ptr(open_),
-                  _lib.ptr(dlog), _lib.ptr(W_out), W_out.size(0) if head else 0, _s(dev))
+                  _lib.ptr(dlog), _lib.ptr(W_out), W_out.size(0) if head else 0, adjt, _s(dev))
         return _stack_bwd_outputs(L, widths, dWp, dbp, P, dev, reducer)
     assert head is None, "dP from the logits gradient only in the single-launch split-3 path"
     if s3f:  # one fused split-3 launch, every layer of a tile in one pass (stack3_bwd.hip)
@@ -233,7 +264,7 @@ def stack_bwd(dp: torch.Tensor | None, x: torch.Tensor, graph: Graph, mean: bool
                   _lib.ptr(csr.col), _lib.ptr(csr.w), _lib.ptr(x), M, L, _lib.ptr(planes_t),
                   arr(*[h.data_ptr() for h in hs]), (ctypes.c_int * (L + 2))(*widths),
                   arr(*[t.data_ptr() for t in dWp]), arr(*[t.data_ptr() for t in dbp]), P,
-                  _lib.ptr(open_), _s(dev))
+                  _lib.ptr(open_), adjt, _s(dev))
     elif s3:  # one split-3 launch per layer (stack3_bwd.hip); dZ between them in dz_ws
         dz_ws = torch.empty(2 * M * 128, dtype=torch.float32, device=dev)
         _lib.call("lgnn_gcn_stack_bwd_s3", _lib.ptr(dp), _lib.ptr(graph.batch),

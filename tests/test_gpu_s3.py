@@ -159,7 +159,7 @@ def test_stack_fwd_s3_without_in_proj(cuda):
     _lib.call("lgnn_gcn_stack_fwd_s3", _lib.ptr(hs[0]), M, 128, 0, _lib.ptr(csr.rowptr),
               _lib.ptr(csr.col), _lib.ptr(csr.w), L, _lib.ptr(planes),
               arr(*[v.data_ptr() for v in bs]), (ctypes.c_int * (L + 1))(128, 128, 128),
-              arr(*[t.data_ptr() for t in out]), _lib.ptr(open_), _lib.stream(cuda))
+              arr(*[t.data_ptr() for t in out]), _lib.ptr(open_), None, _lib.stream(cuda))
     torch.cuda.synchronize()
     for l in (1, 2):
         assert torch.equal(out[l], hs[l]), l

@@ -74,7 +74,7 @@ def run():
         def launch():
             assert f(b.x.data_ptr(), M, 128, 1, csr.rowptr.data_ptr(), csr.col.data_ptr(),
                      csr.w.data_ptr(), L, planes.data_ptr(), bp, widths, Hp, open_.data_ptr(),
-                     s) == 0
+                     None, s) == 0
         for _ in range(3):
             launch()
         torch.cuda.synchronize()
@@ -94,7 +94,8 @@ def run():
     lib.lgnn_s3_debug_stamps.argtypes = [ctypes.c_void_p]
     for _ in range(3):
         assert f(b.x.data_ptr(), M, 128, 1, csr.rowptr.data_ptr(), csr.col.data_ptr(),
-                 csr.w.data_ptr(), L, planes.data_ptr(), bp, widths, Hp, open_.data_ptr(), s) == 0
+                 csr.w.data_ptr(), L, planes.data_ptr(), bp, widths, Hp, open_.data_ptr(), None,
+                 s) == 0
     torch.cuda.synchronize()
     buf = (ctypes.c_ulonglong * (1024 * 64))()
     assert lib.lgnn_s3_debug_stamps(buf) == 0

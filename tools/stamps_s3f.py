@@ -20,8 +20,8 @@ LIB = os.path.join(ROOT, "tools", "_abl", "liblgnn_s3f_%s.so")
 VARIANTS = {"default": [], "stamps": ["-DLGNN_STAMPS"]}
 for k, v in [("nomfma", 1), ("noglobal", 16)]:
     VARIANTS[k] = [f"-DLGNN_ABLATE={v}"]
-VARIANTS["nosb"] = ["-DLGNN_S3F_NOSB"]
-VARIANTS["nosb_stamps"] = ["-DLGNN_S3F_NOSB", "-DLGNN_STAMPS"]
+VARIANTS["sb"] = ["-DLGNN_S3F_SB"]
+VARIANTS["sb_stamps"] = ["-DLGNN_S3F_SB", "-DLGNN_STAMPS"]
 NAMES = ["prologue (adj, dZ_L)", "l2 G^T,G", "l2 images", "l2 dW", "l2 dH+dZ", "l1 G^T,G",
          "l1 images", "l1 dW", "l1 dH+dZ", "l0 X + dW", "tile tail"]
 
@@ -55,7 +55,11 @@ def run():
     Ws = [torch.randn(D, D, device=dev, generator=gen) / 11.3 for _ in range(L + 1)]
     Hs = [torch.randn(M, D, device=dev, generator=gen) for _ in range(L + 1)]
     dP = torch.randn(b.num_graphs, D, device=dev, generator=gen)
-    _, planes_t = ops.weight_planes(Ws, D, transposed=True)
+    # the forward's Â^T planes handed to the backward (STAMPS_ADJT=0: rebuilt from the CSR)
+    keep = {}
+    ops.stack_fwd(b.x, g, Ws, [torch.zeros(D, device=dev)] * (L + 1), keep)
+    planes_t = keep["planes_t"]
+    adjt_ptr = ops._adjt_ptr(planes_t, L) if os.environ.get("STAMPS_ADJT", "1") != "0" else None
     s = torch.cuda.current_stream().cuda_stream
     arr = ctypes.c_void_p * (L + 1)
     for v in [*VARIANTS, *[p for p in PREBUILT if os.path.exists(LIB % p)]]:
@@ -70,7 +74,7 @@ def run():
         args = (dP.data_ptr(), g.batch.data_ptr(), g.gptr.data_ptr(), 1, b.num_graphs,
                 csr.rowptr.data_ptr(), csr.col.data_ptr(), csr.w.data_ptr(), b.x.data_ptr(), M, L,
                 planes_t.data_ptr(), arr(*[h.data_ptr() for h in Hs]),
-                (ctypes.c_int * (L + 2))(D, D, D, D), dWp, dbp, P, open_.data_ptr(), s)
+                (ctypes.c_int * (L + 2))(D, D, D, D), dWp, dbp, P, open_.data_ptr(), adjt_ptr, s)
         for _ in range(3):
             assert lib.lgnn_gcn_stack_bwd_s3f(*args) == 0
         torch.cuda.synchronize()
