@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 12
+#define LGNN_ABI_VERSION 13
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -254,6 +254,44 @@ int lgnn_bn_bwd_apply(const float* dA, const float* Z, const float* mask, int64_
                       const float* scale, const float* shift, const float* mean,
                       const float* invstd, const double* sums, double count, int training,
                       float* dZ, float* dgamma, float* dbeta, void* stream);
+/* sums[2N] = the fixed-order sum of num_partials fp64 partial rows part[p][2N] (the BN-fused
+ * linear kernels below write one row per workgroup). */
+int lgnn_bn_partials_reduce(const double* part, int num_partials, int N, double* sums,
+                            void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * The GIN MLP's linear layers with BatchNorm folded into them (the same arithmetic as the
+ * lgnn_bn_* kernels above, without their passes over HBM). Fast-path shapes only (K, N <= 128,
+ * multiples of 4); one partial row per workgroup, lgnn_bn_fused_partials(M) rows.
+ * lgnn_node_linear_fwd_bn = lgnn_node_linear_fwd (no tile selection) with exactly one of
+ *   stats_part: [P][2N] fp64 per-workgroup (sum y, sum y^2) of the output Y (then
+ *     lgnn_bn_partials_reduce -> lgnn_bn_finalize), or
+ *   bn_scale / bn_shift [K] (+ bn_mask [M,K], nullable): the input rows are first mapped to
+ *     ELU(X*scale + shift) [* mask] — lgnn_bn_act fused into the load — and that activation is
+ *     also written to bn_out [M,K] (the backward's dW input); no gather.
+ * lgnn_node_linear_bwd_bn = lgnn_node_linear_bwd in LGNN_GRAD_DIRECT mode (no gather) with
+ *   bn_mode LGNN_BN_GSTATS: the dX output is the gradient dA of a BN + ELU (+ mask) output whose
+ *     input is bn_Z [M,K]; gstats_part [P][2K] receives per-workgroup (sum g, sum g*xhat)
+ *     (lgnn_bn_bwd_stats fused into the dX epilogue), or
+ *   bn_mode LGNN_BN_GIN (act NONE): dY is such a dA [M,N] of BN input bn_Z [M,N]; the kernel
+ *     applies the BN backward (lgnn_bn_bwd_apply's dZ, with bn_sums / count / training) before
+ *     using it, so dZ never goes to HBM.
+ * ------------------------------------------------------------------------------------------- */
+#define LGNN_BN_GSTATS 3
+#define LGNN_BN_GIN 4
+int lgnn_bn_fused_partials(int64_t num_rows);
+int lgnn_node_linear_fwd_bn(const float* X, int64_t M, int K, const int32_t* rowptr,
+                            const int32_t* col, const float* w, float self_scale, const float* W,
+                            const float* b, int N, int act, float* Y, float* S_out,
+                            double* stats_part, const float* bn_scale, const float* bn_shift,
+                            const float* bn_mask, float* bn_out, void* stream);
+int lgnn_node_linear_bwd_bn(int bn_mode, const float* dY, const float* H, int act,
+                            const float* X, int64_t M, int K, const float* W, int N,
+                            float* dXpre, float* dW_partial, float* db_partial, int num_partials,
+                            const float* bn_Z, const float* bn_mask, const float* bn_scale,
+                            const float* bn_shift, const float* bn_mean, const float* bn_invstd,
+                            double* gstats_part, const double* bn_sums, double count,
+                            int training, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * GATConv attention (PyG 2.5.1 GATConv(d1, d2//H, heads=H, dropout=p), reference gat.py:31:

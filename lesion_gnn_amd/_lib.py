@@ -18,6 +18,7 @@ LIB_PATH = os.path.join(_HERE, "liblgnn.so")
 LGNN_LOOPS_KEEP, LGNN_LOOPS_REMAINING, LGNN_LOOPS_READD = 0, 1, 2
 LGNN_NORM_NONE, LGNN_NORM_GCN = 0, 1
 LGNN_ACT_NONE, LGNN_ACT_ELU = 0, 1
+LGNN_BN_GSTATS, LGNN_BN_GIN = 3, 4
 LGNN_GRAD_DIRECT, LGNN_GRAD_POOL, LGNN_GRAD_TRANSPOSE = 0, 1, 2
 LGNN_TILE_OPEN_EXTRA = 7  # tile_open words after the per-tile flags (count + barrier words)
 LGNN_S3_ADJT_TILE_BYTES = 16384  # lgnn.h: fp32 Â per tile, split-3 forward -> fused backward
@@ -81,6 +82,12 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_node_linear_fwd_tiles": (I32, [P, I64, I32, P, P, P, F32, P, P, I32, I32, P, P, P, I32,
                                          P]),
     "lgnn_bn_bwd_apply": (I32, [P, P, P, I64, I32, P, P, P, P, P, F64, I32, P, P, P, P]),
+    "lgnn_bn_partials_reduce": (I32, [P, I32, I32, P, P]),
+    "lgnn_bn_fused_partials": (I32, [I64]),
+    "lgnn_node_linear_fwd_bn": (I32, [P, I64, I32, P, P, P, F32, P, P, I32, I32, P, P, P, P, P, P,
+                                      P, P]),
+    "lgnn_node_linear_bwd_bn": (I32, [I32, P, P, I32, P, I64, I32, P, I32, P, P, P, I32, P, P, P,
+                                      P, P, P, P, P, F64, I32, P]),
     "lgnn_gcn_stack_bwd_s3f": (I32, [P, P, P, I32, I64, P, P, P, P, I64, I32, P, P, P, P, P,
                                      I32, P, P, P]),
     "lgnn_gcn_stack_fwd_s3_all": (I32, [P, I64, I32, I32, P, P, P, I32, P, P, P, P, P, P, P, P, P]),
@@ -93,7 +100,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 _lib = None
 

@@ -53,6 +53,11 @@ __device__ __forceinline__ float elu_f(float x) {
 #endif
 // ELU derivative from the saved OUTPUT h = elu(z): z > 0 <=> h > 0; exp(z) = h + 1.
 __device__ __forceinline__ float elu_grad_from_out(float h) { return h > 0.f ? 1.f : h + 1.f; }
+// ELU'(zn) for zn = z * scale + shift (BatchNorm then ELU): 1 above 0, exp(zn) below (exp2 form)
+__device__ __forceinline__ float bn_elu_grad(float z, float sc, float sh) {
+  const float zn = fmaf(z, sc, sh);
+  return zn > 0.f ? 1.f : __builtin_amdgcn_exp2f(zn * 1.44269504088896341f);
+}
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }

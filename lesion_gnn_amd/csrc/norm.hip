@@ -25,12 +25,6 @@ inline int row_blocks(int64_t M) {
   return (int)(b < 1 ? 1 : b);
 }
 
-// ELU'(zn) for zn = z * scale + shift: 1 above 0, exp(zn) below (exp2 form)
-__device__ __forceinline__ float bn_elu_grad(float z, float sc, float sh) {
-  const float zn = fmaf(z, sc, sh);
-  return zn > 0.f ? 1.f : __builtin_amdgcn_exp2f(zn * 1.44269504088896341f);
-}
-
 __device__ __forceinline__ f32x4 ld4c(const float* p, int c, int N) {
   return c < N ? ld4(p + c) : f32x4{0.f, 0.f, 0.f, 0.f};
 }
@@ -323,6 +317,15 @@ extern "C" int lgnn_bn_bwd_stats(const float* dA, const float* Z, const float* m
   LGNN_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_colsum_reduce, dim3((2 * N + NT / RED_SPLIT - 1) / (NT / RED_SPLIT)),
                      dim3(NT), 0, s, part, P, 2 * N, sums);
+  LGNN_LAUNCH_CHECK();
+  return LGNN_OK;
+}
+
+extern "C" int lgnn_bn_partials_reduce(const double* part, int num_partials, int N,
+                                       double* sums, void* stream) {
+  if (num_partials <= 0 || N <= 0 || !part || !sums) return LGNN_EINVAL;
+  hipLaunchKernelGGL(k_colsum_reduce, dim3((2 * N + NT / RED_SPLIT - 1) / (NT / RED_SPLIT)),
+                     dim3(NT), 0, as_stream(stream), part, num_partials, 2 * N, sums);
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
 }

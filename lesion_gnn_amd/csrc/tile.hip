@@ -23,7 +23,7 @@ namespace lgnn_tile {
 
 
 // The layer-wise kernels: the bodies in tile_lw.h on their own LDS.
-template <bool GATHER, int ACT>
+template <bool GATHER, int ACT, int BNM = BN_NONE>
 __global__ __launch_bounds__(NT, 2) void k_fwd(const float* __restrict__ X, int64_t M, int K,
                                                const int32_t* __restrict__ rowptr,
                                                const int32_t* __restrict__ col,
@@ -31,27 +31,30 @@ __global__ __launch_bounds__(NT, 2) void k_fwd(const float* __restrict__ X, int6
                                                const float* __restrict__ W,
                                                const float* __restrict__ b, int N,
                                                float* __restrict__ Y, float* __restrict__ S_out,
-                                               const int32_t* __restrict__ tmask, int want) {
+                                               const int32_t* __restrict__ tmask, int want,
+                                               BnFuse bn) {
   __shared__ __attribute__((aligned(16))) float A[TM * LDS];
   __shared__ __attribute__((aligned(16))) float S[GATHER ? TM * LDS : 4];
   __shared__ TileIdx ti;
-  fwd_tiles<GATHER, ACT>(A, S, ti, X, M, K, rowptr, col, w, self_scale, W, b, N, Y, S_out, tmask,
-                         want);
+  fwd_tiles<GATHER, ACT, BNM>(A, S, ti, X, M, K, rowptr, col, w, self_scale, W, b, N, Y, S_out,
+                              tmask, want, bn);
 }
 
-template <int GMODE, int ACT, bool DX>
+template <int GMODE, int ACT, bool DX, int BNM = BN_NONE>
 __global__ __launch_bounds__(NT, 2) void k_bwd(
     const float* __restrict__ dY, const int64_t* __restrict__ batch,
     const int32_t* __restrict__ gptr, int pool_mean, const int32_t* __restrict__ tptr,
     const int32_t* __restrict__ tidx, const float* __restrict__ tw, float tself,
     const float* __restrict__ H, const float* __restrict__ X, int64_t M, int K,
     const float* __restrict__ W, int N, float* __restrict__ dXpre, float* __restrict__ dWp,
-    float* __restrict__ dbp, const int32_t* __restrict__ tmask, int want, int accumulate) {
+    float* __restrict__ dbp, const int32_t* __restrict__ tmask, int want, int accumulate,
+    BnFuse bn) {
   __shared__ __attribute__((aligned(16))) float A[TM * LDS];
   __shared__ __attribute__((aligned(16))) float C[TM * LDS];
   __shared__ TileIdx ti;
-  bwd_tiles<GMODE, ACT, DX>(A, C, ti, dY, batch, gptr, pool_mean, tptr, tidx, tw, tself, H, X, M,
-                            K, W, N, dXpre, dWp, dbp, tmask, want, accumulate);
+  bwd_tiles<GMODE, ACT, DX, BNM>(A, C, ti, dY, batch, gptr, pool_mean, tptr, tidx, tw, tself, H,
+                                 X, M, K, W, N, dXpre, dWp, dbp, tmask, want, accumulate, nullptr,
+                                 nullptr, 0, bn);
 }
 
 
@@ -679,7 +682,7 @@ hipError_t lgnn_tile_fwd(hipStream_t s, const float* X, int64_t M, int K, const 
   dim3 grid((unsigned)(ntiles < 512 ? ntiles : 512));
 #define LGNN_TF(G, A)                                                                         \
   hipLaunchKernelGGL((k_fwd<G, A>), grid, dim3(NT), 0, s, X, M, K, rowptr, col, w, self_scale, \
-                     W, b, N, Y, S_out, tile_mask, want)
+                     W, b, N, Y, S_out, tile_mask, want, BnFuse{})
   if (rowptr) {
     if (act == LGNN_ACT_ELU) LGNN_TF(true, LGNN_ACT_ELU);
     else LGNN_TF(true, LGNN_ACT_NONE);
@@ -701,7 +704,7 @@ hipError_t lgnn_tile_bwd(hipStream_t s, int grad_mode, const float* dY, const in
 #define LGNN_TB(GM, AC, D)                                                                     \
   hipLaunchKernelGGL((k_bwd<GM, AC, D>), grid, dim3(NT), 0, s, dY, batch, gptr, pool_mean, tptr, \
                      tidx, tw, tself, H, X, M, K, W, N, dXpre, dWp, dbp, tile_mask, want,        \
-                     accumulate)
+                     accumulate, BnFuse{})
 #define LGNN_TB_D(GM, AC) \
   if (dXpre) LGNN_TB(GM, AC, true); else LGNN_TB(GM, AC, false);
   if (act == LGNN_ACT_ELU) {
@@ -721,6 +724,116 @@ hipError_t lgnn_tile_bwd(hipStream_t s, int grad_mode, const float* dY, const in
 // ------------------------------------------------------------------------------------------
 // C ABI: fused GCN stack forward
 // ------------------------------------------------------------------------------------------
+// ------------------------------------------------------------------------------------------
+// C ABI: layer-wise linear kernels with BatchNorm folded in (the GIN MLP)
+// ------------------------------------------------------------------------------------------
+extern "C" int lgnn_bn_fused_partials(int64_t M) {
+  if (M < 0) return LGNN_EINVAL;
+  return lgnn_tile_partials(M);
+}
+
+extern "C" int lgnn_node_linear_fwd_bn(const float* X, int64_t M, int K, const int32_t* rowptr,
+                                       const int32_t* col, const float* w, float self_scale,
+                                       const float* W, const float* b, int N, int act, float* Y,
+                                       float* S_out, double* stats_part, const float* bn_scale,
+                                       const float* bn_shift, const float* bn_mask,
+                                       float* bn_out, void* stream) {
+  if (M < 0 || !W || !Y || (M > 0 && !X) || !lgnn_tile_fits(M, K, N)) return LGNN_EINVAL;
+  if (act != LGNN_ACT_NONE && act != LGNN_ACT_ELU) return LGNN_EINVAL;
+  const bool stats = stats_part != nullptr, bnin = bn_scale != nullptr;
+  if (stats == bnin) return LGNN_EINVAL;  // exactly one of the two
+  if (bnin && (rowptr || !bn_shift || !bn_out)) return LGNN_EINVAL;
+  if (rowptr && !col) return LGNN_EINVAL;
+  const int P = lgnn_tile_partials(M);
+  BnFuse bn = {};
+  bn.part = stats_part;
+  bn.scale = bn_scale;
+  bn.shift = bn_shift;
+  bn.mask = bn_mask;
+  bn.act_out = bn_out;
+  hipStream_t s = as_stream(stream);
+  if (M == 0) {  // the partial rows still hold zeros
+    if (stats && hipMemsetAsync(stats_part, 0, (size_t)P * 2 * N * sizeof(double), s) != hipSuccess)
+      return (int)hipGetLastError();
+    return LGNN_OK;
+  }
+  const dim3 grid((unsigned)P);  // the stats need one partial row per workgroup
+  float* So = rowptr ? S_out : nullptr;
+#define LGNN_TFB(G, A, BM)                                                                      \
+  hipLaunchKernelGGL((k_fwd<G, A, BM>), grid, dim3(NT), 0, s, X, M, K, rowptr, col, w,        \
+                     self_scale, W, b, N, Y, So, nullptr, 0, bn)
+  if (stats) {
+    if (rowptr) {
+      if (act == LGNN_ACT_ELU) LGNN_TFB(true, LGNN_ACT_ELU, BN_STATS);
+      else LGNN_TFB(true, LGNN_ACT_NONE, BN_STATS);
+    } else {
+      if (act == LGNN_ACT_ELU) LGNN_TFB(false, LGNN_ACT_ELU, BN_STATS);
+      else LGNN_TFB(false, LGNN_ACT_NONE, BN_STATS);
+    }
+  } else {
+    if (act == LGNN_ACT_ELU) LGNN_TFB(false, LGNN_ACT_ELU, BN_IN);
+    else LGNN_TFB(false, LGNN_ACT_NONE, BN_IN);
+  }
+#undef LGNN_TFB
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? LGNN_OK : (int)e;
+}
+
+extern "C" int lgnn_node_linear_bwd_bn(int bn_mode, const float* dY, const float* H, int act,
+                                       const float* X, int64_t M, int K, const float* W, int N,
+                                       float* dXpre, float* dW_partial, float* db_partial,
+                                       int num_partials, const float* bn_Z, const float* bn_mask,
+                                       const float* bn_scale, const float* bn_shift,
+                                       const float* bn_mean, const float* bn_invstd,
+                                       double* gstats_part, const double* bn_sums, double count,
+                                       int training, void* stream) {
+  if (M < 0 || !W || !dW_partial || !lgnn_tile_fits(M, K, N)) return LGNN_EINVAL;
+  if (num_partials != lgnn_tile_partials(M)) return LGNN_EINVAL;
+  if (M > 0 && (!dY || !X)) return LGNN_EINVAL;
+  if (!bn_Z || !bn_scale || !bn_shift || !bn_mean || !bn_invstd) return LGNN_EINVAL;
+  if (act != LGNN_ACT_NONE && act != LGNN_ACT_ELU) return LGNN_EINVAL;
+  if (act == LGNN_ACT_ELU && !H) return LGNN_EINVAL;
+  if (bn_mode == BN_GSTATS && (!dXpre || !gstats_part)) return LGNN_EINVAL;
+  if (bn_mode == BN_GIN && (act != LGNN_ACT_NONE || (training && (!bn_sums || count <= 0.0))))
+    return LGNN_EINVAL;
+  if (bn_mode != BN_GSTATS && bn_mode != BN_GIN) return LGNN_EINVAL;
+  BnFuse bn = {};
+  bn.part = gstats_part;
+  bn.scale = bn_scale;
+  bn.shift = bn_shift;
+  bn.mean = bn_mean;
+  bn.invstd = bn_invstd;
+  bn.Z = bn_Z;
+  bn.mask = bn_mask;
+  bn.sums = bn_sums;
+  bn.count = count;
+  bn.training = training;
+  hipStream_t s = as_stream(stream);
+  if (M == 0) {
+    if (hipMemsetAsync(dW_partial, 0, (size_t)num_partials * N * K * 4, s) != hipSuccess ||
+        (db_partial && hipMemsetAsync(db_partial, 0, (size_t)num_partials * N * 4, s)) ||
+        (gstats_part &&
+         hipMemsetAsync(gstats_part, 0, (size_t)num_partials * 2 * K * sizeof(double), s)))
+      return (int)hipGetLastError();
+    return LGNN_OK;
+  }
+  const dim3 grid((unsigned)num_partials);
+#define LGNN_TBB(AC, D, BM)                                                                     \
+  hipLaunchKernelGGL((k_bwd<LGNN_GRAD_DIRECT, AC, D, BM>), grid, dim3(NT), 0, s, dY, nullptr,  \
+                     nullptr, 0, nullptr, nullptr, nullptr, 0.f, H, X, M, K, W, N, dXpre,      \
+                     dW_partial, db_partial, nullptr, 0, 0, bn)
+  if (bn_mode == BN_GSTATS) {
+    if (act == LGNN_ACT_ELU) LGNN_TBB(LGNN_ACT_ELU, true, BN_GSTATS);
+    else LGNN_TBB(LGNN_ACT_NONE, true, BN_GSTATS);
+  } else {
+    if (dXpre) LGNN_TBB(LGNN_ACT_NONE, true, BN_GIN);
+    else LGNN_TBB(LGNN_ACT_NONE, false, BN_GIN);
+  }
+#undef LGNN_TBB
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? LGNN_OK : (int)e;
+}
+
 extern "C" int lgnn_tile_count(int64_t M) {
   if (M < 0) return LGNN_EINVAL;
   return (int)((M + lgnn_tile::TM - 1) / lgnn_tile::TM);

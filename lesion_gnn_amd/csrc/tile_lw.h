@@ -66,7 +66,7 @@ __device__ __forceinline__ f32x4 agg_row_global(const TileIdx& ti, int rr,
 // ------------------------------------------------------------------------------------------
 // forward: Y = act(P(X) W^T + b); optional S_out = P(X)
 // ------------------------------------------------------------------------------------------
-template <bool GATHER, int ACT>
+template <bool GATHER, int ACT, int BNM = BN_NONE>
 __device__ __forceinline__ void fwd_tiles(float* A, float* S, TileIdx& ti,
                                           const float* __restrict__ X, int64_t M, int K,
                                           const int32_t* __restrict__ rowptr,
@@ -75,15 +75,28 @@ __device__ __forceinline__ void fwd_tiles(float* A, float* S, TileIdx& ti,
                                           const float* __restrict__ W,
                                           const float* __restrict__ b, int N,
                                           float* __restrict__ Y, float* __restrict__ S_out,
-                                          const int32_t* __restrict__ tmask, int want) {
+                                          const int32_t* __restrict__ tmask, int want,
+                                          const BnFuse& bn = BnFuse{}) {
+  static_assert(BNM == BN_NONE || BNM == BN_STATS || (BNM == BN_IN && !GATHER), "");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, li = lane & 31, hw = wave * 2 + h;
   const int64_t ntiles = (M + TM - 1) / TM;
   const int n = wave * 32 + li;
   const int ncl = n < N ? n : N - 1;
   const bool wave_active = wave * 32 < N;
+  double s0[4] = {0.0, 0.0, 0.0, 0.0}, s1[4] = {0.0, 0.0, 0.0, 0.0};  // BN_STATS
   int64_t t = seek_tile(blockIdx.x, ntiles, tmask, want);
-  if (t >= ntiles) return;
+  if (t >= ntiles) {
+    if constexpr (BNM == BN_STATS) bn_part_write(reinterpret_cast<double*>(A), s0, s1, bn.part, N);
+    return;
+  }
+  // BN_IN: the input columns' constants (k = 4 li ..)
+  f32x4 bsc = {}, bsh = {};
+  if constexpr (BNM == BN_IN) {
+    const int kq = 4 * li < K ? 4 * li : K - 4;
+    bsc = ld4(bn.scale + kq);
+    bsh = ld4(bn.shift + kq);
+  }
   float bf[64];
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
@@ -121,7 +134,23 @@ __device__ __forceinline__ void fwd_tiles(float* A, float* S, TileIdx& ti,
 #pragma unroll
       for (int it = 0; it < 8; ++it) xr[it] = zero4();
     }
-    store_rows_lds(A, xr, M, K, r0);
+    if constexpr (BNM == BN_IN) {  // A = ELU(X * scale + shift) * mask, also to act_out
+      const bool kin = 4 * li < K;
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int rr = hw + 8 * it;
+        const int64_t row = r0 + rr;
+        f32x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = elu_f(fmaf(xr[it][j], bsc[j], bsh[j]));
+        const bool ok = kin && row < M;
+        if (bn.mask && ok) v *= ld4(bn.mask + row * K + 4 * li);
+        if (ok) st4(bn.act_out + row * K + 4 * li, v);
+        st4(A + rr * LDS + 4 * li, sel4(ok, v));
+      }
+    } else {
+      store_rows_lds(A, xr, M, K, r0);
+    }
     if constexpr (GATHER && !(ABL & 2)) idx_store(ti, staged, R, r0);
     __syncthreads();
     // prefetch: next tile's rows and index head fly during this tile's aggregation and MFMAs
@@ -184,17 +213,28 @@ __device__ __forceinline__ void fwd_tiles(float* A, float* S, TileIdx& ti,
 #pragma unroll
       for (int it = 0; it < 8; ++it) {
         const int rr = hw + 8 * it;
-        bst4(bY, (int)((r0 + rr) * N + 4 * li) * 4, ld4(A + rr * LDS + 4 * li));
+        const f32x4 v = ld4(A + rr * LDS + 4 * li);
+        bst4(bY, (int)((r0 + rr) * N + 4 * li) * 4, v);
+        if constexpr (BNM == BN_STATS) {
+          if (r0 + rr < M) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              s0[j] += (double)v[j];
+              s1[j] += (double)v[j] * (double)v[j];
+            }
+          }
+        }
       }
     }
     __syncthreads();
   }
+  if constexpr (BNM == BN_STATS) bn_part_write(reinterpret_cast<double*>(A), s0, s1, bn.part, N);
 }
 
 // ------------------------------------------------------------------------------------------
 // backward: dZ = G ⊙ act'(H); dW += dZ^T S (S = X, direct); db += colsum dZ; dXpre = dZ W
 // ------------------------------------------------------------------------------------------
-template <int GMODE, int ACT, bool DX>
+template <int GMODE, int ACT, bool DX, int BNM = BN_NONE>
 __device__ __forceinline__ void bwd_tiles(
     float* A, float* C, TileIdx& ti,
     const float* __restrict__ dY, const int64_t* __restrict__ batch,
@@ -204,7 +244,9 @@ __device__ __forceinline__ void bwd_tiles(
     const float* __restrict__ W, int N, float* __restrict__ dXpre, float* __restrict__ dWp,
     float* __restrict__ dbp, const int32_t* __restrict__ tmask, int want, int accumulate,
     const float* __restrict__ dlog = nullptr, const float* __restrict__ Wout = nullptr,
-    int nclass = 0) {
+    int nclass = 0, const BnFuse& bn = BnFuse{}) {
+  static_assert(BNM == BN_NONE || (BNM == BN_GSTATS && DX) ||
+                    (BNM == BN_GIN && GMODE == LGNN_GRAD_DIRECT && ACT == LGNN_ACT_NONE), "");
   // GRAD_POOL with dlog: the pooled-output gradient is formed on the fly from the logits'
   // gradient, dP[g][n] = sum_c dlog[g][c] Wout[c][n] (out_proj backward, nclass classes)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -219,6 +261,25 @@ __device__ __forceinline__ void bwd_tiles(
   float dbacc = 0.f;
   const int kx = 32 * wave + li;
   const int kxc = kx < K ? kx : K - 1;
+  // BatchNorm constants of this lane's 4 columns: the dY columns (BN_GIN) or the dX columns
+  // (BN_GSTATS)
+  f32x4 bsc = {}, bsh = {}, bmu = {}, bis = {}, bmg = {}, bmgx = {};
+  double s0[4] = {0.0, 0.0, 0.0, 0.0}, s1[4] = {0.0, 0.0, 0.0, 0.0};
+  if constexpr (BNM != BN_NONE) {
+    const int W4 = BNM == BN_GIN ? N : K;
+    const int cq = 4 * li < W4 ? 4 * li : W4 - 4;
+    bsc = ld4(bn.scale + cq);
+    bsh = ld4(bn.shift + cq);
+    bmu = ld4(bn.mean + cq);
+    bis = ld4(bn.invstd + cq);
+    if (BNM == BN_GIN && bn.training) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bmg[j] = (float)(bn.sums[cq + j] / bn.count);
+        bmgx[j] = (float)(bn.sums[N + cq + j] / bn.count);
+      }
+    }
+  }
 
   // pipeline prologue (TRANSPOSE): the first tile's dY rows and transpose-CSR index block
   f32x4 dr[8];
@@ -294,6 +355,7 @@ __device__ __forceinline__ void bwd_tiles(
         const int64_t rc = row < M ? row : M - 1;
         if constexpr (GMODE == LGNN_GRAD_DIRECT) {
           g[it] = ld4(dY + rc * N + oc);
+          if constexpr (BNM == BN_GIN) hv[it] = ld4(bn.Z + rc * N + oc);  // BN input rows
         } else {
           const int64_t gi = batch[rc];
           if (dlog) {
@@ -318,6 +380,22 @@ __device__ __forceinline__ void bwd_tiles(
         if constexpr (ACT == LGNN_ACT_ELU) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[j] *= elu_grad_from_out(hv[it][j]);
+        }
+        if constexpr (BNM == BN_GIN) {  // dZ = BN backward of the ELU(BN(Z)) * mask output
+          const int64_t row = r0 + rr;
+          const int64_t rc = row < M ? row : M - 1;
+          const f32x4 m = bn.mask ? ld4(bn.mask + rc * N + oc) : f32x4{1.f, 1.f, 1.f, 1.f};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float z = hv[it][j];
+            const float gg = v[j] * bn_elu_grad(z, bsc[j], bsh[j]) * m[j];
+            if (bn.training) {
+              const float xh = (z - bmu[j]) * bis[j];
+              v[j] = bsc[j] * (gg - bmg[j] - xh * bmgx[j]);
+            } else {
+              v[j] = bsc[j] * gg;
+            }
+          }
         }
         st4(C + rr * LDS + 4 * li, sel4(oin && r0 + rr < M, v));
       }
@@ -390,12 +468,29 @@ __device__ __forceinline__ void bwd_tiles(
 #pragma unroll
         for (int it = 0; it < 8; ++it) {
           const int rr = hw + 8 * it;
-          bst4(bdX, (int)((r0 + rr) * K + 4 * li) * 4, ld4(A + rr * LDS + 4 * li));
+          const f32x4 v = ld4(A + rr * LDS + 4 * li);
+          bst4(bdX, (int)((r0 + rr) * K + 4 * li) * 4, v);
+          if constexpr (BNM == BN_GSTATS) {  // the BN backward's batch sums over dX = dA
+            const int64_t row = r0 + rr;
+            if (row < M) {
+              const f32x4 z = ld4(bn.Z + row * K + 4 * li);
+              const f32x4 m = bn.mask ? ld4(bn.mask + row * K + 4 * li)
+                                      : f32x4{1.f, 1.f, 1.f, 1.f};
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const float gg = v[j] * bn_elu_grad(z[j], bsc[j], bsh[j]) * m[j];
+                const float xh = (z[j] - bmu[j]) * bis[j];
+                s0[j] += (double)gg;
+                s1[j] += (double)gg * (double)xh;
+              }
+            }
+          }
         }
       }
     }
     __syncthreads();
   }
+  if constexpr (BNM == BN_GSTATS) bn_part_write(reinterpret_cast<double*>(A), s0, s1, bn.part, K);
   // accumulate: add into slot blockIdx.x (written by the fused stack backward) if this
   // workgroup processed any tile; otherwise leave the slot untouched
   if (accumulate && tfirst >= ntiles) return;

@@ -250,6 +250,51 @@ __device__ __forceinline__ void grid_exit(int32_t* sync) {
 }
 
 // Layer-wise (open-tile) LDS of tile_lw.h's bodies, aliased onto a fused kernel's LDS.
+// BatchNorm1d (+ ELU + dropout mask) folded into the layer-wise kernels (the GIN MLP,
+// Lin -> BN -> ELU -> Lin; norm.hip holds the standalone kernels with the same arithmetic).
+// Template mode BNM of fwd_tiles / bwd_tiles:
+//   BN_STATS   forward epilogue: per-workgroup fp64 sums of Y and Y^2 per column -> part
+//   BN_IN      forward prologue: X := ELU(X * scale + shift) * mask, also written to act_out
+//   BN_GSTATS  backward dX epilogue: sums of g and g * xhat, g = dX * mask * ELU'(Z*sc+sh),
+//              xhat = (Z - mean) * invstd (the BN backward's batch sums) -> part
+//   BN_GIN     backward prologue (DIRECT): dY := scale * (g - sums0/count - xhat * sums1/count)
+//              (training) or scale * g (eval), g as above from the given dY
+// part: [gridDim.x][2 * width] (sum kind, column), every workgroup writes its row.
+enum { BN_NONE = 0, BN_STATS = 1, BN_IN = 2, BN_GSTATS = LGNN_BN_GSTATS, BN_GIN = LGNN_BN_GIN };
+struct BnFuse {
+  double* part;
+  const float* scale;
+  const float* shift;
+  const float* mean;
+  const float* invstd;
+  const float* Z;
+  const float* mask;
+  const double* sums;
+  double count;
+  int training;
+  float* act_out;
+};
+
+// Fold the 8 row groups' fp64 column sums (s0, s1: 4 columns 4 li.. per lane) in a fixed order
+// and write this workgroup's partial row; `red` = 16 KiB of free LDS. Every thread calls it.
+__device__ __forceinline__ void bn_part_write(double* red, const double (&s0)[4],
+                                              const double (&s1)[4], double* part, int N) {
+  const int tid = threadIdx.x, li = tid & 31, hw = tid >> 5;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    red[(hw * 2 + 0) * 128 + 4 * li + j] = s0[j];
+    red[(hw * 2 + 1) * 128 + 4 * li + j] = s1[j];
+  }
+  __syncthreads();
+  if (tid < 256) {
+    const int k = tid >> 7, c = tid & 127;
+    double t = red[k * 128 + c];
+#pragma unroll
+    for (int g = 1; g < 8; ++g) t += red[(g * 2 + k) * 128 + c];
+    if (c < N) part[(int64_t)blockIdx.x * 2 * N + k * N + c] = t;
+  }
+}
+
 struct LwSmem {
   float A[TM * LDS];
   float C[TM * LDS];

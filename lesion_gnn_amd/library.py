@@ -545,7 +545,7 @@ def gin_conv_bwd(dH: Tensor, S: Tensor, Z1: Tensor, A1: Tensor, H: Tensor, W1: T
                  mask: Optional[Tensor], g: list[Tensor], training: bool, count: int,
                  act: int, affine: bool, gathered: bool, eps: float,
                  want_dx: bool) -> list[Tensor]:
-    from .ops import _GINConv
+    from .ops import _GINConv, gin_bn_fused
 
     ctx = _Ctx((want_dx,))
     ctx.save_for_backward(S.contiguous(), Z1, A1, H, W1.contiguous(), W2.contiguous(), mean,
@@ -553,6 +553,7 @@ def gin_conv_bwd(dH: Tensor, S: Tensor, Z1: Tensor, A1: Tensor, H: Tensor, W1: T
     ctx.graph, ctx.self_scale, ctx.gathered = TGraph(g, "gin"), 1.0 + eps, gathered
     ctx.training, ctx.count, ctx.group, ctx.act = training, float(count), None, act
     ctx.affine = affine
+    ctx.bn_fused = gin_bn_fused(W1.shape[1], W1.shape[0], W2.shape[0])
     grads = _GINConv.backward(ctx, dH)[:7]
     return _grad_list(grads, H.device)
 

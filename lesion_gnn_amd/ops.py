@@ -776,6 +776,16 @@ def bn_bwd_apply(dA, Z, mask, scale, shift, mean, invstd, sums, count, training,
     return dZ, dg, db
 
 
+# GIN: BatchNorm folded into the MLP's two linear launches (LGNN_BN_FUSED=0: the separate
+# lgnn_bn_* passes)
+BN_FUSED = os.environ.get("LGNN_BN_FUSED", "1") != "0"
+
+
+def gin_bn_fused(K: int, N1: int, N2: int) -> bool:
+    """True when _GINConv runs its BatchNorm inside the linear kernels (fast-path shapes)."""
+    return BN_FUSED and fast_shape(K, N1) and fast_shape(N1, N2)
+
+
 def _global_count(M: int, group, dev, fixed=None) -> float:
     if group is None:
         return float(M)
@@ -805,6 +815,9 @@ class _GINConv(torch.autograd.Function):
         M = x.size(0)
         N1 = W1.size(0)
         fast = fast_shape(W1.size(1), N1)
+        if gin_bn_fused(W1.size(1), N1, W2.size(0)):
+            return _GINConv._forward_fused(ctx, x, W1, b1, W2, b2, csr, self_scale, graph, bn,
+                                           training, mask, act, group, sync_count, gamma)
         if fast:
             Z1, S = linear_fwd(x, W1, b1, _lib.LGNN_ACT_NONE, csr, self_scale, save_s=True)
         else:
@@ -832,7 +845,110 @@ class _GINConv(torch.autograd.Function):
         return H
 
     @staticmethod
+    def _forward_fused(ctx, x, W1, b1, W2, b2, csr, self_scale, graph, bn, training, mask, act,
+                       group, sync_count, gamma):
+        """BatchNorm folded into the two linear launches (lgnn_node_linear_fwd_bn): the BN
+        statistics in the first one's epilogue, BN + ELU (+ mask) in the second one's prologue.
+        Same arithmetic as the unfused sequence except the fixed order of the fp64 sums."""
+        M, N1 = x.size(0), W1.size(0)
+        dev = x.device
+        P = _lib.load().lgnn_bn_fused_partials(M)
+        Z1 = torch.empty(M, N1, dtype=torch.float32, device=dev)
+        S = torch.empty_like(x)
+        count = float(M)
+        sums = None
+        if training:
+            part = torch.empty(P * 2 * N1, dtype=torch.float64, device=dev)
+            _lib.call("lgnn_node_linear_fwd_bn", _lib.ptr(x), M, x.size(1), _lib.ptr(csr.rowptr),
+                      _lib.ptr(csr.col), _lib.ptr(csr.w), float(self_scale), _lib.ptr(W1),
+                      _lib.ptr(b1), N1, _lib.LGNN_ACT_NONE, _lib.ptr(Z1), _lib.ptr(S),
+                      _lib.ptr(part), None, None, None, None, _s(dev))
+            sums = torch.empty(2 * N1, dtype=torch.float64, device=dev)
+            _lib.call("lgnn_bn_partials_reduce", _lib.ptr(part), P, N1, _lib.ptr(sums), _s(dev))
+            count = _global_count(M, group, dev, sync_count)
+            if count <= 1:
+                raise ValueError("Expected more than 1 value per channel when training")
+            if group is not None:
+                import torch.distributed as dist
+
+                dist.all_reduce(sums, group=group)
+        else:
+            Z1, S = linear_fwd(x, W1, b1, _lib.LGNN_ACT_NONE, csr, self_scale, save_s=True)
+        mean, invstd, scale, shift = bn_finalize(sums, count, bn, training, N1, dev)
+        A1 = torch.empty_like(Z1)
+        N2 = W2.size(0)
+        H = torch.empty(M, N2, dtype=torch.float32, device=dev)
+        _lib.call("lgnn_node_linear_fwd_bn", _lib.ptr(Z1), M, N1, None, None, None, 0.0,
+                  _lib.ptr(W2), _lib.ptr(b2), N2, act, _lib.ptr(H), None, None, _lib.ptr(scale),
+                  _lib.ptr(shift), _lib.ptr(mask), _lib.ptr(A1), _s(dev))
+        ctx.save_for_backward(S, Z1, A1, H, W1, W2, mean, invstd, scale, shift, mask)
+        ctx.graph, ctx.self_scale, ctx.gathered = graph, self_scale, False
+        ctx.training, ctx.count, ctx.group, ctx.act = training, count, group, act
+        ctx.bn_sums = sums
+        ctx.affine = gamma is not None
+        ctx.bn_fused = True
+        return H
+
+    @staticmethod
+    def _backward_fused(ctx, dH):
+        S, Z1, A1, H, W1, W2, mean, invstd, scale, shift, mask = ctx.saved_tensors
+        csr = ctx.graph.csr("gin")
+        M, N1 = Z1.shape
+        N2 = W2.size(0)
+        K = S.size(1)
+        dev = Z1.device
+        P = _lib.load().lgnn_bn_fused_partials(M)
+        red: list = []
+        # Lin2 backward; its dX (= dA1) epilogue also sums the BN backward's (g, g xhat)
+        dA1 = torch.empty_like(Z1)
+        slab2 = torch.empty(P * (N2 * N1 + N2), dtype=torch.float32, device=dev)
+        gpart = torch.empty(P * 2 * N1, dtype=torch.float64, device=dev)
+        _lib.call("lgnn_node_linear_bwd_bn", _lib.LGNN_BN_GSTATS, _lib.ptr(_f32c(dH)), _lib.ptr(H),
+                  ctx.act, _lib.ptr(A1), M, N1, _lib.ptr(W2), N2, _lib.ptr(dA1), _lib.ptr(slab2),
+                  _lib.ptr(slab2[P * N2 * N1:]), P, _lib.ptr(Z1), _lib.ptr(mask),
+                  _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(mean), _lib.ptr(invstd),
+                  _lib.ptr(gpart), None, 0.0, int(ctx.training), _s(dev))
+        dW2 = torch.empty(N2, N1, dtype=torch.float32, device=dev)
+        db2 = torch.empty(N2, dtype=torch.float32, device=dev)
+        red += [(slab2[:P * N2 * N1], P, N2 * N1, dW2), (slab2[P * N2 * N1:], P, N2, db2)]
+        local = torch.empty(2 * N1, dtype=torch.float64, device=dev)
+        _lib.call("lgnn_bn_partials_reduce", _lib.ptr(gpart), P, N1, _lib.ptr(local), _s(dev))
+        sums = local
+        if ctx.training and ctx.group is not None:
+            import torch.distributed as dist
+
+            sums = local.clone()
+            dist.all_reduce(sums, group=ctx.group)
+        # Lin1 backward with the BN backward applied to dA1 as it is loaded
+        want_dx = ctx.needs_input_grad[0]
+        dxpre = torch.empty(M, K, dtype=torch.float32, device=dev) if want_dx else None
+        slab1 = torch.empty(P * (N1 * K + N1), dtype=torch.float32, device=dev)
+        _lib.call("lgnn_node_linear_bwd_bn", _lib.LGNN_BN_GIN, _lib.ptr(dA1), None,
+                  _lib.LGNN_ACT_NONE, _lib.ptr(S), M, K, _lib.ptr(W1), N1, _lib.ptr(dxpre),
+                  _lib.ptr(slab1), _lib.ptr(slab1[P * N1 * K:]), P, _lib.ptr(Z1), _lib.ptr(mask),
+                  _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(mean), _lib.ptr(invstd), None,
+                  _lib.ptr(sums), float(ctx.count), int(ctx.training), _s(dev))
+        dW1 = torch.empty(N1, K, dtype=torch.float32, device=dev)
+        db1 = torch.empty(N1, dtype=torch.float32, device=dev)
+        red += [(slab1[:P * N1 * K], P, N1 * K, dW1), (slab1[P * N1 * K:], P, N1, db1)]
+        reduce_multi(red, dev)
+        dg = dbt = None
+        if ctx.affine:
+            dg = torch.empty(N1, dtype=torch.float32, device=dev)
+            dbt = torch.empty(N1, dtype=torch.float32, device=dev)
+            _lib.call("lgnn_bn_bwd_apply", None, None, None, 0, N1, _lib.ptr(scale),
+                      _lib.ptr(shift), _lib.ptr(mean), _lib.ptr(invstd), _lib.ptr(local), 1.0, 0,
+                      None, _lib.ptr(dg), _lib.ptr(dbt), _s(dev))
+        dx = None
+        if want_dx:
+            dx = spmm_raw(csr.tptr, csr.tidx, csr.tw, ctx.self_scale, dxpre)
+        return (dx, dW1, db1, dg, dbt, dW2, db2, None, None, None, None, None, None, None,
+                None)
+
+    @staticmethod
     def backward(ctx, dH):
+        if getattr(ctx, "bn_fused", False):
+            return _GINConv._backward_fused(ctx, dH)
         S, Z1, A1, H, W1, W2, mean, invstd, scale, shift, mask = ctx.saved_tensors
         csr = ctx.graph.csr("gin")
         dA1, dW2, db2 = linear_bwd(_lib.LGNN_GRAD_DIRECT, _f32c(dH), H=H, act=ctx.act, X=A1, W=W2)
