@@ -255,9 +255,17 @@ int lgnn_bn_bwd_apply(const float* dA, const float* Z, const float* mask, int64_
                       const float* invstd, const double* sums, double count, int training,
                       float* dZ, float* dgamma, float* dbeta, void* stream);
 /* sums[2N] = the fixed-order sum of num_partials fp64 partial rows part[p][2N] (the BN-fused
- * linear kernels below write one row per workgroup). */
+ * linear kernels below write one row per workgroup); dgamma = sums[N..2N), dbeta = sums[0..N)
+ * (each nullable: the backward's affine gradients, as lgnn_bn_bwd_apply's). */
 int lgnn_bn_partials_reduce(const double* part, int num_partials, int N, double* sums,
-                            void* stream);
+                            float* dgamma, float* dbeta, void* stream);
+/* lgnn_bn_partials_reduce + lgnn_bn_finalize (training) in one launch (no SyncBN all-reduce
+ * between them). */
+int lgnn_bn_partials_finalize(const double* part, int num_partials, int N, double* sums,
+                              double count, const float* gamma, const float* beta, float eps,
+                              float momentum, float* running_mean, float* running_var,
+                              int64_t* num_batches_tracked, float* mean, float* invstd,
+                              float* scale, float* shift, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * The GIN MLP's linear layers with BatchNorm folded into them (the same arithmetic as the

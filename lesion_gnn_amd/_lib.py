@@ -82,7 +82,9 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_node_linear_fwd_tiles": (I32, [P, I64, I32, P, P, P, F32, P, P, I32, I32, P, P, P, I32,
                                          P]),
     "lgnn_bn_bwd_apply": (I32, [P, P, P, I64, I32, P, P, P, P, P, F64, I32, P, P, P, P]),
-    "lgnn_bn_partials_reduce": (I32, [P, I32, I32, P, P]),
+    "lgnn_bn_partials_reduce": (I32, [P, I32, I32, P, P, P, P]),
+    "lgnn_bn_partials_finalize": (I32, [P, I32, I32, P, F64, P, P, F32, F32, P, P, P, P, P, P, P,
+                                        P]),
     "lgnn_bn_fused_partials": (I32, [I64]),
     "lgnn_node_linear_fwd_bn": (I32, [P, I64, I32, P, P, P, F32, P, P, I32, I32, P, P, P, P, P, P,
                                       P, P]),

@@ -130,28 +130,24 @@ __global__ __launch_bounds__(NT) void k_colsum_reduce(const double* __restrict__
   }
 }
 
-// Per-column constants. training: batch mean / biased var from sums (count rows), running stats
-// updated with the unbiased var (torch.nn.BatchNorm1d, momentum m):
+// Per-column constants. training: batch mean / biased var from the sums s0 = sum z, s1 = sum z^2
+// (count rows), running stats updated with the unbiased var (torch.nn.BatchNorm1d, momentum m):
 //   running = (1 - m) * running + m * stat.  eval: running stats used as is.
 // scale = gamma * invstd, shift = beta - mean * scale (gamma/beta NULL: 1 / 0).
-__global__ __launch_bounds__(NT) void k_bn_finalize(const double* __restrict__ sums, double count,
-                                                    const float* __restrict__ gamma,
-                                                    const float* __restrict__ beta, float eps,
-                                                    float momentum, int training, int N,
-                                                    float* __restrict__ running_mean,
-                                                    float* __restrict__ running_var,
-                                                    int64_t* __restrict__ num_batches_tracked,
-                                                    float* __restrict__ mean_out,
-                                                    float* __restrict__ invstd_out,
-                                                    float* __restrict__ scale,
-                                                    float* __restrict__ shift) {
-  const int c = blockIdx.x * NT + threadIdx.x;
-  if (c == 0 && training && num_batches_tracked) *num_batches_tracked += 1;
-  if (c >= N) return;
+__device__ __forceinline__ void bn_finalize_col(int c, double s0, double s1, double count,
+                                                const float* __restrict__ gamma,
+                                                const float* __restrict__ beta, float eps,
+                                                float momentum, int training,
+                                                float* __restrict__ running_mean,
+                                                float* __restrict__ running_var,
+                                                float* __restrict__ mean_out,
+                                                float* __restrict__ invstd_out,
+                                                float* __restrict__ scale,
+                                                float* __restrict__ shift) {
   double mean, var;
   if (training) {
-    mean = sums[c] / count;
-    var = sums[N + c] / count - mean * mean;
+    mean = s0 / count;
+    var = s1 / count - mean * mean;
     if (var < 0.0) var = 0.0;
     if (running_mean) {
       const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
@@ -170,6 +166,73 @@ __global__ __launch_bounds__(NT) void k_bn_finalize(const double* __restrict__ s
   invstd_out[c] = is;
   scale[c] = sc;
   shift[c] = (beta ? beta[c] : 0.f) - m * sc;
+}
+
+__global__ __launch_bounds__(NT) void k_bn_finalize(const double* __restrict__ sums, double count,
+                                                    const float* __restrict__ gamma,
+                                                    const float* __restrict__ beta, float eps,
+                                                    float momentum, int training, int N,
+                                                    float* __restrict__ running_mean,
+                                                    float* __restrict__ running_var,
+                                                    int64_t* __restrict__ num_batches_tracked,
+                                                    float* __restrict__ mean_out,
+                                                    float* __restrict__ invstd_out,
+                                                    float* __restrict__ scale,
+                                                    float* __restrict__ shift) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c == 0 && training && num_batches_tracked) *num_batches_tracked += 1;
+  if (c >= N) return;
+  bn_finalize_col(c, training ? sums[c] : 0.0, training ? sums[N + c] : 0.0, count, gamma, beta,
+                  eps, momentum, training, running_mean, running_var, mean_out, invstd_out,
+                  scale, shift);
+}
+
+// The BN-fused linear kernels' partial rows [P][2N] -> sums (fixed order: 8 strided groups per
+// column, folded in group order); then (FIN) the per-column constants as k_bn_finalize, and/or
+// (PG) the affine parameters' gradients as k_bn_param_grads: one launch instead of two.
+template <bool FIN, bool PG>
+__global__ __launch_bounds__(NT) void k_bn_reduce_tail(
+    const double* __restrict__ part, int P, int N, double* __restrict__ sums, double count,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
+    int training, float* __restrict__ running_mean, float* __restrict__ running_var,
+    int64_t* __restrict__ num_batches_tracked, float* __restrict__ mean_out,
+    float* __restrict__ invstd_out, float* __restrict__ scale, float* __restrict__ shift,
+    float* __restrict__ dg, float* __restrict__ db) {
+  // 8 columns per block, 32 strided groups of partial rows per column (latency: ~P/32 loads
+  // per thread, 4 in flight)
+  constexpr int RCOL = 8, RGRP = NT / RCOL;
+  __shared__ double red[RGRP][2][RCOL];
+  const int cl = threadIdx.x % RCOL, g = threadIdx.x / RCOL;
+  const int c = blockIdx.x * RCOL + cl;
+  double s0 = 0.0, s1 = 0.0;
+  if (c < N) {
+#pragma unroll 4
+    for (int p = g; p < P; p += RGRP) {
+      s0 += part[(int64_t)p * 2 * N + c];
+      s1 += part[(int64_t)p * 2 * N + N + c];
+    }
+  }
+  red[g][0][cl] = s0;
+  red[g][1][cl] = s1;
+  __syncthreads();
+  if (g != 0 || c >= N) return;
+  double t0 = red[0][0][cl], t1 = red[0][1][cl];
+#pragma unroll 8
+  for (int k = 1; k < RGRP; ++k) {
+    t0 += red[k][0][cl];
+    t1 += red[k][1][cl];
+  }
+  sums[c] = t0;
+  sums[N + c] = t1;
+  if constexpr (PG) {
+    if (dg) dg[c] = (float)t1;
+    if (db) db[c] = (float)t0;
+  }
+  if constexpr (FIN) {
+    if (c == 0 && training && num_batches_tracked) *num_batches_tracked += 1;
+    bn_finalize_col(c, t0, t1, count, gamma, beta, eps, momentum, training, running_mean,
+                    running_var, mean_out, invstd_out, scale, shift);
+  }
 }
 
 // A = ELU(Z * scale + shift) [* mask]; per-column constants in registers (thread mapping above)
@@ -322,10 +385,35 @@ extern "C" int lgnn_bn_bwd_stats(const float* dA, const float* Z, const float* m
 }
 
 extern "C" int lgnn_bn_partials_reduce(const double* part, int num_partials, int N,
-                                       double* sums, void* stream) {
+                                       double* sums, float* dgamma, float* dbeta, void* stream) {
   if (num_partials <= 0 || N <= 0 || !part || !sums) return LGNN_EINVAL;
-  hipLaunchKernelGGL(k_colsum_reduce, dim3((2 * N + NT / RED_SPLIT - 1) / (NT / RED_SPLIT)),
-                     dim3(NT), 0, as_stream(stream), part, num_partials, 2 * N, sums);
+  const dim3 grid((unsigned)((N + 7) / 8));
+  if (dgamma || dbeta)
+    hipLaunchKernelGGL((k_bn_reduce_tail<false, true>), grid, dim3(NT), 0, as_stream(stream),
+                       part, num_partials, N, sums, 0.0, nullptr, nullptr, 0.f, 0.f, 0, nullptr,
+                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, dgamma, dbeta);
+  else
+    hipLaunchKernelGGL((k_bn_reduce_tail<false, false>), grid, dim3(NT), 0, as_stream(stream),
+                       part, num_partials, N, sums, 0.0, nullptr, nullptr, 0.f, 0.f, 0, nullptr,
+                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+  LGNN_LAUNCH_CHECK();
+  return LGNN_OK;
+}
+
+extern "C" int lgnn_bn_partials_finalize(const double* part, int num_partials, int N,
+                                         double* sums, double count, const float* gamma,
+                                         const float* beta, float eps, float momentum,
+                                         float* running_mean, float* running_var,
+                                         int64_t* num_batches_tracked, float* mean,
+                                         float* invstd, float* scale, float* shift,
+                                         void* stream) {
+  if (num_partials <= 0 || N <= 0 || !part || !sums || count <= 0.0) return LGNN_EINVAL;
+  if (!mean || !invstd || !scale || !shift) return LGNN_EINVAL;
+  if ((running_mean == nullptr) != (running_var == nullptr)) return LGNN_EINVAL;
+  hipLaunchKernelGGL((k_bn_reduce_tail<true, false>), dim3((unsigned)((N + 7) / 8)), dim3(NT),
+                     0, as_stream(stream), part, num_partials, N, sums, count, gamma, beta, eps,
+                     momentum, 1, running_mean, running_var, num_batches_tracked, mean, invstd,
+                     scale, shift, nullptr, nullptr);
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
 }

@@ -722,7 +722,10 @@ def bn_stats(Z: torch.Tensor) -> torch.Tensor:
     return sums
 
 
-def bn_finalize(sums, count: float, bn: torch.nn.BatchNorm1d, training: bool, N: int, dev):
+def bn_finalize(sums, count: float, bn: torch.nn.BatchNorm1d, training: bool, N: int, dev,
+                part: tuple | None = None):
+    """The BN constants (+ running-stat update). part = (partial rows, P): sums are first reduced
+    from the BN-fused kernels' partial rows into `sums`, in the same launch (training only)."""
     f = dict(dtype=torch.float32, device=dev)
     mean, invstd, scale, shift = (torch.empty(N, **f) for _ in range(4))
     track = bn.track_running_stats and bn.running_mean is not None
@@ -732,6 +735,13 @@ def bn_finalize(sums, count: float, bn: torch.nn.BatchNorm1d, training: bool, N:
     momentum = bn.momentum if bn.momentum is not None else 0.1
     if nbt is not None and bn.momentum is None:  # cumulative moving average (torch semantics)
         momentum = 1.0 / float(bn.num_batches_tracked.item() + 1)
+    if part is not None:
+        _lib.call("lgnn_bn_partials_finalize", _lib.ptr(part[0]), part[1], N, _lib.ptr(sums),
+                  float(count), _lib.ptr(bn.weight) if bn.affine else None,
+                  _lib.ptr(bn.bias) if bn.affine else None, float(bn.eps), float(momentum),
+                  _lib.ptr(rm), _lib.ptr(rv), _lib.ptr(nbt), _lib.ptr(mean), _lib.ptr(invstd),
+                  _lib.ptr(scale), _lib.ptr(shift), _s(dev))
+        return mean, invstd, scale, shift
     _lib.call("lgnn_bn_finalize", _lib.ptr(sums), float(count),
               _lib.ptr(bn.weight) if bn.affine else None, _lib.ptr(bn.bias) if bn.affine else None,
               float(bn.eps), float(momentum), int(training), N, _lib.ptr(rm), _lib.ptr(rv),
@@ -864,17 +874,22 @@ class _GINConv(torch.autograd.Function):
                       _lib.ptr(b1), N1, _lib.LGNN_ACT_NONE, _lib.ptr(Z1), _lib.ptr(S),
                       _lib.ptr(part), None, None, None, None, _s(dev))
             sums = torch.empty(2 * N1, dtype=torch.float64, device=dev)
-            _lib.call("lgnn_bn_partials_reduce", _lib.ptr(part), P, N1, _lib.ptr(sums), _s(dev))
             count = _global_count(M, group, dev, sync_count)
             if count <= 1:
                 raise ValueError("Expected more than 1 value per channel when training")
-            if group is not None:
+            if group is None:  # sums + the BN constants in one launch
+                mean, invstd, scale, shift = bn_finalize(sums, count, bn, training, N1, dev,
+                                                         part=(part, P))
+            else:
                 import torch.distributed as dist
 
+                _lib.call("lgnn_bn_partials_reduce", _lib.ptr(part), P, N1, _lib.ptr(sums), None,
+                          None, _s(dev))
                 dist.all_reduce(sums, group=group)
+                mean, invstd, scale, shift = bn_finalize(sums, count, bn, training, N1, dev)
         else:
             Z1, S = linear_fwd(x, W1, b1, _lib.LGNN_ACT_NONE, csr, self_scale, save_s=True)
-        mean, invstd, scale, shift = bn_finalize(sums, count, bn, training, N1, dev)
+            mean, invstd, scale, shift = bn_finalize(sums, count, bn, training, N1, dev)
         A1 = torch.empty_like(Z1)
         N2 = W2.size(0)
         H = torch.empty(M, N2, dtype=torch.float32, device=dev)
@@ -912,7 +927,12 @@ class _GINConv(torch.autograd.Function):
         db2 = torch.empty(N2, dtype=torch.float32, device=dev)
         red += [(slab2[:P * N2 * N1], P, N2 * N1, dW2), (slab2[P * N2 * N1:], P, N2, db2)]
         local = torch.empty(2 * N1, dtype=torch.float64, device=dev)
-        _lib.call("lgnn_bn_partials_reduce", _lib.ptr(gpart), P, N1, _lib.ptr(local), _s(dev))
+        dg = dbt = None
+        if ctx.affine:  # the affine gradients come out of the same launch (local sums)
+            dg = torch.empty(N1, dtype=torch.float32, device=dev)
+            dbt = torch.empty(N1, dtype=torch.float32, device=dev)
+        _lib.call("lgnn_bn_partials_reduce", _lib.ptr(gpart), P, N1, _lib.ptr(local),
+                  _lib.ptr(dg), _lib.ptr(dbt), _s(dev))
         sums = local
         if ctx.training and ctx.group is not None:
             import torch.distributed as dist
@@ -932,13 +952,6 @@ class _GINConv(torch.autograd.Function):
         db1 = torch.empty(N1, dtype=torch.float32, device=dev)
         red += [(slab1[:P * N1 * K], P, N1 * K, dW1), (slab1[P * N1 * K:], P, N1, db1)]
         reduce_multi(red, dev)
-        dg = dbt = None
-        if ctx.affine:
-            dg = torch.empty(N1, dtype=torch.float32, device=dev)
-            dbt = torch.empty(N1, dtype=torch.float32, device=dev)
-            _lib.call("lgnn_bn_bwd_apply", None, None, None, 0, N1, _lib.ptr(scale),
-                      _lib.ptr(shift), _lib.ptr(mean), _lib.ptr(invstd), _lib.ptr(local), 1.0, 0,
-                      None, _lib.ptr(dg), _lib.ptr(dbt), _s(dev))
         dx = None
         if want_dx:
             dx = spmm_raw(csr.tptr, csr.tidx, csr.tw, ctx.self_scale, dxpre)
