@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 13
+#define LGNN_ABI_VERSION 14
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -287,6 +287,23 @@ int lgnn_bn_partials_finalize(const double* part, int num_partials, int N, doubl
  * ------------------------------------------------------------------------------------------- */
 #define LGNN_BN_GSTATS 3
 #define LGNN_BN_GIN 4
+/* Split-3 variants (bf16 MFMA at fp32 accuracy, liblgnn lin3.hip) of the two calls below: the
+ * same arguments with `planes` / `planes_t` (lgnn_weight_planes of W: the weight and, for dX, the
+ * transposed planes of this one layer) in place of W; either BN option (or none: stats_part and
+ * bn_scale NULL, bn_mode 0) as lgnn_node_linear_fwd_bn / _bwd_bn. */
+int lgnn_node_linear_fwd_s3(const float* X, int64_t M, int K, const int32_t* rowptr,
+                            const int32_t* col, const float* w, float self_scale,
+                            const uint16_t* planes, const float* b, int N, int act, float* Y,
+                            float* S_out, double* stats_part, const float* bn_scale,
+                            const float* bn_shift, const float* bn_mask, float* bn_out,
+                            void* stream);
+int lgnn_node_linear_bwd_s3(int bn_mode, const float* dY, const float* H, int act,
+                            const float* X, int64_t M, int K, const uint16_t* planes_t, int N,
+                            float* dXpre, float* dW_partial, float* db_partial, int num_partials,
+                            const float* bn_Z, const float* bn_mask, const float* bn_scale,
+                            const float* bn_shift, const float* bn_mean, const float* bn_invstd,
+                            double* gstats_part, const double* bn_sums, double count,
+                            int training, void* stream);
 int lgnn_bn_fused_partials(int64_t num_rows);
 int lgnn_node_linear_fwd_bn(const float* X, int64_t M, int K, const int32_t* rowptr,
                             const int32_t* col, const float* w, float self_scale, const float* W,

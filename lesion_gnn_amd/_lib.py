@@ -90,6 +90,10 @@ SIGNATURES: dict[str, tuple] = {
                                       P, P]),
     "lgnn_node_linear_bwd_bn": (I32, [I32, P, P, I32, P, I64, I32, P, I32, P, P, P, I32, P, P, P,
                                       P, P, P, P, P, F64, I32, P]),
+    "lgnn_node_linear_fwd_s3": (I32, [P, I64, I32, P, P, P, F32, P, P, I32, I32, P, P, P, P, P, P,
+                                      P, P]),
+    "lgnn_node_linear_bwd_s3": (I32, [I32, P, P, I32, P, I64, I32, P, I32, P, P, P, I32, P, P, P,
+                                      P, P, P, P, P, F64, I32, P]),
     "lgnn_gcn_stack_bwd_s3f": (I32, [P, P, P, I32, I64, P, P, P, P, I64, I32, P, P, P, P, P,
                                      I32, P, P, P]),
     "lgnn_gcn_stack_fwd_s3_all": (I32, [P, I64, I32, I32, P, P, P, I32, P, P, P, P, P, P, P, P, P]),
@@ -102,7 +106,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 _lib = None
 

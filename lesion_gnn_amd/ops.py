@@ -791,6 +791,13 @@ def bn_bwd_apply(dA, Z, mask, scale, shift, mean, invstd, sums, count, training,
 BN_FUSED = os.environ.get("LGNN_BN_FUSED", "1") != "0"
 
 
+# GEMM arithmetic of the BN-fused GIN MLP kernels: "f32" = fp32 MFMA (tile_lw.h, the default),
+# "s3" = split-3 bf16 MFMA (lin3.hip, fp32 accuracy). The layer-wise kernels are bound by the
+# per-tile load latency, not by the MFMA pipe: at C4 the split-3 pair measured 0.735 ms per step
+# against 0.703 for fp32 (same box), so split-3 stays opt-in (LGNN_GIN_MFMA=s3).
+GIN_MFMA = os.environ.get("LGNN_GIN_MFMA", "f32")
+
+
 def gin_bn_fused(K: int, N1: int, N2: int) -> bool:
     """True when _GINConv runs its BatchNorm inside the linear kernels (fast-path shapes)."""
     return BN_FUSED and fast_shape(K, N1) and fast_shape(N1, N2)
@@ -867,10 +874,18 @@ class _GINConv(torch.autograd.Function):
         S = torch.empty_like(x)
         count = float(M)
         sums = None
+        s3 = GIN_MFMA == "s3"  # split-3 kernels: both layers' weight planes in one launch
+        fname = "lgnn_node_linear_fwd_s3" if s3 else "lgnn_node_linear_fwd_bn"
+        if s3:
+            planes, planes_t = weight_planes([W1, W2], x.size(1), transposed=True)
+            w1, w2 = planes[0].data_ptr(), planes[1].data_ptr()
+            ctx.gin_planes_t = planes_t
+        else:
+            w1, w2 = W1.data_ptr(), W2.data_ptr()
         if training:
             part = torch.empty(P * 2 * N1, dtype=torch.float64, device=dev)
-            _lib.call("lgnn_node_linear_fwd_bn", _lib.ptr(x), M, x.size(1), _lib.ptr(csr.rowptr),
-                      _lib.ptr(csr.col), _lib.ptr(csr.w), float(self_scale), _lib.ptr(W1),
+            _lib.call(fname, _lib.ptr(x), M, x.size(1), _lib.ptr(csr.rowptr),
+                      _lib.ptr(csr.col), _lib.ptr(csr.w), float(self_scale), w1,
                       _lib.ptr(b1), N1, _lib.LGNN_ACT_NONE, _lib.ptr(Z1), _lib.ptr(S),
                       _lib.ptr(part), None, None, None, None, _s(dev))
             sums = torch.empty(2 * N1, dtype=torch.float64, device=dev)
@@ -888,14 +903,20 @@ class _GINConv(torch.autograd.Function):
                 dist.all_reduce(sums, group=group)
                 mean, invstd, scale, shift = bn_finalize(sums, count, bn, training, N1, dev)
         else:
-            Z1, S = linear_fwd(x, W1, b1, _lib.LGNN_ACT_NONE, csr, self_scale, save_s=True)
+            if s3:
+                _lib.call(fname, _lib.ptr(x), M, x.size(1), _lib.ptr(csr.rowptr),
+                          _lib.ptr(csr.col), _lib.ptr(csr.w), float(self_scale), w1,
+                          _lib.ptr(b1), N1, _lib.LGNN_ACT_NONE, _lib.ptr(Z1), _lib.ptr(S),
+                          None, None, None, None, None, _s(dev))
+            else:
+                Z1, S = linear_fwd(x, W1, b1, _lib.LGNN_ACT_NONE, csr, self_scale, save_s=True)
             mean, invstd, scale, shift = bn_finalize(sums, count, bn, training, N1, dev)
         A1 = torch.empty_like(Z1)
         N2 = W2.size(0)
         H = torch.empty(M, N2, dtype=torch.float32, device=dev)
-        _lib.call("lgnn_node_linear_fwd_bn", _lib.ptr(Z1), M, N1, None, None, None, 0.0,
-                  _lib.ptr(W2), _lib.ptr(b2), N2, act, _lib.ptr(H), None, None, _lib.ptr(scale),
-                  _lib.ptr(shift), _lib.ptr(mask), _lib.ptr(A1), _s(dev))
+        _lib.call(fname, _lib.ptr(Z1), M, N1, None, None, None, 0.0, w2, _lib.ptr(b2), N2, act,
+                  _lib.ptr(H), None, None, _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(mask),
+                  _lib.ptr(A1), _s(dev))
         ctx.save_for_backward(S, Z1, A1, H, W1, W2, mean, invstd, scale, shift, mask)
         ctx.graph, ctx.self_scale, ctx.gathered = graph, self_scale, False
         ctx.training, ctx.count, ctx.group, ctx.act = training, count, group, act
@@ -914,12 +935,22 @@ class _GINConv(torch.autograd.Function):
         dev = Z1.device
         P = _lib.load().lgnn_bn_fused_partials(M)
         red: list = []
+        s3 = GIN_MFMA == "s3"
+        fname = "lgnn_node_linear_bwd_s3" if s3 else "lgnn_node_linear_bwd_bn"
+        if s3:  # the forward's transposed planes (rebuilt when the ctx does not carry them)
+            planes_t = getattr(ctx, "gin_planes_t", None)
+            if planes_t is None:
+                planes_t = weight_planes([W1, W2], K, transposed=True)[1]
+            w1 = planes_t.data_ptr()
+            w2 = w1 + 2 * 3 * 128 * 128
+        else:
+            w1, w2 = W1.data_ptr(), W2.data_ptr()
         # Lin2 backward; its dX (= dA1) epilogue also sums the BN backward's (g, g xhat)
         dA1 = torch.empty_like(Z1)
         slab2 = torch.empty(P * (N2 * N1 + N2), dtype=torch.float32, device=dev)
         gpart = torch.empty(P * 2 * N1, dtype=torch.float64, device=dev)
-        _lib.call("lgnn_node_linear_bwd_bn", _lib.LGNN_BN_GSTATS, _lib.ptr(_f32c(dH)), _lib.ptr(H),
-                  ctx.act, _lib.ptr(A1), M, N1, _lib.ptr(W2), N2, _lib.ptr(dA1), _lib.ptr(slab2),
+        _lib.call(fname, _lib.LGNN_BN_GSTATS, _lib.ptr(_f32c(dH)), _lib.ptr(H),
+                  ctx.act, _lib.ptr(A1), M, N1, w2, N2, _lib.ptr(dA1), _lib.ptr(slab2),
                   _lib.ptr(slab2[P * N2 * N1:]), P, _lib.ptr(Z1), _lib.ptr(mask),
                   _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(mean), _lib.ptr(invstd),
                   _lib.ptr(gpart), None, 0.0, int(ctx.training), _s(dev))
@@ -943,8 +974,8 @@ class _GINConv(torch.autograd.Function):
         want_dx = ctx.needs_input_grad[0]
         dxpre = torch.empty(M, K, dtype=torch.float32, device=dev) if want_dx else None
         slab1 = torch.empty(P * (N1 * K + N1), dtype=torch.float32, device=dev)
-        _lib.call("lgnn_node_linear_bwd_bn", _lib.LGNN_BN_GIN, _lib.ptr(dA1), None,
-                  _lib.LGNN_ACT_NONE, _lib.ptr(S), M, K, _lib.ptr(W1), N1, _lib.ptr(dxpre),
+        _lib.call(fname, _lib.LGNN_BN_GIN, _lib.ptr(dA1), None,
+                  _lib.LGNN_ACT_NONE, _lib.ptr(S), M, K, w1, N1, _lib.ptr(dxpre),
                   _lib.ptr(slab1), _lib.ptr(slab1[P * N1 * K:]), P, _lib.ptr(Z1), _lib.ptr(mask),
                   _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(mean), _lib.ptr(invstd), None,
                   _lib.ptr(sums), float(ctx.count), int(ctx.training), _s(dev))
