@@ -22,10 +22,14 @@ struct AdamJobs {
   float* m[LGNN_MAX_ADAM];
   float* v[LGNN_MAX_ADAM];
   int64_t off[LGNN_MAX_ADAM + 1];  // prefix of the element counts
+  int boff[LGNN_MAX_ADAM + 1];     // prefix of the workgroups per tensor
   int n;
 };
 
-// blockIdx.y = tensor (uniform: its pointers are scalar loads), blockIdx.x strides its elements
+constexpr int kE = 2;  // elements per thread: workgroups in proportion to each tensor's size
+
+// 1-D grid: workgroup b takes tensor j with boff[j] <= b < boff[j + 1] (uniform: its pointers are
+// scalar loads) and strides that tensor's elements with the tensor's other workgroups
 __global__ __launch_bounds__(kT) void k_adam(AdamJobs J, float* __restrict__ step,
                                              unsigned int* __restrict__ ticket, float lr,
                                              float beta1, float beta2, float eps, float wd,
@@ -34,13 +38,16 @@ __global__ __launch_bounds__(kT) void k_adam(AdamJobs J, float* __restrict__ ste
   const float bc1 = 1.f - powf(beta1, t);
   const float bc2s = sqrtf(1.f - powf(beta2, t));
   const float step_size = lr / bc1;
-  const int j = blockIdx.y;
+  int j = 0;
+  while (j + 1 < J.n && J.boff[j + 1] <= (int)blockIdx.x) ++j;
+  const int lb = (int)blockIdx.x - J.boff[j], nb = J.boff[j + 1] - J.boff[j];
   const int64_t n = J.off[j + 1] - J.off[j];
   float* __restrict__ P = J.p[j];
   const float* __restrict__ G = J.g[j];
   float* __restrict__ Mv = J.m[j];
   float* __restrict__ Vv = J.v[j];
-  for (int64_t k = (int64_t)blockIdx.x * kT + threadIdx.x; k < n; k += (int64_t)gridDim.x * kT) {
+#pragma unroll 2
+  for (int64_t k = (int64_t)lb * kT + threadIdx.x; k < n; k += (int64_t)nb * kT) {
     float p = P[k];
     float g = G[k];
     if (maximize) g = -g;
@@ -57,7 +64,7 @@ __global__ __launch_bounds__(kT) void k_adam(AdamJobs J, float* __restrict__ ste
   __syncthreads();
   if (threadIdx.x == 0) {
     __threadfence();
-    if (atomicAdd(ticket, 1u) == gridDim.x * gridDim.y - 1) {
+    if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
       step[0] = t;
       *ticket = 0u;
       __threadfence();
@@ -78,6 +85,7 @@ extern "C" int lgnn_adam_step(int n, float* const* params, const float* const* g
   AdamJobs J = {};
   J.n = n;
   J.off[0] = 0;
+  J.boff[0] = 0;
   for (int i = 0; i < n; ++i) {
     if (numels[i] < 0 || (numels[i] > 0 && (!params[i] || !grads[i] || !exp_avg[i] ||
         !exp_avg_sq[i])))
@@ -87,13 +95,11 @@ extern "C" int lgnn_adam_step(int n, float* const* params, const float* const* g
     J.m[i] = exp_avg[i];
     J.v[i] = exp_avg_sq[i];
     J.off[i + 1] = J.off[i] + numels[i];
+    const int64_t nb = (numels[i] + kE * kT - 1) / (kE * kT);
+    J.boff[i + 1] = J.boff[i] + (int)(nb > 0 ? nb : 1);
   }
-  int64_t mx = 1;
-  for (int i = 0; i < n; ++i) mx = numels[i] > mx ? numels[i] : mx;
-  // few workgroups (the ticket is one contended atomic per workgroup): 8+ elements per thread
-  int64_t g = (mx + 8 * kT - 1) / (8 * kT);
-  if (g > 64) g = 64;
-  hipLaunchKernelGGL(k_adam, dim3((unsigned)g, (unsigned)(n > 0 ? n : 1)), dim3(kT), 0,
+  if (n == 0) J.boff[1] = 1;
+  hipLaunchKernelGGL(k_adam, dim3((unsigned)J.boff[n > 0 ? n : 1]), dim3(kT), 0,
                      as_stream(stream), J, step, ticket, lr, beta1, beta2, eps, weight_decay,
                      decoupled, maximize, advance);
   LGNN_LAUNCH_CHECK();

@@ -458,6 +458,14 @@ def mm_dense(a: torch.Tensor, b: torch.Tensor, bf16: bool) -> torch.Tensor:
     return torch.mm(a, b)
 
 
+def addmm_dense(bias: torch.Tensor, a: torch.Tensor, b: torch.Tensor, bf16: bool) -> torch.Tensor:
+    """bias + a @ b with the bias added in the library GEMM's epilogue (no separate add pass)."""
+    if bf16:
+        return torch.addmm(bias, a.to(torch.bfloat16), b.to(torch.bfloat16),
+                           out_dtype=torch.float32)
+    return torch.addmm(bias, a, b)
+
+
 def dw_dense(dy: torch.Tensor, x: torch.Tensor, bf16: bool) -> torch.Tensor:
     """dW = dy^T x over M rows (M >> N, K): split-K — S row chunks as one batched GEMM, then a
     fixed-order sum over the chunks (deterministic). The library's single GEMM parallelises
@@ -493,9 +501,7 @@ class _DenseLinear(torch.autograd.Function):
         x, W = _f32c(x), _f32c(W)
         if bf16:  # each operand rounded once; the backward reuses the bf16 copies
             x, W = x.to(torch.bfloat16), W.to(torch.bfloat16)
-        y = mm_dense(x, W.t(), bf16)
-        if b is not None:
-            y += b
+        y = addmm_dense(_f32c(b), x, W.t(), bf16) if b is not None else mm_dense(x, W.t(), bf16)
         ctx.save_for_backward(x, W)
         ctx.bf16, ctx.has_b = bf16, b is not None
         return y
