@@ -13,7 +13,9 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblgnn.so")
+# LGNN_LIB_PATH: an alternative build of the same library (A/B timing of kernel variants,
+# tools/ab_lib.sh); the default is the in-tree build
+LIB_PATH = os.environ.get("LGNN_LIB_PATH") or os.path.join(_HERE, "liblgnn.so")
 
 LGNN_LOOPS_KEEP, LGNN_LOOPS_REMAINING, LGNN_LOOPS_READD = 0, 1, 2
 LGNN_NORM_NONE, LGNN_NORM_GCN = 0, 1

@@ -859,6 +859,9 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
         const int tq = fresh_tid();
         const int64_t row = tn * TM + tq;
         pre_g = (has_next && tq < TM && row < M) ? a.batch[row] : 0;
+        // this tile's X rows for the in_proj phase: in flight during the last conv's dW / dH
+        const int h = (tq >> 5) & 1, k = 32 * (tq >> 6) + (tq & 31);
+        load_pt(xp, a.X, (ABL & 16) ? 0 : M, r0, a.width[0], k, a.width[0], h);
       }
       STAMP(stamp++);
       // dW_l += G^T H: A = G (P layout, node steps), B = H image rows k = 32 kb + li
@@ -930,7 +933,6 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
       {
         const int tq = fresh_tid();
         const int h = (tq >> 5) & 1, li = tq & 31, k = 32 * (tq >> 6) + li;
-        load_pt(xp, a.X, (ABL & 16) ? 0 : M, r0, K, k, K, h);
         float sacc = 0.f;
 #pragma unroll
         for (int q = 0; q < 2; ++q)
