@@ -81,8 +81,8 @@ def step_bytes(b, wl) -> float:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
     ap.add_argument("--graphs-per-gpu", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -262,10 +262,12 @@ def time_dominant_kernels(model, b, dev):
                       planes_t.data_ptr(), Hp, (ctypes.c_int * (L + 2))(*widths), dWp, dbp, P,
                       open_.data_ptr(), _lib.ptr(adjt), s)
 
-        out.append({"kernel": f"lgnn_s3::k_s3_fbwd<{L + 1}> (fused GCN backward, all layers, "
+        out.append({"kernel": f"lgnn_s3::k_s3_fbwd<{L + 1}, {str(ops.ADJT).lower()}> (fused GCN "
+                              "backward, all layers, "
                               "split-3 bf16 MFMA)",
                     "ms": _time_launches(bwd_s3f, dev), "flops": bwd_flops,
-                    "peak": MFMA_S3_PEAK_TF, "trace_name": f"void lgnn_s3::k_s3_fbwd<{L + 1}>"})
+                    "peak": MFMA_S3_PEAK_TF,
+                    "trace_name": f"void lgnn_s3::k_s3_fbwd<{L + 1}, {str(ops.ADJT).lower()}>"})
     else:
         out.append({"kernel": f"lgnn_tile::k_stack_bwd<{L + 1}> (fused GCN backward, all "
                               "layers)",
@@ -286,7 +288,7 @@ def time_dominant_kernels(model, b, dev):
         out.append({"kernel": "lgnn_s3::k_s3_fwd<true> (fused GCN forward, all layers, "
                               "split-3 bf16 MFMA)",
                     "ms": _time_launches(fwd, dev), "flops": lin + agg, "peak": MFMA_S3_PEAK_TF,
-                    "trace_name": "void lgnn_s3::k_s3_fwd<true>"})
+                    "trace_name": "void lgnn_s3::k_s3_fwd<true>("})
         return out
 
     def fwd():
