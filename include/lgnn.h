@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 14
+#define LGNN_ABI_VERSION 16
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -287,6 +287,21 @@ int lgnn_bn_partials_finalize(const double* part, int num_partials, int N, doubl
  * ------------------------------------------------------------------------------------------- */
 #define LGNN_BN_GSTATS 3
 #define LGNN_BN_GIN 4
+/* lgnn_node_linear_bwd_bn with the layer's output gradient taken from the pooled readout
+ * (LGNN_GRAD_POOL, bn_mode LGNN_BN_GSTATS only): row i's gradient is
+ *   (dlogits[batch[i]] . Wout)[n] (/ |graph| when pool_mean),
+ * i.e. the global pool + out_proj backward (lgnn_pool_head_bwd's dpooled and lgnn_pool_bwd)
+ * folded into the load, in the same arithmetic; dY is unused (NULL). The GIN model's last conv. */
+int lgnn_node_linear_bwd_bn_pool(int bn_mode, const float* dY, const float* H, int act,
+                                 const float* X, int64_t M, int K, const float* W, int N,
+                                 float* dXpre, float* dW_partial, float* db_partial,
+                                 int num_partials, const float* bn_Z, const float* bn_mask,
+                                 const float* bn_scale, const float* bn_shift,
+                                 const float* bn_mean, const float* bn_invstd,
+                                 double* gstats_part, const double* bn_sums, double count,
+                                 int training, const int64_t* batch, const int32_t* gptr,
+                                 int pool_mean, const float* dlogits, const float* Wout,
+                                 int num_classes, void* stream);
 /* Split-3 variants (bf16 MFMA at fp32 accuracy, liblgnn lin3.hip) of the two calls below: the
  * same arguments with `planes` / `planes_t` (lgnn_weight_planes of W: the weight and, for dX, the
  * transposed planes of this one layer) in place of W; either BN option (or none: stats_part and
@@ -330,11 +345,12 @@ int lgnn_node_linear_bwd_bn(int bn_mode, const float* dY, const float* H, int ac
 int lgnn_gat_att(const float* XP, int64_t M, int H, int C, const float* att_src,
                  const float* att_dst, float* a_s, float* a_d, void* stream);
 /* alpha = softmax_i(leaky_relu(a_s[j] + a_d[i])) (PyG utils.softmax, +1e-16; written if
- * non-NULL), Y_i = act(sum_j alpha_ij mask_ij XP_j + bias) */
+ * non-NULL), Y_i = act(sum_j alpha_ij mask_ij XP_j + bias); Y_bf16 (nullable) also receives Y
+ * rounded to bf16 (RNE, torch's .to(bfloat16)): the next layer's bf16 GEMM operand */
 int lgnn_gat_fwd(const int32_t* rowptr, const int32_t* col, const float* XP, const float* a_s,
                  const float* a_d, int64_t M, int H, int C, float negative_slope,
                  const float* edge_mask, const float* bias, int act, float* alpha, float* Y,
-                 void* stream);
+                 uint16_t* Y_bf16, void* stream);
 /* Backward, target rows: dZ = dY * act'(Y); da_e = d(logit) per edge; da_d = row sums. */
 int lgnn_gat_bwd_edge(const int32_t* rowptr, const int32_t* col, const float* XP,
                       const float* a_s, const float* a_d, const float* alpha,
@@ -348,7 +364,7 @@ int lgnn_gat_bwd_node(const int32_t* tptr, const int32_t* tidx, const int32_t* t
                       const float* alpha, const float* edge_mask, const float* da_e,
                       const float* da_d, const float* dZ, const float* XP, const float* att_src,
                       const float* att_dst, int64_t M, int H, int C, float* dXP,
-                      float* partials, int num_partials, void* stream);
+                      float* partials, int num_partials, uint16_t* dXP_bf16, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Fused GCN layer stack, forward (one launch for the whole model body below the readout).

@@ -65,10 +65,11 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_bn_act": (I32, [P, I64, I32, P, P, P, P, P]),
     "lgnn_bn_bwd_stats": (I32, [P, P, P, I64, I32, P, P, P, P, P, P, SZ, P]),
     "lgnn_gat_att": (I32, [P, I64, I32, I32, P, P, P, P, P]),
-    "lgnn_gat_fwd": (I32, [P, P, P, P, P, I64, I32, I32, F32, P, P, I32, P, P, P]),
+    "lgnn_gat_fwd": (I32, [P, P, P, P, P, I64, I32, I32, F32, P, P, I32, P, P, P, P]),
     "lgnn_gat_bwd_edge": (I32, [P, P, P, P, P, P, P, P, P, I32, I64, I32, I32, F32, P, P, P, P]),
     "lgnn_gat_bwd_num_partials": (I32, [I64]),
-    "lgnn_gat_bwd_node": (I32, [P, P, P, P, P, P, P, P, P, P, P, I64, I32, I32, P, P, I32, P]),
+    "lgnn_gat_bwd_node": (I32, [P, P, P, P, P, P, P, P, P, P, P, I64, I32, I32, P, P, I32, P,
+                                P]),
     "lgnn_gcn_stack_fwd": (I32, [P, I64, I32, I32, P, P, P, I32, P, P, P, P, P, P]),
     "lgnn_gcn_stack_fwd_s3": (I32, [P, I64, I32, I32, P, P, P, I32, P, P, P, P, P, P, P]),
     "lgnn_weight_planes_bytes": (SZ, [I32]),
@@ -92,6 +93,9 @@ SIGNATURES: dict[str, tuple] = {
                                       P, P]),
     "lgnn_node_linear_bwd_bn": (I32, [I32, P, P, I32, P, I64, I32, P, I32, P, P, P, I32, P, P, P,
                                       P, P, P, P, P, F64, I32, P]),
+    "lgnn_node_linear_bwd_bn_pool": (I32, [I32, P, P, I32, P, I64, I32, P, I32, P, P, P, I32, P,
+                                           P, P, P, P, P, P, P, F64, I32, P, P, I32, P, P, I32,
+                                           P]),
     "lgnn_node_linear_fwd_s3": (I32, [P, I64, I32, P, P, P, F32, P, P, I32, I32, P, P, P, P, P, P,
                                       P, P]),
     "lgnn_node_linear_bwd_s3": (I32, [I32, P, P, I32, P, I64, I32, P, I32, P, P, P, I32, P, P, P,
@@ -108,7 +112,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 14
+ABI_VERSION = 16
 
 _lib = None
 

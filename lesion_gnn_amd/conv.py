@@ -126,6 +126,25 @@ class GINConv(nn.Module):
                             mlp.lins[1].bias, g, self.initial_eps, mask, act, self.sync_group,
                             self.sync_count)
 
+    def head_fusable(self, x: torch.Tensor) -> bool:
+        mlp = self.nn
+        return ops.gin_conv_head_eligible(x, mlp.lins[0].weight, mlp.lins[1].weight)
+
+    def forward_head(self, x: torch.Tensor, g, act: int, W_out: torch.Tensor,
+                     b_out: torch.Tensor, mean: bool) -> torch.Tensor:
+        """forward(x) followed by global pool + out_proj (W_out, b_out) in one autograd node
+        (ops.gin_conv_head): the model's last conv and readout. Returns the logits."""
+        mlp = self.nn
+        bn = mlp.norms[0].module
+        mask = None
+        if mlp.dropout > 0.0 and self.training:
+            p = mlp.dropout
+            mask = (torch.rand(x.size(0), mlp.channel_list[1], device=x.device) >= p).float()
+            mask.mul_(1.0 / (1.0 - p))
+        return ops.gin_conv_head(x, mlp.lins[0].weight, mlp.lins[0].bias, bn, mlp.lins[1].weight,
+                                 mlp.lins[1].bias, W_out, b_out, g, self.initial_eps, mask, act,
+                                 self.sync_group, self.sync_count, mean)
+
 
 class GATConv(nn.Module):
     """PyG 2.5.1 GATConv(in, out, heads, dropout) with concat=True, negative_slope=0.2,

@@ -105,6 +105,13 @@ __global__ __launch_bounds__(NT) void k_gat_att(const float* __restrict__ XP, in
 // ------------------------------------------------------------------------------------------
 // forward: softmax over each target row + weighted sum of source rows (+ bias, ELU)
 // ------------------------------------------------------------------------------------------
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+// four fp32 -> bf16 (round to nearest even, as torch's .to(torch.bfloat16)), one 8-B store
+__device__ __forceinline__ void st4_bf16(uint16_t* p, f32x4 v) {
+  *reinterpret_cast<unsigned long long*>(p) =
+      __builtin_bit_cast(unsigned long long, __builtin_convertvector(v, bf16x4_t));
+}
+
 template <int ACT, int NS>
 __global__ __launch_bounds__(NT) void k_gat_fwd(const int32_t* __restrict__ rowptr,
                                                 const int32_t* __restrict__ col,
@@ -113,7 +120,8 @@ __global__ __launch_bounds__(NT) void k_gat_fwd(const int32_t* __restrict__ rowp
                                                 const float* __restrict__ a_d, int64_t M, int H,
                                                 int C, float slope, const float* __restrict__ mask,
                                                 const float* __restrict__ bias,
-                                                float* __restrict__ alpha, float* __restrict__ Y) {
+                                                float* __restrict__ alpha, float* __restrict__ Y,
+                                                uint16_t* __restrict__ Yb) {
   constexpr int EBN = EB / NS;
   const Lane L = lane_row();
   if (L.row >= M) return;
@@ -189,6 +197,7 @@ __global__ __launch_bounds__(NT) void k_gat_fwd(const int32_t* __restrict__ rowp
           for (int j = 0; j < 4; ++j) o[j] = elu_f(o[j]);
         }
         st4(Y + L.row * HC + P.f[s], o);
+        if (Yb) st4_bf16(Yb + L.row * HC + P.f[s], o);  // the next bf16 GEMM's operand
       }
     }
   }
@@ -282,7 +291,7 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_node(
     const float* __restrict__ mask, const float* __restrict__ da_e,
     const float* __restrict__ da_d, const float* __restrict__ dZ, const float* __restrict__ XP,
     const float* __restrict__ att_src, const float* __restrict__ att_dst, int64_t M, int H,
-    int C, float* __restrict__ dXP, float* __restrict__ part) {
+    int C, float* __restrict__ dXP, float* __restrict__ part, uint16_t* __restrict__ dXPb) {
   __shared__ __attribute__((aligned(16))) float red[RB][3 * MAXS * 128];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int li = lane & 31, hw = wave * 2 + (lane >> 5);
@@ -332,6 +341,7 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_node(
       const f32x4 o = acc + sda * ld4(att_src + fc) + dd * ld4(att_dst + fc);
       if (act) {
         st4(dXP + row * HC + f, o);
+        if (dXPb) st4_bf16(dXPb + row * HC + f, o);  // the lin backward's bf16 operand
         ps[st] += sda * xp;
         pd[st] += dd * xp;
         pb[st] += ld4(dZ + row * HC + f);
@@ -387,14 +397,15 @@ extern "C" int lgnn_gat_att(const float* XP, int64_t M, int H, int C, const floa
 extern "C" int lgnn_gat_fwd(const int32_t* rowptr, const int32_t* col, const float* XP,
                             const float* a_s, const float* a_d, int64_t M, int H, int C,
                             float negative_slope, const float* edge_mask, const float* bias,
-                            int act, float* alpha, float* Y, void* stream) {
+                            int act, float* alpha, float* Y, uint16_t* Y_bf16, void* stream) {
   if (M < 0 || !shape_ok(H, C) || (act != LGNN_ACT_NONE && act != LGNN_ACT_ELU))
     return LGNN_EINVAL;
   if (M > 0 && (!rowptr || !col || !XP || !a_s || !a_d || !Y)) return LGNN_EINVAL;
   if (M == 0) return LGNN_OK;
 #define LGNN_GF(A_, NS_)                                                                     \
   hipLaunchKernelGGL((k_gat_fwd<A_, NS_>), dim3(row_grid(M)), dim3(NT), 0, as_stream(stream),    \
-                     rowptr, col, XP, a_s, a_d, M, H, C, negative_slope, edge_mask, bias, alpha, Y)
+                     rowptr, col, XP, a_s, a_d, M, H, C, negative_slope, edge_mask, bias, alpha, Y, \
+                     Y_bf16)
 #define LGNN_GF_NS(A_)                    \
   switch (ns_of(C)) {                     \
     case 1: LGNN_GF(A_, 1); break;        \
@@ -455,14 +466,14 @@ extern "C" int lgnn_gat_bwd_node(const int32_t* tptr, const int32_t* tidx, const
                                  const float* da_d, const float* dZ, const float* XP,
                                  const float* att_src, const float* att_dst, int64_t M, int H,
                                  int C, float* dXP, float* partials, int num_partials,
-                                 void* stream) {
+                                 uint16_t* dXP_bf16, void* stream) {
   if (M < 0 || !shape_ok(H, C) || !att_src || !att_dst || !partials) return LGNN_EINVAL;
   if (num_partials != lgnn_gat_bwd_num_partials(M)) return LGNN_EINVAL;
   if (M > 0 && (!tptr || !tidx || !tmap || !alpha || !da_e || !da_d || !dZ || !XP || !dXP))
     return LGNN_EINVAL;
   hipLaunchKernelGGL(k_gat_bwd_node, dim3(num_partials), dim3(NT), 0, as_stream(stream), tptr,
                      tidx, tmap, alpha, edge_mask, da_e, da_d, dZ, XP, att_src, att_dst, M, H, C,
-                     dXP, partials);
+                     dXP, partials, dXP_bf16);
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
 }

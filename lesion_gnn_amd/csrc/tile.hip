@@ -48,13 +48,14 @@ __global__ __launch_bounds__(NT, 2) void k_bwd(
     const float* __restrict__ H, const float* __restrict__ X, int64_t M, int K,
     const float* __restrict__ W, int N, float* __restrict__ dXpre, float* __restrict__ dWp,
     float* __restrict__ dbp, const int32_t* __restrict__ tmask, int want, int accumulate,
-    BnFuse bn) {
+    BnFuse bn, const float* __restrict__ dlog = nullptr, const float* __restrict__ Wout = nullptr,
+    int nclass = 0) {
   __shared__ __attribute__((aligned(16))) float A[TM * LDS];
   __shared__ __attribute__((aligned(16))) float C[TM * LDS];
   __shared__ TileIdx ti;
   bwd_tiles<GMODE, ACT, DX, BNM>(A, C, ti, dY, batch, gptr, pool_mean, tptr, tidx, tw, tself, H,
-                                 X, M, K, W, N, dXpre, dWp, dbp, tmask, want, accumulate, nullptr,
-                                 nullptr, 0, bn);
+                                 X, M, K, W, N, dXpre, dWp, dbp, tmask, want, accumulate, dlog,
+                                 Wout, nclass, bn);
 }
 
 
@@ -787,9 +788,25 @@ extern "C" int lgnn_node_linear_bwd_bn(int bn_mode, const float* dY, const float
                                        const float* bn_mean, const float* bn_invstd,
                                        double* gstats_part, const double* bn_sums, double count,
                                        int training, void* stream) {
+  return lgnn_node_linear_bwd_bn_pool(bn_mode, dY, H, act, X, M, K, W, N, dXpre, dW_partial,
+                                      db_partial, num_partials, bn_Z, bn_mask, bn_scale, bn_shift,
+                                      bn_mean, bn_invstd, gstats_part, bn_sums, count, training,
+                                      nullptr, nullptr, 0, nullptr, nullptr, 0, stream);
+}
+
+extern "C" int lgnn_node_linear_bwd_bn_pool(
+    int bn_mode, const float* dY, const float* H, int act, const float* X, int64_t M, int K,
+    const float* W, int N, float* dXpre, float* dW_partial, float* db_partial, int num_partials,
+    const float* bn_Z, const float* bn_mask, const float* bn_scale, const float* bn_shift,
+    const float* bn_mean, const float* bn_invstd, double* gstats_part, const double* bn_sums,
+    double count, int training, const int64_t* batch, const int32_t* gptr, int pool_mean,
+    const float* dlogits, const float* Wout, int num_classes, void* stream) {
+  const bool pool = batch != nullptr;
+  if (pool && (!gptr || bn_mode != BN_GSTATS || !dlogits || !Wout || num_classes < 1))
+    return LGNN_EINVAL;
   if (M < 0 || !W || !dW_partial || !lgnn_tile_fits(M, K, N)) return LGNN_EINVAL;
   if (num_partials != lgnn_tile_partials(M)) return LGNN_EINVAL;
-  if (M > 0 && (!dY || !X)) return LGNN_EINVAL;
+  if (M > 0 && ((!dY && !pool) || !X)) return LGNN_EINVAL;
   if (!bn_Z || !bn_scale || !bn_shift || !bn_mean || !bn_invstd) return LGNN_EINVAL;
   if (act != LGNN_ACT_NONE && act != LGNN_ACT_ELU) return LGNN_EINVAL;
   if (act == LGNN_ACT_ELU && !H) return LGNN_EINVAL;
@@ -822,7 +839,15 @@ extern "C" int lgnn_node_linear_bwd_bn(int bn_mode, const float* dY, const float
   hipLaunchKernelGGL((k_bwd<LGNN_GRAD_DIRECT, AC, D, BM>), grid, dim3(NT), 0, s, dY, nullptr,  \
                      nullptr, 0, nullptr, nullptr, nullptr, 0.f, H, X, M, K, W, N, dXpre,      \
                      dW_partial, db_partial, nullptr, 0, 0, bn)
-  if (bn_mode == BN_GSTATS) {
+#define LGNN_TBP(AC)                                                                            \
+  hipLaunchKernelGGL((k_bwd<LGNN_GRAD_POOL, AC, true, BN_GSTATS>), grid, dim3(NT), 0, s, nullptr, \
+                     batch, gptr, pool_mean, nullptr, nullptr, nullptr, 0.f, H, X, M, K, W, N,    \
+                     dXpre, dW_partial, db_partial, nullptr, 0, 0, bn, dlogits, Wout,           \
+                     num_classes)
+  if (pool) {  // the pooled-output gradient formed from dlogits and out_proj's W (no dH tensor)
+    if (act == LGNN_ACT_ELU) LGNN_TBP(LGNN_ACT_ELU);
+    else LGNN_TBP(LGNN_ACT_NONE);
+  } else if (bn_mode == BN_GSTATS) {
     if (act == LGNN_ACT_ELU) LGNN_TBB(LGNN_ACT_ELU, true, BN_GSTATS);
     else LGNN_TBB(LGNN_ACT_NONE, true, BN_GSTATS);
   } else {
@@ -830,6 +855,7 @@ extern "C" int lgnn_node_linear_bwd_bn(int bn_mode, const float* dY, const float
     else LGNN_TBB(LGNN_ACT_NONE, false, BN_GIN);
   }
 #undef LGNN_TBB
+#undef LGNN_TBP
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? LGNN_OK : (int)e;
 }

@@ -358,10 +358,14 @@ __device__ __forceinline__ void bwd_tiles(
           if constexpr (BNM == BN_GIN) hv[it] = ld4(bn.Z + rc * N + oc);  // BN input rows
         } else {
           const int64_t gi = batch[rc];
-          if (dlog) {
+          if (dlog) {  // k_head_bwd's arithmetic: an fmaf chain over the classes in order
             f32x4 acc = zero4();
-            for (int c = 0; c < nclass; ++c)
-              acc += dlog[gi * nclass + c] * ld4(Wout + (int64_t)c * N + oc);
+            for (int c = 0; c < nclass; ++c) {
+              const float d = dlog[gi * nclass + c];
+              const f32x4 wv = ld4(Wout + (int64_t)c * N + oc);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) acc[j] = fmaf(d, wv[j], acc[j]);
+            }
             g[it] = acc;
           } else {
             g[it] = ld4(dY + gi * N + oc);

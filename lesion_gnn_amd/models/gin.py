@@ -50,9 +50,15 @@ class GIN(nn.Module):
                 num_graphs: int | None = None) -> torch.Tensor:
         g = as_graph(edge_index, x.size(0), batch, num_graphs)
         h = ops.node_linear(x, self.in_proj.weight, self.in_proj.bias)
-        for conv in self.convs:
+        drop = self.dropout.p > 0.0 and self.training
+        last = len(self.convs) - 1
+        for i, conv in enumerate(self.convs):
+            if i == last and not drop and conv.head_fusable(h):
+                # last conv + readout as one node: no dH tensor in the backward
+                return conv.forward_head(h, g, _lib.LGNN_ACT_ELU, self.out_proj.weight,
+                                         self.out_proj.bias, self.pool == "mean")
             h = conv(h, g, act=_lib.LGNN_ACT_ELU)
-            if self.dropout.p > 0.0 and self.training:
+            if drop:
                 h = F.dropout(h, self.dropout.p, True)
         return ops.pool_head(h, self.out_proj.weight, self.out_proj.bias, g, self.pool == "mean")
 

@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 
 import torch
 
@@ -839,8 +840,10 @@ class _GINConv(torch.autograd.Function):
         N1 = W1.size(0)
         fast = fast_shape(W1.size(1), N1)
         if gin_bn_fused(W1.size(1), N1, W2.size(0)):
-            return _GINConv._forward_fused(ctx, x, W1, b1, W2, b2, csr, self_scale, graph, bn,
-                                           training, mask, act, group, sync_count, gamma)
+            H, saved = _GINConv._forward_fused(ctx, x, W1, b1, W2, b2, csr, self_scale, graph, bn,
+                                               training, mask, act, group, sync_count, gamma)
+            ctx.save_for_backward(*saved)
+            return H
         if fast:
             Z1, S = linear_fwd(x, W1, b1, _lib.LGNN_ACT_NONE, csr, self_scale, save_s=True)
         else:
@@ -923,17 +926,18 @@ class _GINConv(torch.autograd.Function):
         _lib.call(fname, _lib.ptr(Z1), M, N1, None, None, None, 0.0, w2, _lib.ptr(b2), N2, act,
                   _lib.ptr(H), None, None, _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(mask),
                   _lib.ptr(A1), _s(dev))
-        ctx.save_for_backward(S, Z1, A1, H, W1, W2, mean, invstd, scale, shift, mask)
         ctx.graph, ctx.self_scale, ctx.gathered = graph, self_scale, False
         ctx.training, ctx.count, ctx.group, ctx.act = training, count, group, act
         ctx.bn_sums = sums
         ctx.affine = gamma is not None
         ctx.bn_fused = True
-        return H
+        return H, (S, Z1, A1, H, W1, W2, mean, invstd, scale, shift, mask)
 
     @staticmethod
-    def _backward_fused(ctx, dH):
-        S, Z1, A1, H, W1, W2, mean, invstd, scale, shift, mask = ctx.saved_tensors
+    def _backward_fused(ctx, dH, pool: tuple | None = None):
+        """pool = (dlogits, W_out, graph, mean): the output gradient comes from the pooled readout
+        (global pool + out_proj backward folded into Lin2's backward load; dH is None)."""
+        S, Z1, A1, H, W1, W2, mean, invstd, scale, shift, mask = ctx.saved_tensors[:11]
         csr = ctx.graph.csr("gin")
         M, N1 = Z1.shape
         N2 = W2.size(0)
@@ -955,11 +959,21 @@ class _GINConv(torch.autograd.Function):
         dA1 = torch.empty_like(Z1)
         slab2 = torch.empty(P * (N2 * N1 + N2), dtype=torch.float32, device=dev)
         gpart = torch.empty(P * 2 * N1, dtype=torch.float64, device=dev)
-        _lib.call(fname, _lib.LGNN_BN_GSTATS, _lib.ptr(_f32c(dH)), _lib.ptr(H),
-                  ctx.act, _lib.ptr(A1), M, N1, w2, N2, _lib.ptr(dA1), _lib.ptr(slab2),
-                  _lib.ptr(slab2[P * N2 * N1:]), P, _lib.ptr(Z1), _lib.ptr(mask),
-                  _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(mean), _lib.ptr(invstd),
-                  _lib.ptr(gpart), None, 0.0, int(ctx.training), _s(dev))
+        if pool is not None:
+            dlog, W_out, pg, pmean = pool
+            _lib.call("lgnn_node_linear_bwd_bn_pool", _lib.LGNN_BN_GSTATS, None, _lib.ptr(H),
+                      ctx.act, _lib.ptr(A1), M, N1, w2, N2, _lib.ptr(dA1), _lib.ptr(slab2),
+                      _lib.ptr(slab2[P * N2 * N1:]), P, _lib.ptr(Z1), _lib.ptr(mask),
+                      _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(mean), _lib.ptr(invstd),
+                      _lib.ptr(gpart), None, 0.0, int(ctx.training), _lib.ptr(pg.batch),
+                      _lib.ptr(pg.gptr), int(pmean), _lib.ptr(dlog), _lib.ptr(W_out),
+                      W_out.size(0), _s(dev))
+        else:
+            _lib.call(fname, _lib.LGNN_BN_GSTATS, _lib.ptr(_f32c(dH)), _lib.ptr(H),
+                      ctx.act, _lib.ptr(A1), M, N1, w2, N2, _lib.ptr(dA1), _lib.ptr(slab2),
+                      _lib.ptr(slab2[P * N2 * N1:]), P, _lib.ptr(Z1), _lib.ptr(mask),
+                      _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(mean), _lib.ptr(invstd),
+                      _lib.ptr(gpart), None, 0.0, int(ctx.training), _s(dev))
         dW2 = torch.empty(N2, N1, dtype=torch.float32, device=dev)
         db2 = torch.empty(N2, dtype=torch.float32, device=dev)
         red += [(slab2[:P * N2 * N1], P, N2 * N1, dW2), (slab2[P * N2 * N1:], P, N2, db2)]
@@ -1026,6 +1040,60 @@ class _GINConv(torch.autograd.Function):
                 None)
 
 
+class _GINConvHead(torch.autograd.Function):
+    """The GIN model's last conv + global pool + out_proj as one autograd node (BN-fused fp32
+    path): its backward forms each row's output gradient from dlogits (out_proj backward + pool
+    backward folded into Lin2's backward load, lgnn_node_linear_bwd_bn_pool) instead of
+    materialising dH; out_proj's dW / db come from lgnn_pool_head_bwd (same arithmetic as the
+    unfused chain)."""
+
+    @staticmethod
+    def forward(ctx, x, W1, b1, gamma, beta, W2, b2, W_out, b_out, graph, bn, training, eps,
+                mask, act, group, sync_count, mean):
+        _lib.require_gpu(x, W1, W2, W_out)
+        x, W1, b1, W2, b2 = (_f32c(t) for t in (x, W1, b1, W2, b2))
+        W_out, b_out = _f32c(W_out), _f32c(b_out)
+        csr = graph.csr("gin")
+        H, saved = _GINConv._forward_fused(ctx, x, W1, b1, W2, b2, csr, 1.0 + float(eps), graph,
+                                           bn, training, mask, act, group, sync_count, gamma)
+        pooled, logits = pool_head_fwd(H, graph, mean, W_out, b_out)
+        ctx.save_for_backward(*saved, pooled, W_out)
+        ctx.head_graph, ctx.head_mean = graph, mean
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        pooled, W_out = ctx.saved_tensors[11:13]
+        dlogits = _f32c(dlogits)
+        B, D = pooled.shape
+        C = W_out.size(0)
+        dev = pooled.device
+        dWo = torch.empty(C, D, dtype=torch.float32, device=dev)
+        dbo = torch.empty(C, dtype=torch.float32, device=dev)
+        _lib.call("lgnn_pool_head_bwd", _lib.ptr(dlogits), _lib.ptr(pooled), B, D,
+                  _lib.ptr(W_out), C, None, _lib.ptr(dWo), _lib.ptr(dbo), _s(dev))
+        g = _GINConv._backward_fused(ctx, None, pool=(dlogits, W_out, ctx.head_graph,
+                                                      ctx.head_mean))
+        return (*g[:7], dWo, dbo) + (None,) * 9
+
+
+def gin_conv_head_eligible(x, W1, W2) -> bool:
+    """Whether gin_conv_head runs fused (eager, BN-fused fp32 kernels, fast-path shapes)."""
+    return (not _compiling() and GIN_MFMA == "f32" and
+            gin_bn_fused(x.size(1), W1.size(0), W2.size(0)))
+
+
+def gin_conv_head(x, W1, b1, bn, W2, b2, W_out, b_out, graph: Graph, eps: float = 0.0,
+                  mask=None, act: int = _lib.LGNN_ACT_ELU, group=None, sync_count=None,
+                  mean: bool = True):
+    """gin_conv followed by pool_head (the GIN model's last conv and readout) as one node."""
+    training = bn.training or not bn.track_running_stats
+    gamma = bn.weight if bn.affine else None
+    beta = bn.bias if bn.affine else None
+    return _GINConvHead.apply(x, W1, b1, gamma, beta, W2, b2, W_out, b_out, graph, bn, training,
+                              eps, mask, act, group, sync_count, mean)
+
+
 def gin_conv(x, W1, b1, bn, W2, b2, graph: Graph, eps: float = 0.0, mask=None,
              act: int = _lib.LGNN_ACT_ELU, group=None, sync_count=None):
     """bn: the torch.nn.BatchNorm1d holding gamma/beta and the running statistics."""
@@ -1076,7 +1144,10 @@ class _GATConv(torch.autograd.Function):
         dev = x.device
         dense = bf16 or not fast_shape(W.size(1), HC)
         if bf16:  # GEMM operands rounded once; the backward reuses the bf16 copies
-            xg, Wg = x.to(torch.bfloat16), W.to(torch.bfloat16)
+            xg = _bf16_copy_of(x)  # the previous GAT layer may have written it already
+            if xg is None:
+                xg = x.to(torch.bfloat16)
+            Wg = W.to(torch.bfloat16)
         else:
             xg, Wg = x, W
         XP = mm_dense(xg, Wg.t(), bf16) if dense else linear_fwd(x, W, None, _lib.LGNN_ACT_NONE)
@@ -1087,14 +1158,18 @@ class _GATConv(torch.autograd.Function):
         cap = csr.col.numel()
         alpha = torch.empty(cap, heads, dtype=torch.float32, device=dev)
         Y = torch.empty(M, HC, dtype=torch.float32, device=dev)
+        # bf16 mode: the kernel also writes Y in bf16 for the next layer's GEMM (no cast pass)
+        Yb = torch.empty(M, HC, dtype=torch.bfloat16, device=dev) if bf16 and BF16_OUT else None
         _lib.call("lgnn_gat_fwd", _lib.ptr(csr.rowptr), _lib.ptr(csr.col), _lib.ptr(XP),
                   _lib.ptr(a_s), _lib.ptr(a_d), M, heads, C, float(slope), _lib.ptr(mask),
-                  _lib.ptr(bias), act, _lib.ptr(alpha), _lib.ptr(Y), _s(dev))
+                  _lib.ptr(bias), act, _lib.ptr(alpha), _lib.ptr(Y), _lib.ptr(Yb), _s(dev))
         ctx.save_for_backward(xg, Wg, att_src, att_dst, XP, a_s, a_d, alpha, Y, mask)
         ctx.graph, ctx.heads, ctx.slope, ctx.act = graph, heads, slope, act
         ctx.bf16, ctx.dense = bf16, dense
         ctx.has_bias = bias is not None
         ctx.att_shape = (1, heads, C)
+        if Yb is not None:
+            _remember_bf16(Y, Yb)
         return Y
 
     @staticmethod
@@ -1115,15 +1190,22 @@ class _GATConv(torch.autograd.Function):
         P = _lib.load().lgnn_gat_bwd_num_partials(M)
         part = torch.empty(P * 3 * HC, dtype=torch.float32, device=dev)
         dXP = torch.empty_like(XP)
+        # bf16 dense lin: the kernel also writes dXP in bf16 (the GEMMs' operand, no cast pass)
+        dXPb = torch.empty(M, HC, dtype=torch.bfloat16, device=dev) \
+            if ctx.dense and ctx.bf16 and BF16_OUT else None
         _lib.call("lgnn_gat_bwd_node", _lib.ptr(csr.tptr), _lib.ptr(csr.tidx),
                   _lib.ptr(csr.tmap), _lib.ptr(alpha), _lib.ptr(mask), _lib.ptr(da_e),
                   _lib.ptr(da_d), _lib.ptr(dZ), _lib.ptr(XP), _lib.ptr(att_src),
-                  _lib.ptr(att_dst), M, H, C, _lib.ptr(dXP), _lib.ptr(part), P, _s(dev))
+                  _lib.ptr(att_dst), M, H, C, _lib.ptr(dXP), _lib.ptr(part), P, _lib.ptr(dXPb),
+                  _s(dev))
         red = torch.empty(3 * HC, dtype=torch.float32, device=dev)
         _lib.call("lgnn_reduce_partials", _lib.ptr(part), P, 3 * HC, _lib.ptr(red), _s(dev))
         want_dx = ctx.needs_input_grad[0]
         if ctx.dense:
-            dg = dXP.to(torch.bfloat16) if ctx.bf16 else dXP  # rounded once for both
+            if ctx.bf16:  # rounded once for both products
+                dg = dXPb if dXPb is not None else dXP.to(torch.bfloat16)
+            else:
+                dg = dXP
             dW = dw_dense(dg, x, ctx.bf16)
             dx = mm_dense(dg, W, ctx.bf16) if want_dx else None
         else:
@@ -1133,6 +1215,29 @@ class _GATConv(torch.autograd.Function):
         datt_d = red[HC:2 * HC].view(ctx.att_shape)
         dbias = red[2 * HC:] if ctx.has_bias else None
         return dx, dW, datt_s, datt_d, dbias, None, None, None, None, None, None
+
+
+# bf16 GAT: the attention kernels write their fp32 outputs' bf16 copies for the following bf16
+# GEMMs (LGNN_BF16_OUT=0: torch casts instead; the values are identical, RNE both ways)
+BF16_OUT = os.environ.get("LGNN_BF16_OUT", "1") != "0"
+_BF16_COPIES: dict = {}
+
+
+def _remember_bf16(y: torch.Tensor, yb: torch.Tensor) -> None:
+    key = id(y)
+    _BF16_COPIES[key] = (weakref.ref(y), y._version, yb)
+    weakref.finalize(y, _BF16_COPIES.pop, key, None)
+
+
+def _bf16_copy_of(x: torch.Tensor):
+    """The bf16 copy a GAT layer wrote beside its output x, if x is that output unchanged."""
+    rec = _BF16_COPIES.get(id(x))
+    if rec is None:
+        return None
+    ref, version, xb = rec
+    if ref() is not x or x._version != version:
+        return None
+    return xb
 
 
 def gat_conv(x, W, att_src, att_dst, bias, graph: Graph, heads: int, slope: float = 0.2,

@@ -130,7 +130,7 @@ def test_gat_alpha_rows_sum_to_one(cuda):
     out = torch.empty(b.num_nodes, 64, device=cuda)
     _lib.call("lgnn_gat_fwd", csr.rowptr.data_ptr(), csr.col.data_ptr(), XP.data_ptr(),
               a_s.data_ptr(), a_d.data_ptr(), b.num_nodes, 4, 16, 0.2, None, None, 0,
-              alpha.data_ptr(), out.data_ptr(), _lib.stream())
+              alpha.data_ptr(), out.data_ptr(), None, _lib.stream())
     nnz = int(csr.rowptr[-1])
     rows = torch.repeat_interleave(torch.arange(b.num_nodes, device=cuda),
                                    (csr.rowptr[1:] - csr.rowptr[:-1]).long())
@@ -173,3 +173,26 @@ def test_reference_config_training_step(cuda):
     loss = module.training_step(b.to(cuda))
     want = ref.criterion("MSE", oref(b.x, b.edge_index, b.batch, b.num_graphs), b.y, 5)
     torch.testing.assert_close(loss.detach().cpu(), want.detach(), rtol=1e-5, atol=1e-6)
+
+
+
+def test_gat_bf16_copies_match_torch_cast(cuda, monkeypatch):
+    """bf16 GAT: the bf16 operand copies the attention kernels write beside their fp32 outputs
+    (lgnn_gat_fwd's Y_bf16, lgnn_gat_bwd_node's dXP_bf16) equal torch's RNE cast, so a C3 step
+    with them is bit-identical to the same step casting in torch (LGNN_BF16_OUT=0)."""
+    from lesion_gnn_amd import ops
+
+    b = synth.make_batch(96, k=6, d_in=1025, seed=17, sizes="lognormal", last_channel_class=True)
+    torch.manual_seed(5)
+    m = GAT(1025, [128] * 4, 1, heads=4, dropout=0.0, precision="bf16").to(cuda).train()
+    res = []
+    for on in (True, False):
+        monkeypatch.setattr(ops, "BF16_OUT", on)
+        out = m(b.x.to(cuda), b.edge_index.to(cuda), b.batch.to(cuda), b.num_graphs)
+        loss = torch.nn.functional.mse_loss(out.squeeze(1), b.y.to(cuda).float())
+        m.zero_grad(set_to_none=True)
+        loss.backward()
+        res.append((out.detach().cpu(), {k: p.grad.detach().cpu() for k, p in m.named_parameters()}))
+    assert torch.equal(res[0][0], res[1][0])
+    for k in res[1][1]:
+        assert torch.equal(res[0][1][k], res[1][1][k]), k

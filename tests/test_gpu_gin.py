@@ -132,3 +132,31 @@ def test_gin_bn_fused_matches_unfused_with_dropout(cuda, monkeypatch):
                                        msg=lambda msg: f"{k}: {msg}")
         for k in s2:
             torch.testing.assert_close(s1[k].float(), s2[k].float(), rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("pool", ["add", "mean"])
+def test_gin_last_conv_readout_fused_bitexact(cuda, pool, monkeypatch):
+    """The last conv + global pool + out_proj as one node (ops.gin_conv_head: the readout's
+    backward folded into Lin2's backward load) is bit-identical to the separate conv and
+    pool_head nodes (same arithmetic: k_head_bwd's fmaf chain, then / |graph|), and matches the
+    oracle; ragged graphs, SyncBN-free training mode."""
+    sizes = [1, 5, 64, 200, 2, 33, 90, 17] * 4
+    b = synth.make_batch(len(sizes), k=6, d_in=64, seed=21, sizes=sizes)
+    ours, oref = make_pair(64, [64, 128, 96], pool=pool)
+    ours = ours.to(cuda).train()
+    sd = {k: v.clone() for k, v in ours.state_dict().items()}
+    res = []
+    for fused in (True, False):
+        if not fused:
+            monkeypatch.setattr(ops, "gin_conv_head_eligible", lambda *a: False)
+        ours.load_state_dict(sd)
+        res.append(step(ours, b, cuda))
+    (l1, _, g1, s1), (l2, _, g2, s2) = res
+    assert torch.equal(l1, l2)
+    for k in g2:
+        assert torch.equal(g1[k], g2[k]), k
+    for k in s2:
+        assert torch.equal(s1[k], s2[k]), k
+    lr_, _, gr, _ = step(oref.train(), b, "cpu")
+    torch.testing.assert_close(l1, lr_, rtol=0, atol=1e-4 * max(1.0, lr_.abs().max().item()))
+    assert_grads(g1, gr)
