@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 16
+#define LGNN_ABI_VERSION 17
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -82,6 +82,15 @@ int lgnn_graph_build(const int64_t* edge_index, int64_t num_edges, int64_t num_n
                      int32_t* tidx, float* tw, int32_t* tmap, int32_t* tile_open,
                      const int64_t* batch, int64_t num_graphs, int32_t* gptr, int32_t* err_count,
                      void* workspace, size_t workspace_bytes, void* stream);
+/* lgnn_graph_build for a consumer that reads the source (transpose) CSR only for open tiles
+ * (the fused GCN stack): tile_open and tptr required, tmap NULL; the tiles' open flags are set
+ * by the count and scan passes, and tidx / tw are filled only when some tile is open (tptr is
+ * always written). Same target CSR, flags and weights as lgnn_graph_build. */
+int lgnn_graph_build_lazy(const int64_t* edge_index, int64_t E, int64_t N, int loops, int norm,
+                          int32_t* rowptr, int32_t* col, float* w, int32_t* tptr, int32_t* tidx,
+                          float* tw, int32_t* tmap, int32_t* tile_open, const int64_t* batch,
+                          int64_t num_graphs, int32_t* gptr, int32_t* err_count, void* workspace,
+                          size_t workspace_bytes, void* stream);
 
 /* Graph offsets from a sorted PyG `batch` vector (Batch.ptr): ptr[g] = first node of graph g,
  * ptr[B] = M. Replaces the count/offset half of PyG scatter(reduce='mean') over `batch`. */

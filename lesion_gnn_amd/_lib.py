@@ -37,6 +37,8 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_abi_version": (I32, []),
     "lgnn_status_string": (ctypes.c_char_p, [I32]),
     "lgnn_graph_workspace_bytes": (SZ, [I64, I64]),
+    "lgnn_graph_build_lazy": (I32, [P, I64, I64, I32, I32, P, P, P, P, P, P, P, P, P, I64, P, P,
+                                    P, SZ, P]),
     "lgnn_graph_build": (I32, [P, I64, I64, I32, I32, P, P, P, P, P, P, P, P, P, I64, P, P, P,
                                SZ, P]),
     "lgnn_batch_ptr": (I32, [P, I64, I64, P, P]),
@@ -112,7 +114,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 _lib = None
 

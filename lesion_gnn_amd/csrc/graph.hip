@@ -184,9 +184,15 @@ __device__ __forceinline__ bool chunk_binned(const EdgeChunk& c, int64_t& smin, 
   return H < 0 || H - L < kBins;
 }
 
+// open-tile flag setter: the first writer of a tile also counts it (tile_open[ntiles])
+__device__ __forceinline__ void mark_open(int32_t* tile_open, int64_t t, int64_t ntiles) {
+  if (atomicCAS(&tile_open[t], 0, 1) == 0) atomicAdd(&tile_open[ntiles], 1);
+}
+
 __global__ __launch_bounds__(kThreads) void k_count(const int64_t* __restrict__ ei, int64_t E,
                                                     int64_t N, int loops, int32_t* cnt,
-                                                    int32_t* tcnt, int32_t* err) {
+                                                    int32_t* tcnt, int32_t* err,
+                                                    int32_t* tile_open) {
   __shared__ int hist[kBins];
   __shared__ int red[2 * kThreads / 64];
   const int lane = threadIdx.x & 63;
@@ -197,6 +203,15 @@ __global__ __launch_bounds__(kThreads) void k_count(const int64_t* __restrict__ 
   for (int it = 0; it < kPer; ++it) {
     const Run r = wave_run(c.use[it] ? c.d[it] : -2 - lane);
     if (c.use[it] && r.head) atomicAdd(&cnt[c.d[it]], r.len);
+  }
+  if (tile_open) {  // lazy transpose: the tiles an edge leaves are known before the fill
+    const int64_t ntiles = (N + 63) >> 6;
+#pragma unroll
+    for (int it = 0; it < kPer; ++it)
+      if (c.use[it] && (c.s[it] >> 6) != (c.d[it] >> 6)) {
+        if (tile_open[c.d[it] >> 6] == 0) mark_open(tile_open, c.d[it] >> 6, ntiles);
+        if (tile_open[c.s[it] >> 6] == 0) mark_open(tile_open, c.s[it] >> 6, ntiles);
+      }
   }
   if (!tcnt) return;
   int64_t smin;
@@ -223,7 +238,8 @@ __global__ __launch_bounds__(kThreads) void k_fill(const int64_t* __restrict__ e
                                                    const int32_t* __restrict__ rowptr,
                                                    int32_t* fill, int32_t* col, int32_t* eid,
                                                    const int32_t* __restrict__ tptr,
-                                                   int32_t* tfill, int32_t* tidx, int32_t* teid) {
+                                                   int32_t* tfill, int32_t* tidx, int32_t* teid,
+                                                   const int32_t* lazy_open) {
   __shared__ int hist[kBins];
   __shared__ int red[2 * kThreads / 64];
   const int lane = threadIdx.x & 63;
@@ -244,6 +260,8 @@ __global__ __launch_bounds__(kThreads) void k_fill(const int64_t* __restrict__ e
     }
   }
   if (!tptr) return;
+  if (lazy_open && __hip_atomic_load(lazy_open, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+    return;  // lazy transpose, no open tile: the source CSR is not needed
   int64_t smin;
   if (chunk_binned(c, smin, red)) {
     for (int b = threadIdx.x; b < kBins; b += kThreads) hist[b] = 0;
@@ -301,7 +319,8 @@ __global__ __launch_bounds__(kScanT) void k_scan(const int32_t* __restrict__ cnt
                                                  int32_t* __restrict__ tptr,
                                                  int32_t* __restrict__ fill,
                                                  int32_t* __restrict__ tfill,
-                                                 float* __restrict__ dis) {
+                                                 float* __restrict__ dis,
+                                                 int32_t* tile_open) {
   __shared__ int wsc[kScanT / 64];
   __shared__ int s_pre;
   const bool tr = blockIdx.y == 1;
@@ -345,6 +364,15 @@ __global__ __launch_bounds__(kScanT) void k_scan(const int32_t* __restrict__ cnt
   __syncthreads();
   int run = s_pre + x - s;
   for (int w = 0; w < wave; ++w) run += wsc[w];
+  if (!tr && tile_open) {  // lazy transpose: tiles with more CSR entries than a tile stages
+    int ts = s;            // (a 64-row tile = 16 threads' elements; tiles never straddle blocks)
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) ts += __shfl_xor(ts, o, 64);
+    if ((tid & 15) == 0 && i0 < N && ts > 1024) {
+      const int64_t t = i0 >> 6;
+      if (tile_open[t] == 0) mark_open(tile_open, t, (N + 63) >> 6);
+    }
+  }
 #pragma unroll
   for (int j = 0; j < kScanPer; ++j) {
     const int64_t i = i0 + j;
@@ -383,8 +411,10 @@ __global__ __launch_bounds__(kFinT) void k_finish(int64_t N, int64_t E, int add_
                                                      int32_t* tidx, int32_t* teid, float* tw,
                                                      const float* __restrict__ dis,
                                                      const int32_t* __restrict__ ws_err,
-                                                     int32_t* err_out, int32_t* tile_open) {
+                                                     int32_t* err_out, int32_t* tile_open,
+                                                     int lazy) {
   __shared__ int32_t s_key[kFinishCap];
+  if (lazy && blockIdx.y == 1 && tile_open[(N + 63) >> 6] == 0) return;  // no source CSR needed
   if (err_out && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *err_out = *ws_err;
   __shared__ int32_t s_val[kFinishCap];
   const bool tr = blockIdx.y == 1;
@@ -441,9 +471,7 @@ __global__ __launch_bounds__(kFinT) void k_finish(int64_t N, int64_t E, int add_
   // 64-node tiles an edge leaves (source CSR pass) are open: the fused layer stacks skip them.
   // So are tiles with more CSR entries than a tile stages in LDS (lgnn_tile CAPE = 1024).
   // flag setter: the first writer of a tile also counts it (tile_open[ntiles])
-  auto mark = [&](int64_t t) {
-    if (atomicCAS(&tile_open[t], 0, 1) == 0) atomicAdd(&tile_open[(N + 63) >> 6], 1);
-  };
+  auto mark = [&](int64_t t) { mark_open(tile_open, t, (N + 63) >> 6); };
   if (tile_open && !tr && i < N && (i & 63) == 0) {
     const int64_t iend64 = i + 64 < N ? i + 64 : N;
     if (ptr[iend64] - ptr[i] > 1024) mark(i >> 6);
@@ -517,12 +545,40 @@ extern "C" size_t lgnn_graph_workspace_bytes(int64_t num_nodes, int64_t num_edge
   return ws_total(num_nodes, num_edges);
 }
 
+static int graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loops, int norm,
+                       int32_t* rowptr, int32_t* col, float* w, int32_t* tptr, int32_t* tidx,
+                       float* tw, int32_t* tmap, int32_t* tile_open, const int64_t* batch,
+                       int64_t num_graphs, int32_t* gptr, int32_t* err_count, void* workspace,
+                       size_t workspace_bytes, void* stream, int lazy);
+
 extern "C" int lgnn_graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loops,
                                 int norm, int32_t* rowptr, int32_t* col, float* w, int32_t* tptr,
                                 int32_t* tidx, float* tw, int32_t* tmap, int32_t* tile_open,
                                 const int64_t* batch, int64_t num_graphs, int32_t* gptr,
                                 int32_t* err_count, void* workspace,
                                 size_t workspace_bytes, void* stream) {
+  return graph_build(edge_index, E, N, loops, norm, rowptr, col, w, tptr, tidx, tw, tmap,
+                     tile_open, batch, num_graphs, gptr, err_count, workspace, workspace_bytes,
+                     stream, 0);
+}
+
+extern "C" int lgnn_graph_build_lazy(const int64_t* edge_index, int64_t E, int64_t N, int loops,
+                                     int norm, int32_t* rowptr, int32_t* col, float* w,
+                                     int32_t* tptr, int32_t* tidx, float* tw, int32_t* tmap,
+                                     int32_t* tile_open, const int64_t* batch,
+                                     int64_t num_graphs, int32_t* gptr, int32_t* err_count,
+                                     void* workspace, size_t workspace_bytes, void* stream) {
+  if (!tile_open || !tptr || tmap) return LGNN_EINVAL;
+  return graph_build(edge_index, E, N, loops, norm, rowptr, col, w, tptr, tidx, tw, tmap,
+                     tile_open, batch, num_graphs, gptr, err_count, workspace, workspace_bytes,
+                     stream, 1);
+}
+
+static int graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loops, int norm,
+                       int32_t* rowptr, int32_t* col, float* w, int32_t* tptr, int32_t* tidx,
+                       float* tw, int32_t* tmap, int32_t* tile_open, const int64_t* batch,
+                       int64_t num_graphs, int32_t* gptr, int32_t* err_count, void* workspace,
+                       size_t workspace_bytes, void* stream, int lazy) {
   if (N < 0 || E < 0 || loops < 0 || loops > 2 || norm < 0 || norm > 1) return LGNN_EINVAL;
   if (!rowptr || !col || (E > 0 && !edge_index)) return LGNN_EINVAL;
   if (N + E >= (int64_t)1 << 30) return LGNN_EINVAL;
@@ -550,25 +606,27 @@ extern "C" int lgnn_graph_build(const int64_t* edge_index, int64_t E, int64_t N,
   }
   if (E > 0) {
     hipLaunchKernelGGL(k_count, dim3((unsigned)((E + kChunk - 1) / kChunk)), dim3(kThreads), 0,
-                       s, edge_index, E, N, loops, ws.cnt, tptr ? ws.tcnt : nullptr, ws.err);
+                       s, edge_index, E, N, loops, ws.cnt, tptr ? ws.tcnt : nullptr, ws.err,
+                       lazy ? tile_open : nullptr);
     LGNN_LAUNCH_CHECK();
   }
   {
     const int64_t nblk = (N + 1 + kScanBlk - 1) / kScanBlk;
     dim3 sg((unsigned)nblk, tptr ? 2u : 1u);
     hipLaunchKernelGGL(k_scan, sg, dim3(kScanT), 0, s, ws.cnt, ws.tcnt, N, add_loop, ws.stat,
-                       rowptr, tptr, ws.fill, ws.tfill, ws.dis);
+                       rowptr, tptr, ws.fill, ws.tfill, ws.dis, lazy ? tile_open : nullptr);
     LGNN_LAUNCH_CHECK();
   }
   if (E > 0) {
     hipLaunchKernelGGL(k_fill, dim3((unsigned)((E + kChunk - 1) / kChunk)), dim3(kThreads), 0,
                        s, edge_index, E, N, loops, rowptr, ws.fill, col, ws.eid, tptr, ws.tfill,
-                       tidx, ws.teid);
+                       tidx, ws.teid, lazy ? tile_open + (N + 63) / 64 : nullptr);
     LGNN_LAUNCH_CHECK();
   }
   dim3 fg((unsigned)((N + kFinT - 1) / kFinT), tptr ? 2u : 1u);
   hipLaunchKernelGGL(k_finish, fg, dim3(kFinT), 0, s, N, E, add_loop, norm, rowptr, col,
-                     ws.eid, w, tptr, tidx, ws.teid, tw, ws.dis, ws.err, err_count, tile_open);
+                     ws.eid, w, tptr, tidx, ws.teid, tw, ws.dis, ws.err, err_count, tile_open,
+                     lazy);
   LGNN_LAUNCH_CHECK();
   if (tmap) {
     const int g = grid_for(E + N, 2048);

@@ -17,6 +17,9 @@ from . import _lib
 KIND = {
     # kind: (loops mode, norm mode, self_scale of the aggregation)
     "gcn": (_lib.LGNN_LOOPS_REMAINING, _lib.LGNN_NORM_GCN),
+    # the "gcn" build for the fused GCN stack alone: its source (transpose) CSR is built only
+    # when some tile is open (lgnn_graph_build_lazy) — the closed tiles' backward never reads it
+    "gcn_lazy": (_lib.LGNN_LOOPS_REMAINING, _lib.LGNN_NORM_GCN),
     "gin": (_lib.LGNN_LOOPS_KEEP, _lib.LGNN_NORM_NONE),
     "gat": (_lib.LGNN_LOOPS_READD, _lib.LGNN_NORM_NONE),
 }
@@ -105,7 +108,7 @@ class Graph:
             tw=torch.empty(cap, dtype=torch.float32, device=dev),
             tmap=torch.empty(cap, **i32) if kind == "gat" else None,
             tile_open=torch.empty((n + 63) // 64 + _lib.LGNN_TILE_OPEN_EXTRA, **i32)
-            if kind == "gcn" else None,
+            if kind in ("gcn", "gcn_lazy") else None,
             err=torch.empty(1, **i32),
         )
         lib = _lib.load()
@@ -114,7 +117,8 @@ class Graph:
         gptr = None  # the graph offsets ride along with the first build
         if self._gptr is None and self.batch is not None:
             gptr = self._gptr = torch.empty(self.num_graphs + 1, dtype=torch.int32, device=dev)
-        _lib.call("lgnn_graph_build", _lib.ptr(self.edge_index), e, n, loops, norm,
+        _lib.call("lgnn_graph_build_lazy" if kind == "gcn_lazy" else "lgnn_graph_build",
+                  _lib.ptr(self.edge_index), e, n, loops, norm,
                   _lib.ptr(c.rowptr), _lib.ptr(c.col), _lib.ptr(c.w), _lib.ptr(c.tptr),
                   _lib.ptr(c.tidx), _lib.ptr(c.tw), _lib.ptr(c.tmap), _lib.ptr(c.tile_open),
                   _lib.ptr(self.batch) if gptr is not None else None,

@@ -71,6 +71,9 @@ STACK_MAX = 8  # LGNN_MAX_STACK
 
 # fused stack backward on/off (LGNN_FUSED_BWD=0 selects the layer-wise backward; diagnostics)
 FUSED_BWD = os.environ.get("LGNN_FUSED_BWD", "1") != "0"
+# the fused stack's graph build skips the transpose CSR when no tile is open
+# (LGNN_LAZY_TRANSPOSE=0: always built)
+LAZY_TRANSPOSE = os.environ.get("LGNN_LAZY_TRANSPOSE", "1") != "0"
 
 
 # GEMM arithmetic of the fused GCN stack: "s3" = bf16 MFMA on three-plane split operands (fp32
@@ -155,13 +158,15 @@ def _adjt_ptr(planes_t: torch.Tensor, L: int):
     return planes_t.data_ptr() + 2 * base if planes_t.numel() > base else None
 
 
-def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list, keep: dict | None = None):
+def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list, keep: dict | None = None,
+              kind: str = "gcn"):
     """in_proj + L x ELU(GCNConv) forward, every width <= 128: returns ([H_0..H_L],
     [S_1..S_L]). Tiles no edge leaves run fused through every layer (lgnn_gcn_stack_fwd); the
     rest (graphs straddling 64-node tiles) layer by layer (lgnn_node_linear_fwd_tiles), into the
-    same buffers. With graphs aligned to tiles (C2: N = 64) the second group is empty."""
-    csr = graph.csr("gcn")
-    open_ = graph.tile_open("gcn")
+    same buffers. With graphs aligned to tiles (C2: N = 64) the second group is empty.
+    kind: the graph build ("gcn", or "gcn_lazy" when only the fused backward follows)."""
+    csr = graph.csr(kind)
+    open_ = graph.tile_open(kind)
     M = x.size(0)
     L = len(Ws) - 1
     dev = x.device
@@ -215,14 +220,14 @@ def head_in_stack_bwd(graph: Graph, L: int, C: int, s3: bool) -> bool:
 
 def stack_bwd(dp: torch.Tensor | None, x: torch.Tensor, graph: Graph, mean: bool, Ws: list,
               hs: list, ss: list, reducer: list, planes_t: torch.Tensor | None = None,
-              head: tuple | None = None):
+              head: tuple | None = None, kind: str = "gcn"):
     """Backward of stack_fwd from the pooled-output gradient dp down to in_proj, L = 1 or 2
     convs, no input gradient. Closed tiles run fused (lgnn_gcn_stack_bwd, one launch); open
     tiles layer by layer (lgnn_node_linear_bwd_tiles, want_open = 1, accumulate = 1) into the
     same partial slots. Returns [(dW_l, db_l)] for l = 0..L; the slab reductions are appended
     to `reducer`. head = (dlogits, W_out) replaces dp where head_in_stack_bwd() allows."""
-    csr = graph.csr("gcn")
-    open_ = graph.tile_open("gcn")
+    csr = graph.csr(kind)
+    open_ = graph.tile_open(kind)
     M = x.size(0)
     L = len(Ws) - 1
     dev = x.device
@@ -606,15 +611,22 @@ class _GCNStack(torch.autograd.Function):
         _lib.require_gpu(x, *params)
         x = _f32c(x)
         params = [_f32c(p) for p in params]
-        csr = graph.csr("gcn")
         W_in, b_in = params[0], params[1]
         Ws = [params[2 * l] for l in range(L + 1)]
         fused = L + 1 <= STACK_MAX and all(fast_shape(W.size(1), W.size(0)) for W in Ws)
+        keep = {} if fused and MFMA_MODE == "s3" and BWD_S3 and L >= 1 else None
+        # only the fused kernels read this build (the backward's fused path, the condition
+        # backward() tests): its transpose CSR is then built only if some tile is open
+        lazy = LAZY_TRANSPOSE and isinstance(graph, Graph) and fused and FUSED_BWD and \
+            (1 <= L <= 2 or keep is not None) and not ctx.needs_input_grad[0]
+        kind = "gcn_lazy" if lazy else "gcn"
+        ctx.kind = kind
+        csr = graph.csr(kind)
         ctx.fused = fused
         ctx.planes_t = None
         if fused:
-            keep = {} if MFMA_MODE == "s3" and BWD_S3 and L >= 1 else None
-            hs, ss = stack_fwd(x, graph, Ws, [params[2 * l + 1] for l in range(L + 1)], keep)
+            hs, ss = stack_fwd(x, graph, Ws, [params[2 * l + 1] for l in range(L + 1)], keep,
+                               kind)
             ctx.planes_t = keep.get("planes_t") if keep else None
             ctx.saved_s = [True] * L
         else:
@@ -646,7 +658,8 @@ class _GCNStack(torch.autograd.Function):
         ss = saved[3 + L:3 + 2 * L]
         params = saved[3 + 2 * L:]
         graph = ctx.graph
-        csr = graph.csr("gcn")
+        kind = getattr(ctx, "kind", "gcn")
+        csr = graph.csr(kind)
         W_out = params[2 + 2 * L]
         dlogits = _f32c(dlogits)
         grads = [None] * len(params)
@@ -663,10 +676,11 @@ class _GCNStack(torch.autograd.Function):
                 red += [(dlogits, dlogits.size(0), C * D, dWo, pooled, D),
                         (dlogits, dlogits.size(0), C, dbo)]
                 outs = stack_bwd(None, x, graph, ctx.mean, Ws, hs, ss, red, ctx.planes_t,
-                                 head=(dlogits, W_out))
+                                 head=(dlogits, W_out), kind=kind)
             else:
                 dp, dWo, dbo = pool_head_bwd(dlogits, pooled, W_out)
-                outs = stack_bwd(dp, x, graph, ctx.mean, Ws, hs, ss, red, ctx.planes_t)
+                outs = stack_bwd(dp, x, graph, ctx.mean, Ws, hs, ss, red, ctx.planes_t,
+                                 kind=kind)
             grads[2 + 2 * L], grads[3 + 2 * L] = dWo, dbo
             for l, (dW, db) in enumerate(outs):
                 grads[2 * l], grads[2 * l + 1] = dW, db

@@ -359,7 +359,7 @@ def test_open_tiles_in_fused_launch(cuda, open_in_fused, monkeypatch):
         loss.backward()
         results.append((logits.detach().cpu(),
                         {k: p.grad.detach().cpu() for k, p in ours.named_parameters()}))
-        words = g.tile_open("gcn").cpu().tolist()
+        words = g.tile_open("gcn_lazy" if ops.LAZY_TRANSPOSE else "gcn").cpu().tolist()
         assert words[nt] > 0  # this batch has open tiles
         assert words[nt + 1:] == [0] * 6, words[nt:]
     lr_, _, gr = run_step(oref, b, "cpu")
@@ -399,3 +399,34 @@ def test_head_backward_folded_into_stack(cuda, classes, pool, monkeypatch):
         for k in gr:
             torch.testing.assert_close(go[k], gr[k], atol=1e-5, rtol=1e-4,
                                        msg=lambda m: f"{k}: {m}")
+
+
+
+@pytest.mark.parametrize("case", ["aligned", "ragged", "capacity"])
+def test_lazy_transpose_build(cuda, case):
+    """lgnn_graph_build_lazy (the fused GCN stack's build): the target CSR, the tile flags (cross
+    edges marked in the count pass, the > 1024-entry capacity rule in the scan) and tptr equal
+    the full build's bit for bit; the source CSR (tidx / tw) is built exactly when some tile is
+    open (ragged graphs, dense tiles) and then equals the full build's."""
+    if case == "aligned":
+        b = synth.make_batch(64, n=64, k=8, d_in=8, seed=51)
+    elif case == "ragged":
+        b = synth.make_batch(9, k=6, d_in=8, seed=52, sizes=[1, 5, 64, 200, 2, 33, 512, 17, 64])
+    else:
+        b = synth.make_batch(6, n=64, k=20, d_in=8, seed=53, sizes=[64, 64, 64, 64, 64, 64])
+    g = Graph(b.edge_index.to(cuda), b.num_nodes)
+    full, lazy = g.csr("gcn"), g.csr("gcn_lazy")
+    nnz = int(full.rowptr[-1])  # arrays have capacity E + N; entries past nnz are unused
+    for name in ("rowptr", "tptr", "err"):
+        assert torch.equal(getattr(full, name), getattr(lazy, name)), name
+    for name in ("col", "w"):
+        assert torch.equal(getattr(full, name)[:nnz], getattr(lazy, name)[:nnz]), name
+    to_full, to_lazy = g.tile_open("gcn").cpu(), g.tile_open("gcn_lazy").cpu()
+    assert torch.equal(to_full, to_lazy)
+    nt = (b.num_nodes + 63) // 64
+    n_open = int(to_lazy[nt])
+    assert (n_open == 0) == (case == "aligned")
+    if n_open:
+        assert int(full.tptr[-1]) == nnz
+        assert torch.equal(full.tidx[:nnz], lazy.tidx[:nnz])
+        assert torch.equal(full.tw[:nnz], lazy.tw[:nnz])
