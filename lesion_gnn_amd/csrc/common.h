@@ -53,6 +53,16 @@ __device__ __forceinline__ float elu_f(float x) {
 #endif
 // ELU derivative from the saved OUTPUT h = elu(z): z > 0 <=> h > 0; exp(z) = h + 1.
 __device__ __forceinline__ float elu_grad_from_out(float h) { return h > 0.f ? 1.f : h + 1.f; }
+// Blocks are dealt round-robin over the 8 XCDs (observed placement, speed only): block b's
+// position in a contiguous per-XCD run of the grid (bijective for any grid size), so the rows an
+// XCD's blocks visit are one contiguous range and the neighbour rows they gather (same graph:
+// adjacent rows) stay in that XCD's L2.
+__device__ __forceinline__ int64_t xcd_block() {
+  const int64_t nwg = gridDim.x, b = blockIdx.x;
+  const int64_t q = nwg / 8, r = nwg % 8, xcd = b % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+}
+
 // ELU'(zn) for zn = z * scale + shift (BatchNorm then ELU): 1 above 0, exp(zn) below (exp2 form)
 __device__ __forceinline__ float bn_elu_grad(float z, float sc, float sh) {
   const float zn = fmaf(z, sc, sh);

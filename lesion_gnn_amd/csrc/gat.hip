@@ -39,16 +39,6 @@ struct Lane {
   int64_t row;
 };
 
-// Blocks are dealt round-robin over the 8 XCDs (observed placement, speed only): block b's
-// position in a contiguous per-XCD run of the grid (bijective for any grid size), so the rows an
-// XCD's blocks visit are one contiguous range and the neighbour rows they gather (same graph:
-// adjacent rows) stay in that XCD's L2.
-__device__ __forceinline__ int64_t xcd_block() {
-  const int64_t nwg = gridDim.x, b = blockIdx.x;
-  const int64_t q = nwg / 8, r = nwg % 8, xcd = b % 8;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
-}
-
 __device__ __forceinline__ Lane lane_row() {
   Lane l;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;

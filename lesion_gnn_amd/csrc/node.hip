@@ -556,7 +556,7 @@ __global__ __launch_bounds__(NT) void k_spmm(const int32_t* __restrict__ rowptr,
                                              float* __restrict__ Y) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int h = lane >> 5, li = lane & 31;
-  const int64_t row = ((int64_t)blockIdx.x * 4 + wave) * 2 + h;
+  const int64_t row = (xcd_block() * 4 + wave) * 2 + h;  // XCD-contiguous rows
   if (row >= M) return;
   const int e0 = rowptr[row], e1 = rowptr[row + 1];
   for (int k = 4 * li; k < D; k += 128) {

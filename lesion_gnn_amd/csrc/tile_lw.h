@@ -85,7 +85,7 @@ __device__ __forceinline__ void fwd_tiles(float* A, float* S, TileIdx& ti,
   const int ncl = n < N ? n : N - 1;
   const bool wave_active = wave * 32 < N;
   double s0[4] = {0.0, 0.0, 0.0, 0.0}, s1[4] = {0.0, 0.0, 0.0, 0.0};  // BN_STATS
-  int64_t t = seek_tile(blockIdx.x, ntiles, tmask, want);
+  int64_t t = seek_tile(xcd_block(), ntiles, tmask, want);  // XCD-contiguous tiles
   if (t >= ntiles) {
     if constexpr (BNM == BN_STATS) bn_part_write(reinterpret_cast<double*>(A), s0, s1, bn.part, N);
     return;
@@ -284,7 +284,7 @@ __device__ __forceinline__ void bwd_tiles(
   // pipeline prologue (TRANSPOSE): the first tile's dY rows and transpose-CSR index block
   f32x4 dr[8];
   IdxRegs R;
-  const int64_t tfirst = seek_tile(blockIdx.x, ntiles, tmask, want);
+  const int64_t tfirst = seek_tile(xcd_block(), ntiles, tmask, want);  // XCD-contiguous tiles
   if constexpr (GMODE == LGNN_GRAD_TRANSPOSE) {
     const int64_t t0 = tfirst;
     if (t0 < ntiles) {
