@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 17
+#define LGNN_ABI_VERSION 18
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -573,6 +573,30 @@ size_t lgnn_cc_pool_workspace_bytes(int64_t num_pixels, int channels, int num_se
 int lgnn_cc_pool(const float* features, int channels, int64_t num_pixels, const int64_t* cc,
                  int num_segments, int reduce_max, float* out, int32_t* counts_out, int32_t* err,
                  void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * bf16 dense GEMMs (bf16 GEMM operands rounded round-to-nearest-even as torch's
+ * .to(torch.bfloat16), fp32 accumulation and output). Replace the bf16 nn.Linear / GATConv.lin
+ * GEMMs of the bf16 configuration — in_proj (reference src/lesion_gnn/models/gat.py:29,
+ * nn.Linear(1025, 128)) and GATConv.lin (gat.py:31, PyG Linear(bias=False)) — forward and
+ * backward. Weight operands: lgnn_bf16_weight_prep writes Wb [128][lgnn_bf16_kpad(K)] (bf16 W,
+ * zero-padded) and, when WTb != NULL (requires K <= 128), WTb [128][lgnn_bf16_kpad(N)] (bf16
+ * W^T) for dX = dY W.
+ *   lgnn_bf16_gemm: Y[M][N] = A[M][K] W^T (+ bias), N <= 128; A fp32 (a_is_f32 = 1, rounded
+ *     as loaded, any K) or bf16 (K % 4 == 0); writes Y fp32 and/or Yb bf16 (either nullable).
+ *     For dX: A = dY (bf16, K = N), Wb = WTb, N = K.
+ *   lgnn_bf16_wgrad: partials [num_partials][N][K] of dW = dY^T X (dYb bf16 [M][N], N even;
+ *     X fp32 or bf16 [M][K]); num_partials from lgnn_bf16_wgrad_partials(M, K); sum them with
+ *     lgnn_reduce_partials (fixed order). M * K * 4 < 2^31 for both entries.
+ * ------------------------------------------------------------------------------------------- */
+int lgnn_bf16_kpad(int K);
+int lgnn_bf16_weight_prep(const float* W, int N, int K, uint16_t* Wb, uint16_t* WTb,
+                          void* stream);
+int lgnn_bf16_gemm(const void* A, int a_is_f32, int64_t M, int K, const uint16_t* Wb,
+                   const float* bias, int N, float* Y, uint16_t* Yb, void* stream);
+int lgnn_bf16_wgrad_partials(int64_t M, int K);
+int lgnn_bf16_wgrad(const uint16_t* dYb, int N, const void* X, int x_is_f32, int64_t M, int K,
+                    float* partials, int num_partials, void* stream);
 
 #ifdef __cplusplus
 }

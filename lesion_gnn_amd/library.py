@@ -241,10 +241,11 @@ def _(x, W, b, bf16):
 @custom_op("lgnn::dense_linear_bwd", mutates_args=(), device_types="cuda")
 def dense_linear_bwd(dy: Tensor, x: Tensor, W: Tensor, has_b: bool, bf16: bool,
                      want_dx: bool) -> list[Tensor]:
-    from .ops import _DenseLinear
+    from .ops import _DenseLinear, bf16_mfma_fits
 
     ctx = _Ctx((want_dx,))
-    xs = x.to(torch.bfloat16) if bf16 else x.contiguous()
+    # the MFMA kernels round an fp32 x themselves (as the eager path hands it over)
+    xs = x.to(torch.bfloat16) if bf16 and not bf16_mfma_fits(W.shape[0]) else x.contiguous()
     ctx.save_for_backward(xs, W.contiguous())
     ctx.bf16, ctx.has_b = bf16, has_b
     dx, dW, db = _DenseLinear.backward(ctx, dy)[:3]

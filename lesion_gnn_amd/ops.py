@@ -495,6 +495,64 @@ def dw_dense(dy: torch.Tensor, x: torch.Tensor, bf16: bool) -> torch.Tensor:
     return dW
 
 
+# bf16 GEMMs on the hand-written MFMA kernels (csrc/bflin.hip); LGNN_BF16_MFMA=0 routes them to
+# the library GEMMs above instead (A/B and fallback for N > 128)
+BF16_MFMA = os.environ.get("LGNN_BF16_MFMA", "1") != "0"
+
+
+def bf16_mfma_fits(N: int) -> bool:
+    return BF16_MFMA and 1 <= N <= 128 and N % 2 == 0
+
+
+def bf16_weight_operands(W: torch.Tensor, want_t: bool):
+    """(Wb, WTb): bf16 W [128][kpad(K)] and, when want_t and K <= 128, bf16 W^T [128][kpad(N)]
+    (zero-padded operands of lgnn_bf16_gemm), in one launch."""
+    W = _f32c(W)
+    N, K = W.shape
+    lib = _lib.load()
+    Wb = torch.empty(128 * lib.lgnn_bf16_kpad(K), dtype=torch.bfloat16, device=W.device)
+    WTb = torch.empty(128 * lib.lgnn_bf16_kpad(N), dtype=torch.bfloat16, device=W.device) \
+        if want_t and K <= 128 else None
+    _lib.call("lgnn_bf16_weight_prep", _lib.ptr(W), N, K, _lib.ptr(Wb), _lib.ptr(WTb),
+              _s(W.device))
+    return Wb, WTb
+
+
+def bf16_gemm(A: torch.Tensor, Wb: torch.Tensor, bias, N: int, want_yb: bool = False):
+    """Y = bf16(A) bf16(W)^T (+ bias) in fp32 (and its bf16 copy when want_yb): A fp32 (rounded
+    in the kernel) or bf16."""
+    A = A.contiguous()
+    M, K = A.shape
+    Y = torch.empty(M, N, dtype=torch.float32, device=A.device)
+    Yb = torch.empty(M, N, dtype=torch.bfloat16, device=A.device) if want_yb else None
+    _lib.call("lgnn_bf16_gemm", _lib.ptr(A), int(A.dtype == torch.float32), M, K, _lib.ptr(Wb),
+              _lib.ptr(_f32c(bias) if bias is not None else None), N, _lib.ptr(Y), _lib.ptr(Yb),
+              _s(A.device))
+    return Y, Yb
+
+
+def bf16_wgrad(dYb: torch.Tensor, X: torch.Tensor, N: int) -> torch.Tensor:
+    """dW = bf16(dY)^T bf16(X): partial slabs over row splits, summed in fixed order."""
+    X = X.contiguous()
+    M, K = X.shape
+    if X.dtype != torch.float32 and K % 2:  # bf16 X needs even rows; bf16 -> fp32 is exact
+        X = X.float()
+    dev = X.device
+    S = _lib.load().lgnn_bf16_wgrad_partials(M, K)
+    part = torch.empty(S * N * K, dtype=torch.float32, device=dev)
+    _lib.call("lgnn_bf16_wgrad", _lib.ptr(dYb), N, _lib.ptr(X), int(X.dtype == torch.float32), M,
+              K, _lib.ptr(part), S, _s(dev))
+    dW = torch.empty(N, K, dtype=torch.float32, device=dev)
+    _lib.call("lgnn_reduce_partials", _lib.ptr(part), S, N * K, _lib.ptr(dW), _s(dev))
+    return dW
+
+
+def _bf16_operand(t: torch.Tensor) -> torch.Tensor:
+    """The bf16 copy a kernel wrote beside t, else t's own cast."""
+    tb = _bf16_copy_of(t)
+    return tb if tb is not None else t.to(torch.bfloat16)
+
+
 class _DenseLinear(torch.autograd.Function):
     """y = x W^T + b for shapes outside the tile kernels (K > 128, K % 4 != 0: the reference's
     in_proj with 1025 input channels, gat.py:29 / lesions.py:142,169) or in bf16 mode. A plain
@@ -505,6 +563,19 @@ class _DenseLinear(torch.autograd.Function):
     def forward(ctx, x, W, b, bf16):
         _lib.require_gpu(x, W)
         x, W = _f32c(x), _f32c(W)
+        if bf16 and bf16_mfma_fits(W.size(0)):
+            # hand-written bf16 MFMA GEMM: an fp32 x is rounded as the kernel loads it (no copy);
+            # the output's bf16 copy feeds the next bf16 GEMM
+            xb = _bf16_copy_of(x)
+            A = xb if xb is not None else x
+            Wb, WTb = bf16_weight_operands(W, True)
+            y, yb = bf16_gemm(A, Wb, b, W.size(0), want_yb=BF16_OUT)
+            if yb is not None:
+                _remember_bf16(y, yb)
+            ctx.save_for_backward(A, W)
+            ctx.wt = WTb
+            ctx.bf16, ctx.has_b = bf16, b is not None
+            return y
         if bf16:  # each operand rounded once; the backward reuses the bf16 copies
             x, W = x.to(torch.bfloat16), W.to(torch.bfloat16)
         y = addmm_dense(_f32c(b), x, W.t(), bf16) if b is not None else mm_dense(x, W.t(), bf16)
@@ -517,6 +588,22 @@ class _DenseLinear(torch.autograd.Function):
         x, W = ctx.saved_tensors
         dy = _f32c(dy)
         db = dy.sum(0) if ctx.has_b else None
+        N, K = W.shape
+        if ctx.bf16 and bf16_mfma_fits(N):
+            dyb = _bf16_operand(dy)
+            dW = bf16_wgrad(dyb, x, N)
+            dx = None
+            if ctx.needs_input_grad[0]:
+                if K <= 128:
+                    WTb = getattr(ctx, "wt", None)
+                    if WTb is None:
+                        WTb = bf16_weight_operands(W, True)[1]
+                    dx, dxb = bf16_gemm(dyb, WTb, None, K, want_yb=BF16_OUT)
+                    if dxb is not None:
+                        _remember_bf16(dx, dxb)
+                else:
+                    dx = mm_dense(dyb, W.to(torch.bfloat16), True)
+            return dx, dW, db, None
         if ctx.bf16:  # dy rounded once for both products
             dy = dy.to(torch.bfloat16)
         dW = dw_dense(dy, x, ctx.bf16)
@@ -1157,14 +1244,25 @@ class _GATConv(torch.autograd.Function):
         C = HC // heads
         dev = x.device
         dense = bf16 or not fast_shape(W.size(1), HC)
-        if bf16:  # GEMM operands rounded once; the backward reuses the bf16 copies
+        mfma = bf16 and bf16_mfma_fits(HC)
+        ctx.wt = None
+        if mfma:  # hand-written bf16 MFMA lin; x rounded in the kernel unless a copy exists
+            xb = _bf16_copy_of(x)
+            xg, Wg = (xb if xb is not None else x), W
+            Wb, ctx.wt = bf16_weight_operands(W, True)
+        elif bf16:  # GEMM operands rounded once; the backward reuses the bf16 copies
             xg = _bf16_copy_of(x)  # the previous GAT layer may have written it already
             if xg is None:
                 xg = x.to(torch.bfloat16)
             Wg = W.to(torch.bfloat16)
         else:
             xg, Wg = x, W
-        XP = mm_dense(xg, Wg.t(), bf16) if dense else linear_fwd(x, W, None, _lib.LGNN_ACT_NONE)
+        if mfma:
+            XP = bf16_gemm(xg, Wb, None, HC)[0]
+        elif dense:
+            XP = mm_dense(xg, Wg.t(), bf16)
+        else:
+            XP = linear_fwd(x, W, None, _lib.LGNN_ACT_NONE)
         a_s = torch.empty(M, heads, dtype=torch.float32, device=dev)
         a_d = torch.empty(M, heads, dtype=torch.float32, device=dev)
         _lib.call("lgnn_gat_att", _lib.ptr(XP), M, heads, C, _lib.ptr(att_src), _lib.ptr(att_dst),
@@ -1215,7 +1313,22 @@ class _GATConv(torch.autograd.Function):
         red = torch.empty(3 * HC, dtype=torch.float32, device=dev)
         _lib.call("lgnn_reduce_partials", _lib.ptr(part), P, 3 * HC, _lib.ptr(red), _s(dev))
         want_dx = ctx.needs_input_grad[0]
-        if ctx.dense:
+        if ctx.bf16 and bf16_mfma_fits(HC):
+            dg = dXPb if dXPb is not None else dXP.to(torch.bfloat16)
+            dW = bf16_wgrad(dg, x, HC)
+            dx = None
+            if want_dx:
+                K = W.size(1)
+                if K <= 128:
+                    WTb = getattr(ctx, "wt", None)
+                    if WTb is None:
+                        WTb = bf16_weight_operands(W, True)[1]
+                    dx, dxb = bf16_gemm(dg, WTb, None, K, want_yb=BF16_OUT)
+                    if dxb is not None:
+                        _remember_bf16(dx, dxb)
+                else:
+                    dx = mm_dense(dg, W.to(torch.bfloat16), True)
+        elif ctx.dense:
             if ctx.bf16:  # rounded once for both products
                 dg = dXPb if dXPb is not None else dXP.to(torch.bfloat16)
             else:
