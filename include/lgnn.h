@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 18
+#define LGNN_ABI_VERSION 19
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -579,11 +579,14 @@ int lgnn_cc_pool(const float* features, int channels, int64_t num_pixels, const 
  * .to(torch.bfloat16), fp32 accumulation and output). Replace the bf16 nn.Linear / GATConv.lin
  * GEMMs of the bf16 configuration — in_proj (reference src/lesion_gnn/models/gat.py:29,
  * nn.Linear(1025, 128)) and GATConv.lin (gat.py:31, PyG Linear(bias=False)) — forward and
- * backward. Weight operands: lgnn_bf16_weight_prep writes Wb [128][lgnn_bf16_kpad(K)] (bf16 W,
- * zero-padded) and, when WTb != NULL (requires K <= 128), WTb [128][lgnn_bf16_kpad(N)] (bf16
- * W^T) for dX = dY W.
+ * backward. Weight operands: lgnn_bf16_weight_prep writes Wb = bf16 W as a zero-padded
+ * [128][lgnn_bf16_kpad(K)] matrix and, when WTb != NULL (requires K <= 128), WTb = bf16 W^T as
+ * [128][lgnn_bf16_kpad(N)], both in MFMA fragment order: element (r, q) at
+ * ((((q / 16) * 4 + r / 32) * 64 + 32 ((q / 8) & 1) + r % 32) * 8 + q % 8.
  *   lgnn_bf16_gemm: Y[M][N] = A[M][K] W^T (+ bias), N <= 128; A fp32 (a_is_f32 = 1, rounded
- *     as loaded, any K) or bf16 (K % 4 == 0); writes Y fp32 and/or Yb bf16 (either nullable).
+ *     as loaded, any K) or bf16 (K % 4 == 0); writes Y fp32 and/or Yb bf16 (either nullable);
+ *     colsum_part (nullable) [ceil(M / 64)][N]: each 64-row tile's column sums of Y (sum them
+ *     with lgnn_reduce_partials: the bias gradient of a following Linear, fixed order).
  *     For dX: A = dY (bf16, K = N), Wb = WTb, N = K.
  *   lgnn_bf16_wgrad: partials [num_partials][N][K] of dW = dY^T X (dYb bf16 [M][N], N even;
  *     X fp32 or bf16 [M][K]); num_partials from lgnn_bf16_wgrad_partials(M, K); sum them with
@@ -593,7 +596,8 @@ int lgnn_bf16_kpad(int K);
 int lgnn_bf16_weight_prep(const float* W, int N, int K, uint16_t* Wb, uint16_t* WTb,
                           void* stream);
 int lgnn_bf16_gemm(const void* A, int a_is_f32, int64_t M, int K, const uint16_t* Wb,
-                   const float* bias, int N, float* Y, uint16_t* Yb, void* stream);
+                   const float* bias, int N, float* Y, uint16_t* Yb, float* colsum_part,
+                   void* stream);
 int lgnn_bf16_wgrad_partials(int64_t M, int K);
 int lgnn_bf16_wgrad(const uint16_t* dYb, int N, const void* X, int x_is_f32, int64_t M, int K,
                     float* partials, int num_partials, void* stream);

@@ -49,6 +49,12 @@ __device__ __forceinline__ f32x16 mfma_bf(u32x4 a, u32x4 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
                                                  __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
 }
+// a value through an empty asm: a select feeding a buffer offset stays a v_cndmask instead of being
+// sunk into two branch-guarded loads (whose join makes the wait-count pass drain to vmcnt(0))
+__device__ __forceinline__ int opaque(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
 __device__ __forceinline__ uint32_t ldb32(Buf b, int off) {
   return __builtin_amdgcn_raw_buffer_load_b32(b, off, 0, 0);
 }
@@ -62,25 +68,31 @@ struct ARegs {
   uint32_t v[AF32 ? 16 : 8];
 };
 
-// AF32 && VEC: K % 4 == 0 (one 16-B load per row); AF32 && !VEC: any K (four 4-B loads);
-// bf16 A: K % 4 == 0 (one 8-B load per row)
-template <bool AF32, bool VEC>
+// One 16-B (fp32) or 8-B (bf16) load per row and lane. FULL: the chunk lies inside K, so no
+// column test; else every group past K reads 0 and (fp32, K % 4 != 0: !VEC) the one group that
+// straddles K loads dword by dword. Rows past M read 0 through the buffer range. Buffer loads
+// need dword alignment only, so fp32 rows of any K take the 16-B form. Branch-free, so the
+// compiler's wait counts stay exact across the unrolled chunk sequence.
+template <bool AF32, bool VEC, bool FULL>
 __device__ __forceinline__ void gemm_load_a(ARegs<AF32>& R, Buf bA, int K, int c, int rq, int kq) {
   const int k = c * BK + kq;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = rq + 4 * i;
-    if constexpr (AF32 && VEC) {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(bA, k < K ? (row * K + k) * 4 : OOB,
-                                                            0, 0);
+    const int off = row * K + k;
+    if constexpr (AF32 && (FULL || VEC)) {
+      const u32x4 v =
+          __builtin_amdgcn_raw_buffer_load_b128(bA, FULL ? off * 4 : opaque(k < K ? off * 4 : OOB), 0, 0);
 #pragma unroll
       for (int j = 0; j < 4; ++j) R.v[4 * i + j] = v[j];
     } else if constexpr (AF32) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) R.v[4 * i + j] = ldb32(bA, k + j < K ? (row * K + k + j) * 4 : OOB);
+      for (int j = 0; j < 4; ++j)
+        R.v[4 * i + j] = ldb32(bA, opaque(k + j < K ? (off + j) * 4 : OOB));
     } else {
       const u32x2 v = __builtin_bit_cast(
-          u32x2, __builtin_amdgcn_raw_buffer_load_b64(bA, k < K ? (row * K + k) * 2 : OOB, 0, 0));
+          u32x2, __builtin_amdgcn_raw_buffer_load_b64(bA, FULL ? off * 2 : opaque(k < K ? off * 2 : OOB),
+                                                      0, 0));
       R.v[2 * i] = v[0];
       R.v[2 * i + 1] = v[1];
     }
@@ -105,41 +117,40 @@ __device__ __forceinline__ void gemm_store_a(unsigned char* img, const ARegs<AF3
   }
 }
 
-// W fragments of chunk c: row 32 wave + li of the [128][Kp] bf16 operand, k 16 s + 8 h .. + 7
-__device__ __forceinline__ void gemm_load_b(u32x4 (&b)[4], const uint16_t* __restrict__ Wrow,
-                                            int c, int h) {
+// Weight operand in fragment order: for chunk c, k-step s and wave w, the 64 lanes' 16-B MFMA
+// fragments (row 32 w + li, columns 64 c + 16 s + 8 h .. + 7) are 1 KiB contiguous, so each wave
+// load reads whole cache lines. Element (row r, column q) sits at
+//   ((((q / 16) * 4 + r / 32) * 64 + 32 ((q / 8) & 1) + r % 32) * 8 + q % 8.
+__device__ __forceinline__ void gemm_load_b(u32x4 (&b)[4], Buf bW, int wlane, int c, int h) {
 #pragma unroll
   for (int s = 0; s < 4; ++s)
-    b[s] = *reinterpret_cast<const u32x4*>(Wrow + c * BK + 16 * s + 8 * h);
+    b[s] = __builtin_amdgcn_raw_buffer_load_b128(bW, ((c * 4 + s) * 4 * 512 + wlane) * 2, 0, 0);
 }
 
-template <bool AF32, bool VEC>
+// NCK > 0: exactly NCK chunks (Kp = 64 NCK), the loop fully unrolled — chunks 0 .. NCK - 2 are
+// inside K, only the last tests columns; NCK = 0: any Kp, every chunk tests its columns.
+template <bool AF32, bool VEC, int NCK>
 __global__ __launch_bounds__(NT) void k_bf_gemm(const void* __restrict__ A, int64_t M, int K,
                                                 const uint16_t* __restrict__ Wb, int Kp,
                                                 const float* __restrict__ bias, int N,
-                                                float* __restrict__ Y, uint16_t* __restrict__ Yb) {
+                                                float* __restrict__ Y, uint16_t* __restrict__ Yb,
+                                                float* __restrict__ colsum) {
   __shared__ __attribute__((aligned(16))) unsigned char img[2][TM * ROWB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, li = lane & 31;
   const int64_t r0 = xcd_block() * TM;
   constexpr int ESZ = AF32 ? 4 : 2;
   const Buf bA = mkbuf(static_cast<const char*>(A) + r0 * K * ESZ, (M - r0) * K * ESZ);
+  const Buf bW = mkbuf(Wb, (int64_t)128 * Kp * 2);
   const int rq = 16 * wave + (lane >> 4), kq = 4 * (lane & 15);
-  const int nck = Kp / BK;
-  const uint16_t* Wrow = Wb + (int64_t)(32 * wave + li) * Kp;
+  const int nck = NCK > 0 ? NCK : Kp / BK;
+  const int wrow = wave * 512 + lane * 8;  // this lane's fragment within a (chunk, k-step)
   f32x16 acc0 = {}, acc1 = {};
-  ARegs<AF32> R;
-  u32x4 b0[4], b1[4];
-  gemm_load_a<AF32, VEC>(R, bA, K, 0, rq, kq);
-  gemm_load_b(b0, Wrow, 0, h);
-  auto step = [&](int c, const u32x4(&bc)[4], u32x4(&bn)[4]) {
-    unsigned char* im = img[c & 1];
-    gemm_store_a<AF32>(im, R, rq, kq);
-    if (c + 1 < nck) {
-      gemm_load_a<AF32, VEC>(R, bA, K, c + 1, rq, kq);
-      gemm_load_b(bn, Wrow, c + 1, h);
-    }
-    __syncthreads();  // image c complete (and image c - 1's reads done two chunks ago)
+  auto load_a = [&](ARegs<AF32>& R, int c) {
+    if (NCK > 0 && c < NCK - 1) gemm_load_a<AF32, VEC, true>(R, bA, K, c, rq, kq);
+    else gemm_load_a<AF32, VEC, false>(R, bA, K, c, rq, kq);
+  };
+  auto mfma_chunk = [&](const unsigned char* im, const u32x4(&bc)[4]) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const u32x4 a0 = lds16(im + swz(li, 2 * s + h));
@@ -148,9 +159,49 @@ __global__ __launch_bounds__(NT) void k_bf_gemm(const void* __restrict__ A, int6
       acc1 = mfma_bf(a1, bc[s], acc1);
     }
   };
-  for (int c = 0; c < nck; c += 2) {
-    step(c, b0, b1);
-    if (c + 1 < nck) step(c + 1, b1, b0);
+  if constexpr (NCK > 0) {
+    // D register sets, the chunk sequence unrolled: chunks c + 1 .. c + D are in flight while
+    // chunk c is stored and used (D = 3 for the 17-chunk in_proj: 48 KiB per workgroup)
+    constexpr int D = NCK >= 8 ? 3 : 2;
+    ARegs<AF32> R[D];
+    u32x4 Bq[D][4];
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      if (d < NCK) {
+        load_a(R[d], d);
+        gemm_load_b(Bq[d], bW, wrow, d, h);
+      }
+#pragma unroll
+    for (int c = 0; c < NCK; ++c) {
+      unsigned char* im = img[c & 1];
+      gemm_store_a<AF32>(im, R[c % D], rq, kq);
+      if (c + D < NCK) load_a(R[c % D], c + D);
+      __syncthreads();  // image c complete (and image c - 2's reads done before barrier c - 1)
+      mfma_chunk(im, Bq[c % D]);
+      if (c + D < NCK) gemm_load_b(Bq[c % D], bW, wrow, c + D, h);
+    }
+  } else {
+    // any Kp: two register sets, ping-pong
+    ARegs<AF32> R0, R1;
+    u32x4 b0[4], b1[4];
+    load_a(R0, 0);
+    gemm_load_b(b0, bW, wrow, 0, h);
+    if (nck > 1) {
+      load_a(R1, 1);
+      gemm_load_b(b1, bW, wrow, 1, h);
+    }
+    auto step = [&](int c, ARegs<AF32>& R, u32x4(&bc)[4]) {
+      unsigned char* im = img[c & 1];
+      gemm_store_a<AF32>(im, R, rq, kq);
+      if (c + 2 < nck) load_a(R, c + 2);
+      __syncthreads();
+      mfma_chunk(im, bc);
+      if (c + 2 < nck) gemm_load_b(bc, bW, wrow, c + 2, h);
+    };
+    for (int c = 0; c < nck; c += 2) {
+      step(c, R0, b0);
+      if (c + 1 < nck) step(c + 1, R1, b1);
+    }
   }
   // epilogue (P layout): + b; fp32 rows and their bf16 copy as 128-B / 64-B row segments
   const int n = 32 * wave + li;
@@ -158,52 +209,87 @@ __global__ __launch_bounds__(NT) void k_bf_gemm(const void* __restrict__ A, int6
   const float bv = (bias && nok) ? bias[n] : 0.f;
   const Buf bY = mkbuf(Y ? Y + r0 * N : nullptr, Y ? (M - r0) * N * 4 : 0);
   const Buf bYb = mkbuf(Yb ? Yb + r0 * N : nullptr, Yb ? (M - r0) * N * 2 : 0);
+  const int ncol = nok ? n : OOB / 4;  // out-of-range column: every store lands past the range
+  if (colsum) {  // this tile's column sums of Y (rows past M hold 0): 32 rows per lane half
+    float cs = 0.f;
 #pragma unroll
-  for (int q = 0; q < 2; ++q)
+    for (int r = 0; r < 16; ++r) cs += acc0[r];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float v = (q ? acc1[r] : acc0[r]) + bv;
-      const int e = m * N + n;
-      if (Y) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), bY, nok ? e * 4 : OOB, 0, 0);
-      if (Yb)
+    for (int r = 0; r < 16; ++r) cs += acc1[r];
+    cs += __shfl_xor(cs, 32, 64);
+    const int64_t rows = M - r0 < TM ? M - r0 : TM;
+    if (h == 0 && nok) colsum[(r0 / TM) * N + n] = cs + (float)rows * bv;
+  }
+  if (Y) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float v = (q ? acc1[r] : acc0[r]) + bv;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), bY, (m * N + ncol) * 4, 0, 0);
+      }
+  }
+  if (Yb) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float v = (q ? acc1[r] : acc0[r]) + bv;
         __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(pk2(v, 0.f) & 0xffffu), bYb,
-                                              nok ? e * 2 : OOB, 0, 0);
-    }
+                                              (m * N + ncol) * 2, 0, 0);
+      }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
-// dW partial slabs: part[s][n][k] = sum over split s's row chunks of dY[m][n] X[m][k]
+// dW partial slabs: part[s][n][k] = sum over split s's CPB row chunks of dY[m][n] X[m][k]
 // ------------------------------------------------------------------------------------------
 template <bool XF32>
 struct WRegs {
-  uint32_t x[XF32 ? 16 : 8];  // X: XF32 k = lane, rows 16 w + 8 g + j; bf16 k pair, 8 rows
-  uint32_t y[16];             // dY: n pair 2 lane, rows 16 w + 8 g + j (g < 2, j < 8)
+  // X: XF32 k = k0 + 4 (lane & 15) + 0..3 of rows 16 w + 4 (lane >> 4) + i (i < 4); bf16 the k
+  // pair 2 (lane & 31) of rows 16 w + 8 (lane >> 5) + j (j < 8)
+  uint32_t x[XF32 ? 16 : 8];
+  uint32_t y[16];  // dY: n pair 2 lane, rows 16 w + 8 g + j (g < 2, j < 8)
 };
 
-template <bool XF32>
-__device__ __forceinline__ void wg_load(WRegs<XF32>& R, Buf bX, Buf bY, int64_t M, int K, int N,
-                                        int64_t m0, int k0, int lane, int wave) {
-  // every row offset below is < M * K * size (checked on the host: < 2^31)
+// Rows past M read 0 through the buffer ranges (offsets computed in 32 bits: M K size < 2^31 is
+// checked on the host, and a row past M lands past the range or wraps negative, i.e. past it
+// too). Columns n >= N of dY and k >= K of X are not masked: they only feed dW entries the slab
+// store drops. No selects, so no branches: the compiler's wait counts stay exact. FULL: the
+// k-block lies inside K (16-B loads); else dword loads, each range-checked on its own.
+template <bool XF32, bool FULL>
+__device__ __forceinline__ void wg_load(WRegs<XF32>& R, Buf bX, Buf bY, int K, int N, int m0,
+                                        int k0, int lane, int wave) {
+  const int n = 2 * lane;
 #pragma unroll
   for (int g = 0; g < 2; ++g)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int64_t m = m0 + 16 * wave + 8 * g + j;
-      const bool mok = m < M;
-      const int n = 2 * lane;
-      R.y[8 * g + j] = ldb32(bY, mok && n < N ? (int)((m * N + n) * 2) : OOB);
-      if constexpr (XF32) {
-        const int k = k0 + lane;
-        R.x[8 * g + j] = ldb32(bX, mok && k < K ? (int)((m * K + k) * 4) : OOB);
+      const int m = m0 + 16 * wave + 8 * g + j;
+      R.y[8 * g + j] = ldb32(bY, (m * N + n) * 2);
+    }
+  if constexpr (XF32) {
+    const int k = k0 + 4 * (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int off = (m0 + 16 * wave + 4 * (lane >> 4) + i) * K + k;
+      if constexpr (FULL) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(bX, off * 4, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) R.x[4 * i + j] = v[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) R.x[4 * i + j] = ldb32(bX, (off + j) * 4);
       }
     }
-  if constexpr (!XF32) {  // lanes 0-31 rows 16 w + j, lanes 32-63 rows 16 w + 8 + j
+  } else {  // lanes 0-31 rows 16 w + j, lanes 32-63 rows 16 w + 8 + j
     const int k = k0 + 2 * (lane & 31);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int64_t m = m0 + 16 * wave + 8 * (lane >> 5) + j;
-      R.x[j] = ldb32(bX, m < M && k < K ? (int)((m * K + k) * 2) : OOB);
+      const int m = m0 + 16 * wave + 8 * (lane >> 5) + j;
+      R.x[j] = ldb32(bX, (m * K + k) * 2);
     }
   }
 }
@@ -228,45 +314,45 @@ __device__ __forceinline__ void wg_store(unsigned char* iy, unsigned char* ix, c
     const int ch = 2 * wave + g;  // rows 8 ch .. 8 ch + 7 of the chunk
     *reinterpret_cast<u32x4*>(iy + swz(2 * lane, ch)) = pack_halves<false>(R.y + 8 * g);
     *reinterpret_cast<u32x4*>(iy + swz(2 * lane + 1, ch)) = pack_halves<true>(R.y + 8 * g);
-    if constexpr (XF32) {
-      u32x4 o;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        o[i] = pk2(__uint_as_float(R.x[8 * g + 2 * i]), __uint_as_float(R.x[8 * g + 2 * i + 1]));
-      *reinterpret_cast<u32x4*>(ix + swz(lane, ch)) = o;
-    }
   }
-  if constexpr (!XF32) {
+  if constexpr (XF32) {  // column k + j: rows 16 w + 4 q .. + 3 as one 8-B write
+    const int q = lane >> 4, kq = 4 * (lane & 15);
+    const int ch = 2 * wave + (q >> 1), off = (q & 1) * 8;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      u32x2 o;
+      o[0] = pk2(__uint_as_float(R.x[j]), __uint_as_float(R.x[4 + j]));
+      o[1] = pk2(__uint_as_float(R.x[8 + j]), __uint_as_float(R.x[12 + j]));
+      *reinterpret_cast<u32x2*>(ix + swz(kq + j, ch) + off) = o;
+    }
+  } else {
     const int ch = 2 * wave + (lane >> 5), k = 2 * (lane & 31);
     *reinterpret_cast<u32x4*>(ix + swz(k, ch)) = pack_halves<false>(R.x);
     *reinterpret_cast<u32x4*>(ix + swz(k + 1, ch)) = pack_halves<true>(R.x);
   }
 }
 
-template <bool XF32>
-__global__ __launch_bounds__(NT) void k_bf_wgrad(const uint16_t* __restrict__ dYb, int N,
-                                                 const void* __restrict__ X, int64_t M, int K,
-                                                 int nkb, int S, float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) unsigned char iy[2][128 * ROWB];  // dY^T [n][m]
-  __shared__ __attribute__((aligned(16))) unsigned char ix[2][64 * ROWB];   // X^T [k][m]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+struct WgSmem {
+  unsigned char y[2][128 * ROWB];  // dY^T [n][m]
+  unsigned char x[2][64 * ROWB];   // X^T [k][m]
+};
+
+// the split's CPB chunks, fully unrolled with two register sets in flight
+template <bool XF32, bool FULL, int CPB>
+__device__ __forceinline__ void wg_run(WgSmem& sm, f32x16& acc0, f32x16& acc1, Buf bX, Buf bY,
+                                       int K, int N, int c0, int k0, int lane, int wave) {
   const int h = lane >> 5, li = lane & 31;
-  const int64_t L = xcd_block();  // blocks of one row split (adjacent k-blocks) share an XCD
-  const int kb = (int)(L % nkb), s = (int)(L / nkb);
-  const int k0 = kb * BK;
-  const int64_t nch = (M + TM - 1) / TM;
-  constexpr int ESZ = XF32 ? 4 : 2;
-  const Buf bX = mkbuf(X, M * K * ESZ), bY = mkbuf(dYb, M * N * 2);
-  f32x16 acc0 = {}, acc1 = {};
-  WRegs<XF32> R;
-  int64_t c = s;
-  if (c < nch) wg_load<XF32>(R, bX, bY, M, K, N, c * TM, k0, lane, wave);
-  for (int it = 0; c < nch; c += S, ++it) {
-    unsigned char* py = iy[it & 1];
-    unsigned char* px = ix[it & 1];
+  WRegs<XF32> R0, R1;
+  wg_load<XF32, FULL>(R0, bX, bY, K, N, c0 * TM, k0, lane, wave);
+  if (CPB > 1) wg_load<XF32, FULL>(R1, bX, bY, K, N, (c0 + 1) * TM, k0, lane, wave);
+#pragma unroll
+  for (int i = 0; i < CPB; ++i) {
+    WRegs<XF32>& R = (i & 1) ? R1 : R0;
+    unsigned char* py = sm.y[i & 1];
+    unsigned char* px = sm.x[i & 1];
     wg_store<XF32>(py, px, R, lane, wave);
-    if (c + S < nch) wg_load<XF32>(R, bX, bY, M, K, N, (c + S) * TM, k0, lane, wave);
-    __syncthreads();
+    if (i + 2 < CPB) wg_load<XF32, FULL>(R, bX, bY, K, N, (c0 + i + 2) * TM, k0, lane, wave);
+    __syncthreads();  // images i complete (images i - 2's reads done before barrier i - 1)
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
       const u32x4 a = lds16(py + swz(32 * wave + li, 2 * st + h));
@@ -276,6 +362,25 @@ __global__ __launch_bounds__(NT) void k_bf_wgrad(const uint16_t* __restrict__ dY
       acc1 = mfma_bf(a, x1, acc1);
     }
   }
+}
+
+template <bool XF32, int CPB>
+__global__ __launch_bounds__(NT) void k_bf_wgrad(const uint16_t* __restrict__ dYb, int N,
+                                                 const void* __restrict__ X, int64_t M, int K,
+                                                 int nkb, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) WgSmem sm;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h = lane >> 5, li = lane & 31;
+  const int64_t L = xcd_block();  // the k-blocks of one row split are adjacent: one XCD's L2
+  const int kb = (int)(L % nkb), s = (int)(L / nkb);
+  const int k0 = kb * BK;
+  constexpr int ESZ = XF32 ? 4 : 2;
+  const Buf bX = mkbuf(X, M * K * ESZ), bY = mkbuf(dYb, M * N * 2);
+  f32x16 acc0 = {}, acc1 = {};
+  if (k0 + BK <= K)  // uniform: one unrolled body per block
+    wg_run<XF32, true, CPB>(sm, acc0, acc1, bX, bY, K, N, s * CPB, k0, lane, wave);
+  else
+    wg_run<XF32, false, CPB>(sm, acc0, acc1, bX, bY, K, N, s * CPB, k0, lane, wave);
   // slab s: rows n = 32 w + (r & 3) + 8 (r >> 2) + 4 h, columns k0 + 32 kk + li
   float* slab = part + (int64_t)s * N * K;
 #pragma unroll
@@ -290,23 +395,23 @@ __global__ __launch_bounds__(NT) void k_bf_wgrad(const uint16_t* __restrict__ dY
 }
 
 // ------------------------------------------------------------------------------------------
-// weight operands: Wb [128][Kp] = bf16(W), WTb [128][Np] = bf16(W^T), zero-padded
+// weight operands: Wb [128][Kp] = bf16(W), WTb [128][Np] = bf16(W^T), zero-padded, in the
+// fragment order of gemm_load_b
 // ------------------------------------------------------------------------------------------
 __global__ void k_bf_wprep(const float* __restrict__ W, int N, int K, int Kp, int Np,
                            uint16_t* __restrict__ Wb, uint16_t* __restrict__ WTb) {
   const int64_t n1 = (int64_t)128 * Kp, n2 = WTb ? (int64_t)128 * Np : 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n1 + n2;
        i += (int64_t)gridDim.x * blockDim.x) {
-    if (i < n1) {
-      const int n = (int)(i / Kp), k = (int)(i % Kp);
-      const float v = (n < N && k < K) ? W[(int64_t)n * K + k] : 0.f;
-      Wb[i] = (uint16_t)(pk2(v, 0.f) & 0xffffu);
-    } else {
-      const int64_t j = i - n1;
-      const int k = (int)(j / Np), n = (int)(j % Np);
-      const float v = (n < N && k < K) ? W[(int64_t)n * K + k] : 0.f;
-      WTb[j] = (uint16_t)(pk2(v, 0.f) & 0xffffu);
-    }
+    // element i of the fragment order: (row r, column q) of the [128][width] operand
+    const bool t = i >= n1;
+    const int64_t j = t ? i - n1 : i;
+    const int e = (int)(j & 7), lane = (int)((j >> 3) & 63), wave = (int)((j >> 9) & 3);
+    const int64_t cs = j >> 11;  // 4 chunk + k-step
+    const int r = 32 * wave + (lane & 31), q = (int)(cs * 16) + 8 * (lane >> 5) + e;
+    const int n = t ? q : r, k = t ? r : q;  // W^T: row k, column n
+    const float v = (n < N && k < K) ? W[(int64_t)n * K + k] : 0.f;
+    (t ? WTb : Wb)[j] = (uint16_t)(pk2(v, 0.f) & 0xffffu);
   }
 }
 
@@ -333,53 +438,85 @@ extern "C" int lgnn_bf16_weight_prep(const float* W, int N, int K, uint16_t* Wb,
 }
 
 extern "C" int lgnn_bf16_gemm(const void* A, int a_is_f32, int64_t M, int K, const uint16_t* Wb,
-                              const float* bias, int N, float* Y, uint16_t* Yb, void* stream) {
+                              const float* bias, int N, float* Y, uint16_t* Yb, float* colsum_part,
+                              void* stream) {
   if (M < 0 || K < 1 || N < 1 || N > 128 || !Wb || (!Y && !Yb)) return LGNN_EINVAL;
   if (M > 0 && !A) return LGNN_EINVAL;
   if (!a_is_f32 && K % 4 != 0) return LGNN_EINVAL;
-  if (M * (int64_t)K * 4 >= ((int64_t)1 << 31) || M * (int64_t)N * 4 >= ((int64_t)1 << 31))
+  // 32-bit buffer offsets; a masked column's stores land at >= 2^30 bytes, past Yb's range too
+  if ((M + TM) * (int64_t)K * 4 >= ((int64_t)1 << 31) || M * (int64_t)N * 4 >= ((int64_t)1 << 30))
     return LGNN_EINVAL;
   if (M == 0) return LGNN_OK;
-  const int Kp = lgnn_bf16_kpad(K);
+  const int Kp = lgnn_bf16_kpad(K), nck = Kp / BK;
   const dim3 grid((unsigned)((M + TM - 1) / TM)), block(NT);
   hipStream_t s = as_stream(stream);
-  if (!a_is_f32)
-    hipLaunchKernelGGL((k_bf_gemm<false, true>), grid, block, 0, s, A, M, K, Wb, Kp, bias, N, Y,
-                       Yb);
-  else if (K % 4 == 0)
-    hipLaunchKernelGGL((k_bf_gemm<true, true>), grid, block, 0, s, A, M, K, Wb, Kp, bias, N, Y, Yb);
-  else
-    hipLaunchKernelGGL((k_bf_gemm<true, false>), grid, block, 0, s, A, M, K, Wb, Kp, bias, N, Y,
-                       Yb);
+#define LGNN_BFG(AF, V, NC) \
+  hipLaunchKernelGGL((k_bf_gemm<AF, V, NC>), grid, block, 0, s, A, M, K, Wb, Kp, bias, N, Y, Yb, \
+                     colsum_part)
+  // the unrolled bodies: K <= 128 (the GAT layers, dX) and K <= 1088 (the reference in_proj,
+  // 1025 input channels); other widths run the generic loop
+  const bool v = K % 4 == 0;
+  if (!a_is_f32) {
+    if (nck == 2) LGNN_BFG(false, true, 2);
+    else LGNN_BFG(false, true, 0);
+  } else if (nck == 2) {
+    if (v) LGNN_BFG(true, true, 2);
+    else LGNN_BFG(true, false, 2);
+  } else if (nck == 17) {
+    if (v) LGNN_BFG(true, true, 17);
+    else LGNN_BFG(true, false, 17);
+  } else {
+    if (v) LGNN_BFG(true, true, 0);
+    else LGNN_BFG(true, false, 0);
+  }
+#undef LGNN_BFG
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? LGNN_OK : (int)e;
 }
 
-extern "C" int lgnn_bf16_wgrad_partials(int64_t M, int K) {
-  // about 512 workgroups (two per CU) over (k-block, row split), at most one split per chunk
-  const int64_t nch = (M + TM - 1) / TM;
+// chunks per split: the smallest of 3, 6, 12, 24 that keeps the grid within about 480
+// workgroups (two per CU fit at once)
+static int wg_cpb(int64_t M, int K) {
+  const int64_t nch = std::max<int64_t>((M + TM - 1) / TM, 1);
   const int nkb = lgnn_bf16_kpad(K) / BK;
-  int64_t S = (512 + nkb - 1) / std::max(nkb, 1);
-  S = std::min<int64_t>(std::max<int64_t>(S, 1), std::max<int64_t>(nch, 1));
-  return (int)S;
+  for (int cpb = 3; cpb < 24; cpb *= 2)
+    if (nkb * ((nch + cpb - 1) / cpb) <= 480) return cpb;
+  return 24;
+}
+
+extern "C" int lgnn_bf16_wgrad_partials(int64_t M, int K) {
+  if (M < 0 || K < 1) return 0;
+  const int64_t nch = std::max<int64_t>((M + TM - 1) / TM, 1);
+  const int cpb = wg_cpb(M, K);
+  return (int)((nch + cpb - 1) / cpb);
 }
 
 extern "C" int lgnn_bf16_wgrad(const uint16_t* dYb, int N, const void* X, int x_is_f32, int64_t M,
                                int K, float* partials, int num_partials, void* stream) {
-  if (M < 0 || K < 1 || N < 1 || N > 128 || N % 2 != 0 || !partials || num_partials < 1)
-    return LGNN_EINVAL;
+  if (M < 0 || K < 1 || N < 1 || N > 128 || N % 2 != 0 || !partials) return LGNN_EINVAL;
+  if (num_partials != lgnn_bf16_wgrad_partials(M, K)) return LGNN_EINVAL;
   if (M > 0 && (!dYb || !X)) return LGNN_EINVAL;
   if (!x_is_f32 && K % 2 != 0) return LGNN_EINVAL;
-  if (M * (int64_t)K * 4 >= ((int64_t)1 << 31)) return LGNN_EINVAL;
-  const int nkb = lgnn_bf16_kpad(K) / BK;
+  if ((M + 32 * TM) * (int64_t)K * 4 >= ((int64_t)1 << 31)) return LGNN_EINVAL;
+  const int nkb = lgnn_bf16_kpad(K) / BK, cpb = wg_cpb(M, K);
   const dim3 grid((unsigned)(nkb * num_partials)), block(NT);
   hipStream_t s = as_stream(stream);
-  if (x_is_f32)
-    hipLaunchKernelGGL((k_bf_wgrad<true>), grid, block, 0, s, dYb, N, X, M, K, nkb, num_partials,
-                       partials);
-  else
-    hipLaunchKernelGGL((k_bf_wgrad<false>), grid, block, 0, s, dYb, N, X, M, K, nkb, num_partials,
-                       partials);
+#define LGNN_BFW(XF, C) \
+  hipLaunchKernelGGL((k_bf_wgrad<XF, C>), grid, block, 0, s, dYb, N, X, M, K, nkb, partials)
+#define LGNN_BFW_C(XF)              \
+  switch (cpb) {                    \
+    case 3: LGNN_BFW(XF, 3); break;   \
+    case 6: LGNN_BFW(XF, 6); break;   \
+    case 12: LGNN_BFW(XF, 12); break; \
+    default: LGNN_BFW(XF, 24); break; \
+  }
+  if (x_is_f32) {
+    LGNN_BFW_C(true)
+  } else {
+    LGNN_BFW_C(false)
+  }
+#undef LGNN_BFW_C
+#undef LGNN_BFW
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? LGNN_OK : (int)e;
 }

@@ -518,17 +518,43 @@ def bf16_weight_operands(W: torch.Tensor, want_t: bool):
     return Wb, WTb
 
 
-def bf16_gemm(A: torch.Tensor, Wb: torch.Tensor, bias, N: int, want_yb: bool = False):
+def bf16_gemm(A: torch.Tensor, Wb: torch.Tensor, bias, N: int, want_yb: bool = False,
+              want_colsum: bool = False):
     """Y = bf16(A) bf16(W)^T (+ bias) in fp32 (and its bf16 copy when want_yb): A fp32 (rounded
-    in the kernel) or bf16."""
+    in the kernel) or bf16. want_colsum: Y's per-tile column sums are remembered beside Y
+    (colsum_of: a following Linear's bias gradient without a pass over Y)."""
     A = A.contiguous()
     M, K = A.shape
     Y = torch.empty(M, N, dtype=torch.float32, device=A.device)
     Yb = torch.empty(M, N, dtype=torch.bfloat16, device=A.device) if want_yb else None
+    cs = torch.empty((M + 63) // 64 * N, dtype=torch.float32, device=A.device) \
+        if want_colsum and M > 0 else None
     _lib.call("lgnn_bf16_gemm", _lib.ptr(A), int(A.dtype == torch.float32), M, K, _lib.ptr(Wb),
               _lib.ptr(_f32c(bias) if bias is not None else None), N, _lib.ptr(Y), _lib.ptr(Yb),
-              _s(A.device))
+              _lib.ptr(cs), _s(A.device))
+    if cs is not None:
+        _COLSUMS[id(Y)] = (weakref.ref(Y), Y._version, cs)
+        weakref.finalize(Y, _COLSUMS.pop, id(Y), None)
     return Y, Yb
+
+
+_COLSUMS: dict = {}
+
+
+def colsum_of(y: torch.Tensor):
+    """y.sum(0) from the per-tile column sums its producing GEMM wrote (fixed order), if y is
+    that output unchanged; else None."""
+    rec = _COLSUMS.get(id(y))
+    if rec is None:
+        return None
+    ref, version, cs = rec
+    if ref() is not y or y._version != version:
+        return None
+    N = y.size(1)
+    out = torch.empty(N, dtype=torch.float32, device=y.device)
+    _lib.call("lgnn_reduce_partials", _lib.ptr(cs), cs.numel() // N, N, _lib.ptr(out),
+              _s(y.device))
+    return out
 
 
 def bf16_wgrad(dYb: torch.Tensor, X: torch.Tensor, N: int) -> torch.Tensor:
@@ -587,7 +613,11 @@ class _DenseLinear(torch.autograd.Function):
     def backward(ctx, dy):
         x, W = ctx.saved_tensors
         dy = _f32c(dy)
-        db = dy.sum(0) if ctx.has_b else None
+        db = None
+        if ctx.has_b:  # from the column sums dy's producing GEMM wrote, when it was ours
+            db = colsum_of(dy)
+            if db is None:
+                db = dy.sum(0)
         N, K = W.shape
         if ctx.bf16 and bf16_mfma_fits(N):
             dyb = _bf16_operand(dy)
@@ -1323,7 +1353,8 @@ class _GATConv(torch.autograd.Function):
                     WTb = getattr(ctx, "wt", None)
                     if WTb is None:
                         WTb = bf16_weight_operands(W, True)[1]
-                    dx, dxb = bf16_gemm(dg, WTb, None, K, want_yb=BF16_OUT)
+                    # dx's column sums ride along: the in_proj backward's bias gradient
+                    dx, dxb = bf16_gemm(dg, WTb, None, K, want_yb=BF16_OUT, want_colsum=True)
                     if dxb is not None:
                         _remember_bf16(dx, dxb)
                 else:

@@ -38,6 +38,13 @@ def check_product(got: torch.Tensor, a: np.ndarray, b: np.ndarray, add=0.0):
     assert (err <= bound).all(), f"max err {err.max():.3e}, worst ratio {(err / bound).max():.2f}"
 
 
+def frag_order(mat: np.ndarray) -> np.ndarray:
+    """[128][width] -> the kernels' fragment order (include/lgnn.h, lgnn_bf16_weight_prep)."""
+    j = np.arange(mat.size)
+    e, lane, w, cs = j & 7, (j >> 3) & 63, (j >> 9) & 3, j >> 11
+    return mat[32 * w + (lane & 31), cs * 16 + 8 * (lane >> 5) + e]
+
+
 def _weights(N, K, dev, seed=0):
     g = torch.Generator().manual_seed(seed)
     return (torch.randn(N, K, generator=g) / K ** 0.5).to(dev)
@@ -50,12 +57,12 @@ def test_weight_prep_bitexact(cuda, N, K):
     kp, npad = _lib.load().lgnn_bf16_kpad(K), _lib.load().lgnn_bf16_kpad(N)
     want = np.zeros((128, kp), np.uint16)
     want[:N, :K] = bf16_rne(W.cpu().numpy())
-    assert np.array_equal(Wb.view(torch.int16).cpu().numpy().view(np.uint16).reshape(128, kp), want)
+    assert np.array_equal(Wb.view(torch.int16).cpu().numpy().view(np.uint16), frag_order(want))
     if K <= 128:
         wt = np.zeros((128, npad), np.uint16)
         wt[:K, :N] = bf16_rne(W.cpu().numpy()).T
-        got = WTb.view(torch.int16).cpu().numpy().view(np.uint16).reshape(128, npad)
-        assert np.array_equal(got, wt)
+        got = WTb.view(torch.int16).cpu().numpy().view(np.uint16)
+        assert np.array_equal(got, frag_order(wt))
     else:
         assert WTb is None
 
@@ -129,8 +136,27 @@ def test_bad_arguments_refused(cuda):
     Wb = torch.zeros(128 * 64, dtype=torch.bfloat16, device=cuda)
     Y = torch.empty(64, 128, device=cuda)
     rc = lib.lgnn_bf16_gemm(_lib.ptr(A), 0, 64, 30, _lib.ptr(Wb), None, 128, _lib.ptr(Y), None,
-                            None)
+                            None, None)
     assert rc == -22  # LGNN_EINVAL
     rc = lib.lgnn_bf16_gemm(_lib.ptr(A), 0, 64, 32, _lib.ptr(Wb), None, 129, _lib.ptr(Y), None,
-                            None)
+                            None, None)
     assert rc == -22  # LGNN_EINVAL
+
+
+@pytest.mark.parametrize("M,bias", [(42279, False), (4133, True), (1, True)])
+def test_colsum_rides_along(cuda, M, bias):
+    """want_colsum: the per-tile column sums the GEMM writes reduce (fixed order) to Y.sum(0);
+    colsum_of refuses a Y modified in place."""
+    K, N = 128, 128
+    g = torch.Generator().manual_seed(M)
+    A = torch.randn(M, K, generator=g).to(cuda).to(torch.bfloat16)
+    W = _weights(N, K, cuda, seed=5)
+    b = torch.randn(N, generator=g).to(cuda) if bias else None
+    Wb, _ = ops.bf16_weight_operands(W, False)
+    Y, _ = ops.bf16_gemm(A, Wb, b, N, want_colsum=True)
+    cs = ops.colsum_of(Y)
+    ref = Y.double().sum(0)
+    bound = 2.0 ** -18 * Y.double().abs().sum(0) + 1e-30
+    assert ((cs.double() - ref).abs() <= bound).all()
+    Y.add_(1.0)
+    assert ops.colsum_of(Y) is None
