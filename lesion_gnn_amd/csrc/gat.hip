@@ -112,6 +112,26 @@ __device__ __forceinline__ void st4_bf16(uint16_t* p, f32x4 v) {
       __builtin_bit_cast(unsigned long long, __builtin_convertvector(v, bf16x4_t));
 }
 
+// + bias, activation; fp32 row and (Yb) its bf16 copy, the next bf16 GEMM's operand
+template <int ACT, int NS>
+__device__ __forceinline__ void gat_out(const Pass<NS>& P, const f32x4 (&acc)[NS],
+                                        const float* __restrict__ bias, float* __restrict__ Y,
+                                        uint16_t* __restrict__ Yb, int64_t base) {
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    if (P.act[s]) {
+      const f32x4 bv = bias ? ld4(bias + P.fc[s]) : f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 o = acc[s] + bv;
+      if (ACT == LGNN_ACT_ELU) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = elu_f(o[j]);
+      }
+      st4(Y + base + P.f[s], o);
+      if (Yb) st4_bf16(Yb + base + P.f[s], o);
+    }
+  }
+}
+
 template <int ACT, int NS>
 __global__ __launch_bounds__(NT) void k_gat_fwd(const int32_t* __restrict__ rowptr,
                                                 const int32_t* __restrict__ col,
@@ -131,6 +151,45 @@ __global__ __launch_bounds__(NT) void k_gat_fwd(const int32_t* __restrict__ rowp
     const Pass<NS> P(p, L.li, HC, C);
     const int head = P.head;
     const float ad = a_d[L.row * H + head];
+    if (e1 - e0 <= EBN) {  // short row (k-NN graphs: k + 1 entries): one gather of everything,
+      // the same operations in the same order as the three passes below
+      int c[EBN];
+      float a[EBN];
+#pragma unroll
+      for (int u = 0; u < EBN; ++u) {
+        c[u] = col[e0 + u < e1 ? e0 + u : e0];
+        a[u] = a_s[(int64_t)c[u] * H + head];
+      }
+      f32x4 xv[EBN][NS];
+#pragma unroll
+      for (int u = 0; u < EBN; ++u)
+#pragma unroll
+        for (int s = 0; s < NS; ++s) xv[u][s] = ld4(XP + (int64_t)c[u] * HC + P.fc[s]);
+      float m = -INFINITY;
+#pragma unroll
+      for (int u = 0; u < EBN; ++u)
+        if (e0 + u < e1) m = fmaxf(m, leaky(a[u] + ad, slope));
+      float sum = 0.f;
+#pragma unroll
+      for (int u = 0; u < EBN; ++u)
+        if (e0 + u < e1) sum += expf(leaky(a[u] + ad, slope) - m);
+      sum += EPS16;
+      f32x4 acc[NS];
+#pragma unroll
+      for (int s = 0; s < NS; ++s) acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < EBN; ++u) {
+        if (e0 + u < e1) {
+          float al = expf(leaky(a[u] + ad, slope) - m) / sum;
+          if (P.leader && alpha) alpha[(int64_t)(e0 + u) * H + head] = al;
+          if (mask) al *= mask[(int64_t)(e0 + u) * H + head];
+#pragma unroll
+          for (int s = 0; s < NS; ++s) acc[s] += al * xv[u][s];
+        }
+      }
+      gat_out<ACT, NS>(P, acc, bias, Y, Yb, L.row * HC);
+      continue;
+    }
     // pass 1: row max of the logits (PyG: scatter max of the detached logits)
     float m = -INFINITY;
     for (int e = e0; e < e1; e += EB) {
@@ -187,19 +246,7 @@ __global__ __launch_bounds__(NT) void k_gat_fwd(const int32_t* __restrict__ rowp
         }
       }
     }
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      if (P.act[s]) {
-        const f32x4 bv = bias ? ld4(bias + P.fc[s]) : f32x4{0.f, 0.f, 0.f, 0.f};
-        f32x4 o = acc[s] + bv;
-        if (ACT == LGNN_ACT_ELU) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = elu_f(o[j]);
-        }
-        st4(Y + L.row * HC + P.f[s], o);
-        if (Yb) st4_bf16(Yb + L.row * HC + P.f[s], o);  // the next bf16 GEMM's operand
-      }
-    }
+    gat_out<ACT, NS>(P, acc, bias, Y, Yb, L.row * HC);
   }
 }
 
@@ -238,8 +285,44 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_edge(
       if (P.act[s]) st4(dZ + L.row * HC + P.f[s], dz[s]);
     }
     const float ad = a_d[L.row * H + head];
-    // two sweeps over the row: sweep 0 accumulates s_i, sweep 1 emits the logit gradients
     float s_i = 0.f, dad = 0.f;
+    if (e1 - e0 <= EBN) {  // short row: one gather of the source rows, the dot products kept
+      // (the same operations in the same order as the two sweeps below)
+      int c[EBN];
+#pragma unroll
+      for (int u = 0; u < EBN; ++u) c[u] = col[e0 + u < e1 ? e0 + u : e0];
+      f32x4 xv[EBN][NS];
+#pragma unroll
+      for (int u = 0; u < EBN; ++u)
+#pragma unroll
+        for (int s = 0; s < NS; ++s) xv[u][s] = ld4(XP + (int64_t)c[u] * HC + P.fc[s]);
+      float d[EBN], al[EBN];
+#pragma unroll
+      for (int u = 0; u < EBN; ++u) {
+        const int ee = e0 + u < e1 ? e0 + u : e0;
+        float part = 0.f;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) part += dot4(dz[s], xv[u][s]);
+        d[u] = group_sum(part, P.G);
+        if (mask) d[u] *= mask[(int64_t)ee * H + head];
+        al[u] = alpha[(int64_t)ee * H + head];
+      }
+#pragma unroll
+      for (int u = 0; u < EBN; ++u)
+        if (e0 + u < e1) s_i += al[u] * d[u];
+#pragma unroll
+      for (int u = 0; u < EBN; ++u) {
+        if (e0 + u < e1) {
+          const float pre = a_s[(int64_t)c[u] * H + head] + ad;
+          const float da = al[u] * (d[u] - s_i) * (pre > 0.f ? 1.f : slope);
+          dad += da;
+          if (P.leader) da_e[(int64_t)(e0 + u) * H + head] = da;
+        }
+      }
+      if (P.leader) da_d[L.row * H + head] = dad;
+      continue;
+    }
+    // two sweeps over the row: sweep 0 accumulates s_i, sweep 1 emits the logit gradients
 #pragma unroll 1
     for (int sweep = 0; sweep < 2; ++sweep) {
       for (int e = e0; e < e1; e += EBN) {
