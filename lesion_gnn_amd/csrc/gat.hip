@@ -22,7 +22,44 @@ constexpr int EB = 8;       // edges in flight per batch
 constexpr int MAXS = 4;     // feature strips of 128 (H*C <= 512)
 constexpr float EPS16 = 1e-16f;
 
+// optional occupancy floor of the row kernels (waves per SIMD; 0 = the compiler's choice). Forcing
+// one below their register demand spills, which costs far more than the waves gain (C3 step
+// 0.73 -> 1.32 ms at 6 waves); the 32-bit buffer offsets are what lowered the demand
+#ifndef LGNN_GAT_WPE
+#define LGNN_GAT_WPE 0
+#endif
+#if LGNN_GAT_WPE > 0
+#define GAT_OCC __attribute__((amdgpu_waves_per_eu(LGNN_GAT_WPE)))
+#else
+#define GAT_OCC
+#endif
+
 __device__ __forceinline__ float leaky(float v, float slope) { return v > 0.f ? v : v * slope; }
+
+// Raw buffer access (SGPR descriptor + 32-bit byte offset): one VGPR per gathered address instead
+// of two, which is what bounds these gather kernels' registers (8 source rows in flight). Every
+// array addressed this way is < 4 GiB (checked on the host, bytes_ok).
+typedef __amdgpu_buffer_rsrc_t Buf;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ Buf mkbuf(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)(uint32_t)bytes,
+                                           0x00020000);
+}
+__device__ __forceinline__ f32x4 bld4(Buf r, uint32_t off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ float bld1(Buf r, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ int bldi(Buf r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+}
+__device__ __forceinline__ void bst1(Buf r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), r, off, 0, 0);
+}
+__device__ __forceinline__ void bst4(Buf r, uint32_t off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
+}
 
 // sum over the G = C/4 lanes of a head group (all lanes receive the sum)
 __device__ __forceinline__ float group_sum(float v, int G) {
@@ -133,7 +170,7 @@ __device__ __forceinline__ void gat_out(const Pass<NS>& P, const f32x4 (&acc)[NS
 }
 
 template <int ACT, int NS>
-__global__ __launch_bounds__(NT) void k_gat_fwd(const int32_t* __restrict__ rowptr,
+__global__ __launch_bounds__(NT) GAT_OCC void k_gat_fwd(const int32_t* __restrict__ rowptr,
                                                 const int32_t* __restrict__ col,
                                                 const float* __restrict__ XP,
                                                 const float* __restrict__ a_s,
@@ -146,6 +183,9 @@ __global__ __launch_bounds__(NT) void k_gat_fwd(const int32_t* __restrict__ rowp
   const Lane L = lane_row();
   if (L.row >= M) return;
   const int HC = H * C;
+  const int64_t cap = rowptr[M];  // CSR entries: the extent of col and the per-edge arrays
+  const Buf bX = mkbuf(XP, M * HC * 4), bA = mkbuf(a_s, M * H * 4), bC = mkbuf(col, cap * 4);
+  const Buf bAl = mkbuf(alpha, alpha ? cap * H * 4 : 0), bM = mkbuf(mask, mask ? cap * H * 4 : 0);
   const int e0 = rowptr[L.row], e1 = rowptr[L.row + 1];
   for (int p = 0; p < num_passes(HC, NS); ++p) {
     const Pass<NS> P(p, L.li, HC, C);
@@ -157,14 +197,14 @@ __global__ __launch_bounds__(NT) void k_gat_fwd(const int32_t* __restrict__ rowp
       float a[EBN];
 #pragma unroll
       for (int u = 0; u < EBN; ++u) {
-        c[u] = col[e0 + u < e1 ? e0 + u : e0];
-        a[u] = a_s[(int64_t)c[u] * H + head];
+        c[u] = bldi(bC, (uint32_t)(e0 + u < e1 ? e0 + u : e0) * 4u);
+        a[u] = bld1(bA, (uint32_t)(c[u] * H + head) * 4u);
       }
       f32x4 xv[EBN][NS];
 #pragma unroll
       for (int u = 0; u < EBN; ++u)
 #pragma unroll
-        for (int s = 0; s < NS; ++s) xv[u][s] = ld4(XP + (int64_t)c[u] * HC + P.fc[s]);
+        for (int s = 0; s < NS; ++s) xv[u][s] = bld4(bX, ((uint32_t)c[u] * HC + P.fc[s]) * 4u);
       float m = -INFINITY;
 #pragma unroll
       for (int u = 0; u < EBN; ++u)
@@ -180,9 +220,10 @@ __global__ __launch_bounds__(NT) void k_gat_fwd(const int32_t* __restrict__ rowp
 #pragma unroll
       for (int u = 0; u < EBN; ++u) {
         if (e0 + u < e1) {
+          const uint32_t eo = (uint32_t)((e0 + u) * H + head) * 4u;
           float al = expf(leaky(a[u] + ad, slope) - m) / sum;
-          if (P.leader && alpha) alpha[(int64_t)(e0 + u) * H + head] = al;
-          if (mask) al *= mask[(int64_t)(e0 + u) * H + head];
+          if (P.leader && alpha) bst1(bAl, eo, al);
+          if (mask) al *= bld1(bM, eo);
 #pragma unroll
           for (int s = 0; s < NS; ++s) acc[s] += al * xv[u][s];
         }
@@ -197,7 +238,7 @@ __global__ __launch_bounds__(NT) void k_gat_fwd(const int32_t* __restrict__ rowp
 #pragma unroll
       for (int u = 0; u < EB; ++u) {
         const int ee = e + u < e1 ? e + u : e0;
-        v[u] = a_s[(int64_t)col[ee] * H + head];
+        v[u] = bld1(bA, (uint32_t)(bldi(bC, (uint32_t)ee * 4u) * H + head) * 4u);
       }
 #pragma unroll
       for (int u = 0; u < EB; ++u)
@@ -210,7 +251,7 @@ __global__ __launch_bounds__(NT) void k_gat_fwd(const int32_t* __restrict__ rowp
 #pragma unroll
       for (int u = 0; u < EB; ++u) {
         const int ee = e + u < e1 ? e + u : e0;
-        v[u] = a_s[(int64_t)col[ee] * H + head];
+        v[u] = bld1(bA, (uint32_t)(bldi(bC, (uint32_t)ee * 4u) * H + head) * 4u);
       }
 #pragma unroll
       for (int u = 0; u < EB; ++u)
@@ -227,20 +268,21 @@ __global__ __launch_bounds__(NT) void k_gat_fwd(const int32_t* __restrict__ rowp
 #pragma unroll
       for (int u = 0; u < EBN; ++u) {
         const int ee = e + u < e1 ? e + u : e0;
-        c[u] = col[ee];
-        a[u] = a_s[(int64_t)c[u] * H + head];
+        c[u] = bldi(bC, (uint32_t)ee * 4u);
+        a[u] = bld1(bA, (uint32_t)(c[u] * H + head) * 4u);
       }
       f32x4 xv[EBN][NS];
 #pragma unroll
       for (int u = 0; u < EBN; ++u)
 #pragma unroll
-        for (int s = 0; s < NS; ++s) xv[u][s] = ld4(XP + (int64_t)c[u] * HC + P.fc[s]);
+        for (int s = 0; s < NS; ++s) xv[u][s] = bld4(bX, ((uint32_t)c[u] * HC + P.fc[s]) * 4u);
 #pragma unroll
       for (int u = 0; u < EBN; ++u) {
         if (e + u < e1) {
+          const uint32_t eo = (uint32_t)((e + u) * H + head) * 4u;
           float al = expf(leaky(a[u] + ad, slope) - m) / sum;
-          if (P.leader && alpha) alpha[(int64_t)(e + u) * H + head] = al;
-          if (mask) al *= mask[(int64_t)(e + u) * H + head];
+          if (P.leader && alpha) bst1(bAl, eo, al);
+          if (mask) al *= bld1(bM, eo);
 #pragma unroll
           for (int s = 0; s < NS; ++s) acc[s] += al * xv[u][s];
         }
@@ -258,7 +300,7 @@ __global__ __launch_bounds__(NT) void k_gat_fwd(const int32_t* __restrict__ rowp
 //   da_e[ij] = da_ij (per edge),  da_d[i] = sum_j da_ij
 // ------------------------------------------------------------------------------------------
 template <int ACT, int NS>
-__global__ __launch_bounds__(NT) void k_gat_bwd_edge(
+__global__ __launch_bounds__(NT) GAT_OCC void k_gat_bwd_edge(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const float* __restrict__ XP, const float* __restrict__ a_s, const float* __restrict__ a_d,
     const float* __restrict__ alpha, const float* __restrict__ mask, const float* __restrict__ dY,
@@ -268,6 +310,10 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_edge(
   const Lane L = lane_row();
   if (L.row >= M) return;
   const int HC = H * C;
+  const int64_t cap = rowptr[M];  // CSR entries: the extent of col and the per-edge arrays
+  const Buf bX = mkbuf(XP, M * HC * 4), bA = mkbuf(a_s, M * H * 4), bC = mkbuf(col, cap * 4);
+  const Buf bAl = mkbuf(alpha, cap * H * 4), bM = mkbuf(mask, mask ? cap * H * 4 : 0);
+  const Buf bDa = mkbuf(da_e, cap * H * 4);
   const int e0 = rowptr[L.row], e1 = rowptr[L.row + 1];
   for (int p = 0; p < num_passes(HC, NS); ++p) {
     const Pass<NS> P(p, L.li, HC, C);
@@ -290,22 +336,22 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_edge(
       // (the same operations in the same order as the two sweeps below)
       int c[EBN];
 #pragma unroll
-      for (int u = 0; u < EBN; ++u) c[u] = col[e0 + u < e1 ? e0 + u : e0];
+      for (int u = 0; u < EBN; ++u) c[u] = bldi(bC, (uint32_t)(e0 + u < e1 ? e0 + u : e0) * 4u);
       f32x4 xv[EBN][NS];
 #pragma unroll
       for (int u = 0; u < EBN; ++u)
 #pragma unroll
-        for (int s = 0; s < NS; ++s) xv[u][s] = ld4(XP + (int64_t)c[u] * HC + P.fc[s]);
+        for (int s = 0; s < NS; ++s) xv[u][s] = bld4(bX, ((uint32_t)c[u] * HC + P.fc[s]) * 4u);
       float d[EBN], al[EBN];
 #pragma unroll
       for (int u = 0; u < EBN; ++u) {
-        const int ee = e0 + u < e1 ? e0 + u : e0;
+        const uint32_t eo = (uint32_t)((e0 + u < e1 ? e0 + u : e0) * H + head) * 4u;
         float part = 0.f;
 #pragma unroll
         for (int s = 0; s < NS; ++s) part += dot4(dz[s], xv[u][s]);
         d[u] = group_sum(part, P.G);
-        if (mask) d[u] *= mask[(int64_t)ee * H + head];
-        al[u] = alpha[(int64_t)ee * H + head];
+        if (mask) d[u] *= bld1(bM, eo);
+        al[u] = bld1(bAl, eo);
       }
 #pragma unroll
       for (int u = 0; u < EBN; ++u)
@@ -313,10 +359,10 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_edge(
 #pragma unroll
       for (int u = 0; u < EBN; ++u) {
         if (e0 + u < e1) {
-          const float pre = a_s[(int64_t)c[u] * H + head] + ad;
+          const float pre = bld1(bA, (uint32_t)(c[u] * H + head) * 4u) + ad;
           const float da = al[u] * (d[u] - s_i) * (pre > 0.f ? 1.f : slope);
           dad += da;
-          if (P.leader) da_e[(int64_t)(e0 + u) * H + head] = da;
+          if (P.leader) bst1(bDa, (uint32_t)((e0 + u) * H + head) * 4u, da);
         }
       }
       if (P.leader) da_d[L.row * H + head] = dad;
@@ -328,29 +374,30 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_edge(
       for (int e = e0; e < e1; e += EBN) {
         int c[EBN];
 #pragma unroll
-        for (int u = 0; u < EBN; ++u) c[u] = col[e + u < e1 ? e + u : e0];
+        for (int u = 0; u < EBN; ++u) c[u] = bldi(bC, (uint32_t)(e + u < e1 ? e + u : e0) * 4u);
         f32x4 xv[EBN][NS];
 #pragma unroll
         for (int u = 0; u < EBN; ++u)
 #pragma unroll
-          for (int s = 0; s < NS; ++s) xv[u][s] = ld4(XP + (int64_t)c[u] * HC + P.fc[s]);
+          for (int s = 0; s < NS; ++s) xv[u][s] = bld4(bX, ((uint32_t)c[u] * HC + P.fc[s]) * 4u);
 #pragma unroll
         for (int u = 0; u < EBN; ++u) {
           const int ee = e + u < e1 ? e + u : e0;
+          const uint32_t eo = (uint32_t)(ee * H + head) * 4u;
           float part = 0.f;
 #pragma unroll
           for (int s = 0; s < NS; ++s) part += dot4(dz[s], xv[u][s]);
           float d = group_sum(part, P.G);
-          if (mask) d *= mask[(int64_t)ee * H + head];
-          const float al = alpha[(int64_t)ee * H + head];
+          if (mask) d *= bld1(bM, eo);
+          const float al = bld1(bAl, eo);
           if (sweep == 0) {
             if (e + u < e1) s_i += al * d;
           } else {
-            const float pre = a_s[(int64_t)c[u] * H + head] + ad;
+            const float pre = bld1(bA, (uint32_t)(c[u] * H + head) * 4u) + ad;
             const float da = al * (d - s_i) * (pre > 0.f ? 1.f : slope);
             if (e + u < e1) {
               dad += da;
-              if (P.leader) da_e[(int64_t)ee * H + head] = da;
+              if (P.leader) bst1(bDa, eo, da);
             }
           }
         }
@@ -368,25 +415,30 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_edge(
 // Persistent over rows (block b owns rows b*8 + hw + 8*P*t), fixed-order in-block combine.
 // Features are walked in strips of 128 (strip st = features [128 st, 128 st + 128)).
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void k_gat_bwd_node(
+template <int NST>  // 128-feature strips: ceil(H*C / 128)
+__global__ __launch_bounds__(NT) GAT_OCC void k_gat_bwd_node(
     const int32_t* __restrict__ tptr, const int32_t* __restrict__ tidx,
     const int32_t* __restrict__ tmap, const float* __restrict__ alpha,
     const float* __restrict__ mask, const float* __restrict__ da_e,
     const float* __restrict__ da_d, const float* __restrict__ dZ, const float* __restrict__ XP,
     const float* __restrict__ att_src, const float* __restrict__ att_dst, int64_t M, int H,
     int C, float* __restrict__ dXP, float* __restrict__ part, uint16_t* __restrict__ dXPb) {
-  __shared__ __attribute__((aligned(16))) float red[RB][3 * MAXS * 128];
+  __shared__ __attribute__((aligned(16))) float red[RB][3 * NST * 128];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int li = lane & 31, hw = wave * 2 + (lane >> 5);
   const int HC = H * C;
-  f32x4 ps[MAXS], pd[MAXS], pb[MAXS];
+  f32x4 ps[NST], pd[NST], pb[NST];
 #pragma unroll
-  for (int q = 0; q < MAXS; ++q) ps[q] = pd[q] = pb[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int q = 0; q < NST; ++q) ps[q] = pd[q] = pb[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t cap = M > 0 ? tptr[M] : 0;  // transpose-CSR entries
+  const Buf bT = mkbuf(tidx, cap * 4), bP = mkbuf(tmap, cap * 4), bZ = mkbuf(dZ, M * HC * 4);
+  const Buf bAl = mkbuf(alpha, cap * H * 4), bM = mkbuf(mask, mask ? cap * H * 4 : 0);
+  const Buf bDa = mkbuf(da_e, cap * H * 4);
   // (plain block order: the XCD-contiguous mapping of lane_row measured 3 us slower here)
   for (int64_t row = (int64_t)blockIdx.x * RB + hw; row < M; row += (int64_t)gridDim.x * RB) {
     const int q0 = tptr[row], q1 = tptr[row + 1];
 #pragma unroll
-    for (int st = 0; st < MAXS; ++st) {
+    for (int st = 0; st < NST; ++st) {
       const int s0 = st * 128;
       if (s0 >= HC) break;
       const int f = s0 + 4 * li;
@@ -399,18 +451,19 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_node(
         int ti[EB], pp[EB];
 #pragma unroll
         for (int u = 0; u < EB; ++u) {
-          const int qq = q + u < q1 ? q + u : q0;
-          ti[u] = tidx[qq];
-          pp[u] = tmap[qq];
+          const uint32_t qo = (uint32_t)(q + u < q1 ? q + u : q0) * 4u;
+          ti[u] = bldi(bT, qo);
+          pp[u] = bldi(bP, qo);
         }
         f32x4 dv[EB];
         float al[EB], da[EB];
 #pragma unroll
         for (int u = 0; u < EB; ++u) {
-          dv[u] = ld4(dZ + (int64_t)ti[u] * HC + fc);
-          al[u] = alpha[(int64_t)pp[u] * H + head];
-          if (mask) al[u] *= mask[(int64_t)pp[u] * H + head];
-          da[u] = da_e[(int64_t)pp[u] * H + head];
+          const uint32_t eo = (uint32_t)(pp[u] * H + head) * 4u;
+          dv[u] = bld4(bZ, ((uint32_t)ti[u] * HC + fc) * 4u);
+          al[u] = bld1(bAl, eo);
+          if (mask) al[u] *= bld1(bM, eo);
+          da[u] = bld1(bDa, eo);
         }
 #pragma unroll
         for (int u = 0; u < EB; ++u) {
@@ -433,15 +486,15 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_node(
     }
   }
 #pragma unroll
-  for (int st = 0; st < MAXS; ++st) {
-    st4(&red[hw][(0 * MAXS + st) * 128 + 4 * li], ps[st]);
-    st4(&red[hw][(1 * MAXS + st) * 128 + 4 * li], pd[st]);
-    st4(&red[hw][(2 * MAXS + st) * 128 + 4 * li], pb[st]);
+  for (int st = 0; st < NST; ++st) {
+    st4(&red[hw][(0 * NST + st) * 128 + 4 * li], ps[st]);
+    st4(&red[hw][(1 * NST + st) * 128 + 4 * li], pd[st]);
+    st4(&red[hw][(2 * NST + st) * 128 + 4 * li], pb[st]);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < 3 * HC; i += NT) {
     const int kind = i / HC, f = i % HC;
-    const int idx = (kind * MAXS + f / 128) * 128 + f % 128;
+    const int idx = (kind * NST + f / 128) * 128 + f % 128;
     float t = red[0][idx];
 #pragma unroll
     for (int r = 1; r < RB; ++r) t += red[r][idx];
@@ -457,6 +510,9 @@ inline bool shape_ok(int H, int C) {
 inline int ns_of(int C) { return C <= 128 ? 1 : C / 128; }
 
 inline unsigned row_grid(int64_t M) { return (unsigned)((M + RB - 1) / RB); }
+
+// node arrays addressed by 32-bit byte offsets (the per-edge arrays: documented in lgnn.h)
+inline bool bytes_ok(int64_t M, int H, int C) { return M * H * C * 4 < ((int64_t)1 << 32); }
 
 }  // namespace
 
@@ -485,6 +541,7 @@ extern "C" int lgnn_gat_fwd(const int32_t* rowptr, const int32_t* col, const flo
   if (M < 0 || !shape_ok(H, C) || (act != LGNN_ACT_NONE && act != LGNN_ACT_ELU))
     return LGNN_EINVAL;
   if (M > 0 && (!rowptr || !col || !XP || !a_s || !a_d || !Y)) return LGNN_EINVAL;
+  if (!bytes_ok(M, H, C)) return LGNN_EINVAL;
   if (M == 0) return LGNN_OK;
 #define LGNN_GF(A_, NS_)                                                                     \
   hipLaunchKernelGGL((k_gat_fwd<A_, NS_>), dim3(row_grid(M)), dim3(NT), 0, as_stream(stream),    \
@@ -517,6 +574,7 @@ extern "C" int lgnn_gat_bwd_edge(const int32_t* rowptr, const int32_t* col, cons
   if (M > 0 && (!rowptr || !col || !XP || !a_s || !a_d || !alpha || !dY || !dZ || !da_e || !da_d))
     return LGNN_EINVAL;
   if (act == LGNN_ACT_ELU && M > 0 && !Y) return LGNN_EINVAL;
+  if (!bytes_ok(M, H, C)) return LGNN_EINVAL;
   if (M == 0) return LGNN_OK;
 #define LGNN_GB(A_, NS_)                                                                   \
   hipLaunchKernelGGL((k_gat_bwd_edge<A_, NS_>), dim3(row_grid(M)), dim3(NT), 0,               \
@@ -541,8 +599,9 @@ extern "C" int lgnn_gat_bwd_edge(const int32_t* rowptr, const int32_t* col, cons
 
 extern "C" int lgnn_gat_bwd_num_partials(int64_t M) {
   if (M < 0) return LGNN_EINVAL;
+  // persistent rows; enough workgroups to keep LGNN_GAT_WPE waves per SIMD resident
   const int64_t b = (M + RB - 1) / RB;
-  return (int)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
+  return (int)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
 }
 
 extern "C" int lgnn_gat_bwd_node(const int32_t* tptr, const int32_t* tidx, const int32_t* tmap,
@@ -555,9 +614,17 @@ extern "C" int lgnn_gat_bwd_node(const int32_t* tptr, const int32_t* tidx, const
   if (num_partials != lgnn_gat_bwd_num_partials(M)) return LGNN_EINVAL;
   if (M > 0 && (!tptr || !tidx || !tmap || !alpha || !da_e || !da_d || !dZ || !XP || !dXP))
     return LGNN_EINVAL;
-  hipLaunchKernelGGL(k_gat_bwd_node, dim3(num_partials), dim3(NT), 0, as_stream(stream), tptr,
-                     tidx, tmap, alpha, edge_mask, da_e, da_d, dZ, XP, att_src, att_dst, M, H, C,
-                     dXP, partials, dXP_bf16);
+  if (!bytes_ok(M, H, C)) return LGNN_EINVAL;
+#define LGNN_GN(NST_)                                                                        \
+  hipLaunchKernelGGL(k_gat_bwd_node<NST_>, dim3(num_partials), dim3(NT), 0, as_stream(stream),  \
+                     tptr, tidx, tmap, alpha, edge_mask, da_e, da_d, dZ, XP, att_src, att_dst, M, \
+                     H, C, dXP, partials, dXP_bf16)
+  switch ((H * C + 127) / 128) {
+    case 1: LGNN_GN(1); break;
+    case 2: LGNN_GN(2); break;
+    default: LGNN_GN(4); break;
+  }
+#undef LGNN_GN
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
 }
