@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 19
+#define LGNN_ABI_VERSION 20
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -595,6 +595,11 @@ int lgnn_cc_pool(const float* features, int channels, int64_t num_pixels, const 
 int lgnn_bf16_kpad(int K);
 int lgnn_bf16_weight_prep(const float* W, int N, int K, uint16_t* Wb, uint16_t* WTb,
                           void* stream);
+/* lgnn_bf16_weight_prep for n <= 8 weights in one launch (ABI v20): W[j] [N[j]][K[j]] fp32 ->
+ * Wb[j] (and WTb[j], nullable, when K[j] <= 128), the same operands as n separate calls. The
+ * bf16 GAT forward prepares in_proj's and every GATConv.lin's operands this way once per step. */
+int lgnn_bf16_weight_prep_multi(int n, const float* const* W, const int* N, const int* K,
+                                uint16_t* const* Wb, uint16_t* const* WTb, void* stream);
 int lgnn_bf16_gemm(const void* A, int a_is_f32, int64_t M, int K, const uint16_t* Wb,
                    const float* bias, int N, float* Y, uint16_t* Yb, float* colsum_part,
                    void* stream);

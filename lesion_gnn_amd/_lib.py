@@ -69,6 +69,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_gat_att": (I32, [P, I64, I32, I32, P, P, P, P, P]),
     "lgnn_bf16_kpad": (I32, [I32]),
     "lgnn_bf16_weight_prep": (I32, [P, I32, I32, P, P, P]),
+    "lgnn_bf16_weight_prep_multi": (I32, [I32, P, P, P, P, P, P]),
     "lgnn_bf16_gemm": (I32, [P, I32, I64, I32, P, P, I32, P, P, P, P]),
     "lgnn_bf16_wgrad_partials": (I32, [I64, I32]),
     "lgnn_bf16_wgrad": (I32, [P, I32, P, I32, I64, I32, P, I32, P]),
@@ -119,7 +120,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 _lib = None
 

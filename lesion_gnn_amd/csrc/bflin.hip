@@ -415,6 +415,39 @@ __global__ void k_bf_wprep(const float* __restrict__ W, int N, int K, int Kp, in
   }
 }
 
+// several weights' operands in one launch: job j owns blocks [first[j], first[j + 1])
+constexpr int kMaxPrep = 8;
+struct PrepJobs {
+  const float* W[kMaxPrep];
+  uint16_t* Wb[kMaxPrep];
+  uint16_t* WTb[kMaxPrep];
+  int N[kMaxPrep], K[kMaxPrep], Kp[kMaxPrep], Np[kMaxPrep];
+  int first[kMaxPrep + 1];
+  int n;
+};
+
+__global__ void k_bf_wprep_multi(PrepJobs jobs) {
+  int j = 0;
+  while (j + 1 < jobs.n && (int)blockIdx.x >= jobs.first[j + 1]) ++j;
+  const int nb = jobs.first[j + 1] - jobs.first[j];
+  const int N = jobs.N[j], K = jobs.K[j], Kp = jobs.Kp[j], Np = jobs.Np[j];
+  const float* __restrict__ W = jobs.W[j];
+  uint16_t* __restrict__ Wb = jobs.Wb[j];
+  uint16_t* __restrict__ WTb = jobs.WTb[j];
+  const int64_t n1 = (int64_t)128 * Kp, n2 = WTb ? (int64_t)128 * Np : 0;
+  for (int64_t i = (int64_t)(blockIdx.x - jobs.first[j]) * blockDim.x + threadIdx.x; i < n1 + n2;
+       i += (int64_t)nb * blockDim.x) {
+    const bool t = i >= n1;  // the same element map as k_bf_wprep
+    const int64_t q0 = t ? i - n1 : i;
+    const int e = (int)(q0 & 7), lane = (int)((q0 >> 3) & 63), wave = (int)((q0 >> 9) & 3);
+    const int64_t cs = q0 >> 11;
+    const int r = 32 * wave + (lane & 31), q = (int)(cs * 16) + 8 * (lane >> 5) + e;
+    const int n = t ? q : r, k = t ? r : q;
+    const float v = (n < N && k < K) ? W[(int64_t)n * K + k] : 0.f;
+    (t ? WTb : Wb)[q0] = (uint16_t)(pk2(v, 0.f) & 0xffffu);
+  }
+}
+
 }  // namespace lgnn_bf
 
 using namespace lgnn_bf;
@@ -433,6 +466,31 @@ extern "C" int lgnn_bf16_weight_prep(const float* W, int N, int K, uint16_t* Wb,
   const int grid = (int)std::min<int64_t>((total + 255) / 256, 1024);
   hipLaunchKernelGGL(k_bf_wprep, dim3(grid), dim3(256), 0, as_stream(stream), W, N, K, Kp, Np, Wb,
                      WTb);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? LGNN_OK : (int)e;
+}
+
+extern "C" int lgnn_bf16_weight_prep_multi(int n, const float* const* W, const int* N,
+                                           const int* K, uint16_t* const* Wb,
+                                           uint16_t* const* WTb, void* stream) {
+  if (n < 1 || n > kMaxPrep || !W || !N || !K || !Wb || !WTb) return LGNN_EINVAL;
+  PrepJobs jobs{};
+  jobs.n = n;
+  jobs.first[0] = 0;
+  for (int j = 0; j < n; ++j) {
+    if (!W[j] || !Wb[j] || N[j] < 1 || N[j] > 128 || K[j] < 1) return LGNN_EINVAL;
+    if (WTb[j] && K[j] > 128) return LGNN_EINVAL;
+    jobs.W[j] = W[j];
+    jobs.Wb[j] = Wb[j];
+    jobs.WTb[j] = WTb[j];
+    jobs.N[j] = N[j];
+    jobs.K[j] = K[j];
+    jobs.Kp[j] = lgnn_bf16_kpad(K[j]);
+    jobs.Np[j] = lgnn_bf16_kpad(N[j]);
+    const int64_t total = (int64_t)128 * jobs.Kp[j] + (WTb[j] ? (int64_t)128 * jobs.Np[j] : 0);
+    jobs.first[j + 1] = jobs.first[j] + (int)std::min<int64_t>((total + 255) / 256, 512);
+  }
+  hipLaunchKernelGGL(k_bf_wprep_multi, dim3(jobs.first[n]), dim3(256), 0, as_stream(stream), jobs);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? LGNN_OK : (int)e;
 }

@@ -120,6 +120,15 @@ __global__ __launch_bounds__(RT) void k_reduce_multi(ReduceJobs jobs) {
     for (; p < P; p += 16) s = fmaf(part[(int64_t)p * rows + c], f[(int64_t)p * width + d], s);
     P = 0;  // fall through to the fixed-order wave fold
   }
+  // slot order p = wave, wave + 16, ... in every lane; 16 loads in flight (many-slot jobs such
+  // as the GAT attention partials, 2048 slots of 384 columns, are latency bound)
+  for (; p + 16 * 15 < P; p += 16 * 16) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = part[(int64_t)(p + 16 * u) * len + ic];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) s += v[u];
+  }
   for (; p + 48 < P; p += 64) {
     const float v0 = part[(int64_t)p * len + ic], v1 = part[(int64_t)(p + 16) * len + ic];
     const float v2 = part[(int64_t)(p + 32) * len + ic], v3 = part[(int64_t)(p + 48) * len + ic];

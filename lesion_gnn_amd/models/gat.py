@@ -48,6 +48,9 @@ class GAT(nn.Module):
     def forward(self, x: torch.Tensor, edge_index, batch: torch.Tensor,
                 num_graphs: int | None = None) -> torch.Tensor:
         g = as_graph(edge_index, x.size(0), batch, num_graphs)
+        if self.bf16 and not torch.compiler.is_compiling():
+            # every bf16 GEMM's weight operands for this step in one launch
+            ops.bf16_prepare_weights([self.in_proj.weight] + [c.lin.weight for c in self.convs])
         h = ops.linear_auto(x, self.in_proj.weight, self.in_proj.bias, self.bf16)
         for conv in self.convs:
             h = conv(h, g, act=_lib.LGNN_ACT_ELU, bf16=self.bf16)

@@ -504,10 +504,47 @@ def bf16_mfma_fits(N: int) -> bool:
     return BF16_MFMA and 1 <= N <= 128 and N % 2 == 0
 
 
+# operands prepared ahead for this forward (bf16_prepare_weights), each taken once
+_PREPARED: dict = {}
+
+
+def bf16_prepare_weights(weights: list) -> None:
+    """The bf16 operands (Wb and, when K <= 128, WTb) of several weights in one launch
+    (lgnn_bf16_weight_prep_multi). Each is handed out ONCE by bf16_weight_operands for the same
+    tensor at the same version, so a later step (the optimizer updates weights in place, without
+    a version bump) always prepares afresh."""
+    ws = [_f32c(W) for W in weights if bf16_mfma_fits(W.size(0))][:8]
+    if not ws:
+        return
+    lib = _lib.load()
+    ops_ = []
+    for W in ws:
+        N, K = W.shape
+        Wb = torch.empty(128 * lib.lgnn_bf16_kpad(K), dtype=torch.bfloat16, device=W.device)
+        WTb = torch.empty(128 * lib.lgnn_bf16_kpad(N), dtype=torch.bfloat16, device=W.device) \
+            if K <= 128 else None
+        ops_.append((W, Wb, WTb))
+    n = len(ops_)
+    P_ = ctypes.c_void_p * n
+    I_ = ctypes.c_int * n
+    _lib.call("lgnn_bf16_weight_prep_multi", n, P_(*[o[0].data_ptr() for o in ops_]),
+              I_(*[o[0].size(0) for o in ops_]), I_(*[o[0].size(1) for o in ops_]),
+              P_(*[o[1].data_ptr() for o in ops_]),
+              P_(*[o[2].data_ptr() if o[2] is not None else None for o in ops_]),
+              _s(ws[0].device))
+    for W, Wb, WTb in ops_:
+        _PREPARED[id(W)] = (weakref.ref(W), W._version, Wb, WTb)
+
+
 def bf16_weight_operands(W: torch.Tensor, want_t: bool):
     """(Wb, WTb): bf16 W [128][kpad(K)] and, when want_t and K <= 128, bf16 W^T [128][kpad(N)]
-    (zero-padded operands of lgnn_bf16_gemm), in one launch."""
+    (zero-padded operands of lgnn_bf16_gemm), in one launch — or the pair bf16_prepare_weights
+    made for W in this forward."""
     W = _f32c(W)
+    rec = _PREPARED.pop(id(W), None)
+    if rec is not None and rec[0]() is W and rec[1] == W._version \
+            and (rec[3] is not None or not want_t or W.size(1) > 128):
+        return rec[2], rec[3]
     N, K = W.shape
     lib = _lib.load()
     Wb = torch.empty(128 * lib.lgnn_bf16_kpad(K), dtype=torch.bfloat16, device=W.device)
@@ -541,9 +578,10 @@ def bf16_gemm(A: torch.Tensor, Wb: torch.Tensor, bias, N: int, want_yb: bool = F
 _COLSUMS: dict = {}
 
 
-def colsum_of(y: torch.Tensor):
+def colsum_of(y: torch.Tensor, reducer: list = None):
     """y.sum(0) from the per-tile column sums its producing GEMM wrote (fixed order), if y is
-    that output unchanged; else None."""
+    that output unchanged; else None. With `reducer` the slab reduction is appended to that job
+    list (the caller launches the batch, reduce_multi) instead of launched here."""
     rec = _COLSUMS.get(id(y))
     if rec is None:
         return None
@@ -552,13 +590,17 @@ def colsum_of(y: torch.Tensor):
         return None
     N = y.size(1)
     out = torch.empty(N, dtype=torch.float32, device=y.device)
-    _lib.call("lgnn_reduce_partials", _lib.ptr(cs), cs.numel() // N, N, _lib.ptr(out),
-              _s(y.device))
+    if reducer is not None:
+        reducer.append((cs, cs.numel() // N, N, out))
+    else:
+        _lib.call("lgnn_reduce_partials", _lib.ptr(cs), cs.numel() // N, N, _lib.ptr(out),
+                  _s(y.device))
     return out
 
 
-def bf16_wgrad(dYb: torch.Tensor, X: torch.Tensor, N: int) -> torch.Tensor:
-    """dW = bf16(dY)^T bf16(X): partial slabs over row splits, summed in fixed order."""
+def bf16_wgrad(dYb: torch.Tensor, X: torch.Tensor, N: int, reducer: list = None) -> torch.Tensor:
+    """dW = bf16(dY)^T bf16(X): partial slabs over row splits, summed in fixed order (with
+    `reducer`: the sum is appended to the caller's job list, launched with its other slabs)."""
     X = X.contiguous()
     M, K = X.shape
     if X.dtype != torch.float32 and K % 2:  # bf16 X needs even rows; bf16 -> fp32 is exact
@@ -569,7 +611,10 @@ def bf16_wgrad(dYb: torch.Tensor, X: torch.Tensor, N: int) -> torch.Tensor:
     _lib.call("lgnn_bf16_wgrad", _lib.ptr(dYb), N, _lib.ptr(X), int(X.dtype == torch.float32), M,
               K, _lib.ptr(part), S, _s(dev))
     dW = torch.empty(N, K, dtype=torch.float32, device=dev)
-    _lib.call("lgnn_reduce_partials", _lib.ptr(part), S, N * K, _lib.ptr(dW), _s(dev))
+    if reducer is not None:
+        reducer.append((part, S, N * K, dW))
+    else:
+        _lib.call("lgnn_reduce_partials", _lib.ptr(part), S, N * K, _lib.ptr(dW), _s(dev))
     return dW
 
 
@@ -613,15 +658,18 @@ class _DenseLinear(torch.autograd.Function):
     def backward(ctx, dy):
         x, W = ctx.saved_tensors
         dy = _f32c(dy)
+        N, K = W.shape
+        mfma = ctx.bf16 and bf16_mfma_fits(N)
+        jobs = [] if mfma else None  # db's and dW's slab sums in one launch
         db = None
         if ctx.has_b:  # from the column sums dy's producing GEMM wrote, when it was ours
-            db = colsum_of(dy)
+            db = colsum_of(dy, jobs)
             if db is None:
                 db = dy.sum(0)
-        N, K = W.shape
-        if ctx.bf16 and bf16_mfma_fits(N):
+        if mfma:
             dyb = _bf16_operand(dy)
-            dW = bf16_wgrad(dyb, x, N)
+            dW = bf16_wgrad(dyb, x, N, jobs)
+            reduce_multi(jobs, dW.device)
             dx = None
             if ctx.needs_input_grad[0]:
                 if K <= 128:
@@ -1341,11 +1389,13 @@ class _GATConv(torch.autograd.Function):
                   _lib.ptr(att_dst), M, H, C, _lib.ptr(dXP), _lib.ptr(part), P, _lib.ptr(dXPb),
                   _s(dev))
         red = torch.empty(3 * HC, dtype=torch.float32, device=dev)
-        _lib.call("lgnn_reduce_partials", _lib.ptr(part), P, 3 * HC, _lib.ptr(red), _s(dev))
         want_dx = ctx.needs_input_grad[0]
         if ctx.bf16 and bf16_mfma_fits(HC):
             dg = dXPb if dXPb is not None else dXP.to(torch.bfloat16)
-            dW = bf16_wgrad(dg, x, HC)
+            # the attention partials and lin's dW slabs summed in one launch
+            jobs = [(part, P, 3 * HC, red)]
+            dW = bf16_wgrad(dg, x, HC, jobs)
+            reduce_multi(jobs, dev)
             dx = None
             if want_dx:
                 K = W.size(1)
@@ -1359,16 +1409,17 @@ class _GATConv(torch.autograd.Function):
                         _remember_bf16(dx, dxb)
                 else:
                     dx = mm_dense(dg, W.to(torch.bfloat16), True)
-        elif ctx.dense:
-            if ctx.bf16:  # rounded once for both products
-                dg = dXPb if dXPb is not None else dXP.to(torch.bfloat16)
-            else:
-                dg = dXP
-            dW = dw_dense(dg, x, ctx.bf16)
-            dx = mm_dense(dg, W, ctx.bf16) if want_dx else None
         else:
-            dx, dW, _ = linear_bwd(_lib.LGNN_GRAD_DIRECT, dXP, H=None, act=_lib.LGNN_ACT_NONE,
-                                   X=x, W=W, want_dx=want_dx, want_db=False)
+            _lib.call("lgnn_reduce_partials", _lib.ptr(part), P, 3 * HC, _lib.ptr(red), _s(dev))
+            if ctx.dense:
+                # rounded once for both products
+                dg = (dXPb if dXPb is not None else dXP.to(torch.bfloat16)) if ctx.bf16 else dXP
+                dW = dw_dense(dg, x, ctx.bf16)
+                dx = mm_dense(dg, W, ctx.bf16) if want_dx else None
+            else:
+                dx, dW, _ = linear_bwd(_lib.LGNN_GRAD_DIRECT, dXP, H=None,
+                                       act=_lib.LGNN_ACT_NONE, X=x, W=W, want_dx=want_dx,
+                                       want_db=False)
         datt_s = red[:HC].view(ctx.att_shape)
         datt_d = red[HC:2 * HC].view(ctx.att_shape)
         dbias = red[2 * HC:] if ctx.has_bias else None

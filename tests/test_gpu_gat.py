@@ -196,3 +196,26 @@ def test_gat_bf16_copies_match_torch_cast(cuda, monkeypatch):
     assert torch.equal(res[0][0], res[1][0])
     for k in res[1][1]:
         assert torch.equal(res[0][1][k], res[1][1][k]), k
+
+
+def test_gat_bf16_batched_weight_prep_bitwise(cuda, monkeypatch):
+    """bf16 GAT: the weight operands prepared for the whole step in one launch
+    (lgnn_bf16_weight_prep_multi) and the attention / lin slab sums batched per layer give a
+    step bit-identical to per-layer preparation; and no prepared operand survives the step."""
+    from lesion_gnn_amd import ops
+
+    b = synth.make_batch(64, k=6, d_in=1025, seed=23, sizes="lognormal", last_channel_class=True)
+    torch.manual_seed(7)
+    m = GAT(1025, [128] * 4, 1, heads=4, dropout=0.0, precision="bf16").to(cuda).train()
+    real = ops.bf16_prepare_weights
+    res = []
+    for batched in (True, False):
+        monkeypatch.setattr(ops, "bf16_prepare_weights", real if batched else (lambda ws: None))
+        out = m(b.x.to(cuda), b.edge_index.to(cuda), b.batch.to(cuda), b.num_graphs)
+        assert not ops._PREPARED
+        m.zero_grad(set_to_none=True)
+        out.square().sum().backward()
+        res.append((out.detach().cpu(), {n: p.grad.detach().cpu() for n, p in m.named_parameters()}))
+    assert torch.equal(res[0][0], res[1][0])
+    for n in res[1][1]:
+        assert torch.equal(res[0][1][n], res[1][1][n]), n
