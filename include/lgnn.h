@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 20
+#define LGNN_ABI_VERSION 21
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -311,6 +311,20 @@ int lgnn_node_linear_bwd_bn_pool(int bn_mode, const float* dY, const float* H, i
                                  int training, const int64_t* batch, const int32_t* gptr,
                                  int pool_mean, const float* dlogits, const float* Wout,
                                  int num_classes, void* stream);
+/* lgnn_node_linear_bwd_bn (bn_mode LGNN_BN_GSTATS) with the output gradient gathered through the
+ * transpose CSR as it is loaded (ABI v21): row i's gradient is
+ *   tself * dS[i] + sum_{e in T(i)} tw_e dS[tidx_e]   (LGNN_GRAD_TRANSPOSE),
+ * dS [M,N] being the NEXT GINConv's pre-aggregation input gradient (its Lin1 dX). This is the
+ * backward of that conv's aggregation (PyG GINConv propagate + (1 + eps) x, reference gin.py:23)
+ * folded into this conv's Lin2 backward, so the aggregated gradient never goes to HBM. */
+int lgnn_node_linear_bwd_bn_gather(const float* dS, const int32_t* tptr, const int32_t* tidx,
+                                   const float* tw, float tself, const float* H, int act,
+                                   const float* X, int64_t M, int K, const float* W, int N,
+                                   float* dXpre, float* dW_partial, float* db_partial,
+                                   int num_partials, const float* bn_Z, const float* bn_mask,
+                                   const float* bn_scale, const float* bn_shift,
+                                   const float* bn_mean, const float* bn_invstd,
+                                   double* gstats_part, void* stream);
 /* Split-3 variants (bf16 MFMA at fp32 accuracy, liblgnn lin3.hip) of the two calls below: the
  * same arguments with `planes` / `planes_t` (lgnn_weight_planes of W: the weight and, for dX, the
  * transposed planes of this one layer) in place of W; either BN option (or none: stats_part and

@@ -101,6 +101,8 @@ SIGNATURES: dict[str, tuple] = {
                                       P, P]),
     "lgnn_node_linear_bwd_bn": (I32, [I32, P, P, I32, P, I64, I32, P, I32, P, P, P, I32, P, P, P,
                                       P, P, P, P, P, F64, I32, P]),
+    "lgnn_node_linear_bwd_bn_gather": (I32, [P, P, P, P, F32, P, I32, P, I64, I32, P, I32, P, P,
+                                              P, I32, P, P, P, P, P, P, P, P]),
     "lgnn_node_linear_bwd_bn_pool": (I32, [I32, P, P, I32, P, I64, I32, P, I32, P, P, P, I32, P,
                                            P, P, P, P, P, P, P, F64, I32, P, P, I32, P, P, I32,
                                            P]),
@@ -120,7 +122,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 _lib = None
 

@@ -126,6 +126,18 @@ class GINConv(nn.Module):
                             mlp.lins[1].bias, g, self.initial_eps, mask, act, self.sync_group,
                             self.sync_count)
 
+    def stack_spec(self, x: torch.Tensor, act: int) -> dict:
+        """This conv's weights, BatchNorm, eps and dropout mask for ops.gin_stack."""
+        mlp = self.nn
+        mask = None
+        if mlp.dropout > 0.0 and self.training:
+            p = mlp.dropout
+            mask = (torch.rand(x.size(0), mlp.channel_list[1], device=x.device) >= p).float()
+            mask.mul_(1.0 / (1.0 - p))
+        return dict(W1=mlp.lins[0].weight, b1=mlp.lins[0].bias, bn=mlp.norms[0].module,
+                    W2=mlp.lins[1].weight, b2=mlp.lins[1].bias, eps=self.initial_eps, mask=mask,
+                    act=act, group=self.sync_group, sync_count=self.sync_count)
+
     def head_fusable(self, x: torch.Tensor) -> bool:
         mlp = self.nn
         return ops.gin_conv_head_eligible(x, mlp.lins[0].weight, mlp.lins[1].weight)

@@ -794,16 +794,18 @@ extern "C" int lgnn_node_linear_bwd_bn(int bn_mode, const float* dY, const float
                                       nullptr, nullptr, 0, nullptr, nullptr, 0, stream);
 }
 
-extern "C" int lgnn_node_linear_bwd_bn_pool(
+static int node_linear_bwd_bn_impl(
     int bn_mode, const float* dY, const float* H, int act, const float* X, int64_t M, int K,
     const float* W, int N, float* dXpre, float* dW_partial, float* db_partial, int num_partials,
     const float* bn_Z, const float* bn_mask, const float* bn_scale, const float* bn_shift,
     const float* bn_mean, const float* bn_invstd, double* gstats_part, const double* bn_sums,
     double count, int training, const int64_t* batch, const int32_t* gptr, int pool_mean,
-    const float* dlogits, const float* Wout, int num_classes, void* stream) {
+    const float* dlogits, const float* Wout, int num_classes, const int32_t* tptr,
+    const int32_t* tidx, const float* tw, float tself, void* stream) {
   const bool pool = batch != nullptr;
   if (pool && (!gptr || bn_mode != BN_GSTATS || !dlogits || !Wout || num_classes < 1))
     return LGNN_EINVAL;
+  if (tptr && (pool || bn_mode != BN_GSTATS || !tidx || !tw)) return LGNN_EINVAL;
   if (M < 0 || !W || !dW_partial || !lgnn_tile_fits(M, K, N)) return LGNN_EINVAL;
   if (num_partials != lgnn_tile_partials(M)) return LGNN_EINVAL;
   if (M > 0 && ((!dY && !pool) || !X)) return LGNN_EINVAL;
@@ -844,9 +846,16 @@ extern "C" int lgnn_node_linear_bwd_bn_pool(
                      batch, gptr, pool_mean, nullptr, nullptr, nullptr, 0.f, H, X, M, K, W, N,    \
                      dXpre, dW_partial, db_partial, nullptr, 0, 0, bn, dlogits, Wout,           \
                      num_classes)
+#define LGNN_TBT(AC)                                                                            \
+  hipLaunchKernelGGL((k_bwd<LGNN_GRAD_TRANSPOSE, AC, true, BN_GSTATS>), grid, dim3(NT), 0, s, dY, \
+                     nullptr, nullptr, 0, tptr, tidx, tw, tself, H, X, M, K, W, N, dXpre,        \
+                     dW_partial, db_partial, nullptr, 0, 0, bn)
   if (pool) {  // the pooled-output gradient formed from dlogits and out_proj's W (no dH tensor)
     if (act == LGNN_ACT_ELU) LGNN_TBP(LGNN_ACT_ELU);
     else LGNN_TBP(LGNN_ACT_NONE);
+  } else if (tptr) {  // dY = tself dS + A^T dS gathered through the transpose CSR as loaded
+    if (act == LGNN_ACT_ELU) LGNN_TBT(LGNN_ACT_ELU);
+    else LGNN_TBT(LGNN_ACT_NONE);
   } else if (bn_mode == BN_GSTATS) {
     if (act == LGNN_ACT_ELU) LGNN_TBB(LGNN_ACT_ELU, true, BN_GSTATS);
     else LGNN_TBB(LGNN_ACT_NONE, true, BN_GSTATS);
@@ -856,8 +865,36 @@ extern "C" int lgnn_node_linear_bwd_bn_pool(
   }
 #undef LGNN_TBB
 #undef LGNN_TBP
+#undef LGNN_TBT
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? LGNN_OK : (int)e;
+}
+
+extern "C" int lgnn_node_linear_bwd_bn_pool(
+    int bn_mode, const float* dY, const float* H, int act, const float* X, int64_t M, int K,
+    const float* W, int N, float* dXpre, float* dW_partial, float* db_partial, int num_partials,
+    const float* bn_Z, const float* bn_mask, const float* bn_scale, const float* bn_shift,
+    const float* bn_mean, const float* bn_invstd, double* gstats_part, const double* bn_sums,
+    double count, int training, const int64_t* batch, const int32_t* gptr, int pool_mean,
+    const float* dlogits, const float* Wout, int num_classes, void* stream) {
+  return node_linear_bwd_bn_impl(bn_mode, dY, H, act, X, M, K, W, N, dXpre, dW_partial,
+                                 db_partial, num_partials, bn_Z, bn_mask, bn_scale, bn_shift,
+                                 bn_mean, bn_invstd, gstats_part, bn_sums, count, training, batch,
+                                 gptr, pool_mean, dlogits, Wout, num_classes, nullptr, nullptr,
+                                 nullptr, 0.f, stream);
+}
+
+extern "C" int lgnn_node_linear_bwd_bn_gather(
+    const float* dS, const int32_t* tptr, const int32_t* tidx, const float* tw, float tself,
+    const float* H, int act, const float* X, int64_t M, int K, const float* W, int N,
+    float* dXpre, float* dW_partial, float* db_partial, int num_partials, const float* bn_Z,
+    const float* bn_mask, const float* bn_scale, const float* bn_shift, const float* bn_mean,
+    const float* bn_invstd, double* gstats_part, void* stream) {
+  if (!tptr) return LGNN_EINVAL;
+  return node_linear_bwd_bn_impl(BN_GSTATS, dS, H, act, X, M, K, W, N, dXpre, dW_partial,
+                                 db_partial, num_partials, bn_Z, bn_mask, bn_scale, bn_shift,
+                                 bn_mean, bn_invstd, gstats_part, nullptr, 0.0, 0, nullptr,
+                                 nullptr, 0, nullptr, nullptr, 0, tptr, tidx, tw, tself, stream);
 }
 
 extern "C" int lgnn_tile_count(int64_t M) {

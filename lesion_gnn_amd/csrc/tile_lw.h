@@ -281,14 +281,18 @@ __device__ __forceinline__ void bwd_tiles(
     }
   }
 
-  // pipeline prologue (TRANSPOSE): the first tile's dY rows and transpose-CSR index block
+  // pipeline prologue (TRANSPOSE): the first tile's dY rows and transpose-CSR index block.
+  // With the BN_GSTATS epilogue the next tile's rows are NOT prefetched into registers (PREF):
+  // their 32 VGPRs live across the MFMAs pushed that variant past 256 and spilled ~96 (GIN
+  // Lin2 backward under the model-wide node); its rows are loaded at the tile's start instead.
+  constexpr bool PREF = !(GMODE == LGNN_GRAD_TRANSPOSE && BNM == BN_GSTATS);
   f32x4 dr[8];
   IdxRegs R;
   const int64_t tfirst = seek_tile(xcd_block(), ntiles, tmask, want);  // XCD-contiguous tiles
   if constexpr (GMODE == LGNN_GRAD_TRANSPOSE) {
     const int64_t t0 = tfirst;
     if (t0 < ntiles) {
-      if constexpr (!(ABL & 16)) load_rows(dr, bdY, N, (int)(t0 * TM));
+      if constexpr (!(ABL & 16) && PREF) load_rows(dr, bdY, N, (int)(t0 * TM));
       if constexpr (!(ABL & 2)) {
         idx_load_head(R, tptr, M, t0 * TM);
         idx_load_body(R, tidx, tw);
@@ -306,6 +310,8 @@ __device__ __forceinline__ void bwd_tiles(
       if constexpr (ABL & 16) {
 #pragma unroll
         for (int it = 0; it < 8; ++it) dr[it] = zero4();
+      } else if constexpr (!PREF) {
+        load_rows(dr, bdY, N, (int)r0);
       }
       store_rows_lds(A, dr, M, N, r0);
       if constexpr (!(ABL & 2)) idx_store(ti, staged, R, r0);
@@ -321,7 +327,7 @@ __device__ __forceinline__ void bwd_tiles(
       __syncthreads();
       // prefetch: next tile's dY rows and index head
       if (has_next) {
-        if constexpr (!(ABL & 16)) load_rows(dr, bdY, N, (int)(tn * TM));
+        if constexpr (!(ABL & 16) && PREF) load_rows(dr, bdY, N, (int)(tn * TM));
         if constexpr (!(ABL & 2)) idx_load_head(R, tptr, M, tn * TM);
       }
       auto agg_tile = [&](auto staged_tag) {

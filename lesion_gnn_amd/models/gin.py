@@ -9,6 +9,7 @@ plus the model's F.elu (gin.py:31) runs as one HIP autograd node (ops.gin_conv).
 from __future__ import annotations
 
 import dataclasses
+import os
 from itertools import pairwise
 
 import torch
@@ -20,6 +21,10 @@ from ..conv import MLP, GINConv
 from ..graph import as_graph
 from ..utils.placeholder import Placeholder
 from .base import BaseModelConfig, BaseModule
+
+
+# the GIN model as one autograd node (ops.gin_stack) when eligible; LGNN_GIN_STACK=0: per-conv
+STACK = os.environ.get("LGNN_GIN_STACK", "1") != "0"
 
 
 class GIN(nn.Module):
@@ -49,8 +54,16 @@ class GIN(nn.Module):
     def forward(self, x: torch.Tensor, edge_index, batch: torch.Tensor,
                 num_graphs: int | None = None) -> torch.Tensor:
         g = as_graph(edge_index, x.size(0), batch, num_graphs)
-        h = ops.node_linear(x, self.in_proj.weight, self.in_proj.bias)
         drop = self.dropout.p > 0.0 and self.training
+        if STACK and not drop and ops.gin_stack_eligible(
+                x, self.in_proj.weight,
+                [(c.nn.lins[0].weight, c.nn.lins[1].weight) for c in self.convs]):
+            # the whole model as one autograd node: each conv's aggregation backward is gathered
+            # by the layer below it instead of a separate transpose pass
+            convs = [c.stack_spec(x, _lib.LGNN_ACT_ELU) for c in self.convs]
+            return ops.gin_stack(x, self.in_proj.weight, self.in_proj.bias, convs,
+                                 self.out_proj.weight, self.out_proj.bias, g, self.pool == "mean")
+        h = ops.node_linear(x, self.in_proj.weight, self.in_proj.bias)
         last = len(self.convs) - 1
         for i, conv in enumerate(self.convs):
             if i == last and not drop and conv.head_fusable(h):

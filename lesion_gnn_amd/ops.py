@@ -1113,9 +1113,14 @@ class _GINConv(torch.autograd.Function):
         return H, (S, Z1, A1, H, W1, W2, mean, invstd, scale, shift, mask)
 
     @staticmethod
-    def _backward_fused(ctx, dH, pool: tuple | None = None):
+    def _backward_fused(ctx, dH, pool: tuple | None = None, gather: tuple | None = None,
+                        defer_dx: bool = False):
         """pool = (dlogits, W_out, graph, mean): the output gradient comes from the pooled readout
-        (global pool + out_proj backward folded into Lin2's backward load; dH is None)."""
+        (global pool + out_proj backward folded into Lin2's backward load; dH is None).
+        gather = (dS, tself): the output gradient is the next conv's aggregation backward,
+        tself dS + A^T dS, gathered as Lin2's backward loads it (dH is None). defer_dx: return
+        this conv's pre-aggregation input gradient (for the previous layer to gather) instead
+        of aggregating it here."""
         S, Z1, A1, H, W1, W2, mean, invstd, scale, shift, mask = ctx.saved_tensors[:11]
         csr = ctx.graph.csr("gin")
         M, N1 = Z1.shape
@@ -1138,7 +1143,15 @@ class _GINConv(torch.autograd.Function):
         dA1 = torch.empty_like(Z1)
         slab2 = torch.empty(P * (N2 * N1 + N2), dtype=torch.float32, device=dev)
         gpart = torch.empty(P * 2 * N1, dtype=torch.float64, device=dev)
-        if pool is not None:
+        if gather is not None:
+            dS, tself = gather
+            _lib.call("lgnn_node_linear_bwd_bn_gather", _lib.ptr(dS), _lib.ptr(csr.tptr),
+                      _lib.ptr(csr.tidx), _lib.ptr(csr.tw), float(tself), _lib.ptr(H), ctx.act,
+                      _lib.ptr(A1), M, N1, w2, N2, _lib.ptr(dA1), _lib.ptr(slab2),
+                      _lib.ptr(slab2[P * N2 * N1:]), P, _lib.ptr(Z1), _lib.ptr(mask),
+                      _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(mean), _lib.ptr(invstd),
+                      _lib.ptr(gpart), _s(dev))
+        elif pool is not None:
             dlog, W_out, pg, pmean = pool
             _lib.call("lgnn_node_linear_bwd_bn_pool", _lib.LGNN_BN_GSTATS, None, _lib.ptr(H),
                       ctx.act, _lib.ptr(A1), M, N1, w2, N2, _lib.ptr(dA1), _lib.ptr(slab2),
@@ -1184,7 +1197,8 @@ class _GINConv(torch.autograd.Function):
         reduce_multi(red, dev)
         dx = None
         if want_dx:
-            dx = spmm_raw(csr.tptr, csr.tidx, csr.tw, ctx.self_scale, dxpre)
+            dx = dxpre if defer_dx else spmm_raw(csr.tptr, csr.tidx, csr.tw, ctx.self_scale,
+                                                 dxpre)
         return (dx, dW1, db1, dg, dbt, dW2, db2, None, None, None, None, None, None, None,
                 None)
 
@@ -1254,6 +1268,107 @@ class _GINConvHead(torch.autograd.Function):
         g = _GINConv._backward_fused(ctx, None, pool=(dlogits, W_out, ctx.head_graph,
                                                       ctx.head_mean))
         return (*g[:7], dWo, dbo) + (None,) * 9
+
+
+class _SubCtx:
+    """The per-conv state _GINConv._forward_fused / _backward_fused keep on an autograd ctx,
+    for one conv inside the _GINStack node."""
+
+    def __init__(self, needs_dx: bool):
+        self.needs_input_grad = (needs_dx,)
+        self.saved_tensors = ()
+
+    def save_for_backward(self, *t):
+        self.saved_tensors = t
+
+
+class _GINStack(torch.autograd.Function):
+    """The whole GIN model (in_proj + every GINConv + global pool + out_proj, reference
+    gin.py:17-35) as one autograd node on the BN-fused fp32 kernels. Same kernels as the
+    per-conv nodes, except the backward of each conv's aggregation: instead of a transpose-CSR
+    pass over its input gradient (spmm), the previous layer's backward gathers that gradient as
+    it loads it (lgnn_node_linear_bwd_bn_gather for a conv's Lin2, lgnn_node_linear_bwd in
+    LGNN_GRAD_TRANSPOSE mode for in_proj), so no aggregated gradient goes through HBM."""
+
+    @staticmethod
+    def forward(ctx, x, graph, mean, specs, W_in, b_in, W_out, b_out, *flat):
+        _lib.require_gpu(x, W_in, W_out)
+        x, W_in, b_in, W_out, b_out = (_f32c(t) for t in (x, W_in, b_in, W_out, b_out))
+        csr = graph.csr("gin")
+        h = linear_fwd(x, W_in, b_in, _lib.LGNN_ACT_NONE)
+        subs, saved = [], [x, W_in]
+        for i, sp in enumerate(specs):
+            W1, b1, gamma, beta, W2, b2 = flat[6 * i:6 * i + 6]
+            sub = _SubCtx(True)
+            h, sv = _GINConv._forward_fused(sub, h, _f32c(W1), _f32c(b1), _f32c(W2), _f32c(b2),
+                                            csr, 1.0 + float(sp["eps"]), graph, sp["bn"],
+                                            sp["training"], sp["mask"], sp["act"], sp["group"],
+                                            sp["sync_count"], gamma)
+            sub.n_saved = len(sv)
+            saved += list(sv)
+            subs.append(sub)
+        pooled, logits = pool_head_fwd(h, graph, mean, W_out, b_out)
+        ctx.save_for_backward(*saved, pooled, W_out)
+        ctx.subs, ctx.graph, ctx.mean = subs, graph, mean
+        ctx.in_self = [1.0 + float(sp["eps"]) for sp in specs]
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        saved = ctx.saved_tensors
+        x, W_in = saved[0], saved[1]
+        pooled, W_out = saved[-2], saved[-1]
+        dlogits = _f32c(dlogits)
+        B, D = pooled.shape
+        C = W_out.size(0)
+        dev = pooled.device
+        dWo = torch.empty(C, D, dtype=torch.float32, device=dev)
+        dbo = torch.empty(C, dtype=torch.float32, device=dev)
+        _lib.call("lgnn_pool_head_bwd", _lib.ptr(dlogits), _lib.ptr(pooled), B, D,
+                  _lib.ptr(W_out), C, None, _lib.ptr(dWo), _lib.ptr(dbo), _s(dev))
+        off = 2
+        for sub in ctx.subs:
+            sub.saved_tensors = saved[off:off + sub.n_saved]
+            off += sub.n_saved
+        L = len(ctx.subs)
+        grads = [None] * L
+        dS = None
+        for i in range(L - 1, -1, -1):
+            sub = ctx.subs[i]
+            if i == L - 1:
+                g = _GINConv._backward_fused(sub, None, pool=(dlogits, W_out, ctx.graph,
+                                                               ctx.mean), defer_dx=True)
+            else:
+                g = _GINConv._backward_fused(sub, None, gather=(dS, ctx.in_self[i + 1]),
+                                             defer_dx=True)
+            dS = g[0]
+            grads[i] = g[1:7]
+        # in_proj: its output gradient is the first conv's aggregation backward, gathered
+        dx, dW_in, db_in = linear_bwd(_lib.LGNN_GRAD_TRANSPOSE, dS, H=None, act=_lib.LGNN_ACT_NONE,
+                                      X=x, W=W_in, tcsr=ctx.graph.csr("gin"),
+                                      tself=ctx.in_self[0], want_dx=ctx.needs_input_grad[0])
+        flat = [t for g in grads for t in g]
+        return (dx, None, None, None, dW_in, db_in, dWo, dbo, *flat)
+
+
+def gin_stack_eligible(x, W_in, convs_W) -> bool:
+    """Whether the GIN model runs as one _GINStack node (eager, BN-fused fp32 kernels, every
+    layer on the fast-path shapes)."""
+    return (not _compiling() and GIN_MFMA == "f32" and fast_shape(x.size(1), W_in.size(0)) and
+            all(gin_bn_fused(W1.size(1), W1.size(0), W2.size(0)) for W1, W2 in convs_W))
+
+
+def gin_stack(x, W_in, b_in, convs: list, W_out, b_out, graph: Graph, mean: bool):
+    """convs: per GINConv a dict (W1, b1, bn, W2, b2, eps, mask, act, group, sync_count)."""
+    specs, flat = [], []
+    for c in convs:
+        bn = c["bn"]
+        training = bn.training or not bn.track_running_stats
+        specs.append(dict(bn=bn, training=training, eps=c["eps"], mask=c["mask"], act=c["act"],
+                          group=c["group"], sync_count=c["sync_count"]))
+        flat += [c["W1"], c["b1"], bn.weight if bn.affine else None,
+                 bn.bias if bn.affine else None, c["W2"], c["b2"]]
+    return _GINStack.apply(x, graph, mean, specs, W_in, b_in, W_out, b_out, *flat)
 
 
 def gin_conv_head_eligible(x, W1, W2) -> bool:

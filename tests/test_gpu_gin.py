@@ -140,6 +140,9 @@ def test_gin_last_conv_readout_fused_bitexact(cuda, pool, monkeypatch):
     backward folded into Lin2's backward load) is bit-identical to the separate conv and
     pool_head nodes (same arithmetic: k_head_bwd's fmaf chain, then / |graph|), and matches the
     oracle; ragged graphs, SyncBN-free training mode."""
+    from lesion_gnn_amd.models import gin as gin_mod
+
+    monkeypatch.setattr(gin_mod, "STACK", False)  # per-conv nodes (the model-wide one: below)
     sizes = [1, 5, 64, 200, 2, 33, 90, 17] * 4
     b = synth.make_batch(len(sizes), k=6, d_in=64, seed=21, sizes=sizes)
     ours, oref = make_pair(64, [64, 128, 96], pool=pool)
@@ -160,3 +163,48 @@ def test_gin_last_conv_readout_fused_bitexact(cuda, pool, monkeypatch):
     lr_, _, gr, _ = step(oref.train(), b, "cpu")
     torch.testing.assert_close(l1, lr_, rtol=0, atol=1e-4 * max(1.0, lr_.abs().max().item()))
     assert_grads(g1, gr)
+
+
+@pytest.mark.parametrize("sizes,pool,eval_mode", [
+    ([64] * 1024, "add", False),                      # C4 shape: every tile closed
+    ([1, 5, 64, 200, 2, 33, 90, 17] * 4, "mean", False),  # ragged: open tiles, global gathers
+    ([1, 5, 64, 200, 2, 33, 90, 17] * 4, "add", True),    # eval: running statistics
+])
+def test_gin_stack_node(cuda, sizes, pool, eval_mode, monkeypatch):
+    """The whole GIN model as one autograd node (ops.gin_stack: each conv's aggregation backward
+    gathered by the layer below — lgnn_node_linear_bwd_bn_gather / in_proj in transpose mode —
+    instead of a transpose spmm) against the per-conv nodes (within 1e-5 of each tensor's scale:
+    the same sums, the self term added after the neighbours instead of before) and the oracle;
+    running statistics identical in value."""
+    from lesion_gnn_amd.models import gin as gin_mod
+
+    b = synth.make_batch(len(sizes), k=8 if len(sizes) > 100 else 6, d_in=128, seed=31,
+                         sizes=sizes)
+    ours, oref = make_pair(128, [128, 128, 96], pool=pool)
+    ours = ours.to(cuda).train()
+    if eval_mode:  # one training step first so the running statistics are not the initial ones
+        step(ours, b, cuda)
+        step(oref.train(), b, "cpu")
+        ours.eval()
+        oref.eval()
+    sd = {k: v.clone() for k, v in ours.state_dict().items()}
+    res = []
+    for stack in (True, False):
+        monkeypatch.setattr(gin_mod, "STACK", stack)
+        ours.load_state_dict(sd)
+        res.append(step(ours, b, cuda))
+    (l1, _, g1, s1), (l2, _, g2, s2) = res
+    torch.testing.assert_close(l1, l2, rtol=0, atol=1e-5 * max(1.0, l2.abs().max().item()))
+    for k in g2:
+        torch.testing.assert_close(g1[k], g2[k], rtol=0,
+                                   atol=max(1e-5 * g2[k].abs().max().item(), 1e-7),
+                                   msg=lambda msg: f"{k}: {msg}")
+    for k in s2:
+        torch.testing.assert_close(s1[k].float(), s2[k].float(), rtol=1e-6, atol=1e-7)
+    lr_, _, gr, _ = step(oref, b, "cpu")
+    torch.testing.assert_close(l1, lr_, rtol=0, atol=1e-4 * max(1.0, lr_.abs().max().item()))
+    for k in gr:  # 5e-6 floor: in_proj.bias feeds BatchNorm through equal-degree aggregation,
+        # so its gradient vanishes analytically (DESIGN §2, parity bar)
+        torch.testing.assert_close(g1[k], gr[k], rtol=0,
+                                   atol=max(1e-4 * gr[k].abs().max().item(), 5e-6),
+                                   msg=lambda m: f"{k}: {m}")
