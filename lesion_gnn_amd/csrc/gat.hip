@@ -28,6 +28,9 @@ constexpr float EPS16 = 1e-16f;
 #ifndef LGNN_GAT_WPE
 #define LGNN_GAT_WPE 0
 #endif
+#ifndef LGNN_GAT_NODE_XCD
+#define LGNN_GAT_NODE_XCD 1
+#endif
 #if LGNN_GAT_WPE > 0
 #define GAT_OCC __attribute__((amdgpu_waves_per_eu(LGNN_GAT_WPE)))
 #else
@@ -434,8 +437,18 @@ __global__ __launch_bounds__(NT) GAT_OCC void k_gat_bwd_node(
   const Buf bT = mkbuf(tidx, cap * 4), bP = mkbuf(tmap, cap * 4), bZ = mkbuf(dZ, M * HC * 4);
   const Buf bAl = mkbuf(alpha, cap * H * 4), bM = mkbuf(mask, mask ? cap * H * 4 : 0);
   const Buf bDa = mkbuf(da_e, cap * H * 4);
+#if LGNN_GAT_NODE_XCD
+  // rows in 8 contiguous ranges, range x walked by the workgroups on XCD x (blocks are dealt
+  // round-robin over the XCDs): the alpha / da_e entries a source row gathers through tmap, and
+  // the dZ rows, belong to its own graph, so they stay in that XCD's L2
+  const int64_t xcd = blockIdx.x % 8, nb = ((int64_t)gridDim.x - xcd + 7) / 8;
+  const int64_t span = ((M + 7) / 8 + RB - 1) / RB * RB;
+  const int64_t rbeg = xcd * span, rend = rbeg + span < M ? rbeg + span : M;
+  for (int64_t row = rbeg + (int64_t)(blockIdx.x / 8) * RB + hw; row < rend; row += nb * RB) {
+#else
   // (plain block order: the XCD-contiguous mapping of lane_row measured 3 us slower here)
   for (int64_t row = (int64_t)blockIdx.x * RB + hw; row < M; row += (int64_t)gridDim.x * RB) {
+#endif
     const int q0 = tptr[row], q1 = tptr[row + 1];
 #pragma unroll
     for (int st = 0; st < NST; ++st) {
