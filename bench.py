@@ -559,6 +559,10 @@ def main():
                          "frac": round(achieved / peak, 4),
                          "traffic": round(traffic) if traffic else None,
                          "traffic_source": tsrc, "kernel": kt["kernel"],
+                         # the same useful fp32 FLOP against the fp32 MFMA peak (what an fp32
+                         # GEMM kernel of these shapes is bounded by); `frac` prices the split-3
+                         # algorithm's own ceiling (6 bf16 products per fp32 product)
+                         "frac_of_fp32_mfma_peak": round(achieved / MFMA_F32_PEAK_TF, 4),
                          "avg_launch_ms": round(kt["ms"], 5), "flops_per_launch": kt["flops"]})
         rows.sort(key=lambda r: -r["avg_launch_ms"])
         out["roofline"] = rows[0]  # the dominant kernel (longest launch)

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 21
+#define LGNN_ABI_VERSION 22
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -380,6 +380,18 @@ int lgnn_gat_bwd_edge(const int32_t* rowptr, const int32_t* col, const float* XP
                       const float* edge_mask, const float* dY, const float* Y, int act, int64_t M,
                       int H, int C, float negative_slope, float* dZ, float* da_e, float* da_d,
                       void* stream);
+/* lgnn_gat_bwd_edge with the output gradient formed from the readout's gradient (ABI v22):
+ * dY[i] = (dlogits[batch[i]] . Wout) (/ |graph| when pool_mean), with lgnn_pool_head_bwd's and
+ * lgnn_pool_bwd's arithmetic (bitwise), so the GAT model's last conv needs no dH tensor: the
+ * global_mean_pool / global_add_pool + out_proj backward (reference gat.py:56-58) folded into
+ * this kernel's load. Wout [num_classes][H*C]; dY is not an argument. */
+int lgnn_gat_bwd_edge_pool(const int32_t* rowptr, const int32_t* col, const float* XP,
+                           const float* a_s, const float* a_d, const float* alpha,
+                           const float* edge_mask, const float* Y, int act, int64_t M, int H,
+                           int C, float negative_slope, const int64_t* batch,
+                           const int32_t* gptr, int pool_mean, const float* dlogits,
+                           const float* Wout, int num_classes, float* dZ, float* da_e,
+                           float* da_d, void* stream);
 /* Backward, source rows (transpose CSR + tmap from lgnn_graph_build): dXP, and per-block column
  * partials [P][3][H*C] = (d att_src, d att_dst, d bias) for lgnn_reduce_partials. */
 int lgnn_gat_bwd_num_partials(int64_t M);

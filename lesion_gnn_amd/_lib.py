@@ -75,6 +75,8 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_bf16_wgrad": (I32, [P, I32, P, I32, I64, I32, P, I32, P]),
     "lgnn_gat_fwd": (I32, [P, P, P, P, P, I64, I32, I32, F32, P, P, I32, P, P, P, P]),
     "lgnn_gat_bwd_edge": (I32, [P, P, P, P, P, P, P, P, P, I32, I64, I32, I32, F32, P, P, P, P]),
+    "lgnn_gat_bwd_edge_pool": (I32, [P, P, P, P, P, P, P, P, I32, I64, I32, I32, F32, P, P, I32,
+                                      P, P, I32, P, P, P, P]),
     "lgnn_gat_bwd_num_partials": (I32, [I64]),
     "lgnn_gat_bwd_node": (I32, [P, P, P, P, P, P, P, P, P, P, P, I64, I32, I32, P, P, I32, P,
                                 P]),
@@ -122,7 +124,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 21
+ABI_VERSION = 22
 
 _lib = None
 

@@ -187,6 +187,19 @@ class GATConv(nn.Module):
         return ops.gat_conv(x, self.lin.weight, self.att_src, self.att_dst, self.bias, g,
                             self.heads, self.negative_slope, mask, act, bf16)
 
+    def forward_head(self, x: torch.Tensor, g, act: int, W_out: torch.Tensor,
+                     b_out: torch.Tensor, mean: bool, bf16: bool = False) -> torch.Tensor:
+        """forward(x) followed by global pool + out_proj (W_out, b_out) in one autograd node
+        (ops.gat_conv_head): the model's last conv and readout. Returns the logits."""
+        mask = None
+        if self.dropout > 0.0 and self.training:
+            cap = g.csr("gat").col.numel()
+            mask = (torch.rand(cap, self.heads, device=x.device) >= self.dropout).float()
+            mask.mul_(1.0 / (1.0 - self.dropout))
+        return ops.gat_conv_head(x, self.lin.weight, self.att_src, self.att_dst, self.bias,
+                                 W_out, b_out, g, self.heads, self.negative_slope, mask, act,
+                                 bf16, mean)
+
 
 def global_mean_pool(x: torch.Tensor, batch: torch.Tensor, size: int | None = None,
                      graph: Graph | None = None) -> torch.Tensor:

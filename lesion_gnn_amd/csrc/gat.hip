@@ -302,13 +302,26 @@ __global__ __launch_bounds__(NT) GAT_OCC void k_gat_fwd(const int32_t* __restric
 //   de_ij = alpha_ij (dal_ij - s_i);  da_ij = de_ij * leaky'(a_s[j] + a_d[i])
 //   da_e[ij] = da_ij (per edge),  da_d[i] = sum_j da_ij
 // ------------------------------------------------------------------------------------------
-template <int ACT, int NS>
+// Readout gradient (POOL): the layer's output gradient is not a tensor but formed per row from
+// the logits' gradient, dY[i] = (dlog[g] . Wout) / |g| (g = batch[i]; mean pooling), with
+// k_head_bwd's fmaf chain over the classes and k_pool_bwd's division: the global pool + out_proj
+// backward folded into this load, bitwise what those two kernels would have written.
+struct PoolGrad {
+  const int64_t* batch;
+  const int32_t* gptr;
+  const float* dlog;  // [B][nclass]
+  const float* Wout;  // [nclass][H*C]
+  int nclass;
+  int mean;
+};
+
+template <int ACT, int NS, bool POOL = false>
 __global__ __launch_bounds__(NT) GAT_OCC void k_gat_bwd_edge(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const float* __restrict__ XP, const float* __restrict__ a_s, const float* __restrict__ a_d,
     const float* __restrict__ alpha, const float* __restrict__ mask, const float* __restrict__ dY,
     const float* __restrict__ Y, int64_t M, int H, int C, float slope, float* __restrict__ dZ,
-    float* __restrict__ da_e, float* __restrict__ da_d) {
+    float* __restrict__ da_e, float* __restrict__ da_d, PoolGrad pg = PoolGrad{}) {
   constexpr int EBN = EB / NS;
   const Lane L = lane_row();
   if (L.row >= M) return;
@@ -324,7 +337,23 @@ __global__ __launch_bounds__(NT) GAT_OCC void k_gat_bwd_edge(
     f32x4 dz[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      dz[s] = ld4(dY + L.row * HC + P.fc[s]);
+      if constexpr (POOL) {
+        const int64_t g = pg.batch[L.row];
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int c = 0; c < pg.nclass; ++c) {
+          const float d = pg.dlog[g * pg.nclass + c];
+          const f32x4 wv = ld4(pg.Wout + (int64_t)c * HC + P.fc[s]);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[j] = fmaf(d, wv[j], acc[j]);
+        }
+        if (pg.mean) {
+          const int cnt = pg.gptr[g + 1] - pg.gptr[g];
+          acc = acc / (float)(cnt > 0 ? cnt : 1);
+        }
+        dz[s] = acc;
+      } else {
+        dz[s] = ld4(dY + L.row * HC + P.fc[s]);
+      }
       if (ACT == LGNN_ACT_ELU) {
         const f32x4 y = ld4(Y + L.row * HC + P.fc[s]);
 #pragma unroll
@@ -577,22 +606,32 @@ extern "C" int lgnn_gat_fwd(const int32_t* rowptr, const int32_t* col, const flo
   return LGNN_OK;
 }
 
-extern "C" int lgnn_gat_bwd_edge(const int32_t* rowptr, const int32_t* col, const float* XP,
-                                 const float* a_s, const float* a_d, const float* alpha,
-                                 const float* edge_mask, const float* dY, const float* Y,
-                                 int act, int64_t M, int H, int C, float negative_slope,
-                                 float* dZ, float* da_e, float* da_d, void* stream) {
+namespace {
+int gat_bwd_edge_launch(const int32_t* rowptr, const int32_t* col, const float* XP,
+                        const float* a_s, const float* a_d, const float* alpha,
+                        const float* edge_mask, const float* dY, const float* Y, int act,
+                        int64_t M, int H, int C, float slope, float* dZ, float* da_e, float* da_d,
+                        const PoolGrad* pg, void* stream) {
   if (M < 0 || !shape_ok(H, C) || (act != LGNN_ACT_NONE && act != LGNN_ACT_ELU))
     return LGNN_EINVAL;
-  if (M > 0 && (!rowptr || !col || !XP || !a_s || !a_d || !alpha || !dY || !dZ || !da_e || !da_d))
+  if (M > 0 && (!rowptr || !col || !XP || !a_s || !a_d || !alpha || (!dY && !pg) || !dZ ||
+                !da_e || !da_d))
     return LGNN_EINVAL;
   if (act == LGNN_ACT_ELU && M > 0 && !Y) return LGNN_EINVAL;
   if (!bytes_ok(M, H, C)) return LGNN_EINVAL;
   if (M == 0) return LGNN_OK;
-#define LGNN_GB(A_, NS_)                                                                   \
-  hipLaunchKernelGGL((k_gat_bwd_edge<A_, NS_>), dim3(row_grid(M)), dim3(NT), 0,               \
-                     as_stream(stream), rowptr, col, XP, a_s, a_d, alpha, edge_mask, dY, Y, M, \
-                     H, C, negative_slope, dZ, da_e, da_d)
+  const PoolGrad p = pg ? *pg : PoolGrad{};
+#define LGNN_GB(A_, NS_)                                                                        \
+  do {                                                                                          \
+    if (pg)                                                                                     \
+      hipLaunchKernelGGL((k_gat_bwd_edge<A_, NS_, true>), dim3(row_grid(M)), dim3(NT), 0,        \
+                         as_stream(stream), rowptr, col, XP, a_s, a_d, alpha, edge_mask, dY, Y, \
+                         M, H, C, slope, dZ, da_e, da_d, p);                                    \
+    else                                                                                        \
+      hipLaunchKernelGGL((k_gat_bwd_edge<A_, NS_, false>), dim3(row_grid(M)), dim3(NT), 0,       \
+                         as_stream(stream), rowptr, col, XP, a_s, a_d, alpha, edge_mask, dY, Y, \
+                         M, H, C, slope, dZ, da_e, da_d, p);                                    \
+  } while (0)
 #define LGNN_GB_NS(A_)                    \
   switch (ns_of(C)) {                     \
     case 1: LGNN_GB(A_, 1); break;        \
@@ -608,6 +647,30 @@ extern "C" int lgnn_gat_bwd_edge(const int32_t* rowptr, const int32_t* col, cons
 #undef LGNN_GB
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
+}
+}  // namespace
+
+extern "C" int lgnn_gat_bwd_edge(const int32_t* rowptr, const int32_t* col, const float* XP,
+                                 const float* a_s, const float* a_d, const float* alpha,
+                                 const float* edge_mask, const float* dY, const float* Y,
+                                 int act, int64_t M, int H, int C, float negative_slope,
+                                 float* dZ, float* da_e, float* da_d, void* stream) {
+  if (M > 0 && !dY) return LGNN_EINVAL;
+  return gat_bwd_edge_launch(rowptr, col, XP, a_s, a_d, alpha, edge_mask, dY, Y, act, M, H, C,
+                             negative_slope, dZ, da_e, da_d, nullptr, stream);
+}
+
+extern "C" int lgnn_gat_bwd_edge_pool(const int32_t* rowptr, const int32_t* col, const float* XP,
+                                      const float* a_s, const float* a_d, const float* alpha,
+                                      const float* edge_mask, const float* Y, int act, int64_t M,
+                                      int H, int C, float negative_slope, const int64_t* batch,
+                                      const int32_t* gptr, int pool_mean, const float* dlogits,
+                                      const float* Wout, int num_classes, float* dZ, float* da_e,
+                                      float* da_d, void* stream) {
+  if (M > 0 && (!batch || !gptr || !dlogits || !Wout || num_classes < 1)) return LGNN_EINVAL;
+  const PoolGrad pg{batch, gptr, dlogits, Wout, num_classes, pool_mean ? 1 : 0};
+  return gat_bwd_edge_launch(rowptr, col, XP, a_s, a_d, alpha, edge_mask, nullptr, Y, act, M, H,
+                             C, negative_slope, dZ, da_e, da_d, &pg, stream);
 }
 
 extern "C" int lgnn_gat_bwd_num_partials(int64_t M) {

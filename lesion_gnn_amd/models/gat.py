@@ -10,6 +10,7 @@ every conv one HIP autograd node (ops.gat_conv) with the ELU fused.
 from __future__ import annotations
 
 import dataclasses
+import os
 from itertools import pairwise
 
 import torch
@@ -20,6 +21,10 @@ from ..conv import GATConv
 from ..graph import as_graph
 from ..utils.placeholder import Placeholder
 from .base import BaseModelConfig, BaseModule
+
+
+# the last GATConv + readout as one autograd node (ops.gat_conv_head); LGNN_GAT_HEAD=0: separate
+HEAD_FOLD = os.environ.get("LGNN_GAT_HEAD", "1") != "0"
 
 
 class GAT(nn.Module):
@@ -52,7 +57,13 @@ class GAT(nn.Module):
             # every bf16 GEMM's weight operands for this step in one launch
             ops.bf16_prepare_weights([self.in_proj.weight] + [c.lin.weight for c in self.convs])
         h = ops.linear_auto(x, self.in_proj.weight, self.in_proj.bias, self.bf16)
-        for conv in self.convs:
+        last = len(self.convs) - 1
+        for i, conv in enumerate(self.convs):
+            if i == last and HEAD_FOLD and not torch.compiler.is_compiling():
+                # last conv + readout as one node: the readout's backward is formed inside the
+                # attention backward's load, no dH tensor
+                return conv.forward_head(h, g, _lib.LGNN_ACT_ELU, self.out_proj.weight,
+                                         self.out_proj.bias, self.pool == "mean", self.bf16)
             h = conv(h, g, act=_lib.LGNN_ACT_ELU, bf16=self.bf16)
         return ops.pool_head(h, self.out_proj.weight, self.out_proj.bias, g, self.pool == "mean")
 

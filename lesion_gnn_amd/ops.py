@@ -1484,8 +1484,10 @@ class _GATConv(torch.autograd.Function):
         return Y
 
     @staticmethod
-    def backward(ctx, dY):
-        x, W, att_src, att_dst, XP, a_s, a_d, alpha, Y, mask = ctx.saved_tensors
+    def backward(ctx, dY, pool: tuple | None = None):
+        """pool = (dlogits, W_out, graph, mean): the output gradient is formed from the readout's
+        gradient inside the edge kernel (lgnn_gat_bwd_edge_pool; dY is None)."""
+        x, W, att_src, att_dst, XP, a_s, a_d, alpha, Y, mask = ctx.saved_tensors[:10]
         csr = ctx.graph.csr("gat")
         M, HC = Y.shape
         H = ctx.heads
@@ -1494,10 +1496,18 @@ class _GATConv(torch.autograd.Function):
         dZ = torch.empty_like(Y)
         da_e = torch.empty_like(alpha)
         da_d = torch.empty(M, H, dtype=torch.float32, device=dev)
-        _lib.call("lgnn_gat_bwd_edge", _lib.ptr(csr.rowptr), _lib.ptr(csr.col), _lib.ptr(XP),
-                  _lib.ptr(a_s), _lib.ptr(a_d), _lib.ptr(alpha), _lib.ptr(mask),
-                  _lib.ptr(_f32c(dY)), _lib.ptr(Y), ctx.act, M, H, C, float(ctx.slope),
-                  _lib.ptr(dZ), _lib.ptr(da_e), _lib.ptr(da_d), _s(dev))
+        if pool is not None:
+            dlog, W_out, pg, pmean = pool
+            _lib.call("lgnn_gat_bwd_edge_pool", _lib.ptr(csr.rowptr), _lib.ptr(csr.col),
+                      _lib.ptr(XP), _lib.ptr(a_s), _lib.ptr(a_d), _lib.ptr(alpha), _lib.ptr(mask),
+                      _lib.ptr(Y), ctx.act, M, H, C, float(ctx.slope), _lib.ptr(pg.batch),
+                      _lib.ptr(pg.gptr), int(pmean), _lib.ptr(dlog), _lib.ptr(W_out),
+                      W_out.size(0), _lib.ptr(dZ), _lib.ptr(da_e), _lib.ptr(da_d), _s(dev))
+        else:
+            _lib.call("lgnn_gat_bwd_edge", _lib.ptr(csr.rowptr), _lib.ptr(csr.col),
+                      _lib.ptr(XP), _lib.ptr(a_s), _lib.ptr(a_d), _lib.ptr(alpha),
+                      _lib.ptr(mask), _lib.ptr(_f32c(dY)), _lib.ptr(Y), ctx.act, M, H, C,
+                      float(ctx.slope), _lib.ptr(dZ), _lib.ptr(da_e), _lib.ptr(da_d), _s(dev))
         P = _lib.load().lgnn_gat_bwd_num_partials(M)
         part = torch.empty(P * 3 * HC, dtype=torch.float32, device=dev)
         dXP = torch.empty_like(XP)
@@ -1568,6 +1578,53 @@ def _bf16_copy_of(x: torch.Tensor):
     if ref() is not x or x._version != version:
         return None
     return xb
+
+
+class _GATConvHead(torch.autograd.Function):
+    """The GAT model's last GATConv + global pool + out_proj as one autograd node: its backward
+    forms the conv's output gradient from dlogits inside the edge kernel (out_proj backward +
+    pool backward folded into the load, lgnn_gat_bwd_edge_pool) instead of writing dH
+    (k_pool_bwd); out_proj's dW / db from lgnn_pool_head_bwd. Bitwise the separate nodes."""
+
+    @staticmethod
+    def forward(ctx, x, W, att_src, att_dst, bias, W_out, b_out, graph, heads, slope, mask, act,
+                bf16, mean):
+        sub = _SubCtx(True)
+        Y = _GATConv.forward(sub, x, W, att_src, att_dst, bias, graph, heads, slope, mask, act,
+                             bf16)
+        W_out, b_out = _f32c(W_out), _f32c(b_out)
+        pooled, logits = pool_head_fwd(Y, graph, mean, W_out, b_out)
+        ctx.save_for_backward(*sub.saved_tensors, pooled, W_out)
+        sub.saved_tensors = ()
+        ctx.sub, ctx.head_graph, ctx.head_mean = sub, graph, mean
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        saved = ctx.saved_tensors
+        pooled, W_out = saved[10], saved[11]
+        dlogits = _f32c(dlogits)
+        B, D = pooled.shape
+        C = W_out.size(0)
+        dev = pooled.device
+        dWo = torch.empty(C, D, dtype=torch.float32, device=dev)
+        dbo = torch.empty(C, dtype=torch.float32, device=dev)
+        _lib.call("lgnn_pool_head_bwd", _lib.ptr(dlogits), _lib.ptr(pooled), B, D,
+                  _lib.ptr(W_out), C, None, _lib.ptr(dWo), _lib.ptr(dbo), _s(dev))
+        sub = ctx.sub
+        sub.saved_tensors = saved[:10]
+        sub.needs_input_grad = (ctx.needs_input_grad[0],)
+        g = _GATConv.backward(sub, None, pool=(dlogits, W_out, ctx.head_graph, ctx.head_mean))
+        sub.saved_tensors = ()
+        return (*g[:5], dWo, dbo) + (None,) * 7
+
+
+def gat_conv_head(x, W, att_src, att_dst, bias, W_out, b_out, graph: Graph, heads: int,
+                  slope: float = 0.2, mask=None, act: int = _lib.LGNN_ACT_NONE,
+                  bf16: bool = False, mean: bool = True):
+    """gat_conv followed by pool_head (the GAT model's last conv and readout) as one node."""
+    return _GATConvHead.apply(x, W, att_src, att_dst, bias, W_out, b_out, graph, heads, slope,
+                              mask, act, bf16, mean)
 
 
 def gat_conv(x, W, att_src, att_dst, bias, graph: Graph, heads: int, slope: float = 0.2,

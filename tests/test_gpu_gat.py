@@ -219,3 +219,35 @@ def test_gat_bf16_batched_weight_prep_bitwise(cuda, monkeypatch):
     assert torch.equal(res[0][0], res[1][0])
     for n in res[1][1]:
         assert torch.equal(res[0][1][n], res[1][1][n]), n
+
+
+@pytest.mark.parametrize("precision,pool,dropout", [("bf16", "mean", 0.0), ("fp32", "add", 0.0),
+                                                    ("fp32", "mean", 0.3)])
+def test_gat_last_conv_readout_fused_bitwise(cuda, monkeypatch, precision, pool, dropout):
+    """The last GATConv + global pool + out_proj as one node (ops.gat_conv_head: the readout's
+    backward formed inside lgnn_gat_bwd_edge_pool's load) is bit-identical to the separate conv
+    and pool_head nodes (k_head_bwd's fmaf chain, then k_pool_bwd's division), same dropout
+    masks; and matches the oracle (dropout 0)."""
+    from lesion_gnn_amd.models import gat as gat_mod
+
+    b = synth.make_batch(48, k=6, d_in=64, seed=27, sizes="lognormal")
+    torch.manual_seed(9)
+    m = GAT(64, [128] * 4, 1, heads=4, dropout=dropout, precision=precision,
+            pool=pool).to(cuda).train()
+    res = []
+    for fold in (True, False):
+        monkeypatch.setattr(gat_mod, "HEAD_FOLD", fold)
+        torch.manual_seed(13)
+        out = m(b.x.to(cuda), b.edge_index.to(cuda), b.batch.to(cuda), b.num_graphs)
+        m.zero_grad(set_to_none=True)
+        out.square().sum().backward()
+        res.append((out.detach().cpu(), {n: p.grad.detach().cpu() for n, p in m.named_parameters()}))
+    assert torch.equal(res[0][0], res[1][0])
+    for n in res[1][1]:
+        assert torch.equal(res[0][1][n], res[1][1][n]), n
+    if dropout == 0.0 and precision == "fp32":
+        oref = ref.GAT(64, [128] * 4, 1, heads=4, dropout=0.0, pool=pool)
+        oref.load_state_dict(m.state_dict())
+        want = oref(b.x, b.edge_index, b.batch, b.num_graphs)
+        torch.testing.assert_close(res[0][0], want.detach(), rtol=0,
+                                   atol=1e-4 * max(1.0, want.abs().max().item()))
