@@ -178,7 +178,12 @@ def loss_fn(wl, logits, y, oracle=False):
 
         return ops.cross_entropy(logits, y)
     # reference regression head: clamp(logits.squeeze(1), 0, C-1) then MSE (gat.py:94-95)
-    return torch.nn.functional.mse_loss(logits.squeeze(1).clamp(0, wl["classes"] - 1), y.float())
+    if oracle:
+        return torch.nn.functional.mse_loss(logits.squeeze(1).clamp(0, wl["classes"] - 1),
+                                            y.float())
+    from lesion_gnn_amd import ops  # HIP clamp + criterion (one launch each way)
+
+    return ops.regression_loss(logits, y, 0.0, float(wl["classes"] - 1), "MSE")[1]
 
 
 def _time_launches(launch, dev, reps=20):

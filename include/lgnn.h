@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 22
+#define LGNN_ABI_VERSION 23
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -472,6 +472,18 @@ int lgnn_ce_fwd(const float* logits, const int64_t* target, const float* weight,
 int lgnn_ce_bwd(const float* logits, const int64_t* target, const float* weight, int64_t B, int C,
                 const float* lse, const float* wsum, const float* grad_loss, float* dlogits,
                 void* stream);
+/* Regression head + criterion (ABI v23): pred = clamp(z, lo, hi) (reference gat.py:94-95,
+ * gin.py:66-67: logits.squeeze(1).clamp(0, C - 1)) and loss = mean l(pred - y) with
+ * l = nn.MSELoss (smooth_l1 = 0) or nn.SmoothL1Loss(beta = 1) (models/base.py:95-96), one
+ * workgroup, fixed-order sum. target: int64 class labels (target_is_i64; the reference's
+ * y.float()) or fp32 [B]. Backward: dz = [lo <= z <= hi] (grad_pred + grad_loss / B l'(pred - y));
+ * grad_loss / grad_pred nullable (not both). */
+int lgnn_regression_fwd(const float* z, const void* target, int target_is_i64, int64_t B,
+                        float lo, float hi, int smooth_l1, float* pred, float* loss,
+                        void* stream);
+int lgnn_regression_bwd(const float* z, const void* target, int target_is_i64, int64_t B,
+                        float lo, float hi, int smooth_l1, const float* grad_loss,
+                        const float* grad_pred, float* dz, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Fused GCN layer stack, backward, for the tiles with tile_open[t] == 0 (L = 1 or 2 convs).

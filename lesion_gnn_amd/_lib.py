@@ -77,6 +77,8 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_gat_bwd_edge": (I32, [P, P, P, P, P, P, P, P, P, I32, I64, I32, I32, F32, P, P, P, P]),
     "lgnn_gat_bwd_edge_pool": (I32, [P, P, P, P, P, P, P, P, I32, I64, I32, I32, F32, P, P, I32,
                                       P, P, I32, P, P, P, P]),
+    "lgnn_regression_fwd": (I32, [P, P, I32, I64, F32, F32, I32, P, P, P]),
+    "lgnn_regression_bwd": (I32, [P, P, I32, I64, F32, F32, I32, P, P, P, P]),
     "lgnn_gat_bwd_num_partials": (I32, [I64]),
     "lgnn_gat_bwd_node": (I32, [P, P, P, P, P, P, P, P, P, P, P, I64, I32, I32, P, P, I32, P,
                                 P]),
@@ -124,7 +126,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 22
+ABI_VERSION = 23
 
 _lib = None
 

@@ -79,6 +79,56 @@ __global__ __launch_bounds__(256) void k_ce_bwd(const float* __restrict__ z,
   dz[idx] = gloss[0] * wt / wsum[0] * (p - (c == t ? 1.f : 0.f));
 }
 
+// Regression head + criterion (reference gat.py:94-95 / gin.py:66-67: logits.squeeze(1).clamp(0,
+// C - 1), then models/base.py:95-96 nn.MSELoss() / nn.SmoothL1Loss(), mean reduction):
+//   p_i = clamp(z_i, lo, hi);  loss = (1/B) sum_i l(p_i - y_i)
+//   l(d) = d^2 (MSE) | (|d| < 1 ? d^2 / 2 : |d| - 1/2) (SmoothL1, beta = 1)
+//   dz_i = [lo <= z_i <= hi] (g_p[i] + g_loss / B * l'(p_i - y_i))   (torch's clamp backward
+//   passes the gradient where lo <= z <= hi; l'(d) = 2d | clamp(d, -1, 1))
+// Targets are read as int64 class labels (y.float() in the reference) or fp32.
+template <typename T>
+__device__ __forceinline__ float target_at(const T* y, int64_t i) { return (float)y[i]; }
+
+__device__ __forceinline__ float reg_term(float d, int smooth) {
+  if (!smooth) return d * d;
+  const float a = fabsf(d);
+  return a < 1.f ? 0.5f * d * d : a - 0.5f;
+}
+
+template <typename T>
+__global__ __launch_bounds__(CT) void k_reg_fwd(const float* __restrict__ z,
+                                                const T* __restrict__ y, int64_t B, float lo,
+                                                float hi, int smooth, float* __restrict__ pred,
+                                                float* __restrict__ loss) {
+  __shared__ float red[CT / 64 + 1];
+  float acc = 0.f;
+  for (int64_t i = threadIdx.x; i < B; i += CT) {
+    const float p = fminf(fmaxf(z[i], lo), hi);
+    pred[i] = p;
+    acc += reg_term(p - target_at(y, i), smooth);
+  }
+  const float t = block_sum_fixed(acc, red);
+  if (threadIdx.x == 0) loss[0] = t / (float)B;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_reg_bwd(const float* __restrict__ z,
+                                                 const T* __restrict__ y, int64_t B, float lo,
+                                                 float hi, int smooth,
+                                                 const float* __restrict__ gloss,
+                                                 const float* __restrict__ gpred,
+                                                 float* __restrict__ dz) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= B) return;
+  const float zi = z[i];
+  const float p = fminf(fmaxf(zi, lo), hi);
+  const float d = p - target_at(y, i);
+  const float dl = smooth ? fminf(fmaxf(d, -1.f), 1.f) : 2.f * d;
+  float g = gloss ? gloss[0] / (float)B * dl : 0.f;
+  if (gpred) g += gpred[i];
+  dz[i] = (zi >= lo && zi <= hi) ? g : 0.f;
+}
+
 // job j: out_j[i] = sum_{p < P_j} part_j[p * len_j + i] in slot order (as lgnn_reduce_partials);
 // with a factor (outer-product job): out_j[c * width_j + d] =
 //   sum_p part_j[p * (len_j / width_j) + c] * factor_j[p * width_j + d]
@@ -169,6 +219,38 @@ extern "C" int lgnn_ce_bwd(const float* logits, const int64_t* target, const flo
   hipLaunchKernelGGL(k_ce_bwd, dim3((unsigned)((B * C + 255) / 256)), dim3(256), 0,
                      as_stream(stream), logits, target, weight, B, C, lse, wsum, grad_loss,
                      dlogits);
+  LGNN_LAUNCH_CHECK();
+  return LGNN_OK;
+}
+
+extern "C" int lgnn_regression_fwd(const float* z, const void* target, int target_is_i64,
+                                   int64_t B, float lo, float hi, int smooth_l1, float* pred,
+                                   float* loss, void* stream) {
+  if (B <= 0 || !z || !target || !pred || !loss || !(lo <= hi)) return LGNN_EINVAL;
+  if (target_is_i64)
+    hipLaunchKernelGGL(k_reg_fwd<int64_t>, dim3(1), dim3(CT), 0, as_stream(stream), z,
+                       static_cast<const int64_t*>(target), B, lo, hi, smooth_l1, pred, loss);
+  else
+    hipLaunchKernelGGL(k_reg_fwd<float>, dim3(1), dim3(CT), 0, as_stream(stream), z,
+                       static_cast<const float*>(target), B, lo, hi, smooth_l1, pred, loss);
+  LGNN_LAUNCH_CHECK();
+  return LGNN_OK;
+}
+
+extern "C" int lgnn_regression_bwd(const float* z, const void* target, int target_is_i64,
+                                   int64_t B, float lo, float hi, int smooth_l1,
+                                   const float* grad_loss, const float* grad_pred, float* dz,
+                                   void* stream) {
+  if (B <= 0 || !z || !target || !dz || (!grad_loss && !grad_pred)) return LGNN_EINVAL;
+  const dim3 grid((unsigned)((B + 255) / 256));
+  if (target_is_i64)
+    hipLaunchKernelGGL(k_reg_bwd<int64_t>, grid, dim3(256), 0, as_stream(stream), z,
+                       static_cast<const int64_t*>(target), B, lo, hi, smooth_l1, grad_loss,
+                       grad_pred, dz);
+  else
+    hipLaunchKernelGGL(k_reg_bwd<float>, grid, dim3(256), 0, as_stream(stream), z,
+                       static_cast<const float*>(target), B, lo, hi, smooth_l1, grad_loss,
+                       grad_pred, dz);
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
 }

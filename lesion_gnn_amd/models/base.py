@@ -72,14 +72,26 @@ class CrossEntropyLoss(nn.Module):
         return ops.cross_entropy(logits, target, self.weight)
 
 
+class RegressionLoss(nn.Module):
+    """nn.MSELoss() / nn.SmoothL1Loss() (mean reduction, reference base.py:95-96) on the HIP
+    regression criterion (ops.regression_loss); BaseModule.training_step runs the regression
+    clamp in the same launch."""
+
+    def __init__(self, kind: str):
+        super().__init__()
+        self.kind = kind
+
+    def forward(self, pred: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+        inf = float("inf")
+        return ops.regression_loss(pred, target, -inf, inf, self.kind)[1]
+
+
 def make_criterion(cfg: OptimizerConfig) -> nn.Module:
     kind = LossType(cfg.loss_type)
     if kind is LossType.CE:
         # reference base.py:93-94 reads the placeholder (unset -> ValueError, as there)
         return CrossEntropyLoss(weight=cfg.class_weights.value)
-    if kind is LossType.MSE:
-        return nn.MSELoss()
-    return nn.SmoothL1Loss()
+    return RegressionLoss(kind.value)
 
 
 class BaseModule(nn.Module):
@@ -101,17 +113,25 @@ class BaseModule(nn.Module):
     def is_regression(self) -> bool:
         return self.loss_type in (LossType.MSE, LossType.SMOOTH_L1)
 
-    def forward(self, data) -> torch.Tensor:
-        """data: object with x, edge_index (or adj_t / a Graph), batch [, num_graphs]."""
+    def _model_logits(self, data) -> torch.Tensor:
         edge_index = getattr(data, "adj_t", None)
         if edge_index is None:
             edge_index = data.edge_index
-        logits = self.model(data.x, edge_index, data.batch, getattr(data, "num_graphs", None))
+        return self.model(data.x, edge_index, data.batch, getattr(data, "num_graphs", None))
+
+    def forward(self, data) -> torch.Tensor:
+        """data: object with x, edge_index (or adj_t / a Graph), batch [, num_graphs]."""
+        logits = self._model_logits(data)
         if self.is_regression:
             logits = torch.clamp(logits.squeeze(1), min=0, max=self.num_classes - 1)
         return logits
 
     def training_step(self, batch, batch_idx: int = 0) -> torch.Tensor:
+        if self.is_regression and isinstance(self.criterion, RegressionLoss):
+            # the clamp (forward) and the criterion in one HIP launch each way; y read as given
+            # (the reference's y.float() happens in the kernel)
+            return ops.regression_loss(self._model_logits(batch), batch.y, 0.0,
+                                       float(self.num_classes - 1), self.criterion.kind)[1]
         logits = self(batch)
         y = batch.y.float() if self.is_regression else batch.y
         return self.criterion(logits, y)

@@ -1642,6 +1642,56 @@ def gat_conv(x, W, att_src, att_dst, bias, graph: Graph, heads: int, slope: floa
 # ----------------------------------------------------------------------------------------------
 
 
+class _Regression(torch.autograd.Function):
+    """The regression head and criterion: pred = clamp(z.squeeze(1), lo, hi) (reference
+    gat.py:94-95 / gin.py:66-67) and loss = nn.MSELoss / nn.SmoothL1Loss (models/base.py:95-96)
+    of (pred, y.float()), in one HIP launch forward (lgnn_regression_fwd) and one backward,
+    instead of torch's clamp / compare / mse / mean / where kernels. Returns (pred, loss)."""
+
+    @staticmethod
+    def forward(ctx, z, y, lo, hi, smooth):
+        _lib.require_gpu(z, y)
+        ctx.needs_reshape = z.dim() == 2
+        z = _f32c(z).reshape(-1)
+        B = z.numel()
+        if y.numel() != B:
+            raise ValueError("regression target must have one value per graph")
+        yi64 = y.dtype == torch.int64
+        yc = y.contiguous() if yi64 else y.to(torch.float32).contiguous()
+        pred = torch.empty(B, dtype=torch.float32, device=z.device)
+        loss = torch.empty((), dtype=torch.float32, device=z.device)
+        _lib.call("lgnn_regression_fwd", _lib.ptr(z), _lib.ptr(yc), int(yi64), B, float(lo),
+                  float(hi), int(smooth), _lib.ptr(pred), _lib.ptr(loss), _s(z.device))
+        ctx.save_for_backward(z, yc)
+        ctx.cfg = (int(yi64), B, float(lo), float(hi), int(smooth))
+        ctx.set_materialize_grads(False)
+        return pred, loss
+
+    @staticmethod
+    def backward(ctx, gpred, gloss):
+        z, yc = ctx.saved_tensors
+        yi64, B, lo, hi, smooth = ctx.cfg
+        dz = torch.empty_like(z)
+        if gpred is None and gloss is None:
+            return None, None, None, None, None
+        _lib.call("lgnn_regression_bwd", _lib.ptr(z), _lib.ptr(yc), yi64, B, lo, hi, smooth,
+                  _lib.ptr(_f32c(gloss) if gloss is not None else None),
+                  _lib.ptr(_f32c(gpred).reshape(-1) if gpred is not None else None),
+                  _lib.ptr(dz), _s(z.device))
+        return dz.view(-1, 1) if ctx.needs_reshape else dz, None, None, None, None
+
+
+def regression_loss(logits: torch.Tensor, y: torch.Tensor, lo: float, hi: float,
+                    kind: str = "MSE"):
+    """(pred, loss): pred = clamp(logits.squeeze(1), lo, hi); loss = MSE or SmoothL1 (beta 1,
+    mean) of (pred, y.float()). lo = -inf, hi = inf: the bare criterion."""
+    if kind not in ("MSE", "SmoothL1"):
+        raise ValueError(kind)
+    if logits.dim() == 2 and logits.size(1) != 1:
+        raise ValueError("regression logits must be [B] or [B, 1]")
+    return _Regression.apply(logits, y, lo, hi, kind == "SmoothL1")
+
+
 class _CrossEntropy(torch.autograd.Function):
     """nn.CrossEntropyLoss(weight) with mean reduction (reference models/base.py:93-94) in two
     HIP kernels (lgnn_ce_fwd / lgnn_ce_bwd) instead of log_softmax + nll_loss + their backward."""
