@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 23
+#define LGNN_ABI_VERSION 24
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -641,6 +641,14 @@ int lgnn_bf16_weight_prep_multi(int n, const float* const* W, const int* N, cons
 int lgnn_bf16_gemm(const void* A, int a_is_f32, int64_t M, int K, const uint16_t* Wb,
                    const float* bias, int N, float* Y, uint16_t* Yb, float* colsum_part,
                    void* stream);
+/* lgnn_bf16_gemm for GATConv.lin's forward with the attention scores in its epilogue (ABI v24):
+ * Y = bf16(A) bf16(W)^T (A bf16, or fp32 rounded as loaded; 64 < K <= 128; no bias;
+ * N = H * C <= 128) and
+ * a_s[m][h] = <Y[m][hC .. hC + C), att_src[h]>, a_d likewise with att_dst (PyG GATConv
+ * alpha_src / alpha_dst, reference gat.py:31), so lgnn_gat_att does not run. */
+int lgnn_bf16_gemm_att(const void* A, int a_is_f32, int64_t M, int K, const uint16_t* Wb, int N,
+                       float* Y, uint16_t* Yb, const float* att_src, const float* att_dst, int H,
+                       int C, float* a_s, float* a_d, void* stream);
 int lgnn_bf16_wgrad_partials(int64_t M, int K);
 int lgnn_bf16_wgrad(const uint16_t* dYb, int N, const void* X, int x_is_f32, int64_t M, int K,
                     float* partials, int num_partials, void* stream);

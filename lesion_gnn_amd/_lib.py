@@ -68,6 +68,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_bn_bwd_stats": (I32, [P, P, P, I64, I32, P, P, P, P, P, P, SZ, P]),
     "lgnn_gat_att": (I32, [P, I64, I32, I32, P, P, P, P, P]),
     "lgnn_bf16_kpad": (I32, [I32]),
+    "lgnn_bf16_gemm_att": (I32, [P, I32, I64, I32, P, I32, P, P, P, P, I32, I32, P, P, P]),
     "lgnn_bf16_weight_prep": (I32, [P, I32, I32, P, P, P]),
     "lgnn_bf16_weight_prep_multi": (I32, [I32, P, P, P, P, P, P]),
     "lgnn_bf16_gemm": (I32, [P, I32, I64, I32, P, P, I32, P, P, P, P]),
@@ -126,7 +127,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 23
+ABI_VERSION = 24
 
 _lib = None
 

@@ -129,13 +129,27 @@ __device__ __forceinline__ void gemm_load_b(u32x4 (&b)[4], Buf bW, int wlane, in
 
 // NCK > 0: exactly NCK chunks (Kp = 64 NCK), the loop fully unrolled — chunks 0 .. NCK - 2 are
 // inside K, only the last tests columns; NCK = 0: any Kp, every chunk tests its columns.
-template <bool AF32, bool VEC, int NCK>
+// GATConv attention scores of the output (ATT): a_s[m][h] = <Y[m][hC .. hC + C), att_src[h]>,
+// a_d likewise (PyG GATConv alpha_src / alpha_dst, reference gat.py:31): the tile's Y values go
+// to LDS and each thread takes (row, head) pairs, so lgnn_gat_att's pass over XP disappears.
+struct AttOut {
+  const float* src;  // [H*C]
+  const float* dst;
+  float* a_s;        // [M][H]
+  float* a_d;
+  int H, C;
+};
+constexpr int YLD = 128 + 4;  // LDS row stride of the staged Y tile (floats)
+
+template <bool AF32, bool VEC, int NCK, bool ATT = false>
 __global__ __launch_bounds__(NT) void k_bf_gemm(const void* __restrict__ A, int64_t M, int K,
                                                 const uint16_t* __restrict__ Wb, int Kp,
                                                 const float* __restrict__ bias, int N,
                                                 float* __restrict__ Y, uint16_t* __restrict__ Yb,
-                                                float* __restrict__ colsum) {
+                                                float* __restrict__ colsum,
+                                                AttOut att = AttOut{}) {
   __shared__ __attribute__((aligned(16))) unsigned char img[2][TM * ROWB];
+  __shared__ __attribute__((aligned(16))) float ytile[ATT ? TM * YLD : 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, li = lane & 31;
   const int64_t r0 = xcd_block() * TM;
@@ -240,6 +254,34 @@ __global__ __launch_bounds__(NT) void k_bf_gemm(const void* __restrict__ A, int6
         __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(pk2(v, 0.f) & 0xffffu), bYb,
                                               (m * N + ncol) * 2, 0, 0);
       }
+  }
+  if constexpr (ATT) {
+    if (nok) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
+          ytile[m * YLD + n] = (q ? acc1[r] : acc0[r]) + bv;
+        }
+    }
+    __syncthreads();
+    const int H = att.H, C = att.C;
+    const int64_t rows = M - r0 < TM ? M - r0 : TM;
+    for (int p = tid; p < TM * H; p += NT) {
+      const int m = p / H, hd = p % H;
+      if (m >= rows) continue;
+      const float* yr = ytile + m * YLD + hd * C;
+      const float* ws = att.src + hd * C;
+      const float* wd = att.dst + hd * C;
+      float ps = 0.f, pd = 0.f;
+      for (int c = 0; c < C; ++c) {
+        ps = fmaf(yr[c], ws[c], ps);
+        pd = fmaf(yr[c], wd[c], pd);
+      }
+      att.a_s[(r0 + m) * H + hd] = ps;
+      att.a_d[(r0 + m) * H + hd] = pd;
+    }
   }
 }
 
@@ -491,6 +533,32 @@ extern "C" int lgnn_bf16_weight_prep_multi(int n, const float* const* W, const i
     jobs.first[j + 1] = jobs.first[j] + (int)std::min<int64_t>((total + 255) / 256, 512);
   }
   hipLaunchKernelGGL(k_bf_wprep_multi, dim3(jobs.first[n]), dim3(256), 0, as_stream(stream), jobs);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? LGNN_OK : (int)e;
+}
+
+extern "C" int lgnn_bf16_gemm_att(const void* A, int a_is_f32, int64_t M, int K,
+                                  const uint16_t* Wb, int N,
+                                  float* Y, uint16_t* Yb, const float* att_src,
+                                  const float* att_dst, int H, int C, float* a_s, float* a_d,
+                                  void* stream) {
+  // the GATConv.lin forward, 64 < K <= 128 (two chunks), with the scores
+  if (M < 0 || K <= BK || K > 2 * BK || K % 4 != 0 || N < 1 || N > 128 || !Wb || !Y)
+    return LGNN_EINVAL;
+  if (H < 1 || C < 1 || H * C != N || !att_src || !att_dst || !a_s || !a_d) return LGNN_EINVAL;
+  if (M > 0 && !A) return LGNN_EINVAL;
+  if ((M + TM) * (int64_t)K * 4 >= ((int64_t)1 << 31) || M * (int64_t)N * 4 >= ((int64_t)1 << 30))
+    return LGNN_EINVAL;
+  if (M == 0) return LGNN_OK;
+  const int Kp = lgnn_bf16_kpad(K);
+  const AttOut att{att_src, att_dst, a_s, a_d, H, C};
+  const dim3 grid((unsigned)((M + TM - 1) / TM));
+  if (a_is_f32)  // rounded to bf16 as loaded, as lgnn_bf16_gemm does
+    hipLaunchKernelGGL((k_bf_gemm<true, true, 2, true>), grid, dim3(NT), 0, as_stream(stream), A,
+                       M, K, Wb, Kp, nullptr, N, Y, Yb, nullptr, att);
+  else
+    hipLaunchKernelGGL((k_bf_gemm<false, true, 2, true>), grid, dim3(NT), 0, as_stream(stream), A,
+                       M, K, Wb, Kp, nullptr, N, Y, Yb, nullptr, att);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? LGNN_OK : (int)e;
 }

@@ -1456,16 +1456,27 @@ class _GATConv(torch.autograd.Function):
             Wg = W.to(torch.bfloat16)
         else:
             xg, Wg = x, W
-        if mfma:
+        a_s = torch.empty(M, heads, dtype=torch.float32, device=dev)
+        a_d = torch.empty(M, heads, dtype=torch.float32, device=dev)
+        scored = False
+        if mfma and GAT_GEMM_ATT and 64 < xg.size(1) <= 128:
+            # the attention scores come out of the lin GEMM's epilogue (no lgnn_gat_att pass)
+            XP = torch.empty(M, HC, dtype=torch.float32, device=dev)
+            xg = xg.contiguous()
+            _lib.call("lgnn_bf16_gemm_att", _lib.ptr(xg), int(xg.dtype == torch.float32), M,
+                      xg.size(1),
+                      _lib.ptr(Wb), HC, _lib.ptr(XP), None, _lib.ptr(att_src), _lib.ptr(att_dst),
+                      heads, C, _lib.ptr(a_s), _lib.ptr(a_d), _s(dev))
+            scored = True
+        elif mfma:
             XP = bf16_gemm(xg, Wb, None, HC)[0]
         elif dense:
             XP = mm_dense(xg, Wg.t(), bf16)
         else:
             XP = linear_fwd(x, W, None, _lib.LGNN_ACT_NONE)
-        a_s = torch.empty(M, heads, dtype=torch.float32, device=dev)
-        a_d = torch.empty(M, heads, dtype=torch.float32, device=dev)
-        _lib.call("lgnn_gat_att", _lib.ptr(XP), M, heads, C, _lib.ptr(att_src), _lib.ptr(att_dst),
-                  _lib.ptr(a_s), _lib.ptr(a_d), _s(dev))
+        if not scored:
+            _lib.call("lgnn_gat_att", _lib.ptr(XP), M, heads, C, _lib.ptr(att_src),
+                      _lib.ptr(att_dst), _lib.ptr(a_s), _lib.ptr(a_d), _s(dev))
         cap = csr.col.numel()
         alpha = torch.empty(cap, heads, dtype=torch.float32, device=dev)
         Y = torch.empty(M, HC, dtype=torch.float32, device=dev)
@@ -1560,6 +1571,8 @@ class _GATConv(torch.autograd.Function):
 # bf16 GAT: the attention kernels write their fp32 outputs' bf16 copies for the following bf16
 # GEMMs (LGNN_BF16_OUT=0: torch casts instead; the values are identical, RNE both ways)
 BF16_OUT = os.environ.get("LGNN_BF16_OUT", "1") != "0"
+# bf16 GATConv.lin forward with the attention scores in its epilogue (lgnn_bf16_gemm_att)
+GAT_GEMM_ATT = os.environ.get("LGNN_GAT_GEMM_ATT", "1") != "0"
 _BF16_COPIES: dict = {}
 
 

@@ -251,3 +251,29 @@ def test_gat_last_conv_readout_fused_bitwise(cuda, monkeypatch, precision, pool,
         want = oref(b.x, b.edge_index, b.batch, b.num_graphs)
         torch.testing.assert_close(res[0][0], want.detach(), rtol=0,
                                    atol=1e-4 * max(1.0, want.abs().max().item()))
+
+
+def test_gat_scores_in_gemm_epilogue(cuda, monkeypatch):
+    """bf16 GAT: the attention scores computed in the lin GEMM's epilogue (lgnn_bf16_gemm_att,
+    an fmaf chain per (row, head) over the staged fp32 Y tile) against lgnn_gat_att (the same
+    products summed as dot4 + butterfly): outputs and gradients within 1e-3 of their scale,
+    the bf16 bar (a last-bit difference in a score can flip a later operand's bf16 rounding,
+    2^-8 relative; test_gat_c3_bf16)."""
+    from lesion_gnn_amd import ops
+
+    b = synth.make_batch(96, k=6, d_in=1025, seed=29, sizes="lognormal", last_channel_class=True)
+    torch.manual_seed(4)
+    m = GAT(1025, [128] * 4, 1, heads=4, dropout=0.0, precision="bf16").to(cuda).train()
+    res = []
+    for on in (True, False):
+        monkeypatch.setattr(ops, "GAT_GEMM_ATT", on)
+        out = m(b.x.to(cuda), b.edge_index.to(cuda), b.batch.to(cuda), b.num_graphs)
+        m.zero_grad(set_to_none=True)
+        out.square().sum().backward()
+        res.append((out.detach().cpu(), {n: p.grad.detach().cpu() for n, p in m.named_parameters()}))
+    torch.testing.assert_close(res[0][0], res[1][0], rtol=0,
+                               atol=1e-3 * max(1.0, res[1][0].abs().max().item()))
+    for n in res[1][1]:
+        torch.testing.assert_close(res[0][1][n], res[1][1][n], rtol=0,
+                                   atol=max(1e-3 * res[1][1][n].abs().max().item(), 1e-8),
+                                   msg=lambda msg: f"{n}: {msg}")
