@@ -62,8 +62,12 @@ __global__ __launch_bounds__(kT) void k_adam(AdamJobs J, float* __restrict__ ste
   }
   if (!advance) return;
   __syncthreads();
+  // The last workgroup to arrive advances the step. No release fence before the ticket: the only
+  // cross-workgroup hazard is step[0] (read at the top, written by the last arrival), and every
+  // workgroup's read of it has returned before its ticket is taken (the loop consumed it). A
+  // device-scope fence here wrote back each XCD's dirty L2 (the parameters and moments this
+  // kernel just updated) once per workgroup.
   if (threadIdx.x == 0) {
-    __threadfence();
     if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
       step[0] = t;
       *ticket = 0u;
