@@ -285,7 +285,11 @@ __device__ __forceinline__ void bwd_tiles(
   // With the BN_GSTATS epilogue the next tile's rows are NOT prefetched into registers (PREF):
   // their 32 VGPRs live across the MFMAs pushed that variant past 256 and spilled ~96 (GIN
   // Lin2 backward under the model-wide node); its rows are loaded at the tile's start instead.
-  constexpr bool PREF = !(GMODE == LGNN_GRAD_TRANSPOSE && BNM == BN_GSTATS);
+#ifndef LGNN_TPREF_ALL
+#define LGNN_TPREF_ALL 0
+#endif
+  constexpr bool PREF =
+      !(GMODE == LGNN_GRAD_TRANSPOSE && (BNM == BN_GSTATS || LGNN_TPREF_ALL));
   f32x4 dr[8];
   IdxRegs R;
   const int64_t tfirst = seek_tile(xcd_block(), ntiles, tmask, want);  // XCD-contiguous tiles
