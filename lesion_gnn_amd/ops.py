@@ -1114,7 +1114,8 @@ class _GINConv(torch.autograd.Function):
 
     @staticmethod
     def _backward_fused(ctx, dH, pool: tuple | None = None, gather: tuple | None = None,
-                        defer_dx: bool = False, reducer: list | None = None):
+                        defer_dx: bool = False, reducer: list | None = None,
+                        extra_red: list | None = None):
         """pool = (dlogits, W_out, graph, mean): the output gradient comes from the pooled readout
         (global pool + out_proj backward folded into Lin2's backward load; dH is None).
         gather = (dS, tself): the output gradient is the next conv's aggregation backward,
@@ -1195,6 +1196,8 @@ class _GINConv(torch.autograd.Function):
         dW1 = torch.empty(N1, K, dtype=torch.float32, device=dev)
         db1 = torch.empty(N1, dtype=torch.float32, device=dev)
         red += [(slab1[:P * N1 * K], P, N1 * K, dW1), (slab1[P * N1 * K:], P, N1, db1)]
+        if extra_red:  # e.g. out_proj's dW / db as outer-product jobs (no k_head_bwd launch)
+            red += extra_red
         if reducer is not None:
             reducer.extend(red)
         else:
@@ -1274,6 +1277,11 @@ class _GINConvHead(torch.autograd.Function):
         return (*g[:7], dWo, dbo) + (None,) * 9
 
 
+# out_proj's dW / db as outer-product jobs of a layer's slab reduction (GIN / GAT model nodes);
+# LGNN_HEAD_JOBS=0: the separate lgnn_pool_head_bwd launch
+HEAD_JOBS = os.environ.get("LGNN_HEAD_JOBS", "1") != "0"
+
+
 class _SubCtx:
     """The per-conv state _GINConv._forward_fused / _backward_fused keep on an autograd ctx,
     for one conv inside the _GINStack node."""
@@ -1328,8 +1336,13 @@ class _GINStack(torch.autograd.Function):
         dev = pooled.device
         dWo = torch.empty(C, D, dtype=torch.float32, device=dev)
         dbo = torch.empty(C, dtype=torch.float32, device=dev)
-        _lib.call("lgnn_pool_head_bwd", _lib.ptr(dlogits), _lib.ptr(pooled), B, D,
-                  _lib.ptr(W_out), C, None, _lib.ptr(dWo), _lib.ptr(dbo), _s(dev))
+        # out_proj's dW = dlogits^T pooled and db = colsum dlogits join the last conv's slab
+        # reductions (outer-product jobs): no k_head_bwd launch
+        head_jobs = [(dlogits, B, C * D, dWo, pooled, D), (dlogits, B, C, dbo)]
+        if not HEAD_JOBS:
+            _lib.call("lgnn_pool_head_bwd", _lib.ptr(dlogits), _lib.ptr(pooled), B, D,
+                      _lib.ptr(W_out), C, None, _lib.ptr(dWo), _lib.ptr(dbo), _s(dev))
+            head_jobs = None
         off = 2
         for sub in ctx.subs:
             sub.saved_tensors = saved[off:off + sub.n_saved]
@@ -1343,7 +1356,8 @@ class _GINStack(torch.autograd.Function):
             sub = ctx.subs[i]
             if i == L - 1:
                 g = _GINConv._backward_fused(sub, None, pool=(dlogits, W_out, ctx.graph,
-                                                               ctx.mean), defer_dx=True)
+                                                               ctx.mean), defer_dx=True,
+                                             extra_red=head_jobs)
             else:
                 g = _GINConv._backward_fused(sub, None, gather=(dS, ctx.in_self[i + 1]),
                                              defer_dx=True)
@@ -1495,9 +1509,10 @@ class _GATConv(torch.autograd.Function):
         return Y
 
     @staticmethod
-    def backward(ctx, dY, pool: tuple | None = None):
+    def backward(ctx, dY, pool: tuple | None = None, extra_red: list | None = None):
         """pool = (dlogits, W_out, graph, mean): the output gradient is formed from the readout's
-        gradient inside the edge kernel (lgnn_gat_bwd_edge_pool; dY is None)."""
+        gradient inside the edge kernel (lgnn_gat_bwd_edge_pool; dY is None). extra_red: more
+        slab / outer-product jobs for this layer's reduction launch."""
         x, W, att_src, att_dst, XP, a_s, a_d, alpha, Y, mask = ctx.saved_tensors[:10]
         csr = ctx.graph.csr("gat")
         M, HC = Y.shape
@@ -1535,7 +1550,7 @@ class _GATConv(torch.autograd.Function):
         if ctx.bf16 and bf16_mfma_fits(HC):
             dg = dXPb if dXPb is not None else dXP.to(torch.bfloat16)
             # the attention partials and lin's dW slabs summed in one launch
-            jobs = [(part, P, 3 * HC, red)]
+            jobs = [(part, P, 3 * HC, red)] + (extra_red or [])
             dW = bf16_wgrad(dg, x, HC, jobs)
             reduce_multi(jobs, dev)
             dx = None
@@ -1552,7 +1567,11 @@ class _GATConv(torch.autograd.Function):
                 else:
                     dx = mm_dense(dg, W.to(torch.bfloat16), True)
         else:
-            _lib.call("lgnn_reduce_partials", _lib.ptr(part), P, 3 * HC, _lib.ptr(red), _s(dev))
+            if extra_red:
+                reduce_multi([(part, P, 3 * HC, red)] + extra_red, dev)
+            else:
+                _lib.call("lgnn_reduce_partials", _lib.ptr(part), P, 3 * HC, _lib.ptr(red),
+                          _s(dev))
             if ctx.dense:
                 # rounded once for both products
                 dg = (dXPb if dXPb is not None else dXP.to(torch.bfloat16)) if ctx.bf16 else dXP
@@ -1597,7 +1616,8 @@ class _GATConvHead(torch.autograd.Function):
     """The GAT model's last GATConv + global pool + out_proj as one autograd node: its backward
     forms the conv's output gradient from dlogits inside the edge kernel (out_proj backward +
     pool backward folded into the load, lgnn_gat_bwd_edge_pool) instead of writing dH
-    (k_pool_bwd); out_proj's dW / db from lgnn_pool_head_bwd. Bitwise the separate nodes."""
+    (k_pool_bwd); out_proj's dW / db are outer-product jobs of the layer's slab reduction.
+    Bitwise the separate nodes except out_proj's dW / db (another fixed summation order)."""
 
     @staticmethod
     def forward(ctx, x, W, att_src, att_dst, bias, W_out, b_out, graph, heads, slope, mask, act,
@@ -1622,12 +1642,17 @@ class _GATConvHead(torch.autograd.Function):
         dev = pooled.device
         dWo = torch.empty(C, D, dtype=torch.float32, device=dev)
         dbo = torch.empty(C, dtype=torch.float32, device=dev)
-        _lib.call("lgnn_pool_head_bwd", _lib.ptr(dlogits), _lib.ptr(pooled), B, D,
-                  _lib.ptr(W_out), C, None, _lib.ptr(dWo), _lib.ptr(dbo), _s(dev))
         sub = ctx.sub
         sub.saved_tensors = saved[:10]
         sub.needs_input_grad = (ctx.needs_input_grad[0],)
-        g = _GATConv.backward(sub, None, pool=(dlogits, W_out, ctx.head_graph, ctx.head_mean))
+        # out_proj's dW / db as outer-product jobs of the layer's reduction (no k_head_bwd)
+        head_jobs = [(dlogits, B, C * D, dWo, pooled, D), (dlogits, B, C, dbo)]
+        if not HEAD_JOBS:
+            _lib.call("lgnn_pool_head_bwd", _lib.ptr(dlogits), _lib.ptr(pooled), B, D,
+                      _lib.ptr(W_out), C, None, _lib.ptr(dWo), _lib.ptr(dbo), _s(dev))
+            head_jobs = None
+        g = _GATConv.backward(sub, None, pool=(dlogits, W_out, ctx.head_graph, ctx.head_mean),
+                              extra_red=head_jobs)
         sub.saved_tensors = ()
         return (*g[:5], dWo, dbo) + (None,) * 7
 
