@@ -412,7 +412,7 @@ __global__ __launch_bounds__(kFinT) void k_finish(int64_t N, int64_t E, int add_
                                                      const float* __restrict__ dis,
                                                      const int32_t* __restrict__ ws_err,
                                                      int32_t* err_out, int32_t* tile_open,
-                                                     int lazy) {
+                                                     int lazy, int32_t* __restrict__ inv) {
   __shared__ int32_t s_key[kFinishCap];
   if (lazy && blockIdx.y == 1 && tile_open[(N + 63) >> 6] == 0) return;  // no source CSR needed
   if (err_out && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *err_out = *ws_err;
@@ -455,7 +455,10 @@ __global__ __launch_bounds__(kFinT) void k_finish(int64_t N, int64_t E, int add_
     for (int j = eb + threadIdx.x; j < ee; j += kFinT) {
       idx[j] = s_val[j - eb];
       key[j] = s_key[j - eb];
+      if (inv && !tr) inv[s_key[j - eb]] = j;  // k_tmap_inv's map, while the keys are at hand
     }
+  } else if (inv && !tr && i < N) {
+    for (int j = ptr[i]; j < ptr[i + 1]; ++j) inv[key[j]] = j;
   }
   if (wt) {
     // row of each entry: binary search is avoided by a per-thread row walk (rows are short)
@@ -490,15 +493,8 @@ __global__ __launch_bounds__(kFinT) void k_finish(int64_t N, int64_t E, int add_
 }
 
 // tmap[q] = position in the target CSR of the edge at source-CSR position q (both CSRs hold the
-// same entries; edge ids are unique: e for edges, E + i for appended loops).
-__global__ __launch_bounds__(kThreads) void k_tmap_inv(const int32_t* __restrict__ rowptr,
-                                                       int64_t N, const int32_t* __restrict__ eid,
-                                                       int32_t* __restrict__ inv) {
-  const int nnz = rowptr[N];
-  for (int p = blockIdx.x * kThreads + threadIdx.x; p < nnz; p += gridDim.x * kThreads)
-    inv[eid[p]] = p;
-}
-
+// same entries; edge ids are unique: e for edges, E + i for appended loops); inv (edge id ->
+// target-CSR position) is written by k_finish's target side.
 __global__ __launch_bounds__(kThreads) void k_tmap(const int32_t* __restrict__ tptr, int64_t N,
                                                    const int32_t* __restrict__ teid,
                                                    const int32_t* __restrict__ inv,
@@ -624,14 +620,13 @@ static int graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loop
     LGNN_LAUNCH_CHECK();
   }
   dim3 fg((unsigned)((N + kFinT - 1) / kFinT), tptr ? 2u : 1u);
+  // with tmap, the target side of k_finish also writes inv (edge id -> target-CSR position)
   hipLaunchKernelGGL(k_finish, fg, dim3(kFinT), 0, s, N, E, add_loop, norm, rowptr, col,
                      ws.eid, w, tptr, tidx, ws.teid, tw, ws.dis, ws.err, err_count, tile_open,
-                     lazy);
+                     lazy, tmap ? ws.inv : nullptr);
   LGNN_LAUNCH_CHECK();
   if (tmap) {
     const int g = grid_for(E + N, 2048);
-    hipLaunchKernelGGL(k_tmap_inv, dim3(g), dim3(kThreads), 0, s, rowptr, N, ws.eid, ws.inv);
-    LGNN_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_tmap, dim3(g), dim3(kThreads), 0, s, tptr, N, ws.teid, ws.inv, tmap);
     LGNN_LAUNCH_CHECK();
   }
