@@ -64,10 +64,31 @@ __device__ __forceinline__ void bst4(Buf r, uint32_t off, f32x4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
 }
 
-// sum over the G = C/4 lanes of a head group (all lanes receive the sum)
+// sum over the G = C/4 lanes of a head group (all lanes receive the sum). Within a 16-lane DPP
+// row the butterfly runs on DPP moves instead of LDS permutes: xor 1 / xor 2 are quad
+// permutations; at the xor-4 (xor-8) stage every lane of a 4 (8)-lane block already holds that
+// block's sum, so the half-row (row) mirror reads a lane of the partner block with the same
+// value the xor partner holds — the same additions in the same order, bitwise.
+#ifndef LGNN_GAT_DPP
+#define LGNN_GAT_DPP 1
+#endif
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
 __device__ __forceinline__ float group_sum(float v, int G) {
+#if LGNN_GAT_DPP
+  if (G >= 2) v += dppf<0xB1>(v);   // quad_perm [1, 0, 3, 2]: lane ^ 1
+  if (G >= 4) v += dppf<0x4E>(v);   // quad_perm [2, 3, 0, 1]: lane ^ 2
+  if (G >= 8) v += dppf<0x141>(v);  // row_half_mirror
+  if (G >= 16) v += dppf<0x140>(v); // row_mirror
+  if (G >= 32) v += __shfl_xor(v, 16, 64);
+  return v;
+#else
   for (int o = 1; o < G; o <<= 1) v += __shfl_xor(v, o, 64);
   return v;
+#endif
 }
 
 __device__ __forceinline__ float dot4(f32x4 a, f32x4 b) {
