@@ -1114,15 +1114,14 @@ class _GINConv(torch.autograd.Function):
 
     @staticmethod
     def _backward_fused(ctx, dH, pool: tuple | None = None, gather: tuple | None = None,
-                        defer_dx: bool = False, reducer: list | None = None,
-                        extra_red: list | None = None):
+                        defer_dx: bool = False, extra_red: list | None = None):
         """pool = (dlogits, W_out, graph, mean): the output gradient comes from the pooled readout
         (global pool + out_proj backward folded into Lin2's backward load; dH is None).
         gather = (dS, tself): the output gradient is the next conv's aggregation backward,
         tself dS + A^T dS, gathered as Lin2's backward loads it (dH is None). defer_dx: return
         this conv's pre-aggregation input gradient (for the previous layer to gather) instead
-        of aggregating it here. reducer: the dW / db slab sums are appended to this job list
-        (one launch for the caller's whole backward) instead of launched here."""
+        of aggregating it here. extra_red: more slab / outer-product jobs for this conv's
+        reduction launch."""
         S, Z1, A1, H, W1, W2, mean, invstd, scale, shift, mask = ctx.saved_tensors[:11]
         csr = ctx.graph.csr("gin")
         M, N1 = Z1.shape
@@ -1198,10 +1197,7 @@ class _GINConv(torch.autograd.Function):
         red += [(slab1[:P * N1 * K], P, N1 * K, dW1), (slab1[P * N1 * K:], P, N1, db1)]
         if extra_red:  # e.g. out_proj's dW / db as outer-product jobs (no k_head_bwd launch)
             red += extra_red
-        if reducer is not None:
-            reducer.extend(red)
-        else:
-            reduce_multi(red, dev)
+        reduce_multi(red, dev)
         dx = None
         if want_dx:
             dx = dxpre if defer_dx else spmm_raw(csr.tptr, csr.tidx, csr.tw, ctx.self_scale,
