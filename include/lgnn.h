@@ -31,6 +31,7 @@ extern "C" {
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
 #define LGNN_ENOSPC (-28)
+#define LGNN_EBUSY (-16) /* a grid-barrier launch cannot have all its workgroups resident */
 
 /* tile flag arrays (tile_open) hold ceil(N/64) + LGNN_TILE_OPEN_EXTRA int32: one flag per 64-node
  * tile, the number of flagged tiles, then six words the fused GCN stack kernels use as grid-barrier
@@ -558,7 +559,14 @@ int lgnn_gcn_stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t*
  *   [C][N_L] (C <= 8) the pooled-output gradient dP = dlogits Wout (out_proj backward) is formed
  *   inside the kernel and dP may be NULL (lgnn_pool_head_bwd then only needs dWout / dbout, and
  *   can run concurrently).
+ * Both _all entries return LGNN_EBUSY (nothing launched) when the device cannot hold every
+ * workgroup of the launch at once (its grid barriers need co-residency): the caller then runs the
+ * open tiles in separate launches. lgnn_fused_grid_capacity(which) = workgroups resident at once
+ * (occupancy per CU x CUs; which 0 = forward, 1 = backward), or an error code (< 0). A barrier
+ * that still times out (~0.5 s) counts itself in the third barrier word (tile_open[ntiles + 3]
+ * forward, [ntiles + 6] backward), which stays set until the next graph build zeroes it.
  * ------------------------------------------------------------------------------------------- */
+int lgnn_fused_grid_capacity(int which);
 int lgnn_gcn_stack_fwd_s3_all(const float* X, int64_t M, int d_in, int has_in_proj,
                               const int32_t* rowptr, const int32_t* col, const float* w, int L,
                               const uint16_t* planes, const float* const* W,

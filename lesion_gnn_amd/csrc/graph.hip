@@ -533,6 +533,7 @@ extern "C" const char* lgnn_status_string(int status) {
     case LGNN_OK: return "ok";
     case LGNN_EINVAL: return "invalid argument";
     case LGNN_ENOSPC: return "workspace too small";
+    case LGNN_EBUSY: return "grid-barrier launch cannot be co-resident";
     default: return status > 0 ? hipGetErrorString((hipError_t)status) : "unknown error";
   }
 }

@@ -64,11 +64,15 @@ __global__ __launch_bounds__(kT) void k_adam(AdamJobs J, float* __restrict__ ste
   __syncthreads();
   // The last workgroup to arrive advances the step. No release fence before the ticket: the only
   // cross-workgroup hazard is step[0] (read at the top, written by the last arrival), and every
-  // workgroup's read of it has returned before its ticket is taken (the loop consumed it). A
+  // workgroup's read of it has returned before its ticket is taken (see `inc` below). A
   // device-scope fence here wrote back each XCD's dirty L2 (the parameters and moments this
   // kernel just updated) once per workgroup.
+  // The ticket's operand depends on t, so this workgroup's read of step[0] has returned before
+  // its ticket is taken even when its loop ran no iteration (a numel-0 tensor): t >= 1 always,
+  // but the compiler cannot drop the dependency.
+  const unsigned int inc = t < 0.f ? 2u : 1u;
   if (threadIdx.x == 0) {
-    if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
+    if (atomicAdd(ticket, inc) == gridDim.x - 1) {
       step[0] = t;
       *ticket = 0u;
       __threadfence();

@@ -445,6 +445,31 @@ extern "C" int lgnn_s3_debug_stamps(unsigned long long* host_out) {
 }
 #endif
 
+hipError_t lgnn_s3_fbwd_occupancy(int* per_cu);  // stack3_bwd.hip
+
+// Workgroups of a fused stack kernel that can be resident on this device at once (occupancy
+// per CU x CU count), cached per device: which = 0 forward (k_s3_fwd<true>), 1 backward
+// (k_s3_fbwd<3, true>). A negative value is a HIP error code.
+extern "C" int lgnn_fused_grid_capacity(int which) {
+  static int cache[2][16];
+  static bool have[2][16];
+  int dev = 0;
+  if (which < 0 || which > 1) return LGNN_EINVAL;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return -(int)hipErrorInvalidDevice;
+  if (have[which][dev]) return cache[which][dev];
+  int cus = 0, per_cu = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return -(int)hipGetLastError();
+  const hipError_t e = which == 0
+      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lgnn_s3::k_s3_fwd<true>,
+                                                     lgnn_tile::NT, 0)
+      : lgnn_s3_fbwd_occupancy(&per_cu);
+  if (e != hipSuccess) return -(int)e;
+  cache[which][dev] = cus * per_cu;
+  have[which][dev] = true;
+  return cache[which][dev];
+}
+
 extern "C" size_t lgnn_weight_planes_bytes(int nl) {
   if (nl < 1 || nl > LGNN_MAX_STACK) return 0;
   return (size_t)nl * 3 * lgnn_s3::PLANE * sizeof(uint16_t);
@@ -530,6 +555,12 @@ static int stack_fwd_s3(const float* X, int64_t M, int d_in, int has_in_proj,
   if (!X) return LGNN_EINVAL;
   const int64_t ntiles = (M + lgnn_tile::TM - 1) / lgnn_tile::TM;
   dim3 grid((unsigned)(ntiles < 512 ? ntiles : 512));
+  // open tiles behind grid barriers need every workgroup resident at once: refuse (the caller
+  // then runs them in separate launches) rather than let a barrier time out
+  if (sync) {
+    const int cap = lgnn_fused_grid_capacity(0);
+    if (cap < (int)grid.x) return cap == LGNN_EINVAL ? cap : cap < 0 ? -cap : LGNN_EBUSY;
+  }
   hipStream_t s = as_stream(stream);
   if (has_in_proj)
     hipLaunchKernelGGL(lgnn_s3::k_s3_fwd<true>, grid, dim3(lgnn_tile::NT), 0, s, X, M, rowptr,

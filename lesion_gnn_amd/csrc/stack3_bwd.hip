@@ -1122,6 +1122,10 @@ static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* g
     return LGNN_OK;
   }
   const dim3 grid((unsigned)num_partials), blk(lgnn_tile::NT);
+  if (o.sync) {  // open tiles behind grid barriers: every workgroup must be resident at once
+    const int cap = lgnn_fused_grid_capacity(1);
+    if (cap < (int)grid.x) return cap == LGNN_EINVAL ? cap : cap < 0 ? -cap : LGNN_EBUSY;
+  }
   if (L == 1 && adjt)
     hipLaunchKernelGGL((lgnn_s3::k_s3_fbwd<2, true>), grid, blk, 0, s, rowptr, col, w, M, a,
                        tile_open, o);
@@ -1136,6 +1140,11 @@ static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* g
                        tile_open, o);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? LGNN_OK : (int)e;
+}
+
+hipError_t lgnn_s3_fbwd_occupancy(int* per_cu) {
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, lgnn_s3::k_s3_fbwd<3, true>,
+                                                      lgnn_tile::NT, 0);
 }
 
 #ifdef LGNN_STAMPS

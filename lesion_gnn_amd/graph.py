@@ -183,6 +183,17 @@ class Graph:
             self._aux[key] = t
         return self._aux[key]
 
+    def barrier_timeouts(self, kind: str = "gcn") -> int:
+        """Grid barriers of the fused stack kernels' open-tile phase that gave up waiting since
+        this graph's build (forward + backward words of tile_open; synchronises). Non-zero means
+        a launch whose workgroups were not all resident: its results are wrong."""
+        c = self._csr.get(kind)
+        if c is None or c.tile_open is None:
+            return 0
+        n = (self.num_nodes + 63) // 64
+        t = c.tile_open
+        return int(t[n + 3].item()) + int(t[n + 6].item())
+
     def dropped_edges(self, kind: str) -> int:
         """Number of edges with an out-of-range index (synchronises)."""
         return int(self.csr(kind).err.item())

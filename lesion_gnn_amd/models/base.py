@@ -137,8 +137,8 @@ class BaseModule(nn.Module):
         return self.criterion(logits, y)
 
     def configure_optimizers(self):
-        """Reference base.py:162-188: the optimizer, plus a torch.optim.lr_scheduler by name
-        (the pl_bolts LinearWarmupCosineAnnealingLR is not available in this build). Adam and
+        """Reference base.py:162-188: the optimizer, plus a torch.optim.lr_scheduler by name or
+        pl_bolts' LinearWarmupCosineAnnealingLR (restated in lesion_gnn_amd.optim). Adam and
         AdamW step in one HIP launch (lesion_gnn_amd.optim, same update as torch's)."""
         from .. import optim as lgnn_optim
 
@@ -151,9 +151,10 @@ class BaseModule(nn.Module):
         sc = self.lr_scheduler_config
         if sc is None:
             return optimizer
-        if sc.name == "LinearWarmupCosineAnnealingLR":
-            raise NotImplementedError("pl_bolts LinearWarmupCosineAnnealingLR is not available")
-        scheduler = getattr(torch.optim.lr_scheduler, sc.name)(optimizer, **sc.kwargs)
+        if sc.name == "LinearWarmupCosineAnnealingLR":  # reference base.py:174-175 (pl_bolts)
+            scheduler = lgnn_optim.LinearWarmupCosineAnnealingLR(optimizer, **sc.kwargs)
+        else:
+            scheduler = getattr(torch.optim.lr_scheduler, sc.name)(optimizer, **sc.kwargs)
         return {"optimizer": optimizer,
                 "lr_scheduler": {"scheduler": scheduler, "monitor": sc.monitor,
                                  "interval": sc.interval, "frequency": sc.frequency}}

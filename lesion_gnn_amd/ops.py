@@ -102,7 +102,37 @@ OPEN_IN_FUSED_BWD = OPEN_IN_FUSED
 HEAD_FOLD = os.environ.get("LGNN_HEAD_FOLD", "1") != "0"
 
 
+_CAPACITY: dict = {}
+
+
+def fused_grid_capacity(direction: str, dev) -> int:
+    """Workgroups of the fused split-3 forward / backward kernel the device holds at once
+    (lgnn_fused_grid_capacity: occupancy per CU x CU count), cached per device."""
+    key = (direction, torch.device(dev).index)
+    cap = _CAPACITY.get(key)
+    if cap is None:
+        with torch.cuda.device(dev):
+            cap = int(_lib.load().lgnn_fused_grid_capacity(0 if direction == "fwd" else 1))
+        if cap < 0:
+            _lib.check(cap, "lgnn_fused_grid_capacity")
+        _CAPACITY[key] = cap
+    return cap
+
+
 def _open_in_fused(mode, graph: Graph, direction: str) -> bool:
+    """Run the open tiles inside the fused launch (behind grid barriers)? Only when every
+    workgroup of that launch can be resident at once (a partitioned or smaller device, or CUs
+    held by other kernels' reservations, refuse it; the C entry refuses it too)."""
+    if not _mode_open_in_fused(mode, graph, direction):
+        return False
+    M = graph.num_nodes
+    ntiles = (M + 63) // 64
+    grid = min(ntiles, 512) if direction == "fwd" else \
+        _lib.load().lgnn_gcn_stack_bwd_partials(M)
+    return grid <= fused_grid_capacity(direction, graph.edge_index.device)
+
+
+def _mode_open_in_fused(mode, graph: Graph, direction: str) -> bool:
     if mode in ("1", True):
         return True
     if mode in ("0", False):

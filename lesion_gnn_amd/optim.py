@@ -10,6 +10,8 @@ No CPU path: parameters and gradients must be contiguous fp32 GPU tensors.
 from __future__ import annotations
 
 import ctypes
+import math
+import warnings
 
 import torch
 
@@ -82,3 +84,39 @@ class AdamW(Adam):
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 1e-2, maximize: bool = False, amsgrad: bool = False):
         super().__init__(params, lr, betas, eps, weight_decay, maximize, amsgrad, decoupled=True)
+
+
+class LinearWarmupCosineAnnealingLR(torch.optim.lr_scheduler.LRScheduler):
+    """pl_bolts.optimizers.lr_scheduler.LinearWarmupCosineAnnealingLR (pl_bolts 0.7.0), the
+    scheduler the reference's configure_optimizers builds by name (models/base.py:174-175; pl_bolts
+    is not installed here). A closed-form schedule per base lr b, epoch e (= last_epoch), warmup
+    w, max m, start s, minimum eta:
+      e < w:  s + e (b - s) / max(1, w - 1)          (linear warmup from s to b)
+      e >= w: eta + (b - eta) (1 + cos(pi (e - w) / (m - w))) / 2   (cosine to eta at e = m)
+    pl_bolts' get_lr() applies the same values recursively (each step from the group's current
+    lr); _get_closed_form_lr() is this formula. This scheduler computes it directly, so its
+    values match pl_bolts' closed form exactly and its recursive form to fp rounding."""
+
+    def __init__(self, optimizer, warmup_epochs: int, max_epochs: int,
+                 warmup_start_lr: float = 0.0, eta_min: float = 0.0, last_epoch: int = -1):
+        self.warmup_epochs = int(warmup_epochs)
+        self.max_epochs = int(max_epochs)
+        self.warmup_start_lr = float(warmup_start_lr)
+        self.eta_min = float(eta_min)
+        super().__init__(optimizer, last_epoch)
+
+    def _closed_form(self, base_lr: float) -> float:
+        e, w, m = self.last_epoch, self.warmup_epochs, self.max_epochs
+        if e < w:
+            return self.warmup_start_lr + e * (base_lr - self.warmup_start_lr) / max(1, w - 1)
+        span = max(1, m - w)
+        return self.eta_min + 0.5 * (base_lr - self.eta_min) * (1 + math.cos(math.pi * (e - w)
+                                                                               / span))
+
+    def get_lr(self):
+        if not getattr(self, "_get_lr_called_within_step", True):
+            warnings.warn("To get the last learning rate computed by the scheduler, please use "
+                          "`get_last_lr()`.", UserWarning)
+        return [self._closed_form(b) for b in self.base_lrs]
+
+    _get_closed_form_lr = get_lr

@@ -179,3 +179,49 @@ def test_cc_pool_out_of_range_raises(cuda):
     cc = torch.tensor([0, 1, 5], device=cuda)
     with pytest.raises(IndexError):
         ops.cc_pool(torch.ones(2, 3, device=cuda), cc, 2, reduce_max=False)
+
+
+@pytest.mark.parametrize("kind", ["MSE", "SmoothL1"])
+def test_drgnet_module_regression_training_step(cuda, kind):
+    """DRGNetModule.training_step for a regression config (the fused clamp + criterion path of
+    BaseModule) must hand data.edge_weight to DRGNet.forward (reference drgnet.py:103, 4th
+    position) through the _model_logits hook: loss and every gradient against the oracle DRGNet
+    with the same GaussianDistance weights, and against the same module without edge weights
+    (which must differ)."""
+    from types import SimpleNamespace
+
+    from lesion_gnn_amd.models import DRGNetModelConfig, OptimizerConfig, get_model
+
+    cfg = DRGNetModelConfig(optimizer=OptimizerConfig(loss_type=kind),
+                            gnn_hidden_dim=8, num_layers=2, sortpool_k=10)
+    cfg.num_classes.value, cfg.input_features.value = 5, 16
+    torch.manual_seed(1234)
+    module = get_model(cfg)
+    with torch.no_grad():
+        for c in module.model.graph_convs:
+            c.lin_rel.weight.mul_(0.25)
+            c.lin_root.weight.mul_(0.25)
+    module = module.to(cuda).eval()  # MLP dropout 0.5 off, as the oracle comparison needs
+    oref = ref.DRGNet(16, 8, 2, 10, 1).eval()
+    oref.load_state_dict({k: v.cpu() for k, v in module.model.state_dict().items()})
+    b = synth.make_batch(20, n=24, k=6, d_in=16, seed=32, sizes="lognormal")
+    ew = ref.gaussian_distance(b.edge_index, b.pos, 0.1).float()
+    assert _key_margin(oref, b, ew, 10) >= 1e-5
+    data = SimpleNamespace(x=b.x.to(cuda), edge_index=b.edge_index.to(cuda),
+                           batch=b.batch.to(cuda), y=b.y.to(cuda), edge_weight=ew.to(cuda),
+                           num_graphs=b.num_graphs)
+    loss = module.training_step(data)
+    loss.backward()
+    want = ref.criterion(kind, oref(b.x, b.edge_index, b.batch, ew, b.num_graphs), b.y, 5)
+    want.backward()
+    torch.testing.assert_close(loss.detach().cpu(), want.detach(), rtol=1e-5, atol=1e-6)
+    for (n1, p1), (n2, p2) in zip(oref.named_parameters(), module.model.named_parameters()):
+        assert n1 == n2
+        s = p1.grad.abs().max().item()
+        torch.testing.assert_close(p2.grad.cpu(), p1.grad, rtol=0, atol=max(1e-4 * s, 1e-6),
+                                   msg=lambda m: f"{n1}: {m}")
+    # the weights matter: without them the loss differs
+    data.edge_weight = None
+    with torch.no_grad():
+        unweighted = module.training_step(data)
+    assert abs(unweighted.item() - loss.item()) > 1e-6

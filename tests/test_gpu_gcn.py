@@ -362,6 +362,7 @@ def test_open_tiles_in_fused_launch(cuda, open_in_fused, monkeypatch):
         words = g.tile_open("gcn_lazy" if ops.LAZY_TRANSPOSE else "gcn").cpu().tolist()
         assert words[nt] > 0  # this batch has open tiles
         assert words[nt + 1:] == [0] * 6, words[nt:]
+        assert g.barrier_timeouts("gcn_lazy" if ops.LAZY_TRANSPOSE else "gcn") == 0
     lr_, _, gr = run_step(oref, b, "cpu")
     for lo, go in results:
         torch.testing.assert_close(lo, lr_, atol=1e-4, rtol=0)
@@ -430,3 +431,24 @@ def test_lazy_transpose_build(cuda, case):
         assert int(full.tptr[-1]) == nnz
         assert torch.equal(full.tidx[:nnz], lazy.tidx[:nnz])
         assert torch.equal(full.tw[:nnz], lazy.tw[:nnz])
+
+
+def test_fused_grid_capacity(cuda):
+    """The open-tile phase of the fused split-3 launches runs behind grid barriers, so every
+    workgroup must be resident: the device's capacity (occupancy x CUs) covers both launches'
+    largest grids on MI355X (forward 512, backward lgnn_gcn_stack_bwd_partials), so
+    _open_in_fused keeps the one-launch path there; a smaller capacity turns it off."""
+    from lesion_gnn_amd import _lib
+    from lesion_gnn_amd.graph import Graph
+
+    fwd = ops.fused_grid_capacity("fwd", cuda)
+    bwd = ops.fused_grid_capacity("bwd", cuda)
+    assert fwd >= 512 and bwd >= _lib.load().lgnn_gcn_stack_bwd_partials(1 << 20), (fwd, bwd)
+    b = synth.make_batch(64, k=8, d_in=128, seed=3)
+    g = Graph(b.edge_index.to(cuda), b.num_nodes, b.batch.to(cuda), b.num_graphs)
+    assert ops._open_in_fused("auto", g, "fwd") and ops._open_in_fused("auto", g, "bwd")
+    ops._CAPACITY[("fwd", torch.device(cuda).index)] = 1
+    try:
+        assert not ops._open_in_fused("auto", g, "fwd")
+    finally:
+        ops._CAPACITY.clear()

@@ -73,3 +73,35 @@ def test_adam_rejects_cpu_and_amsgrad(cuda):
     w.grad = torch.zeros(2)
     with pytest.raises(_lib.LgnnError):
         optim.Adam([w]).step()
+
+
+def test_adam_many_tensors_captured_no_host_sync(cuda):
+    """Many small tensors (three launches of LGNN_MAX_ADAM, so several step readers per step) plus
+    numel-0 tensors — whose workgroups run no loop iteration but still read the step count and
+    take a ticket — replayed from a captured graph 12 times back to back with no host sync in
+    between: the device step counter and every parameter match torch.optim.Adam."""
+    shapes = [(3,), (0,), (17, 5), (1,), (64,), (0, 4), (130,), (2, 2)] * 5
+    p, q = _params(cuda, shapes, 11), _params(cuda, shapes, 11)
+    gen = torch.Generator(device="cpu").manual_seed(2)
+    grads = [torch.randn(s, generator=gen).to(cuda) for s in shapes]
+    for a, b, g in zip(p, q, grads):
+        a.grad, b.grad = g.clone(), g.clone()
+    o = optim.Adam(p, lr=3e-3, betas=(0.85, 0.99), weight_decay=1e-3)
+    r = torch.optim.Adam(q, lr=3e-3, betas=(0.85, 0.99), weight_decay=1e-3, foreach=False)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        o.step()  # warm-up: allocates the state outside capture
+    torch.cuda.current_stream().wait_stream(s)
+    r.step()
+    gph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gph):
+        o.step()
+    for _ in range(12):
+        gph.replay()
+    for _ in range(12):
+        r.step()
+    torch.cuda.synchronize()
+    assert float(o.state[p[0]]["step"]) == 13.0
+    for a, b in zip(p, q):
+        torch.testing.assert_close(a.detach(), b.detach(), rtol=1e-5, atol=1e-7)
