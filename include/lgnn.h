@@ -584,6 +584,29 @@ int lgnn_gcn_stack_bwd_s3f_all(const float* dP, const int64_t* batch, const int3
                                void* stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * Dropout. Replaces: the Bernoulli draws of torch's dropout on the hot path — nn.Dropout between
+ * GIN convs (reference src/lesion_gnn/models/gin.py:27,32), the Dropout of PyG's MLP after each
+ * BatchNorm + ELU (gin.py:23) and GATConv's attention dropout (gat.py:31; PyG 2.5.1
+ * F.dropout(alpha, p) before the aggregation).
+ * lgnn_dropout_masks: num_masks (<= LGNN_MAX_MASKS) fp32 masks in ONE launch; mask j (host arrays:
+ *   out[j] device pointer, 16-B aligned, numel[j] elements, thr[j], scale[j]) holds
+ *     out[j][i] = u(j, i) >= thr[j] ? scale[j] : 0,
+ *     u(j, i) = mix(key + j * 0xD1B54A32D192ED03 + i * G) >> 40,  key = mix(seed ^ counter * G),
+ *   mix = the splitmix64 finalizer, G = 0x9E3779B97F4A7C15, thr = (uint32)(p * 2^24) (<= 2^24),
+ *   scale = fp32(1 / (1 - p)). state: device uint64[4] = [seed, counter, ticket, 0]; with
+ *   advance != 0 the launch increments the counter when done (a captured graph draws fresh masks
+ *   per replay). The masks are a pure function of (seed, counter, j, i): the CPU oracle
+ *   regenerates them bit for bit (parity with dropout on).
+ * lgnn_mask_mul: y = x * mask elementwise (n floats, 16-B aligned; y may alias x) — the dropout
+ *   product and its backward dx = dy * mask.
+ * ------------------------------------------------------------------------------------------- */
+#define LGNN_MAX_MASKS 16
+int lgnn_dropout_masks(int num_masks, float* const* out, const int64_t* numel,
+                       const uint32_t* thr, const float* scale, uint64_t* state, int advance,
+                       void* stream);
+int lgnn_mask_mul(const float* x, const float* mask, float* y, int64_t n, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
  * Sort pooling (DGCNN). Replaces: PyG 2.5.1 SortAggregation(k) as DRGNet applies it to the
  * concatenated GraphConv outputs (reference src/lesion_gnn/models/drgnet.py:37, called at :59).
  *   x [M, D] fp32 (rows of one graph contiguous, PyG Batch order), gptr [B+1] int32 (Batch.ptr);

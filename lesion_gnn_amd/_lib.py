@@ -121,6 +121,8 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_gcn_stack_bwd_s3f_all": (I32, [P, P, P, I32, I64, P, P, P, P, P, P, P, I64, I32, P, P, P,
                                          P, P, P, P, I32, P, P, P, P, I32, P, P]),
     "lgnn_fused_grid_capacity": (I32, [I32]),
+    "lgnn_dropout_masks": (I32, [I32, P, P, P, P, P, I32, P]),
+    "lgnn_mask_mul": (I32, [P, P, P, I64, P]),
     "lgnn_sort_pool_workspace_bytes": (SZ, []),
     "lgnn_sort_pool_fwd": (I32, [P, I64, I32, P, I64, I32, P, P, P, P, SZ, P]),
     "lgnn_sort_pool_bwd": (I32, [P, P, P, P, P, I64, I32, I32, P, P]),

@@ -14,7 +14,7 @@ import math
 import torch
 import torch.nn as nn
 
-from . import _lib, ops
+from . import _lib, dropout, ops
 from .graph import Graph, as_graph
 
 
@@ -96,6 +96,7 @@ class MLP(nn.Module):
                              "gin.py:23 uses [d1, d2, d2])")
         self.channel_list = list(channel_list)
         self.dropout = float(dropout)
+        self._dropout_key = repr(self.dropout)
         self.lins = nn.ModuleList([nn.Linear(a, b) for a, b in
                                    zip(channel_list[:-1], channel_list[1:])])
         self.norms = nn.ModuleList([BatchNorm(channel_list[1])])
@@ -113,27 +114,29 @@ class GINConv(nn.Module):
         self.sync_group = None  # torch.distributed group for SyncBN (None: per-replica stats)
         self.sync_count = None  # fixed global node count under SyncBN (None: all-reduced)
 
-    def forward(self, x: torch.Tensor, edge_index, act: int = _lib.LGNN_ACT_NONE) -> torch.Tensor:
+    def _mask(self, x: torch.Tensor, mask):
+        """The MLP's dropout mask: the model's (drawn with its other masks in one launch), else
+        one drawn here from the device's global generator; None when dropout is inactive."""
+        mlp = self.nn
+        if mask is not None or mlp.dropout == 0.0 or not self.training:
+            return mask if (mlp.dropout > 0.0 and self.training) else None
+        return dropout.masks(dropout.global_state(x.device),
+                             [(x.size(0), mlp.channel_list[1])], dropout.key(mlp, mlp.dropout))[0]
+
+    def forward(self, x: torch.Tensor, edge_index, act: int = _lib.LGNN_ACT_NONE,
+                mask: torch.Tensor | None = None) -> torch.Tensor:
         g = as_graph(edge_index, x.size(0))
         mlp = self.nn
         bn = mlp.norms[0].module
-        mask = None
-        if mlp.dropout > 0.0 and self.training:
-            p = mlp.dropout
-            mask = (torch.rand(x.size(0), mlp.channel_list[1], device=x.device) >= p).float()
-            mask.mul_(1.0 / (1.0 - p))
+        mask = self._mask(x, mask)
         return ops.gin_conv(x, mlp.lins[0].weight, mlp.lins[0].bias, bn, mlp.lins[1].weight,
                             mlp.lins[1].bias, g, self.initial_eps, mask, act, self.sync_group,
                             self.sync_count)
 
-    def stack_spec(self, x: torch.Tensor, act: int) -> dict:
+    def stack_spec(self, x: torch.Tensor, act: int, mask: torch.Tensor | None = None) -> dict:
         """This conv's weights, BatchNorm, eps and dropout mask for ops.gin_stack."""
         mlp = self.nn
-        mask = None
-        if mlp.dropout > 0.0 and self.training:
-            p = mlp.dropout
-            mask = (torch.rand(x.size(0), mlp.channel_list[1], device=x.device) >= p).float()
-            mask.mul_(1.0 / (1.0 - p))
+        mask = self._mask(x, mask)
         return dict(W1=mlp.lins[0].weight, b1=mlp.lins[0].bias, bn=mlp.norms[0].module,
                     W2=mlp.lins[1].weight, b2=mlp.lins[1].bias, eps=self.initial_eps, mask=mask,
                     act=act, group=self.sync_group, sync_count=self.sync_count)
@@ -143,16 +146,13 @@ class GINConv(nn.Module):
         return ops.gin_conv_head_eligible(x, mlp.lins[0].weight, mlp.lins[1].weight)
 
     def forward_head(self, x: torch.Tensor, g, act: int, W_out: torch.Tensor,
-                     b_out: torch.Tensor, mean: bool) -> torch.Tensor:
+                     b_out: torch.Tensor, mean: bool, mask: torch.Tensor | None = None
+                     ) -> torch.Tensor:
         """forward(x) followed by global pool + out_proj (W_out, b_out) in one autograd node
         (ops.gin_conv_head): the model's last conv and readout. Returns the logits."""
         mlp = self.nn
         bn = mlp.norms[0].module
-        mask = None
-        if mlp.dropout > 0.0 and self.training:
-            p = mlp.dropout
-            mask = (torch.rand(x.size(0), mlp.channel_list[1], device=x.device) >= p).float()
-            mask.mul_(1.0 / (1.0 - p))
+        mask = self._mask(x, mask)
         return ops.gin_conv_head(x, mlp.lins[0].weight, mlp.lins[0].bias, bn, mlp.lins[1].weight,
                                  mlp.lins[1].bias, W_out, b_out, g, self.initial_eps, mask, act,
                                  self.sync_group, self.sync_count, mean)
@@ -168,6 +168,7 @@ class GATConv(nn.Module):
         super().__init__()
         self.in_channels, self.out_channels, self.heads = in_channels, out_channels, heads
         self.negative_slope, self.dropout = negative_slope, dropout
+        self._dropout_key = repr(float(dropout))
         self.lin = nn.Linear(in_channels, heads * out_channels, bias=False)
         self.att_src = nn.Parameter(torch.empty(1, heads, out_channels))
         self.att_dst = nn.Parameter(torch.empty(1, heads, out_channels))
@@ -176,26 +177,31 @@ class GATConv(nn.Module):
         glorot_(self.att_src)
         glorot_(self.att_dst)
 
+    def mask_shape(self, g) -> tuple:
+        """The attention-dropout mask: one multiplier per (target-CSR slot, head)."""
+        return (g.csr("gat").col.numel(), self.heads)
+
+    def _mask(self, x: torch.Tensor, g, mask):
+        if self.dropout == 0.0 or not self.training:
+            return None
+        if mask is not None:
+            return mask
+        return dropout.masks(dropout.global_state(x.device), [self.mask_shape(g)],
+                             dropout.key(self, self.dropout))[0]
+
     def forward(self, x: torch.Tensor, edge_index, act: int = _lib.LGNN_ACT_NONE,
-                bf16: bool = False) -> torch.Tensor:
+                bf16: bool = False, mask: torch.Tensor | None = None) -> torch.Tensor:
         g = as_graph(edge_index, x.size(0))
-        mask = None
-        if self.dropout > 0.0 and self.training:
-            cap = g.csr("gat").col.numel()
-            mask = (torch.rand(cap, self.heads, device=x.device) >= self.dropout).float()
-            mask.mul_(1.0 / (1.0 - self.dropout))
+        mask = self._mask(x, g, mask)
         return ops.gat_conv(x, self.lin.weight, self.att_src, self.att_dst, self.bias, g,
                             self.heads, self.negative_slope, mask, act, bf16)
 
     def forward_head(self, x: torch.Tensor, g, act: int, W_out: torch.Tensor,
-                     b_out: torch.Tensor, mean: bool, bf16: bool = False) -> torch.Tensor:
+                     b_out: torch.Tensor, mean: bool, bf16: bool = False,
+                     mask: torch.Tensor | None = None) -> torch.Tensor:
         """forward(x) followed by global pool + out_proj (W_out, b_out) in one autograd node
         (ops.gat_conv_head): the model's last conv and readout. Returns the logits."""
-        mask = None
-        if self.dropout > 0.0 and self.training:
-            cap = g.csr("gat").col.numel()
-            mask = (torch.rand(cap, self.heads, device=x.device) >= self.dropout).float()
-            mask.mul_(1.0 / (1.0 - self.dropout))
+        mask = self._mask(x, g, mask)
         return ops.gat_conv_head(x, self.lin.weight, self.att_src, self.att_dst, self.bias,
                                  W_out, b_out, g, self.heads, self.negative_slope, mask, act,
                                  bf16, mean)

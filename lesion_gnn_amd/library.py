@@ -398,6 +398,55 @@ segment_pool.register_autograd(_segpool_backward, setup_context=_segpool_setup)
 
 
 # ----------------------------------------------------------------------------------------------
+# dropout (lesion_gnn_amd.dropout): masks from the device generator, the mask product
+# ----------------------------------------------------------------------------------------------
+
+
+@custom_op("lgnn::dropout_masks", mutates_args=("state",), device_types="cuda",
+           tags=(torch.Tag.nondeterministic_seeded,))
+def dropout_masks(state: Tensor, numels: list[int], thr: int, scale: float) -> Tensor:
+    """lgnn_dropout_masks: every mask in one flat fp32 tensor (lesion_gnn_amd.dropout layout),
+    the state's counter advanced. Tagged nondeterministic_seeded so the compiler neither merges
+    two calls nor recomputes one in the backward (the backward needs the forward's masks)."""
+    from .dropout import dropout_masks_raw
+
+    return dropout_masks_raw(state, list(numels), thr, scale)
+
+
+@dropout_masks.register_fake
+def _(state, numels, thr, scale):
+    tot = 0
+    for n in numels:
+        tot += (n + 3) // 4 * 4
+    return state.new_empty(tot, dtype=torch.float32)
+
+
+@custom_op("lgnn::mask_mul", mutates_args=(), device_types="cuda")
+def mask_mul(x: Tensor, m: Tensor) -> Tensor:
+    """lgnn_mask_mul: x * m (dropout between convs)."""
+    from .dropout import _mul
+
+    return _mul(x, m)
+
+
+@mask_mul.register_fake
+def _(x, m):
+    return torch.empty_like(x)
+
+
+def _mask_mul_setup(ctx, inputs, output):
+    ctx.save_for_backward(inputs[1])
+
+
+def _mask_mul_backward(ctx, grad):
+    (m,) = ctx.saved_tensors
+    return torch.ops.lgnn.mask_mul(grad, m), None
+
+
+mask_mul.register_autograd(_mask_mul_backward, setup_context=_mask_mul_setup)
+
+
+# ----------------------------------------------------------------------------------------------
 # GATConv
 # ----------------------------------------------------------------------------------------------
 

@@ -17,6 +17,7 @@ import torch
 import torch.nn as nn
 
 from .. import _lib, ops
+from .. import dropout as lgnn_dropout
 from ..conv import GATConv
 from ..graph import as_graph
 from ..utils.placeholder import Placeholder
@@ -49,6 +50,18 @@ class GAT(nn.Module):
         self.st = None
         self.out_proj = nn.Linear(hiddden_channels[-1], num_classes)
         self.pool = pool
+        self.dropout_p = float(dropout)
+        self._dropout_key = repr(self.dropout_p)
+        # the attention-dropout generator (lesion_gnn_amd.dropout; not in state_dict)
+        self.register_buffer("_dropout_rng", lgnn_dropout.new_state(), persistent=False)
+
+    def dropout_masks(self, g) -> list | None:
+        """Every conv's attention-dropout mask of this forward, in one launch (mask l -> conv l);
+        None when dropout is inactive."""
+        if self.dropout_p == 0.0 or not self.training or not len(self.convs):
+            return None
+        return lgnn_dropout.masks(self._dropout_rng, [c.mask_shape(g) for c in self.convs],
+                                  lgnn_dropout.key(self, self.dropout_p))
 
     def forward(self, x: torch.Tensor, edge_index, batch: torch.Tensor,
                 num_graphs: int | None = None) -> torch.Tensor:
@@ -56,15 +69,18 @@ class GAT(nn.Module):
         if self.bf16 and not torch.compiler.is_compiling():
             # every bf16 GEMM's weight operands for this step in one launch
             ops.bf16_prepare_weights([self.in_proj.weight] + [c.lin.weight for c in self.convs])
+        ms = self.dropout_masks(g)
         h = ops.linear_auto(x, self.in_proj.weight, self.in_proj.bias, self.bf16)
         last = len(self.convs) - 1
         for i, conv in enumerate(self.convs):
+            m = ms[i] if ms is not None else None
             if i == last and HEAD_FOLD and not torch.compiler.is_compiling():
                 # last conv + readout as one node: the readout's backward is formed inside the
                 # attention backward's load, no dH tensor
                 return conv.forward_head(h, g, _lib.LGNN_ACT_ELU, self.out_proj.weight,
-                                         self.out_proj.bias, self.pool == "mean", self.bf16)
-            h = conv(h, g, act=_lib.LGNN_ACT_ELU, bf16=self.bf16)
+                                         self.out_proj.bias, self.pool == "mean", self.bf16,
+                                         mask=m)
+            h = conv(h, g, act=_lib.LGNN_ACT_ELU, bf16=self.bf16, mask=m)
         return ops.pool_head(h, self.out_proj.weight, self.out_proj.bias, g, self.pool == "mean")
 
 

@@ -16,6 +16,7 @@ import torch
 import torch.nn as nn
 
 from .. import _lib, ops
+from .. import dropout as lgnn_dropout
 from ..conv import GCNConv
 from ..graph import as_graph
 from ..utils.placeholder import Placeholder
@@ -34,6 +35,9 @@ class GCN(nn.Module):
         self.out_proj = nn.Linear(hidden_channels[-1], num_classes)
         self.dropout = nn.Dropout(dropout)
         self.pool = pool
+        self._dropout_key = repr(float(dropout))
+        # the dropout generator (lesion_gnn_amd.dropout; not in state_dict)
+        self.register_buffer("_dropout_rng", lgnn_dropout.new_state(), persistent=False)
 
     def flat_params(self) -> list[torch.Tensor]:
         ps = [self.in_proj.weight, self.in_proj.bias]
@@ -47,10 +51,13 @@ class GCN(nn.Module):
         mean = self.pool == "mean"
         if self.dropout.p == 0.0 or not self.training:
             return ops.gcn_stack(x, g, self.flat_params(), len(self.convs), mean)
+        # the dropout after each conv (mask l follows conv l), all masks in one launch
+        ms = lgnn_dropout.masks(self._dropout_rng,
+                                [(x.size(0), c.out_channels) for c in self.convs],
+                                lgnn_dropout.key(self, self.dropout.p))
         h = ops.node_linear(x, self.in_proj.weight, self.in_proj.bias)
-        for conv in self.convs:
-            h = conv(h, g, act=_lib.LGNN_ACT_ELU)
-            h = self.dropout(h)
+        for conv, m in zip(self.convs, ms):
+            h = lgnn_dropout.mask_mul(conv(h, g, act=_lib.LGNN_ACT_ELU), m)
         return ops.pool_head(h, self.out_proj.weight, self.out_proj.bias, g, mean)
 
 

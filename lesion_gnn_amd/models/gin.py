@@ -14,9 +14,9 @@ from itertools import pairwise
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from .. import _lib, ops
+from .. import dropout as lgnn_dropout
 from ..conv import MLP, GINConv
 from ..graph import as_graph
 from ..utils.placeholder import Placeholder
@@ -40,6 +40,21 @@ class GIN(nn.Module):
         self.out_proj = nn.Linear(hidden_channels[-1], num_classes)
         self.dropout = nn.Dropout(dropout)
         self.pool = pool
+        self._dropout_key = repr(float(dropout))
+        # the dropout generator (lesion_gnn_amd.dropout; not in state_dict)
+        self.register_buffer("_dropout_rng", lgnn_dropout.new_state(), persistent=False)
+
+    def dropout_masks(self, x: torch.Tensor) -> list | None:
+        """This forward's masks in one launch: conv l's MLP dropout (mask 2l, reference gin.py:23)
+        and the dropout after conv l (mask 2l + 1, gin.py:32); None when dropout is inactive."""
+        if self.dropout.p == 0.0 or not self.training or not len(self.convs):
+            return None
+        M = x.size(0)
+        shapes = []
+        for c in self.convs:
+            shapes += [(M, c.nn.channel_list[1]), (M, c.nn.channel_list[2])]
+        return lgnn_dropout.masks(self._dropout_rng, shapes,
+                                  lgnn_dropout.key(self, self.dropout.p))
 
     def set_sync_bn(self, group, global_count: int | None = None) -> None:
         """SyncBatchNorm over a torch.distributed group (RCCL): BN statistics and their backward
@@ -63,6 +78,7 @@ class GIN(nn.Module):
             convs = [c.stack_spec(x, _lib.LGNN_ACT_ELU) for c in self.convs]
             return ops.gin_stack(x, self.in_proj.weight, self.in_proj.bias, convs,
                                  self.out_proj.weight, self.out_proj.bias, g, self.pool == "mean")
+        ms = self.dropout_masks(x) if drop else None
         h = ops.node_linear(x, self.in_proj.weight, self.in_proj.bias)
         last = len(self.convs) - 1
         for i, conv in enumerate(self.convs):
@@ -70,9 +86,9 @@ class GIN(nn.Module):
                 # last conv + readout as one node: no dH tensor in the backward
                 return conv.forward_head(h, g, _lib.LGNN_ACT_ELU, self.out_proj.weight,
                                          self.out_proj.bias, self.pool == "mean")
-            h = conv(h, g, act=_lib.LGNN_ACT_ELU)
+            h = conv(h, g, act=_lib.LGNN_ACT_ELU, mask=ms[2 * i] if drop else None)
             if drop:
-                h = F.dropout(h, self.dropout.p, True)
+                h = lgnn_dropout.mask_mul(h, ms[2 * i + 1])
         return ops.pool_head(h, self.out_proj.weight, self.out_proj.bias, g, self.pool == "mean")
 
 

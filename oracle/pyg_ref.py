@@ -27,10 +27,62 @@ from __future__ import annotations
 import math
 from itertools import pairwise
 
+import numpy as np
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 from torch import Tensor
+
+# ----------------------------------------------------------------------------------------------
+# dropout masks: the device generator of lgnn_dropout_masks (include/lgnn.h), restated in numpy
+# ----------------------------------------------------------------------------------------------
+
+_GOLD = np.uint64(0x9E3779B97F4A7C15)
+_STREAM = np.uint64(0xD1B54A32D192ED03)
+
+
+def _mix64(z: np.ndarray) -> np.ndarray:
+    """splitmix64 finalizer (uint64 arithmetic wraps mod 2^64 in numpy arrays)."""
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+class DropoutMasks:
+    """The masks one lgnn_dropout_masks launch draws from generator state (seed, counter): mask
+    j (the j-th shape of the launch) element i is scale when its 24 bits u(j, i) >= thr, else 0.
+    The oracle applies them where torch's F.dropout draws its Bernoulli mask (same semantics:
+    keep with probability 1 - p, scale 1 / (1 - p)); the models below take them as `masks`.
+    Test infrastructure: it restates the product's generator so parity can be checked with
+    dropout on; it is not torch's generator (no PyG run could be pinned to it anyway)."""
+
+    def __init__(self, seed: int, counter: int, p: float):
+        with np.errstate(over="ignore"):
+            z = np.array([seed & (2 ** 64 - 1)], dtype=np.uint64) ^ \
+                (np.array([counter & (2 ** 64 - 1)], dtype=np.uint64) * _GOLD)
+            self.key = _mix64(z)[0]
+        self.thr = int(p * 16777216.0)
+        self.scale = np.float32(1.0 / (1.0 - p))
+        self.p = p
+
+    def mask(self, j: int, n: int) -> Tensor:
+        """Elements 0..n-1 of mask j, fp32."""
+        with np.errstate(over="ignore"):
+            i = np.arange(n, dtype=np.uint64)
+            base = (np.array([self.key], dtype=np.uint64)
+                    + np.array([j], dtype=np.uint64) * _STREAM)
+            h = _mix64(base + i * _GOLD)
+        u = (h >> np.uint64(40)).astype(np.int64)
+        return torch.from_numpy(np.where(u >= self.thr, self.scale, np.float32(0.0))
+                                .astype(np.float32))
+
+
+def _dropout(x: Tensor, p: float, training: bool, m: Tensor | None) -> Tensor:
+    """F.dropout, or x * m when the step's device mask m is given (parity runs)."""
+    if m is None or not training or p == 0.0:
+        return F.dropout(x, p=p, training=training)
+    return x * m.view_as(x)
+
 
 # ----------------------------------------------------------------------------------------------
 # scatter helpers (PyG 2.5.1 torch_geometric.utils.scatter on CPU == ATen scatter_add_/reduce_)
@@ -204,12 +256,12 @@ class MLP(nn.Module):
         self.norms = nn.ModuleList([BatchNorm(c) for c in channel_list[1:-1]])
         self.dropout = dropout
 
-    def forward(self, x: Tensor) -> Tensor:
+    def forward(self, x: Tensor, m: Tensor | None = None) -> Tensor:
         for lin, norm in zip(self.lins[:-1], self.norms):
             x = lin(x)
             x = norm(x)
             x = F.elu(x)
-            x = F.dropout(x, p=self.dropout, training=self.training)
+            x = _dropout(x, self.dropout, self.training, m)
         return self.lins[-1](x)
 
 
@@ -221,11 +273,11 @@ class GINConv(nn.Module):
         self.nn = mlp
         self.register_buffer("eps", torch.zeros(1))
 
-    def forward(self, x: Tensor, edge_index: Tensor) -> Tensor:
+    def forward(self, x: Tensor, edge_index: Tensor, m: Tensor | None = None) -> Tensor:
         x_j = x.index_select(0, edge_index[0])
         out = scatter_sum(x_j, edge_index[1], x.size(0))
         out = out + (1 + self.eps) * x
-        return self.nn(out)
+        return self.nn(out, m)
 
 
 def edge_softmax(src: Tensor, index: Tensor, num_nodes: int) -> Tensor:
@@ -281,7 +333,11 @@ class GATConv(nn.Module):
         glorot_(self.att_src)
         glorot_(self.att_dst)
 
-    def forward(self, x: Tensor, edge_index: Tensor) -> Tensor:
+    def forward(self, x: Tensor, edge_index: Tensor, masks: DropoutMasks | None = None,
+                stream: int = 0) -> Tensor:
+        """masks: the step's device masks (parity with dropout on). The device mask of this conv
+        is indexed by target-CSR position (rows by target, edge order within a row, the
+        appended self loop last) x head: the stable sort of this edge list by target."""
         H, C = self.heads, self.out_channels
         n = x.size(0)
         xs = linear(x, self.lin.weight, None, getattr(self, "bf16", False)).view(-1, H, C)
@@ -292,7 +348,12 @@ class GATConv(nn.Module):
         alpha = a_src.index_select(0, src) + a_dst.index_select(0, dst)  # alpha_j + alpha_i
         alpha = F.leaky_relu(alpha, self.negative_slope)
         alpha = edge_softmax(alpha, dst, n)
-        alpha = F.dropout(alpha, p=self.dropout, training=self.training)
+        m = None
+        if masks is not None and self.training and self.dropout > 0.0:
+            perm = torch.sort(dst, stable=True).indices
+            m = torch.empty(alpha.shape)
+            m[perm] = masks.mask(stream, alpha.numel()).view(alpha.shape)
+        alpha = _dropout(alpha, self.dropout, self.training, m)
         msg = alpha.unsqueeze(-1) * xs.index_select(0, src)
         out = scatter_sum(msg, dst, n)
         return out.view(-1, H * C) + self.bias
@@ -329,11 +390,13 @@ class GCN(nn.Module):
         self.dropout = nn.Dropout(dropout)
         self.pool = pool
 
-    def forward(self, x, edge_index, batch, num_graphs=None):
+    def forward(self, x, edge_index, batch, num_graphs=None, masks: DropoutMasks | None = None):
+        """masks: the step's device masks; mask l follows conv l."""
         x = self.in_proj(x)
-        for conv in self.convs:
+        for i, conv in enumerate(self.convs):
             x = F.elu(conv(x, edge_index))
-            x = self.dropout(x)
+            m = masks.mask(i, x.numel()) if masks is not None else None
+            x = _dropout(x, self.dropout.p, self.training, m)
         x = _pool(self.pool)(x, batch, num_graphs)
         return self.out_proj(x)
 
@@ -351,11 +414,16 @@ class GIN(nn.Module):
         self.dropout = nn.Dropout(dropout)
         self.pool = pool
 
-    def forward(self, x, edge_index, batch, num_graphs=None):
+    def forward(self, x, edge_index, batch, num_graphs=None, masks: DropoutMasks | None = None):
+        """masks: the step's device masks; conv l's MLP dropout takes mask 2l, the dropout after
+        conv l (gin.py:32) mask 2l + 1."""
         x = self.in_proj(x)
-        for conv in self.convs:
-            x = F.elu(conv(x, edge_index))
-            x = self.dropout(x)
+        for i, conv in enumerate(self.convs):
+            n = x.size(0) * conv.nn.lins[0].out_features
+            m1 = masks.mask(2 * i, n) if masks is not None else None
+            x = F.elu(conv(x, edge_index, m1))
+            m2 = masks.mask(2 * i + 1, x.numel()) if masks is not None else None
+            x = _dropout(x, self.dropout.p, self.training, m2)
         x = _pool(self.pool)(x, batch, num_graphs)
         return self.out_proj(x)
 
@@ -375,11 +443,12 @@ class GAT(nn.Module):
         self.out_proj = nn.Linear(hiddden_channels[-1], num_classes)
         self.pool = pool
 
-    def forward(self, x, edge_index, batch, num_graphs=None):
+    def forward(self, x, edge_index, batch, num_graphs=None, masks: DropoutMasks | None = None):
+        """masks: the step's device masks; conv l's attention dropout takes mask l."""
         x = linear(x, self.in_proj.weight, self.in_proj.bias, self.bf16)
-        for conv in self.convs:
+        for i, conv in enumerate(self.convs):
             conv.bf16 = self.bf16
-            x = F.elu(conv(x, edge_index))
+            x = F.elu(conv(x, edge_index, masks, i))
         x = _pool(self.pool)(x, batch, num_graphs)
         return self.out_proj(x)
 
