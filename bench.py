@@ -50,6 +50,12 @@ WORKLOADS = {
     "c3f32": dict(model="gat", sizes="lognormal", n=64, k=6, d_in=1025, hidden=[128] * 4,
                   heads=4, classes=5, loss="MSE", pool="mean", last_channel_class=True,
                   desc="C3 in fp32: 3-layer GAT (4 heads), d_in 1025, log-normal N, k=6, MSE"),
+    "refcfg": dict(model="gat", sizes="lognormal", n=64, k=6, d_in=1025, hidden=[128] * 4,
+                   heads=2, classes=5, loss="MSE", pool="mean", last_channel_class=True,
+                   dropout=0.35, compile=True,
+                   desc="reference experiment (configs/config.py:47-65): GAT [128]*4, heads 2, "
+                        "dropout 0.35, torch.compile(dynamic=True), d_in 1025, KNN k=6, MSE, "
+                        "fp32, log-normal N"),
     "c4": dict(model="gin", sizes="fixed", n=64, k=8, d_in=128, hidden=[128, 128, 128],
                classes=5, loss="CE", pool="add",
                desc="C4: GIN + global_add_pool, SyncBN across ranks, fwd+CE+bwd+Adam"),
@@ -164,10 +170,11 @@ def build_model(wl, oracle=False):
 
         mods = {"gcn": models.GCN, "gin": models.GIN, "gat": models.GAT}
     out = 1 if wl["loss"] == "MSE" else wl["classes"]
+    p = wl.get("dropout", 0.0)
     if wl["model"] == "gat":
-        return mods["gat"](wl["d_in"], wl["hidden"], out, heads=wl["heads"], dropout=0.0,
+        return mods["gat"](wl["d_in"], wl["hidden"], out, heads=wl["heads"], dropout=p,
                            precision=wl.get("precision", "fp32"))
-    return mods[wl["model"]](wl["d_in"], wl["hidden"], out, 0.0, pool=wl["pool"])
+    return mods[wl["model"]](wl["d_in"], wl["hidden"], out, p, pool=wl["pool"])
 
 
 def loss_fn(wl, logits, y, oracle=False):
@@ -458,6 +465,9 @@ def main():
     B = args.graphs_per_gpu
     b = make_batch(wl, B, seed=100 + rank).to(dev)
     model = build_model(wl).to(dev)
+    run = model
+    if wl.get("compile"):  # reference gat.py:84: torch.compile(model, dynamic=True)
+        run = torch.compile(model, dynamic=True)
     if world > 1:
         ldist.broadcast_params(model)
         if wl["model"] == "gin":  # SyncBN: full-batch statistics across the ranks
@@ -475,7 +485,7 @@ def main():
     one = torch.ones((), device=dev)  # the loss gradient, allocated once (no fill per step)
 
     def fwd_bwd():
-        loss_fn(wl, model(b.x, b.edge_index, b.batch, B), b.y).backward(one)
+        loss_fn(wl, run(b.x, b.edge_index, b.batch, B), b.y).backward(one)
 
     def exchange():
         if world > 1:  # one flat RCCL all-reduce; equal shards -> weights 1/world

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 24
+#define LGNN_ABI_VERSION 25
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -582,6 +582,36 @@ int lgnn_gcn_stack_bwd_s3f_all(const float* dP, const int64_t* batch, const int3
                                float* dS_ws, int32_t* tile_open, const float* dlogits,
                                const float* Wout, int num_classes, const void* adjt,
                                void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Dense GEMMs at fp32 accuracy on bf16 MFMA ("split-3"), any width. Replace: the plain
+ * nn.Linear shapes outside the 128-feature tile kernels — the reference's fp32 in_proj
+ * nn.Linear(1025, 128) (src/lesion_gnn/models/gat.py:29; configs/config.py:52-65) and every
+ * GATConv.lin / GraphConv / in_proj wider than 128 (scripts/sweep.py:126) — forward and backward,
+ * i.e. the cuBLAS addmm / mm torch runs for them.
+ * Every fp32 operand is held as three bf16 planes x = hi + mid + lo (each the RNE bf16 of what the
+ * planes above left) and a product as the six plane products reaching 2^-24: fp32-class results
+ * (error comparable to an fp32 GEMM's). planes = 1 instead rounds each operand once to bf16 (RNE)
+ * and accumulates in fp32 (the bf16 GEMM mode of BASELINE config C3, any width).
+ * lgnn_s3_weight_planes: the weight operand of lgnn_s3_gemm for B = W [rows][cols] (transposed 0:
+ *   Y = A W^T) or B = W^T (transposed 1: Y = A W), i.e. [ceil(out/128)][planes][128][kpad(in)]
+ *   bf16 in MFMA fragment order, zero-padded; lgnn_s3_weight_planes_numel(out, in, planes) its
+ *   size in elements (out = B's rows, in = B's columns).
+ * lgnn_s3_gemm: Y[M][N] = A[M][K] B[N][K]^T (+ bias[N]), A fp32 (split or rounded as loaded).
+ *   colsum_part (nullable): [ceil(M/64)][N] per-64-row-tile column sums of Y (fixed order).
+ * lgnn_s3_wgrad: partial slabs of dW[N][K] = dY^T X (dY [M][N], X [M][K] fp32, N even):
+ *   partials [num_partials][N][K], num_partials = lgnn_s3_wgrad_partials(M, K, N), summed in fixed
+ *   order by lgnn_reduce_partials(_multi); db_partials (nullable) [num_partials][N] the matching
+ *   column sums of dY (the bias gradient).
+ * ------------------------------------------------------------------------------------------- */
+size_t lgnn_s3_weight_planes_numel(int out_features, int in_features, int planes);
+int lgnn_s3_weight_planes(const float* W, int rows, int cols, int transposed, int planes,
+                          uint16_t* Wp, void* stream);
+int lgnn_s3_gemm(const float* A, int64_t M, int K, const uint16_t* Wp, int N, int planes,
+                 const float* bias, float* Y, float* colsum_part, void* stream);
+int lgnn_s3_wgrad_partials(int64_t M, int K, int N);
+int lgnn_s3_wgrad(const float* dY, int N, const float* X, int64_t M, int K, int planes,
+                  float* partials, int num_partials, float* db_partials, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Dropout. Replaces: the Bernoulli draws of torch's dropout on the hot path — nn.Dropout between

@@ -122,6 +122,11 @@ SIGNATURES: dict[str, tuple] = {
                                          P, P, P, P, I32, P, P, P, P, I32, P, P]),
     "lgnn_fused_grid_capacity": (I32, [I32]),
     "lgnn_dropout_masks": (I32, [I32, P, P, P, P, P, I32, P]),
+    "lgnn_s3_weight_planes_numel": (SZ, [I32, I32, I32]),
+    "lgnn_s3_weight_planes": (I32, [P, I32, I32, I32, I32, P, P]),
+    "lgnn_s3_gemm": (I32, [P, I64, I32, P, I32, I32, P, P, P, P]),
+    "lgnn_s3_wgrad_partials": (I32, [I64, I32, I32]),
+    "lgnn_s3_wgrad": (I32, [P, I32, P, I64, I32, I32, P, I32, P, P]),
     "lgnn_mask_mul": (I32, [P, P, P, I64, P]),
     "lgnn_sort_pool_workspace_bytes": (SZ, []),
     "lgnn_sort_pool_fwd": (I32, [P, I64, I32, P, I64, I32, P, P, P, P, SZ, P]),
@@ -130,7 +135,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 24
+ABI_VERSION = 25
 
 _lib = None
 

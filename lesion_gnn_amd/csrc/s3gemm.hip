@@ -1,0 +1,496 @@
+// Dense GEMMs at fp32 accuracy on bf16 MFMA ("split-3"), any N, any K — the plain nn.Linear
+// shapes outside the fused tile kernels, which the previous rounds sent to the vendor library:
+//   * the reference's own in_proj, nn.Linear(1025, 128) in fp32 (gat.py:29; configs/config.py:
+//     52-65 trains the GAT in fp32 on 1024 encoder channels + the lesion class, lesions.py:142,169)
+//     forward Y = X W^T + b and weight gradient dW = dY^T X,
+//   * every GATConv.lin / GraphConv / in_proj wider than the 128-feature tiles (the sweep's
+//     widths 256 / 512, scripts/sweep.py:126) and its input gradient dX = dY W,
+//   * with PLANES = 1 the same kernels are the bf16-operand GEMMs of the bf16 mode for N > 128.
+//
+// Split-3 (as stack3.hip): every fp32 operand x is three bf16 planes hi + mid + lo (each the RNE
+// bf16 of what the planes above left; residual <= 2^-24 |x|), a product is the six plane
+// products that reach 2^-24 (s3_util.h mfma_s3); bf16 x bf16 products are exact in fp32 and the
+// MFMA accumulates in fp32, so the result has fp32-class error at 16/6 = 2.7x the fp32 MFMA rate.
+// The fp32 A operand (node features / output gradient) is split as it is loaded; the weight
+// operand's planes are written once per step (lgnn_s3_weight_planes) in the MFMA fragment order.
+//
+//   k_s3_gemm   Y[M][N] = A[M][K] B[N][K]^T (+ bias): grid (64-row tiles, 128-column blocks);
+//               4 waves, wave w owns columns 32 w .. + 31 of the block; the A chunk (64 rows x 64
+//               k) goes through three XOR-swizzled LDS planes, double-buffered; the B fragments
+//               come straight from L2 (whole 1-KiB lines per wave load), one chunk ahead.
+//   k_s3_wgrad  dW partial slabs part[s][n][k] = sum over row split s of dY[m][n] X[m][k]: the
+//               transposed images dY^T [n][m] and X^T [k][m] per plane (one buffer: 72 KiB, two
+//               workgroups per CU), the next chunk's rows in registers during the MFMAs; the
+//               slabs are summed in fixed order by lgnn_reduce_partials(_multi) (deterministic).
+#include <algorithm>
+
+#include "common.h"
+#include "s3_util.h"
+
+namespace lgnn_s3g {
+using namespace lgnn_tile;
+using lgnn_s3::bf16x2;
+using lgnn_s3::f32x2;
+using lgnn_s3::lds16;
+using lgnn_s3::mfma16;
+using lgnn_s3::mfma_s3;
+using lgnn_s3::split2;
+using lgnn_s3::Split2;
+using lgnn_s3::u32x2;
+
+constexpr int BK = 64;          // k per chunk
+constexpr int ROWB = BK * 2;    // bytes per image row (bf16)
+constexpr int IMG = TM * ROWB;  // bytes per 64-row image plane
+constexpr int OOB = 0x7ff00000;  // buffer offset past every range: loads return 0
+
+__device__ __forceinline__ int swz(int row, int chunk) {
+  return row * ROWB + ((chunk ^ (row & 7)) << 4);
+}
+__device__ __forceinline__ int opaque(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+__device__ __forceinline__ uint32_t ldb32(Buf b, int off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(b, off, 0, 0);
+}
+__device__ __forceinline__ uint32_t rne16(float v) {  // bf16 bits of v (RNE), low half
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2{v, 0.f}), bf16x2)) & 0xffffu;
+}
+
+// products of one k-step: PLANES = 3 -> the six split-3 products, 1 -> the single bf16 product
+template <int PLANES>
+__device__ __forceinline__ f32x16 mma(const u32x4 (&a)[PLANES], const u32x4 (&b)[PLANES],
+                                      f32x16 c) {
+  if constexpr (PLANES == 3) return mfma_s3(a, b, c);
+  else return mfma16(a[0], b[0], c);
+}
+
+// ------------------------------------------------------------------------------------------
+// Y = A B^T (+ bias)
+// ------------------------------------------------------------------------------------------
+// A registers: rows 16 wave + 4 i + (lane >> 4) (i < 4), k = 4 (lane & 15) + 0..3, fp32.
+struct ARegs {
+  uint32_t v[16];
+};
+
+// One 16-B load per row and lane, branch-free (a join of guarded loads would make the wait-count
+// pass drain every load in flight): a group at or past K reads 0 through an out-of-range offset,
+// and with K % 4 != 0 (!VEC) the group straddling K zeroes its columns >= K after the load (it
+// reads the next row's head, or 0 past the buffer). Rows past M read 0 through the buffer range.
+template <bool VEC>
+__device__ __forceinline__ void load_a(ARegs& R, Buf bA, int K, int c, int rq, int kq) {
+  const int k = c * BK + kq;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int off = (rq + 4 * i) * K + k;
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(bA, opaque(k < K ? off * 4 : OOB), 0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) R.v[4 * i + j] = (VEC || k + j < K) ? v[j] : 0u;
+  }
+}
+
+// the chunk's four fp32 per row -> PLANES bf16 planes (8 B per row and plane)
+template <int PLANES>
+__device__ __forceinline__ void store_a(unsigned char* img, const ARegs& R, int rq, int kq) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int pos = swz(rq + 4 * i, kq >> 3) + ((kq & 7) << 1);
+    const float* f = reinterpret_cast<const float*>(R.v + 4 * i);
+    if constexpr (PLANES == 3) {
+      const Split2 a = split2(f[0], f[1]), b = split2(f[2], f[3]);
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        *reinterpret_cast<u32x2*>(img + p * IMG + pos) = u32x2{a.p[p], b.p[p]};
+    } else {
+      *reinterpret_cast<u32x2*>(img + pos) =
+          u32x2{rne16(f[0]) | (rne16(f[1]) << 16), rne16(f[2]) | (rne16(f[3]) << 16)};
+    }
+  }
+}
+
+// Weight planes in fragment order (as bflin.hip's weight operand): for 128-column block nb,
+// plane p, chunk c, k-step s and wave w, the 64 lanes' 16-B fragments (row 32 w + li, columns
+// 64 c + 16 s + 8 h .. + 7) are 1 KiB contiguous. Plane (nb, p) starts at (nb PLANES + p) 128 Kp.
+template <int PLANES>
+__device__ __forceinline__ void load_b(u32x4 (&b)[4][PLANES], Buf bW, int64_t pstride, int wlane,
+                                       int c) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int p = 0; p < PLANES; ++p)
+      b[s][p] = __builtin_amdgcn_raw_buffer_load_b128(
+          bW, (int)(p * pstride * 2) + ((c * 4 + s) * 4 * 512 + wlane) * 2, 0, 0);
+}
+
+template <int PLANES, bool VEC>
+__global__ __launch_bounds__(NT, 2) void k_s3_gemm(const float* __restrict__ A, int64_t M, int K,
+                                                   const uint16_t* __restrict__ Wp, int Kp,
+                                                   const float* __restrict__ bias, int N,
+                                                   float* __restrict__ Y,
+                                                   float* __restrict__ colsum) {
+  __shared__ __attribute__((aligned(16))) unsigned char img[2][PLANES * IMG];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, li = lane & 31;
+  const int64_t r0 = xcd_block() * TM;
+  const int nb = blockIdx.y;
+  const Buf bA = mkbuf(A + r0 * K, (M - r0) * K * 4);
+  const int64_t pstride = (int64_t)128 * Kp;  // bf16 elements per plane
+  const Buf bW = mkbuf(Wp + nb * PLANES * pstride, PLANES * pstride * 2);
+  const int rq = 16 * wave + (lane >> 4), kq = 4 * (lane & 15);
+  const int nck = Kp / BK;
+  const int wlane = wave * 512 + lane * 8;
+  f32x16 acc0 = {}, acc1 = {};
+  auto ld_a = [&](ARegs& R, int c) { load_a<VEC>(R, bA, K, c, rq, kq); };
+  auto chunk = [&](const unsigned char* im, const u32x4 (&bc)[4][PLANES]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      u32x4 a0[PLANES], a1[PLANES];
+#pragma unroll
+      for (int p = 0; p < PLANES; ++p) {
+        a0[p] = lds16(im + p * IMG + swz(li, 2 * s + h));
+        a1[p] = lds16(im + p * IMG + swz(32 + li, 2 * s + h));
+      }
+      acc0 = mma<PLANES>(a0, bc[s], acc0);
+      acc1 = mma<PLANES>(a1, bc[s], acc1);
+    }
+  };
+  // two register sets ping-pong: chunk c + 1's loads are in flight while chunk c is used
+  ARegs R0, R1;
+  u32x4 b0[4][PLANES], b1[4][PLANES];
+  ld_a(R0, 0);
+  load_b<PLANES>(b0, bW, pstride, wlane, 0);
+  if (nck > 1) {
+    ld_a(R1, 1);
+    load_b<PLANES>(b1, bW, pstride, wlane, 1);
+  }
+  auto step = [&](int c, ARegs& R, u32x4 (&bc)[4][PLANES]) {
+    unsigned char* im = img[c & 1];
+    store_a<PLANES>(im, R, rq, kq);
+    if (c + 2 < nck) ld_a(R, c + 2);
+    lds_barrier();  // image c complete (image c - 2's reads finished before barrier c - 1)
+    chunk(im, bc);
+    if (c + 2 < nck) load_b<PLANES>(bc, bW, pstride, wlane, c + 2);
+  };
+  for (int c = 0; c < nck; c += 2) {
+    step(c, R0, b0);
+    if (c + 1 < nck) step(c + 1, R1, b1);
+  }
+  // epilogue: + bias; fp32 rows as 128-B segments per (row, wave); optional column sums
+  const int n = nb * 128 + 32 * wave + li;
+  const bool nok = n < N;
+  const float bv = (bias && nok) ? bias[n] : 0.f;
+  const Buf bY = mkbuf(Y + r0 * N, (M - r0) * N * 4);
+  const int ncol = nok ? n : OOB / 4;
+  if (colsum) {  // this tile's column sums of Y (rows past M hold 0)
+    float cs = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) cs += acc0[r] + acc1[r];
+    cs += __shfl_xor(cs, 32, 64);
+    const int64_t rows = M - r0 < TM ? M - r0 : TM;
+    if (h == 0 && nok) colsum[(r0 / TM) * N + n] = cs + (float)rows * bv;
+  }
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const float v = (q ? acc1[r] : acc0[r]) + bv;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), bY, (m * N + ncol) * 4, 0, 0);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// dW partial slabs: part[s][n][k] = sum over split s's CPB row chunks of dY[m][n] X[m][k]
+// ------------------------------------------------------------------------------------------
+struct WRegs {
+  float y[16][2];  // dY: columns nb 128 + 2 lane + 0..1 of rows 16 w + 8 g + j (g < 2, j < 8)
+  uint32_t x[16];  // X: k = k0 + 4 (lane & 15) + 0..3 of rows 16 w + 4 (lane >> 4) + i
+};
+
+template <bool FULL>
+__device__ __forceinline__ void wg_load(WRegs& R, Buf bX, Buf bY, int K, int N, int m0, int k0,
+                                        int n0, int lane, int wave) {
+  const int n = n0 + 2 * lane;
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int m = m0 + 16 * wave + 8 * g + j;
+      // N even (checked on the host): the pair is in range or wholly past it
+      const u32x2 v = __builtin_bit_cast(
+          u32x2, __builtin_amdgcn_raw_buffer_load_b64(bY, opaque(n < N ? (m * N + n) * 4 : OOB), 0,
+                                                      0));
+      R.y[8 * g + j][0] = __uint_as_float(v[0]);
+      R.y[8 * g + j][1] = __uint_as_float(v[1]);
+    }
+  const int k = k0 + 4 * (lane & 15);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int off = (m0 + 16 * wave + 4 * (lane >> 4) + i) * K + k;
+    if constexpr (FULL) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(bX, off * 4, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) R.x[4 * i + j] = v[j];
+    } else {  // as load_a: one 16-B load, columns >= K zeroed
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(bX, opaque(k < K ? off * 4 : OOB), 0, 0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) R.x[4 * i + j] = k + j < K ? v[j] : 0u;
+    }
+  }
+}
+
+// image layouts per plane: Y^T [n 0..127][m 0..63], X^T [k 0..63][m 0..63], bf16, swizzled rows
+constexpr int WY = 128 * ROWB;
+constexpr int WX = 64 * ROWB;
+
+template <int PLANES>
+__device__ __forceinline__ void wg_store(unsigned char* iy, unsigned char* ix, const WRegs& R,
+                                         int lane, int wave) {
+  // dY^T: lane's column pair (2 lane, 2 lane + 1), rows 8 ch .. 8 ch + 7 of the chunk -> one 16-B
+  // write per (column, plane)
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int ch = 2 * wave + g;
+    uint32_t lo[PLANES][4], hi[PLANES][4];  // packed (row 2i, row 2i + 1) per column
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float* a = R.y[8 * g + 2 * i];
+      const float* b = R.y[8 * g + 2 * i + 1];
+      if constexpr (PLANES == 3) {
+        const Split2 c0 = split2(a[0], b[0]), c1 = split2(a[1], b[1]);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          lo[p][i] = c0.p[p];
+          hi[p][i] = c1.p[p];
+        }
+      } else {
+        lo[0][i] = rne16(a[0]) | (rne16(b[0]) << 16);
+        hi[0][i] = rne16(a[1]) | (rne16(b[1]) << 16);
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < PLANES; ++p) {
+      *reinterpret_cast<u32x4*>(iy + p * WY + swz(2 * lane, ch)) =
+          u32x4{lo[p][0], lo[p][1], lo[p][2], lo[p][3]};
+      *reinterpret_cast<u32x4*>(iy + p * WY + swz(2 * lane + 1, ch)) =
+          u32x4{hi[p][0], hi[p][1], hi[p][2], hi[p][3]};
+    }
+  }
+  // X^T: column kq + j, rows 16 w + 4 q .. + 3 as one 8-B write per plane
+  const int q = lane >> 4, kq = 4 * (lane & 15);
+  const int ch = 2 * wave + (q >> 1), off = (q & 1) * 8;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float x0 = __uint_as_float(R.x[j]), x1 = __uint_as_float(R.x[4 + j]);
+    const float x2 = __uint_as_float(R.x[8 + j]), x3 = __uint_as_float(R.x[12 + j]);
+    if constexpr (PLANES == 3) {
+      const Split2 a = split2(x0, x1), b = split2(x2, x3);
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        *reinterpret_cast<u32x2*>(ix + p * WX + swz(kq + j, ch) + off) = u32x2{a.p[p], b.p[p]};
+    } else {
+      *reinterpret_cast<u32x2*>(ix + swz(kq + j, ch) + off) =
+          u32x2{rne16(x0) | (rne16(x1) << 16), rne16(x2) | (rne16(x3) << 16)};
+    }
+  }
+}
+
+template <int PLANES, bool FULL>
+__device__ __forceinline__ void wg_run(unsigned char* sm, f32x16& acc0, f32x16& acc1, Buf bX,
+                                       Buf bY, int K, int N, int c0, int cpb, int64_t M, int k0,
+                                       int n0, int lane, int wave, float (&cs)[2]) {
+  const int h = lane >> 5, li = lane & 31;
+  unsigned char* iy = sm;
+  unsigned char* ix = sm + PLANES * WY;
+  const int ncm = (int)((M + TM - 1) / TM);
+  const int cend = std::min(c0 + cpb, ncm);
+  WRegs R;
+  if (c0 < cend) wg_load<FULL>(R, bX, bY, K, N, c0 * TM, k0, n0, lane, wave);
+  for (int c = c0; c < cend; ++c) {
+    if (c > c0) lds_barrier();  // the previous chunk's image reads are done
+    wg_store<PLANES>(iy, ix, R, lane, wave);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {  // the bias gradient's column sums, fixed row order
+      cs[0] += R.y[j][0];
+      cs[1] += R.y[j][1];
+    }
+    if (c + 1 < cend) wg_load<FULL>(R, bX, bY, K, N, (c + 1) * TM, k0, n0, lane, wave);
+    lds_barrier();  // images complete (the next chunk's loads stay in flight)
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      u32x4 a[PLANES], x0[PLANES], x1[PLANES];
+#pragma unroll
+      for (int p = 0; p < PLANES; ++p) {
+        a[p] = lds16(iy + p * WY + swz(32 * wave + li, 2 * st + h));
+        x0[p] = lds16(ix + p * WX + swz(li, 2 * st + h));
+        x1[p] = lds16(ix + p * WX + swz(32 + li, 2 * st + h));
+      }
+      acc0 = mma<PLANES>(a, x0, acc0);
+      acc1 = mma<PLANES>(a, x1, acc1);
+    }
+  }
+}
+
+template <int PLANES>
+__global__ __launch_bounds__(NT, 2) void k_s3_wgrad(const float* __restrict__ dY, int N,
+                                                    const float* __restrict__ X, int64_t M, int K,
+                                                    int nkb, int cpb, float* __restrict__ part,
+                                                    float* __restrict__ dbpart) {
+  __shared__ __attribute__((aligned(16))) unsigned char sm[PLANES * (WY + WX)];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h = lane >> 5, li = lane & 31;
+  const int64_t L = xcd_block();  // the k-blocks of one row split are adjacent: one XCD's L2
+  const int kb = (int)(L % nkb), s = (int)(L / nkb);
+  const int k0 = kb * BK, n0 = blockIdx.y * 128;
+  const Buf bX = mkbuf(X, M * K * 4), bY = mkbuf(dY, M * N * 4);
+  f32x16 acc0 = {}, acc1 = {};
+  float cs[2] = {0.f, 0.f};
+  if (k0 + BK <= K)  // uniform: one body per block
+    wg_run<PLANES, true>(sm, acc0, acc1, bX, bY, K, N, s * cpb, cpb, M, k0, n0, lane, wave, cs);
+  else
+    wg_run<PLANES, false>(sm, acc0, acc1, bX, bY, K, N, s * cpb, cpb, M, k0, n0, lane, wave, cs);
+  if (dbpart && kb == 0) {  // db partial row s: the 4 waves' column sums folded in wave order
+    float* red = reinterpret_cast<float*>(sm);
+    __syncthreads();
+    red[wave * 128 + 2 * lane] = cs[0];
+    red[wave * 128 + 2 * lane + 1] = cs[1];
+    __syncthreads();
+    if (threadIdx.x < 128 && n0 + (int)threadIdx.x < N) {
+      const int t = threadIdx.x;
+      dbpart[(int64_t)s * N + n0 + t] = ((red[t] + red[128 + t]) + red[256 + t]) + red[384 + t];
+    }
+  }
+  // slab s: rows n = n0 + 32 w + (r & 3) + 8 (r >> 2) + 4 h, columns k0 + 32 kk + li
+  float* slab = part + (int64_t)s * N * K;
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int k = k0 + 32 * kk + li;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int n = n0 + 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (n < N && k < K) slab[(int64_t)n * K + k] = kk ? acc1[r] : acc0[r];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// weight planes: Wp[nb][p][128][Kp] of W [N][K] (or of W^T [K][N] with transposed = 1: the
+// operand of dX = dY W), fragment order, zero-padded, PLANES = 3 (split) or 1 (bf16 RNE)
+// ------------------------------------------------------------------------------------------
+__global__ void k_s3_wprep(const float* __restrict__ W, int rows, int cols, int transposed,
+                           int planes, int Kp, int nnb, uint16_t* __restrict__ Wp) {
+  const int64_t per = (int64_t)128 * Kp;  // elements of one plane of one block
+  const int64_t total = per * nnb;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int nb = (int)(i / per);
+    const int64_t j = i % per;
+    const int e = (int)(j & 7), lane = (int)((j >> 3) & 63), wave = (int)((j >> 9) & 3);
+    const int64_t cs = j >> 11;  // 4 chunk + k-step
+    const int r = nb * 128 + 32 * wave + (lane & 31);       // output column (operand row)
+    const int q = (int)(cs * 16) + 8 * (lane >> 5) + e;     // reduction index
+    // operand element (r, q) of B [R][Q]: W[r][q], or W^T: W[q][r]
+    float v = 0.f;
+    if (!transposed) {
+      if (r < rows && q < cols) v = W[(int64_t)r * cols + q];
+    } else {
+      if (r < cols && q < rows) v = W[(int64_t)q * cols + r];
+    }
+    uint16_t* base = Wp + (int64_t)nb * planes * per + j;
+    for (int p = 0; p < planes; ++p) {
+      const uint32_t b = rne16(v);
+      base[p * per] = (uint16_t)b;
+      v -= __uint_as_float(b << 16);
+    }
+  }
+}
+
+}  // namespace lgnn_s3g
+
+using namespace lgnn_s3g;
+
+// ------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------
+extern "C" size_t lgnn_s3_weight_planes_numel(int out_features, int in_features, int planes) {
+  if (out_features < 1 || in_features < 1 || (planes != 1 && planes != 3)) return 0;
+  const int Kp = (in_features + BK - 1) / BK * BK, nnb = (out_features + 127) / 128;
+  return (size_t)nnb * planes * 128 * Kp;
+}
+
+extern "C" int lgnn_s3_weight_planes(const float* W, int rows, int cols, int transposed,
+                                     int planes, uint16_t* Wp, void* stream) {
+  if (!W || !Wp || rows < 1 || cols < 1 || (planes != 1 && planes != 3)) return LGNN_EINVAL;
+  const int out = transposed ? cols : rows, in = transposed ? rows : cols;
+  const int Kp = (in + BK - 1) / BK * BK, nnb = (out + 127) / 128;
+  const int64_t total = (int64_t)128 * Kp * nnb;
+  const int grid = (int)std::min<int64_t>((total + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_s3_wprep, dim3(grid), dim3(256), 0, as_stream(stream), W, rows, cols,
+                     transposed, planes, Kp, nnb, Wp);
+  LGNN_LAUNCH_CHECK();
+  return LGNN_OK;
+}
+
+extern "C" int lgnn_s3_gemm(const float* A, int64_t M, int K, const uint16_t* Wp, int N,
+                            int planes, const float* bias, float* Y, float* colsum_part,
+                            void* stream) {
+  if (M < 0 || K < 1 || N < 1 || !Wp || !Y || (planes != 1 && planes != 3)) return LGNN_EINVAL;
+  if (M > 0 && !A) return LGNN_EINVAL;
+  const int Kp = (K + BK - 1) / BK * BK;
+  // 32-bit buffer offsets: A's tile range, Y's range (a masked column stores at >= 2^31 - 2^20
+  // bytes, past it), and one weight block's planes
+  if ((M + TM) * (int64_t)K * 4 >= ((int64_t)1 << 31) || M * (int64_t)N * 4 >= ((int64_t)1 << 30) ||
+      (int64_t)3 * 128 * Kp * 2 >= ((int64_t)1 << 31))
+    return LGNN_EINVAL;
+  if (M == 0) return LGNN_OK;
+  const dim3 grid((unsigned)((M + TM - 1) / TM), (unsigned)((N + 127) / 128)), block(NT);
+  hipStream_t s = as_stream(stream);
+  const bool v = K % 4 == 0;
+  if (planes == 3) {
+    if (v) hipLaunchKernelGGL((k_s3_gemm<3, true>), grid, block, 0, s, A, M, K, Wp, Kp, bias, N, Y, colsum_part);
+    else hipLaunchKernelGGL((k_s3_gemm<3, false>), grid, block, 0, s, A, M, K, Wp, Kp, bias, N, Y, colsum_part);
+  } else {
+    if (v) hipLaunchKernelGGL((k_s3_gemm<1, true>), grid, block, 0, s, A, M, K, Wp, Kp, bias, N, Y, colsum_part);
+    else hipLaunchKernelGGL((k_s3_gemm<1, false>), grid, block, 0, s, A, M, K, Wp, Kp, bias, N, Y, colsum_part);
+  }
+  LGNN_LAUNCH_CHECK();
+  return LGNN_OK;
+}
+
+// row chunks per split: the smallest power-of-two multiple of 2 keeping the grid within about
+// 2 workgroups per CU (512), at least 2 chunks per split
+static int s3_wg_cpb(int64_t M, int K, int N) {
+  const int64_t nch = std::max<int64_t>((M + TM - 1) / TM, 1);
+  const int64_t work = (int64_t)((K + BK - 1) / BK) * ((N + 127) / 128);
+  for (int cpb = 2; cpb < 256; cpb *= 2)
+    if (work * ((nch + cpb - 1) / cpb) <= 512) return cpb;
+  return 256;
+}
+
+extern "C" int lgnn_s3_wgrad_partials(int64_t M, int K, int N) {
+  if (M < 0 || K < 1 || N < 1) return 0;
+  const int64_t nch = std::max<int64_t>((M + TM - 1) / TM, 1);
+  const int cpb = s3_wg_cpb(M, K, N);
+  return (int)((nch + cpb - 1) / cpb);
+}
+
+extern "C" int lgnn_s3_wgrad(const float* dY, int N, const float* X, int64_t M, int K, int planes,
+                             float* partials, int num_partials, float* db_partials,
+                             void* stream) {
+  if (M < 0 || K < 1 || N < 1 || N % 2 != 0 || !partials || (planes != 1 && planes != 3))
+    return LGNN_EINVAL;
+  if (num_partials != lgnn_s3_wgrad_partials(M, K, N)) return LGNN_EINVAL;
+  if (M > 0 && (!dY || !X)) return LGNN_EINVAL;
+  if ((M + TM) * (int64_t)std::max(K, N) * 4 >= ((int64_t)1 << 31)) return LGNN_EINVAL;
+  const int nkb = (K + BK - 1) / BK, cpb = s3_wg_cpb(M, K, N);
+  const dim3 grid((unsigned)(nkb * num_partials), (unsigned)((N + 127) / 128)), block(NT);
+  hipStream_t s = as_stream(stream);
+  if (planes == 3)
+    hipLaunchKernelGGL((k_s3_wgrad<3>), grid, block, 0, s, dY, N, X, M, K, nkb, cpb, partials,
+                       db_partials);
+  else
+    hipLaunchKernelGGL((k_s3_wgrad<1>), grid, block, 0, s, dY, N, X, M, K, nkb, cpb, partials,
+                       db_partials);
+  LGNN_LAUNCH_CHECK();
+  return LGNN_OK;
+}

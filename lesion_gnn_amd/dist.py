@@ -46,3 +46,39 @@ def broadcast_params(module: torch.nn.Module, src: int = 0, group=None) -> None:
     """Start every replica from rank `src`'s weights."""
     for t in list(module.parameters()) + list(module.buffers()):
         dist.broadcast(t.data, src=src, group=group)
+
+
+class GradBucket:
+    """The flat-gradient exchange split into its device part and its collective, so a training
+    step captured in HIP graphs keeps every copy / scale kernel inside the graphs and only the
+    RCCL call outside them (a collective is never captured):
+      pack()    flat <- concat(grad_i) * local / global   (capturable: end of the backward graph)
+      reduce()  all_reduce(flat, SUM)                      (eager, RCCL over xGMI)
+      unpack()  grad_i <- flat[slice_i]                    (capturable: head of the optimizer graph)
+    The flat buffer is allocated once, so replays of the captured parts reuse it. Equivalent to
+    allreduce_grads (tests/test_distributed.py)."""
+
+    def __init__(self, params: list[torch.nn.Parameter], local_count: int, global_count: int,
+                 group=None):
+        self.params = list(params)
+        self.scale = local_count / global_count
+        self.group = group
+        n = sum(p.numel() for p in self.params)
+        dev = self.params[0].device if self.params else torch.device("cpu")
+        self.flat = torch.empty(n, dtype=torch.float32, device=dev)
+        self.views = []
+        off = 0
+        for p in self.params:
+            self.views.append(self.flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+
+    def pack(self) -> None:
+        torch.cat([p.grad.reshape(-1) for p in self.params], out=self.flat)
+        self.flat.mul_(self.scale)
+
+    def reduce(self) -> None:
+        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+
+    def unpack(self) -> None:
+        for p, v in zip(self.params, self.views):
+            p.grad.copy_(v)

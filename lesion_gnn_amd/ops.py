@@ -486,43 +486,68 @@ def node_linear(x, W, b=None, graph: Graph | None = None, kind: str = "gcn",
     return _NodeLinear.apply(x, W, b, graph, kind, self_scale, act)
 
 
-def mm_dense(a: torch.Tensor, b: torch.Tensor, bf16: bool) -> torch.Tensor:
-    """a @ b in fp32 out: a plain library GEMM (hipBLASLt through torch) — fp32 operands, or
-    bf16-rounded operands with fp32 accumulation and fp32 output (aten::mm.dtype)."""
-    if bf16:
-        return torch.mm(a.to(torch.bfloat16), b.to(torch.bfloat16), out_dtype=torch.float32)
-    return torch.mm(a, b)
+def dense_planes(W: torch.Tensor, transposed: bool, bf16: bool) -> torch.Tensor:
+    """The weight operand of dense_mm for W [rows][cols] (lgnn_s3_weight_planes): B = W
+    (Y = A W^T) or B = W^T (transposed: Y = A W); three bf16 planes (fp32 accuracy) or, in bf16
+    mode, one RNE-rounded plane. One launch; the optimizer updates W in place each step, so the
+    planes are written afresh by every forward / backward that uses them."""
+    W = _f32c(W)
+    rows, cols = W.shape
+    out, inn = (cols, rows) if transposed else (rows, cols)
+    planes = 1 if bf16 else 3
+    n = _lib.load().lgnn_s3_weight_planes_numel(out, inn, planes)
+    Wp = torch.empty(n, dtype=torch.int16, device=W.device)
+    _lib.call("lgnn_s3_weight_planes", _lib.ptr(W), rows, cols, int(transposed), planes,
+              _lib.ptr(Wp), _s(W.device))
+    return Wp
 
 
-def addmm_dense(bias: torch.Tensor, a: torch.Tensor, b: torch.Tensor, bf16: bool) -> torch.Tensor:
-    """bias + a @ b with the bias added in the library GEMM's epilogue (no separate add pass)."""
-    if bf16:
-        return torch.addmm(bias, a.to(torch.bfloat16), b.to(torch.bfloat16),
-                           out_dtype=torch.float32)
-    return torch.addmm(bias, a, b)
+def dense_mm(a: torch.Tensor, Wp: torch.Tensor, N: int, bias, bf16: bool,
+             want_colsum: bool = False) -> torch.Tensor:
+    """Y = a B^T (+ bias) on the split-3 (fp32 accuracy) or bf16-operand MFMA kernel
+    (lgnn_s3_gemm); B's planes from dense_planes. a is fp32 (a bf16 copy is widened: exact)."""
+    a = a.float().contiguous() if a.dtype != torch.float32 else a.contiguous()
+    M, K = a.shape
+    Y = torch.empty(M, N, dtype=torch.float32, device=a.device)
+    cs = torch.empty((M + 63) // 64 * N, dtype=torch.float32, device=a.device) \
+        if want_colsum and M > 0 else None
+    _lib.call("lgnn_s3_gemm", _lib.ptr(a), M, K, _lib.ptr(Wp), N, 1 if bf16 else 3,
+              _lib.ptr(_f32c(bias) if bias is not None else None), _lib.ptr(Y), _lib.ptr(cs),
+              _s(a.device))
+    if cs is not None:
+        _COLSUMS[id(Y)] = (weakref.ref(Y), Y._version, cs)
+        weakref.finalize(Y, _COLSUMS.pop, id(Y), None)
+    return Y
 
 
-def dw_dense(dy: torch.Tensor, x: torch.Tensor, bf16: bool) -> torch.Tensor:
-    """dW = dy^T x over M rows (M >> N, K): split-K — S row chunks as one batched GEMM, then a
-    fixed-order sum over the chunks (deterministic). The library's single GEMM parallelises
-    over the small N x K output only (C3 in_proj, M = 40k: 252 -> 112 us fp32, 181 -> 51 us
-    bf16 on MI355X, tools/gemm_probe.py)."""
-    M = x.size(0)
-    S = 32 if bf16 else 16
-    m = M // S
-    if m < 256:
-        return mm_dense(dy.t(), x, bf16)
-    head = S * m
-    xs, ds = x[:head].view(S, m, -1), dy[:head].view(S, m, -1)
-    if bf16:
-        part = torch.bmm(ds.to(torch.bfloat16).transpose(1, 2), xs.to(torch.bfloat16),
-                         out_dtype=torch.float32)
+def dense_wgrad(dy: torch.Tensor, x: torch.Tensor, bf16: bool, want_db: bool = False,
+                reducer: list | None = None):
+    """(dW, db) = (dy^T x, dy.sum(0)) on lgnn_s3_wgrad: partial slabs over row splits (and the
+    bias gradient's partial rows from the same pass over dy), summed in fixed order by one
+    reduction launch (or appended to `reducer`, the caller's batched reduction)."""
+    dy = dy.float().contiguous() if dy.dtype != torch.float32 else dy.contiguous()
+    x = x.float().contiguous() if x.dtype != torch.float32 else x.contiguous()
+    M, K = x.shape
+    N = dy.size(1)
+    dev = x.device
+    if N % 2:  # the kernel reads dY in column pairs: pad one zero column (exact)
+        dy = torch.nn.functional.pad(dy, (0, 1))
+    Ne = dy.size(1)
+    S = _lib.load().lgnn_s3_wgrad_partials(M, K, Ne)
+    part = torch.empty(S * Ne * K, dtype=torch.float32, device=dev)
+    dbp = torch.empty(S * Ne, dtype=torch.float32, device=dev) if want_db else None
+    _lib.call("lgnn_s3_wgrad", _lib.ptr(dy), Ne, _lib.ptr(x), M, K, 1 if bf16 else 3,
+              _lib.ptr(part), S, _lib.ptr(dbp), _s(dev))
+    dW = torch.empty(Ne, K, dtype=torch.float32, device=dev)
+    db = torch.empty(Ne, dtype=torch.float32, device=dev) if want_db else None
+    jobs = [(part, S, Ne * K, dW)] + ([(dbp, S, Ne, db)] if want_db else [])
+    if reducer is not None:
+        reducer.extend(jobs)
     else:
-        part = torch.bmm(ds.transpose(1, 2), xs)
-    dW = part.sum(0)
-    if head < M:
-        dW += mm_dense(dy[head:].t(), x[head:], bf16)
-    return dW
+        reduce_multi(jobs, dev)
+    if Ne != N:
+        dW, db = dW[:N], (db[:N] if db is not None else None)
+    return dW, db
 
 
 # bf16 GEMMs on the hand-written MFMA kernels (csrc/bflin.hip); LGNN_BF16_MFMA=0 routes them to
@@ -656,9 +681,11 @@ def _bf16_operand(t: torch.Tensor) -> torch.Tensor:
 
 class _DenseLinear(torch.autograd.Function):
     """y = x W^T + b for shapes outside the tile kernels (K > 128, K % 4 != 0: the reference's
-    in_proj with 1025 input channels, gat.py:29 / lesions.py:142,169) or in bf16 mode. A plain
-    GEMM, so it goes to the vendor library (hipBLASLt) rather than a hand-written kernel; the
-    backward is dW = dy^T x, db = colsum dy, dx = dy W in the same precision."""
+    in_proj with 1025 input channels, gat.py:29 / lesions.py:142,169) or in bf16 mode, on the
+    hand-written MFMA GEMMs: bf16 mode with N <= 128 on bflin.hip, everything else on the
+    split-3 kernels of s3gemm.hip (fp32 accuracy; bf16 mode N > 128: one rounded plane). The
+    backward is dW = dy^T x, db = colsum dy (from the same pass), dx = dy W in the same
+    precision."""
 
     @staticmethod
     def forward(ctx, x, W, b, bf16):
@@ -677,9 +704,8 @@ class _DenseLinear(torch.autograd.Function):
             ctx.wt = WTb
             ctx.bf16, ctx.has_b = bf16, b is not None
             return y
-        if bf16:  # each operand rounded once; the backward reuses the bf16 copies
-            x, W = x.to(torch.bfloat16), W.to(torch.bfloat16)
-        y = addmm_dense(_f32c(b), x, W.t(), bf16) if b is not None else mm_dense(x, W.t(), bf16)
+        # split-3 MFMA GEMM at fp32 accuracy (bf16 mode: RNE-rounded operands, N > 128)
+        y = dense_mm(x, dense_planes(W, False, bf16), W.size(0), b, bf16)
         ctx.save_for_backward(x, W)
         ctx.bf16, ctx.has_b = bf16, b is not None
         return y
@@ -694,7 +720,7 @@ class _DenseLinear(torch.autograd.Function):
         db = None
         if ctx.has_b:  # from the column sums dy's producing GEMM wrote, when it was ours
             db = colsum_of(dy, jobs)
-            if db is None:
+            if db is None and mfma:
                 db = dy.sum(0)
         if mfma:
             dyb = _bf16_operand(dy)
@@ -710,12 +736,13 @@ class _DenseLinear(torch.autograd.Function):
                     if dxb is not None:
                         _remember_bf16(dx, dxb)
                 else:
-                    dx = mm_dense(dyb, W.to(torch.bfloat16), True)
+                    dx = dense_mm(dyb, dense_planes(W, True, True), K, None, True)
             return dx, dW, db, None
-        if ctx.bf16:  # dy rounded once for both products
-            dy = dy.to(torch.bfloat16)
-        dW = dw_dense(dy, x, ctx.bf16)
-        dx = mm_dense(dy, W, ctx.bf16) if ctx.needs_input_grad[0] else None
+        dW, db2 = dense_wgrad(dy, x, ctx.bf16, want_db=ctx.has_b and db is None)
+        if db is None and ctx.has_b:
+            db = db2
+        dx = dense_mm(dy, dense_planes(W, True, ctx.bf16), K, None, ctx.bf16) \
+            if ctx.needs_input_grad[0] else None
         return dx, dW, db, None
 
 
@@ -1489,12 +1516,7 @@ class _GATConv(torch.autograd.Function):
             xb = _bf16_copy_of(x)
             xg, Wg = (xb if xb is not None else x), W
             Wb, ctx.wt = bf16_weight_operands(W, True)
-        elif bf16:  # GEMM operands rounded once; the backward reuses the bf16 copies
-            xg = _bf16_copy_of(x)  # the previous GAT layer may have written it already
-            if xg is None:
-                xg = x.to(torch.bfloat16)
-            Wg = W.to(torch.bfloat16)
-        else:
+        else:  # fp32, or bf16 wider than 128: the operands are split / rounded in the GEMMs
             xg, Wg = x, W
         a_s = torch.empty(M, heads, dtype=torch.float32, device=dev)
         a_d = torch.empty(M, heads, dtype=torch.float32, device=dev)
@@ -1510,8 +1532,8 @@ class _GATConv(torch.autograd.Function):
             scored = True
         elif mfma:
             XP = bf16_gemm(xg, Wb, None, HC)[0]
-        elif dense:
-            XP = mm_dense(xg, Wg.t(), bf16)
+        elif dense:  # split-3 MFMA GEMM (fp32 accuracy), or one rounded plane in bf16 mode
+            XP = dense_mm(xg, dense_planes(Wg, False, bf16), HC, None, bf16)
         else:
             XP = linear_fwd(x, W, None, _lib.LGNN_ACT_NONE)
         if not scored:
@@ -1563,9 +1585,9 @@ class _GATConv(torch.autograd.Function):
         P = _lib.load().lgnn_gat_bwd_num_partials(M)
         part = torch.empty(P * 3 * HC, dtype=torch.float32, device=dev)
         dXP = torch.empty_like(XP)
-        # bf16 dense lin: the kernel also writes dXP in bf16 (the GEMMs' operand, no cast pass)
+        # bf16 MFMA lin: the kernel also writes dXP in bf16 (the GEMMs' operand, no cast pass)
         dXPb = torch.empty(M, HC, dtype=torch.bfloat16, device=dev) \
-            if ctx.dense and ctx.bf16 and BF16_OUT else None
+            if ctx.bf16 and bf16_mfma_fits(HC) and BF16_OUT else None
         _lib.call("lgnn_gat_bwd_node", _lib.ptr(csr.tptr), _lib.ptr(csr.tidx),
                   _lib.ptr(csr.tmap), _lib.ptr(alpha), _lib.ptr(mask), _lib.ptr(da_e),
                   _lib.ptr(da_d), _lib.ptr(dZ), _lib.ptr(XP), _lib.ptr(att_src),
@@ -1591,18 +1613,17 @@ class _GATConv(torch.autograd.Function):
                     if dxb is not None:
                         _remember_bf16(dx, dxb)
                 else:
-                    dx = mm_dense(dg, W.to(torch.bfloat16), True)
+                    dx = dense_mm(dg, dense_planes(W, True, True), K, None, True)
         else:
             if extra_red:
                 reduce_multi([(part, P, 3 * HC, red)] + extra_red, dev)
             else:
                 _lib.call("lgnn_reduce_partials", _lib.ptr(part), P, 3 * HC, _lib.ptr(red),
                           _s(dev))
-            if ctx.dense:
-                # rounded once for both products
-                dg = (dXPb if dXPb is not None else dXP.to(torch.bfloat16)) if ctx.bf16 else dXP
-                dW = dw_dense(dg, x, ctx.bf16)
-                dx = mm_dense(dg, W, ctx.bf16) if want_dx else None
+            if ctx.dense:  # split-3 (or bf16-rounded) MFMA GEMMs on the fp32 dXP
+                dW = dense_wgrad(dXP, x, ctx.bf16)[0]
+                dx = dense_mm(dXP, dense_planes(W, True, ctx.bf16), W.size(1), None, ctx.bf16) \
+                    if want_dx else None
             else:
                 dx, dW, _ = linear_bwd(_lib.LGNN_GRAD_DIRECT, dXP, H=None,
                                        act=_lib.LGNN_ACT_NONE, X=x, W=W, want_dx=want_dx,

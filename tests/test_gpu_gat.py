@@ -236,9 +236,10 @@ def test_gat_last_conv_readout_fused_bitwise(cuda, monkeypatch, precision, pool,
     m = GAT(64, [128] * 4, 1, heads=4, dropout=dropout, precision=precision,
             pool=pool).to(cuda).train()
     res = []
+    rng = m._dropout_rng.clone()  # both runs draw the same device dropout masks
     for fold in (True, False):
         monkeypatch.setattr(gat_mod, "HEAD_FOLD", fold)
-        torch.manual_seed(13)
+        m._dropout_rng.copy_(rng)
         out = m(b.x.to(cuda), b.edge_index.to(cuda), b.batch.to(cuda), b.num_graphs)
         m.zero_grad(set_to_none=True)
         out.square().sum().backward()
