@@ -452,6 +452,65 @@ def dry_run(args, wl, world, rank):
         raise SystemExit("bench.py --dry-run: all-reduce result wrong")
 
 
+def step_plan(world: int, capture: bool, collectives_in_fwd: bool) -> tuple:
+    """How one training step runs (no collective is ever inside a captured HIP graph):
+      ("eager",)                                   --graph 0, or SyncBN at N > 1 (its RCCL
+                                                   all-reduces sit inside forward and backward)
+      ("graph:step",)                              N = 1: forward + backward + Adam, one graph
+      ("graph:fwd_bwd+pack", "rccl", "graph:unpack+opt")   N > 1: the gradient bucket is packed
+                                                   (and scaled) at the end of the first graph and
+                                                   unpacked at the head of the second; only the
+                                                   flat RCCL all-reduce runs between them."""
+    if not capture or (world > 1 and collectives_in_fwd):
+        return ("eager",)
+    if world == 1:
+        return ("graph:step",)
+    return ("graph:fwd_bwd+pack", "rccl", "graph:unpack+opt")
+
+
+def make_step(plan: tuple, fwd_bwd, bucket, opt, dev):
+    """The step callable for `plan` (step_plan). Graph plans warm up eagerly on a side stream,
+    then capture; the eager plan zeroes the gradients, runs forward + backward, exchanges the
+    flat gradient (N > 1) and steps the optimizer."""
+    def eager_step():
+        opt.zero_grad(set_to_none=True)
+        fwd_bwd()
+        if bucket is not None:
+            bucket.pack()
+            bucket.reduce()
+            bucket.unpack()
+        opt.step()
+
+    if plan == ("eager",):
+        return eager_step
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            eager_step()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    opt.zero_grad(set_to_none=True)
+    if plan == ("graph:step",):
+        g_step = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_step):
+            fwd_bwd()
+            opt.step()
+        return g_step.replay
+    g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g_fb):
+        fwd_bwd()
+        bucket.pack()
+    with torch.cuda.graph(g_opt):
+        bucket.unpack()
+        opt.step()
+
+    def step():
+        g_fb.replay()
+        bucket.reduce()  # RCCL stays outside the captured graphs
+        g_opt.replay()
+    return step
+
+
 def main():
     args = parse()
     wl = WORKLOADS[args.workload]
@@ -487,45 +546,10 @@ def main():
     def fwd_bwd():
         loss_fn(wl, run(b.x, b.edge_index, b.batch, B), b.y).backward(one)
 
-    def exchange():
-        if world > 1:  # one flat RCCL all-reduce; equal shards -> weights 1/world
-            ldist.allreduce_grads(params, B, B * world)
-
-    def eager_step():
-        opt.zero_grad(set_to_none=True)
-        fwd_bwd()
-        exchange()
-        opt.step()
-
-    step = eager_step
-    if args.graph:
-        side = torch.cuda.Stream(dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):
-            for _ in range(3):
-                eager_step()
-        torch.cuda.current_stream(dev).wait_stream(side)
-        opt.zero_grad(set_to_none=True)
-        if world == 1:  # nothing between backward and optimizer: one graph for the whole step
-            g_step = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g_step):
-                fwd_bwd()
-                opt.step()
-
-            def step():
-                g_step.replay()
-        else:
-            g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g_fb):
-                fwd_bwd()
-            with torch.cuda.graph(g_opt):
-                opt.step()
-
-            def step():
-                g_fb.replay()
-                exchange()  # RCCL stays outside the captured graphs
-                g_opt.replay()
-
+    # GIN under SyncBN all-reduces inside its forward and backward (RCCL collectives)
+    plan = step_plan(world, bool(args.graph), world > 1 and wl["model"] == "gin")
+    bucket = ldist.GradBucket(params, B, B * world) if world > 1 else None
+    step = make_step(plan, fwd_bwd, bucket, opt, dev)
     for _ in range(args.warmup):
         step()
     if world > 1:
@@ -552,7 +576,7 @@ def main():
         "dtype": "bf16 GEMM operands, f32 accumulate" if wl.get("precision") == "bf16" else "f32",
         "data": "synthetic k-NN lesion graphs (pos~U[0,1)^2, x~N(0,1)), random-init weights",
         "config": {"workload": wl["desc"], "name": args.workload,
-                   "step_launch": "hip_graph_replay" if args.graph else "eager",
+                   "step_launch": " | ".join(plan),
                    "adam": args.opt, "graphs_per_gpu": B, "global_batch": B * world,
                    "nodes": b.num_nodes, "edges": b.num_edges, "k": wl["k"], "d_in": wl["d_in"],
                    "hidden": wl["hidden"], "parallelism": f"dp{world}"},

@@ -81,3 +81,108 @@ def test_shard_bounds_balance_edges():
     assert b[0] == 0 and b[-1] == 8 and b == sorted(b)
     assert ldist.shard_bounds([5] * 8, 4) == [0, 2, 4, 6, 8]
     assert ldist.shard_bounds([], 3) == [0, 0, 0, 0]
+
+
+def test_bench_step_plan():
+    """bench.py's step structure: a collective is never inside a captured graph — SyncBN (GIN,
+    C4) at N > 1 runs eagerly (its all-reduces sit inside forward and backward); otherwise the
+    flat-gradient RCCL all-reduce is the only eager part between two graphs."""
+    import bench
+
+    assert bench.step_plan(1, True, False) == ("graph:step",)
+    assert bench.step_plan(1, True, True) == ("graph:step",)  # one rank: SyncBN is local
+    assert bench.step_plan(2, True, False) == ("graph:fwd_bwd+pack", "rccl", "graph:unpack+opt")
+    assert bench.step_plan(8, True, True) == ("eager",)
+    assert bench.step_plan(4, False, False) == ("eager",)
+
+
+class _SyncNormNet(torch.nn.Module):
+    """A SyncBN-shaped CPU model: the forward normalises with batch statistics all-reduced over
+    the group (autograd through the all-reduce, as SyncBN's backward all-reduces too)."""
+
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(5)
+        self.lin = torch.nn.Linear(6, 4)
+        self.out = torch.nn.Linear(4, 3)
+
+    def forward(self, x, world):
+        z = self.lin(x)
+        s = torch.stack([z.sum(0), (z * z).sum(0)])
+        n = torch.tensor(float(x.size(0)))
+        if world > 1:
+            import torch.distributed.nn.functional as dnf
+
+            s = dnf.all_reduce(s)
+            n = n * world
+        mean = s[0] / n
+        var = s[1] / n - mean * mean
+        return self.out(torch.nn.functional.elu((z - mean) / torch.sqrt(var + 1e-5)))
+
+
+def _plan_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    import bench
+
+    g = torch.Generator().manual_seed(0)
+    X, Y = torch.randn(16, 6, generator=g), torch.randint(0, 3, (16,), generator=g)
+    x, y = X[8 * rank:8 * rank + 8], Y[8 * rank:8 * rank + 8]
+    m = _SyncNormNet()
+    ldist.broadcast_params(m)
+    params = list(m.parameters())
+    opt = torch.optim.SGD(params, lr=0.1)
+    bucket = ldist.GradBucket(params, 8, 16)
+
+    def fwd_bwd():
+        torch.nn.functional.cross_entropy(m(x, world), y).backward()
+
+    plan = bench.step_plan(world, True, True)
+    step = bench.make_step(plan, fwd_bwd, bucket, opt, torch.device("cpu"))
+    for _ in range(3):
+        step()
+    # the bucket exchange equals allreduce_grads on the same gradients
+    opt.zero_grad(set_to_none=True)
+    fwd_bwd()
+    ref_grads = [p.grad.clone() for p in params]
+    bucket.pack()
+    bucket.reduce()
+    bucket.unpack()
+    via_bucket = [p.grad.clone() for p in params]
+    for p, g0 in zip(params, ref_grads):
+        p.grad = g0
+    ldist.allreduce_grads(params, 8, 16)
+    same = all(torch.allclose(a, p.grad, atol=1e-7) for a, p in zip(via_bucket, params))
+    if rank == 0:
+        out.put(({k: v.detach().numpy().copy() for k, v in m.state_dict().items()}, same, plan))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_syncbn_step_plan_two_ranks_matches_full_batch():
+    """bench.py's N > 1 step for a model with collectives inside forward / backward (the C4 GIN
+    + SyncBN structure), world size 2 on gloo: three steps of the plan bench would run leave the
+    same weights as three full-batch single-process steps; the GradBucket exchange equals the
+    flat all-reduce."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_plan_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    state, same, plan = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert plan == ("eager",) and same
+    g = torch.Generator().manual_seed(0)
+    X, Y = torch.randn(16, 6, generator=g), torch.randint(0, 3, (16,), generator=g)
+    m = _SyncNormNet()
+    opt = torch.optim.SGD(m.parameters(), lr=0.1)
+    for _ in range(3):
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(m(X, 1), Y).backward()
+        opt.step()
+    for k, v in m.state_dict().items():
+        torch.testing.assert_close(torch.from_numpy(state[k]), v, atol=1e-6, rtol=1e-5)
