@@ -24,6 +24,7 @@
 namespace {
 
 constexpr int kT = 256;
+constexpr int64_t kMaxBlocks = 512;
 constexpr uint64_t kGold = 0x9E3779B97F4A7C15ull;
 constexpr uint64_t kStream = 0xD1B54A32D192ED03ull;
 
@@ -108,6 +109,13 @@ extern "C" int lgnn_dropout_masks(int num_masks, float* const* out, const int64_
   MaskJobs J = {};
   J.nj = num_masks;
   J.boff[0] = 0;
+  int64_t total = 0;
+  for (int i = 0; i < num_masks; ++i) total += numel[i] > 0 ? numel[i] : 0;
+  // elements per workgroup: at least 4 per thread, and few enough workgroups (<= ~512 + jobs)
+  // that the one same-address ticket atomic per workgroup stays cheap (it serialises in L2)
+  int64_t per = (total + kMaxBlocks - 1) / kMaxBlocks;
+  per = (per + 4 * kT - 1) / (4 * kT) * (4 * kT);
+  if (per < 4 * kT) per = 4 * kT;
   for (int i = 0; i < num_masks; ++i) {
     if (numel[i] < 0 || (numel[i] > 0 && !out[i]) || thr[i] > (1u << 24)) return LGNN_EINVAL;
     if (reinterpret_cast<uintptr_t>(out[i]) % 16) return LGNN_EINVAL;
@@ -115,8 +123,7 @@ extern "C" int lgnn_dropout_masks(int num_masks, float* const* out, const int64_
     J.n[i] = numel[i];
     J.thr[i] = thr[i];
     J.scale[i] = scale[i];
-    int64_t nb = (numel[i] + 4 * kT - 1) / (4 * kT);
-    if (nb > 2048) nb = 2048;  // grid-stride beyond 2048 workgroups per job
+    const int64_t nb = (numel[i] + per - 1) / per;
     J.boff[i + 1] = J.boff[i] + (int)(nb > 0 ? nb : 1);
   }
   hipLaunchKernelGGL(k_masks, dim3((unsigned)J.boff[num_masks]), dim3(kT), 0, as_stream(stream), J,

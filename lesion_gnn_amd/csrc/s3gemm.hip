@@ -95,15 +95,16 @@ __device__ __forceinline__ void store_a(unsigned char* img, const ARegs& R, int 
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int pos = swz(rq + 4 * i, kq >> 3) + ((kq & 7) << 1);
-    const float* f = reinterpret_cast<const float*>(R.v + 4 * i);
+    const float f0 = __uint_as_float(R.v[4 * i]), f1 = __uint_as_float(R.v[4 * i + 1]);
+    const float f2 = __uint_as_float(R.v[4 * i + 2]), f3 = __uint_as_float(R.v[4 * i + 3]);
     if constexpr (PLANES == 3) {
-      const Split2 a = split2(f[0], f[1]), b = split2(f[2], f[3]);
+      const Split2 a = split2(f0, f1), b = split2(f2, f3);
 #pragma unroll
       for (int p = 0; p < 3; ++p)
         *reinterpret_cast<u32x2*>(img + p * IMG + pos) = u32x2{a.p[p], b.p[p]};
     } else {
       *reinterpret_cast<u32x2*>(img + pos) =
-          u32x2{rne16(f[0]) | (rne16(f[1]) << 16), rne16(f[2]) | (rne16(f[3]) << 16)};
+          u32x2{rne16(f0) | (rne16(f1) << 16), rne16(f2) | (rne16(f3) << 16)};
     }
   }
 }
@@ -122,7 +123,12 @@ __device__ __forceinline__ void load_b(u32x4 (&b)[4][PLANES], Buf bW, int64_t ps
           bW, (int)(p * pstride * 2) + ((c * 4 + s) * 4 * 512 + wlane) * 2, 0, 0);
 }
 
-template <int PLANES, bool VEC>
+// NCK > 0: exactly NCK chunks, the chunk sequence fully unrolled (straight-line code: the
+// compiler's wait counts stay exact, every load stays in flight across the LDS-only barriers);
+// NCK = 0: any K, a loop over chunk pairs whose body is the same branch-free sequence (an odd
+// chunk count runs one all-zero chunk). Prefetches past the last chunk read zeros (offsets past
+// the buffers' ranges), so no load is guarded by a branch.
+template <int PLANES, bool VEC, int NCK>
 __global__ __launch_bounds__(NT, 2) void k_s3_gemm(const float* __restrict__ A, int64_t M, int K,
                                                    const uint16_t* __restrict__ Wp, int Kp,
                                                    const float* __restrict__ bias, int N,
@@ -137,10 +143,8 @@ __global__ __launch_bounds__(NT, 2) void k_s3_gemm(const float* __restrict__ A, 
   const int64_t pstride = (int64_t)128 * Kp;  // bf16 elements per plane
   const Buf bW = mkbuf(Wp + nb * PLANES * pstride, PLANES * pstride * 2);
   const int rq = 16 * wave + (lane >> 4), kq = 4 * (lane & 15);
-  const int nck = Kp / BK;
   const int wlane = wave * 512 + lane * 8;
   f32x16 acc0 = {}, acc1 = {};
-  auto ld_a = [&](ARegs& R, int c) { load_a<VEC>(R, bA, K, c, rq, kq); };
   auto chunk = [&](const unsigned char* im, const u32x4 (&bc)[4][PLANES]) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -154,26 +158,33 @@ __global__ __launch_bounds__(NT, 2) void k_s3_gemm(const float* __restrict__ A, 
       acc1 = mma<PLANES>(a1, bc[s], acc1);
     }
   };
-  // two register sets ping-pong: chunk c + 1's loads are in flight while chunk c is used
+  // two register sets ping-pong: chunk c + 2's loads are issued while chunk c is used
   ARegs R0, R1;
   u32x4 b0[4][PLANES], b1[4][PLANES];
-  ld_a(R0, 0);
+  load_a<VEC>(R0, bA, K, 0, rq, kq);
   load_b<PLANES>(b0, bW, pstride, wlane, 0);
-  if (nck > 1) {
-    ld_a(R1, 1);
-    load_b<PLANES>(b1, bW, pstride, wlane, 1);
-  }
+  load_a<VEC>(R1, bA, K, 1, rq, kq);
+  load_b<PLANES>(b1, bW, pstride, wlane, 1);
   auto step = [&](int c, ARegs& R, u32x4 (&bc)[4][PLANES]) {
     unsigned char* im = img[c & 1];
     store_a<PLANES>(im, R, rq, kq);
-    if (c + 2 < nck) ld_a(R, c + 2);
+    load_a<VEC>(R, bA, K, c + 2, rq, kq);
     lds_barrier();  // image c complete (image c - 2's reads finished before barrier c - 1)
     chunk(im, bc);
-    if (c + 2 < nck) load_b<PLANES>(bc, bW, pstride, wlane, c + 2);
+    load_b<PLANES>(bc, bW, pstride, wlane, c + 2);
   };
-  for (int c = 0; c < nck; c += 2) {
-    step(c, R0, b0);
-    if (c + 1 < nck) step(c + 1, R1, b1);
+  if constexpr (NCK > 0) {
+#pragma unroll
+    for (int c = 0; c < NCK; ++c) {
+      if (c & 1) step(c, R1, b1);
+      else step(c, R0, b0);
+    }
+  } else {
+    const int npair = (Kp / BK + 1) / 2;
+    for (int cp = 0; cp < npair; ++cp) {
+      step(2 * cp, R0, b0);
+      step(2 * cp + 1, R1, b1);
+    }
   }
   // epilogue: + bias; fp32 rows as 128-B segments per (row, wave); optional column sums
   const int n = nb * 128 + 32 * wave + li;
@@ -203,7 +214,7 @@ __global__ __launch_bounds__(NT, 2) void k_s3_gemm(const float* __restrict__ A, 
 // dW partial slabs: part[s][n][k] = sum over split s's CPB row chunks of dY[m][n] X[m][k]
 // ------------------------------------------------------------------------------------------
 struct WRegs {
-  float y[16][2];  // dY: columns nb 128 + 2 lane + 0..1 of rows 16 w + 8 g + j (g < 2, j < 8)
+  u32x2 y[16];  // dY (fp32 bits): columns n0 + 2 lane + 0..1 of rows 16 w + 8 g + j (g, j < 2, 8)
   uint32_t x[16];  // X: k = k0 + 4 (lane & 15) + 0..3 of rows 16 w + 4 (lane >> 4) + i
 };
 
@@ -217,11 +228,9 @@ __device__ __forceinline__ void wg_load(WRegs& R, Buf bX, Buf bY, int K, int N, 
     for (int j = 0; j < 8; ++j) {
       const int m = m0 + 16 * wave + 8 * g + j;
       // N even (checked on the host): the pair is in range or wholly past it
-      const u32x2 v = __builtin_bit_cast(
+      R.y[8 * g + j] = __builtin_bit_cast(
           u32x2, __builtin_amdgcn_raw_buffer_load_b64(bY, opaque(n < N ? (m * N + n) * 4 : OOB), 0,
                                                       0));
-      R.y[8 * g + j][0] = __uint_as_float(v[0]);
-      R.y[8 * g + j][1] = __uint_as_float(v[1]);
     }
   const int k = k0 + 4 * (lane & 15);
 #pragma unroll
@@ -247,25 +256,27 @@ template <int PLANES>
 __device__ __forceinline__ void wg_store(unsigned char* iy, unsigned char* ix, const WRegs& R,
                                          int lane, int wave) {
   // dY^T: lane's column pair (2 lane, 2 lane + 1), rows 8 ch .. 8 ch + 7 of the chunk -> one 16-B
-  // write per (column, plane)
+  // write per (column, plane); register elements by constant index only (no pointers: a pointer
+  // into the array would move it to scratch)
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
     const int ch = 2 * wave + g;
     uint32_t lo[PLANES][4], hi[PLANES][4];  // packed (row 2i, row 2i + 1) per column
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float* a = R.y[8 * g + 2 * i];
-      const float* b = R.y[8 * g + 2 * i + 1];
+      const int ra = 8 * g + 2 * i, rb = ra + 1;
+      const float ya0 = __uint_as_float(R.y[ra][0]), ya1 = __uint_as_float(R.y[ra][1]);
+      const float yb0 = __uint_as_float(R.y[rb][0]), yb1 = __uint_as_float(R.y[rb][1]);
       if constexpr (PLANES == 3) {
-        const Split2 c0 = split2(a[0], b[0]), c1 = split2(a[1], b[1]);
+        const Split2 c0 = split2(ya0, yb0), c1 = split2(ya1, yb1);
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
           lo[p][i] = c0.p[p];
           hi[p][i] = c1.p[p];
         }
       } else {
-        lo[0][i] = rne16(a[0]) | (rne16(b[0]) << 16);
-        hi[0][i] = rne16(a[1]) | (rne16(b[1]) << 16);
+        lo[0][i] = rne16(ya0) | (rne16(yb0) << 16);
+        hi[0][i] = rne16(ya1) | (rne16(yb1) << 16);
       }
     }
 #pragma unroll
@@ -305,16 +316,18 @@ __device__ __forceinline__ void wg_run(unsigned char* sm, f32x16& acc0, f32x16& 
   const int ncm = (int)((M + TM - 1) / TM);
   const int cend = std::min(c0 + cpb, ncm);
   WRegs R;
-  if (c0 < cend) wg_load<FULL>(R, bX, bY, K, N, c0 * TM, k0, n0, lane, wave);
+  // branch-free: the prefetch of the chunk after the split's last one reads the next split's
+  // rows (or zeros past M) and is dropped
+  wg_load<FULL>(R, bX, bY, K, N, c0 * TM, k0, n0, lane, wave);
   for (int c = c0; c < cend; ++c) {
-    if (c > c0) lds_barrier();  // the previous chunk's image reads are done
+    lds_barrier();  // the previous chunk's image reads are done
     wg_store<PLANES>(iy, ix, R, lane, wave);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {  // the bias gradient's column sums, fixed row order
-      cs[0] += R.y[j][0];
-      cs[1] += R.y[j][1];
+      cs[0] += __uint_as_float(R.y[j][0]);
+      cs[1] += __uint_as_float(R.y[j][1]);
     }
-    if (c + 1 < cend) wg_load<FULL>(R, bX, bY, K, N, (c + 1) * TM, k0, n0, lane, wave);
+    wg_load<FULL>(R, bX, bY, K, N, (c + 1) * TM, k0, n0, lane, wave);
     lds_barrier();  // images complete (the next chunk's loads stay in flight)
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
@@ -446,13 +459,27 @@ extern "C" int lgnn_s3_gemm(const float* A, int64_t M, int K, const uint16_t* Wp
   const dim3 grid((unsigned)((M + TM - 1) / TM), (unsigned)((N + 127) / 128)), block(NT);
   hipStream_t s = as_stream(stream);
   const bool v = K % 4 == 0;
-  if (planes == 3) {
-    if (v) hipLaunchKernelGGL((k_s3_gemm<3, true>), grid, block, 0, s, A, M, K, Wp, Kp, bias, N, Y, colsum_part);
-    else hipLaunchKernelGGL((k_s3_gemm<3, false>), grid, block, 0, s, A, M, K, Wp, Kp, bias, N, Y, colsum_part);
-  } else {
-    if (v) hipLaunchKernelGGL((k_s3_gemm<1, true>), grid, block, 0, s, A, M, K, Wp, Kp, bias, N, Y, colsum_part);
-    else hipLaunchKernelGGL((k_s3_gemm<1, false>), grid, block, 0, s, A, M, K, Wp, Kp, bias, N, Y, colsum_part);
+  const int nck = Kp / BK;
+#define LGNN_S3G(P, V, NC) \
+  hipLaunchKernelGGL((k_s3_gemm<P, V, NC>), grid, block, 0, s, A, M, K, Wp, Kp, bias, N, Y, \
+                     colsum_part)
+#define LGNN_S3G_N(P, V)                 \
+  switch (nck) {                         \
+    case 2: LGNN_S3G(P, V, 2); break;    \
+    case 4: LGNN_S3G(P, V, 4); break;    \
+    case 8: LGNN_S3G(P, V, 8); break;    \
+    case 17: LGNN_S3G(P, V, 17); break;  \
+    default: LGNN_S3G(P, V, 0); break;   \
   }
+  // the unrolled bodies: K <= 128 / 256 / 512 (lins and their dX) and 1025..1088 (the
+  // reference in_proj); other widths run the pair loop
+  if (planes == 3) {
+    if (v) { LGNN_S3G_N(3, true) } else { LGNN_S3G_N(3, false) }
+  } else {
+    if (v) { LGNN_S3G_N(1, true) } else { LGNN_S3G_N(1, false) }
+  }
+#undef LGNN_S3G_N
+#undef LGNN_S3G
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
 }

@@ -613,8 +613,8 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
 #pragma unroll
         for (int i = 0; i < TM * TM / 4 / NT; ++i) st4(scr + 4 * (tq + i * NT), zero4());
         if (tq <= TM) sm.rp[tq] = R.rp;
-        if (tq == 0) sm.flag = 0;
       }
+      if (tq == 0) sm.flag = 0;  // set below when some Â weight of the tile is inexact in bf16
       if (tq < TM) {
         const int64_t row = r0 + tq;
         const int64_t g = pre_g;
@@ -683,12 +683,15 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
 #pragma unroll
       for (int y = 0; y < 16; ++y) f[y] = scr[(16 * aq + perm16(y)) * TM + am];
       uint32_t q[3][8];
+      uint32_t inexact = 0;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const Split2 s2 = split2(f[2 * i], f[2 * i + 1]);
 #pragma unroll
         for (int p = 0; p < 3; ++p) q[p][i] = s2.p[p];
+        inexact |= s2.p[1] | s2.p[2];
       }
+      if (__any(inexact != 0) && (tq & 63) == 0) sm.flag = 1;
       lds_barrier();  // every scratch read done (the planes overwrite it)
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
@@ -731,12 +734,15 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
           *reinterpret_cast<u32x4*>(dst) = u32x4{q[p][0], q[p][1], q[p][2], q[p][3]};
           *reinterpret_cast<u32x4*>(dst + 16) = u32x4{q[p][4], q[p][5], q[p][6], q[p][7]};
         }
+        if (__any(inexact) && (tq & 63) == 0) sm.flag = 1;
       }
-      (void)inexact;  // the fused kernel always takes the six products (no per-tile branch)
       lds_barrier();
     }
     if (has_next) idx_load_body(R, col, w);
     }
+    // every Â weight exact in bf16 (k-regular kNN graphs with k a power of two: 1/k): the
+    // aggregation products take three plane products instead of six and read one Â plane
+    const bool aexact = __builtin_amdgcn_readfirstlane(sm.flag) == 0;
     STAMP(stamp++);
 
     f32x16 xp[2];  // X rows of the in_proj phase (issued during the last conv's dH)
@@ -771,17 +777,29 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
         f32x16 gt[2] = {f32x16{}, f32x16{}};
         const int tq = fresh_tid();
         const int h = (tq >> 5) & 1, li = tq & 31, wv = tq >> 6;
+        if (aexact) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
+          for (int s = 0; s < 4; ++s) {
 #pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            const int off = (32 * q + li) * ADJ_LD * 2 + 16 * (2 * s + h);
-            u32x4 at[3];
-#pragma unroll
-            for (int p = 0; p < 3; ++p) at[p] = lds16(sm.Adj[p] + off);
-            if constexpr (!(ABL & 1)) gt[q] = mfma_s3(dzp[s], at, gt[q]);
+            for (int q = 0; q < 2; ++q) {
+              const int off = (32 * q + li) * ADJ_LD * 2 + 16 * (2 * s + h);
+              const u32x4 a0 = lds16(sm.Adj[0] + off);
+              if constexpr (!(ABL & 1)) gt[q] = mfma_s3_bexact(dzp[s], a0, gt[q]);
+            }
           }
-          S3F_SB();
+        } else {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              const int off = (32 * q + li) * ADJ_LD * 2 + 16 * (2 * s + h);
+              u32x4 at[3];
+#pragma unroll
+              for (int p = 0; p < 3; ++p) at[p] = lds16(sm.Adj[p] + off);
+              if constexpr (!(ABL & 1)) gt[q] = mfma_s3(dzp[s], at, gt[q]);
+            }
+            S3F_SB();
+          }
         }
 #pragma unroll
         for (int q = 0; q < 2; ++q)
@@ -800,17 +818,29 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
       {
         const int tq = fresh_tid();
         const int h = (tq >> 5) & 1, li = tq & 31;
+        if (aexact) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
+          for (int s = 0; s < 4; ++s) {
 #pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            const int off = (32 * q + li) * ADJ_LD * 2 + 16 * (2 * s + h);
-            u32x4 at[3];
-#pragma unroll
-            for (int p = 0; p < 3; ++p) at[p] = lds16(sm.Adj[p] + off);
-            if constexpr (!(ABL & 1)) g[q] = mfma_s3(at, dzp[s], g[q]);
+            for (int q = 0; q < 2; ++q) {
+              const int off = (32 * q + li) * ADJ_LD * 2 + 16 * (2 * s + h);
+              const u32x4 a0 = lds16(sm.Adj[0] + off);
+              if constexpr (!(ABL & 1)) g[q] = mfma_s3_aexact(a0, dzp[s], g[q]);
+            }
           }
-          S3F_SB();
+        } else {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              const int off = (32 * q + li) * ADJ_LD * 2 + 16 * (2 * s + h);
+              u32x4 at[3];
+#pragma unroll
+              for (int p = 0; p < 3; ++p) at[p] = lds16(sm.Adj[p] + off);
+              if constexpr (!(ABL & 1)) g[q] = mfma_s3(at, dzp[s], g[q]);
+            }
+            S3F_SB();
+          }
         }
       }
       STAMP(stamp++);

@@ -478,22 +478,21 @@ def gat_conv_bwd(dY: Tensor, x: Tensor, W: Tensor, att_src: Tensor, att_dst: Ten
                  XP: Tensor, a_s: Tensor, a_d: Tensor, alpha: Tensor, Y: Tensor,
                  mask: Optional[Tensor], g: list[Tensor], heads: int, slope: float, act: int,
                  bf16: bool, has_bias: bool, want_dx: bool) -> list[Tensor]:
-    from .ops import _GATConv, fast_shape
+    from .ops import GAT_S3, _GATConv, fast_shape
 
     HC = W.shape[0]
     ctx = _Ctx((want_dx,))
     ctx.save_for_backward(x.contiguous(), W.contiguous(), att_src.reshape(-1),
                           att_dst.reshape(-1), XP, a_s, a_d, alpha, Y, mask)
     ctx.graph, ctx.heads, ctx.slope, ctx.act = TGraph(g, "gat"), heads, slope, act
-    ctx.bf16, ctx.dense = bf16, bf16 or not fast_shape(W.shape[1], HC)
+    ctx.bf16, ctx.dense = bf16, bf16 or not fast_shape(W.shape[1], HC) or GAT_S3
     ctx.has_bias = has_bias
     ctx.att_shape = tuple(att_src.shape)
-    dx, dW, da_s, da_d, db = _GATConv.backward(ctx, dY)[:5]
-    # the eager backward returns the three attention/bias gradients as views of one reduction
-    # buffer; a custom op's outputs may not alias each other
-    da_s, da_d = da_s.clone(), da_d.clone()
-    db = db.clone() if db is not None else None
-    return _grad_list([dx, dW, da_s, da_d, db], x.device)
+    dx, dW = _GATConv.backward(ctx, dY)[:2]
+    # the attention / bias gradients are ONE reduction buffer [att_src | att_dst | bias]
+    # (outputs of a custom op may not alias each other): returned whole and split into views by
+    # the autograd formula below, instead of three copies
+    return _grad_list([dx, dW, ctx.red], x.device)
 
 
 @gat_conv_bwd.register_fake
@@ -501,8 +500,7 @@ def _(dY, x, W, att_src, att_dst, XP, a_s, a_d, alpha, Y, mask, g, heads, slope,
       has_bias, want_dx):
     dev = x.device
     return [torch.empty_like(x) if want_dx else _none(dev), torch.empty_like(W),
-            torch.empty_like(att_src), torch.empty_like(att_dst),
-            W.new_empty(W.shape[0]) if has_bias else _none(dev)]
+            W.new_empty(3 * W.shape[0])]
 
 
 def _gat_setup(ctx, inputs, output):
@@ -516,10 +514,14 @@ def _gat_setup(ctx, inputs, output):
 def _gat_backward(ctx, grads):
     x, W, att_src, att_dst, XP, a_s, a_d, alpha, Y, mask, *g = ctx.saved_tensors
     heads, slope, act, bf16, has_bias = ctx.meta
-    dx, dW, da_s, da_d, db = torch.ops.lgnn.gat_conv_bwd(
+    dx, dW, red = torch.ops.lgnn.gat_conv_bwd(
         grads[0], x, W, att_src, att_dst, XP, a_s, a_d, alpha, Y, _opt(mask), g, heads, slope,
         act, bf16, has_bias, ctx.needs_input_grad[0])
-    return (_opt(dx), dW, da_s, da_d, _opt(db), [None] * len(g), None, None, None, None, None)
+    HC = W.shape[0]
+    da_s = red[:HC].view(att_src.shape)
+    da_d = red[HC:2 * HC].view(att_dst.shape)
+    db = red[2 * HC:] if has_bias else None
+    return (_opt(dx), dW, da_s, da_d, db, [None] * len(g), None, None, None, None, None)
 
 
 gat_conv.register_autograd(_gat_backward, setup_context=_gat_setup)

@@ -1509,7 +1509,9 @@ class _GATConv(torch.autograd.Function):
         HC = W.size(0)
         C = HC // heads
         dev = x.device
-        dense = bf16 or not fast_shape(W.size(1), HC)
+        # fp32: the lin on the split-3 MFMA GEMMs (s3gemm.hip) at every width — they beat the
+        # fp32-MFMA tile kernels (2.7x the MFMA rate at fp32 accuracy); LGNN_GAT_S3=0: tiles
+        dense = bf16 or not fast_shape(W.size(1), HC) or GAT_S3
         mfma = bf16 and bf16_mfma_fits(HC)
         ctx.wt = None
         if mfma:  # hand-written bf16 MFMA lin; x rounded in the kernel unless a copy exists
@@ -1628,12 +1630,14 @@ class _GATConv(torch.autograd.Function):
                 dx, dW, _ = linear_bwd(_lib.LGNN_GRAD_DIRECT, dXP, H=None,
                                        act=_lib.LGNN_ACT_NONE, X=x, W=W, want_dx=want_dx,
                                        want_db=False)
+        ctx.red = red  # the compiled path returns the one buffer (lgnn::gat_conv_bwd)
         datt_s = red[:HC].view(ctx.att_shape)
         datt_d = red[HC:2 * HC].view(ctx.att_shape)
         dbias = red[2 * HC:] if ctx.has_bias else None
         return dx, dW, datt_s, datt_d, dbias, None, None, None, None, None, None
 
 
+GAT_S3 = os.environ.get("LGNN_GAT_S3", "1") != "0"
 # bf16 GAT: the attention kernels write their fp32 outputs' bf16 copies for the following bf16
 # GEMMs (LGNN_BF16_OUT=0: torch casts instead; the values are identical, RNE both ways)
 BF16_OUT = os.environ.get("LGNN_BF16_OUT", "1") != "0"

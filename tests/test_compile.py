@@ -18,8 +18,7 @@ from lesion_gnn_amd.models import DRGNet, GAT, GCN, GIN
 # of an absent tensor, autograd bookkeeping, and the functionalized running-stat update
 GLUE = {"<built-in function getitem>", "aten.empty.memory_format", "aten.detach.default",
         "auto_functionalized_v2", "auto_functionalized"}
-# dropout: the masks are views into one lgnn::dropout_masks output (offsets are symbolic-size
-# arithmetic; views launch nothing)
+# views of one op output (offsets are symbolic-size arithmetic; views launch nothing)
 VIEWS = {"aten.slice.Tensor", "aten.view.default", "<built-in function add>",
          "<built-in function floordiv>", "<built-in function mul>"}
 
@@ -80,9 +79,10 @@ def test_models_trace_to_lgnn_ops_only(name):
             else {"lgnn.gcn_stack.default"}
     out, fw, bw = trace(m.to("meta"), meta_args(b))
     assert out.shape[0] == b.num_graphs
-    extra = (fw | bw) - GLUE
-    if drop:
-        extra = {t for t in extra - VIEWS if not t.startswith("<function sym_")}  # the generator state's counter advance is the op's declared mutation
+    # views launch nothing (the dropout masks are views of one op output; GAT's attention / bias
+    # gradients views of one reduction buffer)
+    extra = {t for t in (fw | bw) - GLUE - VIEWS if not t.startswith("<function sym_")}
+    if drop:  # the generator state's counter advance is the op's declared mutation
         assert "auto_functionalized_v2" in fw or "lgnn.dropout_masks.default" in fw, sorted(fw)
     assert all(t.startswith("lgnn.") for t in extra), sorted(extra)
     assert want <= fw | bw, (want, sorted(fw | bw))

@@ -153,3 +153,37 @@ def test_config_compile_true_module(cuda):
     assert torch.equal(lc, le)
     for (k, p), (k2, q) in zip(mc.named_parameters(), me.named_parameters()):
         assert k.replace("_orig_mod.", "") == k2 and torch.equal(p.grad, q.grad), k
+
+
+def test_compiled_reference_config_step_runs_only_lgnn_kernels(cuda):
+    """The reference experiment's step (configs/config.py:52-65: GAT heads 2, dropout 0.35,
+    compile=True, MSE, d_in 1025) under torch.compile launches no Triton kernel (Inductor has
+    nothing to generate: every op is an lgnn custom op) and no vendor-library GEMM, and no
+    device copy (the attention / bias gradients come out of one reduction buffer as views)."""
+    from torch.profiler import ProfilerActivity, profile
+
+    from lesion_gnn_amd.models import get_model
+    from tests.test_config import reference_model_section
+
+    cfg = reference_model_section()
+    cfg.num_classes.value = 5
+    cfg.input_features.value = 1025
+    cfg.optimizer.class_weights.value = torch.ones(5)
+    torch.manual_seed(1234)
+    torch._dynamo.reset()
+    module = get_model(cfg).to(cuda).train()
+    b = synth.make_batch(64, k=6, d_in=1025, seed=3, sizes="lognormal",
+                         last_channel_class=True).to(cuda)
+    for _ in range(2):  # compile + warm up
+        module.zero_grad(set_to_none=True)
+        module.training_step(b).backward()
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        module.zero_grad(set_to_none=True)
+        module.training_step(b).backward()
+        torch.cuda.synchronize()
+    names = [e.name for e in prof.events() if e.device_type.name == "CUDA"]
+    assert names and any("k_gat_fwd" in n for n in names), sorted(set(names))
+    assert not [n for n in names if "triton" in n.lower()], sorted(set(names))
+    assert not [n for n in names if n.startswith(("Cijk", "Custom_Cijk"))], sorted(set(names))
+    assert not [n for n in names if "copyBuffer" in n or "Memcpy" in n], sorted(set(names))
