@@ -92,6 +92,15 @@ int lgnn_graph_build_lazy(const int64_t* edge_index, int64_t E, int64_t N, int l
                           float* tw, int32_t* tmap, int32_t* tile_open, const int64_t* batch,
                           int64_t num_graphs, int32_t* gptr, int32_t* err_count, void* workspace,
                           size_t workspace_bytes, void* stream);
+/* lgnn_graph_build_sync: the same build (lazy != 0: as lgnn_graph_build_lazy) in ONE persistent
+ * launch — the five phases behind grid barriers, every workgroup resident at once (grid sized from
+ * the occupancy query). sync: 4 int32 owned by the caller, zero before the first call and re-armed
+ * by every launch (one sync triple per stream: two builds that may run concurrently need two). */
+int lgnn_graph_build_sync(const int64_t* edge_index, int64_t E, int64_t N, int loops, int norm,
+                          int32_t* rowptr, int32_t* col, float* w, int32_t* tptr, int32_t* tidx,
+                          float* tw, int32_t* tmap, int32_t* tile_open, const int64_t* batch,
+                          int64_t num_graphs, int32_t* gptr, int32_t* err_count, void* workspace,
+                          size_t workspace_bytes, int lazy, int32_t* sync, void* stream);
 
 /* Graph offsets from a sorted PyG `batch` vector (Batch.ptr): ptr[g] = first node of graph g,
  * ptr[B] = M. Replaces the count/offset half of PyG scatter(reduce='mean') over `batch`. */

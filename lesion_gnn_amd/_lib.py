@@ -41,6 +41,8 @@ SIGNATURES: dict[str, tuple] = {
                                     P, SZ, P]),
     "lgnn_graph_build": (I32, [P, I64, I64, I32, I32, P, P, P, P, P, P, P, P, P, I64, P, P, P,
                                SZ, P]),
+    "lgnn_graph_build_sync": (I32, [P, I64, I64, I32, I32, P, P, P, P, P, P, P, P, P, I64, P, P,
+                                    P, SZ, I32, P, P]),
     "lgnn_batch_ptr": (I32, [P, I64, I64, P, P]),
     "lgnn_node_linear_fwd": (I32, [P, I64, I32, P, P, P, F32, P, P, I32, I32, P, P, P]),
     "lgnn_bwd_num_partials": (I32, [I64, I32, I32, I32]),

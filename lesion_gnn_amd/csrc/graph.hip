@@ -15,6 +15,7 @@
 //             messages in), compute GCN weights, write back coalesced. Run for both CSRs.
 // The result is identical run to run.
 #include "common.h"
+#include "tile_util.h"
 
 namespace {
 
@@ -98,13 +99,12 @@ __device__ __forceinline__ bool edge_ok(int64_t s, int64_t d, int64_t N) {
 
 // First launch of a build: zero the counters, scan flags and tile flags (ntiles + the count),
 // and, when a batch vector is given, the graph offsets (as lgnn_batch_ptr).
-__global__ __launch_bounds__(kThreads) void k_prep(int32_t* __restrict__ zero, int64_t nzero,
-                                                   int32_t* __restrict__ tile_open,
-                                                   int64_t ntiles,
-                                                   const int64_t* __restrict__ batch, int64_t M,
-                                                   int64_t B, int32_t* __restrict__ gptr) {
-  const int64_t i0 = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  const int64_t step = (int64_t)gridDim.x * kThreads;
+__device__ __forceinline__ void prep_body(int32_t* __restrict__ zero, int64_t nzero,
+                                          int32_t* __restrict__ tile_open, int64_t ntiles,
+                                          const int64_t* __restrict__ batch, int64_t M, int64_t B,
+                                          int32_t* __restrict__ gptr, int bx, int gx) {
+  const int64_t i0 = (int64_t)bx * kThreads + threadIdx.x;
+  const int64_t step = (int64_t)gx * kThreads;
   for (int64_t i = i0; i < nzero; i += step) zero[i] = 0;
   if (tile_open)  // flags, their count, and the fused kernels' grid-barrier words
     for (int64_t t = i0; t < ntiles + LGNN_TILE_OPEN_EXTRA; t += step) tile_open[t] = 0;
@@ -119,6 +119,14 @@ __global__ __launch_bounds__(kThreads) void k_prep(int32_t* __restrict__ zero, i
       for (int64_t q = prev + 1; q <= cur; ++q) gptr[q] = (int32_t)i;
     }
   }
+}
+
+__global__ __launch_bounds__(kThreads) void k_prep(int32_t* __restrict__ zero, int64_t nzero,
+                                                   int32_t* __restrict__ tile_open,
+                                                   int64_t ntiles,
+                                                   const int64_t* __restrict__ batch, int64_t M,
+                                                   int64_t B, int32_t* __restrict__ gptr) {
+  prep_body(zero, nzero, tile_open, ntiles, batch, M, B, gptr, blockIdx.x, gridDim.x);
 }
 
 // Edge passes. A block takes a chunk of kChunk consecutive edges, kPer per thread, so every
@@ -189,14 +197,11 @@ __device__ __forceinline__ void mark_open(int32_t* tile_open, int64_t t, int64_t
   if (atomicCAS(&tile_open[t], 0, 1) == 0) atomicAdd(&tile_open[ntiles], 1);
 }
 
-__global__ __launch_bounds__(kThreads) void k_count(const int64_t* __restrict__ ei, int64_t E,
-                                                    int64_t N, int loops, int32_t* cnt,
-                                                    int32_t* tcnt, int32_t* err,
-                                                    int32_t* tile_open) {
-  __shared__ int hist[kBins];
-  __shared__ int red[2 * kThreads / 64];
+__device__ __forceinline__ void count_body(const int64_t* __restrict__ ei, int64_t E, int64_t N,
+                                           int loops, int32_t* cnt, int32_t* tcnt, int32_t* err,
+                                           int32_t* tile_open, int* hist, int* red, int64_t bx) {
   const int lane = threadIdx.x & 63;
-  const int64_t c0 = (int64_t)blockIdx.x * kChunk;
+  const int64_t c0 = bx * kChunk;
   EdgeChunk c;
   load_chunk(c, ei, E, N, loops, c0, err);
 #pragma unroll
@@ -231,19 +236,25 @@ __global__ __launch_bounds__(kThreads) void k_count(const int64_t* __restrict__ 
   }
 }
 
-// fill[d] / tfill[s] start at the row offsets (set by k_scan); slots come from atomics on them,
-// so the order inside a row is arbitrary here and restored by k_finish (sort by edge id).
-__global__ __launch_bounds__(kThreads) void k_fill(const int64_t* __restrict__ ei, int64_t E,
-                                                   int64_t N, int loops,
-                                                   const int32_t* __restrict__ rowptr,
-                                                   int32_t* fill, int32_t* col, int32_t* eid,
-                                                   const int32_t* __restrict__ tptr,
-                                                   int32_t* tfill, int32_t* tidx, int32_t* teid,
-                                                   const int32_t* lazy_open) {
+__global__ __launch_bounds__(kThreads) void k_count(const int64_t* __restrict__ ei, int64_t E,
+                                                    int64_t N, int loops, int32_t* cnt,
+                                                    int32_t* tcnt, int32_t* err,
+                                                    int32_t* tile_open) {
   __shared__ int hist[kBins];
   __shared__ int red[2 * kThreads / 64];
+  count_body(ei, E, N, loops, cnt, tcnt, err, tile_open, hist, red, blockIdx.x);
+}
+
+// fill[d] / tfill[s] start at the row offsets (set by k_scan); slots come from atomics on them,
+// so the order inside a row is arbitrary here and restored by k_finish (sort by edge id).
+__device__ __forceinline__ void fill_body(const int64_t* __restrict__ ei, int64_t E, int64_t N,
+                                          int loops, const int32_t* __restrict__ rowptr,
+                                          int32_t* fill, int32_t* col, int32_t* eid,
+                                          const int32_t* __restrict__ tptr, int32_t* tfill,
+                                          int32_t* tidx, int32_t* teid, const int32_t* lazy_open,
+                                          int* hist, int* red, int64_t bx) {
   const int lane = threadIdx.x & 63;
-  const int64_t c0 = (int64_t)blockIdx.x * kChunk;
+  const int64_t c0 = bx * kChunk;
   EdgeChunk c;
   load_chunk(c, ei, E, N, loops, c0, nullptr);
 #pragma unroll
@@ -294,6 +305,19 @@ __global__ __launch_bounds__(kThreads) void k_fill(const int64_t* __restrict__ e
   }
 }
 
+__global__ __launch_bounds__(kThreads) void k_fill(const int64_t* __restrict__ ei, int64_t E,
+                                                   int64_t N, int loops,
+                                                   const int32_t* __restrict__ rowptr,
+                                                   int32_t* fill, int32_t* col, int32_t* eid,
+                                                   const int32_t* __restrict__ tptr,
+                                                   int32_t* tfill, int32_t* tidx, int32_t* teid,
+                                                   const int32_t* lazy_open) {
+  __shared__ int hist[kBins];
+  __shared__ int red[2 * kThreads / 64];
+  fill_body(ei, E, N, loops, rowptr, fill, col, eid, tptr, tfill, tidx, teid, lazy_open, hist, red,
+            blockIdx.x);
+}
+
 // Both degree scans (blockIdx.y = 0: rowptr from cnt, 1: tptr from tcnt) in ONE launch over
 // 1024-element blocks: block b sums its elements and publishes the sum (flagged) in stat[b] at
 // once; its 256 threads then read the sums of blocks 0..b-1 in parallel (each spinning until its
@@ -312,24 +336,27 @@ __device__ __forceinline__ int scan_val(const int32_t* __restrict__ c, int64_t i
   return i < N ? c[i] + add : 0;
 }
 
-__global__ __launch_bounds__(kScanT) void k_scan(const int32_t* __restrict__ cnt,
-                                                 const int32_t* __restrict__ tcnt, int64_t N,
-                                                 int add, int32_t* stat,
-                                                 int32_t* __restrict__ rowptr,
-                                                 int32_t* __restrict__ tptr,
-                                                 int32_t* __restrict__ fill,
-                                                 int32_t* __restrict__ tfill,
-                                                 float* __restrict__ dis,
-                                                 int32_t* tile_open) {
-  __shared__ int wsc[kScanT / 64];
-  __shared__ int s_pre;
-  const bool tr = blockIdx.y == 1;
+struct ScanSmem {
+  int wsc[kScanT / 64];
+  int wpre[kScanT / 64];
+  int s_pre;
+};
+
+__device__ __forceinline__ void scan_body(const int32_t* __restrict__ cnt,
+                                          const int32_t* __restrict__ tcnt, int64_t N, int add,
+                                          int32_t* stat, int32_t* __restrict__ rowptr,
+                                          int32_t* __restrict__ tptr, int32_t* __restrict__ fill,
+                                          int32_t* __restrict__ tfill, float* __restrict__ dis,
+                                          int32_t* tile_open, ScanSmem& sm, int bx, int by,
+                                          int nblk) {
+  int* wsc = sm.wsc;
+  const bool tr = by == 1;
   const int32_t* __restrict__ c = tr ? tcnt : cnt;
   int32_t* __restrict__ out = tr ? tptr : rowptr;
   int32_t* __restrict__ fl = tr ? tfill : fill;
-  int32_t* st = stat + (int64_t)blockIdx.y * gridDim.x;
+  int32_t* st = stat + (int64_t)by * nblk;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t i0 = (int64_t)blockIdx.x * kScanBlk + (int64_t)tid * kScanPer;
+  const int64_t i0 = (int64_t)bx * kScanBlk + (int64_t)tid * kScanPer;
   int v[kScanPer];
   int s = 0;
 #pragma unroll
@@ -346,10 +373,10 @@ __global__ __launch_bounds__(kScanT) void k_scan(const int32_t* __restrict__ cnt
   if (lane == 63) wsc[wave] = x;
   __syncthreads();
   if (tid == 0)
-    __hip_atomic_store(&st[blockIdx.x], (wsc[0] + wsc[1] + wsc[2] + wsc[3]) | kScanFlag,
+    __hip_atomic_store(&st[bx], (wsc[0] + wsc[1] + wsc[2] + wsc[3]) | kScanFlag,
                        __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   int pre = 0;  // sums of the preceding blocks, thread-strided, then combined in wave order
-  for (int j = tid; j < (int)blockIdx.x; j += kScanT) {
+  for (int j = tid; j < bx; j += kScanT) {
     int f;
     while (((f = __hip_atomic_load(&st[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) &
             kScanFlag) == 0)
@@ -357,12 +384,11 @@ __global__ __launch_bounds__(kScanT) void k_scan(const int32_t* __restrict__ cnt
     pre += f & (kScanFlag - 1);
   }
   for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
-  __shared__ int wpre[kScanT / 64];
-  if (lane == 0) wpre[wave] = pre;
+  if (lane == 0) sm.wpre[wave] = pre;
   __syncthreads();
-  if (tid == 0) s_pre = wpre[0] + wpre[1] + wpre[2] + wpre[3];
+  if (tid == 0) sm.s_pre = sm.wpre[0] + sm.wpre[1] + sm.wpre[2] + sm.wpre[3];
   __syncthreads();
-  int run = s_pre + x - s;
+  int run = sm.s_pre + x - s;
   for (int w = 0; w < wave; ++w) run += wsc[w];
   if (!tr && tile_open) {  // lazy transpose: tiles with more CSR entries than a tile stages
     int ts = s;            // (a 64-row tile = 16 threads' elements; tiles never straddle blocks)
@@ -386,6 +412,20 @@ __global__ __launch_bounds__(kScanT) void k_scan(const int32_t* __restrict__ cnt
   }
 }
 
+__global__ __launch_bounds__(kScanT) void k_scan(const int32_t* __restrict__ cnt,
+                                                 const int32_t* __restrict__ tcnt, int64_t N,
+                                                 int add, int32_t* stat,
+                                                 int32_t* __restrict__ rowptr,
+                                                 int32_t* __restrict__ tptr,
+                                                 int32_t* __restrict__ fill,
+                                                 int32_t* __restrict__ tfill,
+                                                 float* __restrict__ dis,
+                                                 int32_t* tile_open) {
+  __shared__ ScanSmem sm;
+  scan_body(cnt, tcnt, N, add, stat, rowptr, tptr, fill, tfill, dis, tile_open, sm, blockIdx.x,
+            blockIdx.y, gridDim.x);
+}
+
 // insertion sort of n (key, val) pairs by key (keys distinct)
 template <typename KP, typename VP>
 __device__ __forceinline__ void sort_row(KP key, VP val, int n) {
@@ -402,38 +442,41 @@ __device__ __forceinline__ void sort_row(KP key, VP val, int n) {
   }
 }
 
-// blockIdx.y = 0: target CSR (rowptr/col/eid/w); 1: source CSR (tptr/tidx/teid/tw).
+// by = 0: target CSR (rowptr/col/eid/w); 1: source CSR (tptr/tidx/teid/tw). One virtual block
+// = kFinT rows, run by kFinT threads (tid = 0..63) with `sync` their barrier: the whole workgroup
+// of k_finish, or one wave of the fused build (k_build) with its own staging arrays.
 // Weight of entry (row i, neighbour j): GCN (dis(src) * 1) * dis(dst) = dis(j) * dis(i).
-__global__ __launch_bounds__(kFinT) void k_finish(int64_t N, int64_t E, int add_loop, int norm,
-                                                     const int32_t* __restrict__ rowptr,
-                                                     int32_t* col, int32_t* eid, float* w,
-                                                     const int32_t* __restrict__ tptr,
-                                                     int32_t* tidx, int32_t* teid, float* tw,
-                                                     const float* __restrict__ dis,
-                                                     const int32_t* __restrict__ ws_err,
-                                                     int32_t* err_out, int32_t* tile_open,
-                                                     int lazy, int32_t* __restrict__ inv) {
-  __shared__ int32_t s_key[kFinishCap];
-  if (lazy && blockIdx.y == 1 && tile_open[(N + 63) >> 6] == 0) return;  // no source CSR needed
-  if (err_out && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *err_out = *ws_err;
-  __shared__ int32_t s_val[kFinishCap];
-  const bool tr = blockIdx.y == 1;
+template <typename Sync>
+__device__ __forceinline__ void finish_body(int64_t N, int64_t E, int add_loop, int norm,
+                                            const int32_t* __restrict__ rowptr, int32_t* col,
+                                            int32_t* eid, float* w,
+                                            const int32_t* __restrict__ tptr, int32_t* tidx,
+                                            int32_t* teid, float* tw,
+                                            const float* __restrict__ dis,
+                                            const int32_t* __restrict__ ws_err, int32_t* err_out,
+                                            int32_t* tile_open, int lazy,
+                                            int32_t* __restrict__ inv, int32_t* s_key,
+                                            int32_t* s_val, int64_t bx, int by, int tid,
+                                            Sync sync) {
+  if (lazy && by == 1 && tile_open[(N + 63) >> 6] == 0) return;  // no source CSR needed
+  if (err_out && bx == 0 && by == 0 && tid == 0) *err_out = *ws_err;
+  const bool tr = by == 1;
   const int32_t* __restrict__ ptr = tr ? tptr : rowptr;
   int32_t* idx = tr ? tidx : col;
   int32_t* key = tr ? teid : eid;
   float* wt = tr ? tw : w;
-  const int64_t i0 = (int64_t)blockIdx.x * kFinT;
-  const int64_t i = i0 + threadIdx.x;
+  const int64_t i0 = bx * kFinT;
+  const int64_t i = i0 + tid;
   const int64_t iend = i0 + kFinT < N ? i0 + kFinT : N;
   const int eb = ptr[i0], ee = ptr[iend];
   const bool staged = ee - eb <= kFinishCap;
   if (staged) {
-    for (int j = eb + threadIdx.x; j < ee; j += kFinT) {
+    for (int j = eb + tid; j < ee; j += kFinT) {
       s_key[j - eb] = key[j];
       s_val[j - eb] = idx[j];
     }
   }
-  __syncthreads();
+  sync();
   if (i < N) {
     const int r0 = ptr[i], r1 = ptr[i + 1];
     if (staged) {
@@ -450,9 +493,9 @@ __global__ __launch_bounds__(kFinT) void k_finish(int64_t N, int64_t E, int add_
       sort_row(key + r0, idx + r0, r1 - r0);
     }
   }
-  __syncthreads();
+  sync();
   if (staged) {
-    for (int j = eb + threadIdx.x; j < ee; j += kFinT) {
+    for (int j = eb + tid; j < ee; j += kFinT) {
       idx[j] = s_val[j - eb];
       key[j] = s_key[j - eb];
       if (inv && !tr) inv[s_key[j - eb]] = j;  // k_tmap_inv's map, while the keys are at hand
@@ -490,6 +533,35 @@ __global__ __launch_bounds__(kFinT) void k_finish(int64_t N, int64_t E, int add_
       }
     }
   }
+  sync();  // the staging arrays are free for the next virtual block
+}
+
+struct BlockSync {
+  __device__ void operator()() const { __syncthreads(); }
+};
+// one wave: its LDS accesses are ordered by a wave-scope fence (no cross-wave barrier)
+struct WaveSync {
+  __device__ void operator()() const {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+};
+
+__global__ __launch_bounds__(kFinT) void k_finish(int64_t N, int64_t E, int add_loop, int norm,
+                                                     const int32_t* __restrict__ rowptr,
+                                                     int32_t* col, int32_t* eid, float* w,
+                                                     const int32_t* __restrict__ tptr,
+                                                     int32_t* tidx, int32_t* teid, float* tw,
+                                                     const float* __restrict__ dis,
+                                                     const int32_t* __restrict__ ws_err,
+                                                     int32_t* err_out, int32_t* tile_open,
+                                                     int lazy, int32_t* __restrict__ inv) {
+  __shared__ int32_t s_key[kFinishCap];
+  __shared__ int32_t s_val[kFinishCap];
+  finish_body(N, E, add_loop, norm, rowptr, col, eid, w, tptr, tidx, teid, tw, dis, ws_err,
+              err_out, tile_open, lazy, inv, s_key, s_val, blockIdx.x, blockIdx.y, threadIdx.x,
+              BlockSync{});
 }
 
 // tmap[q] = position in the target CSR of the edge at source-CSR position q (both CSRs hold the
@@ -502,6 +574,89 @@ __global__ __launch_bounds__(kThreads) void k_tmap(const int32_t* __restrict__ t
   const int nnz = tptr[N];
   for (int q = blockIdx.x * kThreads + threadIdx.x; q < nnz; q += gridDim.x * kThreads)
     tmap[q] = inv[teid[q]];
+}
+
+// ---------------------------------------------------------------------------------------------
+// The whole build in ONE persistent launch (k_build): the phases of the launches above (prep,
+// count, scan, fill, finish, tmap) run back to back, separated by grid barriers (tile_util.h
+// grid_sync on a caller-owned, self-re-arming word triple), each workgroup striding over the
+// phase's virtual blocks. Every workgroup must be resident at once: the grid is sized from the
+// occupancy query. The finish phase runs its 64-row virtual blocks one per wave. Saves the
+// launch gaps and the fill / drain of five dependent launches (C2: 36 -> see DESIGN §4.1).
+struct BuildArgs {
+  const int64_t* ei;
+  int64_t E, N;
+  int loops, norm, add_loop, lazy;
+  int32_t *rowptr, *col, *tptr, *tidx, *tmap, *tile_open, *gptr, *err_count;
+  float *w, *tw;
+  const int64_t* batch;
+  int64_t num_graphs;
+  GraphWs ws;
+};
+
+union BuildSmem {
+  struct {
+    int hist[kBins];
+    int red[2 * kThreads / 64];
+  } e;
+  ScanSmem scan;
+  struct {
+    int32_t key[kThreads / 64][kFinishCap];
+    int32_t val[kThreads / 64][kFinishCap];
+  } fin;
+};
+
+__global__ __launch_bounds__(kThreads) void k_build(BuildArgs a, int32_t* sync) {
+  __shared__ BuildSmem sm;
+  const int G = gridDim.x, b = blockIdx.x;
+  const int64_t N = a.N, E = a.E, ntiles = (N + 63) / 64;
+  {
+    const int64_t nzero = (int64_t)(a.ws.zero_bytes / 4);
+    prep_body(a.ws.err, nzero, a.tile_open, ntiles, a.batch, N, a.num_graphs, a.gptr, b, G);
+  }
+  lgnn_tile::grid_sync(sync, 1);
+  const int64_t nch = (E + kChunk - 1) / kChunk;
+  for (int64_t c = b; c < nch; c += G) {
+    __syncthreads();  // the previous chunk's LDS reads are done
+    count_body(a.ei, E, N, a.loops, a.ws.cnt, a.tptr ? a.ws.tcnt : nullptr, a.ws.err,
+               a.lazy ? a.tile_open : nullptr, sm.e.hist, sm.e.red, c);
+  }
+  lgnn_tile::grid_sync(sync, 2);
+  {
+    const int nblk = (int)((N + 1 + kScanBlk - 1) / kScanBlk), ny = a.tptr ? 2 : 1;
+    for (int v = b; v < nblk * ny; v += G) {
+      __syncthreads();
+      scan_body(a.ws.cnt, a.ws.tcnt, N, a.add_loop, a.ws.stat, a.rowptr, a.tptr, a.ws.fill,
+                a.ws.tfill, a.ws.dis, a.lazy ? a.tile_open : nullptr, sm.scan, v % nblk,
+                v / nblk, nblk);
+    }
+  }
+  lgnn_tile::grid_sync(sync, 3);
+  for (int64_t c = b; c < nch; c += G) {
+    __syncthreads();
+    fill_body(a.ei, E, N, a.loops, a.rowptr, a.ws.fill, a.col, a.ws.eid, a.tptr, a.ws.tfill,
+              a.tidx, a.ws.teid, a.lazy ? a.tile_open + ntiles : nullptr, sm.e.hist, sm.e.red, c);
+  }
+  lgnn_tile::grid_sync(sync, 4);
+  {
+    __syncthreads();  // the union's finish arrays overlay the fill bins
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t nfin = (N + kFinT - 1) / kFinT;
+    const int ny = a.tptr ? 2 : 1;
+    for (int64_t v = (int64_t)b * (kThreads / 64) + wave; v < nfin * ny;
+         v += (int64_t)G * (kThreads / 64))
+      finish_body(N, E, a.add_loop, a.norm, a.rowptr, a.col, a.ws.eid, a.w, a.tptr, a.tidx,
+                  a.ws.teid, a.tw, a.ws.dis, a.ws.err, a.err_count, a.tile_open, a.lazy,
+                  a.tmap ? a.ws.inv : nullptr, sm.fin.key[wave], sm.fin.val[wave], v % nfin,
+                  (int)(v / nfin), lane, WaveSync{});
+  }
+  if (a.tmap) {
+    lgnn_tile::grid_sync(sync, 5);
+    const int nnz = a.tptr[N];
+    for (int q = b * kThreads + threadIdx.x; q < nnz; q += G * kThreads)
+      a.tmap[q] = a.ws.inv[a.ws.teid[q]];
+  }
+  lgnn_tile::grid_exit(sync);
 }
 
 __global__ void k_batch_ptr(const int64_t* __restrict__ batch, int64_t M, int64_t B,
@@ -546,7 +701,35 @@ static int graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loop
                        int32_t* rowptr, int32_t* col, float* w, int32_t* tptr, int32_t* tidx,
                        float* tw, int32_t* tmap, int32_t* tile_open, const int64_t* batch,
                        int64_t num_graphs, int32_t* gptr, int32_t* err_count, void* workspace,
-                       size_t workspace_bytes, void* stream, int lazy);
+                       size_t workspace_bytes, void* stream, int lazy, int32_t* sync = nullptr);
+
+// workgroups of k_build resident at once on this device (occupancy x CUs), cached per device
+static int build_capacity() {
+  static int cache[16];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 0;
+  if (cache[dev] > 0) return cache[dev];
+  int cus = 0, per = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_build, kThreads, 0) != hipSuccess)
+    return 0;
+  cache[dev] = cus * per;
+  return cache[dev];
+}
+
+extern "C" int lgnn_graph_build_sync(const int64_t* edge_index, int64_t E, int64_t N, int loops,
+                                     int norm, int32_t* rowptr, int32_t* col, float* w,
+                                     int32_t* tptr, int32_t* tidx, float* tw, int32_t* tmap,
+                                     int32_t* tile_open, const int64_t* batch,
+                                     int64_t num_graphs, int32_t* gptr, int32_t* err_count,
+                                     void* workspace, size_t workspace_bytes, int lazy,
+                                     int32_t* sync, void* stream) {
+  if (!sync) return LGNN_EINVAL;
+  if (lazy && (!tile_open || !tptr || tmap)) return LGNN_EINVAL;
+  return graph_build(edge_index, E, N, loops, norm, rowptr, col, w, tptr, tidx, tw, tmap,
+                     tile_open, batch, num_graphs, gptr, err_count, workspace, workspace_bytes,
+                     stream, lazy ? 1 : 0, sync);
+}
 
 extern "C" int lgnn_graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loops,
                                 int norm, int32_t* rowptr, int32_t* col, float* w, int32_t* tptr,
@@ -575,7 +758,7 @@ static int graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loop
                        int32_t* rowptr, int32_t* col, float* w, int32_t* tptr, int32_t* tidx,
                        float* tw, int32_t* tmap, int32_t* tile_open, const int64_t* batch,
                        int64_t num_graphs, int32_t* gptr, int32_t* err_count, void* workspace,
-                       size_t workspace_bytes, void* stream, int lazy) {
+                       size_t workspace_bytes, void* stream, int lazy, int32_t* sync) {
   if (N < 0 || E < 0 || loops < 0 || loops > 2 || norm < 0 || norm > 1) return LGNN_EINVAL;
   if (!rowptr || !col || (E > 0 && !edge_index)) return LGNN_EINVAL;
   if (N + E >= (int64_t)1 << 30) return LGNN_EINVAL;
@@ -586,6 +769,39 @@ static int graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loop
   hipStream_t s = as_stream(stream);
   const int add_loop = loops == LGNN_LOOPS_KEEP ? 0 : 1;
   GraphWs ws = carve(workspace, N, E);
+  const int cap = (sync && N > 0) ? build_capacity() : 0;
+  if (cap > 0) {  // one persistent launch (k_build)
+    BuildArgs a{};
+    a.ei = edge_index;
+    a.E = E;
+    a.N = N;
+    a.loops = loops;
+    a.norm = norm;
+    a.add_loop = add_loop;
+    a.lazy = lazy;
+    a.rowptr = rowptr;
+    a.col = col;
+    a.tptr = tptr;
+    a.tidx = tidx;
+    a.tmap = tmap;
+    a.tile_open = tile_open;
+    a.gptr = gptr;
+    a.err_count = err_count;
+    a.w = w;
+    a.tw = tw;
+    a.batch = batch;
+    a.num_graphs = num_graphs;
+    a.ws = ws;
+    const int64_t nch = (E + kChunk - 1) / kChunk;
+    const int64_t nfin = (N + kFinT - 1) / kFinT * (tptr ? 2 : 1);
+    int64_t g = nch;
+    if ((nfin + 3) / 4 > g) g = (nfin + 3) / 4;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    hipLaunchKernelGGL(k_build, dim3((unsigned)g), dim3(kThreads), 0, s, a, sync);
+    LGNN_LAUNCH_CHECK();
+    return LGNN_OK;
+  }
   {
     const int64_t nzero = (int64_t)(ws.zero_bytes / 4);
     const int64_t ntiles = (N + 63) / 64;

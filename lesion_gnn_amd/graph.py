@@ -10,6 +10,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import os
+
 import torch
 
 from . import _lib
@@ -117,13 +119,18 @@ class Graph:
         gptr = None  # the graph offsets ride along with the first build
         if self._gptr is None and self.batch is not None:
             gptr = self._gptr = torch.empty(self.num_graphs + 1, dtype=torch.int32, device=dev)
-        _lib.call("lgnn_graph_build_lazy" if kind == "gcn_lazy" else "lgnn_graph_build",
-                  _lib.ptr(self.edge_index), e, n, loops, norm,
-                  _lib.ptr(c.rowptr), _lib.ptr(c.col), _lib.ptr(c.w), _lib.ptr(c.tptr),
-                  _lib.ptr(c.tidx), _lib.ptr(c.tw), _lib.ptr(c.tmap), _lib.ptr(c.tile_open),
-                  _lib.ptr(self.batch) if gptr is not None else None,
-                  self.num_graphs if gptr is not None else 0, _lib.ptr(gptr), _lib.ptr(c.err),
-                  _lib.ptr(ws), ws_bytes, _lib.stream(dev))
+        args = (_lib.ptr(self.edge_index), e, n, loops, norm,
+                _lib.ptr(c.rowptr), _lib.ptr(c.col), _lib.ptr(c.w), _lib.ptr(c.tptr),
+                _lib.ptr(c.tidx), _lib.ptr(c.tw), _lib.ptr(c.tmap), _lib.ptr(c.tile_open),
+                _lib.ptr(self.batch) if gptr is not None else None,
+                self.num_graphs if gptr is not None else 0, _lib.ptr(gptr), _lib.ptr(c.err),
+                _lib.ptr(ws), ws_bytes)
+        if FUSED_BUILD:  # one persistent launch (lgnn_graph_build_sync)
+            _lib.call("lgnn_graph_build_sync", *args, int(kind == "gcn_lazy"),
+                      _lib.ptr(_build_sync(dev)), _lib.stream(dev))
+        else:
+            _lib.call("lgnn_graph_build_lazy" if kind == "gcn_lazy" else "lgnn_graph_build",
+                      *args, _lib.stream(dev))
         self._csr[kind] = c
         return c
 
@@ -197,6 +204,21 @@ class Graph:
     def dropped_edges(self, kind: str) -> int:
         """Number of edges with an out-of-range index (synchronises)."""
         return int(self.csr(kind).err.item())
+
+
+# the graph build as one persistent launch (LGNN_FUSED_BUILD=0: the five-launch pipeline)
+FUSED_BUILD = os.environ.get("LGNN_FUSED_BUILD", "1") != "0"
+_SYNC: dict = {}
+
+
+def _build_sync(dev) -> torch.Tensor:
+    """The fused build's grid-barrier words for this device (zeroed once, re-armed by every
+    launch). One per device: this package issues its builds on one stream per device."""
+    key = torch.device(dev).index
+    t = _SYNC.get(key)
+    if t is None:
+        t = _SYNC[key] = torch.zeros(4, dtype=torch.int32, device=dev)
+    return t
 
 
 def adj_t_to_edge_index(adj_t, with_values: bool = False):

@@ -1,0 +1,66 @@
+"""GPU: the graph build as ONE persistent launch (lgnn_graph_build_sync, k_build: prep / count /
+scan / fill / finish / tmap behind grid barriers) is bit-identical to the five-launch pipeline
+(lgnn_graph_build / _lazy) for every CSR kind the models use — GCN (gcn_norm weights), its lazy
+variant with the tile flags, GAT (remove + add self loops, with tmap), GIN (loops kept) — on
+k-NN, irregular, shuffled-with-duplicates, invalid-edge and empty inputs; built twice in a row
+(the barrier words re-arm: all zero afterwards, no barrier timed out)."""
+import pytest
+import torch
+
+from lesion_gnn_amd import graph as graph_mod
+from lesion_gnn_amd import synth
+from lesion_gnn_amd.graph import Graph
+
+pytestmark = pytest.mark.gpu
+
+
+def _cases():
+    b1 = synth.make_batch(1024, n=64, k=8, seed=1)
+    b2 = synth.make_batch(12, k=8, seed=2, sizes=[1, 3, 7, 64, 65, 2, 130, 1, 9, 16, 8, 33],
+                          loop=False)
+    perm = torch.randperm(b2.edge_index.size(1), generator=torch.Generator().manual_seed(0))
+    ei2 = torch.cat([b2.edge_index[:, perm], torch.tensor([[5, 5, 5, 70, 70], [5, 5, 6, 71, 71]])],
+                    1)
+    b3 = synth.make_batch(300, k=6, seed=3, sizes="lognormal")
+    bad = torch.tensor([[0, 1, 7, -1, 2], [1, 0, 0, 2, 2]])
+    return {"knn_c2": (b1.edge_index, b1.num_nodes), "irregular": (ei2, b2.num_nodes),
+            "lognormal": (b3.edge_index, b3.num_nodes), "invalid": (bad, 3),
+            "no_edges": (torch.empty(2, 0, dtype=torch.long), 70),
+            "big_rows": (torch.stack([torch.arange(3000) % 50, torch.zeros(3000, dtype=torch.long)]),
+                         50)}
+
+
+FIELDS = ("rowptr", "col", "w", "tptr", "tidx", "tw", "tmap", "tile_open", "err")
+
+
+def _build(ei, n, kind, fused, cuda, monkeypatch):
+    monkeypatch.setattr(graph_mod, "FUSED_BUILD", fused)
+    g = Graph(ei.to(cuda), n)
+    c = g.csr(kind)
+    nnz = int(c.rowptr[-1].item())
+    out = {}
+    for f in FIELDS:
+        t = getattr(c, f)
+        if t is None:
+            continue
+        if f in ("col", "w", "tidx", "tw", "tmap"):
+            t = t[:nnz]
+        if f in ("tptr", "tidx", "tw") and kind == "gcn_lazy" and int(c.tile_open[(n + 63) // 64]) == 0:
+            continue  # the lazy build leaves the source CSR unwritten when no tile is open
+        out[f] = t.cpu()
+    return out
+
+
+@pytest.mark.parametrize("case", ["knn_c2", "irregular", "lognormal", "invalid", "no_edges",
+                                  "big_rows"])
+@pytest.mark.parametrize("kind", ["gcn", "gcn_lazy", "gat", "gin"])
+def test_fused_build_bitexact(cuda, monkeypatch, case, kind):
+    ei, n = _cases()[case]
+    want = _build(ei, n, kind, False, cuda, monkeypatch)
+    for _ in range(2):
+        got = _build(ei, n, kind, True, cuda, monkeypatch)
+        assert set(got) == set(want)
+        for f in want:
+            assert torch.equal(got[f], want[f]), (case, kind, f)
+    sync = graph_mod._build_sync(cuda).cpu().tolist()
+    assert sync == [0, 0, 0, 0], sync  # re-armed, no barrier gave up
