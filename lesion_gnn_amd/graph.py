@@ -206,8 +206,12 @@ class Graph:
         return int(self.csr(kind).err.item())
 
 
-# the graph build as one persistent launch (LGNN_FUSED_BUILD=0: the five-launch pipeline)
-FUSED_BUILD = os.environ.get("LGNN_FUSED_BUILD", "1") != "0"
+# the graph build as one persistent launch (LGNN_FUSED_BUILD=1); off by default: measured on
+# MI355X at C2 it takes 242 us against 36 us for the five launches — every grid barrier's
+# agent-scope release writes back the workgroup's XCD L2 and the acquire invalidates it, so the
+# CSR data each phase produces crosses the XCDs through memory instead of the kernel boundary's
+# single write-back (profiles/r03f_c2_per_step.txt)
+FUSED_BUILD = os.environ.get("LGNN_FUSED_BUILD", "0") == "1"
 _SYNC: dict = {}
 
 
