@@ -314,6 +314,68 @@ def time_dominant_kernels(model, b, dev):
     return out
 
 
+def time_gat_in_proj(model, b, dev, wl):
+    """The GAT workloads' two largest launches, both on the in_proj nn.Linear(d_in, 128) (the
+    reference's 1024 encoder channels + lesion class, gat.py:29), timed alone on the step's own
+    node features: the forward GEMM Y = X W^T + b and the weight gradient dW = dY^T X (+ db),
+    split-3 bf16 MFMA at fp32 accuracy (s3gemm.hip) in fp32 mode, the one-plane bf16 kernels
+    (bflin.hip) in bf16 mode. Useful FLOP per launch 2 M d_in h; algorithmic HBM bytes per launch
+    X once (M d_in 4) + Y (or dY) once (M h 4)."""
+    from lesion_gnn_amd import _lib, ops
+
+    x = b.x
+    M, K = x.shape
+    W = model.in_proj.weight.detach()
+    bias = model.in_proj.bias.detach()
+    N = W.size(0)
+    dy = torch.randn(M, N, device=dev)
+    flops = 2.0 * M * K * N
+    nbytes = 4.0 * M * K + 4.0 * M * N
+    lib = _lib.load()
+    s = torch.cuda.current_stream(dev).cuda_stream
+    out = []
+    if wl.get("precision") == "bf16":
+        Wb, _ = ops.bf16_weight_operands(W, False)
+        Y = torch.empty(M, N, device=dev)
+        S = lib.lgnn_bf16_wgrad_partials(M, K)
+        part = torch.empty(S * N * K, device=dev)
+        dyb = dy.to(torch.bfloat16)
+
+        def fwd():
+            _lib.call("lgnn_bf16_gemm", x.data_ptr(), 1, M, K, Wb.data_ptr(), bias.data_ptr(), N,
+                      Y.data_ptr(), None, None, s)
+
+        def wgrad():
+            _lib.call("lgnn_bf16_wgrad", dyb.data_ptr(), N, x.data_ptr(), 1, M, K,
+                      part.data_ptr(), S, s)
+        names = ("void lgnn_bf::k_bf_gemm<true, false, 17", "void lgnn_bf::k_bf_wgrad<true")
+        peak = 16 * MFMA_F32_PEAK_TF  # dense bf16: one plane product per product
+        label = "bf16 MFMA (bflin.hip)"
+    else:
+        Wp = ops.dense_planes(W, False, False)
+        Y = torch.empty(M, N, device=dev)
+        S = lib.lgnn_s3_wgrad_partials(M, K, N)
+        part = torch.empty(S * N * K, device=dev)
+        dbp = torch.empty(S * N, device=dev)
+
+        def fwd():
+            _lib.call("lgnn_s3_gemm", x.data_ptr(), M, K, Wp.data_ptr(), N, 3, bias.data_ptr(),
+                      Y.data_ptr(), None, s)
+
+        def wgrad():
+            _lib.call("lgnn_s3_wgrad", dy.data_ptr(), N, x.data_ptr(), M, K, 3, part.data_ptr(),
+                      S, dbp.data_ptr(), s)
+        names = ("void lgnn_s3g::k_s3_gemm<3, false, 17>", "void lgnn_s3g::k_s3_wgrad<3>")
+        peak = MFMA_S3_PEAK_TF
+        label = "split-3 bf16 MFMA at fp32 accuracy (s3gemm.hip)"
+    for what, fn, name in (("forward GEMM Y = X W^T + b", fwd, names[0]),
+                           ("weight gradient dW = dY^T X (+ db)", wgrad, names[1])):
+        out.append({"kernel": f"in_proj {what} [{M} x {K}] -> {N}, {label}",
+                    "ms": _time_launches(fn, dev), "flops": flops, "bytes": nbytes,
+                    "peak": peak, "trace_name": name})
+    return out
+
+
 def time_knn(b, wl, dev):
     """The data-side k-NN graph build of this batch (KNNGraph(k, loop=True), reference
     configs/config.py:47): GPU (lgnn_knn_graph, one launch for the whole batch, HIP events) vs
@@ -605,6 +667,29 @@ def main():
                          "avg_launch_ms": round(kt["ms"], 5), "flops_per_launch": kt["flops"]})
         rows.sort(key=lambda r: -r["avg_launch_ms"])
         out["roofline"] = rows[0]  # the dominant kernel (longest launch)
+        out["roofline_next"] = rows[1:]
+    if rank == 0 and not args.no_kernel_timing and wl["model"] == "gat":
+        rows = []
+        for kt in time_gat_in_proj(model, b, dev, wl):
+            sec = kt["ms"] * 1e-3
+            tf = kt["flops"] / sec / 1e12
+            gbs = kt["bytes"] / sec / 1e9
+            f_mfma, f_hbm = tf / kt["peak"], gbs / HBM_PEAK_GBS
+            traffic, tsrc = pmc_traffic(kt["trace_name"])
+            mfma_bound = f_mfma >= f_hbm  # the roof the kernel is closer to
+            rows.append({"bound": "mfma" if mfma_bound else "hbm",
+                         "achieved": round(tf if mfma_bound else gbs, 2),
+                         "peak": kt["peak"] if mfma_bound else HBM_PEAK_GBS,
+                         "unit": "TFLOP/s" if mfma_bound else "GB/s",
+                         "frac": round(max(f_mfma, f_hbm), 4),
+                         "frac_mfma": round(f_mfma, 4), "frac_hbm": round(f_hbm, 4),
+                         "achieved_TFLOPs": round(tf, 2), "achieved_GBps": round(gbs, 1),
+                         "traffic": round(traffic) if traffic else None, "traffic_source": tsrc,
+                         "kernel": kt["kernel"], "avg_launch_ms": round(kt["ms"], 5),
+                         "flops_per_launch": kt["flops"], "algorithmic_bytes_per_launch":
+                         kt["bytes"]})
+        rows.sort(key=lambda r: -r["avg_launch_ms"])
+        out["roofline"] = rows[0]
         out["roofline_next"] = rows[1:]
     if rank == 0 and not args.no_kernel_timing:
         out["knn_graph"] = time_knn(b, wl, dev)

@@ -39,8 +39,10 @@ constexpr int OOB = 0x7ff00000;  // buffer offset past every range: the load ret
 __device__ __forceinline__ uint32_t pk2(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2{a, b}), bf16x2));
 }
+// 16-B chunk XOR-swizzled by (row >> 1) & 7: the 16 rows of a ds_read_b128 lane group land in
+// 16 distinct 16-B bank slots (s3gemm.hip swz)
 __device__ __forceinline__ int swz(int row, int chunk) {
-  return row * ROWB + ((chunk ^ (row & 7)) << 4);
+  return row * ROWB + ((chunk ^ ((row >> 1) & 7)) << 4);
 }
 __device__ __forceinline__ u32x4 lds16(const unsigned char* p) {
   return *reinterpret_cast<const u32x4*>(p);

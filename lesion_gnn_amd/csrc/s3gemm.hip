@@ -18,10 +18,11 @@
 //               4 waves, wave w owns columns 32 w .. + 31 of the block; the A chunk (64 rows x 64
 //               k) goes through three XOR-swizzled LDS planes, double-buffered; the B fragments
 //               come straight from L2 (whole 1-KiB lines per wave load), one chunk ahead.
-//   k_s3_wgrad  dW partial slabs part[s][n][k] = sum over row split s of dY[m][n] X[m][k]: the
-//               transposed images dY^T [n][m] and X^T [k][m] per plane (one buffer: 72 KiB, two
-//               workgroups per CU), the next chunk's rows in registers during the MFMAs; the
-//               slabs are summed in fixed order by lgnn_reduce_partials(_multi) (deterministic).
+//   k_s3_wgrad2 dW partial slabs part[s][n][k] = sum over row split s of dY[m][n] X[m][k]: a
+//               128 n x 128 k tile per workgroup (64 x 64 per wave), the transposed 32-row images
+//               dY^T and X^T per plane in one 48-KiB buffer, the next chunk's rows in registers
+//               during the MFMAs; the slabs are summed in fixed order by
+//               lgnn_reduce_partials(_multi) (deterministic).
 #include <algorithm>
 
 #include "common.h"
@@ -43,8 +44,12 @@ constexpr int ROWB = BK * 2;    // bytes per image row (bf16)
 constexpr int IMG = TM * ROWB;  // bytes per 64-row image plane
 constexpr int OOB = 0x7ff00000;  // buffer offset past every range: loads return 0
 
+// 128-B image rows, 16-B chunk XOR-swizzled by (row >> 1) & 7: the 16 rows of a ds_read_b128
+// lane group ({0-3, 12-15, 20-27} / {4-11, 16-19, 28-31}, MI355X_MICROARCH.md §LDS) land in 16
+// distinct 16-B bank slots (an (row & 7) key pairs rows 8 apart on one slot: 2-way conflicts,
+// measured 40 % extra LDS cycles)
 __device__ __forceinline__ int swz(int row, int chunk) {
-  return row * ROWB + ((chunk ^ (row & 7)) << 4);
+  return row * ROWB + ((chunk ^ ((row >> 1) & 7)) << 4);
 }
 __device__ __forceinline__ int opaque(int x) {
   asm volatile("" : "+v"(x));
@@ -211,177 +216,151 @@ __global__ __launch_bounds__(NT, 2) void k_s3_gemm(const float* __restrict__ A, 
 }
 
 // ------------------------------------------------------------------------------------------
-// dW partial slabs: part[s][n][k] = sum over split s's CPB row chunks of dY[m][n] X[m][k]
+// dW partial slabs (k_s3_wgrad2): a workgroup owns a 128 (n) x 128 (k) tile of dW and a row
+// split; 4 waves each own 64 n x 64 k (four 32 x 32 accumulators), so every operand fragment a
+// wave reads from LDS feeds two column (row) blocks: 0.5 KiB of LDS per MFMA (a 32-n wave tile
+// took 0.75 KiB and ran LDS-bound: 155 us for the C3 in_proj, 67 % bank-conflict cycles). Chunks of 32
+// rows: the transposed images dY^T [128 n][32 m] and X^T [128 k][32 m] x 3 planes are 48 KiB
+// (single buffer, two workgroups per CU), the next chunk's rows in registers during the MFMAs.
+// Image rows are 64 B (4 chunks of 16 B), chunk-swizzled by (row >> 2) & 3: a 16-lane b128 read
+// group of consecutive rows touches 64 distinct banks.
 // ------------------------------------------------------------------------------------------
-struct WRegs {
-  u32x2 y[16];  // dY (fp32 bits): columns n0 + 2 lane + 0..1 of rows 16 w + 8 g + j (g, j < 2, 8)
-  uint32_t x[16];  // X: k = k0 + 4 (lane & 15) + 0..3 of rows 16 w + 4 (lane >> 4) + i
+constexpr int W2M = 32;               // rows per chunk
+constexpr int W2ROW = W2M * 2;        // bytes per image row (bf16)
+constexpr int W2IMG = 128 * W2ROW;    // bytes per 128-row image plane
+
+__device__ __forceinline__ int w2off(int row, int c16) {  // byte offset of 16-B chunk c16
+  return row * W2ROW + ((c16 ^ ((row >> 2) & 3)) << 4);
+}
+
+// per lane: rows 4 rq .. 4 rq + 3 of the chunk (rq = tid % 8), columns 4 cq .. 4 cq + 3
+// (cq = tid / 8) of the 128-wide block, one 16-B load per row, for dY and for X (rq fast: a
+// 16-lane write group then covers two image rows whole — 2-way bank overlap instead of 4)
+struct W2Regs {
+  u32x4 y[4];
+  u32x4 x[4];
 };
 
-template <bool FULL>
-__device__ __forceinline__ void wg_load(WRegs& R, Buf bX, Buf bY, int K, int N, int m0, int k0,
-                                        int n0, int lane, int wave) {
-  const int n = n0 + 2 * lane;
+__device__ __forceinline__ u32x4 ld16(Buf b, int off, int col, int ncol) {
+  // a 4-column group inside the columns [0, ncol): one 16-B load; at or past it: 0 (OOB offset);
+  // straddling it (ncol % 4 != 0): the columns past it zeroed after the load
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(b, opaque(col < ncol ? off : OOB), 0, 0);
+  u32x4 r;
 #pragma unroll
-  for (int g = 0; g < 2; ++g)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int m = m0 + 16 * wave + 8 * g + j;
-      // N even (checked on the host): the pair is in range or wholly past it
-      R.y[8 * g + j] = __builtin_bit_cast(
-          u32x2, __builtin_amdgcn_raw_buffer_load_b64(bY, opaque(n < N ? (m * N + n) * 4 : OOB), 0,
-                                                      0));
-    }
-  const int k = k0 + 4 * (lane & 15);
+  for (int j = 0; j < 4; ++j) r[j] = col + j < ncol ? v[j] : 0u;
+  return r;
+}
+
+__device__ __forceinline__ void w2_load(W2Regs& R, Buf bY, Buf bX, int N, int K, int m0, int n0,
+                                        int k0, int tid) {
+  const int rq = tid & 7, cq = tid >> 3;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int off = (m0 + 16 * wave + 4 * (lane >> 4) + i) * K + k;
-    if constexpr (FULL) {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(bX, off * 4, 0, 0);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) R.x[4 * i + j] = v[j];
-    } else {  // as load_a: one 16-B load, columns >= K zeroed
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(bX, opaque(k < K ? off * 4 : OOB), 0, 0);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) R.x[4 * i + j] = k + j < K ? v[j] : 0u;
-    }
+    const int m = m0 + 4 * rq + i;
+    const int n = n0 + 4 * cq, k = k0 + 4 * cq;
+    R.y[i] = ld16(bY, (m * N + n) * 4, n, N);
+    R.x[i] = ld16(bX, (m * K + k) * 4, k, K);
   }
 }
 
-// image layouts per plane: Y^T [n 0..127][m 0..63], X^T [k 0..63][m 0..63], bf16, swizzled rows
-constexpr int WY = 128 * ROWB;
-constexpr int WX = 64 * ROWB;
-
+// transposed write of one operand: column c (4 cq + j) gets rows 4 rq .. + 3 as 8 B per plane
 template <int PLANES>
-__device__ __forceinline__ void wg_store(unsigned char* iy, unsigned char* ix, const WRegs& R,
-                                         int lane, int wave) {
-  // dY^T: lane's column pair (2 lane, 2 lane + 1), rows 8 ch .. 8 ch + 7 of the chunk -> one 16-B
-  // write per (column, plane); register elements by constant index only (no pointers: a pointer
-  // into the array would move it to scratch)
-#pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    const int ch = 2 * wave + g;
-    uint32_t lo[PLANES][4], hi[PLANES][4];  // packed (row 2i, row 2i + 1) per column
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ra = 8 * g + 2 * i, rb = ra + 1;
-      const float ya0 = __uint_as_float(R.y[ra][0]), ya1 = __uint_as_float(R.y[ra][1]);
-      const float yb0 = __uint_as_float(R.y[rb][0]), yb1 = __uint_as_float(R.y[rb][1]);
-      if constexpr (PLANES == 3) {
-        const Split2 c0 = split2(ya0, yb0), c1 = split2(ya1, yb1);
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          lo[p][i] = c0.p[p];
-          hi[p][i] = c1.p[p];
-        }
-      } else {
-        lo[0][i] = rne16(ya0) | (rne16(yb0) << 16);
-        hi[0][i] = rne16(ya1) | (rne16(yb1) << 16);
-      }
-    }
-#pragma unroll
-    for (int p = 0; p < PLANES; ++p) {
-      *reinterpret_cast<u32x4*>(iy + p * WY + swz(2 * lane, ch)) =
-          u32x4{lo[p][0], lo[p][1], lo[p][2], lo[p][3]};
-      *reinterpret_cast<u32x4*>(iy + p * WY + swz(2 * lane + 1, ch)) =
-          u32x4{hi[p][0], hi[p][1], hi[p][2], hi[p][3]};
-    }
-  }
-  // X^T: column kq + j, rows 16 w + 4 q .. + 3 as one 8-B write per plane
-  const int q = lane >> 4, kq = 4 * (lane & 15);
-  const int ch = 2 * wave + (q >> 1), off = (q & 1) * 8;
+__device__ __forceinline__ void w2_store1(unsigned char* img, const u32x4 (&v)[4], int tid) {
+  const int rq = tid & 7, cq = tid >> 3;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const float x0 = __uint_as_float(R.x[j]), x1 = __uint_as_float(R.x[4 + j]);
-    const float x2 = __uint_as_float(R.x[8 + j]), x3 = __uint_as_float(R.x[12 + j]);
+    const int row = 4 * cq + j;
+    const int pos = w2off(row, rq >> 1) + (rq & 1) * 8;  // rows 4 rq .. of 32: chunk rq / 2
+    const float f0 = __uint_as_float(v[0][j]), f1 = __uint_as_float(v[1][j]);
+    const float f2 = __uint_as_float(v[2][j]), f3 = __uint_as_float(v[3][j]);
     if constexpr (PLANES == 3) {
-      const Split2 a = split2(x0, x1), b = split2(x2, x3);
+      const Split2 a = split2(f0, f1), b = split2(f2, f3);
 #pragma unroll
       for (int p = 0; p < 3; ++p)
-        *reinterpret_cast<u32x2*>(ix + p * WX + swz(kq + j, ch) + off) = u32x2{a.p[p], b.p[p]};
+        *reinterpret_cast<u32x2*>(img + p * W2IMG + pos) = u32x2{a.p[p], b.p[p]};
     } else {
-      *reinterpret_cast<u32x2*>(ix + swz(kq + j, ch) + off) =
-          u32x2{rne16(x0) | (rne16(x1) << 16), rne16(x2) | (rne16(x3) << 16)};
-    }
-  }
-}
-
-template <int PLANES, bool FULL>
-__device__ __forceinline__ void wg_run(unsigned char* sm, f32x16& acc0, f32x16& acc1, Buf bX,
-                                       Buf bY, int K, int N, int c0, int cpb, int64_t M, int k0,
-                                       int n0, int lane, int wave, float (&cs)[2]) {
-  const int h = lane >> 5, li = lane & 31;
-  unsigned char* iy = sm;
-  unsigned char* ix = sm + PLANES * WY;
-  const int ncm = (int)((M + TM - 1) / TM);
-  const int cend = std::min(c0 + cpb, ncm);
-  WRegs R;
-  // branch-free: the prefetch of the chunk after the split's last one reads the next split's
-  // rows (or zeros past M) and is dropped
-  wg_load<FULL>(R, bX, bY, K, N, c0 * TM, k0, n0, lane, wave);
-  for (int c = c0; c < cend; ++c) {
-    lds_barrier();  // the previous chunk's image reads are done
-    wg_store<PLANES>(iy, ix, R, lane, wave);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {  // the bias gradient's column sums, fixed row order
-      cs[0] += __uint_as_float(R.y[j][0]);
-      cs[1] += __uint_as_float(R.y[j][1]);
-    }
-    wg_load<FULL>(R, bX, bY, K, N, (c + 1) * TM, k0, n0, lane, wave);
-    lds_barrier();  // images complete (the next chunk's loads stay in flight)
-#pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      u32x4 a[PLANES], x0[PLANES], x1[PLANES];
-#pragma unroll
-      for (int p = 0; p < PLANES; ++p) {
-        a[p] = lds16(iy + p * WY + swz(32 * wave + li, 2 * st + h));
-        x0[p] = lds16(ix + p * WX + swz(li, 2 * st + h));
-        x1[p] = lds16(ix + p * WX + swz(32 + li, 2 * st + h));
-      }
-      acc0 = mma<PLANES>(a, x0, acc0);
-      acc1 = mma<PLANES>(a, x1, acc1);
+      *reinterpret_cast<u32x2*>(img + pos) =
+          u32x2{rne16(f0) | (rne16(f1) << 16), rne16(f2) | (rne16(f3) << 16)};
     }
   }
 }
 
 template <int PLANES>
-__global__ __launch_bounds__(NT, 2) void k_s3_wgrad(const float* __restrict__ dY, int N,
-                                                    const float* __restrict__ X, int64_t M, int K,
-                                                    int nkb, int cpb, float* __restrict__ part,
-                                                    float* __restrict__ dbpart) {
-  __shared__ __attribute__((aligned(16))) unsigned char sm[PLANES * (WY + WX)];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+__global__ __launch_bounds__(NT, 2) void k_s3_wgrad2(const float* __restrict__ dY, int N,
+                                                     const float* __restrict__ X, int64_t M,
+                                                     int K, int nkb, int cps,
+                                                     float* __restrict__ part,
+                                                     float* __restrict__ dbpart) {
+  __shared__ __attribute__((aligned(16))) unsigned char sm[2 * PLANES * W2IMG];
+  unsigned char* iy = sm;
+  unsigned char* ix = sm + PLANES * W2IMG;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, li = lane & 31;
+  const int wn = wave & 1, wk = wave >> 1;  // this wave's 64 n x 64 k quarter of the tile
   const int64_t L = xcd_block();  // the k-blocks of one row split are adjacent: one XCD's L2
   const int kb = (int)(L % nkb), s = (int)(L / nkb);
-  const int k0 = kb * BK, n0 = blockIdx.y * 128;
+  const int k0 = kb * 128, n0 = blockIdx.y * 128;
   const Buf bX = mkbuf(X, M * K * 4), bY = mkbuf(dY, M * N * 4);
-  f32x16 acc0 = {}, acc1 = {};
-  float cs[2] = {0.f, 0.f};
-  if (k0 + BK <= K)  // uniform: one body per block
-    wg_run<PLANES, true>(sm, acc0, acc1, bX, bY, K, N, s * cpb, cpb, M, k0, n0, lane, wave, cs);
-  else
-    wg_run<PLANES, false>(sm, acc0, acc1, bX, bY, K, N, s * cpb, cpb, M, k0, n0, lane, wave, cs);
-  if (dbpart && kb == 0) {  // db partial row s: the 4 waves' column sums folded in wave order
-    float* red = reinterpret_cast<float*>(sm);
-    __syncthreads();
-    red[wave * 128 + 2 * lane] = cs[0];
-    red[wave * 128 + 2 * lane + 1] = cs[1];
-    __syncthreads();
-    if (threadIdx.x < 128 && n0 + (int)threadIdx.x < N) {
-      const int t = threadIdx.x;
-      dbpart[(int64_t)s * N + n0 + t] = ((red[t] + red[128 + t]) + red[256 + t]) + red[384 + t];
+  const int64_t nch = (M + W2M - 1) / W2M;
+  const int64_t c0 = (int64_t)s * cps;
+  const int64_t cend = c0 + cps < nch ? c0 + cps : nch;
+  f32x16 acc[2][2] = {{{}, {}}, {{}, {}}};
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};  // column sums of dY (the bias gradient), this lane's 4 n
+  W2Regs R;
+  // branch-free: the prefetch after the split's last chunk reads the next split's rows (or zeros
+  // past M) and is dropped
+  w2_load(R, bY, bX, N, K, (int)(c0 * W2M), n0, k0, tid);
+  for (int64_t c = c0; c < cend; ++c) {
+    lds_barrier();  // the previous chunk's image reads are done
+    w2_store1<PLANES>(iy, R.y, tid);
+    w2_store1<PLANES>(ix, R.x, tid);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cs[j] += __uint_as_float(R.y[i][j]);
+    w2_load(R, bY, bX, N, K, (int)((c + 1) * W2M), n0, k0, tid);
+    lds_barrier();  // images complete (the next chunk's loads stay in flight)
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {  // two k-steps of 16 rows
+      u32x4 a[2][PLANES], b[2][PLANES];
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int p = 0; p < PLANES; ++p) {
+          a[q][p] = lds16(iy + p * W2IMG + w2off(64 * wn + 32 * q + li, 2 * st + h));
+          b[q][p] = lds16(ix + p * W2IMG + w2off(64 * wk + 32 * q + li, 2 * st + h));
+        }
+#pragma unroll
+      for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) acc[qa][qb] = mma<PLANES>(a[qa], b[qb], acc[qa][qb]);
     }
   }
-  // slab s: rows n = n0 + 32 w + (r & 3) + 8 (r >> 2) + 4 h, columns k0 + 32 kk + li
+  // slab s: rows n = n0 + 64 wn + 32 qa + (r & 3) + 8 (r >> 2) + 4 h, columns k0 + 64 wk + 32 qb + li
   float* slab = part + (int64_t)s * N * K;
 #pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    const int k = k0 + 32 * kk + li;
+  for (int qa = 0; qa < 2; ++qa)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int n = n0 + 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (n < N && k < K) slab[(int64_t)n * K + k] = kk ? acc1[r] : acc0[r];
+    for (int qb = 0; qb < 2; ++qb) {
+      const int k = k0 + 64 * wk + 32 * qb + li;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = n0 + 64 * wn + 32 * qa + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (n < N && k < K) slab[(int64_t)n * K + k] = acc[qa][qb][r];
+      }
+    }
+  if (dbpart && kb == 0) {  // db partial row s: the 8 row groups' sums folded in group order
+    float* red = reinterpret_cast<float*>(sm);
+    __syncthreads();
+    const int rq = tid & 7, cq = tid >> 3;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[rq * 128 + 4 * cq + j] = cs[j];
+    __syncthreads();
+    if (tid < 128 && n0 + tid < N) {
+      float t = red[tid];
+#pragma unroll
+      for (int g = 1; g < 8; ++g) t += red[g * 128 + tid];
+      dbpart[(int64_t)s * N + n0 + tid] = t;
     }
   }
 }
@@ -484,39 +463,39 @@ extern "C" int lgnn_s3_gemm(const float* A, int64_t M, int K, const uint16_t* Wp
   return LGNN_OK;
 }
 
-// row chunks per split: the smallest power-of-two multiple of 2 keeping the grid within about
-// 2 workgroups per CU (512), at least 2 chunks per split
-static int s3_wg_cpb(int64_t M, int K, int N) {
-  const int64_t nch = std::max<int64_t>((M + TM - 1) / TM, 1);
-  const int64_t work = (int64_t)((K + BK - 1) / BK) * ((N + 127) / 128);
-  for (int cpb = 2; cpb < 256; cpb *= 2)
-    if (work * ((nch + cpb - 1) / cpb) <= 512) return cpb;
-  return 256;
+// k_s3_wgrad2: 32-row chunks per split, so that the grid (128-wide k-blocks x splits x n-blocks)
+// holds about two workgroups per CU (512), at least 4 chunks per split
+static int s3_wg_cps(int64_t M, int K, int N) {
+  const int64_t nch = std::max<int64_t>((M + W2M - 1) / W2M, 1);
+  const int64_t work = (int64_t)((K + 127) / 128) * ((N + 127) / 128);
+  int64_t splits = std::max<int64_t>(512 / work, 1);
+  int64_t cps = (nch + splits - 1) / splits;
+  if (cps < 4) cps = 4;
+  return (int)cps;
 }
 
 extern "C" int lgnn_s3_wgrad_partials(int64_t M, int K, int N) {
   if (M < 0 || K < 1 || N < 1) return 0;
-  const int64_t nch = std::max<int64_t>((M + TM - 1) / TM, 1);
-  const int cpb = s3_wg_cpb(M, K, N);
-  return (int)((nch + cpb - 1) / cpb);
+  const int64_t nch = std::max<int64_t>((M + W2M - 1) / W2M, 1);
+  const int cps = s3_wg_cps(M, K, N);
+  return (int)((nch + cps - 1) / cps);
 }
 
 extern "C" int lgnn_s3_wgrad(const float* dY, int N, const float* X, int64_t M, int K, int planes,
                              float* partials, int num_partials, float* db_partials,
                              void* stream) {
-  if (M < 0 || K < 1 || N < 1 || N % 2 != 0 || !partials || (planes != 1 && planes != 3))
-    return LGNN_EINVAL;
+  if (M < 0 || K < 1 || N < 1 || !partials || (planes != 1 && planes != 3)) return LGNN_EINVAL;
   if (num_partials != lgnn_s3_wgrad_partials(M, K, N)) return LGNN_EINVAL;
   if (M > 0 && (!dY || !X)) return LGNN_EINVAL;
-  if ((M + TM) * (int64_t)std::max(K, N) * 4 >= ((int64_t)1 << 31)) return LGNN_EINVAL;
-  const int nkb = (K + BK - 1) / BK, cpb = s3_wg_cpb(M, K, N);
+  if ((M + 2 * W2M) * (int64_t)std::max(K, N) * 4 >= ((int64_t)1 << 31)) return LGNN_EINVAL;
+  const int nkb = (K + 127) / 128, cps = s3_wg_cps(M, K, N);
   const dim3 grid((unsigned)(nkb * num_partials), (unsigned)((N + 127) / 128)), block(NT);
   hipStream_t s = as_stream(stream);
   if (planes == 3)
-    hipLaunchKernelGGL((k_s3_wgrad<3>), grid, block, 0, s, dY, N, X, M, K, nkb, cpb, partials,
+    hipLaunchKernelGGL((k_s3_wgrad2<3>), grid, block, 0, s, dY, N, X, M, K, nkb, cps, partials,
                        db_partials);
   else
-    hipLaunchKernelGGL((k_s3_wgrad<1>), grid, block, 0, s, dY, N, X, M, K, nkb, cpb, partials,
+    hipLaunchKernelGGL((k_s3_wgrad2<1>), grid, block, 0, s, dY, N, X, M, K, nkb, cps, partials,
                        db_partials);
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
