@@ -565,6 +565,467 @@ __global__ __launch_bounds__(NT) GAT_OCC void k_gat_bwd_node(
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Row-pipelined variants (one 128-feature pass: H*C <= 128, H <= 4 — every GAT of the reference
+// config and of C3). The kernels above spend a row's life in a chain of dependent round trips
+// (row extent -> column indices -> logit inputs / source rows -> stores) with only the source
+// rows carrying bandwidth, and each wave sees two rows. Here a half wave walks many rows and
+// keeps the chain off the critical path: while row r's source rows are gathered, the column
+// indices of row r + step and the extent of row r + 2 step are already in flight. And the
+// per-edge scalars are loaded edge-parallel, one instruction for 8 edges x 4 heads (lane
+// u + 8 h of a half wave: edge u, head h), then handed to the feature lanes with ds_bpermute
+// instead of 8-24 same-address loads per row. Every quantity is formed with the same
+// operations in the same order as in the kernels above (bitwise the same results; tested).
+// Rows longer than EB entries take an in-place batched walk (not pipelined).
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t OOB = 0x7ff00000u;  // buffer offset past every range: the load returns 0
+
+__device__ __forceinline__ int bperm_i(int v, int src) {
+  return __builtin_amdgcn_ds_bpermute(src << 2, v);
+}
+__device__ __forceinline__ float bperm_f(float v, int src) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src << 2, __builtin_bit_cast(int, v)));
+}
+// max over the 8-lane group of an edge lane (order-free, so any butterfly)
+__device__ __forceinline__ float max8(float v) {
+  v = fmaxf(v, dppf<0xB1>(v));
+  v = fmaxf(v, dppf<0x4E>(v));
+  return fmaxf(v, dppf<0x141>(v));
+}
+
+// the rows of a half wave: 8 contiguous ranges of rows, range x walked by the workgroups on XCD x
+// (dealt round-robin over the XCDs; a launch has >= 8 workgroups), consecutive half waves on
+// consecutive rows — a graph's rows, and the source rows they gather, stay in one XCD's L2
+struct RowWalk {
+  int64_t r, rend, step;
+};
+__device__ __forceinline__ RowWalk row_walk(int64_t M) {
+  const int lane = threadIdx.x & 63, hw = (threadIdx.x >> 6) * 2 + (lane >> 5);
+  const int64_t xcd = blockIdx.x & 7, nb = ((int64_t)gridDim.x - xcd + 7) >> 3;
+  const int64_t span = ((M + 7) / 8 + RB - 1) / RB * RB;  // (k_gat_bwd_node's row sets)
+  RowWalk w;
+  const int64_t rbeg = xcd * span;
+  w.rend = rbeg + span < M ? rbeg + span : M;
+  w.r = rbeg + (int64_t)(blockIdx.x >> 3) * RB + hw;
+  w.step = nb * RB;
+  return w;
+}
+
+struct EdgeLane {
+  int li, hwb, u, hh, hq;  // lane in the half wave, half-wave base lane, edge slot, head slot
+  bool hv;                  // hh < H
+  __device__ __forceinline__ EdgeLane(int H) {
+    const int lane = threadIdx.x & 63;
+    li = lane & 31;
+    hwb = lane & 32;
+    u = li & 7;
+    hh = li >> 3;
+    hv = hh < H;
+    hq = hv ? hh : 0;
+  }
+  // CSR position of edge slot u of the batch starting at b (clamped into the row)
+  __device__ __forceinline__ int pos(int b, int e1) const { return b + (b + u < e1 ? u : 0); }
+};
+
+template <int ACT>
+__global__ __launch_bounds__(NT) void k_gat_fwd_p(const int32_t* __restrict__ rowptr,
+                                                  const int32_t* __restrict__ col,
+                                                  const float* __restrict__ XP,
+                                                  const float* __restrict__ a_s,
+                                                  const float* __restrict__ a_d, int64_t M, int H,
+                                                  int C, float slope,
+                                                  const float* __restrict__ mask,
+                                                  const float* __restrict__ bias,
+                                                  float* __restrict__ alpha, float* __restrict__ Y,
+                                                  uint16_t* __restrict__ Yb) {
+  const EdgeLane L(H);
+  const int HC = H * C;
+  const Pass<1> P(0, L.li, HC, C);
+  const int hbase = L.hwb + 8 * P.head;  // this feature lane's head: its edge lanes
+  RowWalk W = row_walk(M);
+  if (W.r >= W.rend) return;
+  const int64_t cap = rowptr[M];
+  const Buf bR = mkbuf(rowptr, (M + 1) * 4), bC = mkbuf(col, cap * 4);
+  const Buf bX = mkbuf(XP, M * HC * 4), bA = mkbuf(a_s, M * H * 4), bD = mkbuf(a_d, M * H * 4);
+  const Buf bAl = mkbuf(alpha, alpha ? cap * H * 4 : 0), bM = mkbuf(mask, mask ? cap * H * 4 : 0);
+  int64_t r = W.r;
+  int e0 = bldi(bR, (uint32_t)r * 4u), e1 = bldi(bR, (uint32_t)r * 4u + 4u);
+  int cu = bldi(bC, (uint32_t)L.pos(e0, e1) * 4u);
+  int64_t rn = r + W.step;
+  uint32_t ro = rn < W.rend ? (uint32_t)rn * 4u : OOB;
+  int e0n = bldi(bR, ro), e1n = bldi(bR, ro + 4u);
+  for (;;) {
+    const int deg = e1 - e0;
+    // row r: edge lanes load the logit inputs, feature lanes gather the first batch's rows
+    const int eu = L.pos(e0, e1);
+    const float a = bld1(bA, (uint32_t)(cu * H + L.hq) * 4u);
+    const float ad = bld1(bD, (uint32_t)(r * H + L.hq) * 4u);
+    const float mk = mask ? bld1(bM, (uint32_t)(eu * H + L.hq) * 4u) : 1.f;
+    f32x4 xv[EB];
+#pragma unroll
+    for (int k = 0; k < EB; ++k)
+      xv[k] = bld4(bX, ((uint32_t)bperm_i(cu, L.hwb + k) * HC + P.fc[0]) * 4u);
+    // row r + step: its first batch's columns; row r + 2 step: its extent
+    const int64_t rnn = rn + W.step;
+    const int cun = bldi(bC, rn < W.rend ? (uint32_t)L.pos(e0n, e1n) * 4u : OOB);
+    const uint32_t ron = rnn < W.rend ? (uint32_t)rnn * 4u : OOB;
+    const int e0nn = bldi(bR, ron), e1nn = bldi(bR, ron + 4u);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (deg <= EB) {
+      const bool ev = L.u < deg && L.hv;
+      const float lg = leaky(a + ad, slope);
+      const float m = max8(ev ? lg : -INFINITY);
+      const float ex = ev ? expf(lg - m) : 0.f;
+      float sum = 0.f;  // in CSR order (the zeros of absent edges add exactly nothing)
+#pragma unroll
+      for (int k = 0; k < EB; ++k) sum += bperm_f(ex, L.hwb + 8 * L.hh + k);
+      sum += EPS16;
+      const float al = ex / sum;
+      if (alpha && ev) bst1(bAl, (uint32_t)(eu * H + L.hh) * 4u, al);
+      const float alm = mask ? al * mk : al;
+#pragma unroll
+      for (int k = 0; k < EB; ++k) {
+        const float w = bperm_f(alm, hbase + k);
+        if (k < deg) acc += w * xv[k];
+      }
+    } else {  // long row: max, denominator, messages, each a walk over batches of EB entries
+      float m = -INFINITY;
+      for (int b = e0; b < e1; b += EB) {
+        const int c = bldi(bC, (uint32_t)L.pos(b, e1) * 4u);
+        const float lg = leaky(bld1(bA, (uint32_t)(c * H + L.hq) * 4u) + ad, slope);
+        if (b + L.u < e1 && L.hv) m = fmaxf(m, lg);
+      }
+      m = max8(m);
+      float sum = 0.f;
+      for (int b = e0; b < e1; b += EB) {
+        const int c = bldi(bC, (uint32_t)L.pos(b, e1) * 4u);
+        const float lg = leaky(bld1(bA, (uint32_t)(c * H + L.hq) * 4u) + ad, slope);
+        const float ex = b + L.u < e1 && L.hv ? expf(lg - m) : 0.f;
+#pragma unroll
+        for (int k = 0; k < EB; ++k) sum += bperm_f(ex, L.hwb + 8 * L.hh + k);
+      }
+      sum += EPS16;
+      for (int b = e0; b < e1; b += EB) {
+        const int eb = L.pos(b, e1);
+        const bool ev = b + L.u < e1 && L.hv;
+        const int c = bldi(bC, (uint32_t)eb * 4u);
+        const float lg = leaky(bld1(bA, (uint32_t)(c * H + L.hq) * 4u) + ad, slope);
+        const float mb = mask ? bld1(bM, (uint32_t)(eb * H + L.hq) * 4u) : 1.f;
+        f32x4 xb[EB];
+#pragma unroll
+        for (int k = 0; k < EB; ++k)
+          xb[k] = bld4(bX, ((uint32_t)bperm_i(c, L.hwb + k) * HC + P.fc[0]) * 4u);
+        const float al = (ev ? expf(lg - m) : 0.f) / sum;
+        if (alpha && ev) bst1(bAl, (uint32_t)(eb * H + L.hh) * 4u, al);
+        const float alm = mask ? al * mb : al;
+#pragma unroll
+        for (int k = 0; k < EB; ++k) {
+          const float w = bperm_f(alm, hbase + k);
+          if (b + k < e1) acc += w * xb[k];
+        }
+      }
+    }
+    const f32x4 out[1] = {acc};
+    gat_out<ACT, 1>(P, out, bias, Y, Yb, r * HC);
+    if (rn >= W.rend) break;
+    r = rn;
+    rn = rnn;
+    e0 = e0n;
+    e1 = e1n;
+    cu = cun;
+    e0n = e0nn;
+    e1n = e1nn;
+  }
+}
+
+// the output gradient of row r for this feature lane (dY, or the readout's, see PoolGrad), times
+// the activation's derivative
+template <int ACT, bool POOL>
+__device__ __forceinline__ f32x4 dz_row(int64_t r, int HC, int fc, const float* __restrict__ dY,
+                                        const float* __restrict__ Y, const PoolGrad& pg) {
+  f32x4 dz;
+  if constexpr (POOL) {
+    const int64_t g = pg.batch[r];
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < pg.nclass; ++c) {
+      const float d = pg.dlog[g * pg.nclass + c];
+      const f32x4 wv = ld4(pg.Wout + (int64_t)c * HC + fc);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = fmaf(d, wv[j], acc[j]);
+    }
+    if (pg.mean) {
+      const int cnt = pg.gptr[g + 1] - pg.gptr[g];
+      acc = acc / (float)(cnt > 0 ? cnt : 1);
+    }
+    dz = acc;
+  } else {
+    dz = ld4(dY + r * HC + fc);
+  }
+  if (ACT == LGNN_ACT_ELU) {
+    const f32x4 y = ld4(Y + r * HC + fc);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dz[j] *= elu_grad_from_out(y[j]);
+  }
+  return dz;
+}
+
+template <int ACT, bool POOL>
+__global__ __launch_bounds__(NT) void k_gat_bwd_edge_p(
+    const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+    const float* __restrict__ XP, const float* __restrict__ a_s, const float* __restrict__ a_d,
+    const float* __restrict__ alpha, const float* __restrict__ mask, const float* __restrict__ dY,
+    const float* __restrict__ Y, int64_t M, int H, int C, float slope, float* __restrict__ dZ,
+    float* __restrict__ da_e, float* __restrict__ da_d, PoolGrad pg) {
+  const EdgeLane L(H);
+  const int HC = H * C;
+  const Pass<1> P(0, L.li, HC, C);
+  const int hbase = L.hwb + 8 * P.head;
+  const int hlead = L.hwb + L.hq * P.G;  // the first feature lane of edge lane's head
+  RowWalk W = row_walk(M);
+  if (W.r >= W.rend) return;
+  const int64_t cap = rowptr[M];
+  const Buf bR = mkbuf(rowptr, (M + 1) * 4), bC = mkbuf(col, cap * 4);
+  const Buf bX = mkbuf(XP, M * HC * 4), bA = mkbuf(a_s, M * H * 4), bD = mkbuf(a_d, M * H * 4);
+  const Buf bAl = mkbuf(alpha, cap * H * 4), bM = mkbuf(mask, mask ? cap * H * 4 : 0);
+  const Buf bDa = mkbuf(da_e, cap * H * 4);
+  int64_t r = W.r;
+  int e0 = bldi(bR, (uint32_t)r * 4u), e1 = bldi(bR, (uint32_t)r * 4u + 4u);
+  int cu = bldi(bC, (uint32_t)L.pos(e0, e1) * 4u);
+  int64_t rn = r + W.step;
+  uint32_t ro = rn < W.rend ? (uint32_t)rn * 4u : OOB;
+  int e0n = bldi(bR, ro), e1n = bldi(bR, ro + 4u);
+  for (;;) {
+    const int deg = e1 - e0;
+    const int eu = L.pos(e0, e1);
+    const float al = bld1(bAl, (uint32_t)(eu * H + L.hq) * 4u);
+    const float mk = mask ? bld1(bM, (uint32_t)(eu * H + L.hq) * 4u) : 1.f;
+    const float pre = bld1(bA, (uint32_t)(cu * H + L.hq) * 4u) +
+                      bld1(bD, (uint32_t)(r * H + L.hq) * 4u);
+    f32x4 xv[EB];
+#pragma unroll
+    for (int k = 0; k < EB; ++k)
+      xv[k] = bld4(bX, ((uint32_t)bperm_i(cu, L.hwb + k) * HC + P.fc[0]) * 4u);
+    f32x4 dz = dz_row<ACT, POOL>(r, HC, P.fc[0], dY, Y, pg);
+    const int64_t rnn = rn + W.step;
+    const int cun = bldi(bC, rn < W.rend ? (uint32_t)L.pos(e0n, e1n) * 4u : OOB);
+    const uint32_t ron = rnn < W.rend ? (uint32_t)rnn * 4u : OOB;
+    const int e0nn = bldi(bR, ron), e1nn = bldi(bR, ron + 4u);
+    if (!P.act[0]) dz = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (P.act[0]) st4(dZ + r * HC + P.f[0], dz);
+    float dad = 0.f;
+    if (deg <= EB) {
+      float d[EB], alk[EB];
+      float s_i = 0.f;
+#pragma unroll
+      for (int k = 0; k < EB; ++k) {
+        d[k] = group_sum(dot4(dz, xv[k]), P.G);
+        if (mask) d[k] *= bperm_f(mk, hbase + k);
+        alk[k] = bperm_f(al, hbase + k);
+        if (k < deg) s_i += alk[k] * d[k];
+      }
+      float mine = 0.f;  // edge lane (u, h): the logit gradient of its edge and head
+#pragma unroll
+      for (int k = 0; k < EB; ++k) {
+        const float fk = bperm_f(pre > 0.f ? 1.f : slope, hbase + k);
+        const float da = alk[k] * (d[k] - s_i) * fk;
+        if (k < deg) dad += da;
+        const float t = bperm_f(da, hlead);
+        mine = L.u == k ? t : mine;
+      }
+      if (L.u < deg && L.hv) bst1(bDa, (uint32_t)(eu * H + L.hh) * 4u, mine);
+    } else {  // long row: two walks over batches of EB entries (s_i, then the gradients)
+      float s_i = 0.f;
+#pragma unroll 1
+      for (int sweep = 0; sweep < 2; ++sweep) {
+        for (int b = e0; b < e1; b += EB) {
+          const int eb = L.pos(b, e1);
+          const int c = bldi(bC, (uint32_t)eb * 4u);
+          const float alb = bld1(bAl, (uint32_t)(eb * H + L.hq) * 4u);
+          const float mb = mask ? bld1(bM, (uint32_t)(eb * H + L.hq) * 4u) : 1.f;
+          const float preb = bld1(bA, (uint32_t)(c * H + L.hq) * 4u) +
+                             bld1(bD, (uint32_t)(r * H + L.hq) * 4u);
+          f32x4 xb[EB];
+#pragma unroll
+          for (int k = 0; k < EB; ++k)
+            xb[k] = bld4(bX, ((uint32_t)bperm_i(c, L.hwb + k) * HC + P.fc[0]) * 4u);
+          float mine = 0.f;
+#pragma unroll
+          for (int k = 0; k < EB; ++k) {
+            float dk = group_sum(dot4(dz, xb[k]), P.G);
+            if (mask) dk *= bperm_f(mb, hbase + k);
+            const float ak = bperm_f(alb, hbase + k);
+            const float fk = bperm_f(preb > 0.f ? 1.f : slope, hbase + k);
+            if (sweep == 0) {
+              if (b + k < e1) s_i += ak * dk;
+            } else {
+              const float da = ak * (dk - s_i) * fk;
+              if (b + k < e1) dad += da;
+              const float t = bperm_f(da, hlead);
+              mine = L.u == k ? t : mine;
+            }
+          }
+          if (sweep == 1 && b + L.u < e1 && L.hv)
+            bst1(bDa, (uint32_t)(eb * H + L.hh) * 4u, mine);
+        }
+      }
+    }
+    if (P.leader) da_d[r * H + P.head] = dad;
+    if (rn >= W.rend) break;
+    r = rn;
+    rn = rnn;
+    e0 = e0n;
+    e1 = e1n;
+    cu = cun;
+    e0n = e0nn;
+    e1n = e1nn;
+  }
+}
+
+// source-row pass (see k_gat_bwd_node), one 128-feature strip, pipelined: the next row's first
+// batch of transpose entries (target row, target-CSR position) is in flight during this row's
+// gathers. Same per-workgroup partials (grid = lgnn_gat_bwd_num_partials).
+__global__ __launch_bounds__(NT) void k_gat_bwd_node_p(
+    const int32_t* __restrict__ tptr, const int32_t* __restrict__ tidx,
+    const int32_t* __restrict__ tmap, const float* __restrict__ alpha,
+    const float* __restrict__ mask, const float* __restrict__ da_e,
+    const float* __restrict__ da_d, const float* __restrict__ dZ, const float* __restrict__ XP,
+    const float* __restrict__ att_src, const float* __restrict__ att_dst, int64_t M, int H,
+    int C, float* __restrict__ dXP, float* __restrict__ part, uint16_t* __restrict__ dXPb) {
+  __shared__ __attribute__((aligned(16))) float red[RB][3 * 128];
+  const EdgeLane L(H);
+  const int HC = H * C;
+  const Pass<1> P(0, L.li, HC, C);
+  const int hbase = L.hwb + 8 * P.head;
+  const int hw = (threadIdx.x >> 6) * 2 + ((threadIdx.x & 63) >> 5);
+  f32x4 ps = {0.f, 0.f, 0.f, 0.f}, pd = ps, pb = ps;
+  RowWalk W = row_walk(M);
+  if (W.r < W.rend) {
+    const int64_t cap = tptr[M];
+    const Buf bR = mkbuf(tptr, (M + 1) * 4), bT = mkbuf(tidx, cap * 4), bP = mkbuf(tmap, cap * 4);
+    const Buf bZ = mkbuf(dZ, M * HC * 4), bAl = mkbuf(alpha, cap * H * 4);
+    const Buf bM = mkbuf(mask, mask ? cap * H * 4 : 0), bDa = mkbuf(da_e, cap * H * 4);
+    const f32x4 as = ld4(att_src + P.fc[0]), adv = ld4(att_dst + P.fc[0]);
+    int64_t r = W.r;
+    int q0 = bldi(bR, (uint32_t)r * 4u), q1 = bldi(bR, (uint32_t)r * 4u + 4u);
+    int tu = bldi(bT, (uint32_t)L.pos(q0, q1) * 4u), pu = bldi(bP, (uint32_t)L.pos(q0, q1) * 4u);
+    int64_t rn = r + W.step;
+    uint32_t ro = rn < W.rend ? (uint32_t)rn * 4u : OOB;
+    int q0n = bldi(bR, ro), q1n = bldi(bR, ro + 4u);
+    for (;;) {
+      const int deg = q1 - q0;
+      float alu = bld1(bAl, (uint32_t)(pu * H + L.hq) * 4u);
+      const float mk = mask ? bld1(bM, (uint32_t)(pu * H + L.hq) * 4u) : 1.f;
+      const float dau = bld1(bDa, (uint32_t)(pu * H + L.hq) * 4u);
+      f32x4 dv[EB];
+#pragma unroll
+      for (int k = 0; k < EB; ++k)
+        dv[k] = bld4(bZ, ((uint32_t)bperm_i(tu, L.hwb + k) * HC + P.fc[0]) * 4u);
+      const float dd = da_d[r * H + P.head];
+      const f32x4 xp = ld4(XP + r * HC + P.fc[0]);
+      const f32x4 zr = ld4(dZ + r * HC + P.fc[0]);
+      const int64_t rnn = rn + W.step;
+      const uint32_t qn = rn < W.rend ? (uint32_t)L.pos(q0n, q1n) * 4u : OOB;
+      const int tun = bldi(bT, qn), pun = bldi(bP, qn);
+      const uint32_t ron = rnn < W.rend ? (uint32_t)rnn * 4u : OOB;
+      const int q0nn = bldi(bR, ron), q1nn = bldi(bR, ron + 4u);
+      if (mask) alu *= mk;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      float sda = 0.f;
+#pragma unroll
+      for (int k = 0; k < EB; ++k) {
+        const float ak = bperm_f(alu, hbase + k), dk = bperm_f(dau, hbase + k);
+        if (k < deg) {
+          acc += ak * dv[k];
+          sda += dk;
+        }
+      }
+      for (int b = q0 + EB; b < q1; b += EB) {  // entries past the first batch
+        const int qb = L.pos(b, q1);
+        const int tb = bldi(bT, (uint32_t)qb * 4u), pb_ = bldi(bP, (uint32_t)qb * 4u);
+        float alb = bld1(bAl, (uint32_t)(pb_ * H + L.hq) * 4u);
+        if (mask) alb *= bld1(bM, (uint32_t)(pb_ * H + L.hq) * 4u);
+        const float dab = bld1(bDa, (uint32_t)(pb_ * H + L.hq) * 4u);
+        f32x4 db[EB];
+#pragma unroll
+        for (int k = 0; k < EB; ++k)
+          db[k] = bld4(bZ, ((uint32_t)bperm_i(tb, L.hwb + k) * HC + P.fc[0]) * 4u);
+#pragma unroll
+        for (int k = 0; k < EB; ++k) {
+          const float ak = bperm_f(alb, hbase + k), dk = bperm_f(dab, hbase + k);
+          if (b + k < q1) {
+            acc += ak * db[k];
+            sda += dk;
+          }
+        }
+      }
+      const f32x4 o = acc + sda * as + dd * adv;
+      if (P.act[0]) {
+        st4(dXP + r * HC + P.f[0], o);
+        if (dXPb) st4_bf16(dXPb + r * HC + P.f[0], o);
+        ps += sda * xp;
+        pd += dd * xp;
+        pb += zr;
+      }
+      if (rn >= W.rend) break;
+      r = rn;
+      rn = rnn;
+      q0 = q0n;
+      q1 = q1n;
+      tu = tun;
+      pu = pun;
+      q0n = q0nn;
+      q1n = q1nn;
+    }
+  }
+  st4(&red[hw][0 * 128 + 4 * L.li], ps);
+  st4(&red[hw][1 * 128 + 4 * L.li], pd);
+  st4(&red[hw][2 * 128 + 4 * L.li], pb);
+  __syncthreads();
+  for (int i = threadIdx.x; i < 3 * HC; i += NT) {
+    const int kind = i / HC, f = i % HC;
+    const int idx = kind * 128 + f;
+    float t = red[0][idx];
+#pragma unroll
+    for (int q = 1; q < RB; ++q) t += red[q][idx];
+    part[(int64_t)blockIdx.x * 3 * HC + i] = t;
+  }
+}
+
+// the pipelined kernels' shapes, and whether they are enabled (LGNN_GAT_PIPE=0: the kernels above)
+inline bool pipe_ok(int H, int C) {
+  const char* e = getenv("LGNN_GAT_PIPE");
+  return H <= 4 && H * C <= 128 && !(e && e[0] == '0');
+}
+
+// persistent grid of a row-pipelined kernel: the workgroups one launch keeps resident (occupancy
+// API, cached per device and kernel), LGNN_GAT_BPC per CU if set
+template <typename K>
+inline unsigned pipe_grid(K kernel, int slot, int64_t M) {
+  static int cap[16][8];
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  dev &= 15;
+  if (cap[dev][slot] <= 0) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, NT, 0) != hipSuccess || per < 1)
+      per = 4;
+    cap[dev][slot] = cus * per;
+  }
+  int64_t c = cap[dev][slot];
+  if (const char* e = getenv("LGNN_GAT_BPC")) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        atoi(e) > 0)
+      c = (int64_t)cus * atoi(e);
+  }
+  int64_t g = (M + RB - 1) / RB;
+  if (g > c) g = c;
+  return (unsigned)(g < 8 ? 8 : g);
+}
+
 // C a power of two in [4, 512] (the reference sweep: widths 32..512, heads 1/2/4/8), H*C <= 512
 inline bool shape_ok(int H, int C) {
   return H > 0 && C >= 4 && C <= 512 && (C & (C - 1)) == 0 && H * C <= MAXS * 128;
@@ -606,6 +1067,20 @@ extern "C" int lgnn_gat_fwd(const int32_t* rowptr, const int32_t* col, const flo
   if (M > 0 && (!rowptr || !col || !XP || !a_s || !a_d || !Y)) return LGNN_EINVAL;
   if (!bytes_ok(M, H, C)) return LGNN_EINVAL;
   if (M == 0) return LGNN_OK;
+  if (pipe_ok(H, C)) {
+    if (act == LGNN_ACT_ELU)
+      hipLaunchKernelGGL(k_gat_fwd_p<LGNN_ACT_ELU>,
+                         dim3(pipe_grid(k_gat_fwd_p<LGNN_ACT_ELU>, 0, M)), dim3(NT), 0,
+                         as_stream(stream), rowptr, col, XP, a_s, a_d, M, H, C, negative_slope,
+                         edge_mask, bias, alpha, Y, Y_bf16);
+    else
+      hipLaunchKernelGGL(k_gat_fwd_p<LGNN_ACT_NONE>,
+                         dim3(pipe_grid(k_gat_fwd_p<LGNN_ACT_NONE>, 1, M)), dim3(NT), 0,
+                         as_stream(stream), rowptr, col, XP, a_s, a_d, M, H, C, negative_slope,
+                         edge_mask, bias, alpha, Y, Y_bf16);
+    LGNN_LAUNCH_CHECK();
+    return LGNN_OK;
+  }
 #define LGNN_GF(A_, NS_)                                                                     \
   hipLaunchKernelGGL((k_gat_fwd<A_, NS_>), dim3(row_grid(M)), dim3(NT), 0, as_stream(stream),    \
                      rowptr, col, XP, a_s, a_d, M, H, C, negative_slope, edge_mask, bias, alpha, Y, \
@@ -642,6 +1117,21 @@ int gat_bwd_edge_launch(const int32_t* rowptr, const int32_t* col, const float* 
   if (!bytes_ok(M, H, C)) return LGNN_EINVAL;
   if (M == 0) return LGNN_OK;
   const PoolGrad p = pg ? *pg : PoolGrad{};
+  if (pipe_ok(H, C)) {
+#define LGNN_GBP(A_, POOL_, SLOT_)                                                             \
+  hipLaunchKernelGGL((k_gat_bwd_edge_p<A_, POOL_>),                                             \
+                     dim3(pipe_grid(k_gat_bwd_edge_p<A_, POOL_>, SLOT_, M)), dim3(NT), 0,        \
+                     as_stream(stream), rowptr, col, XP, a_s, a_d, alpha, edge_mask, dY, Y, M, H, \
+                     C, slope, dZ, da_e, da_d, p)
+    if (act == LGNN_ACT_ELU) {
+      if (pg) LGNN_GBP(LGNN_ACT_ELU, true, 2); else LGNN_GBP(LGNN_ACT_ELU, false, 3);
+    } else {
+      if (pg) LGNN_GBP(LGNN_ACT_NONE, true, 4); else LGNN_GBP(LGNN_ACT_NONE, false, 5);
+    }
+#undef LGNN_GBP
+    LGNN_LAUNCH_CHECK();
+    return LGNN_OK;
+  }
 #define LGNN_GB(A_, NS_)                                                                        \
   do {                                                                                          \
     if (pg)                                                                                     \
@@ -698,7 +1188,9 @@ extern "C" int lgnn_gat_bwd_num_partials(int64_t M) {
   if (M < 0) return LGNN_EINVAL;
   // persistent rows; enough workgroups to keep LGNN_GAT_WPE waves per SIMD resident
   const int64_t b = (M + RB - 1) / RB;
-  return (int)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
+  // (>= 8: the row-pipelined kernel deals rows to the 8 XCDs' workgroups; <= 1024: 4 per CU,
+  // what its registers keep resident — a second round of workgroups would not be pipelined)
+  return (int)(b < 8 ? 8 : (b > 1024 ? 1024 : b));
 }
 
 extern "C" int lgnn_gat_bwd_node(const int32_t* tptr, const int32_t* tidx, const int32_t* tmap,
@@ -712,6 +1204,13 @@ extern "C" int lgnn_gat_bwd_node(const int32_t* tptr, const int32_t* tidx, const
   if (M > 0 && (!tptr || !tidx || !tmap || !alpha || !da_e || !da_d || !dZ || !XP || !dXP))
     return LGNN_EINVAL;
   if (!bytes_ok(M, H, C)) return LGNN_EINVAL;
+  if (pipe_ok(H, C) && M > 0) {
+    hipLaunchKernelGGL(k_gat_bwd_node_p, dim3(num_partials), dim3(NT), 0, as_stream(stream), tptr,
+                       tidx, tmap, alpha, edge_mask, da_e, da_d, dZ, XP, att_src, att_dst, M, H, C,
+                       dXP, partials, dXP_bf16);
+    LGNN_LAUNCH_CHECK();
+    return LGNN_OK;
+  }
 #define LGNN_GN(NST_)                                                                        \
   hipLaunchKernelGGL(k_gat_bwd_node<NST_>, dim3(num_partials), dim3(NT), 0, as_stream(stream),  \
                      tptr, tidx, tmap, alpha, edge_mask, da_e, da_d, dZ, XP, att_src, att_dst, M, \
