@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 25
+#define LGNN_ABI_VERSION 26
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -606,6 +606,9 @@ int lgnn_gcn_stack_bwd_s3f_all(const float* dP, const int64_t* batch, const int3
  *   Y = A W^T) or B = W^T (transposed 1: Y = A W), i.e. [ceil(out/128)][planes][128][kpad(in)]
  *   bf16 in MFMA fragment order, zero-padded; lgnn_s3_weight_planes_numel(out, in, planes) its
  *   size in elements (out = B's rows, in = B's columns).
+ * lgnn_s3_weight_planes_multi: n (<= LGNN_MAX_WPREP) such operands in ONE launch (job j: W[j],
+ *   rows[j], cols[j], transposed[j] -> Wp[j]; planes shared) — a model's every weight operand of a
+ *   step (forward B = W and backward B = W^T) at once instead of one small launch per GEMM.
  * lgnn_s3_gemm: Y[M][N] = A[M][K] B[N][K]^T (+ bias[N]), A fp32 (split or rounded as loaded).
  *   colsum_part (nullable): [ceil(M/64)][N] per-64-row-tile column sums of Y (fixed order).
  * lgnn_s3_wgrad: partial slabs of dW[N][K] = dY^T X (dY [M][N], X [M][K] fp32, N even):
@@ -616,6 +619,10 @@ int lgnn_gcn_stack_bwd_s3f_all(const float* dP, const int64_t* batch, const int3
 size_t lgnn_s3_weight_planes_numel(int out_features, int in_features, int planes);
 int lgnn_s3_weight_planes(const float* W, int rows, int cols, int transposed, int planes,
                           uint16_t* Wp, void* stream);
+#define LGNN_MAX_WPREP 16
+int lgnn_s3_weight_planes_multi(int n, const float* const* W, const int* rows, const int* cols,
+                                const int* transposed, int planes, uint16_t* const* Wp,
+                                void* stream);
 int lgnn_s3_gemm(const float* A, int64_t M, int K, const uint16_t* Wp, int N, int planes,
                  const float* bias, float* Y, float* colsum_part, void* stream);
 int lgnn_s3_wgrad_partials(int64_t M, int K, int N);

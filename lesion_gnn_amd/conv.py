@@ -190,21 +190,24 @@ class GATConv(nn.Module):
                              dropout.key(self, self.dropout))[0]
 
     def forward(self, x: torch.Tensor, edge_index, act: int = _lib.LGNN_ACT_NONE,
-                bf16: bool = False, mask: torch.Tensor | None = None) -> torch.Tensor:
+                bf16: bool = False, mask: torch.Tensor | None = None,
+                planes: tuple | None = None) -> torch.Tensor:
+        """planes: (lin.weight's, its transpose's) split-3 planes from ops.s3_weight_bundle."""
         g = as_graph(edge_index, x.size(0))
         mask = self._mask(x, g, mask)
         return ops.gat_conv(x, self.lin.weight, self.att_src, self.att_dst, self.bias, g,
-                            self.heads, self.negative_slope, mask, act, bf16)
+                            self.heads, self.negative_slope, mask, act, bf16, planes)
 
     def forward_head(self, x: torch.Tensor, g, act: int, W_out: torch.Tensor,
                      b_out: torch.Tensor, mean: bool, bf16: bool = False,
-                     mask: torch.Tensor | None = None) -> torch.Tensor:
+                     mask: torch.Tensor | None = None, planes: tuple | None = None
+                     ) -> torch.Tensor:
         """forward(x) followed by global pool + out_proj (W_out, b_out) in one autograd node
         (ops.gat_conv_head): the model's last conv and readout. Returns the logits."""
         mask = self._mask(x, g, mask)
         return ops.gat_conv_head(x, self.lin.weight, self.att_src, self.att_dst, self.bias,
                                  W_out, b_out, g, self.heads, self.negative_slope, mask, act,
-                                 bf16, mean)
+                                 bf16, mean, planes)
 
 
 def global_mean_pool(x: torch.Tensor, batch: torch.Tensor, size: int | None = None,

@@ -369,12 +369,12 @@ __global__ __launch_bounds__(NT, 2) void k_s3_wgrad2(const float* __restrict__ d
 // weight planes: Wp[nb][p][128][Kp] of W [N][K] (or of W^T [K][N] with transposed = 1: the
 // operand of dX = dY W), fragment order, zero-padded, PLANES = 3 (split) or 1 (bf16 RNE)
 // ------------------------------------------------------------------------------------------
-__global__ void k_s3_wprep(const float* __restrict__ W, int rows, int cols, int transposed,
-                           int planes, int Kp, int nnb, uint16_t* __restrict__ Wp) {
+__device__ __forceinline__ void wprep_range(const float* __restrict__ W, int rows, int cols,
+                                            int transposed, int planes, int Kp, int nnb,
+                                            uint16_t* __restrict__ Wp, int64_t i0, int64_t stride) {
   const int64_t per = (int64_t)128 * Kp;  // elements of one plane of one block
   const int64_t total = per * nnb;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t i = i0; i < total; i += stride) {
     const int nb = (int)(i / per);
     const int64_t j = i % per;
     const int e = (int)(j & 7), lane = (int)((j >> 3) & 63), wave = (int)((j >> 9) & 3);
@@ -397,6 +397,29 @@ __global__ void k_s3_wprep(const float* __restrict__ W, int rows, int cols, int 
   }
 }
 
+__global__ void k_s3_wprep(const float* __restrict__ W, int rows, int cols, int transposed,
+                           int planes, int Kp, int nnb, uint16_t* __restrict__ Wp) {
+  wprep_range(W, rows, cols, transposed, planes, Kp, nnb, Wp,
+              (int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
+}
+
+struct WprepJobs {
+  const float* W[LGNN_MAX_WPREP];
+  uint16_t* Wp[LGNN_MAX_WPREP];
+  int rows[LGNN_MAX_WPREP], cols[LGNN_MAX_WPREP], tr[LGNN_MAX_WPREP];
+  int Kp[LGNN_MAX_WPREP], nnb[LGNN_MAX_WPREP];
+  int boff[LGNN_MAX_WPREP + 1];  // prefix of the workgroups per job
+  int n, planes;
+};
+
+__global__ void k_s3_wprep_multi(WprepJobs J) {
+  int j = 0;
+  while (j + 1 < J.n && J.boff[j + 1] <= (int)blockIdx.x) ++j;
+  const int lb = (int)blockIdx.x - J.boff[j], nb = J.boff[j + 1] - J.boff[j];
+  wprep_range(J.W[j], J.rows[j], J.cols[j], J.tr[j], J.planes, J.Kp[j], J.nnb[j], J.Wp[j],
+              (int64_t)lb * blockDim.x + threadIdx.x, (int64_t)nb * blockDim.x);
+}
+
 }  // namespace lgnn_s3g
 
 using namespace lgnn_s3g;
@@ -404,6 +427,34 @@ using namespace lgnn_s3g;
 // ------------------------------------------------------------------------------------------
 // C ABI
 // ------------------------------------------------------------------------------------------
+extern "C" int lgnn_s3_weight_planes_multi(int n, const float* const* W, const int* rows,
+                                           const int* cols, const int* transposed, int planes,
+                                           uint16_t* const* Wp, void* stream) {
+  if (n < 1 || n > LGNN_MAX_WPREP || !W || !rows || !cols || !transposed || !Wp ||
+      (planes != 1 && planes != 3))
+    return LGNN_EINVAL;
+  WprepJobs J = {};
+  J.n = n;
+  J.planes = planes;
+  for (int j = 0; j < n; ++j) {
+    if (!W[j] || !Wp[j] || rows[j] < 1 || cols[j] < 1) return LGNN_EINVAL;
+    const int out = transposed[j] ? cols[j] : rows[j], in = transposed[j] ? rows[j] : cols[j];
+    J.W[j] = W[j];
+    J.Wp[j] = Wp[j];
+    J.rows[j] = rows[j];
+    J.cols[j] = cols[j];
+    J.tr[j] = transposed[j] ? 1 : 0;
+    J.Kp[j] = (in + BK - 1) / BK * BK;
+    J.nnb[j] = (out + 127) / 128;
+    const int64_t total = (int64_t)128 * J.Kp[j] * J.nnb[j];
+    J.boff[j + 1] = J.boff[j] + (int)std::min<int64_t>((total + 255) / 256, 512);
+  }
+  hipLaunchKernelGGL(k_s3_wprep_multi, dim3((unsigned)J.boff[n]), dim3(256), 0, as_stream(stream),
+                     J);
+  LGNN_LAUNCH_CHECK();
+  return LGNN_OK;
+}
+
 extern "C" size_t lgnn_s3_weight_planes_numel(int out_features, int in_features, int planes) {
   if (out_features < 1 || in_features < 1 || (planes != 1 && planes != 3)) return 0;
   const int Kp = (in_features + BK - 1) / BK * BK, nnb = (out_features + 127) / 128;

@@ -226,15 +226,32 @@ def _node_linear_backward(ctx, dy):
 node_linear.register_autograd(_node_linear_backward, setup_context=_node_linear_setup)
 
 
+@custom_op("lgnn::s3_weight_planes_multi", mutates_args=(), device_types="cuda")
+def s3_weight_planes_multi(Ws: list[Tensor], transposed: list[bool], bf16: bool) -> Tensor:
+    """ops.s3_weight_bundle: every split-3 weight operand of a step in one flat buffer."""
+    from .ops import s3_bundle_raw
+
+    return s3_bundle_raw(Ws, transposed, bf16)
+
+
+@s3_weight_planes_multi.register_fake
+def _(Ws, transposed, bf16):
+    from .ops import _s3_bundle_sizes
+
+    n = sum(_s3_bundle_sizes([tuple(W.shape) for W in Ws], transposed, bf16))
+    return Ws[0].new_empty(n, dtype=torch.int16)
+
+
 @custom_op("lgnn::dense_linear", mutates_args=(), device_types="cuda")
-def dense_linear(x: Tensor, W: Tensor, b: Optional[Tensor], bf16: bool) -> Tensor:
+def dense_linear(x: Tensor, W: Tensor, b: Optional[Tensor], bf16: bool,
+                 wp: Optional[Tensor]) -> Tensor:
     from .ops import _DenseLinear
 
-    return _DenseLinear.forward(_Ctx(), x, W, b, bf16)
+    return _DenseLinear.forward(_Ctx(), x, W, b, bf16, wp)
 
 
 @dense_linear.register_fake
-def _(x, W, b, bf16):
+def _(x, W, b, bf16, wp=None):
     return x.new_empty(x.shape[0], W.shape[0], dtype=torch.float32)
 
 
@@ -259,7 +276,7 @@ def _(dy, x, W, has_b, bf16, want_dx):
 
 
 def _dense_setup(ctx, inputs, output):
-    x, W, b, bf16 = inputs
+    x, W, b, bf16, _wp = inputs
     ctx.save_for_backward(x, W)
     ctx.meta = (b is not None, bf16)
 
@@ -268,7 +285,7 @@ def _dense_backward(ctx, dy):
     x, W = ctx.saved_tensors
     has_b, bf16 = ctx.meta
     dx, dW, db = torch.ops.lgnn.dense_linear_bwd(dy, x, W, has_b, bf16, ctx.needs_input_grad[0])
-    return _opt(dx), dW, _opt(db), None
+    return _opt(dx), dW, _opt(db), None, None
 
 
 dense_linear.register_autograd(_dense_backward, setup_context=_dense_setup)
@@ -454,19 +471,19 @@ mask_mul.register_autograd(_mask_mul_backward, setup_context=_mask_mul_setup)
 @custom_op("lgnn::gat_conv", mutates_args=(), device_types="cuda")
 def gat_conv(x: Tensor, W: Tensor, att_src: Tensor, att_dst: Tensor, bias: Optional[Tensor],
              g: list[Tensor], heads: int, slope: float, mask: Optional[Tensor], act: int,
-             bf16: bool) -> list[Tensor]:
+             bf16: bool, wp: Optional[Tensor], wpt: Optional[Tensor]) -> list[Tensor]:
     """[Y, XP, a_s, a_d, alpha] (the eager _GATConv forward and what it saves)."""
     from .ops import _GATConv
 
     ctx = _Ctx()
     Y = _GATConv.forward(ctx, x, W, att_src, att_dst, bias, TGraph(g, "gat"), heads, slope, mask,
-                         act, bf16)
+                         act, bf16, wp)
     _x, _W, _as, _ad, XP, a_s, a_d, alpha, _Y, _m = ctx.saved_tensors
     return [Y, XP, a_s, a_d, alpha]
 
 
 @gat_conv.register_fake
-def _(x, W, att_src, att_dst, bias, g, heads, slope, mask, act, bf16):
+def _(x, W, att_src, att_dst, bias, g, heads, slope, mask, act, bf16, wp=None, wpt=None):
     M, HC = x.shape[0], W.shape[0]
     cap = g[GPARTS.index("col")].shape[0]
     return [x.new_empty(M, HC), x.new_empty(M, HC), x.new_empty(M, heads),
@@ -477,11 +494,13 @@ def _(x, W, att_src, att_dst, bias, g, heads, slope, mask, act, bf16):
 def gat_conv_bwd(dY: Tensor, x: Tensor, W: Tensor, att_src: Tensor, att_dst: Tensor,
                  XP: Tensor, a_s: Tensor, a_d: Tensor, alpha: Tensor, Y: Tensor,
                  mask: Optional[Tensor], g: list[Tensor], heads: int, slope: float, act: int,
-                 bf16: bool, has_bias: bool, want_dx: bool) -> list[Tensor]:
+                 bf16: bool, has_bias: bool, want_dx: bool,
+                 wpt: Optional[Tensor]) -> list[Tensor]:
     from .ops import GAT_S3, _GATConv, fast_shape
 
     HC = W.shape[0]
     ctx = _Ctx((want_dx,))
+    ctx.wpt = wpt
     ctx.save_for_backward(x.contiguous(), W.contiguous(), att_src.reshape(-1),
                           att_dst.reshape(-1), XP, a_s, a_d, alpha, Y, mask)
     ctx.graph, ctx.heads, ctx.slope, ctx.act = TGraph(g, "gat"), heads, slope, act
@@ -497,34 +516,123 @@ def gat_conv_bwd(dY: Tensor, x: Tensor, W: Tensor, att_src: Tensor, att_dst: Ten
 
 @gat_conv_bwd.register_fake
 def _(dY, x, W, att_src, att_dst, XP, a_s, a_d, alpha, Y, mask, g, heads, slope, act, bf16,
-      has_bias, want_dx):
+      has_bias, want_dx, wpt=None):
     dev = x.device
     return [torch.empty_like(x) if want_dx else _none(dev), torch.empty_like(W),
             W.new_empty(3 * W.shape[0])]
 
 
 def _gat_setup(ctx, inputs, output):
-    x, W, att_src, att_dst, bias, g, heads, slope, mask, act, bf16 = inputs
+    x, W, att_src, att_dst, bias, g, heads, slope, mask, act, bf16, _wp, wpt = inputs
     Y, XP, a_s, a_d, alpha = output
     ctx.save_for_backward(x, W, att_src, att_dst, XP, a_s, a_d, alpha, Y,
-                          _enc(mask, x.device), *g)
+                          _enc(mask, x.device), _enc(wpt, x.device), *g)
     ctx.meta = (heads, slope, act, bf16, bias is not None)
 
 
 def _gat_backward(ctx, grads):
-    x, W, att_src, att_dst, XP, a_s, a_d, alpha, Y, mask, *g = ctx.saved_tensors
+    x, W, att_src, att_dst, XP, a_s, a_d, alpha, Y, mask, wpt, *g = ctx.saved_tensors
     heads, slope, act, bf16, has_bias = ctx.meta
     dx, dW, red = torch.ops.lgnn.gat_conv_bwd(
         grads[0], x, W, att_src, att_dst, XP, a_s, a_d, alpha, Y, _opt(mask), g, heads, slope,
-        act, bf16, has_bias, ctx.needs_input_grad[0])
+        act, bf16, has_bias, ctx.needs_input_grad[0], _opt(wpt))
     HC = W.shape[0]
     da_s = red[:HC].view(att_src.shape)
     da_d = red[HC:2 * HC].view(att_dst.shape)
     db = red[2 * HC:] if has_bias else None
-    return (_opt(dx), dW, da_s, da_d, db, [None] * len(g), None, None, None, None, None)
+    return (_opt(dx), dW, da_s, da_d, db, [None] * len(g), None, None, None, None, None, None,
+            None)
 
 
 gat_conv.register_autograd(_gat_backward, setup_context=_gat_setup)
+
+
+@custom_op("lgnn::gat_conv_head", mutates_args=(), device_types="cuda")
+def gat_conv_head(x: Tensor, W: Tensor, att_src: Tensor, att_dst: Tensor, bias: Optional[Tensor],
+                  W_out: Tensor, b_out: Tensor, g: list[Tensor], heads: int, slope: float,
+                  mask: Optional[Tensor], act: int, bf16: bool, mean: bool,
+                  wp: Optional[Tensor], wpt: Optional[Tensor]) -> list[Tensor]:
+    """The GAT model's last conv + global pool + out_proj as one node (ops._GATConvHead):
+    [logits, Y, XP, a_s, a_d, alpha, pooled]."""
+    from .ops import _GATConvHead
+
+    ctx = _Ctx()
+    logits = _GATConvHead.forward(ctx, x, W, att_src, att_dst, bias, W_out, b_out,
+                                  TGraph(g, "gat"), heads, slope, mask, act, bf16, mean, wp)
+    s = ctx.saved_tensors  # x, W, att_src, att_dst, XP, a_s, a_d, alpha, Y, mask, pooled, W_out
+    return [logits, s[8], s[4], s[5], s[6], s[7], s[10]]
+
+
+@gat_conv_head.register_fake
+def _(x, W, att_src, att_dst, bias, W_out, b_out, g, heads, slope, mask, act, bf16, mean,
+      wp=None, wpt=None):
+    M, HC = x.shape[0], W.shape[0]
+    cap = g[GPARTS.index("col")].shape[0]
+    B = g[GPARTS.index("gptr")].shape[0] - 1
+    return [x.new_empty(B, W_out.shape[0]), x.new_empty(M, HC), x.new_empty(M, HC),
+            x.new_empty(M, heads), x.new_empty(M, heads), x.new_empty(cap, heads),
+            x.new_empty(B, HC)]
+
+
+@custom_op("lgnn::gat_conv_head_bwd", mutates_args=(), device_types="cuda")
+def gat_conv_head_bwd(dlogits: Tensor, x: Tensor, W: Tensor, att_src: Tensor, att_dst: Tensor,
+                      XP: Tensor, a_s: Tensor, a_d: Tensor, alpha: Tensor, Y: Tensor,
+                      mask: Optional[Tensor], pooled: Tensor, W_out: Tensor, g: list[Tensor],
+                      heads: int, slope: float, act: int, bf16: bool, has_bias: bool, mean: bool,
+                      want_dx: bool, wpt: Optional[Tensor]) -> list[Tensor]:
+    """[dx, dW, red (= [datt_src | datt_dst | dbias]), dW_out, db_out]: the readout's backward
+    formed inside the edge kernel's load (lgnn_gat_bwd_edge_pool), no dH tensor."""
+    from .ops import GAT_S3, _GATConvHead, _SubCtx, fast_shape
+
+    HC = W.shape[0]
+    sub = _SubCtx(want_dx)
+    sub.graph, sub.heads, sub.slope, sub.act = TGraph(g, "gat"), heads, slope, act
+    sub.bf16, sub.dense = bf16, bf16 or not fast_shape(W.shape[1], HC) or GAT_S3
+    sub.has_bias = has_bias
+    sub.att_shape = tuple(att_src.shape)
+    sub.wt = None
+    sub.wpt = wpt
+    ctx = _Ctx((want_dx,))
+    ctx.save_for_backward(x.contiguous(), W.contiguous(), att_src.reshape(-1),
+                          att_dst.reshape(-1), XP, a_s, a_d, alpha, Y, mask, pooled, W_out)
+    ctx.sub, ctx.head_graph, ctx.head_mean = sub, TGraph(g, "gat"), mean
+    grads = _GATConvHead.backward(ctx, dlogits)
+    return _grad_list([grads[0], grads[1], sub.red, grads[5], grads[6]], x.device)
+
+
+@gat_conv_head_bwd.register_fake
+def _(dlogits, x, W, att_src, att_dst, XP, a_s, a_d, alpha, Y, mask, pooled, W_out, g, heads,
+      slope, act, bf16, has_bias, mean, want_dx, wpt=None):
+    dev = x.device
+    return [torch.empty_like(x) if want_dx else _none(dev), torch.empty_like(W),
+            W.new_empty(3 * W.shape[0]), torch.empty_like(W_out), W_out.new_empty(W_out.shape[0])]
+
+
+def _gat_head_setup(ctx, inputs, output):
+    (x, W, att_src, att_dst, bias, W_out, b_out, g, heads, slope, mask, act, bf16, mean, _wp,
+     wpt) = inputs
+    _logits, Y, XP, a_s, a_d, alpha, pooled = output
+    ctx.save_for_backward(x, W, att_src, att_dst, XP, a_s, a_d, alpha, Y, _enc(mask, x.device),
+                          pooled, W_out, _enc(wpt, x.device), *g)
+    ctx.meta = (heads, slope, act, bf16, bias is not None, mean)
+
+
+def _gat_head_backward(ctx, grads):
+    (x, W, att_src, att_dst, XP, a_s, a_d, alpha, Y, mask, pooled, W_out, wpt,
+     *g) = ctx.saved_tensors
+    heads, slope, act, bf16, has_bias, mean = ctx.meta
+    dx, dW, red, dWo, dbo = torch.ops.lgnn.gat_conv_head_bwd(
+        grads[0], x, W, att_src, att_dst, XP, a_s, a_d, alpha, Y, _opt(mask), pooled, W_out, g,
+        heads, slope, act, bf16, has_bias, mean, ctx.needs_input_grad[0], _opt(wpt))
+    HC = W.shape[0]
+    da_s = red[:HC].view(att_src.shape)
+    da_d = red[HC:2 * HC].view(att_dst.shape)
+    db = red[2 * HC:] if has_bias else None
+    return (_opt(dx), dW, da_s, da_d, db, dWo, dbo, [None] * len(g), None, None, None, None,
+            None, None, None, None)
+
+
+gat_conv_head.register_autograd(_gat_head_backward, setup_context=_gat_head_setup)
 
 
 # ----------------------------------------------------------------------------------------------

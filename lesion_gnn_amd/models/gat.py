@@ -26,6 +26,8 @@ from .base import BaseModelConfig, BaseModule
 
 # the last GATConv + readout as one autograd node (ops.gat_conv_head); LGNN_GAT_HEAD=0: separate
 HEAD_FOLD = os.environ.get("LGNN_GAT_HEAD", "1") != "0"
+# fp32: every split-3 weight operand of a step in one launch (GAT.weight_planes); 0: per GEMM
+WEIGHT_BUNDLE = os.environ.get("LGNN_WEIGHT_BUNDLE", "1") != "0"
 
 
 class GAT(nn.Module):
@@ -63,6 +65,24 @@ class GAT(nn.Module):
         return lgnn_dropout.masks(self._dropout_rng, [c.mask_shape(g) for c in self.convs],
                                   lgnn_dropout.key(self, self.dropout_p))
 
+    def weight_planes(self):
+        """fp32: every split-3 weight operand of this step — in_proj's (when it runs on the dense
+        GEMMs), each conv's lin W and (for its dx) W^T — in ONE launch (ops.s3_weight_bundle)
+        instead of one per GEMM. Returns (in_proj's planes | None, [(W's, W^T's) per conv])."""
+        none = (None, [None] * len(self.convs))
+        if self.bf16 or not ops.GAT_S3 or not len(self.convs) or not WEIGHT_BUNDLE:
+            return none
+        grad = torch.is_grad_enabled()
+        specs = [(self.in_proj.weight, False)] if ops.dense_path(self.in_proj.weight, False) \
+            else []
+        for c in self.convs:
+            specs += [(c.lin.weight, False)] + ([(c.lin.weight, True)] if grad else [])
+        views = ops.s3_weight_bundle(specs, False)
+        wp = views.pop(0) if len(specs) > len(self.convs) * (2 if grad else 1) else None
+        per = 2 if grad else 1
+        return wp, [(views[per * i], views[per * i + 1] if grad else None)
+                    for i in range(len(self.convs))]
+
     def forward(self, x: torch.Tensor, edge_index, batch: torch.Tensor,
                 num_graphs: int | None = None) -> torch.Tensor:
         g = as_graph(edge_index, x.size(0), batch, num_graphs)
@@ -70,17 +90,18 @@ class GAT(nn.Module):
             # every bf16 GEMM's weight operands for this step in one launch
             ops.bf16_prepare_weights([self.in_proj.weight] + [c.lin.weight for c in self.convs])
         ms = self.dropout_masks(g)
-        h = ops.linear_auto(x, self.in_proj.weight, self.in_proj.bias, self.bf16)
+        wp, planes = self.weight_planes()
+        h = ops.linear_auto(x, self.in_proj.weight, self.in_proj.bias, self.bf16, wp)
         last = len(self.convs) - 1
         for i, conv in enumerate(self.convs):
             m = ms[i] if ms is not None else None
-            if i == last and HEAD_FOLD and not torch.compiler.is_compiling():
+            if i == last and HEAD_FOLD:
                 # last conv + readout as one node: the readout's backward is formed inside the
                 # attention backward's load, no dH tensor
                 return conv.forward_head(h, g, _lib.LGNN_ACT_ELU, self.out_proj.weight,
                                          self.out_proj.bias, self.pool == "mean", self.bf16,
-                                         mask=m)
-            h = conv(h, g, act=_lib.LGNN_ACT_ELU, bf16=self.bf16, mask=m)
+                                         mask=m, planes=planes[i])
+            h = conv(h, g, act=_lib.LGNN_ACT_ELU, bf16=self.bf16, mask=m, planes=planes[i])
         return ops.pool_head(h, self.out_proj.weight, self.out_proj.bias, g, self.pool == "mean")
 
 

@@ -502,6 +502,50 @@ def dense_planes(W: torch.Tensor, transposed: bool, bf16: bool) -> torch.Tensor:
     return Wp
 
 
+def _s3_bundle_sizes(shapes, transposed, bf16: bool) -> list:
+    """lgnn_s3_weight_planes_numel per operand, restated in Python (Dynamo traces this; a
+    ctypes call would break the graph): ceil(out/128) blocks x planes x 128 x kpad(in, 64)."""
+    planes = 1 if bf16 else 3
+    out = []
+    for (rows, cols), t in zip(shapes, transposed):
+        o, i = (cols, rows) if t else (rows, cols)
+        out.append((o + 127) // 128 * planes * 128 * ((i + 63) // 64 * 64))
+    return out
+
+
+def s3_bundle_raw(Ws: list, transposed: list, bf16: bool) -> torch.Tensor:
+    """The planes of every (W, transposed) operand in one flat int16 buffer (each operand's
+    numel a multiple of 8192: every view 16 KiB aligned), LGNN_MAX_WPREP jobs per launch."""
+    Ws = [_f32c(W) for W in Ws]
+    sizes = _s3_bundle_sizes([tuple(W.shape) for W in Ws], transposed, bf16)
+    flat = torch.empty(sum(sizes), dtype=torch.int16, device=Ws[0].device)
+    views = flat.split(sizes)
+    for j0 in range(0, len(Ws), 16):
+        js = range(j0, min(j0 + 16, len(Ws)))
+        n = len(js)
+        P_ = ctypes.c_void_p * n
+        I_ = ctypes.c_int * n
+        _lib.call("lgnn_s3_weight_planes_multi", n, P_(*[Ws[j].data_ptr() for j in js]),
+                  I_(*[Ws[j].size(0) for j in js]), I_(*[Ws[j].size(1) for j in js]),
+                  I_(*[int(bool(transposed[j])) for j in js]), 1 if bf16 else 3,
+                  P_(*[views[j].data_ptr() for j in js]), _s(flat.device))
+    return flat
+
+
+def s3_weight_bundle(specs: list, bf16: bool) -> list:
+    """Every split-3 weight operand of a step — specs = [(W, transposed)] — in one launch
+    (lgnn_s3_weight_planes_multi) instead of one dense_planes launch per GEMM: returns, per spec,
+    the planes dense_planes(W, transposed, bf16) would (views of one buffer). The optimizer
+    updates the weights in place, so a model asks for its bundle afresh every forward."""
+    Ws = [W.detach() for W, _ in specs]
+    tr = [bool(t) for _, t in specs]
+    if _compiling():
+        flat = torch.ops.lgnn.s3_weight_planes_multi(Ws, tr, bool(bf16))
+    else:
+        flat = s3_bundle_raw(Ws, tr, bf16)
+    return list(flat.split(_s3_bundle_sizes([tuple(W.shape) for W in Ws], tr, bf16)))
+
+
 def dense_mm(a: torch.Tensor, Wp: torch.Tensor, N: int, bias, bf16: bool,
              want_colsum: bool = False) -> torch.Tensor:
     """Y = a B^T (+ bias) on the split-3 (fp32 accuracy) or bf16-operand MFMA kernel
@@ -688,7 +732,7 @@ class _DenseLinear(torch.autograd.Function):
     precision."""
 
     @staticmethod
-    def forward(ctx, x, W, b, bf16):
+    def forward(ctx, x, W, b, bf16, wp=None):
         _lib.require_gpu(x, W)
         x, W = _f32c(x), _f32c(W)
         if bf16 and bf16_mfma_fits(W.size(0)):
@@ -705,7 +749,8 @@ class _DenseLinear(torch.autograd.Function):
             ctx.bf16, ctx.has_b = bf16, b is not None
             return y
         # split-3 MFMA GEMM at fp32 accuracy (bf16 mode: RNE-rounded operands, N > 128)
-        y = dense_mm(x, dense_planes(W, False, bf16), W.size(0), b, bf16)
+        y = dense_mm(x, wp if wp is not None else dense_planes(W, False, bf16), W.size(0), b,
+                     bf16)
         ctx.save_for_backward(x, W)
         ctx.bf16, ctx.has_b = bf16, b is not None
         return y
@@ -737,27 +782,33 @@ class _DenseLinear(torch.autograd.Function):
                         _remember_bf16(dx, dxb)
                 else:
                     dx = dense_mm(dyb, dense_planes(W, True, True), K, None, True)
-            return dx, dW, db, None
+            return dx, dW, db, None, None
         dW, db2 = dense_wgrad(dy, x, ctx.bf16, want_db=ctx.has_b and db is None)
         if db is None and ctx.has_b:
             db = db2
         dx = dense_mm(dy, dense_planes(W, True, ctx.bf16), K, None, ctx.bf16) \
             if ctx.needs_input_grad[0] else None
-        return dx, dW, db, None
+        return dx, dW, db, None, None
 
 
-def dense_linear(x, W, b=None, bf16: bool = False):
+def dense_linear(x, W, b=None, bf16: bool = False, wp=None):
+    """wp: W's split-3 planes from s3_weight_bundle (else made here, one launch)."""
     if _compiling():
-        return torch.ops.lgnn.dense_linear(x, W, b, bool(bf16))
-    return _DenseLinear.apply(x, W, b, bf16)
+        return torch.ops.lgnn.dense_linear(x, W, b, bool(bf16), wp)
+    return _DenseLinear.apply(x, W, b, bf16, wp)
 
 
-def linear_auto(x, W, b=None, bf16: bool = False):
+def dense_path(W, bf16: bool) -> bool:
+    """Whether linear_auto runs W on the split-3 GEMMs (so s3_weight_bundle can prepare it)."""
+    return not bf16 and not fast_shape(W.size(1), W.size(0))
+
+
+def linear_auto(x, W, b=None, bf16: bool = False, wp=None):
     """node_linear (tile kernels) where the shape allows and fp32 is asked for; else the library
     GEMM (dense_linear)."""
     if not bf16 and fast_shape(W.size(1), W.size(0)):
         return node_linear(x, W, b)
-    return dense_linear(x, W, b, bf16)
+    return dense_linear(x, W, b, bf16, wp)
 
 
 class _Spmm(torch.autograd.Function):
@@ -1499,7 +1550,8 @@ class _GATConv(torch.autograd.Function):
     over remove_self_loops + add_self_loops of edge_index (graph kind "gat")."""
 
     @staticmethod
-    def forward(ctx, x, W, att_src, att_dst, bias, graph, heads, slope, mask, act, bf16=False):
+    def forward(ctx, x, W, att_src, att_dst, bias, graph, heads, slope, mask, act, bf16=False,
+                wp=None, wpt=None):
         _lib.require_gpu(x, W, att_src, att_dst)
         x, W = _f32c(x), _f32c(W)
         att_src, att_dst = _f32c(att_src).view(-1), _f32c(att_dst).view(-1)
@@ -1535,7 +1587,8 @@ class _GATConv(torch.autograd.Function):
         elif mfma:
             XP = bf16_gemm(xg, Wb, None, HC)[0]
         elif dense:  # split-3 MFMA GEMM (fp32 accuracy), or one rounded plane in bf16 mode
-            XP = dense_mm(xg, dense_planes(Wg, False, bf16), HC, None, bf16)
+            XP = dense_mm(xg, wp if wp is not None else dense_planes(Wg, False, bf16), HC, None,
+                          bf16)
         else:
             XP = linear_fwd(x, W, None, _lib.LGNN_ACT_NONE)
         if not scored:
@@ -1552,6 +1605,7 @@ class _GATConv(torch.autograd.Function):
         ctx.save_for_backward(xg, Wg, att_src, att_dst, XP, a_s, a_d, alpha, Y, mask)
         ctx.graph, ctx.heads, ctx.slope, ctx.act = graph, heads, slope, act
         ctx.bf16, ctx.dense = bf16, dense
+        ctx.wpt = wpt if dense and not mfma else None  # W^T's planes for dx (s3_weight_bundle)
         ctx.has_bias = bias is not None
         ctx.att_shape = (1, heads, C)
         if Yb is not None:
@@ -1624,8 +1678,9 @@ class _GATConv(torch.autograd.Function):
                           _s(dev))
             if ctx.dense:  # split-3 (or bf16-rounded) MFMA GEMMs on the fp32 dXP
                 dW = dense_wgrad(dXP, x, ctx.bf16)[0]
-                dx = dense_mm(dXP, dense_planes(W, True, ctx.bf16), W.size(1), None, ctx.bf16) \
-                    if want_dx else None
+                wpt = getattr(ctx, "wpt", None)
+                dx = dense_mm(dXP, wpt if wpt is not None else dense_planes(W, True, ctx.bf16),
+                              W.size(1), None, ctx.bf16) if want_dx else None
             else:
                 dx, dW, _ = linear_bwd(_lib.LGNN_GRAD_DIRECT, dXP, H=None,
                                        act=_lib.LGNN_ACT_NONE, X=x, W=W, want_dx=want_dx,
@@ -1634,7 +1689,7 @@ class _GATConv(torch.autograd.Function):
         datt_s = red[:HC].view(ctx.att_shape)
         datt_d = red[HC:2 * HC].view(ctx.att_shape)
         dbias = red[2 * HC:] if ctx.has_bias else None
-        return dx, dW, datt_s, datt_d, dbias, None, None, None, None, None, None
+        return dx, dW, datt_s, datt_d, dbias, None, None, None, None, None, None, None, None
 
 
 GAT_S3 = os.environ.get("LGNN_GAT_S3", "1") != "0"
@@ -1672,10 +1727,10 @@ class _GATConvHead(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, W, att_src, att_dst, bias, W_out, b_out, graph, heads, slope, mask, act,
-                bf16, mean):
+                bf16, mean, wp=None, wpt=None):
         sub = _SubCtx(True)
         Y = _GATConv.forward(sub, x, W, att_src, att_dst, bias, graph, heads, slope, mask, act,
-                             bf16)
+                             bf16, wp, wpt)
         W_out, b_out = _f32c(W_out), _f32c(b_out)
         pooled, logits = pool_head_fwd(Y, graph, mean, W_out, b_out)
         ctx.save_for_backward(*sub.saved_tensors, pooled, W_out)
@@ -1705,25 +1760,34 @@ class _GATConvHead(torch.autograd.Function):
         g = _GATConv.backward(sub, None, pool=(dlogits, W_out, ctx.head_graph, ctx.head_mean),
                               extra_red=head_jobs)
         sub.saved_tensors = ()
-        return (*g[:5], dWo, dbo) + (None,) * 7
+        return (*g[:5], dWo, dbo) + (None,) * 9
 
 
 def gat_conv_head(x, W, att_src, att_dst, bias, W_out, b_out, graph: Graph, heads: int,
                   slope: float = 0.2, mask=None, act: int = _lib.LGNN_ACT_NONE,
-                  bf16: bool = False, mean: bool = True):
+                  bf16: bool = False, mean: bool = True, planes=None):
     """gat_conv followed by pool_head (the GAT model's last conv and readout) as one node."""
+    wp, wpt = planes if planes is not None else (None, None)
+    if _compiling():
+        return torch.ops.lgnn.gat_conv_head(
+            x, W, att_src, att_dst, bias, W_out, b_out, _lgnn().gparts(graph, "gat"), int(heads),
+            float(slope), mask, int(act), bool(bf16), bool(mean), wp, wpt)[0]
     return _GATConvHead.apply(x, W, att_src, att_dst, bias, W_out, b_out, graph, heads, slope,
-                              mask, act, bf16, mean)
+                              mask, act, bf16, mean, wp, wpt)
 
 
 def gat_conv(x, W, att_src, att_dst, bias, graph: Graph, heads: int, slope: float = 0.2,
-             mask=None, act: int = _lib.LGNN_ACT_NONE, bf16: bool = False):
+             mask=None, act: int = _lib.LGNN_ACT_NONE, bf16: bool = False, planes=None):
     """bf16: the lin GEMM (and its backward) on bf16-rounded operands, fp32 accumulate/out;
-    attention, softmax and aggregation stay fp32."""
+    attention, softmax and aggregation stay fp32. planes = (W's, W^T's) split-3 planes from
+    s3_weight_bundle (fp32 / dense path), else each GEMM prepares its own."""
+    wp, wpt = planes if planes is not None else (None, None)
     if _compiling():
         return torch.ops.lgnn.gat_conv(x, W, att_src, att_dst, bias, _lgnn().gparts(graph, "gat"),
-                                       int(heads), float(slope), mask, int(act), bool(bf16))[0]
-    return _GATConv.apply(x, W, att_src, att_dst, bias, graph, heads, slope, mask, act, bf16)
+                                       int(heads), float(slope), mask, int(act), bool(bf16), wp,
+                                       wpt)[0]
+    return _GATConv.apply(x, W, att_src, att_dst, bias, graph, heads, slope, mask, act, bf16, wp,
+                          wpt)
 
 
 # ----------------------------------------------------------------------------------------------

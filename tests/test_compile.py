@@ -19,7 +19,8 @@ from lesion_gnn_amd.models import DRGNet, GAT, GCN, GIN
 GLUE = {"<built-in function getitem>", "aten.empty.memory_format", "aten.detach.default",
         "auto_functionalized_v2", "auto_functionalized"}
 # views of one op output (offsets are symbolic-size arithmetic; views launch nothing)
-VIEWS = {"aten.slice.Tensor", "aten.view.default", "<built-in function add>",
+VIEWS = {"aten.slice.Tensor", "aten.view.default", "aten.split_with_sizes.default",
+         "<built-in function add>",
          "<built-in function floordiv>", "<built-in function mul>"}
 
 
@@ -62,7 +63,7 @@ def test_models_trace_to_lgnn_ops_only(name):
         heads = 2 if "refcfg" in name else 4
         m = GAT(d_in, [128] * 4, 1, heads=heads, dropout=0.35 if drop else 0.0,
                 precision="bf16" if "bf16" in name else "fp32").train()
-        want = {"lgnn.gat_conv.default", "lgnn.graph_build.default", "lgnn.pool_head.default"}
+        want = {"lgnn.gat_conv.default", "lgnn.graph_build.default", "lgnn.gat_conv_head.default"}
     elif name.startswith("gin"):
         b = synth.make_batch(6, n=64, k=8, d_in=128, seed=2)
         m = GIN(128, [128, 128, 128], 5, 0.35 if drop else 0.0, pool="add")
@@ -115,3 +116,17 @@ def test_config_compile_flag_wraps_model():
     assert isinstance(module.model, torch._dynamo.eval_frame.OptimizedModule)
     cfg.compile = False
     assert isinstance(get_model(cfg).model, GAT)
+
+
+def test_weight_bundle_sizes_match_the_library():
+    """ops._s3_bundle_sizes (the Python restatement Dynamo traces) == lgnn_s3_weight_planes_numel
+    for every shape class: K % 64 != 0, N > 128, transposed, 1 and 3 planes."""
+    from lesion_gnn_amd import _lib, ops
+
+    lib = _lib.load()
+    for rows, cols in [(128, 1025), (128, 128), (256, 128), (300, 37), (5, 3), (512, 512)]:
+        for t in (False, True):
+            for bf16 in (False, True):
+                o, i = (cols, rows) if t else (rows, cols)
+                want = lib.lgnn_s3_weight_planes_numel(o, i, 1 if bf16 else 3)
+                assert ops._s3_bundle_sizes([(rows, cols)], [t], bf16) == [want]

@@ -139,3 +139,45 @@ def test_no_library_gemm_in_gat_fp32_step(cuda):
     assert not lib, sorted(lib)
     assert any("k_s3_gemm" in n for n in names), sorted(names)  # the in_proj ran on ours
     assert any("k_s3_wgrad" in n for n in names), sorted(names)
+
+
+def test_weight_bundle_equals_per_gemm_planes(cuda):
+    """ops.s3_weight_bundle (one lgnn_s3_weight_planes_multi launch, more than 16 operands split
+    over launches) writes, per (W, transposed), exactly dense_planes' bytes."""
+    g = torch.Generator().manual_seed(5)
+    shapes = [(128, 1025), (128, 128), (256, 128), (300, 37), (5, 3)] * 4  # 20 operands
+    Ws = [torch.randn(r, c, generator=g).to(cuda) for r, c in shapes]
+    specs = [(W, i % 2 == 1) for i, W in enumerate(Ws)]
+    for bf16 in (False, True):
+        views = ops.s3_weight_bundle(specs, bf16)
+        for (W, t), v in zip(specs, views):
+            assert torch.equal(v, ops.dense_planes(W, t, bf16))
+
+
+@pytest.mark.parametrize("compiled", [False, True])
+def test_gat_weight_bundle_bitwise(cuda, monkeypatch, compiled):
+    """The fp32 GAT step with its weight operands from one bundle launch (GAT.weight_planes) is
+    bit-identical to one plane launch per GEMM — eager and compiled (the bundle rides through the
+    lgnn:: custom ops)."""
+    from lesion_gnn_amd import synth
+    from lesion_gnn_amd.models import GAT
+    from lesion_gnn_amd.models import gat as gat_mod
+
+    torch.manual_seed(0)
+    b = synth.make_batch(48, k=6, d_in=1025, seed=2, sizes="lognormal",
+                         last_channel_class=True).to(cuda)
+    m = GAT(1025, [128] * 4, 1, heads=2, dropout=0.35).to(cuda).train()
+    run = torch.compile(m, dynamic=True) if compiled else m
+    rng = m._dropout_rng.clone()
+    res = []
+    for bundle in (True, False):
+        monkeypatch.setattr(gat_mod, "WEIGHT_BUNDLE", bundle)
+        torch._dynamo.reset()
+        m._dropout_rng.copy_(rng)
+        out = run(b.x, b.edge_index, b.batch, b.num_graphs)
+        m.zero_grad(set_to_none=True)
+        out.square().sum().backward()
+        res.append((out.detach().cpu(), {n: p.grad.detach().cpu() for n, p in m.named_parameters()}))
+    assert torch.equal(res[0][0], res[1][0])
+    for n in res[0][1]:
+        assert torch.equal(res[0][1][n], res[1][1][n]), n
