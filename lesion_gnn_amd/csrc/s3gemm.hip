@@ -94,11 +94,11 @@ __device__ __forceinline__ void load_a(ARegs& R, Buf bA, int K, int c, int rq, i
   }
 }
 
-// the chunk's four fp32 per row -> PLANES bf16 planes (8 B per row and plane)
+// the chunk's four fp32 of row rq + 4 i -> PLANES bf16 planes (8 B per row and plane)
 template <int PLANES>
-__device__ __forceinline__ void store_a(unsigned char* img, const ARegs& R, int rq, int kq) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
+__device__ __forceinline__ void store_a_row(unsigned char* img, const ARegs& R, int rq, int kq,
+                                            int i) {
+  {
     const int pos = swz(rq + 4 * i, kq >> 3) + ((kq & 7) << 1);
     const float f0 = __uint_as_float(R.v[4 * i]), f1 = __uint_as_float(R.v[4 * i + 1]);
     const float f2 = __uint_as_float(R.v[4 * i + 2]), f3 = __uint_as_float(R.v[4 * i + 3]);
@@ -112,6 +112,11 @@ __device__ __forceinline__ void store_a(unsigned char* img, const ARegs& R, int 
           u32x2{rne16(f0) | (rne16(f1) << 16), rne16(f2) | (rne16(f3) << 16)};
     }
   }
+}
+template <int PLANES>
+__device__ __forceinline__ void store_a(unsigned char* img, const ARegs& R, int rq, int kq) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) store_a_row<PLANES>(img, R, rq, kq, i);
 }
 
 // Weight planes in fragment order (as bflin.hip's weight operand): for 128-column block nb,
@@ -150,45 +155,64 @@ __global__ __launch_bounds__(NT, 2) void k_s3_gemm(const float* __restrict__ A, 
   const int rq = 16 * wave + (lane >> 4), kq = 4 * (lane & 15);
   const int wlane = wave * 512 + lane * 8;
   f32x16 acc0 = {}, acc1 = {};
-  auto chunk = [&](const unsigned char* im, const u32x4 (&bc)[4][PLANES]) {
+  // Software pipeline. Chunk c's products run while (a) the A fragments of k-step s + 1 are
+  // read from LDS (two fragment sets: an LDS read's latency is not paid in front of each step)
+  // and (b) chunk c + 1's rows are split into planes and written to the other image (one row per
+  // k-step: the split's VALU work issues in the MFMAs' shadow). sched_barrier fences keep the
+  // compiler from sinking the reads back to their uses. The other image was last read by chunk
+  // c - 1, which every wave finished before the barrier in front of chunk c.
+  auto chunk = [&](const unsigned char* im, const u32x4 (&bc)[4][PLANES], unsigned char* imn,
+                   const ARegs& Rn, bool store_next) {
+    u32x4 a[2][2][PLANES];
+#pragma unroll
+    for (int p = 0; p < PLANES; ++p) {
+      a[0][0][p] = lds16(im + p * IMG + swz(li, h));
+      a[0][1][p] = lds16(im + p * IMG + swz(32 + li, h));
+    }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      u32x4 a0[PLANES], a1[PLANES];
+      if (s + 1 < 4) {
 #pragma unroll
-      for (int p = 0; p < PLANES; ++p) {
-        a0[p] = lds16(im + p * IMG + swz(li, 2 * s + h));
-        a1[p] = lds16(im + p * IMG + swz(32 + li, 2 * s + h));
+        for (int p = 0; p < PLANES; ++p) {
+          a[(s + 1) & 1][0][p] = lds16(im + p * IMG + swz(li, 2 * (s + 1) + h));
+          a[(s + 1) & 1][1][p] = lds16(im + p * IMG + swz(32 + li, 2 * (s + 1) + h));
+        }
       }
-      acc0 = mma<PLANES>(a0, bc[s], acc0);
-      acc1 = mma<PLANES>(a1, bc[s], acc1);
+      __builtin_amdgcn_sched_barrier(0);
+      acc0 = mma<PLANES>(a[s & 1][0], bc[s], acc0);
+      acc1 = mma<PLANES>(a[s & 1][1], bc[s], acc1);
+      if (store_next) store_a_row<PLANES>(imn, Rn, rq, kq, s);
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
-  // two register sets ping-pong: chunk c + 2's loads are issued while chunk c is used
+  // two register sets ping-pong: R[c & 1] holds chunk c's rows until chunk c - 1's products
+  // have stored them, then takes chunk c + 2's
   ARegs R0, R1;
   u32x4 b0[4][PLANES], b1[4][PLANES];
   load_a<VEC>(R0, bA, K, 0, rq, kq);
   load_b<PLANES>(b0, bW, pstride, wlane, 0);
   load_a<VEC>(R1, bA, K, 1, rq, kq);
   load_b<PLANES>(b1, bW, pstride, wlane, 1);
-  auto step = [&](int c, ARegs& R, u32x4 (&bc)[4][PLANES]) {
-    unsigned char* im = img[c & 1];
-    store_a<PLANES>(im, R, rq, kq);
-    load_a<VEC>(R, bA, K, c + 2, rq, kq);
-    lds_barrier();  // image c complete (image c - 2's reads finished before barrier c - 1)
-    chunk(im, bc);
+  store_a<PLANES>(img[0], R0, rq, kq);
+  load_a<VEC>(R0, bA, K, 2, rq, kq);
+  lds_barrier();
+  auto step = [&](int c, ARegs& Rn, u32x4 (&bc)[4][PLANES], bool store_next) {
+    chunk(img[c & 1], bc, img[(c + 1) & 1], Rn, store_next);
+    load_a<VEC>(Rn, bA, K, c + 3, rq, kq);
     load_b<PLANES>(bc, bW, pstride, wlane, c + 2);
+    lds_barrier();  // image c + 1 complete, image c's reads done
   };
   if constexpr (NCK > 0) {
 #pragma unroll
     for (int c = 0; c < NCK; ++c) {
-      if (c & 1) step(c, R1, b1);
-      else step(c, R0, b0);
+      if (c & 1) step(c, R0, b1, c + 1 < NCK);
+      else step(c, R1, b0, c + 1 < NCK);
     }
   } else {
     const int npair = (Kp / BK + 1) / 2;
     for (int cp = 0; cp < npair; ++cp) {
-      step(2 * cp, R0, b0);
-      step(2 * cp + 1, R1, b1);
+      step(2 * cp, R1, b0, true);
+      step(2 * cp + 1, R0, b1, true);
     }
   }
   // epilogue: + bias; fp32 rows as 128-B segments per (row, wave); optional column sums
@@ -489,7 +513,8 @@ extern "C" int lgnn_s3_gemm(const float* A, int64_t M, int K, const uint16_t* Wp
   const dim3 grid((unsigned)((M + TM - 1) / TM), (unsigned)((N + 127) / 128)), block(NT);
   hipStream_t s = as_stream(stream);
   const bool v = K % 4 == 0;
-  const int nck = Kp / BK;
+  const char* loop = getenv("LGNN_S3G_LOOP");  // tuning knob: 1 = the pair loop at every K
+  const int nck = loop && loop[0] == '1' ? -1 : Kp / BK;
 #define LGNN_S3G(P, V, NC) \
   hipLaunchKernelGGL((k_s3_gemm<P, V, NC>), grid, block, 0, s, A, M, K, Wp, Kp, bias, N, Y, \
                      colsum_part)
@@ -516,12 +541,19 @@ extern "C" int lgnn_s3_gemm(const float* A, int64_t M, int K, const uint16_t* Wp
 
 // k_s3_wgrad2: 32-row chunks per split, so that the grid (128-wide k-blocks x splits x n-blocks)
 // holds about two workgroups per CU (512), at least 4 chunks per split
+// (tuning knobs: LGNN_S3_WG_TARGET workgroups, LGNN_S3_WG_MINCPS chunks per split)
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  const int v = e ? atoi(e) : 0;
+  return v > 0 ? v : dflt;
+}
 static int s3_wg_cps(int64_t M, int K, int N) {
   const int64_t nch = std::max<int64_t>((M + W2M - 1) / W2M, 1);
   const int64_t work = (int64_t)((K + 127) / 128) * ((N + 127) / 128);
-  int64_t splits = std::max<int64_t>(512 / work, 1);
+  int64_t splits = std::max<int64_t>(env_int("LGNN_S3_WG_TARGET", 512) / work, 1);
   int64_t cps = (nch + splits - 1) / splits;
-  if (cps < 4) cps = 4;
+  const int mincps = env_int("LGNN_S3_WG_MINCPS", 4);
+  if (cps < mincps) cps = mincps;
   return (int)cps;
 }
 

@@ -1,0 +1,28 @@
+"""Micro-timing of the split-3 GEMMs at the reference in_proj / lin shapes (tuning aid):
+python tools/s3_micro.py -> one line per (kernel, shape): average us over 50 launches."""
+import torch
+
+from lesion_gnn_amd import ops
+
+
+def timeit(fn, n=50):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n * 1e3
+
+
+dev = torch.device("cuda:0")
+for M, K, N in [(42279, 1025, 128), (42279, 128, 128)]:
+    A = torch.randn(M, K, device=dev)
+    W = torch.randn(N, K, device=dev)
+    dY = torch.randn(M, N, device=dev)
+    wp = ops.dense_planes(W, False, False)
+    t_f = timeit(lambda: ops.dense_mm(A, wp, N, None, False))
+    t_w = timeit(lambda: ops.dense_wgrad(dY, A, False))
+    print(f"M={M} K={K} N={N}: gemm {t_f:.1f} us  wgrad(+reduce) {t_w:.1f} us", flush=True)
