@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 26
+#define LGNN_ABI_VERSION 27
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -609,6 +609,9 @@ int lgnn_gcn_stack_bwd_s3f_all(const float* dP, const int64_t* batch, const int3
  * lgnn_s3_weight_planes_multi: n (<= LGNN_MAX_WPREP) such operands in ONE launch (job j: W[j],
  *   rows[j], cols[j], transposed[j] -> Wp[j]; planes shared) — a model's every weight operand of a
  *   step (forward B = W and backward B = W^T) at once instead of one small launch per GEMM.
+ * lgnn_s3_gemm_att: lgnn_s3_gemm (planes = 3) for a GATConv.lin (N = heads * C <= 128, no bias) that also
+ *   writes the attention scores a_s[m][h] = <Y[m][hC ..), att_src[h]>, a_d likewise ([M][heads],
+ *   one fmaf chain over the head's C features in feature order) — replaces lgnn_gat_att's pass.
  * lgnn_s3_gemm: Y[M][N] = A[M][K] B[N][K]^T (+ bias[N]), A fp32 (split or rounded as loaded).
  *   colsum_part (nullable): [ceil(M/64)][N] per-64-row-tile column sums of Y (fixed order).
  * lgnn_s3_wgrad: partial slabs of dW[N][K] = dY^T X (dY [M][N], X [M][K] fp32, N even):
@@ -625,6 +628,9 @@ int lgnn_s3_weight_planes_multi(int n, const float* const* W, const int* rows, c
                                 void* stream);
 int lgnn_s3_gemm(const float* A, int64_t M, int K, const uint16_t* Wp, int N, int planes,
                  const float* bias, float* Y, float* colsum_part, void* stream);
+int lgnn_s3_gemm_att(const float* A, int64_t M, int K, const uint16_t* Wp, int N, int planes,
+                     float* Y, const float* att_src, const float* att_dst, int heads, int C,
+                     float* a_s, float* a_d, void* stream);
 int lgnn_s3_wgrad_partials(int64_t M, int K, int N);
 int lgnn_s3_wgrad(const float* dY, int N, const float* X, int64_t M, int K, int planes,
                   float* partials, int num_partials, float* db_partials, void* stream);

@@ -127,6 +127,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_s3_weight_planes_numel": (SZ, [I32, I32, I32]),
     "lgnn_s3_weight_planes": (I32, [P, I32, I32, I32, I32, P, P]),
     "lgnn_s3_weight_planes_multi": (I32, [I32, P, P, P, P, I32, P, P]),
+    "lgnn_s3_gemm_att": (I32, [P, I64, I32, P, I32, I32, P, P, P, I32, I32, P, P, P]),
     "lgnn_s3_gemm": (I32, [P, I64, I32, P, I32, I32, P, P, P, P]),
     "lgnn_s3_wgrad_partials": (I32, [I64, I32, I32]),
     "lgnn_s3_wgrad": (I32, [P, I32, P, I64, I32, I32, P, I32, P, P]),
@@ -138,7 +139,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 26
+ABI_VERSION = 27
 
 _lib = None
 

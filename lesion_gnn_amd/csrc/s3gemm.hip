@@ -138,12 +138,26 @@ __device__ __forceinline__ void load_b(u32x4 (&b)[4][PLANES], Buf bW, int64_t ps
 // NCK = 0: any K, a loop over chunk pairs whose body is the same branch-free sequence (an odd
 // chunk count runs one all-zero chunk). Prefetches past the last chunk read zeros (offsets past
 // the buffers' ranges), so no load is guarded by a branch.
-template <int PLANES, bool VEC, int NCK>
+// GATConv attention scores of the output (ATT, N <= 128): a_s[m][h] = <Y[m][hC .. hC + C),
+// att_src[h]>, a_d likewise (PyG GATConv alpha_src / alpha_dst, reference gat.py:31), one fmaf
+// chain per (row, head) over the tile's Y staged in the (then free) A images — the fp32 twin of
+// bflin.hip's epilogue, so lgnn_gat_att's pass over XP disappears from the fp32 GAT too.
+struct AttOut {
+  const float* src;  // [H*C]
+  const float* dst;
+  float* a_s;        // [M][H]
+  float* a_d;
+  int H, C;
+};
+constexpr int YLD = 128 + 4;  // LDS row stride of the staged Y tile (floats)
+
+template <int PLANES, bool VEC, int NCK, bool ATT = false>
 __global__ __launch_bounds__(NT, 2) void k_s3_gemm(const float* __restrict__ A, int64_t M, int K,
                                                    const uint16_t* __restrict__ Wp, int Kp,
                                                    const float* __restrict__ bias, int N,
                                                    float* __restrict__ Y,
-                                                   float* __restrict__ colsum) {
+                                                   float* __restrict__ colsum,
+                                                   AttOut att = AttOut{}) {
   __shared__ __attribute__((aligned(16))) unsigned char img[2][PLANES * IMG];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, li = lane & 31;
@@ -237,6 +251,37 @@ __global__ __launch_bounds__(NT, 2) void k_s3_gemm(const float* __restrict__ A, 
       const float v = (q ? acc1[r] : acc0[r]) + bv;
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), bY, (m * N + ncol) * 4, 0, 0);
     }
+  if constexpr (ATT) {
+    static_assert(TM * YLD * 4 <= 2 * PLANES * IMG, "the Y tile fits in the A images");
+    float* ytile = reinterpret_cast<float*>(&img[0][0]);
+    lds_barrier();  // every wave's last image reads are done
+    if (nok) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
+          ytile[m * YLD + n] = (q ? acc1[r] : acc0[r]) + bv;
+        }
+    }
+    lds_barrier();
+    const int H = att.H, C = att.C;
+    const int64_t rows = M - r0 < TM ? M - r0 : TM;
+    for (int p = tid; p < TM * H; p += NT) {
+      const int m = p / H, hd = p % H;
+      if (m >= rows) continue;
+      const float* yr = ytile + m * YLD + hd * C;
+      const float* ws = att.src + hd * C;
+      const float* wd = att.dst + hd * C;
+      float ps = 0.f, pd = 0.f;
+      for (int c = 0; c < C; ++c) {
+        ps = fmaf(yr[c], ws[c], ps);
+        pd = fmaf(yr[c], wd[c], pd);
+      }
+      att.a_s[(r0 + m) * H + hd] = ps;
+      att.a_d[(r0 + m) * H + hd] = pd;
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -535,6 +580,38 @@ extern "C" int lgnn_s3_gemm(const float* A, int64_t M, int K, const uint16_t* Wp
   }
 #undef LGNN_S3G_N
 #undef LGNN_S3G
+  LGNN_LAUNCH_CHECK();
+  return LGNN_OK;
+}
+
+extern "C" int lgnn_s3_gemm_att(const float* A, int64_t M, int K, const uint16_t* Wp, int N,
+                                int planes, float* Y, const float* att_src, const float* att_dst,
+                                int heads, int C, float* a_s, float* a_d, void* stream) {
+  if (M < 0 || K < 1 || N < 1 || N > 128 || !Wp || !Y || planes != 3 || heads < 1 || C < 1 || heads * C != N || !att_src || !att_dst || !a_s || !a_d)
+    return LGNN_EINVAL;
+  if (M > 0 && !A) return LGNN_EINVAL;
+  const int Kp = (K + BK - 1) / BK * BK;
+  if ((M + TM) * (int64_t)K * 4 >= ((int64_t)1 << 31) || M * (int64_t)N * 4 >= ((int64_t)1 << 30) ||
+      (int64_t)3 * 128 * Kp * 2 >= ((int64_t)1 << 31))
+    return LGNN_EINVAL;
+  if (M == 0) return LGNN_OK;
+  const dim3 grid((unsigned)((M + TM - 1) / TM), 1), block(NT);
+  hipStream_t s = as_stream(stream);
+  const AttOut at{att_src, att_dst, a_s, a_d, heads, C};
+  const bool v = K % 4 == 0;
+  const int nck = Kp / BK;
+#define LGNN_S3A(P, V, NC)                                                                      \
+  hipLaunchKernelGGL((k_s3_gemm<P, V, NC, true>), grid, block, 0, s, A, M, K, Wp, Kp, nullptr, N, \
+                     Y, nullptr, at)
+#define LGNN_S3A_N(P, V)                 \
+  switch (nck) {                         \
+    case 2: LGNN_S3A(P, V, 2); break;    \
+    case 17: LGNN_S3A(P, V, 17); break;  \
+    default: LGNN_S3A(P, V, 0); break;   \
+  }
+  if (v) { LGNN_S3A_N(3, true) } else { LGNN_S3A_N(3, false) }
+#undef LGNN_S3A_N
+#undef LGNN_S3A
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
 }

@@ -1586,6 +1586,15 @@ class _GATConv(torch.autograd.Function):
             scored = True
         elif mfma:
             XP = bf16_gemm(xg, Wb, None, HC)[0]
+        elif dense and not bf16 and GAT_GEMM_ATT and HC <= 128:
+            # split-3 (or one rounded plane) with the attention scores in the GEMM's epilogue
+            XP = torch.empty(M, HC, dtype=torch.float32, device=dev)
+            xg = xg.contiguous()
+            _lib.call("lgnn_s3_gemm_att", _lib.ptr(xg), M, xg.size(1),
+                      _lib.ptr(wp if wp is not None else dense_planes(Wg, False, False)), HC, 3,
+                      _lib.ptr(XP), _lib.ptr(att_src), _lib.ptr(att_dst), heads,
+                      C, _lib.ptr(a_s), _lib.ptr(a_d), _s(dev))
+            scored = True
         elif dense:  # split-3 MFMA GEMM (fp32 accuracy), or one rounded plane in bf16 mode
             XP = dense_mm(xg, wp if wp is not None else dense_planes(Wg, False, bf16), HC, None,
                           bf16)

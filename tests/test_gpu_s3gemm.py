@@ -181,3 +181,33 @@ def test_gat_weight_bundle_bitwise(cuda, monkeypatch, compiled):
     assert torch.equal(res[0][0], res[1][0])
     for n in res[0][1]:
         assert torch.equal(res[0][1][n], res[1][1][n]), n
+
+
+@pytest.mark.parametrize("heads,C,K", [(2, 64, 1025), (4, 32, 128), (1, 128, 128), (8, 8, 37)])
+def test_s3_gemm_att_scores(cuda, heads, C, K):
+    """lgnn_s3_gemm_att (the fp32 GATConv.lin with the attention scores in its epilogue): Y equals
+    lgnn_s3_gemm's bit for bit, and a_s / a_d (one fmaf chain per row and head) match
+    lgnn_gat_att's (dot4 + butterfly sums) within fp32 summation error."""
+    from lesion_gnn_amd import _lib
+
+    g = torch.Generator().manual_seed(heads * 100 + C)
+    M, N = 777, heads * C
+    A = torch.randn(M, K, generator=g).to(cuda)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(cuda)
+    att_s = torch.randn(N, generator=g).to(cuda)
+    att_d = torch.randn(N, generator=g).to(cuda)
+    wp = ops.dense_planes(W, False, False)
+    Y = torch.empty(M, N, device=cuda)
+    a_s = torch.empty(M, heads, device=cuda)
+    a_d = torch.empty(M, heads, device=cuda)
+    _lib.call("lgnn_s3_gemm_att", A.data_ptr(), M, K, wp.data_ptr(), N, 3, Y.data_ptr(),
+              att_s.data_ptr(), att_d.data_ptr(), heads, C, a_s.data_ptr(), a_d.data_ptr(),
+              _lib.stream())
+    assert torch.equal(Y, ops.dense_mm(A, wp, N, None, False))
+    r_s = torch.empty_like(a_s)
+    r_d = torch.empty_like(a_d)
+    _lib.call("lgnn_gat_att", Y.data_ptr(), M, heads, C, att_s.data_ptr(), att_d.data_ptr(),
+              r_s.data_ptr(), r_d.data_ptr(), _lib.stream())
+    for got, want in ((a_s, r_s), (a_d, r_d)):
+        scale = (Y.view(M, heads, C).abs() * att_s.view(heads, C).abs()).sum(-1).max().item()
+        assert (got - want).abs().max().item() <= 2e-6 * scale
