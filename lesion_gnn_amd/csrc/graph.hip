@@ -22,6 +22,9 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kFinT = 64;          // k_finish: rows (threads) per block
 constexpr int kFinishCap = 1536;   // staged CSR entries per k_finish block
+// k_build's barrier bound (~4 s): a row longer than kFinishCap is sorted by one thread in global
+// memory (seconds for thousands of entries) while the other workgroups wait at the next barrier
+constexpr int kBuildSpins = 1 << 24;
 
 inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -614,14 +617,14 @@ __global__ __launch_bounds__(kThreads) void k_build(BuildArgs a, int32_t* sync) 
     const int64_t nzero = (int64_t)(a.ws.zero_bytes / 4);
     prep_body(a.ws.err, nzero, a.tile_open, ntiles, a.batch, N, a.num_graphs, a.gptr, b, G);
   }
-  lgnn_tile::grid_sync(sync, 1);
+  lgnn_tile::grid_sync(sync, 1, kBuildSpins);
   const int64_t nch = (E + kChunk - 1) / kChunk;
   for (int64_t c = b; c < nch; c += G) {
     __syncthreads();  // the previous chunk's LDS reads are done
     count_body(a.ei, E, N, a.loops, a.ws.cnt, a.tptr ? a.ws.tcnt : nullptr, a.ws.err,
                a.lazy ? a.tile_open : nullptr, sm.e.hist, sm.e.red, c);
   }
-  lgnn_tile::grid_sync(sync, 2);
+  lgnn_tile::grid_sync(sync, 2, kBuildSpins);
   {
     const int nblk = (int)((N + 1 + kScanBlk - 1) / kScanBlk), ny = a.tptr ? 2 : 1;
     for (int v = b; v < nblk * ny; v += G) {
@@ -631,13 +634,13 @@ __global__ __launch_bounds__(kThreads) void k_build(BuildArgs a, int32_t* sync) 
                 v / nblk, nblk);
     }
   }
-  lgnn_tile::grid_sync(sync, 3);
+  lgnn_tile::grid_sync(sync, 3, kBuildSpins);
   for (int64_t c = b; c < nch; c += G) {
     __syncthreads();
     fill_body(a.ei, E, N, a.loops, a.rowptr, a.ws.fill, a.col, a.ws.eid, a.tptr, a.ws.tfill,
               a.tidx, a.ws.teid, a.lazy ? a.tile_open + ntiles : nullptr, sm.e.hist, sm.e.red, c);
   }
-  lgnn_tile::grid_sync(sync, 4);
+  lgnn_tile::grid_sync(sync, 4, kBuildSpins);
   {
     __syncthreads();  // the union's finish arrays overlay the fill bins
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -651,7 +654,7 @@ __global__ __launch_bounds__(kThreads) void k_build(BuildArgs a, int32_t* sync) 
                   (int)(v / nfin), lane, WaveSync{});
   }
   if (a.tmap) {
-    lgnn_tile::grid_sync(sync, 5);
+    lgnn_tile::grid_sync(sync, 5, kBuildSpins);
     const int nnz = a.tptr[N];
     for (int q = b * kThreads + threadIdx.x; q < nnz; q += G * kThreads)
       a.tmap[q] = a.ws.inv[a.ws.teid[q]];

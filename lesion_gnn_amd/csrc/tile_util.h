@@ -221,7 +221,10 @@ __device__ __forceinline__ void lds_barrier() {
 // invalidate), then __syncthreads before any wave reads (MI355X_MICROARCH.md, correctness
 // boundaries). The spin is bounded (~0.5 s): a barrier that cannot complete yields wrong
 // results, never a hang; it counts itself in sync[2].
-__device__ __forceinline__ void grid_sync(int32_t* sync, int gen) {
+// max_spins x s_sleep(8) (512 clocks): 2^20 ~ 0.25 s — a safety net, not a schedule; a phase
+// with a legitimately long straggler (the graph build's single-thread sort of a row too long for
+// LDS) passes a larger bound
+__device__ __forceinline__ void grid_sync(int32_t* sync, int gen, int max_spins = 1 << 20) {
   __syncthreads();
   if (threadIdx.x == 0) {
     __hip_atomic_fetch_add(sync, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -229,7 +232,7 @@ __device__ __forceinline__ void grid_sync(int32_t* sync, int gen) {
     int spins = 0;
     while (__hip_atomic_load(sync, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(8);
-      if (++spins > (1 << 20)) {
+      if (++spins > max_spins) {
         __hip_atomic_fetch_add(sync + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
