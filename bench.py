@@ -365,7 +365,10 @@ def time_gat_in_proj(model, b, dev, wl):
         def wgrad():
             _lib.call("lgnn_s3_wgrad", dy.data_ptr(), N, x.data_ptr(), M, K, 3, part.data_ptr(),
                       S, dbp.data_ptr(), s)
-        names = ("void lgnn_s3g::k_s3_gemm<3, false, 17>", "void lgnn_s3g::k_s3_wgrad<3>")
+        # the forward kernel runs only at this shape; k_s3_wgrad2 also runs on the lins, so its
+        # traffic entry is the in_proj-only PMC pass of tools/s3_micro.py --inproj
+        names = ("void lgnn_s3g::k_s3_gemm<3, false, 17, false>",
+                 "void lgnn_s3g::k_s3_wgrad2<3> [in_proj 42279 x 1025 -> 128]")
         peak = MFMA_S3_PEAK_TF
         label = "split-3 bf16 MFMA at fp32 accuracy (s3gemm.hip)"
     for what, fn, name in (("forward GEMM Y = X W^T + b", fwd, names[0]),

@@ -1,5 +1,9 @@
 """Micro-timing of the split-3 GEMMs at the reference in_proj / lin shapes (tuning aid):
-python tools/s3_micro.py -> one line per (kernel, shape): average us over 50 launches."""
+python tools/s3_micro.py -> one line per (kernel, shape): average us over 50 launches.
+--inproj: only the in_proj shape (42,279 x 1025 -> 128), e.g. under rocprofv3 --pmc, so that
+k_s3_wgrad2's per-launch HBM bytes belong to that shape alone (the step also runs it on the lins)."""
+import sys
+
 import torch
 
 from lesion_gnn_amd import ops
@@ -18,7 +22,8 @@ def timeit(fn, n=50):
 
 
 dev = torch.device("cuda:0")
-for M, K, N in [(42279, 1025, 128), (42279, 128, 128)]:
+SHAPES = [(42279, 1025, 128)] if "--inproj" in sys.argv else [(42279, 1025, 128), (42279, 128, 128)]
+for M, K, N in SHAPES:
     A = torch.randn(M, K, device=dev)
     W = torch.randn(N, K, device=dev)
     dY = torch.randn(M, N, device=dev)
