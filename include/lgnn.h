@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 27
+#define LGNN_ABI_VERSION 28
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -230,6 +230,13 @@ int lgnn_spmm(const int32_t* rowptr, const int32_t* col, const float* w, float s
 int lgnn_pool_head_fwd(const float* H, const int32_t* gptr, int64_t B, int D, int pool_mean,
                        const float* Wout, const float* bout, int C, float* pooled,
                        float* logits, void* stream);
+
+/* The same with each graph split over `splits` workgroups (few, large graphs: the GAT configs);
+ * part: [B][splits][D] scratch; tickets: int32 [B], zero on entry, left zero. Each graph's
+ * column sums are its splits' fixed-order partial sums added in split order. */
+int lgnn_pool_head_fwd_split(const float* H, const int32_t* gptr, int64_t B, int D, int pool_mean,
+                             const float* Wout, const float* bout, int C, int splits, float* part,
+                             int32_t* tickets, float* pooled, float* logits, void* stream);
 
 /* Backward of lgnn_pool_head_fwd's Linear part:
  *   dpooled = dlogits Wout;  dWout = dlogits^T pooled;  dbout = colsum(dlogits). */

@@ -113,6 +113,84 @@ __global__ __launch_bounds__(NT) void k_pool_head_fwd4(const float* __restrict__
   }
 }
 
+// Few, large graphs (the GAT configs: 64 graphs of ~660 rows) leave most CUs idle with one
+// workgroup per graph, each walking its rows latency-bound. Here graph g is split over S
+// workgroups (rows [n0 + s chunk, ..), chunk = ceil(|g| / S)); each writes its column sums (the
+// fwd4 half-wave order) to part[g][s], and the last of the S to arrive — a per-graph ticket taken
+// with agent-scope acquire-release after the partial's release — sums the S partials in split
+// order, scales, writes pooled and the logits, and re-arms the ticket (zero on entry and exit).
+__global__ __launch_bounds__(NT) void k_pool_head_split(const float* __restrict__ H,
+                                                        const int32_t* __restrict__ gptr, int D,
+                                                        int pool_mean,
+                                                        const float* __restrict__ Wout,
+                                                        const float* __restrict__ bout, int C,
+                                                        int S, float* __restrict__ part,
+                                                        int32_t* __restrict__ tickets,
+                                                        float* __restrict__ pooled,
+                                                        float* __restrict__ logits) {
+  __shared__ __attribute__((aligned(16))) float red[8][512];
+  __shared__ float pl[512];
+  __shared__ int is_last;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 31, hw = wave * 2 + (lane >> 5);
+  const int64_t g = blockIdx.x / S;
+  const int sp = blockIdx.x % S;
+  const int n0 = gptr[g], n1 = gptr[g + 1];
+  const int cnt = n1 - n0, chunk = (cnt + S - 1) / S;
+  const int r0 = n0 + sp * chunk, r1 = r0 + chunk < n1 ? r0 + chunk : n1;
+  for (int s0 = 0; s0 < D; s0 += 128) {
+    const int f = s0 + 4 * li;
+    const int fc = f < D ? f : D - 4;
+    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+    int i = r0 + hw;
+    for (; i + 8 < r1; i += 16) {
+      const f32x4 v0 = ld4(H + (int64_t)i * D + fc);
+      const f32x4 v1 = ld4(H + (int64_t)(i + 8) * D + fc);
+      a0 += v0;
+      a1 += v1;
+    }
+    if (i < r1) a0 += ld4(H + (int64_t)i * D + fc);
+    if (f < D) st4(&red[hw][f], a0 + a1);
+  }
+  __syncthreads();
+  float* mine = part + ((int64_t)g * S + sp) * D;
+  for (int d = threadIdx.x; d < D; d += NT) {
+    float t = red[0][d];
+#pragma unroll
+    for (int r = 1; r < 8; ++r) t += red[r][d];
+    mine[d] = t;
+  }
+  __threadfence();  // this partial, at agent scope, before the ticket
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int prev =
+        __hip_atomic_fetch_add(tickets + g, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    is_last = prev == S - 1;
+  }
+  __syncthreads();
+  if (!is_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the other S - 1 partials
+  const float denom = (float)(cnt > 0 ? cnt : 1);
+  const float* pg = part + (int64_t)g * S * D;
+  for (int d = threadIdx.x; d < D; d += NT) {
+    float t = pg[d];
+    for (int q = 1; q < S; ++q) t += pg[(int64_t)q * D + d];
+    if (pool_mean) t = t / denom;
+    pooled[g * D + d] = t;
+    pl[d] = t;
+  }
+  if (threadIdx.x == 0) tickets[g] = 0;  // re-armed for the next launch (stream order)
+  if (!Wout) return;
+  __syncthreads();
+  for (int c = wave; c < C; c += NT / 64) {
+    float acc = 0.f;
+    for (int d = lane; d < D; d += 64) acc = fmaf(pl[d], Wout[(int64_t)c * D + d], acc);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (lane == 0) logits[g * C + c] = acc + (bout ? bout[c] : 0.f);
+  }
+}
+
 // One launch for the out_proj backward: blocks [0, nb_dp) compute dpooled[g][d] = sum_c
 // dlogits[g][c] Wout[c][d] (one element per thread); the rest compute dWout[c][d] = sum_g
 // dlogits[g][c] pooled[g][d] and dbout[c] (block = (class c, 64-wide feature strip), 16 waves
@@ -195,6 +273,23 @@ extern "C" int lgnn_pool_head_fwd(const float* H, const int32_t* gptr, int64_t B
     hipLaunchKernelGGL(k_pool_head_fwd, dim3((unsigned)((B + 3) / 4)), dim3(NT), 0,
                        as_stream(stream), H, gptr, B, D, pool_mean, Wout, bout, C, pooled,
                        logits);
+  LGNN_LAUNCH_CHECK();
+  return LGNN_OK;
+}
+
+extern "C" int lgnn_pool_head_fwd_split(const float* H, const int32_t* gptr, int64_t B, int D,
+                                        int pool_mean, const float* Wout, const float* bout,
+                                        int C, int splits, float* part, int32_t* tickets,
+                                        float* pooled, float* logits, void* stream) {
+  if (B < 0 || D <= 0 || D > 512 || (D & 3) || !gptr || !pooled || splits < 1 || splits > 64 ||
+      !part || !tickets)
+    return LGNN_EINVAL;
+  if (Wout && (C <= 0 || !logits)) return LGNN_EINVAL;
+  if (B == 0) return LGNN_OK;
+  if (B * splits > (int64_t)1 << 30) return LGNN_EINVAL;
+  hipLaunchKernelGGL(k_pool_head_split, dim3((unsigned)(B * splits)), dim3(NT), 0,
+                     as_stream(stream), H, gptr, D, pool_mean, Wout, bout, C, splits, part,
+                     tickets, pooled, logits);
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
 }

@@ -412,11 +412,43 @@ def spmm_raw(rowptr, col, w, self_scale: float, x: torch.Tensor) -> torch.Tensor
     return y
 
 
+_POOL_TICKETS: dict = {}
+
+
+def pool_tickets(dev, B: int) -> torch.Tensor:
+    """lgnn_pool_head_fwd_split's per-graph tickets for this device: zeroed once, grown as needed,
+    left zero by every launch (one stream per device issues them)."""
+    key = torch.device(dev).index
+    t = _POOL_TICKETS.get(key)
+    if t is None or t.numel() < B:
+        t = _POOL_TICKETS[key] = torch.zeros(max(B, 1024), dtype=torch.int32, device=dev)
+    return t
+
+
+def pool_splits(B: int, M: int, D: int) -> int:
+    """Workgroups per graph of the readout: 1 (one workgroup per graph) unless LGNN_POOL_SPLITS
+    asks for the split kernel. Measured: the split kernel's per-workgroup agent-scope release
+    (before its ticket) writes back the XCD's dirty L2 — the activations the forward just wrote —
+    so it lost everywhere (refcfg 0.642 -> 1.010 ms at 4 splits, C2 0.247 -> 0.450 at 2)."""
+    if D % 4 or D > 512 or B == 0:
+        return 1
+    env = os.environ.get("LGNN_POOL_SPLITS")
+    return max(1, min(64, int(env))) if env else 1
+
+
 def pool_head_fwd(H: torch.Tensor, graph: Graph, mean: bool, Wout=None, bout=None):
     B, D = graph.num_graphs, H.size(1)
     pooled = torch.empty(B, D, dtype=torch.float32, device=H.device)
     C = Wout.size(0) if Wout is not None else 0
     logits = torch.empty(B, C, dtype=torch.float32, device=H.device) if Wout is not None else None
+    S = pool_splits(B, H.size(0), D)
+    if S > 1:
+        part = torch.empty(B * S * D, dtype=torch.float32, device=H.device)
+        _lib.call("lgnn_pool_head_fwd_split", _lib.ptr(H), _lib.ptr(graph.gptr), B, D,
+                  int(mean), _lib.ptr(Wout), _lib.ptr(bout), C, S, _lib.ptr(part),
+                  _lib.ptr(pool_tickets(H.device, B)), _lib.ptr(pooled), _lib.ptr(logits),
+                  _s(H.device))
+        return pooled, logits
     _lib.call("lgnn_pool_head_fwd", _lib.ptr(H), _lib.ptr(graph.gptr), B, D, int(mean),
               _lib.ptr(Wout), _lib.ptr(bout), C, _lib.ptr(pooled), _lib.ptr(logits),
               _s(H.device))
