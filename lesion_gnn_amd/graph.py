@@ -91,8 +91,13 @@ class Graph:
         if kind in self._csr:
             return self._csr[kind]
         if torch.compiler.is_compiling():  # traced: the graph build is one opaque lgnn op
-            rp, col, w, tp, ti, tw, tmap, topen, err = torch.ops.lgnn.graph_build(
-                self.edge_index, self.num_nodes, kind)
+            if self._gptr is None and self.batch is not None:  # Batch.ptr rides along
+                rp, col, w, tp, ti, tw, tmap, topen, err, self._gptr = \
+                    torch.ops.lgnn.graph_build_b(self.edge_index, self.num_nodes, kind,
+                                                 self.batch, self.num_graphs)
+            else:
+                rp, col, w, tp, ti, tw, tmap, topen, err = torch.ops.lgnn.graph_build(
+                    self.edge_index, self.num_nodes, kind)
             c = Csr(rowptr=rp, col=col, w=w, tptr=tp, tidx=ti, tw=tw,
                     tmap=tmap if kind == "gat" else None,
                     tile_open=topen if kind == "gcn" else None, err=err)

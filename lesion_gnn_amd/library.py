@@ -117,6 +117,30 @@ def graph_build(edge_index: Tensor, num_nodes: int, kind: str) -> list[Tensor]:
 
 @graph_build.register_fake
 def _(edge_index, num_nodes, kind):
+    return _graph_build_fake(edge_index, num_nodes, kind)
+
+
+@custom_op("lgnn::graph_build_b", mutates_args=(), device_types="cuda")
+def graph_build_b(edge_index: Tensor, num_nodes: int, kind: str, batch: Tensor,
+                  num_graphs: int) -> list[Tensor]:
+    """graph_build with the batch vector: the graph offsets (Batch.ptr) ride along with the
+    build's first launch (no separate lgnn_batch_ptr launch): [graph_build's nine, gptr]."""
+    from .graph import Graph
+
+    g = Graph(edge_index, num_nodes, batch, num_graphs)
+    c = g.csr(kind)
+    dev = edge_index.device
+    return [c.rowptr, c.col, c.w, c.tptr, c.tidx, c.tw, _enc(c.tmap, dev),
+            _enc(c.tile_open, dev), c.err, g.gptr]
+
+
+@graph_build_b.register_fake
+def _(edge_index, num_nodes, kind, batch, num_graphs):
+    return _graph_build_fake(edge_index, num_nodes, kind) + [
+        batch.new_empty(num_graphs + 1, dtype=torch.int32)]
+
+
+def _graph_build_fake(edge_index, num_nodes, kind):
     n = num_nodes
     cap = edge_index.shape[1] + n
     i32 = dict(dtype=torch.int32)
