@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 28
+#define LGNN_ABI_VERSION 29
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -528,7 +528,7 @@ int lgnn_gcn_stack_bwd(const float* dP, const int64_t* batch, const int32_t* gpt
  * reference (models/base.py:162-188), in one launch over up to 16 fp32 tensors.
  *   decoupled = 0: Adam (L2: g += weight_decay * p); 1: AdamW (p *= 1 - lr * weight_decay).
  *   step: device float, the number of steps taken (read by every workgroup; with advance = 1
- *   incremented once, by the last one); ticket: device uint32, zero before the first call
+ *   incremented once, by the last one); ticket: device uint32[9], zero before the first call
  *   (re-armed by the call). Split a longer list over several calls with advance = 0 on all but
  *   the last (every call of one step then uses the same step count).
  *   Graph-capturable (lr and the betas are launch arguments: fixed in a captured graph).
@@ -652,7 +652,7 @@ int lgnn_s3_wgrad(const float* dY, int N, const float* X, int64_t M, int K, int 
  *     out[j][i] = u(j, i) >= thr[j] ? scale[j] : 0,
  *     u(j, i) = mix(key + j * 0xD1B54A32D192ED03 + i * G) >> 40,  key = mix(seed ^ counter * G),
  *   mix = the splitmix64 finalizer, G = 0x9E3779B97F4A7C15, thr = (uint32)(p * 2^24) (<= 2^24),
- *   scale = fp32(1 / (1 - p)). state: device uint64[4] = [seed, counter, ticket, 0]; with
+ *   scale = fp32(1 / (1 - p)). state: device uint64[8] = [seed, counter, ticket words (zero)]; with
  *   advance != 0 the launch increments the counter when done (a captured graph draws fresh masks
  *   per replay). The masks are a pure function of (seed, counter, j, i): the CPU oracle
  *   regenerates them bit for bit (parity with dropout on).

@@ -69,5 +69,23 @@ __device__ __forceinline__ float bn_elu_grad(float z, float sc, float sh) {
   return zn > 0.f ? 1.f : __builtin_amdgcn_exp2f(zn * 1.44269504088896341f);
 }
 
+// Is this workgroup the last of the grid to get here? (thread 0 asks, after the workgroup's work.)
+// A two-level ticket: workgroup b first takes a ticket on word b % 8 — its group's own word, so a
+// group's same-address atomics serialise in one XCD's L2 in parallel with the others' (blocks are
+// dealt round-robin over the XCDs: speed only, correct for any placement) — then each group's
+// last arrival on word 8. At most ~gridDim/8 + 8 atomics meet on one word instead of gridDim.
+// tk: 9 zeroed words, left zero (re-armed). inc: 1, or any value the caller computes from the
+// data it read first (a dependency that orders those reads before the ticket; inc != 1 never
+// wins). Returns true for exactly one workgroup.
+__device__ __forceinline__ bool last_workgroup(unsigned int* tk, unsigned int inc) {
+  const unsigned int G = gridDim.x, g = blockIdx.x & 7u;
+  const unsigned int ng = (G - g + 7u) >> 3, groups = G < 8u ? G : 8u;
+  if (atomicAdd(tk + g, inc) != ng - 1u) return false;
+  tk[g] = 0u;
+  if (atomicAdd(tk + 8, 1u) != groups - 1u) return false;
+  tk[8] = 0u;
+  return true;
+}
+
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }

@@ -15,10 +15,10 @@
 //   mask[i]  = u >= thr ? scale : 0,   thr = (uint32)(p * 2^24),  scale = fp32(1 / (1 - p))
 // s = the job's stream id, i = the element index within the job's mask.
 //
-// State (device, uint64[4]): [seed, counter, ticket word, 0]. Every workgroup reads the seed and
-// counter; with `advance` the last workgroup to finish increments the counter and re-arms the
-// ticket, so a captured HIP graph draws fresh masks on every replay (torch's generator does the
-// same for captured dropout).
+// State (device, uint64[8]): [seed, counter, 9 ticket words (32-bit), 0...]. Every workgroup reads
+// the seed and counter; with `advance` the last workgroup to finish (last_workgroup: a two-level
+// ticket) increments the counter, so a captured HIP graph draws fresh masks on every replay
+// (torch's generator does the same for captured dropout).
 #include "common.h"
 
 namespace {
@@ -76,13 +76,9 @@ __global__ __launch_bounds__(kT) void k_masks(MaskJobs J, uint64_t* __restrict__
   // the ticket's operand depends on the counter read, so that read has returned before this
   // workgroup's ticket is taken (the last arrival then overwrites the counter safely)
   const unsigned int inc = ctr == ~0ull ? 2u : 1u;
-  if (threadIdx.x == 0) {
-    unsigned int* ticket = reinterpret_cast<unsigned int*>(state + 2);
-    if (atomicAdd(ticket, inc) == gridDim.x - 1) {
-      state[1] = ctr + 1;
-      *ticket = 0u;
-      __threadfence();
-    }
+  if (threadIdx.x == 0 && last_workgroup(reinterpret_cast<unsigned int*>(state + 2), inc)) {
+    state[1] = ctr + 1;
+    __threadfence();
   }
 }
 
@@ -112,7 +108,7 @@ extern "C" int lgnn_dropout_masks(int num_masks, float* const* out, const int64_
   int64_t total = 0;
   for (int i = 0; i < num_masks; ++i) total += numel[i] > 0 ? numel[i] : 0;
   // elements per workgroup: at least 4 per thread, and few enough workgroups (<= ~512 + jobs)
-  // that the one same-address ticket atomic per workgroup stays cheap (it serialises in L2)
+  // that the ticket atomics (last_workgroup: ~64 per word) stay cheap (they serialise in L2)
   int64_t per = (total + kMaxBlocks - 1) / kMaxBlocks;
   per = (per + 4 * kT - 1) / (4 * kT) * (4 * kT);
   if (per < 4 * kT) per = 4 * kT;

@@ -71,12 +71,9 @@ __global__ __launch_bounds__(kT) void k_adam(AdamJobs J, float* __restrict__ ste
   // its ticket is taken even when its loop ran no iteration (a numel-0 tensor): t >= 1 always,
   // but the compiler cannot drop the dependency.
   const unsigned int inc = t < 0.f ? 2u : 1u;
-  if (threadIdx.x == 0) {
-    if (atomicAdd(ticket, inc) == gridDim.x - 1) {
-      step[0] = t;
-      *ticket = 0u;
-      __threadfence();
-    }
+  if (threadIdx.x == 0 && last_workgroup(ticket, inc)) {
+    step[0] = t;
+    __threadfence();
   }
 }
 
@@ -95,8 +92,9 @@ extern "C" int lgnn_adam_step(int n, float* const* params, const float* const* g
   J.off[0] = 0;
   J.boff[0] = 0;
   // elements per workgroup: kE per thread, more when the tensors are large, so the grid stays
-  // within ~512 workgroups (+ one per tensor): the step ticket is one same-address atomic per
-  // workgroup, and those serialise in L2 (C3: 1.8k workgroups cost ~8 us of tickets)
+  // within ~512 workgroups (+ one per tensor): the step ticket (last_workgroup, two levels) is
+  // one same-address atomic per workgroup on its group's word, and those serialise in L2 (C3:
+  // 1.8k workgroups on one word cost ~8 us of tickets)
   int64_t total = 0;
   for (int i = 0; i < n; ++i) total += numels[i] > 0 ? numels[i] : 0;
   int64_t per = (total + 511) / 512;

@@ -9,7 +9,7 @@ function of (seed, counter, stream, element) — see include/lgnn.h — so the C
 (oracle/pyg_ref.py DropoutMasks) regenerates exactly the masks a step used.
 
 A model draws all masks of its forward in ONE launch from its generator state: a non-persistent
-buffer `_dropout_rng` (uint64 [seed, counter, ticket, 0] stored as int64; not in state_dict, so
+buffer `_dropout_rng` (uint64 [seed, counter, ticket words...] x 8, stored as int64; not in state_dict, so
 checkpoint keys stay PyG's; moved by .to(device)). The seed comes from torch's default generator
 when the model is built (torch.manual_seed makes runs reproducible, as for the weights); the launch
 advances the counter on the device, so captured HIP graphs draw fresh masks per replay.
@@ -25,16 +25,20 @@ from . import _lib
 MAX_MASKS = 16  # LGNN_MAX_MASKS
 
 
+STATE_WORDS = 8  # uint64: seed, counter, then the launch's ticket words (lgnn.h)
+
+
 def new_state(seed: int | None = None) -> torch.Tensor:
-    """A generator state [seed, counter = 0, ticket = 0, 0] (CPU; register it as a buffer)."""
+    """A generator state [seed, counter = 0, tickets = 0 ...] (CPU; register it as a buffer)."""
     if seed is None:
         seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-    return torch.tensor([int(seed), 0, 0, 0], dtype=torch.int64)
+    return torch.tensor([int(seed)] + [0] * (STATE_WORDS - 1), dtype=torch.int64)
 
 
 def set_state(state: torch.Tensor, seed: int, counter: int = 0) -> None:
     """Position a generator state (tests: the oracle regenerates the masks from (seed, counter))."""
-    state.copy_(torch.tensor([int(seed), int(counter), 0, 0], dtype=torch.int64))
+    state.copy_(torch.tensor([int(seed), int(counter)] + [0] * (STATE_WORDS - 2),
+                             dtype=torch.int64))
 
 
 def get_state(state: torch.Tensor) -> tuple[int, int]:
@@ -108,8 +112,8 @@ def dropout_masks_raw(state: torch.Tensor, numels: list, thr: int, scale: float)
     """All masks in one flat fp32 allocation (mask j at the sum of the earlier masks' sizes,
     each rounded up to 4 elements: 16-B aligned), drawn by one lgnn_dropout_masks launch."""
     _lib.require_gpu(state)
-    if state.dtype != torch.int64 or state.numel() != 4 or not state.is_contiguous():
-        raise _lib.LgnnError("dropout generator state must be a contiguous int64 [4] tensor")
+    if state.dtype != torch.int64 or state.numel() != STATE_WORDS or not state.is_contiguous():
+        raise _lib.LgnnError("dropout generator state must be a contiguous int64 [8] tensor")
     dev = state.device
     offs, tot = [], 0
     for n in numels:

@@ -62,7 +62,8 @@ class Adam(torch.optim.Optimizer):
                 self.state[p]["step"] = step_t
             ticket = self._tickets.get(gi)
             if ticket is None:
-                ticket = self._tickets[gi] = torch.zeros(1, dtype=torch.int32, device=dev)
+                # lgnn_adam_step's two-level ticket: 9 words, zeroed once, left zero
+                ticket = self._tickets[gi] = torch.zeros(9, dtype=torch.int32, device=dev)
             b1, b2 = group["betas"]
             for c in range(0, len(ps), MAX_TENSORS):
                 chunk = ps[c:c + MAX_TENSORS]
