@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 29
+#define LGNN_ABI_VERSION 30
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -76,6 +76,15 @@ const char* lgnn_status_string(int status);
  * in the same launches. gptr (nullable) [num_graphs + 1]: as lgnn_batch_ptr from batch [N],
  * in the same launches. *err_count is written (not accumulated). Workspace size:
  * lgnn_graph_workspace_bytes. N + E < 2^30. Five launches, no host synchronisation.
+ *
+ * Target-sorted fast path (builds without the source CSR, or lazy ones; no tmap): the first
+ * launch checks edge_index on the device — targets non-decreasing, indices valid, at most one
+ * self loop per row, at most 16 CSR entries per row, runs of at most 64 rows without entries and
+ * (lazy) no edge leaving its 64-node tile. When every check passes (k-NN input collated in graph
+ * order: PyG knn_graph groups the edges by target) the third launch writes the CSR by a scan of
+ * the row lengths and a coalesced copy, and the count / fill / finish launches return at once;
+ * otherwise the general counting-sort launches run. Same outputs either way (bit-identical).
+ * LGNN_GRAPH_SORTED=0 in the environment disables the fast path (A/B, tests).
  * ------------------------------------------------------------------------------------------- */
 size_t lgnn_graph_workspace_bytes(int64_t num_nodes, int64_t num_edges);
 int lgnn_graph_build(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes, int loops,
@@ -85,8 +94,9 @@ int lgnn_graph_build(const int64_t* edge_index, int64_t num_edges, int64_t num_n
                      void* workspace, size_t workspace_bytes, void* stream);
 /* lgnn_graph_build for a consumer that reads the source (transpose) CSR only for open tiles
  * (the fused GCN stack): tile_open and tptr required, tmap NULL; the tiles' open flags are set
- * by the count and scan passes, and tidx / tw are filled only when some tile is open (tptr is
- * always written). Same target CSR, flags and weights as lgnn_graph_build. */
+ * by the count and scan passes, and tptr / tidx / tw are meaningful only when some tile is open
+ * (the sorted fast path leaves them unwritten: it is taken only when no tile is open). Same target
+ * CSR, flags and weights as lgnn_graph_build. */
 int lgnn_graph_build_lazy(const int64_t* edge_index, int64_t E, int64_t N, int loops, int norm,
                           int32_t* rowptr, int32_t* col, float* w, int32_t* tptr, int32_t* tidx,
                           float* tw, int32_t* tmap, int32_t* tile_open, const int64_t* batch,
@@ -101,6 +111,12 @@ int lgnn_graph_build_sync(const int64_t* edge_index, int64_t E, int64_t N, int l
                           float* tw, int32_t* tmap, int32_t* tile_open, const int64_t* batch,
                           int64_t num_graphs, int32_t* gptr, int32_t* err_count, void* workspace,
                           size_t workspace_bytes, int lazy, int32_t* sync, void* stream);
+
+/* Diagnostic (synchronises `stream`): 1 when the last lgnn_graph_build[_lazy] on `workspace`
+ * took the target-sorted fast path, 0 when it ran the general launches. Meaningful only after a
+ * build that tried the fast path (see above). */
+int lgnn_graph_build_path(const void* workspace, int64_t num_nodes, int64_t num_edges,
+                          void* stream);
 
 /* Graph offsets from a sorted PyG `batch` vector (Batch.ptr): ptr[g] = first node of graph g,
  * ptr[B] = M. Replaces the count/offset half of PyG scatter(reduce='mean') over `batch`. */

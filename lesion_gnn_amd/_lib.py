@@ -37,6 +37,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_abi_version": (I32, []),
     "lgnn_status_string": (ctypes.c_char_p, [I32]),
     "lgnn_graph_workspace_bytes": (SZ, [I64, I64]),
+    "lgnn_graph_build_path": (I32, [P, I64, I64, P]),
     "lgnn_graph_build_lazy": (I32, [P, I64, I64, I32, I32, P, P, P, P, P, P, P, P, P, I64, P, P,
                                     P, SZ, P]),
     "lgnn_graph_build": (I32, [P, I64, I64, I32, I32, P, P, P, P, P, P, P, P, P, I64, P, P, P,
@@ -140,7 +141,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 29
+ABI_VERSION = 30
 
 _lib = None
 

@@ -25,11 +25,20 @@ constexpr int kFinishCap = 1536;   // staged CSR entries per k_finish block
 // k_build's barrier bound (~4 s): a row longer than kFinishCap is sorted by one thread in global
 // memory (seconds for thousands of entries) while the other workgroups wait at the next barrier
 constexpr int kBuildSpins = 1 << 24;
+// Target-sorted fast path (k_prep_sorted + the sorted body of k_scan): rows of at most
+// kSortedRowCap CSR entries (a 64-row tile then stays within the fused kernels' 1024 staged
+// entries), runs of at most kGapCap rows without entries, at most one self loop per row
+constexpr int kSortedRowCap = 16;
+constexpr int kGapCap = 64;
+constexpr int kVerdictMax = 256;  // k_prep_sorted workgroups (one verdict word each)
+constexpr int kSortedChunks = 8;   // k_prep_sorted: 64-edge chunks per wave pass
+constexpr int kSortedRows = 256;   // k_scan's sorted body: rows per workgroup (one per thread)
 
 inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
 inline size_t scan_bsum_bytes(int64_t N) {
-  return (size_t)2 * 4 * ((N + 1 + 1023) / 1024);  // 2 arrays x blocks of 1024 elements
+  // 2 arrays x blocks of 1024 elements; the sorted path's scan: one word per 256 rows
+  return (size_t)4 * 4 * ((N + 1 + 1023) / 1024);
 }
 
 struct GraphWs {
@@ -43,6 +52,11 @@ struct GraphWs {
   int32_t* teid;   // [E+N]
   int32_t* inv;    // [E+N] edge id -> target-CSR position (for tmap)
   float* dis;      // [N] deg^-1/2 (GCN normalisation), inf -> 0
+  int32_t* rs;     // [N+1] sorted path: first input edge of each row (rs[N] = E)
+  int32_t* scnt;   // [N] sorted path: entries of each row without its self loop
+  int32_t* lp;     // [N] sorted path: offset of the row's self loop in its input run, or -1
+  int32_t* verdict;  // [kVerdictMax + 1] sorted path: one word per k_prep_sorted workgroup, then
+                     // the summary k_scan writes for k_fill / k_finish
   size_t zero_bytes;
 };
 
@@ -65,12 +79,16 @@ GraphWs carve(void* base, int64_t N, int64_t E) {
   ws.teid = (int32_t*)take((E + N) * 4);
   ws.inv = (int32_t*)take((E + N) * 4);
   ws.dis = (float*)take(N * 4);
+  ws.rs = (int32_t*)take((N + 1) * 4);
+  ws.scnt = (int32_t*)take(N * 4);
+  ws.lp = (int32_t*)take(N * 4);
+  ws.verdict = (int32_t*)take((kVerdictMax + 1) * 4);
   return ws;
 }
 
 size_t ws_total(int64_t N, int64_t E) {
-  return align_up(4) + 2 * align_up((N + 1) * 4) + 3 * align_up(N * 4) + 3 * align_up((E + N) * 4) +
-         2 * align_up(scan_bsum_bytes(N)) + 256;
+  return align_up(4) + 3 * align_up((N + 1) * 4) + 5 * align_up(N * 4) + 3 * align_up((E + N) * 4) +
+         2 * align_up(scan_bsum_bytes(N)) + align_up((kVerdictMax + 1) * 4) + 256;
 }
 
 // Wave-level run detection over consecutive edges: lanes whose target equals the previous
@@ -130,6 +148,143 @@ __global__ __launch_bounds__(kThreads) void k_prep(int32_t* __restrict__ zero, i
                                                    const int64_t* __restrict__ batch, int64_t M,
                                                    int64_t B, int32_t* __restrict__ gptr) {
   prep_body(zero, nzero, tile_open, ntiles, batch, M, B, gptr, blockIdx.x, gridDim.x);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Target-sorted fast path. k-NN input (PyG knn_graph per graph, collated in graph order) arrives
+// grouped by target with rows in ascending order: each row's messages are one contiguous run of
+// edge_index, already in edge-id order, so the counting sort (count / fill / finish) reduces to a
+// scan of the row lengths and a coalesced copy. The first launch (k_prep_sorted, in place of
+// k_prep) does k_prep's zeroing and, per edge, checks the input: targets non-decreasing, indices
+// in range, at most one self loop per row, rows of at most kSortedRowCap entries, empty-row runs
+// of at most kGapCap, and (lazy build) no edge leaving its 64-row tile — any failure sends the
+// build down the general launches. The head edge of each row records the row's run (rs, scnt,
+// lp) and dis. Every workgroup writes its verdict word (no zeroing needed); the later launches
+// OR the words: all clear -> k_scan writes the CSR (sorted body) and k_count / k_fill / k_finish
+// return at once; else they run as before and k_scan runs its scan. The CSR is bit-identical to
+// the general path's: same entry order (the row's edges in edge-id order, its self loop last),
+// the same weight expression.
+struct SortedArgs {
+  const int64_t* ei;
+  int64_t E;
+  int loops, add_loop, norm, need_closed;
+  int32_t *rs, *scnt, *lp;
+  float* dis;
+  int32_t* verdict;
+  int nverdict;
+};
+
+__device__ __forceinline__ void sorted_empty_row(const SortedArgs& a, int64_t r, int64_t start) {
+  a.rs[r] = (int32_t)start;
+  a.scnt[r] = 0;
+  a.lp[r] = -1;
+  a.dis[r] = a.add_loop ? 1.0f / sqrtf(1.0f) : 0.0f;
+}
+
+__global__ __launch_bounds__(kThreads) void k_prep_sorted(int32_t* __restrict__ zero,
+                                                          int64_t nzero,
+                                                          int32_t* __restrict__ tile_open,
+                                                          int64_t ntiles,
+                                                          const int64_t* __restrict__ batch,
+                                                          int64_t M, int64_t B,
+                                                          int32_t* __restrict__ gptr,
+                                                          SortedArgs a) {
+  constexpr int CH = kSortedChunks;
+  const int64_t E = a.E, N = M;
+  const int64_t* __restrict__ src = a.ei;
+  const int64_t* __restrict__ dst = a.ei + E;
+  const bool drop_loops = a.loops != LGNN_LOOPS_KEEP;
+  const int lane = threadIdx.x & 63;
+  const int64_t wv = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
+  const int64_t nwv = ((int64_t)gridDim.x * kThreads) >> 6;
+  int bad = 0;
+  bool prepped = false;
+  // a wave takes CH chunks of 64 consecutive edges (+ one chunk of look-ahead for the row that
+  // runs past the last one), every load issued up front; rows are found by wave run detection.
+  // k_prep's zeroing runs behind the first pass's loads.
+  for (int64_t base = wv * 64 * CH; base < E; base += nwv * 64 * CH) {
+    int64_t s[CH + 1], d[CH + 1];
+#pragma unroll
+    for (int c = 0; c <= CH; ++c) {
+      const int64_t e = base + 64 * c + lane;
+      s[c] = e < E ? src[e] : -1;
+      d[c] = e < E ? dst[e] : -1;
+    }
+    const int64_t before = base > 0 ? dst[base - 1] : -1;
+    if (!prepped) {
+      prep_body(zero, nzero, tile_open, ntiles, batch, M, B, gptr, blockIdx.x, gridDim.x);
+      prepped = true;
+    }
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int64_t e = base + 64 * c + lane;
+      const bool in = e < E;
+      const int64_t last_prev = c == 0 ? before : __shfl(d[c - 1], 63, 64);
+      int64_t dp = __shfl_up(d[c], 1, 64);
+      if (lane == 0) dp = last_prev;
+      const Run r = wave_run(in ? d[c] : -2 - lane);
+      const unsigned long long lm = __ballot(in && drop_loops && s[c] == d[c]);
+      // the chunk's last row continuing into the next chunk: its leading lanes with the same
+      // target (sorted input), and the self loops among them
+      const int64_t dl = __shfl(d[c], 63, 64);
+      const unsigned long long cm = __ballot(dl >= 0 && d[c + 1] == dl);
+      const unsigned long long clm = __ballot(drop_loops && d[c + 1] >= 0 && s[c + 1] == d[c + 1]);
+      const int clen = ~cm == 0 ? 64 : __ffsll((long long)~cm) - 1;
+      const unsigned long long cmask = clen >= 64 ? ~0ull : (1ull << clen) - 1;
+      if (!in) continue;
+      const int64_t sv = s[c], dv = d[c];
+      if (!edge_ok(sv, dv, N) || dp > dv) {
+        bad = 1;
+        continue;
+      }
+      if (a.need_closed && (sv >> 6) != (dv >> 6)) bad = 1;
+      if (dv != dp) {  // head of row dv: the rows since the previous target have no entries
+        const int64_t r0 = dp < 0 ? 0 : dp + 1;
+        if (dv - r0 > kGapCap) {
+          bad = 1;
+        } else {
+          for (int64_t q = r0; q < dv; ++q) sorted_empty_row(a, q, e);
+        }
+        const unsigned long long run = (r.len >= 64 ? ~0ull : ((1ull << r.len) - 1)) << lane;
+        int n = r.len, nl = __popcll(lm & run);
+        int lpos = nl ? __ffsll((long long)(lm & run)) - 1 - lane : -1;
+        if (lane + r.len == 64) {
+          const int cl = __popcll(clm & cmask);
+          if (nl == 0 && cl) lpos = r.len + __ffsll((long long)(clm & cmask)) - 1;
+          nl += cl;
+          n += clen;
+          if (clen == 64) bad = 1;  // longer than any row the fast path takes
+        }
+        const int deg = n - nl;
+        if (n > kSortedRowCap + 1 || nl > 1 || deg + a.add_loop > kSortedRowCap) bad = 1;
+        a.rs[dv] = (int32_t)e;
+        a.scnt[dv] = deg;
+        a.lp[dv] = nl ? lpos : -1;
+        const int dg = deg + a.add_loop;
+        a.dis[dv] = dg > 0 ? 1.0f / sqrtf((float)dg) : 0.0f;
+      }
+      if (e == E - 1) {  // rows after the last target
+        if (N - 1 - dv > kGapCap) {
+          bad = 1;
+        } else {
+          for (int64_t q = dv + 1; q < N; ++q) sorted_empty_row(a, q, E);
+        }
+        a.rs[N] = (int32_t)E;
+      }
+    }
+  }
+  if (!prepped) prep_body(zero, nzero, tile_open, ntiles, batch, M, B, gptr, blockIdx.x, gridDim.x);
+  bad = __syncthreads_or(bad);
+  if (threadIdx.x == 0) a.verdict[blockIdx.x] = bad;
+}
+
+// true when k_prep_sorted found the input target-sorted (every workgroup's verdict clear);
+// block-uniform, every thread of the block must call it
+__device__ __forceinline__ bool sorted_ok(const int32_t* verdict, int nverdict) {
+  if (!verdict) return false;
+  int v = 0;
+  for (int i = threadIdx.x; i < nverdict; i += blockDim.x) v |= verdict[i];
+  return __syncthreads_or(v) == 0;
 }
 
 // Edge passes. A block takes a chunk of kChunk consecutive edges, kPer per thread, so every
@@ -242,9 +397,11 @@ __device__ __forceinline__ void count_body(const int64_t* __restrict__ ei, int64
 __global__ __launch_bounds__(kThreads) void k_count(const int64_t* __restrict__ ei, int64_t E,
                                                     int64_t N, int loops, int32_t* cnt,
                                                     int32_t* tcnt, int32_t* err,
-                                                    int32_t* tile_open) {
+                                                    int32_t* tile_open,
+                                                    const int32_t* verdict, int nverdict) {
   __shared__ int hist[kBins];
   __shared__ int red[2 * kThreads / 64];
+  if (sorted_ok(verdict, nverdict)) return;
   count_body(ei, E, N, loops, cnt, tcnt, err, tile_open, hist, red, blockIdx.x);
 }
 
@@ -314,9 +471,11 @@ __global__ __launch_bounds__(kThreads) void k_fill(const int64_t* __restrict__ e
                                                    int32_t* fill, int32_t* col, int32_t* eid,
                                                    const int32_t* __restrict__ tptr,
                                                    int32_t* tfill, int32_t* tidx, int32_t* teid,
-                                                   const int32_t* lazy_open) {
+                                                   const int32_t* lazy_open,
+                                                   const int32_t* summary) {
   __shared__ int hist[kBins];
   __shared__ int red[2 * kThreads / 64];
+  if (summary && __builtin_amdgcn_readfirstlane(*summary)) return;  // sorted path took it
   fill_body(ei, E, N, loops, rowptr, fill, col, eid, tptr, tfill, tidx, teid, lazy_open, hist, red,
             blockIdx.x);
 }
@@ -375,13 +534,13 @@ __device__ __forceinline__ void scan_body(const int32_t* __restrict__ cnt,
   }
   if (lane == 63) wsc[wave] = x;
   __syncthreads();
-  if (tid == 0)
+  if (tid == 0)  // relaxed: the flag word is its own payload (as in sorted_body)
     __hip_atomic_store(&st[bx], (wsc[0] + wsc[1] + wsc[2] + wsc[3]) | kScanFlag,
-                       __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   int pre = 0;  // sums of the preceding blocks, thread-strided, then combined in wave order
   for (int j = tid; j < bx; j += kScanT) {
     int f;
-    while (((f = __hip_atomic_load(&st[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) &
+    while (((f = __hip_atomic_load(&st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) &
             kScanFlag) == 0)
       __builtin_amdgcn_s_sleep(1);
     pre += f & (kScanFlag - 1);
@@ -415,6 +574,131 @@ __device__ __forceinline__ void scan_body(const int32_t* __restrict__ cnt,
   }
 }
 
+// Sorted body of k_scan (kSortedRows rows per workgroup, one per thread): rowptr = exclusive
+// scan of (entries without the self loop + the appended loop), chained across workgroups as the
+// general scan; then the workgroup copies its rows' input run — one contiguous range of
+// edge_index — into the CSR, coalesced, all loads of a pass issued up front: entry e of row d goes
+// to rowptr[d] + (e - rs[d]), one slot less past the row's self loop (which is skipped); the
+// appended loops take the last slot of each row.
+struct SortedSmem {
+  int32_t rp[kSortedRows + 1];
+  int32_t rs[kSortedRows + 1];
+  int32_t lp[kSortedRows];
+  float dis[kSortedRows];
+  int wsum[kSortedRows / 64];
+  int wpre[kSortedRows / 64];
+};
+
+__device__ __forceinline__ void sorted_body(const SortedArgs& a, int64_t N, int32_t* stat,
+                                            int32_t* __restrict__ rowptr,
+                                            int32_t* __restrict__ col, float* __restrict__ w,
+                                            int32_t* tile_open, int32_t* err_out, SortedSmem& ss,
+                                            int bx) {
+  constexpr int PASS = 8;  // entries per thread per copy pass
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t r0 = (int64_t)bx * kSortedRows;
+  const int nrow = (int)(N - r0 < kSortedRows ? N - r0 : kSortedRows);
+  const int64_t row = r0 + tid;
+  const int64_t E = a.E;
+  const int64_t* __restrict__ src = a.ei;
+  const int64_t* __restrict__ dst = a.ei + E;
+  const bool gcn = a.norm == LGNN_NORM_GCN;
+  // the copy's first pass (edge_index rows and the sources' dis) does not depend on the scan:
+  // issued first, its latency overlaps the scan and the look-back
+  const int in0 = a.rs[r0], in1 = a.rs[r0 + nrow];
+  int64_t sv[PASS], dv[PASS];
+  float ds[PASS];
+  auto load_pass = [&](int e0) {
+#pragma unroll
+    for (int it = 0; it < PASS; ++it) {
+      const int e = e0 + it * kSortedRows + tid;
+      sv[it] = e < in1 ? src[e] : 0;
+      dv[it] = e < in1 ? dst[e] : r0;
+    }
+#pragma unroll
+    for (int it = 0; it < PASS; ++it) ds[it] = gcn && w ? a.dis[sv[it]] : 1.0f;
+  };
+  load_pass(in0);
+  int v = 0;
+  if (tid < nrow) {
+    v = a.scnt[row] + a.add_loop;
+    ss.rs[tid] = a.rs[row];
+    ss.lp[tid] = a.lp[row];
+    ss.dis[tid] = a.dis[row];
+  }
+  if (tid == 0) ss.rs[nrow] = in1;
+  int x = v;  // inclusive scan in the wave
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) ss.wsum[wave] = x;
+  __syncthreads();
+  int tot = 0, before = 0;
+#pragma unroll
+  for (int q = 0; q < kSortedRows / 64; ++q) {
+    tot += ss.wsum[q];
+    before += q < wave ? ss.wsum[q] : 0;
+  }
+  // the flag word carries its own payload (the sum), so relaxed agent-scope atomics suffice: no
+  // release / acquire fence (an agent-scope release writes back the XCD's whole L2)
+  if (tid == 0)
+    __hip_atomic_store(&stat[bx], tot | kScanFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int pre = 0;  // the preceding workgroups' sums, thread-strided, combined in a fixed order
+  for (int j = tid; j < bx; j += kSortedRows) {
+    int f;
+    while (((f = __hip_atomic_load(&stat[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) &
+            kScanFlag) == 0)
+      __builtin_amdgcn_s_sleep(1);
+    pre += f & (kScanFlag - 1);
+  }
+  for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
+  if (lane == 0) ss.wpre[wave] = pre;
+  __syncthreads();
+  int base = 0;
+#pragma unroll
+  for (int q = 0; q < kSortedRows / 64; ++q) base += ss.wpre[q];
+  const int excl = base + before + x - v;
+  if (tid < nrow) {
+    rowptr[row] = excl;
+    ss.rp[tid] = excl;
+  }
+  if (tid == nrow - 1) {
+    ss.rp[nrow] = excl + v;
+    if (r0 + nrow == N) rowptr[N] = excl + v;
+  }
+  if (err_out && bx == 0 && tid == 0) *err_out = 0;
+  __syncthreads();
+  const int64_t ntiles = (N + 63) >> 6;
+  for (int e0 = in0; e0 < in1; e0 += PASS * kSortedRows) {
+    if (e0 != in0) load_pass(e0);
+#pragma unroll
+    for (int it = 0; it < PASS; ++it) {
+      const int e = e0 + it * kSortedRows + tid;
+      if (e >= in1) break;
+      const int dl = (int)(dv[it] - r0);
+      const int off = e - ss.rs[dl], lpd = ss.lp[dl];
+      if (off == lpd) continue;  // the row's self loop: appended at the end instead
+      const int pos = ss.rp[dl] + off - (lpd >= 0 && off > lpd ? 1 : 0);
+      col[pos] = (int32_t)sv[it];
+      if (w) w[pos] = gcn ? (ds[it] * 1.0f) * ss.dis[dl] : 1.0f;
+      if (tile_open && (sv[it] >> 6) != (dv[it] >> 6)) {
+        if (tile_open[dv[it] >> 6] == 0) mark_open(tile_open, dv[it] >> 6, ntiles);
+        if (tile_open[sv[it] >> 6] == 0) mark_open(tile_open, sv[it] >> 6, ntiles);
+      }
+    }
+  }
+  if (a.add_loop && tid < nrow) {
+    const int pos = ss.rp[tid + 1] - 1;
+    col[pos] = (int32_t)row;
+    if (w) {
+      const float di = ss.dis[tid];
+      w[pos] = gcn ? (di * 1.0f) * di : 1.0f;
+    }
+  }
+}
+
 __global__ __launch_bounds__(kScanT) void k_scan(const int32_t* __restrict__ cnt,
                                                  const int32_t* __restrict__ tcnt, int64_t N,
                                                  int add, int32_t* stat,
@@ -423,10 +707,22 @@ __global__ __launch_bounds__(kScanT) void k_scan(const int32_t* __restrict__ cnt
                                                  int32_t* __restrict__ fill,
                                                  int32_t* __restrict__ tfill,
                                                  float* __restrict__ dis,
-                                                 int32_t* tile_open) {
+                                                 int32_t* tile_open, SortedArgs sa,
+                                                 int32_t* __restrict__ col, float* __restrict__ w,
+                                                 int32_t* err_out, int nblk) {
   __shared__ ScanSmem sm;
+  __shared__ SortedSmem ss;
+  const bool fast = sorted_ok(sa.verdict, sa.nverdict);
+  if (sa.verdict && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+    sa.verdict[kVerdictMax] = fast;  // the summary word k_fill / k_finish read
+  if (fast) {
+    if (blockIdx.y == 0 && (int64_t)blockIdx.x * kSortedRows < N)
+      sorted_body(sa, N, stat, rowptr, col, w, tile_open, err_out, ss, blockIdx.x);
+    return;
+  }
+  if ((int)blockIdx.x >= nblk) return;
   scan_body(cnt, tcnt, N, add, stat, rowptr, tptr, fill, tfill, dis, tile_open, sm, blockIdx.x,
-            blockIdx.y, gridDim.x);
+            blockIdx.y, nblk);
 }
 
 // insertion sort of n (key, val) pairs by key (keys distinct)
@@ -446,8 +742,8 @@ __device__ __forceinline__ void sort_row(KP key, VP val, int n) {
 }
 
 // by = 0: target CSR (rowptr/col/eid/w); 1: source CSR (tptr/tidx/teid/tw). One virtual block
-// = kFinT rows, run by kFinT threads (tid = 0..63) with `sync` their barrier: the whole workgroup
-// of k_finish, or one wave of the fused build (k_build) with its own staging arrays.
+// = kFinT rows, run by one wave (tid = lane 0..63) with its own staging arrays and `sync` its
+// wave-scope ordering (k_finish and the fused build's finish phase alike).
 // Weight of entry (row i, neighbour j): GCN (dis(src) * 1) * dis(dst) = dis(j) * dis(i).
 template <typename Sync>
 __device__ __forceinline__ void finish_body(int64_t N, int64_t E, int add_loop, int norm,
@@ -539,9 +835,6 @@ __device__ __forceinline__ void finish_body(int64_t N, int64_t E, int add_loop, 
   sync();  // the staging arrays are free for the next virtual block
 }
 
-struct BlockSync {
-  __device__ void operator()() const { __syncthreads(); }
-};
 // one wave: its LDS accesses are ordered by a wave-scope fence (no cross-wave barrier)
 struct WaveSync {
   __device__ void operator()() const {
@@ -551,7 +844,10 @@ struct WaveSync {
   }
 };
 
-__global__ __launch_bounds__(kFinT) void k_finish(int64_t N, int64_t E, int add_loop, int norm,
+// four 64-row virtual blocks per workgroup, one per wave (each wave its own staging arrays and
+// wave-scope ordering, as k_build's finish phase): a quarter of the workgroups to dispatch
+constexpr int kFinWaves = kThreads / 64;
+__global__ __launch_bounds__(kThreads) void k_finish(int64_t N, int64_t E, int add_loop, int norm,
                                                      const int32_t* __restrict__ rowptr,
                                                      int32_t* col, int32_t* eid, float* w,
                                                      const int32_t* __restrict__ tptr,
@@ -559,12 +855,17 @@ __global__ __launch_bounds__(kFinT) void k_finish(int64_t N, int64_t E, int add_
                                                      const float* __restrict__ dis,
                                                      const int32_t* __restrict__ ws_err,
                                                      int32_t* err_out, int32_t* tile_open,
-                                                     int lazy, int32_t* __restrict__ inv) {
-  __shared__ int32_t s_key[kFinishCap];
-  __shared__ int32_t s_val[kFinishCap];
+                                                     int lazy, int32_t* __restrict__ inv,
+                                                     const int32_t* summary) {
+  __shared__ int32_t s_key[kFinWaves][kFinishCap];
+  __shared__ int32_t s_val[kFinWaves][kFinishCap];
+  if (summary && __builtin_amdgcn_readfirstlane(*summary)) return;  // sorted path took it
+  const int wave = threadIdx.x >> 6;
+  const int64_t v = (int64_t)blockIdx.x * kFinWaves + wave;
+  if (v * kFinT >= N) return;
   finish_body(N, E, add_loop, norm, rowptr, col, eid, w, tptr, tidx, teid, tw, dis, ws_err,
-              err_out, tile_open, lazy, inv, s_key, s_val, blockIdx.x, blockIdx.y, threadIdx.x,
-              BlockSync{});
+              err_out, tile_open, lazy, inv, s_key[wave], s_val[wave], v, blockIdx.y,
+              threadIdx.x & 63, WaveSync{});
 }
 
 // tmap[q] = position in the target CSR of the edge at source-CSR position q (both CSRs hold the
@@ -757,6 +1058,32 @@ extern "C" int lgnn_graph_build_lazy(const int64_t* edge_index, int64_t E, int64
                      stream, 1);
 }
 
+// k_prep_sorted's workgroups (= verdict words)
+static int sorted_grid(int64_t N, int64_t E) {
+  (void)N;
+  const int64_t per = (int64_t)kThreads * kSortedChunks;  // edges per workgroup pass
+  int64_t g = (E + per - 1) / per;
+  return (int)(g < 1 ? 1 : g > kVerdictMax ? kVerdictMax : g);
+}
+
+extern "C" int lgnn_graph_build_path(const void* workspace, int64_t num_nodes, int64_t num_edges,
+                                     void* stream) {
+  if (!workspace || num_nodes <= 0 || num_edges <= 0) return 0;
+  const GraphWs ws = carve(const_cast<void*>(workspace), num_nodes, num_edges);
+  int32_t v = 0;
+  if (hipMemcpyAsync(&v, ws.verdict + kVerdictMax, 4, hipMemcpyDeviceToHost,
+                     as_stream(stream)) != hipSuccess ||
+      hipStreamSynchronize(as_stream(stream)) != hipSuccess)
+    return LGNN_EINVAL;
+  return v ? 1 : 0;
+}
+
+// the target-sorted fast path is tried unless LGNN_GRAPH_SORTED=0 (a test / A-B knob)
+static bool sorted_path_enabled() {
+  const char* e = getenv("LGNN_GRAPH_SORTED");
+  return !(e && e[0] == '0');
+}
+
 static int graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loops, int norm,
                        int32_t* rowptr, int32_t* col, float* w, int32_t* tptr, int32_t* tidx,
                        float* tw, int32_t* tmap, int32_t* tile_open, const int64_t* batch,
@@ -805,12 +1132,33 @@ static int graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loop
     LGNN_LAUNCH_CHECK();
     return LGNN_OK;
   }
+  // target-sorted fast path: only for builds without the source CSR (or lazily with it) and
+  // without tmap
+  SortedArgs sa{};
+  const bool try_sorted = sorted_path_enabled() && N > 0 && E > 0 && !tmap && (!tptr || lazy);
   {
     const int64_t nzero = (int64_t)(ws.zero_bytes / 4);
     const int64_t ntiles = (N + 63) / 64;
-    hipLaunchKernelGGL(k_prep, dim3(grid_for(nzero > N + 1 ? nzero : N + 1, 1024)),
-                       dim3(kThreads), 0, s, ws.err, nzero, tile_open, ntiles, batch, N,
-                       num_graphs, gptr);
+    if (try_sorted) {
+      sa.ei = edge_index;
+      sa.E = E;
+      sa.loops = loops;
+      sa.add_loop = add_loop;
+      sa.norm = norm;
+      sa.need_closed = tptr != nullptr;  // lazy: an edge leaving its tile needs the source CSR
+      sa.rs = ws.rs;
+      sa.scnt = ws.scnt;
+      sa.lp = ws.lp;
+      sa.dis = ws.dis;
+      sa.verdict = ws.verdict;
+      sa.nverdict = sorted_grid(N, E);
+      hipLaunchKernelGGL(k_prep_sorted, dim3(sa.nverdict), dim3(kThreads), 0, s, ws.err, nzero,
+                         tile_open, ntiles, batch, N, num_graphs, gptr, sa);
+    } else {
+      hipLaunchKernelGGL(k_prep, dim3(grid_for(nzero > N + 1 ? nzero : N + 1, 1024)),
+                         dim3(kThreads), 0, s, ws.err, nzero, tile_open, ntiles, batch, N,
+                         num_graphs, gptr);
+    }
     LGNN_LAUNCH_CHECK();
   }
   if (N == 0) {
@@ -823,27 +1171,31 @@ static int graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loop
   if (E > 0) {
     hipLaunchKernelGGL(k_count, dim3((unsigned)((E + kChunk - 1) / kChunk)), dim3(kThreads), 0,
                        s, edge_index, E, N, loops, ws.cnt, tptr ? ws.tcnt : nullptr, ws.err,
-                       lazy ? tile_open : nullptr);
+                       lazy ? tile_open : nullptr, sa.verdict, sa.nverdict);
     LGNN_LAUNCH_CHECK();
   }
   {
     const int64_t nblk = (N + 1 + kScanBlk - 1) / kScanBlk;
-    dim3 sg((unsigned)nblk, tptr ? 2u : 1u);
+    const int64_t nsb = try_sorted ? (N + kSortedRows - 1) / kSortedRows : 0;
+    dim3 sg((unsigned)(nsb > nblk ? nsb : nblk), tptr ? 2u : 1u);
     hipLaunchKernelGGL(k_scan, sg, dim3(kScanT), 0, s, ws.cnt, ws.tcnt, N, add_loop, ws.stat,
-                       rowptr, tptr, ws.fill, ws.tfill, ws.dis, lazy ? tile_open : nullptr);
+                       rowptr, tptr, ws.fill, ws.tfill, ws.dis, lazy ? tile_open : nullptr, sa,
+                       col, w, err_count, (int)nblk);
     LGNN_LAUNCH_CHECK();
   }
   if (E > 0) {
     hipLaunchKernelGGL(k_fill, dim3((unsigned)((E + kChunk - 1) / kChunk)), dim3(kThreads), 0,
                        s, edge_index, E, N, loops, rowptr, ws.fill, col, ws.eid, tptr, ws.tfill,
-                       tidx, ws.teid, lazy ? tile_open + (N + 63) / 64 : nullptr);
+                       tidx, ws.teid, lazy ? tile_open + (N + 63) / 64 : nullptr,
+                       try_sorted ? ws.verdict + kVerdictMax : nullptr);
     LGNN_LAUNCH_CHECK();
   }
-  dim3 fg((unsigned)((N + kFinT - 1) / kFinT), tptr ? 2u : 1u);
+  const int64_t nfin = (N + kFinT - 1) / kFinT;
+  dim3 fg((unsigned)((nfin + kFinWaves - 1) / kFinWaves), tptr ? 2u : 1u);
   // with tmap, the target side of k_finish also writes inv (edge id -> target-CSR position)
-  hipLaunchKernelGGL(k_finish, fg, dim3(kFinT), 0, s, N, E, add_loop, norm, rowptr, col,
+  hipLaunchKernelGGL(k_finish, fg, dim3(kThreads), 0, s, N, E, add_loop, norm, rowptr, col,
                      ws.eid, w, tptr, tidx, ws.teid, tw, ws.dis, ws.err, err_count, tile_open,
-                     lazy, tmap ? ws.inv : nullptr);
+                     lazy, tmap ? ws.inv : nullptr, try_sorted ? ws.verdict + kVerdictMax : nullptr);
   LGNN_LAUNCH_CHECK();
   if (tmap) {
     const int g = grid_for(E + N, 2048);

@@ -137,7 +137,19 @@ class Graph:
             _lib.call("lgnn_graph_build_lazy" if kind == "gcn_lazy" else "lgnn_graph_build",
                       *args, _lib.stream(dev))
         self._csr[kind] = c
+        self._last_ws = (kind, ws)
         return c
+
+    def build_path(self, kind: str) -> str:
+        """Which launches the last eager build of `kind` took: "sorted" (the target-sorted fast
+        path: k-NN input grouped by target) or "general" (the counting sort). Synchronises."""
+        k, ws = getattr(self, "_last_ws", (None, None))
+        if k != kind:
+            raise ValueError(f"no eager build of {kind!r} on this graph")
+        r = _lib.load().lgnn_graph_build_path(_lib.ptr(ws), self.num_nodes, self.num_edges,
+                                              _lib.stream(self.device))
+        _lib.check(r if r < 0 else 0, "lgnn_graph_build_path")
+        return "sorted" if r == 1 else "general"
 
     def weighted(self, edge_weight: torch.Tensor) -> str:
         """Register the CSR pair carrying per-edge weights `edge_weight` [E] (edge order, e.g.

@@ -405,10 +405,11 @@ def test_head_backward_folded_into_stack(cuda, classes, pool, monkeypatch):
 
 @pytest.mark.parametrize("case", ["aligned", "ragged", "capacity"])
 def test_lazy_transpose_build(cuda, case):
-    """lgnn_graph_build_lazy (the fused GCN stack's build): the target CSR, the tile flags (cross
-    edges marked in the count pass, the > 1024-entry capacity rule in the scan) and tptr equal
-    the full build's bit for bit; the source CSR (tidx / tw) is built exactly when some tile is
-    open (ragged graphs, dense tiles) and then equals the full build's."""
+    """lgnn_graph_build_lazy (the fused GCN stack's build): the target CSR and the tile flags
+    (cross edges marked in the count pass, the > 1024-entry capacity rule in the scan) equal the
+    full build's bit for bit; the source CSR (tptr / tidx / tw) is built exactly when some tile
+    is open (ragged graphs, dense tiles) and then equals the full build's (aligned k-NN input
+    takes the target-sorted path, which leaves it unwritten)."""
     if case == "aligned":
         b = synth.make_batch(64, n=64, k=8, d_in=8, seed=51)
     elif case == "ragged":
@@ -418,7 +419,7 @@ def test_lazy_transpose_build(cuda, case):
     g = Graph(b.edge_index.to(cuda), b.num_nodes)
     full, lazy = g.csr("gcn"), g.csr("gcn_lazy")
     nnz = int(full.rowptr[-1])  # arrays have capacity E + N; entries past nnz are unused
-    for name in ("rowptr", "tptr", "err"):
+    for name in ("rowptr", "err"):
         assert torch.equal(getattr(full, name), getattr(lazy, name)), name
     for name in ("col", "w"):
         assert torch.equal(getattr(full, name)[:nnz], getattr(lazy, name)[:nnz]), name
@@ -427,8 +428,10 @@ def test_lazy_transpose_build(cuda, case):
     nt = (b.num_nodes + 63) // 64
     n_open = int(to_lazy[nt])
     assert (n_open == 0) == (case == "aligned")
+    assert g.build_path("gcn_lazy") == ("sorted" if case == "aligned" else "general")
     if n_open:
         assert int(full.tptr[-1]) == nnz
+        assert torch.equal(full.tptr, lazy.tptr)
         assert torch.equal(full.tidx[:nnz], lazy.tidx[:nnz])
         assert torch.equal(full.tw[:nnz], lazy.tw[:nnz])
 

@@ -65,3 +65,58 @@ def test_fused_build_bitexact(cuda, monkeypatch, case, kind):
             assert torch.equal(got[f], want[f]), (case, kind, f)
     sync = graph_mod._build_sync(cuda).cpu().tolist()
     assert sync == [0, 0, 0, 0], sync  # re-armed, no barrier gave up
+
+
+def _sorted_cases():
+    """Target-sorted inputs (k-NN collated in graph order) the fast path takes, and near misses
+    it must hand to the general launches."""
+    c2 = synth.make_batch(64, n=64, k=8, seed=5)
+    ei = c2.edge_index
+    n = c2.num_nodes
+    noloop = synth.make_batch(40, n=64, k=8, seed=6, loop=False)
+    k16 = synth.make_batch(16, n=64, k=16, seed=7)
+    k17 = synth.make_batch(16, n=64, k=17, seed=8)
+    keep = ei[1] != 5  # node 5 receives nothing: a one-row gap
+    # a duplicated non-loop edge inside row 9 (kept, in order) and a second self loop in row 12
+    r9 = int((ei[1] == 9).nonzero()[1])
+    dup = torch.cat([ei[:, :r9 + 1], ei[:, r9:]], 1)
+    r12 = int((ei[1] == 12).nonzero()[0])
+    two = torch.cat([ei[:, :r12], torch.tensor([[12], [12]]), ei[:, r12:]], 1)
+    return {
+        "knn_c2": ((ei, n), "sorted"),
+        "knn_noloop": ((noloop.edge_index, noloop.num_nodes), "sorted"),
+        "k16": ((k16.edge_index, k16.num_nodes), "sorted"),
+        "gap_row": ((ei[:, keep], n), "sorted"),
+        "trailing_isolated": ((ei, n + 20), "sorted"),
+        "dup_edge": ((dup, n), "sorted"),
+        "k17": ((k17.edge_index, k17.num_nodes), "general"),
+        "two_loops": ((two, n), "general"),
+        "trailing_gap": ((ei, n + 200), "general"),
+        "lognormal": ((synth.make_batch(100, k=6, seed=9, sizes="lognormal").edge_index,
+                       synth.make_batch(100, k=6, seed=9, sizes="lognormal").num_nodes),
+                      "general"),
+        "unsorted": ((ei[:, torch.randperm(ei.size(1),
+                                           generator=torch.Generator().manual_seed(1))], n),
+                     "general"),
+        "invalid_tail": ((torch.cat([ei, torch.tensor([[3], [n]])], 1), n), "general"),
+    }
+
+
+@pytest.mark.parametrize("case", list(_sorted_cases()))
+@pytest.mark.parametrize("kind", ["gcn_lazy", "gcn", "gin"])
+def test_sorted_build_bitexact(cuda, monkeypatch, case, kind):
+    """The target-sorted fast path (k_prep_sorted + k_scan's sorted body) writes the same CSR,
+    weights, tile flags and error count as the general counting sort (LGNN_GRAPH_SORTED=0), and
+    is taken exactly for the inputs it covers (lazy GCN builds; the others never try it)."""
+    (ei, n), path = _sorted_cases()[case]
+    monkeypatch.setenv("LGNN_GRAPH_SORTED", "0")
+    want = _build(ei, n, kind, False, cuda, monkeypatch)
+    monkeypatch.setenv("LGNN_GRAPH_SORTED", "1")
+    g = Graph(ei.to(cuda), n)
+    got = _build(ei, n, kind, False, cuda, monkeypatch)
+    assert set(got) == set(want)
+    for f in want:
+        assert torch.equal(got[f], want[f]), (case, kind, f)
+    if kind == "gcn_lazy":
+        g.csr(kind)
+        assert g.build_path(kind) == path, case
