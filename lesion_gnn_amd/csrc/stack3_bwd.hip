@@ -537,7 +537,11 @@ struct FBwdSmem {
   int rp[TM + 1];
   int flag;
   __attribute__((aligned(16))) float dl[TM][kMaxHeadC];  // dlog rows of the tile's graphs, pre-scaled by pscale
+  // 32 KiB: the tile's H_L rows ([row][N_L] fp32, contiguous as in HBM), loaded direct-to-LDS
+  // during the previous tile so the prologue's dZ_L needs no global round trip
+  __attribute__((aligned(16))) float hl[TM * WP];
 };
+static_assert(sizeof(FBwdSmem) <= 160 * 1024, "fused backward LDS exceeds the CU's 160 KiB");
 
 // the tile's fp32 Â [target][source] (the forward's sum) straight into the scratch: 16 wave loads
 // of 1 KiB, no registers, completion by vmcnt
@@ -549,6 +553,43 @@ __device__ __forceinline__ void adj_issue(FBwdSmem& sm, const unsigned char* adj
     __builtin_amdgcn_raw_ptr_buffer_load_lds(
         rs, (__attribute__((address_space(3))) void*)(&sm.Adj[0][0] + c * 1024), 16,
         c * 1024 + lane * 16, 0, 0, 0);
+}
+
+// tile t's H_L rows (ld floats each, contiguous) straight into sm.hl: 1 KiB wave loads, no
+// registers, completion by vmcnt; rows past M are not read (the prologue masks them)
+__device__ __forceinline__ void hl_issue(FBwdSmem& sm, const float* H, int64_t M, int64_t t,
+                                         int ld) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t r0 = t * TM;
+  const int64_t rows = M - r0 < TM ? M - r0 : TM;
+  const Buf rs = mkbuf(H + r0 * ld, rows * ld * 4);
+  const int nch = (TM * ld * 4 + 1023) >> 10;  // <= 32: sm.hl holds TM * WP floats
+  for (int c = wave; c < nch; c += NT / 64)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        rs, (__attribute__((address_space(3))) void*)(reinterpret_cast<unsigned char*>(sm.hl) +
+                                                      c * 1024),
+        16, c * 1024 + lane * 16, 0, 0, 0);
+}
+
+// 4 x 4 transpose inside each quad of lanes (DPP): lane i's v[k] -> lane k's v[i]
+__device__ __forceinline__ float dpp_quad(float x, int ctrl_xor) {
+  const int xi = __builtin_bit_cast(int, x);
+  return __builtin_bit_cast(float, ctrl_xor == 1 ? __builtin_amdgcn_mov_dpp(xi, 0xB1, 0xF, 0xF, false)
+                                                 : __builtin_amdgcn_mov_dpp(xi, 0x4E, 0xF, 0xF, false));
+}
+__device__ __forceinline__ void quad_transpose(float (&v)[4], int qi) {
+  const bool b0 = qi & 1, b1 = qi & 2;
+#pragma unroll
+  for (int k = 0; k < 4; k += 2) {  // exchange at distance 1
+    const float r = dpp_quad(b0 ? v[k] : v[k + 1], 1);
+    if (b0) v[k] = r; else v[k + 1] = r;
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {  // exchange at distance 2
+    const float r = dpp_quad(b1 ? v[k] : v[k + 2], 2);
+    if (b1) v[k] = r; else v[k + 2] = r;
+  }
 }
 
 template <int NL, bool AG>
@@ -579,13 +620,21 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
   // graph of row tq of the tile and its size (tq < TM), loaded a tile ahead
   int64_t pre_g = 0;
   int pre_cnt = 0;
+  float pre_dl[kMaxHeadC];  // dlog row of pre_g (tq < TM), loaded a tile ahead
+#pragma unroll
+  for (int c = 0; c < kMaxHeadC; ++c) pre_dl[c] = 0.f;
   if (t < ntiles) {
+    hl_issue(sm, a.H[L], M, t, NLast);
     {
       const int tq = fresh_tid();
       const int64_t row = t * TM + tq;
       if (tq < TM && row < M) {
         pre_g = a.batch[row];
         pre_cnt = a.gptr[pre_g + 1] - a.gptr[pre_g];
+        if (a.dlog) {
+#pragma unroll
+          for (int c = 0; c < kMaxHeadC; ++c) pre_dl[c] = c < a.C ? a.dlog[pre_g * a.C + c] : 0.f;
+        }
       }
     }
     if constexpr (AG) {
@@ -600,13 +649,6 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
     const int64_t r0 = t * TM;
     const int64_t tn = seek_tile(t + gridDim.x, ntiles, tmask, 0);
     const bool has_next = tn < ntiles;
-    // H_L rows first: their latency overlaps the staging below
-    f32x16 hv[2];
-    {
-      const int tq = fresh_tid();
-      const int h = (tq >> 5) & 1, n = 32 * (tq >> 6) + (tq & 31);
-      load_pt(hv, a.H[L], M, r0, NLast, n, NLast, h);
-    }
     {
       const int tq = fresh_tid();
       if constexpr (!AG) {
@@ -625,13 +667,15 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
         if (a.dlog) {  // zero-padded to kMaxHeadC: the dZ_L loop below runs without branches
           float v[kMaxHeadC];
 #pragma unroll
-          for (int c = 0; c < kMaxHeadC; ++c) v[c] = c < a.C ? a.dlog[g * a.C + c] * ps : 0.f;
+          for (int c = 0; c < kMaxHeadC; ++c) v[c] = pre_dl[c] * ps;
           st4(&sm.dl[tq][0], f32x4{v[0], v[1], v[2], v[3]});
           st4(&sm.dl[tq][4], f32x4{v[4], v[5], v[6], v[7]});
         }
       }
     }
-    lds_barrier();
+    // this tile's H_L rows (and, AG, its Â) were issued during the previous tile: landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();  // ... in every wave; the staging above is visible
     if constexpr (!AG) {
       adj_scatter<true>(scr, sm.rp, R, r0);
       if (has_next) idx_load_head(R, rowptr, M, tn * TM);
@@ -641,6 +685,14 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
     {
       const int tq = fresh_tid();
       const int h = (tq >> 5) & 1, n = 32 * (tq >> 6) + (tq & 31);
+      f32x16 hv[2];  // H_L from the LDS copy (rows past M and features past N_L read 0)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
+          hv[q][r] = (n < NLast && r0 + m < M) ? sm.hl[m * NLast + n] : 0.f;
+        }
       if (a.dlog) {  // dP[g][n] = sum_c dlog[g][c] Wout[c][n], dlog rows staged (scaled) in LDS
         float wo[kMaxHeadC];
 #pragma unroll
@@ -673,8 +725,7 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
       }
     }
     if constexpr (AG) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's Â loads landed
-      lds_barrier();  // ... and every wave's
+      // (every wave's Â loads landed before the barrier above)
       // Â^T planes: row am = source, positions perm16 of targets 16 aq .. (a wave reads 64
       // different banks)
       const int tq = fresh_tid();
@@ -770,6 +821,7 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
       }
       u32x4 dzp[4][3];
       split_p(dz, dzp);
+#ifdef LGNN_S3F_GT_MFMA
       // G^T = dZ^T Â (node on the lane) -> node-major image right away (keeps one pair of
       // accumulators live at a time); the previous layer's dH readers of the image passed the
       // barrier that closed that layer
@@ -813,6 +865,7 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
             for (int p = 0; p < 3; ++p) sts8(sm.Gt[p] + off, o[p]);
           }
       }
+#endif
       // G = Â^T dZ (P layout)
       f32x16 g[2] = {f32x16{}, f32x16{}};
       {
@@ -843,6 +896,27 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
           }
         }
       }
+#ifndef LGNN_S3F_GT_MFMA
+      // G -> node-major image [m][perm16 n] for dH = G W_l: each quad of lanes (4 features,
+      // 4 nodes per register group) transposes its 4 x 4 blocks by DPP, so a lane holds four
+      // consecutive features of one node (no G^T = dZ^T Â products)
+      {
+        const int tq = fresh_tid();
+        const int h = (tq >> 5) & 1, li = tq & 31, wv = tq >> 6, qi = li & 3;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float v[4] = {g[q][4 * j], g[q][4 * j + 1], g[q][4 * j + 2], g[q][4 * j + 3]};
+            quad_transpose(v, qi);
+            u32x2 o[3];
+            split4(f32x4{v[0], v[1], v[2], v[3]}, o);
+            const int off = ap_off(32 * q + 8 * j + 4 * h + qi, 32 * wv + (li & ~3));
+#pragma unroll
+            for (int p = 0; p < 3; ++p) sts8(sm.Gt[p] + off, o[p]);
+          }
+      }
+#endif
       STAMP(stamp++);
       // H_{l-1} -> feature-major image (the previous layer's dW readers passed its barrier)
       {
@@ -885,6 +959,8 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
       if constexpr (AG) {
         if (l == 1 && has_next) adj_issue(sm, a.adjt, tn);
       }
+      // ... and the next tile's H_L rows (the prologue's reads of sm.hl passed many barriers)
+      if (l == 1 && has_next) hl_issue(sm, a.H[L], M, tn, NLast);
       if (l == 1) {  // the next tile's graph ids (their sizes follow in the in_proj phase)
         const int tq = fresh_tid();
         const int64_t row = tn * TM + tq;
@@ -983,6 +1059,11 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
           }
         (void)K;
         pre_cnt = (has_next && tq < TM) ? a.gptr[pre_g + 1] - a.gptr[pre_g] : 0;
+        if (a.dlog) {
+#pragma unroll
+          for (int c = 0; c < kMaxHeadC; ++c)
+            pre_dl[c] = (has_next && tq < TM && c < a.C) ? a.dlog[pre_g * a.C + c] : 0.f;
+        }
       }
       lds_barrier();
       {
