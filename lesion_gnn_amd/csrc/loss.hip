@@ -143,13 +143,40 @@ struct ReduceJobs {
 
 constexpr int RT = 1024;
 __global__ __launch_bounds__(RT) void k_reduce_multi(ReduceJobs jobs) {
-  __shared__ float red[16][64];
+  __shared__ f32x4 red4[16][64];
+  float(*red)[64] = reinterpret_cast<float(*)[64]>(red4);
   const int j = blockIdx.y;
   const int64_t len = jobs.len[j];
-  if ((int64_t)blockIdx.x * 64 >= len) return;
+  // long plain jobs (the dW slabs) take 16-B loads: 4 columns per lane, 256 per block, the same
+  // slot order per column (bitwise the scalar path's sums)
+  const bool vec = !jobs.factor[j] && (len & 3) == 0 && len >= 4096;
+  if ((int64_t)blockIdx.x * (vec ? 256 : 64) >= len) return;
   const float* __restrict__ part = jobs.part[j];
   int P = jobs.P[j];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (vec) {
+    const int64_t i4 = (int64_t)blockIdx.x * 256 + 4 * lane;
+    const int64_t ic4 = i4 < len ? i4 : len - 4;
+    f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
+    int p = wave;
+    for (; p + 16 * 15 < P; p += 16 * 16) {
+      f32x4 v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = ld4(part + (int64_t)(p + 16 * u) * len + ic4);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s4 += v[u];
+    }
+    for (; p < P; p += 16) s4 += ld4(part + (int64_t)p * len + ic4);
+    red4[wave][lane] = s4;
+    __syncthreads();
+    if (wave == 0 && i4 < len) {
+      f32x4 t = red4[0][lane];
+#pragma unroll
+      for (int q = 1; q < 16; ++q) t += red4[q][lane];
+      st4(jobs.out[j] + i4, t);
+    }
+    return;
+  }
   const int64_t i = (int64_t)blockIdx.x * 64 + lane;
   const int64_t ic = i < len ? i : len - 1;
   float s = 0.f;
