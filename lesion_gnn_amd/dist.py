@@ -50,19 +50,27 @@ def broadcast_params(module: torch.nn.Module, src: int = 0, group=None) -> None:
 
 class GradBucket:
     """The flat-gradient exchange split into its device part and its collective, so a training
-    step captured in HIP graphs keeps every copy / scale kernel inside the graphs and only the
-    RCCL call outside them (a collective is never captured):
-      pack()    flat <- concat(grad_i) * local / global   (capturable: end of the backward graph)
-      reduce()  all_reduce(flat, SUM)                      (eager, RCCL over xGMI)
-      unpack()  grad_i <- flat[slice_i]                    (capturable: head of the optimizer graph)
-    The flat buffer is allocated once, so replays of the captured parts reuse it. Equivalent to
-    allreduce_grads (tests/test_distributed.py)."""
+    step captured in HIP graphs keeps every copy kernel inside the graphs and only the RCCL call
+    outside them (a collective is never captured):
+      pack()    flat <- concat(grad_i) [* local / global]  (capturable: ONE cat kernel at the end
+                                                            of the backward graph)
+      reduce()  all_reduce(flat, AVG | SUM)                (eager, RCCL over xGMI)
+      unpack()  grad_i <- flat[slice_i]                    (no kernel: grad_i becomes a view of
+                                                            the reduced buffer, which the optimizer
+                                                            then reads in place)
+    With equal shards (local / global = 1 / world) on RCCL the mean is the collective's own AVG,
+    so pack is the concatenation alone; otherwise (gloo, unequal shards) pack pre-scales and the
+    collective sums. The flat buffer is allocated once, so replays of the captured parts reuse it.
+    Equivalent to allreduce_grads (tests/test_distributed.py)."""
 
     def __init__(self, params: list[torch.nn.Parameter], local_count: int, global_count: int,
                  group=None):
         self.params = list(params)
         self.scale = local_count / global_count
         self.group = group
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.avg = (dist.is_initialized() and dist.get_backend(group) == "nccl"
+                    and local_count * world == global_count)
         n = sum(p.numel() for p in self.params)
         dev = self.params[0].device if self.params else torch.device("cpu")
         self.flat = torch.empty(n, dtype=torch.float32, device=dev)
@@ -74,11 +82,13 @@ class GradBucket:
 
     def pack(self) -> None:
         torch.cat([p.grad.reshape(-1) for p in self.params], out=self.flat)
-        self.flat.mul_(self.scale)
+        if not self.avg and self.scale != 1.0:
+            self.flat.mul_(self.scale)
 
     def reduce(self) -> None:
-        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+        op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
+        dist.all_reduce(self.flat, op=op, group=self.group)
 
     def unpack(self) -> None:
         for p, v in zip(self.params, self.views):
-            p.grad.copy_(v)
+            p.grad = v

@@ -149,11 +149,14 @@ def _plan_worker(rank, world, port, out):
     bucket.pack()
     bucket.reduce()
     bucket.unpack()
+    # unpack launches nothing: every grad is now a view of the reduced flat buffer
+    same_ptr = all(p.grad.data_ptr() == v.data_ptr() for p, v in zip(params, bucket.views))
     via_bucket = [p.grad.clone() for p in params]
     for p, g0 in zip(params, ref_grads):
         p.grad = g0
     ldist.allreduce_grads(params, 8, 16)
-    same = all(torch.allclose(a, p.grad, atol=1e-7) for a, p in zip(via_bucket, params))
+    same = same_ptr and not bucket.avg and all(
+        torch.allclose(a, p.grad, atol=1e-7) for a, p in zip(via_bucket, params))
     if rank == 0:
         out.put(({k: v.detach().numpy().copy() for k, v in m.state_dict().items()}, same, plan))
     dist.barrier()
