@@ -82,6 +82,16 @@ __global__ __launch_bounds__(NT) void k_pool_head_fwd4(const float* __restrict__
     const int fc = f < D ? f : D - 4;
     f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
     int i = n0 + hw;
+    for (; i + 24 < n1; i += 32) {  // four rows in flight, the two-row loop's addition order
+      const f32x4 v0 = ld4(H + (int64_t)i * D + fc);
+      const f32x4 v1 = ld4(H + (int64_t)(i + 8) * D + fc);
+      const f32x4 v2 = ld4(H + (int64_t)(i + 16) * D + fc);
+      const f32x4 v3 = ld4(H + (int64_t)(i + 24) * D + fc);
+      a0 += v0;
+      a1 += v1;
+      a0 += v2;
+      a1 += v3;
+    }
     for (; i + 8 < n1; i += 16) {
       const f32x4 v0 = ld4(H + (int64_t)i * D + fc);
       const f32x4 v1 = ld4(H + (int64_t)(i + 8) * D + fc);
