@@ -73,20 +73,22 @@ __device__ __forceinline__ f32x16 mma(const u32x4 (&a)[PLANES], const u32x4 (&b)
 // ------------------------------------------------------------------------------------------
 // Y = A B^T (+ bias)
 // ------------------------------------------------------------------------------------------
-// A registers: rows 16 wave + 4 i + (lane >> 4) (i < 4), k = 4 (lane & 15) + 0..3, fp32.
+// A registers of a 32 MT-row tile: rows 8 MT wave + 4 i + (lane >> 4) (i < 2 MT),
+// k = 4 (lane & 15) + 0..3, fp32.
+template <int MT>
 struct ARegs {
-  uint32_t v[16];
+  uint32_t v[8 * MT];
 };
 
 // One 16-B load per row and lane, branch-free (a join of guarded loads would make the wait-count
 // pass drain every load in flight): a group at or past K reads 0 through an out-of-range offset,
 // and with K % 4 != 0 (!VEC) the group straddling K zeroes its columns >= K after the load (it
 // reads the next row's head, or 0 past the buffer). Rows past M read 0 through the buffer range.
-template <bool VEC>
-__device__ __forceinline__ void load_a(ARegs& R, Buf bA, int K, int c, int rq, int kq) {
+template <bool VEC, int MT>
+__device__ __forceinline__ void load_a(ARegs<MT>& R, Buf bA, int K, int c, int rq, int kq) {
   const int k = c * BK + kq;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 2 * MT; ++i) {
     const int off = (rq + 4 * i) * K + k;
     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(bA, opaque(k < K ? off * 4 : OOB), 0, 0);
 #pragma unroll
@@ -95,8 +97,8 @@ __device__ __forceinline__ void load_a(ARegs& R, Buf bA, int K, int c, int rq, i
 }
 
 // the chunk's four fp32 of row rq + 4 i -> PLANES bf16 planes (8 B per row and plane)
-template <int PLANES>
-__device__ __forceinline__ void store_a_row(unsigned char* img, const ARegs& R, int rq, int kq,
+template <int PLANES, int MT>
+__device__ __forceinline__ void store_a_row(unsigned char* img, const ARegs<MT>& R, int rq, int kq,
                                             int i) {
   {
     const int pos = swz(rq + 4 * i, kq >> 3) + ((kq & 7) << 1);
@@ -113,10 +115,10 @@ __device__ __forceinline__ void store_a_row(unsigned char* img, const ARegs& R, 
     }
   }
 }
-template <int PLANES>
-__device__ __forceinline__ void store_a(unsigned char* img, const ARegs& R, int rq, int kq) {
+template <int PLANES, int MT>
+__device__ __forceinline__ void store_a(unsigned char* img, const ARegs<MT>& R, int rq, int kq) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) store_a_row<PLANES>(img, R, rq, kq, i);
+  for (int i = 0; i < 2 * MT; ++i) store_a_row<PLANES>(img, R, rq, kq, i);
 }
 
 // Weight planes in fragment order (as bflin.hip's weight operand): for 128-column block nb,
@@ -151,24 +153,27 @@ struct AttOut {
 };
 constexpr int YLD = 128 + 4;  // LDS row stride of the staged Y tile (floats)
 
-template <int PLANES, bool VEC, int NCK, bool ATT = false>
-__global__ __launch_bounds__(NT, 2) void k_s3_gemm(const float* __restrict__ A, int64_t M, int K,
-                                                   const uint16_t* __restrict__ Wp, int Kp,
-                                                   const float* __restrict__ bias, int N,
-                                                   float* __restrict__ Y,
-                                                   float* __restrict__ colsum,
-                                                   AttOut att = AttOut{}) {
-  __shared__ __attribute__((aligned(16))) unsigned char img[2][PLANES * IMG];
+// One tile of 32 MT rows (MT = 2: the 64-row tile; MT = 1: the 32-row tiles that finish a grid
+// whose 64-row tiles would leave a mostly idle last round)
+template <int PLANES, bool VEC, int NCK, bool ATT, int MT>
+__device__ __forceinline__ void gemm_tile(unsigned char (&img)[2][PLANES * IMG], int64_t r0,
+                                          const float* __restrict__ A, int64_t M, int K,
+                                          const uint16_t* __restrict__ Wp, int Kp,
+                                          const float* __restrict__ bias, int N,
+                                          float* __restrict__ Y, float* __restrict__ colsum,
+                                          const AttOut& att) {
+  constexpr int RA = 2 * MT;  // A row groups per lane
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, li = lane & 31;
-  const int64_t r0 = xcd_block() * TM;
   const int nb = blockIdx.y;
   const Buf bA = mkbuf(A + r0 * K, (M - r0) * K * 4);
   const int64_t pstride = (int64_t)128 * Kp;  // bf16 elements per plane
   const Buf bW = mkbuf(Wp + nb * PLANES * pstride, PLANES * pstride * 2);
-  const int rq = 16 * wave + (lane >> 4), kq = 4 * (lane & 15);
+  const int rq = 8 * MT * wave + (lane >> 4), kq = 4 * (lane & 15);
   const int wlane = wave * 512 + lane * 8;
-  f32x16 acc0 = {}, acc1 = {};
+  f32x16 acc[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) acc[t] = f32x16{};
   // Software pipeline. Chunk c's products run while (a) the A fragments of k-step s + 1 are
   // read from LDS (two fragment sets: an LDS read's latency is not paid in front of each step)
   // and (b) chunk c + 1's rows are split into planes and written to the other image (one row per
@@ -176,32 +181,31 @@ __global__ __launch_bounds__(NT, 2) void k_s3_gemm(const float* __restrict__ A, 
   // compiler from sinking the reads back to their uses. The other image was last read by chunk
   // c - 1, which every wave finished before the barrier in front of chunk c.
   auto chunk = [&](const unsigned char* im, const u32x4 (&bc)[4][PLANES], unsigned char* imn,
-                   const ARegs& Rn, bool store_next) {
-    u32x4 a[2][2][PLANES];
+                   const ARegs<MT>& Rn, bool store_next) {
+    u32x4 a[2][MT][PLANES];
 #pragma unroll
-    for (int p = 0; p < PLANES; ++p) {
-      a[0][0][p] = lds16(im + p * IMG + swz(li, h));
-      a[0][1][p] = lds16(im + p * IMG + swz(32 + li, h));
-    }
+    for (int p = 0; p < PLANES; ++p)
+#pragma unroll
+      for (int t = 0; t < MT; ++t) a[0][t][p] = lds16(im + p * IMG + swz(32 * t + li, h));
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       if (s + 1 < 4) {
 #pragma unroll
-        for (int p = 0; p < PLANES; ++p) {
-          a[(s + 1) & 1][0][p] = lds16(im + p * IMG + swz(li, 2 * (s + 1) + h));
-          a[(s + 1) & 1][1][p] = lds16(im + p * IMG + swz(32 + li, 2 * (s + 1) + h));
-        }
+        for (int p = 0; p < PLANES; ++p)
+#pragma unroll
+          for (int t = 0; t < MT; ++t)
+            a[(s + 1) & 1][t][p] = lds16(im + p * IMG + swz(32 * t + li, 2 * (s + 1) + h));
       }
       __builtin_amdgcn_sched_barrier(0);
-      acc0 = mma<PLANES>(a[s & 1][0], bc[s], acc0);
-      acc1 = mma<PLANES>(a[s & 1][1], bc[s], acc1);
-      if (store_next) store_a_row<PLANES>(imn, Rn, rq, kq, s);
+#pragma unroll
+      for (int t = 0; t < MT; ++t) acc[t] = mma<PLANES>(a[s & 1][t], bc[s], acc[t]);
+      if (store_next && s < RA) store_a_row<PLANES>(imn, Rn, rq, kq, s);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
   // two register sets ping-pong: R[c & 1] holds chunk c's rows until chunk c - 1's products
   // have stored them, then takes chunk c + 2's
-  ARegs R0, R1;
+  ARegs<MT> R0, R1;
   u32x4 b0[4][PLANES], b1[4][PLANES];
   load_a<VEC>(R0, bA, K, 0, rq, kq);
   load_b<PLANES>(b0, bW, pstride, wlane, 0);
@@ -210,7 +214,7 @@ __global__ __launch_bounds__(NT, 2) void k_s3_gemm(const float* __restrict__ A, 
   store_a<PLANES>(img[0], R0, rq, kq);
   load_a<VEC>(R0, bA, K, 2, rq, kq);
   lds_barrier();
-  auto step = [&](int c, ARegs& Rn, u32x4 (&bc)[4][PLANES], bool store_next) {
+  auto step = [&](int c, ARegs<MT>& Rn, u32x4 (&bc)[4][PLANES], bool store_next) {
     chunk(img[c & 1], bc, img[(c + 1) & 1], Rn, store_next);
     load_a<VEC>(Rn, bA, K, c + 3, rq, kq);
     load_b<PLANES>(bc, bW, pstride, wlane, c + 2);
@@ -235,20 +239,20 @@ __global__ __launch_bounds__(NT, 2) void k_s3_gemm(const float* __restrict__ A, 
   const float bv = (bias && nok) ? bias[n] : 0.f;
   const Buf bY = mkbuf(Y + r0 * N, (M - r0) * N * 4);
   const int ncol = nok ? n : OOB / 4;
-  if (colsum) {  // this tile's column sums of Y (rows past M hold 0)
+  if (MT == 2 && colsum) {  // this tile's column sums of Y (rows past M hold 0; 64-row grids)
     float cs = 0.f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) cs += acc0[r] + acc1[r];
+    for (int r = 0; r < 16; ++r) cs += acc[0][r] + acc[MT - 1][r];
     cs += __shfl_xor(cs, 32, 64);
     const int64_t rows = M - r0 < TM ? M - r0 : TM;
     if (h == 0 && nok) colsum[(r0 / TM) * N + n] = cs + (float)rows * bv;
   }
 #pragma unroll
-  for (int q = 0; q < 2; ++q)
+  for (int q = 0; q < MT; ++q)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float v = (q ? acc1[r] : acc0[r]) + bv;
+      const float v = acc[q][r] + bv;
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), bY, (m * N + ncol) * 4, 0, 0);
     }
   if constexpr (ATT) {
@@ -257,17 +261,17 @@ __global__ __launch_bounds__(NT, 2) void k_s3_gemm(const float* __restrict__ A, 
     lds_barrier();  // every wave's last image reads are done
     if (nok) {
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
+      for (int q = 0; q < MT; ++q)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
-          ytile[m * YLD + n] = (q ? acc1[r] : acc0[r]) + bv;
+          ytile[m * YLD + n] = acc[q][r] + bv;
         }
     }
     lds_barrier();
     const int H = att.H, C = att.C;
-    const int64_t rows = M - r0 < TM ? M - r0 : TM;
-    for (int p = tid; p < TM * H; p += NT) {
+    const int64_t rows = M - r0 < 32 * MT ? M - r0 : 32 * MT;
+    for (int p = tid; p < 32 * MT * H; p += NT) {
       const int m = p / H, hd = p % H;
       if (m >= rows) continue;
       const float* yr = ytile + m * YLD + hd * C;
@@ -281,6 +285,30 @@ __global__ __launch_bounds__(NT, 2) void k_s3_gemm(const float* __restrict__ A, 
       att.a_s[(r0 + m) * H + hd] = ps;
       att.a_d[(r0 + m) * H + hd] = pd;
     }
+  }
+}
+
+// Grid: n64 tiles of 64 rows (blocks 0 .. n64 - 1, dealt to the XCDs in contiguous ranges), then
+// 32-row tiles for the remaining rows. With more 64-row tiles than resident workgroups the
+// launch's last round would hold a few of them on an otherwise idle chip; the host keeps whole
+// rounds of 64-row tiles and cuts the rest in halves (lgnn_s3_gemm: the reference in_proj at
+// 42,279 rows is 661 tiles over 512 slots).
+template <int PLANES, bool VEC, int NCK, bool ATT = false>
+__global__ __launch_bounds__(NT, 2) void k_s3_gemm(const float* __restrict__ A, int64_t M, int K,
+                                                   const uint16_t* __restrict__ Wp, int Kp,
+                                                   const float* __restrict__ bias, int N,
+                                                   float* __restrict__ Y,
+                                                   float* __restrict__ colsum, int n64,
+                                                   AttOut att = AttOut{}) {
+  __shared__ __attribute__((aligned(16))) unsigned char img[2][PLANES * IMG];
+  const int64_t b = blockIdx.x;
+  if (b < n64) {
+    const int64_t q = n64 / 8, r = n64 % 8, xcd = b % 8;
+    const int64_t t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+    gemm_tile<PLANES, VEC, NCK, ATT, 2>(img, t * TM, A, M, K, Wp, Kp, bias, N, Y, colsum, att);
+  } else {
+    gemm_tile<PLANES, VEC, NCK, ATT, 1>(img, (int64_t)n64 * TM + (b - n64) * 32, A, M, K, Wp, Kp,
+                                        bias, N, Y, nullptr, att);
   }
 }
 
@@ -543,6 +571,33 @@ extern "C" int lgnn_s3_weight_planes(const float* W, int rows, int cols, int tra
   return LGNN_OK;
 }
 
+// Row tiling of k_s3_gemm: whole rounds of 64-row tiles over the resident slots (2 workgroups per
+// CU, divided among the column blocks), the rest as 32-row tiles — for long K only (the in_proj,
+// K = 1025: 75.3 -> 73.5 us; at K = 128 the halves lost more per tile than the round saved);
+// only 64-row tiles when the caller wants per-64-row column sums or LGNN_S3G_HALF=0. Returns
+// grid.x, sets *n64.
+static unsigned s3g_grid(int64_t M, int K, int nblk, bool colsum, int* n64) {
+  const int64_t t64 = (M + TM - 1) / TM;
+  static int slots = -1;
+  if (slots < 0) {
+    int dev = 0, cus = 0;
+    const char* e = getenv("LGNN_S3G_HALF");
+    if (e && e[0] == '0') slots = 0;
+    else if (hipGetDevice(&dev) == hipSuccess &&
+             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      slots = 2 * cus;
+    else slots = 0;
+  }
+  const int64_t per = nblk > 0 ? slots / nblk : 0;
+  if (colsum || K < 512 || per < 8 || t64 <= per) {
+    *n64 = (int)t64;
+    return (unsigned)t64;
+  }
+  const int64_t full = t64 / per * per;  // whole rounds of 64-row tiles
+  *n64 = (int)full;
+  return (unsigned)(full + (M - full * TM + 31) / 32);
+}
+
 extern "C" int lgnn_s3_gemm(const float* A, int64_t M, int K, const uint16_t* Wp, int N,
                             int planes, const float* bias, float* Y, float* colsum_part,
                             void* stream) {
@@ -555,14 +610,16 @@ extern "C" int lgnn_s3_gemm(const float* A, int64_t M, int K, const uint16_t* Wp
       (int64_t)3 * 128 * Kp * 2 >= ((int64_t)1 << 31))
     return LGNN_EINVAL;
   if (M == 0) return LGNN_OK;
-  const dim3 grid((unsigned)((M + TM - 1) / TM), (unsigned)((N + 127) / 128)), block(NT);
+  int n64 = 0;
+  const unsigned gx = s3g_grid(M, K, (N + 127) / 128, colsum_part != nullptr, &n64);
+  const dim3 grid(gx, (unsigned)((N + 127) / 128)), block(NT);
   hipStream_t s = as_stream(stream);
   const bool v = K % 4 == 0;
   const char* loop = getenv("LGNN_S3G_LOOP");  // tuning knob: 1 = the pair loop at every K
   const int nck = loop && loop[0] == '1' ? -1 : Kp / BK;
 #define LGNN_S3G(P, V, NC) \
   hipLaunchKernelGGL((k_s3_gemm<P, V, NC>), grid, block, 0, s, A, M, K, Wp, Kp, bias, N, Y, \
-                     colsum_part)
+                     colsum_part, n64)
 #define LGNN_S3G_N(P, V)                 \
   switch (nck) {                         \
     case 2: LGNN_S3G(P, V, 2); break;    \
@@ -595,14 +652,15 @@ extern "C" int lgnn_s3_gemm_att(const float* A, int64_t M, int K, const uint16_t
       (int64_t)3 * 128 * Kp * 2 >= ((int64_t)1 << 31))
     return LGNN_EINVAL;
   if (M == 0) return LGNN_OK;
-  const dim3 grid((unsigned)((M + TM - 1) / TM), 1), block(NT);
+  int n64 = 0;
+  const dim3 grid(s3g_grid(M, K, 1, false, &n64), 1), block(NT);
   hipStream_t s = as_stream(stream);
   const AttOut at{att_src, att_dst, a_s, a_d, heads, C};
   const bool v = K % 4 == 0;
   const int nck = Kp / BK;
 #define LGNN_S3A(P, V, NC)                                                                      \
   hipLaunchKernelGGL((k_s3_gemm<P, V, NC, true>), grid, block, 0, s, A, M, K, Wp, Kp, nullptr, N, \
-                     Y, nullptr, at)
+                     Y, nullptr, n64, at)
 #define LGNN_S3A_N(P, V)                 \
   switch (nck) {                         \
     case 2: LGNN_S3A(P, V, 2); break;    \
