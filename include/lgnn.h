@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 30
+#define LGNN_ABI_VERSION 31
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -533,6 +533,12 @@ int lgnn_regression_bwd(const float* z, const void* target, int target_is_i64, i
  * accumulate = 1) on the same slabs. No input gradient (the model input needs none).
  * ------------------------------------------------------------------------------------------- */
 int lgnn_gcn_stack_bwd_partials(int64_t num_nodes);
+
+/* Variant of the fused split-3 backward (lgnn_gcn_stack_bwd_s3f[_all] with the forward's Â^T
+ * hand-over): 4 = one wave per SIMD (the default), 8 = two waves per SIMD (k_s3_fbwd8, opt-in;
+ * same results to the parity bar, slower at C2). Returns the previous value, LGNN_EINVAL for any
+ * other argument. Process-wide; not synchronised with launches in flight on other threads. */
+int lgnn_s3f_set_waves(int waves);
 int lgnn_gcn_stack_bwd(const float* dP, const int64_t* batch, const int32_t* gptr, int pool_mean,
                        const int32_t* rowptr, const int32_t* col, const float* w, const float* X,
                        int64_t M, int L, const float* const* W, const float* const* H,

@@ -53,6 +53,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_node_linear_bwd_tiles": (I32, [I32, P, P, P, I32, P, P, P, F32, P, I32, P, I64, I32,
                                          P, P, P, F32, P, I32, P, P, P, I32, P, I32, I32, P]),
     "lgnn_gcn_stack_bwd_partials": (I32, [I64]),
+    "lgnn_s3f_set_waves": (I32, [I32]),
     "lgnn_adam_step": (I32, [I32, P, P, P, P, P, P, P, F32, F32, F32, F32, F32, I32, I32, I32,
                              P]),
     "lgnn_gcn_stack_bwd": (I32, [P, P, P, I32, P, P, P, P, I64, I32, P, P, P, P, P, I32, P, P]),
@@ -141,7 +142,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 30
+ABI_VERSION = 31
 
 _lib = None
 

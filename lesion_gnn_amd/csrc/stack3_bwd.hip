@@ -1662,14 +1662,22 @@ __global__ __launch_bounds__(NT8, 1) void k_s3_fbwd8(int64_t M, FBwdArgs a,
 }  // namespace lgnn_s3
 
 // Fused backward variant (the Â hand-over case): 4 = k_s3_fbwd (the default), 8 = k_s3_fbwd8
-// (two waves per SIMD, LGNN_S3F_WAVES=8: parity-tested, slower at C2 — DESIGN §4.3)
+// (two waves per SIMD: parity-tested, slower at C2 — DESIGN §4.3); LGNN_S3F_WAVES=8 or
+// lgnn_s3f_set_waves selects it
+static int g_s3f_waves = -1;
 static int s3f_waves() {
-  static int v = -1;
-  if (v < 0) {
+  if (g_s3f_waves < 0) {
     const char* e = getenv("LGNN_S3F_WAVES");
-    v = (e && atoi(e) == 8) ? 8 : 4;
+    g_s3f_waves = (e && atoi(e) == 8) ? 8 : 4;
   }
-  return v;
+  return g_s3f_waves;
+}
+
+extern "C" int lgnn_s3f_set_waves(int waves) {
+  if (waves != 4 && waves != 8) return LGNN_EINVAL;
+  const int prev = s3f_waves();
+  g_s3f_waves = waves;
+  return prev;
 }
 
 static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* gptr,

@@ -293,7 +293,7 @@ def test_tile_open_flags(cuda):
     assert Graph(b2.edge_index.to(cuda), b2.num_nodes).tile_open("gcn").cpu().tolist()[:5] == [0] * 5
 
 
-@pytest.mark.parametrize("bwd", ["f32", "s3", "s3f"])
+@pytest.mark.parametrize("bwd", ["f32", "s3", "s3f", "s3f8"])
 @pytest.mark.parametrize("case", ["c2_L2", "irregular_L2", "irregular_L1_add", "dense_tiles",
                                   "c2_L3"])
 def test_gcn_fused_backward(cuda, case, bwd, monkeypatch):
@@ -303,7 +303,16 @@ def test_gcn_fused_backward(cuda, case, bwd, monkeypatch):
     c2_L3: three convs (fp32: layer-wise backward on recomputed aggregates; split-3: fused).
     bwd: the fp32 fused kernel (lgnn_gcn_stack_bwd), the split-3 layer-major kernels
     (lgnn_gcn_stack_bwd_s3) or the fused split-3 kernel (lgnn_gcn_stack_bwd_s3f; L <= 2, so c2_L3
-    takes the layer-major one)."""
+    takes the layer-major one); s3f8: the same entry on its two-waves-per-SIMD variant
+    (lgnn_s3f_set_waves(8): k_s3_fbwd8, used where the forward hands over the tiles' Â)."""
+    if bwd == "s3f8":
+        prev = _lib.load().lgnn_s3f_set_waves(8)
+        assert prev in (4, 8)
+        try:
+            test_gcn_fused_backward(cuda, case, "s3f", monkeypatch)
+        finally:
+            _lib.load().lgnn_s3f_set_waves(prev)
+        return
     pool = "add" if case.endswith("add") else "mean"
     hidden = [128, 128] if "L1" in case else [128] * 4 if "L3" in case else [128, 128, 128]
     if case.startswith("c2"):
