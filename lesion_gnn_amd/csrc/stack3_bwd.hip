@@ -624,6 +624,26 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
   float pre_dl[kMaxHeadC];  // dlog row of pre_g (tq < TM), loaded a tile ahead
 #pragma unroll
   for (int c = 0; c < kMaxHeadC; ++c) pre_dl[c] = 0.f;
+  // out_proj's W as the B operand of the dZ_L product (lane: feature n; K: class 8h + e; classes
+  // past C, features past N_L and the h = 1 half read 0 through the buffer range), split once
+  u32x4 wob[3] = {};
+  if (a.dlog) {
+    const int tq = fresh_tid();
+    const int h = (tq >> 5) & 1, n = 32 * (tq >> 6) + (tq & 31);
+    const Buf bW = mkbuf(a.Wout, (int64_t)a.C * NLast * 4);
+    float f[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      f[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                           bW, (h == 0 && n < NLast) ? (e * NLast + n) * 4
+                                                                     : INT32_MAX - 3, 0, 0));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const Split2 s2 = split2(f[2 * i], f[2 * i + 1]);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) wob[p][i] = s2.p[p];
+    }
+  }
   if (t < ntiles) {
     hl_issue(sm, a.H[L], M, t, NLast);
     {
@@ -694,24 +714,28 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
           const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
           hv[q][r] = (n < NLast && r0 + m < M) ? sm.hl[m * NLast + n] : 0.f;
         }
-      if (a.dlog) {  // dP[g][n] = sum_c dlog[g][c] Wout[c][n], dlog rows staged (scaled) in LDS
-        float wo[kMaxHeadC];
+      if (a.dlog) {
+        // dP[g(m)][n] / |g(m)| = sum_c dl[m][c] Wout[c][n] as ONE split-3 product per node half
+        // (K = the <= 8 classes, zero-padded to 16): A = the staged dl rows (node on the lane:
+        // two 16-B LDS reads per half instead of 32 rows x 8 classes per lane), B = out_proj's
+        // W planes (wob, split once per launch); the output is in P layout, as dZ_L is consumed
+        const int li = tq & 31;
 #pragma unroll
-        for (int c = 0; c < kMaxHeadC; ++c)
-          wo[c] = (c < a.C && n < NLast) ? a.Wout[c * NLast + n] : 0.f;
+        for (int q = 0; q < 2; ++q) {
+          const f32x4 d0 = ld4(&sm.dl[32 * q + li][0]), d1 = ld4(&sm.dl[32 * q + li][4]);
+          u32x4 ad[3];
 #pragma unroll
-        for (int q = 0; q < 2; ++q)
+          for (int i = 0; i < 4; ++i) {
+            const float x0 = h ? 0.f : (i < 2 ? d0[2 * i] : d1[2 * i - 4]);
+            const float x1 = h ? 0.f : (i < 2 ? d0[2 * i + 1] : d1[2 * i - 3]);
+            const Split2 s2 = split2(x0, x1);
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
-            const f32x4 d0 = ld4(&sm.dl[m][0]), d1 = ld4(&sm.dl[m][4]);
-            float gv = d0[0] * wo[0];
-#pragma unroll
-            for (int c = 1; c < 4; ++c) gv = fmaf(d0[c], wo[c], gv);
-#pragma unroll
-            for (int c = 0; c < 4; ++c) gv = fmaf(d1[c], wo[4 + c], gv);
-            dz[q][r] = gv * elu_grad_from_out(hv[q][r]);
+            for (int p = 0; p < 3; ++p) ad[p][i] = s2.p[p];
           }
+          const f32x16 gv = mfma_s3(ad, wob, f32x16{});
+#pragma unroll
+          for (int r = 0; r < 16; ++r) dz[q][r] = gv[r] * elu_grad_from_out(hv[q][r]);
+        }
       } else {
 #pragma unroll
         for (int q = 0; q < 2; ++q)
