@@ -267,12 +267,21 @@ def time_dominant_kernels(model, b, dev):
                   csr.col.data_ptr(), csr.w.data_ptr(), L, planes_f.data_ptr(), bp,
                   (ctypes.c_int * (L + 1))(*widths[1:]), Hp, open_.data_ptr(), _lib.ptr(adjt), s)
 
+        # the step's launch: the _all entry with the logits gradient (dP = dlogits W_out formed
+        # in the kernel's prologue, the dZ_L product), as ops.stack_bwd runs it in the step
+        W_out = model.out_proj.weight.detach()
+        dlog = torch.randn(b.num_graphs, W_out.size(0), device=dev)
+        dS_ws = torch.empty(2 * M * 128, dtype=torch.float32, device=dev)
+        Sp = (ctypes.c_void_p * L)(*[x.data_ptr() for x in hs[1:]])  # open tiles only (none)
+
         def bwd_s3f():
-            _lib.call("lgnn_gcn_stack_bwd_s3f", dP.data_ptr(), g.batch.data_ptr(),
+            _lib.call("lgnn_gcn_stack_bwd_s3f_all", None, g.batch.data_ptr(),
                       g.gptr.data_ptr(), 1, b.num_graphs, csr.rowptr.data_ptr(),
-                      csr.col.data_ptr(), csr.w.data_ptr(), b.x.data_ptr(), M, L,
-                      planes_t.data_ptr(), Hp, (ctypes.c_int * (L + 2))(*widths), dWp, dbp, P,
-                      open_.data_ptr(), _lib.ptr(adjt), s)
+                      csr.col.data_ptr(), csr.w.data_ptr(), csr.tptr.data_ptr(),
+                      csr.tidx.data_ptr(), csr.tw.data_ptr(), b.x.data_ptr(), M, L,
+                      planes_t.data_ptr(), Wp, Hp, Sp, (ctypes.c_int * (L + 2))(*widths), dWp,
+                      dbp, P, dS_ws.data_ptr(), open_.data_ptr(), dlog.data_ptr(),
+                      W_out.data_ptr(), W_out.size(0), _lib.ptr(adjt), s)
 
         out.append({"kernel": f"lgnn_s3::k_s3_fbwd<{L + 1}, {str(ops.ADJT).lower()}> (fused GCN "
                               "backward, all layers, "

@@ -990,7 +990,11 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
         const int tq = fresh_tid();
         const int64_t row = tn * TM + tq;
         pre_g = (has_next && tq < TM && row < M) ? a.batch[row] : 0;
-        // this tile's X rows for the in_proj phase: in flight during the last conv's dW / dH
+      }
+      // this tile's X rows for the in_proj phase, in flight from the first conv's dW on (issued
+      // at the last conv they crowded that phase's load queue: in-step 107.6 -> 106.0 us)
+      if (l == L) {
+        const int tq = fresh_tid();
         const int h = (tq >> 5) & 1, k = 32 * (tq >> 6) + (tq & 31);
         load_pt(xp, a.X, (ABL & 16) ? 0 : M, r0, a.width[0], k, a.width[0], h);
       }
