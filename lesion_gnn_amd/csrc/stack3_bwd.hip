@@ -593,6 +593,20 @@ __device__ __forceinline__ void quad_transpose(float (&v)[4], int qi) {
   }
 }
 
+// The same 4 x 4 transpose on bf16 planes: lane qi holds feature qi of nodes 0, 1 (w0) and
+// 2, 3 (w1) as packed pairs; returns node qi's features 0, 1 and 2, 3 as packed pairs (one
+// exchange of 2 x 2 bf16 blocks with lane qi ^ 1 by v_perm, then of words with lane qi ^ 2)
+__device__ __forceinline__ u32x2 quad_transpose_bf16(uint32_t w0, uint32_t w1, int qi) {
+  const uint32_t sel = (qi & 1) ? 0x03020706u : 0x05040100u;
+  const uint32_t p0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)w0, 0xB1, 0xF, 0xF, false);
+  const uint32_t p1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)w1, 0xB1, 0xF, 0xF, false);
+  const uint32_t a = __builtin_amdgcn_perm(p0, w0, sel);
+  const uint32_t b = __builtin_amdgcn_perm(p1, w1, sel);
+  const bool b1 = qi & 2;
+  const uint32_t r = (uint32_t)__builtin_amdgcn_mov_dpp((int)(b1 ? a : b), 0x4E, 0xF, 0xF, false);
+  return u32x2{b1 ? r : a, b1 ? b : r};
+}
+
 template <int NL, bool AG>
 __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ rowptr,
                                                    const int32_t* __restrict__ col,
@@ -846,51 +860,6 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
       }
       u32x4 dzp[4][3];
       split_p(dz, dzp);
-#ifdef LGNN_S3F_GT_MFMA
-      // G^T = dZ^T Â (node on the lane) -> node-major image right away (keeps one pair of
-      // accumulators live at a time); the previous layer's dH readers of the image passed the
-      // barrier that closed that layer
-      {
-        f32x16 gt[2] = {f32x16{}, f32x16{}};
-        const int tq = fresh_tid();
-        const int h = (tq >> 5) & 1, li = tq & 31, wv = tq >> 6;
-        if (aexact) {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-              const int off = (32 * q + li) * ADJ_LD * 2 + 16 * (2 * s + h);
-              const u32x4 a0 = lds16(sm.Adj[0] + off);
-              if constexpr (!(ABL & 1)) gt[q] = mfma_s3_bexact(dzp[s], a0, gt[q]);
-            }
-          }
-        } else {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-              const int off = (32 * q + li) * ADJ_LD * 2 + 16 * (2 * s + h);
-              u32x4 at[3];
-#pragma unroll
-              for (int p = 0; p < 3; ++p) at[p] = lds16(sm.Adj[p] + off);
-              if constexpr (!(ABL & 1)) gt[q] = mfma_s3(dzp[s], at, gt[q]);
-            }
-            S3F_SB();
-          }
-        }
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
-#pragma unroll
-          for (int gq = 0; gq < 4; ++gq) {
-            u32x2 o[3];
-            split4(f32x4{gt[q][4 * gq], gt[q][4 * gq + 1], gt[q][4 * gq + 2], gt[q][4 * gq + 3]},
-                   o);
-            const int off = ap_off(32 * q + li, 32 * wv + 8 * gq + 4 * h);
-#pragma unroll
-            for (int p = 0; p < 3; ++p) sts8(sm.Gt[p] + off, o[p]);
-          }
-      }
-#endif
       // G = Â^T dZ (P layout)
       f32x16 g[2] = {f32x16{}, f32x16{}};
       {
@@ -921,10 +890,12 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
           }
         }
       }
-#ifndef LGNN_S3F_GT_MFMA
+      // G's operand planes, split once: dW's A operand below, and (transposed) the G image
+      u32x4 gp[4][3];
+      split_p(g, gp);
       // G -> node-major image [m][perm16 n] for dH = G W_l: each quad of lanes (4 features,
-      // 4 nodes per register group) transposes its 4 x 4 blocks by DPP, so a lane holds four
-      // consecutive features of one node (no G^T = dZ^T Â products)
+      // 4 nodes per packed pair of planes) transposes its 4 x 4 blocks of bf16 by DPP + v_perm,
+      // so a lane holds four consecutive features of one node (no G^T = dZ^T Â products)
       {
         const int tq = fresh_tid();
         const int h = (tq >> 5) & 1, li = tq & 31, wv = tq >> 6, qi = li & 3;
@@ -932,16 +903,14 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
         for (int q = 0; q < 2; ++q)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            float v[4] = {g[q][4 * j], g[q][4 * j + 1], g[q][4 * j + 2], g[q][4 * j + 3]};
-            quad_transpose(v, qi);
-            u32x2 o[3];
-            split4(f32x4{v[0], v[1], v[2], v[3]}, o);
+            // nodes 32 q + 8 j + 4 h + 0..3: node step 2 q + (j >> 1), pairs 2 (j & 1) and + 1
+            const int st = 2 * q + (j >> 1), i0 = 2 * (j & 1);
             const int off = ap_off(32 * q + 8 * j + 4 * h + qi, 32 * wv + (li & ~3));
 #pragma unroll
-            for (int p = 0; p < 3; ++p) sts8(sm.Gt[p] + off, o[p]);
+            for (int p = 0; p < 3; ++p)
+              sts8(sm.Gt[p] + off, quad_transpose_bf16(gp[st][p][i0], gp[st][p][i0 + 1], qi));
           }
       }
-#endif
       STAMP(stamp++);
       // H_{l-1} -> feature-major image (the previous layer's dW readers passed its barrier)
       {
@@ -959,25 +928,25 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
             for (int p = 0; p < 3; ++p) sts8(sm.Img[p] + off, o[p]);
           }
       }
-      // W_l^T planes for dH (L2-resident, 1 KiB per wave-load): the first four k-steps fly
-      // during the dW products, the last four during the first half of dH
+      // W_l^T planes for dH (L2-resident, 1 KiB per wave-load), two k-steps at a time: the first
+      // pair flies during the dW products, each later pair during the pair before it
       const uint16_t* wbase;
       {
         const int tq = fresh_tid();
         const int lane = tq & 63, wv = tq >> 6;
         wbase = a.WpT + (size_t)l * 3 * PLANE + wv * 8 * 512 + lane * 8;
       }
-      auto load_w = [&](u32x4 (&wf)[3][4], int half) {
+      auto load_w2 = [&](u32x4 (&wf)[3][2], int pair) {
 #pragma unroll
         for (int p = 0; p < 3; ++p)
 #pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4)
-            wf[p][s4] = (ABL & 16) ? u32x4{}
+          for (int s2 = 0; s2 < 2; ++s2)
+            wf[p][s2] = (ABL & 16) ? u32x4{}
                                    : *reinterpret_cast<const u32x4*>(wbase + p * PLANE +
-                                                                     512 * (4 * half + s4));
+                                                                     512 * (2 * pair + s2));
       };
-      u32x4 wf0[3][4], wf1[3][4];
-      load_w(wf0, 0);
+      u32x4 wa[3][2], wb[3][2];
+      load_w2(wa, 0);
       lds_barrier();  // both images complete
       // the last conv's Â^T reads are done: the next tile's planes load into LDS behind the
       // remaining phases of this tile
@@ -999,10 +968,9 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
         load_pt(xp, a.X, (ABL & 16) ? 0 : M, r0, a.width[0], k, a.width[0], h);
       }
       STAMP(stamp++);
-      // dW_l += G^T H: A = G (P layout, node steps), B = H image rows k = 32 kb + li
+      // dW_l += G^T H: A = G (P layout, node steps: the planes split above), B = H image rows
+      // k = 32 kb + li
       {
-        u32x4 gp[4][3];
-        split_p(g, gp);
         const int tq = fresh_tid();
         const int h = (tq >> 5) & 1, li = tq & 31;
 #pragma unroll
@@ -1024,26 +992,30 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
       {
         const int tq = fresh_tid();
         const int h = (tq >> 5) & 1, li = tq & 31;
-        auto dh_half = [&](const u32x4 (&wf)[3][4], int half) {
+        auto dh_pair = [&](const u32x4 (&wf)[3][2], int pair) {
 #pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4) {
+          for (int s2 = 0; s2 < 2; ++s2) {
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
               u32x4 f[3];
-              const int off = ap_chunk(32 * q + li, 2 * (4 * half + s4) + h);
+              const int off = ap_chunk(32 * q + li, 2 * (2 * pair + s2) + h);
 #pragma unroll
               for (int p = 0; p < 3; ++p) f[p] = lds16(sm.Gt[p] + off);
               u32x4 bw[3];
 #pragma unroll
-              for (int p = 0; p < 3; ++p) bw[p] = wf[p][s4];
+              for (int p = 0; p < 3; ++p) bw[p] = wf[p][s2];
               if constexpr (!(ABL & 1)) dh[q] = mfma_s3(f, bw, dh[q]);
             }
             S3F_SB();
           }
         };
-        load_w(wf1, 1);
-        dh_half(wf0, 0);
-        dh_half(wf1, 1);
+        load_w2(wb, 1);
+        dh_pair(wa, 0);
+        load_w2(wa, 2);
+        dh_pair(wb, 1);
+        load_w2(wb, 3);
+        dh_pair(wa, 2);
+        dh_pair(wb, 3);
       }
       // dZ_{l-1} = dH * ELU'(H_{l-1}) (no ELU below the first conv: in_proj has none); rows past
       // M and features past K are zero

@@ -1,6 +1,7 @@
 set -uo pipefail
-mkdir -p gpurun_out/r03h15
+mkdir -p gpurun_out/r03h16
 export TMPDIR=/tmp
-timeout -k 10 300 python bench.py --steps 100 --warmup 20 --cpu-seconds 0 > gpurun_out/r03h15/bench.json 2> gpurun_out/r03h15/bench.err || { tail -20 gpurun_out/r03h15/bench.err; exit 1; }
-python3 -c "import json; d=json.loads(open('gpurun_out/r03h15/bench.json').read().strip().splitlines()[-1]); r=d['roofline']; print(d['ms_per_step'], r['kernel'][:30], r['avg_launch_ms'], r['frac'])"
-PATTERN=k_s3_fbwd bash tools/ab_prof.sh xearly --workload c2
+timeout -k 10 400 python -u -m pytest tests/test_gpu_gcn.py tests/test_gpu_configs.py tests/test_gpu_golden.py tests/test_gpu_compile.py -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/r03h16/pt.log 2>&1
+rc=$?; tail -2 gpurun_out/r03h16/pt.log; grep -E "^FAILED|^ERROR" gpurun_out/r03h16/pt.log | head -20
+case $rc in 0) ;; *) exit $rc;; esac
+PATTERN=k_s3_fbwd bash tools/ab_prof.sh base --workload c2
