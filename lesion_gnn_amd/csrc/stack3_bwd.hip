@@ -929,7 +929,8 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
           }
       }
       // W_l^T planes for dH (L2-resident, 1 KiB per wave-load), two k-steps at a time: the first
-      // pair flies during the dW products, each later pair during the pair before it
+      // pair flies during the dW products, the second from their middle on, each later pair
+      // during the two before it
       const uint16_t* wbase;
       {
         const int tq = fresh_tid();
@@ -969,20 +970,23 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
       }
       STAMP(stamp++);
       // dW_l += G^T H: A = G (P layout, node steps: the planes split above), B = H image rows
-      // k = 32 kb + li
+      // k = 32 kb + li. Node steps outer: consecutive products go to different accumulators,
+      // each accumulator still takes s = 0..3 in order, and gp[s] is dead after its step — the
+      // second pair of W^T planes loads into the registers the first two steps freed
       {
         const int tq = fresh_tid();
         const int h = (tq >> 5) & 1, li = tq & 31;
 #pragma unroll
-        for (int kb = 0; kb < 4; ++kb) {
+        for (int s = 0; s < 4; ++s) {
 #pragma unroll
-          for (int s = 0; s < 4; ++s) {
+          for (int kb = 0; kb < 4; ++kb) {
             u32x4 hb[3];
             const int off = hf_chunk(32 * kb + li, 2 * s + h);
 #pragma unroll
             for (int p = 0; p < 3; ++p) hb[p] = lds16(sm.Img[p] + off);
             if constexpr (!(ABL & 1)) dw[l][kb] = mfma_s3(gp[s], hb, dw[l][kb]);
           }
+          if (s == 1) load_w2(wb, 1);
           S3F_SB();
         }
       }
@@ -1009,7 +1013,6 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
             S3F_SB();
           }
         };
-        load_w2(wb, 1);
         dh_pair(wa, 0);
         load_w2(wa, 2);
         dh_pair(wb, 1);
@@ -1073,9 +1076,9 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
         const int tq = fresh_tid();
         const int h = (tq >> 5) & 1, li = tq & 31;
 #pragma unroll
-        for (int kb = 0; kb < 4; ++kb) {
+        for (int s = 0; s < 4; ++s) {  // node steps outer, as the conv layers' dW
 #pragma unroll
-          for (int s = 0; s < 4; ++s) {
+          for (int kb = 0; kb < 4; ++kb) {
             u32x4 hb[3];
             const int off = hf_chunk(32 * kb + li, 2 * s + h);
 #pragma unroll
