@@ -184,7 +184,17 @@ __global__ __launch_bounds__(RT) void k_reduce_multi(ReduceJobs jobs) {
   if (const float* __restrict__ f = jobs.factor[j]) {  // sum_p part[p][c] * f[p][d]
     const int width = jobs.width[j];
     const int64_t rows = len / width, c = ic / width, d = ic % width;
-    for (; p + 16 * 15 < P; p += 16 * 16) {  // 32 loads in flight per lane (latency bound)
+    for (; p + 16 * 31 < P; p += 16 * 32) {  // 64 loads in flight per lane (latency bound:
+      float av[32], fv[32];                   // out_proj's dW over 1024 graphs is 2 rounds)
+#pragma unroll
+      for (int u = 0; u < 32; ++u) {
+        av[u] = part[(int64_t)(p + 16 * u) * rows + c];
+        fv[u] = f[(int64_t)(p + 16 * u) * width + d];
+      }
+#pragma unroll
+      for (int u = 0; u < 32; ++u) s = fmaf(av[u], fv[u], s);
+    }
+    for (; p + 16 * 15 < P; p += 16 * 16) {  // then 32 in flight
       float av[16], fv[16];
 #pragma unroll
       for (int u = 0; u < 16; ++u) {

@@ -1,7 +1,7 @@
 set -uo pipefail
-mkdir -p gpurun_out/r03h19
+mkdir -p gpurun_out/r03h20
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_gcn.py tests/test_gpu_configs.py tests/test_gpu_golden.py tests/test_gpu_compile.py -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/r03h19/pt.log 2>&1
-rc=$?; tail -2 gpurun_out/r03h19/pt.log; grep -E "^FAILED|^ERROR" gpurun_out/r03h19/pt.log | head -20
+timeout -k 10 400 python -u -m pytest tests/test_gpu_gcn.py tests/test_gpu_gat.py tests/test_gpu_gin.py tests/test_gpu_loss.py -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/r03h20/pt.log 2>&1
+rc=$?; tail -2 gpurun_out/r03h20/pt.log; grep -E "^FAILED|^ERROR" gpurun_out/r03h20/pt.log | head -20
 case $rc in 0) ;; *) exit $rc;; esac
-PATTERN=k_s3_fbwd bash tools/ab_prof.sh base --workload c2
+PATTERN=k_reduce_multi bash tools/ab_prof.sh base --workload c2
