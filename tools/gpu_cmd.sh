@@ -1,7 +1,7 @@
 set -uo pipefail
-mkdir -p gpurun_out/r03h20
+mkdir -p gpurun_out/r03h22
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_gcn.py tests/test_gpu_gat.py tests/test_gpu_gin.py tests/test_gpu_loss.py -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/r03h20/pt.log 2>&1
-rc=$?; tail -2 gpurun_out/r03h20/pt.log; grep -E "^FAILED|^ERROR" gpurun_out/r03h20/pt.log | head -20
+timeout -k 10 400 python -u -m pytest tests/test_gpu_loss.py tests/test_gpu_gcn.py tests/test_gpu_configs.py -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/r03h22/pt.log 2>&1
+rc=$?; tail -2 gpurun_out/r03h22/pt.log; grep -E "^FAILED|^ERROR" gpurun_out/r03h22/pt.log | head -20
 case $rc in 0) ;; *) exit $rc;; esac
-PATTERN=k_reduce_multi bash tools/ab_prof.sh base --workload c2
+PATTERN=k_ce_ bash tools/ab_prof.sh base --workload c2
