@@ -30,8 +30,8 @@ constexpr int kBuildSpins = 1 << 24;
 // entries), runs of at most kGapCap rows without entries, at most one self loop per row
 constexpr int kSortedRowCap = 16;
 constexpr int kGapCap = 64;
-constexpr int kVerdictMax = 256;  // k_prep_sorted workgroups (one verdict word each)
-constexpr int kSortedChunks = 8;   // k_prep_sorted: 64-edge chunks per wave pass
+constexpr int kVerdictMax = 1024;  // k_prep_sorted workgroups (one verdict word each)
+constexpr int kSortedChunks = 2;   // k_prep_sorted: 64-edge chunks per wave pass (more waves in flight)
 constexpr int kSortedRows = 256;   // k_scan's sorted body: rows per workgroup (one per thread)
 
 inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
@@ -172,6 +172,7 @@ struct SortedArgs {
   float* dis;
   int32_t* verdict;
   int nverdict;
+  int summary_ready;  // k_count ran: verdict[kVerdictMax] already holds the OR of the words
 };
 
 __device__ __forceinline__ void sorted_empty_row(const SortedArgs& a, int64_t r, int64_t start) {
@@ -398,10 +399,13 @@ __global__ __launch_bounds__(kThreads) void k_count(const int64_t* __restrict__ 
                                                     int64_t N, int loops, int32_t* cnt,
                                                     int32_t* tcnt, int32_t* err,
                                                     int32_t* tile_open,
-                                                    const int32_t* verdict, int nverdict) {
+                                                    int32_t* verdict, int nverdict) {
   __shared__ int hist[kBins];
   __shared__ int red[2 * kThreads / 64];
-  if (sorted_ok(verdict, nverdict)) return;
+  const bool fast = sorted_ok(verdict, nverdict);
+  // the summary word for k_scan / k_fill / k_finish (one word to read instead of all of them)
+  if (verdict && blockIdx.x == 0 && threadIdx.x == 0) verdict[kVerdictMax] = fast;
+  if (fast) return;
   count_body(ei, E, N, loops, cnt, tcnt, err, tile_open, hist, red, blockIdx.x);
 }
 
@@ -712,8 +716,10 @@ __global__ __launch_bounds__(kScanT) void k_scan(const int32_t* __restrict__ cnt
                                                  int32_t* err_out, int nblk) {
   __shared__ ScanSmem sm;
   __shared__ SortedSmem ss;
-  const bool fast = sorted_ok(sa.verdict, sa.nverdict);
-  if (sa.verdict && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+  const bool fast = sa.summary_ready
+                        ? (sa.verdict && __builtin_amdgcn_readfirstlane(sa.verdict[kVerdictMax]))
+                        : sorted_ok(sa.verdict, sa.nverdict);
+  if (!sa.summary_ready && sa.verdict && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
     sa.verdict[kVerdictMax] = fast;  // the summary word k_fill / k_finish read
   if (fast) {
     if (blockIdx.y == 0 && (int64_t)blockIdx.x * kSortedRows < N)
@@ -1173,6 +1179,7 @@ static int graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loop
                        s, edge_index, E, N, loops, ws.cnt, tptr ? ws.tcnt : nullptr, ws.err,
                        lazy ? tile_open : nullptr, sa.verdict, sa.nverdict);
     LGNN_LAUNCH_CHECK();
+    sa.summary_ready = sa.verdict != nullptr;
   }
   {
     const int64_t nblk = (N + 1 + kScanBlk - 1) / kScanBlk;
