@@ -82,6 +82,16 @@ __global__ __launch_bounds__(NT) void k_pool_head_fwd4(const float* __restrict__
     const int fc = f < D ? f : D - 4;
     f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
     int i = n0 + hw;
+    for (; i + 56 < n1; i += 64) {  // eight rows in flight, the two-row loop's addition order
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = ld4(H + (int64_t)(i + 8 * u) * D + fc);
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        a0 += v[u];
+        a1 += v[u + 1];
+      }
+    }
     for (; i + 24 < n1; i += 32) {  // four rows in flight, the two-row loop's addition order
       const f32x4 v0 = ld4(H + (int64_t)i * D + fc);
       const f32x4 v1 = ld4(H + (int64_t)(i + 8) * D + fc);
