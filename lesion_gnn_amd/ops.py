@@ -1712,17 +1712,20 @@ class _GATConv(torch.autograd.Function):
                 else:
                     dx = dense_mm(dg, dense_planes(W, True, True), K, None, True)
         else:
-            if extra_red:
-                reduce_multi([(part, P, 3 * HC, red)] + extra_red, dev)
-            else:
-                _lib.call("lgnn_reduce_partials", _lib.ptr(part), P, 3 * HC, _lib.ptr(red),
-                          _s(dev))
+            jobs = [(part, P, 3 * HC, red)] + (extra_red or [])
             if ctx.dense:  # split-3 (or bf16-rounded) MFMA GEMMs on the fp32 dXP
-                dW = dense_wgrad(dXP, x, ctx.bf16)[0]
+                # lin's dW slabs join the attention partials' reduction: one launch per conv
+                dW = dense_wgrad(dXP, x, ctx.bf16, reducer=jobs)[0]
+                reduce_multi(jobs, dev)
                 wpt = getattr(ctx, "wpt", None)
                 dx = dense_mm(dXP, wpt if wpt is not None else dense_planes(W, True, ctx.bf16),
                               W.size(1), None, ctx.bf16) if want_dx else None
             else:
+                if extra_red:
+                    reduce_multi(jobs, dev)
+                else:
+                    _lib.call("lgnn_reduce_partials", _lib.ptr(part), P, 3 * HC, _lib.ptr(red),
+                              _s(dev))
                 dx, dW, _ = linear_bwd(_lib.LGNN_GRAD_DIRECT, dXP, H=None,
                                        act=_lib.LGNN_ACT_NONE, X=x, W=W, want_dx=want_dx,
                                        want_db=False)
