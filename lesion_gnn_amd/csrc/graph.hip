@@ -293,20 +293,28 @@ __device__ __forceinline__ bool sorted_ok(const int32_t* verdict, int nverdict) 
 // targets). Sources are binned in LDS when the chunk's sources span fewer than kBins nodes (the
 // k-NN case: a chunk covers a few graphs), so the transpose needs one global atomic per distinct
 // source per chunk instead of one per edge; otherwise per-edge global atomics.
+// kPer edges per thread (8; 4 when the 8-edge chunks would not give every CU a workgroup: the
+// reference config's 254 k edges took 124 workgroups, count + fill 21 -> 16 us; at C5 k = 16's
+// 933 k edges 4 was slower — more global atomics per edge)
 constexpr int kPer = 8;
 constexpr int kChunk = kThreads * kPer;
+__host__ __device__ constexpr int chunk_of(int per) { return kThreads * per; }
+// fewer 8-edge chunks than CUs: the edge passes take 4 edges per thread instead
+static bool small_edges(int64_t E) { return (E + kChunk - 1) / kChunk < 256; }
 constexpr int kBins = 4096;
 
+template <int PER = kPer>
 struct EdgeChunk {
-  int64_t s[kPer], d[kPer];
-  bool use[kPer];
+  int64_t s[PER], d[PER];
+  bool use[PER];
 };
 
-__device__ __forceinline__ void load_chunk(EdgeChunk& c, const int64_t* __restrict__ ei,
+template <int PER>
+__device__ __forceinline__ void load_chunk(EdgeChunk<PER>& c, const int64_t* __restrict__ ei,
                                            int64_t E, int64_t N, int loops, int64_t c0,
                                            int32_t* err) {
 #pragma unroll
-  for (int it = 0; it < kPer; ++it) {
+  for (int it = 0; it < PER; ++it) {
     const int64_t e = c0 + (int64_t)it * kThreads + threadIdx.x;
     int64_t s = -1, d = -1;
     if (e < E) {
@@ -322,10 +330,11 @@ __device__ __forceinline__ void load_chunk(EdgeChunk& c, const int64_t* __restri
 }
 
 // block-uniform: the chunk's smallest used source and whether all used sources fit the bins
-__device__ __forceinline__ bool chunk_binned(const EdgeChunk& c, int64_t& smin, int* red) {
+template <int PER>
+__device__ __forceinline__ bool chunk_binned(const EdgeChunk<PER>& c, int64_t& smin, int* red) {
   int64_t lo = INT64_MAX, hi = -1;
 #pragma unroll
-  for (int it = 0; it < kPer; ++it)
+  for (int it = 0; it < PER; ++it)
     if (c.use[it]) {
       lo = c.s[it] < lo ? c.s[it] : lo;
       hi = c.s[it] > hi ? c.s[it] : hi;
@@ -356,22 +365,23 @@ __device__ __forceinline__ void mark_open(int32_t* tile_open, int64_t t, int64_t
   if (atomicCAS(&tile_open[t], 0, 1) == 0) atomicAdd(&tile_open[ntiles], 1);
 }
 
+template <int PER = kPer>
 __device__ __forceinline__ void count_body(const int64_t* __restrict__ ei, int64_t E, int64_t N,
                                            int loops, int32_t* cnt, int32_t* tcnt, int32_t* err,
                                            int32_t* tile_open, int* hist, int* red, int64_t bx) {
   const int lane = threadIdx.x & 63;
-  const int64_t c0 = bx * kChunk;
-  EdgeChunk c;
+  const int64_t c0 = bx * chunk_of(PER);
+  EdgeChunk<PER> c;
   load_chunk(c, ei, E, N, loops, c0, err);
 #pragma unroll
-  for (int it = 0; it < kPer; ++it) {
+  for (int it = 0; it < PER; ++it) {
     const Run r = wave_run(c.use[it] ? c.d[it] : -2 - lane);
     if (c.use[it] && r.head) atomicAdd(&cnt[c.d[it]], r.len);
   }
   if (tile_open) {  // lazy transpose: the tiles an edge leaves are known before the fill
     const int64_t ntiles = (N + 63) >> 6;
 #pragma unroll
-    for (int it = 0; it < kPer; ++it)
+    for (int it = 0; it < PER; ++it)
       if (c.use[it] && (c.s[it] >> 6) != (c.d[it] >> 6)) {
         if (tile_open[c.d[it] >> 6] == 0) mark_open(tile_open, c.d[it] >> 6, ntiles);
         if (tile_open[c.s[it] >> 6] == 0) mark_open(tile_open, c.s[it] >> 6, ntiles);
@@ -383,18 +393,19 @@ __device__ __forceinline__ void count_body(const int64_t* __restrict__ ei, int64
     for (int b = threadIdx.x; b < kBins; b += kThreads) hist[b] = 0;
     __syncthreads();
 #pragma unroll
-    for (int it = 0; it < kPer; ++it)
+    for (int it = 0; it < PER; ++it)
       if (c.use[it]) atomicAdd(&hist[c.s[it] - smin], 1);
     __syncthreads();
     for (int b = threadIdx.x; b < kBins; b += kThreads)
       if (hist[b]) atomicAdd(&tcnt[smin + b], hist[b]);
   } else {
 #pragma unroll
-    for (int it = 0; it < kPer; ++it)
+    for (int it = 0; it < PER; ++it)
       if (c.use[it]) atomicAdd(&tcnt[c.s[it]], 1);
   }
 }
 
+template <int PER>
 __global__ __launch_bounds__(kThreads) void k_count(const int64_t* __restrict__ ei, int64_t E,
                                                     int64_t N, int loops, int32_t* cnt,
                                                     int32_t* tcnt, int32_t* err,
@@ -406,11 +417,12 @@ __global__ __launch_bounds__(kThreads) void k_count(const int64_t* __restrict__ 
   // the summary word for k_scan / k_fill / k_finish (one word to read instead of all of them)
   if (verdict && blockIdx.x == 0 && threadIdx.x == 0) verdict[kVerdictMax] = fast;
   if (fast) return;
-  count_body(ei, E, N, loops, cnt, tcnt, err, tile_open, hist, red, blockIdx.x);
+  count_body<PER>(ei, E, N, loops, cnt, tcnt, err, tile_open, hist, red, blockIdx.x);
 }
 
 // fill[d] / tfill[s] start at the row offsets (set by k_scan); slots come from atomics on them,
 // so the order inside a row is arbitrary here and restored by k_finish (sort by edge id).
+template <int PER = kPer>
 __device__ __forceinline__ void fill_body(const int64_t* __restrict__ ei, int64_t E, int64_t N,
                                           int loops, const int32_t* __restrict__ rowptr,
                                           int32_t* fill, int32_t* col, int32_t* eid,
@@ -418,11 +430,11 @@ __device__ __forceinline__ void fill_body(const int64_t* __restrict__ ei, int64_
                                           int32_t* tidx, int32_t* teid, const int32_t* lazy_open,
                                           int* hist, int* red, int64_t bx) {
   const int lane = threadIdx.x & 63;
-  const int64_t c0 = bx * kChunk;
-  EdgeChunk c;
+  const int64_t c0 = bx * chunk_of(PER);
+  EdgeChunk<PER> c;
   load_chunk(c, ei, E, N, loops, c0, nullptr);
 #pragma unroll
-  for (int it = 0; it < kPer; ++it) {
+  for (int it = 0; it < PER; ++it) {
     const int64_t e = c0 + (int64_t)it * kThreads + threadIdx.x;
     const Run r = wave_run(c.use[it] ? c.d[it] : -2 - lane);
     int slot0 = 0;
@@ -441,9 +453,9 @@ __device__ __forceinline__ void fill_body(const int64_t* __restrict__ ei, int64_
   if (chunk_binned(c, smin, red)) {
     for (int b = threadIdx.x; b < kBins; b += kThreads) hist[b] = 0;
     __syncthreads();
-    int rank[kPer];
+    int rank[PER];
 #pragma unroll
-    for (int it = 0; it < kPer; ++it)
+    for (int it = 0; it < PER; ++it)
       rank[it] = c.use[it] ? atomicAdd(&hist[c.s[it] - smin], 1) : 0;
     __syncthreads();
     for (int b = threadIdx.x; b < kBins; b += kThreads) {
@@ -452,7 +464,7 @@ __device__ __forceinline__ void fill_body(const int64_t* __restrict__ ei, int64_
     }
     __syncthreads();
 #pragma unroll
-    for (int it = 0; it < kPer; ++it)
+    for (int it = 0; it < PER; ++it)
       if (c.use[it]) {
         const int pos = hist[c.s[it] - smin] + rank[it];
         tidx[pos] = (int32_t)c.d[it];
@@ -460,7 +472,7 @@ __device__ __forceinline__ void fill_body(const int64_t* __restrict__ ei, int64_
       }
   } else {
 #pragma unroll
-    for (int it = 0; it < kPer; ++it)
+    for (int it = 0; it < PER; ++it)
       if (c.use[it]) {
         const int pos = atomicAdd(&tfill[c.s[it]], 1);
         tidx[pos] = (int32_t)c.d[it];
@@ -469,6 +481,7 @@ __device__ __forceinline__ void fill_body(const int64_t* __restrict__ ei, int64_
   }
 }
 
+template <int PER>
 __global__ __launch_bounds__(kThreads) void k_fill(const int64_t* __restrict__ ei, int64_t E,
                                                    int64_t N, int loops,
                                                    const int32_t* __restrict__ rowptr,
@@ -480,8 +493,8 @@ __global__ __launch_bounds__(kThreads) void k_fill(const int64_t* __restrict__ e
   __shared__ int hist[kBins];
   __shared__ int red[2 * kThreads / 64];
   if (summary && __builtin_amdgcn_readfirstlane(*summary)) return;  // sorted path took it
-  fill_body(ei, E, N, loops, rowptr, fill, col, eid, tptr, tfill, tidx, teid, lazy_open, hist, red,
-            blockIdx.x);
+  fill_body<PER>(ei, E, N, loops, rowptr, fill, col, eid, tptr, tfill, tidx, teid, lazy_open, hist,
+                 red, blockIdx.x);
 }
 
 // Both degree scans (blockIdx.y = 0: rowptr from cnt, 1: tptr from tcnt) in ONE launch over
@@ -1175,9 +1188,16 @@ static int graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loop
     return LGNN_OK;
   }
   if (E > 0) {
-    hipLaunchKernelGGL(k_count, dim3((unsigned)((E + kChunk - 1) / kChunk)), dim3(kThreads), 0,
-                       s, edge_index, E, N, loops, ws.cnt, tptr ? ws.tcnt : nullptr, ws.err,
-                       lazy ? tile_open : nullptr, sa.verdict, sa.nverdict);
+    if (small_edges(E))
+      hipLaunchKernelGGL(k_count<4>, dim3((unsigned)((E + chunk_of(4) - 1) / chunk_of(4))),
+                         dim3(kThreads), 0, s, edge_index, E, N, loops, ws.cnt,
+                         tptr ? ws.tcnt : nullptr, ws.err, lazy ? tile_open : nullptr, sa.verdict,
+                         sa.nverdict);
+    else
+      hipLaunchKernelGGL(k_count<kPer>, dim3((unsigned)((E + kChunk - 1) / kChunk)),
+                         dim3(kThreads), 0, s, edge_index, E, N, loops, ws.cnt,
+                         tptr ? ws.tcnt : nullptr, ws.err, lazy ? tile_open : nullptr, sa.verdict,
+                         sa.nverdict);
     LGNN_LAUNCH_CHECK();
     sa.summary_ready = sa.verdict != nullptr;
   }
@@ -1191,10 +1211,18 @@ static int graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loop
     LGNN_LAUNCH_CHECK();
   }
   if (E > 0) {
-    hipLaunchKernelGGL(k_fill, dim3((unsigned)((E + kChunk - 1) / kChunk)), dim3(kThreads), 0,
-                       s, edge_index, E, N, loops, rowptr, ws.fill, col, ws.eid, tptr, ws.tfill,
-                       tidx, ws.teid, lazy ? tile_open + (N + 63) / 64 : nullptr,
-                       try_sorted ? ws.verdict + kVerdictMax : nullptr);
+    if (small_edges(E))
+      hipLaunchKernelGGL(k_fill<4>, dim3((unsigned)((E + chunk_of(4) - 1) / chunk_of(4))),
+                         dim3(kThreads), 0, s, edge_index, E, N, loops, rowptr, ws.fill, col,
+                         ws.eid, tptr, ws.tfill, tidx, ws.teid,
+                         lazy ? tile_open + (N + 63) / 64 : nullptr,
+                         try_sorted ? ws.verdict + kVerdictMax : nullptr);
+    else
+      hipLaunchKernelGGL(k_fill<kPer>, dim3((unsigned)((E + kChunk - 1) / kChunk)),
+                         dim3(kThreads), 0, s, edge_index, E, N, loops, rowptr, ws.fill, col,
+                         ws.eid, tptr, ws.tfill, tidx, ws.teid,
+                         lazy ? tile_open + (N + 63) / 64 : nullptr,
+                         try_sorted ? ws.verdict + kVerdictMax : nullptr);
     LGNN_LAUNCH_CHECK();
   }
   const int64_t nfin = (N + kFinT - 1) / kFinT;
