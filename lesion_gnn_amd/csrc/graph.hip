@@ -843,11 +843,22 @@ __device__ __forceinline__ void finish_body(int64_t N, int64_t E, int add_loop, 
   if (tile_open && !tr && i < N) {
     const int r0 = ptr[i], r1 = ptr[i + 1];
     const int64_t ti = i >> 6;
+    // a row's neighbours sit in one or two tiles: each tile is looked up (and marked) once per
+    // run of equal neighbour tiles, this row's own tile once per row (marks are idempotent)
+    bool self_done = false;
+    int64_t last = -1;
     for (int j = r0; j < r1; ++j) {
       const int nb = staged ? s_val[j - eb] : idx[j];
-      if ((nb >> 6) != ti) {
-        if (tile_open[ti] == 0) mark(ti);
-        if (tile_open[nb >> 6] == 0) mark(nb >> 6);
+      const int64_t nt = nb >> 6;
+      if (nt != ti) {
+        if (!self_done) {
+          if (tile_open[ti] == 0) mark(ti);
+          self_done = true;
+        }
+        if (nt != last) {
+          if (tile_open[nt] == 0) mark(nt);
+          last = nt;
+        }
       }
     }
   }
