@@ -1,4 +1,4 @@
-# Builds lesion_gnn_amd/liblgnn.so (gfx950 only) and the C oracle helpers.
+# Builds lesion_gnn_amd/liblgnn.so (gfx950 only). The oracle is Python (oracle/pyg_ref.py): nothing to compile.
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function

@@ -101,6 +101,17 @@ def parse():
                     help="1: replay the captured fwd+bwd and optimizer HIP graphs; 0: eager")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend for N > 1 (nccl = RCCL over xGMI on ROCm)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="run the N > 1 step plan (process group, gradient bucket + all-reduce, "
+                         "SyncBN for GIN) even at --gpus 1, over a one-rank group: times the plan "
+                         "a multi-GPU run executes on one GPU")
+    ap.add_argument("--sync-bn", choices=["auto", "on", "off"], default="auto",
+                    help="GIN with a process group: auto/on = SyncBN (full-batch statistics, "
+                         "all-reduces inside forward and backward), off = per-replica statistics "
+                         "(torch DDP's default)")
+    ap.add_argument("--entries", type=int, default=1,
+                    help="1: per-entry HIP-event profile of an eager step (rank 0, after the "
+                         "timed region)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher/rank plumbing only: set up the process group, all-reduce a "
                          "gradient-sized buffer once, print the JSON line with value null; "
@@ -127,6 +138,14 @@ def launch_ranks(args) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
 def setup_dist(args):
     """One process per GPU (LOCAL_RANK = device). Refuses a rank count that differs from
     --gpus, so a run cannot report fewer GPUs than it was asked for."""
@@ -141,9 +160,13 @@ def setup_dist(args):
             dist.init_process_group(args.backend)
     else:
         dev = torch.device("cuda", local)
-        if world > 1:
+        if world > 1 or args.force_dist:
             torch.cuda.set_device(local)
             kw = {"device_id": dev} if args.backend == "nccl" else {}
+            if world == 1:  # --force-dist: a one-rank group on this process
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                os.environ.setdefault("MASTER_PORT", str(_free_port()))
+                kw.update(rank=0, world_size=1)
             dist.init_process_group(args.backend, **kw)
     if world > 1 and dist.get_world_size() != args.gpus:
         raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, "
@@ -388,6 +411,237 @@ def time_gat_in_proj(model, b, dev, wl):
     return out
 
 
+class GraphStats:
+    """Host-side sizes of the batch's CSR the algorithmic byte / FLOP models need: entries (nnz)
+    of the graph kind the model builds, and the rows / entries that sit in open 64-row tiles
+    (an edge leaves the tile or it holds > 1024 entries: the layer-wise kernels take those)."""
+
+    def __init__(self, b, kind):
+        from lesion_gnn_amd.graph import Graph
+
+        g = Graph(b.edge_index, b.num_nodes, b.batch, b.num_graphs)
+        csr = g.csr(kind)
+        rp = csr.rowptr.cpu().long()
+        self.M, self.B = b.num_nodes, b.num_graphs
+        self.nnz = int(rp[-1])
+        self.open_rows = self.open_nnz = 0
+        if csr.tile_open is not None:
+            T = (self.M + 63) // 64
+            flags = csr.tile_open[:T].cpu()
+            for t in torch.nonzero(flags).flatten().tolist():
+                r0, r1 = 64 * t, min(64 * t + 64, self.M)
+                self.open_rows += r1 - r0
+                self.open_nnz += int(rp[r1] - rp[r0])
+
+    def rows(self, tile_open, want_open):
+        """(rows, entries) a *_tiles launch processes."""
+        if tile_open is None:
+            return self.M, self.nnz
+        if want_open:
+            return self.open_rows, self.open_nnz
+        return self.M - self.open_rows, self.nnz - self.open_nnz
+
+
+def _entry_model(name, a, gs):
+    """Algorithmic (bytes, useful FLOP) of one C-ABI launch from its arguments (the positions of
+    include/lgnn.h), fp32: every activation row the launch reads or writes counted once, the CSR
+    entries it walks once (8 B: index + weight), a weight gradient once (N K 4, not the partial
+    slabs); FLOP = the GEMMs + 2 nnz width per aggregation. None for entries without a model."""
+    f4 = 4.0
+    if name in ("lgnn_node_linear_fwd", "lgnn_node_linear_fwd_tiles", "lgnn_node_linear_fwd_bn"):
+        M, K, rowptr, N, S = a[1], a[2], a[3], a[9], a[12]
+        R, nz = gs.rows(a[13], a[14]) if name.endswith("_tiles") else (M, gs.nnz)
+        by = f4 * R * (K + N) + (f4 * R * K if S else 0) + ((8.0 * nz + 4 * R) if rowptr else 0)
+        if name.endswith("_bn"):  # BN_IN: the dropout mask and A1 = ELU(BN(Z1)) (+ mask)
+            by += (f4 * R * K if a[16] else 0) + (f4 * R * K if a[17] else 0)
+        return by, 2.0 * R * K * N + (2.0 * nz * K if rowptr else 0)
+    if name in ("lgnn_node_linear_bwd", "lgnn_node_linear_bwd_tiles"):
+        mode, H, M, K, rowptr, N, dX = a[0], a[9], a[12], a[13], a[14], a[19], a[20]
+        R, nz = gs.rows(a[24], a[25]) if name.endswith("_tiles") else (M, gs.nnz)
+        by = f4 * R * K + f4 * N * K  # X (or S) read once, dW written once
+        fl = 2.0 * R * K * N
+        if mode != 1:  # DIRECT / TRANSPOSE: the output gradient rows (POOL: [B, N], negligible)
+            by += f4 * R * N
+        if mode == 2:  # the transposed aggregation of dY
+            by += 8.0 * nz + 4 * R
+            fl += 2.0 * nz * N
+        if H:
+            by += f4 * R * N
+        if rowptr:  # S recomputed from the forward CSR
+            by += 8.0 * nz + 4 * R
+            fl += 2.0 * nz * K
+        if dX:
+            by += f4 * R * K
+            fl += 2.0 * R * K * N
+        return by, fl
+    if name in ("lgnn_node_linear_bwd_bn", "lgnn_node_linear_bwd_bn_pool",
+                "lgnn_node_linear_bwd_bn_gather"):
+        g = name.endswith("_gather")
+        if g:  # dS, tptr, tidx, tw, tself, H, act, X, M, K, W, N, dX, ..., bn_Z, bn_mask, ...
+            H, M, K, N, dX, Z, mask = a[5], a[8], a[9], a[11], a[12], a[16], a[17]
+        else:  # bn_mode, dY, H, act, X, M, K, W, N, dX, ..., bn_Z, bn_mask, ...
+            H, M, K, N, dX, Z, mask = a[2], a[5], a[6], a[8], a[9], a[13], a[14]
+        by = f4 * M * K + f4 * N * K + (f4 * M * N if H else 0) + (f4 * M * K if dX else 0)
+        by += (f4 * M * K if Z else 0) + (f4 * M * K if mask else 0)
+        fl = 2.0 * M * K * N + (2.0 * M * K * N if dX else 0)
+        if not name.endswith("_pool"):  # the output gradient rows (pool: [B, N])
+            by += f4 * M * N
+        if g:
+            by += 8.0 * gs.nnz + 4 * M
+            fl += 2.0 * gs.nnz * N
+        return by, fl
+    return None
+
+
+def _entry_kernel(name, a):
+    """The HIP kernel (rocprofv3 name prefix) a layer-wise launch runs, from its arguments: the
+    tile.hip templates k_fwd<GATHER, ACT, BN> / k_bwd<GRAD_MODE, ACT, DX, BN>. Launches of one
+    entry with different template arguments are aggregated separately. None: not mapped."""
+    t = lambda v: "true" if v else "false"  # noqa: E731
+    if name in ("lgnn_node_linear_fwd", "lgnn_node_linear_fwd_tiles"):
+        return f"void lgnn_tile::k_fwd<{t(a[3])}, {a[10]}, 0>"
+    if name == "lgnn_node_linear_fwd_bn":
+        bn = 1 if a[13] else (2 if a[14] else 0)
+        return f"void lgnn_tile::k_fwd<{t(a[3])}, {a[10]}, {bn}>"
+    if name in ("lgnn_node_linear_bwd", "lgnn_node_linear_bwd_tiles"):
+        return f"void lgnn_tile::k_bwd<{a[0]}, {a[10]}, {t(a[20])}, 0>"
+    if name == "lgnn_node_linear_bwd_bn":
+        return f"void lgnn_tile::k_bwd<0, {a[3]}, {t(a[9])}, {a[0]}>"
+    if name == "lgnn_node_linear_bwd_bn_pool":
+        return f"void lgnn_tile::k_bwd<1, {a[3]}, true, 3>"
+    if name == "lgnn_node_linear_bwd_bn_gather":
+        return f"void lgnn_tile::k_bwd<2, {a[6]}, true, 3>"
+    return None
+
+
+class EntryTracer:
+    """HIP-event timing of every C-ABI launch of one eager step (lesion_gnn_amd._lib.set_tracer):
+    each launch is bracketed by two events on the current stream, and the step is queued behind
+    a spin kernel long enough that the whole step is enqueued before the GPU reaches it, so the
+    event pairs bracket back-to-back device work, not host latency."""
+
+    def __init__(self, dev):
+        self.dev = dev
+        self.rows = []
+
+    def __call__(self, name, args, launch):
+        s = torch.cuda.current_stream(self.dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        st = launch()
+        e1.record(s)
+        self.rows.append((name, tuple(args), e0, e1))
+        return st
+
+
+def profile_entries(step, dev, gs, reps=5):
+    """Per-entry average launch time over `reps` eager steps (after one untimed), with the
+    algorithmic bytes / FLOP of each launch (_entry_model). Returns rows sorted by time per step,
+    plus the traced share of the step."""
+    from lesion_gnn_amd import _lib
+
+    # spin length: ~40 ms (calibrated), doubled until the step is enqueued before it drains
+    torch.cuda.synchronize(dev)
+    c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    c0.record()
+    torch.cuda._sleep(1_000_000)
+    c1.record()
+    torch.cuda.synchronize(dev)
+    cycles = int(1_000_000 * 40.0 / max(c0.elapsed_time(c1), 1e-3))
+    tracer = EntryTracer(dev)
+    agg: dict = {}
+    step()
+    done, tries = 0, 0
+    while done < reps and tries < 4 * reps:
+        tries += 1
+        torch.cuda.synchronize(dev)
+        tracer.rows = []
+        t0, t1, spun = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        torch.cuda._sleep(cycles)
+        spun.record()
+        t0.record()
+        _lib.set_tracer(tracer)
+        try:
+            step()
+        finally:
+            _lib.set_tracer(None)
+        t1.record()
+        late = spun.query()  # the spin drained before the host finished enqueueing the step
+        torch.cuda.synchronize(dev)
+        if late:
+            cycles *= 2
+            continue
+        done += 1
+        for name, args, e0, e1 in tracer.rows:
+            kern = _entry_kernel(name, args)
+            r = agg.setdefault((name, kern), {"calls": 0, "ms": 0.0, "bytes": 0.0, "flops": 0.0,
+                                              "modelled": True, "max_ms": 0.0})
+            ms = e0.elapsed_time(e1)
+            r["calls"] += 1
+            r["ms"] += ms
+            r["max_ms"] = max(r["max_ms"], ms)
+            m = _entry_model(name, args, gs)
+            if m is None:
+                r["modelled"] = False
+            else:
+                r["bytes"] += m[0]
+                r["flops"] += m[1]
+        agg.setdefault("_step", {"ms": 0.0})["ms"] += t0.elapsed_time(t1)
+    step_ms = agg.pop("_step")["ms"] / max(done, 1)
+    rows = []
+    for (name, kern), r in agg.items():
+        n = r["calls"]
+        row = {"entry": name, "kernel": kern, "calls_per_step": round(n / done, 2),
+               "avg_launch_ms": round(r["ms"] / n, 5), "ms_per_step": round(r["ms"] / done, 5)}
+        if r["modelled"]:
+            sec = r["ms"] * 1e-3
+            row.update({"bytes_per_launch": round(r["bytes"] / n),
+                        "flops_per_launch": round(r["flops"] / n),
+                        "GBps": round(r["bytes"] / sec / 1e9, 1),
+                        "TFLOPs": round(r["flops"] / sec / 1e12, 2)})
+        rows.append(row)
+    rows.sort(key=lambda r: -r["ms_per_step"])
+    traced = sum(r["ms_per_step"] for r in rows)
+    return rows, {"eager_step_ms": round(step_ms, 4), "traced_ms": round(traced, 4),
+                  "steps": done, "spin_cycles": cycles}
+
+
+def layer_roofline(rows, workload):
+    """roofline / roofline_next for the layer-wise workloads (C4 GIN, C5 GCN): the longest modelled
+    launches of the per-entry profile (tile.hip k_fwd / k_bwd: fp32 MFMA GEMMs + CSR gathers).
+    Both roofs are reported; `bound` is the one the kernel is closer to. For C5 (BASELINE
+    configs[4]: "rocprof HBM GB/s vs roofline") the HBM side also carries the rocprofv3 PMC bytes
+    per launch over the same HIP-event launch time (`pmc_GBps`)."""
+    cand = [r for r in rows if "bytes_per_launch" in r]
+    cand.sort(key=lambda r: -r["avg_launch_ms"])
+    out = []
+    for r in cand[:3]:
+        sec = r["avg_launch_ms"] * 1e-3
+        gbs, tf = r["bytes_per_launch"] / sec / 1e9, r["flops_per_launch"] / sec / 1e12
+        f_hbm, f_mfma = gbs / HBM_PEAK_GBS, tf / MFMA_F32_PEAK_TF
+        traffic, tsrc = pmc_traffic(r["kernel"], workload) if r["kernel"] else (None, None)
+        hbm = f_hbm >= f_mfma
+        row = {"bound": "hbm" if hbm else "mfma", "achieved": round(gbs if hbm else tf, 2),
+               "peak": HBM_PEAK_GBS if hbm else MFMA_F32_PEAK_TF,
+               "unit": "GB/s" if hbm else "TFLOP/s", "frac": round(max(f_hbm, f_mfma), 4),
+               "frac_hbm": round(f_hbm, 4), "frac_mfma": round(f_mfma, 4),
+               "achieved_GBps": round(gbs, 1), "achieved_TFLOPs": round(tf, 2),
+               "traffic": round(traffic) if traffic else None, "traffic_source": tsrc,
+               "pmc_GBps": round(traffic / sec / 1e9, 1) if traffic else None,
+               "frac_pmc_hbm": round(traffic / sec / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
+               "kernel": f"{r['entry']} -> {r['kernel']} (fp32 MFMA + CSR gather, tile.hip)",
+               "trace_name": r["kernel"], "calls_per_step": r["calls_per_step"],
+               "avg_launch_ms": r["avg_launch_ms"],
+               "bytes_per_launch": r["bytes_per_launch"],
+               "flops_per_launch": r["flops_per_launch"],
+               "timing": "HIP events around the launch on its stream, eager step queued behind a "
+                         "spin kernel (bench.profile_entries)"}
+        out.append(row)
+    if not out:
+        return None, []
+    return out[0], out[1:]
+
+
 def time_knn(b, wl, dev):
     """The data-side k-NN graph build of this batch (KNNGraph(k, loop=True), reference
     configs/config.py:47): GPU (lgnn_knn_graph, one launch for the whole batch, HIP events) vs
@@ -424,16 +678,20 @@ def time_knn(b, wl, dev):
             "bitexact_vs_batch_edge_index": same}
 
 
-def pmc_traffic(trace_name: str):
+def pmc_traffic(trace_name: str, workload: str | None = None):
     """HBM bytes per launch of `trace_name` from the committed rocprofv3 PMC passes
     (profiles/traffic.json, written by tools/summarize_prof.py from separate FETCH_SIZE and
-    WRITE_SIZE passes of this same bench command: (2*FETCH_SIZE + WRITE_SIZE) * 1024)."""
+    WRITE_SIZE passes of this same bench command: (2*FETCH_SIZE + WRITE_SIZE) * 1024). Keys
+    "<workload>:<kernel>" (passes recorded per workload) are preferred over bare kernel names."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(path):
         return None, None
-    for k, v in json.load(open(path)).items():
-        if k.startswith(trace_name):
-            return v["bytes_per_launch"], v["source"]
+    data = json.load(open(path))
+    prefixes = ([f"{workload}:{trace_name}"] if workload else []) + [trace_name]
+    for pre in prefixes:
+        for k, v in data.items():
+            if k.startswith(pre):
+                return v["bytes_per_launch"], v["source"]
     return None, None
 
 
@@ -528,24 +786,30 @@ def dry_run(args, wl, world, rank):
 
 def step_plan(world: int, capture: bool, collectives_in_fwd: bool) -> tuple:
     """How one training step runs (no collective is ever inside a captured HIP graph):
-      ("eager",)                                   --graph 0, or SyncBN at N > 1 (its RCCL
-                                                   all-reduces sit inside forward and backward)
+      ("eager",)                                   --graph 0
       ("graph:step",)                              N = 1: forward + backward + Adam, one graph
       ("graph:fwd_bwd+pack", "rccl", "graph:unpack+opt")   N > 1: the gradient bucket is packed
                                                    (and scaled) at the end of the first graph and
                                                    unpacked at the head of the second; only the
-                                                   flat RCCL all-reduce runs between them."""
-    if not capture or (world > 1 and collectives_in_fwd):
+                                                   flat RCCL all-reduce runs between them
+      ("graph:segments+pack", "rccl", "graph:unpack+opt")  N > 1 with SyncBN (GIN, C4): its
+                                                   all-reduces sit inside forward and backward, so
+                                                   the first part is captured as a chain of graphs
+                                                   split at each SyncBN exchange (dist.
+                                                   SegmentedCapture), the exchanges eager between
+                                                   them."""
+    if not capture:
         return ("eager",)
     if world == 1:
         return ("graph:step",)
+    if collectives_in_fwd:
+        return ("graph:segments+pack", "rccl", "graph:unpack+opt")
     return ("graph:fwd_bwd+pack", "rccl", "graph:unpack+opt")
 
 
-def make_step(plan: tuple, fwd_bwd, bucket, opt, dev):
-    """The step callable for `plan` (step_plan). Graph plans warm up eagerly on a side stream,
-    then capture; the eager plan zeroes the gradients, runs forward + backward, exchanges the
-    flat gradient (N > 1) and steps the optimizer."""
+def eager_step_fn(fwd_bwd, bucket, opt):
+    """The step run eagerly: zero the gradients, forward + backward, exchange the flat gradient
+    (N > 1) and step the optimizer."""
     def eager_step():
         opt.zero_grad(set_to_none=True)
         fwd_bwd()
@@ -554,7 +818,13 @@ def make_step(plan: tuple, fwd_bwd, bucket, opt, dev):
             bucket.reduce()
             bucket.unpack()
         opt.step()
+    return eager_step
 
+
+def make_step(plan: tuple, fwd_bwd, bucket, opt, dev, info: dict | None = None):
+    """The step callable for `plan` (step_plan). Graph plans warm up eagerly on a side stream,
+    then capture. `info` (optional) receives the executed launch sequence of a segmented plan."""
+    eager_step = eager_step_fn(fwd_bwd, bucket, opt)
     if plan == ("eager",):
         return eager_step
     side = torch.cuda.Stream(dev)
@@ -570,6 +840,24 @@ def make_step(plan: tuple, fwd_bwd, bucket, opt, dev):
             fwd_bwd()
             opt.step()
         return g_step.replay
+    if plan[0] == "graph:segments+pack":
+        from lesion_gnn_amd.dist import SegmentedCapture
+
+        seg = SegmentedCapture(dev)
+
+        def first():
+            fwd_bwd()
+            bucket.pack()
+
+        def second():
+            bucket.unpack()
+            opt.step()
+        seg.capture(first)
+        seg.add_collective(bucket.reduce)
+        seg.capture(second)
+        if info is not None:
+            info["segments"] = " | ".join(seg.plan())
+        return seg.replay
     g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
     with torch.cuda.graph(g_fb):
         fwd_bwd()
@@ -601,9 +889,11 @@ def main():
     run = model
     if wl.get("compile"):  # reference gat.py:84: torch.compile(model, dynamic=True)
         run = torch.compile(model, dynamic=True)
-    if world > 1:
+    multi = world > 1 or args.force_dist  # the N > 1 plan (process group + gradient bucket)
+    sync_bn = wl["model"] == "gin" and multi and args.sync_bn != "off"
+    if multi:
         ldist.broadcast_params(model)
-        if wl["model"] == "gin":  # SyncBN: full-batch statistics across the ranks
+        if sync_bn:  # SyncBN: full-batch statistics across the ranks
             model.set_sync_bn(dist.group.WORLD, global_count=b.num_nodes * world)
     params = list(model.parameters())
     if args.opt == "lgnn":
@@ -621,9 +911,10 @@ def main():
         loss_fn(wl, run(b.x, b.edge_index, b.batch, B), b.y).backward(one)
 
     # GIN under SyncBN all-reduces inside its forward and backward (RCCL collectives)
-    plan = step_plan(world, bool(args.graph), world > 1 and wl["model"] == "gin")
-    bucket = ldist.GradBucket(params, B, B * world) if world > 1 else None
-    step = make_step(plan, fwd_bwd, bucket, opt, dev)
+    plan = step_plan(2 if multi else 1, bool(args.graph), sync_bn)
+    bucket = ldist.GradBucket(params, B, B * world) if multi else None
+    plan_info: dict = {}
+    step = make_step(plan, fwd_bwd, bucket, opt, dev, plan_info)
     for _ in range(args.warmup):
         step()
     if world > 1:
@@ -651,11 +942,14 @@ def main():
         "data": "synthetic k-NN lesion graphs (pos~U[0,1)^2, x~N(0,1)), random-init weights",
         "config": {"workload": wl["desc"], "name": args.workload,
                    "step_launch": " | ".join(plan),
+                   "sync_bn": sync_bn, "process_group": multi,
                    "adam": args.opt, "graphs_per_gpu": B, "global_batch": B * world,
                    "nodes": b.num_nodes, "edges": b.num_edges, "k": wl["k"], "d_in": wl["d_in"],
                    "hidden": wl["hidden"], "parallelism": f"dp{world}"},
-        "dist": {"backend": args.backend if world > 1 else None, "world_size": world},
+        "dist": {"backend": args.backend if multi else None, "world_size": world},
     }
+    if plan_info.get("segments"):
+        out["config"]["step_segments"] = plan_info["segments"]
     bpb = step_bytes(b, wl)
     out["step_hbm_roofline"] = {
         "bytes_per_graph": round(bpb / B, 1),
@@ -703,13 +997,21 @@ def main():
         rows.sort(key=lambda r: -r["avg_launch_ms"])
         out["roofline"] = rows[0]
         out["roofline_next"] = rows[1:]
+    if rank == 0 and args.entries and not args.no_kernel_timing:
+        kind = {"gcn": "gcn", "gin": "gin", "gat": "gat"}[wl["model"]]
+        rows, tot = profile_entries(eager_step_fn(fwd_bwd, bucket, opt), dev,
+                                    GraphStats(b, kind))
+        out["entries"] = rows[:16]
+        out["entries_total"] = tot
+        if args.workload in ("c4", "c5k4", "c5k16"):
+            out["roofline"], out["roofline_next"] = layer_roofline(rows, args.workload)
     if rank == 0 and not args.no_kernel_timing:
         out["knn_graph"] = time_knn(b, wl, dev)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(wl, B, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if multi:
         dist.destroy_process_group()
 
 

@@ -193,5 +193,19 @@ def require_gpu(*tensors: torch.Tensor) -> None:
                             "tensor. There is no CPU fallback by design.")
 
 
+# Measurement hook (bench.py's per-entry HIP-event timing): when set, every call() runs as
+# _TRACER(name, args, launch) so the tracer can bracket the launch with events on its stream.
+_TRACER = None
+
+
+def set_tracer(tracer) -> None:
+    global _TRACER
+    _TRACER = tracer
+
+
 def call(name: str, *args) -> None:
-    check(getattr(load(), name)(*args), name)
+    fn = getattr(load(), name)
+    if _TRACER is None:
+        check(fn(*args), name)
+    else:
+        check(_TRACER(name, args, lambda: fn(*args)), name)

@@ -74,9 +74,9 @@ __device__ __forceinline__ float bn_elu_grad(float z, float sc, float sh) {
 // group's same-address atomics serialise in one XCD's L2 in parallel with the others' (blocks are
 // dealt round-robin over the XCDs: speed only, correct for any placement) — then each group's
 // last arrival on word 8. At most ~gridDim/8 + 8 atomics meet on one word instead of gridDim.
-// tk: 9 zeroed words, left zero (re-armed). inc: 1, or any value the caller computes from the
-// data it read first (a dependency that orders those reads before the ticket; inc != 1 never
-// wins). Returns true for exactly one workgroup.
+// tk: 9 zeroed words, left zero (re-armed). inc: 1, computed by ticket_after(x) from data the
+// caller read first (a dependency that orders those reads before the ticket). Returns true for
+// exactly one workgroup.
 __device__ __forceinline__ bool last_workgroup(unsigned int* tk, unsigned int inc) {
   const unsigned int G = gridDim.x, g = blockIdx.x & 7u;
   const unsigned int ng = (G - g + 7u) >> 3, groups = G < 8u ? G : 8u;
@@ -85,6 +85,16 @@ __device__ __forceinline__ bool last_workgroup(unsigned int* tk, unsigned int in
   if (atomicAdd(tk + 8, 1u) != groups - 1u) return false;
   tk[8] = 0u;
   return true;
+}
+
+// The ticket increment 1, as a value the compiler must compute after `dep` has arrived: the empty
+// asm takes dep as an input and may (as far as the compiler knows) rewrite the 1, so the load
+// behind dep completes before the ticket atomic that consumes the result is issued. The value is
+// always 1 (round 3 used `dep-condition ? 2 : 1`, whose 2 would wedge the ticket words).
+__device__ __forceinline__ unsigned int ticket_after(unsigned int dep) {
+  unsigned int one = 1u;
+  asm volatile("" : "+v"(one) : "v"(dep));
+  return one;
 }
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }

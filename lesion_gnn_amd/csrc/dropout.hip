@@ -75,7 +75,7 @@ __global__ __launch_bounds__(kT) void k_masks(MaskJobs J, uint64_t* __restrict__
   __syncthreads();
   // the ticket's operand depends on the counter read, so that read has returned before this
   // workgroup's ticket is taken (the last arrival then overwrites the counter safely)
-  const unsigned int inc = ctr == ~0ull ? 2u : 1u;
+  const unsigned int inc = ticket_after((unsigned int)ctr ^ (unsigned int)(ctr >> 32));
   if (threadIdx.x == 0 && last_workgroup(reinterpret_cast<unsigned int*>(state + 2), inc)) {
     state[1] = ctr + 1;
     __threadfence();

@@ -68,9 +68,8 @@ __global__ __launch_bounds__(kT) void k_adam(AdamJobs J, float* __restrict__ ste
   // device-scope fence here wrote back each XCD's dirty L2 (the parameters and moments this
   // kernel just updated) once per workgroup.
   // The ticket's operand depends on t, so this workgroup's read of step[0] has returned before
-  // its ticket is taken even when its loop ran no iteration (a numel-0 tensor): t >= 1 always,
-  // but the compiler cannot drop the dependency.
-  const unsigned int inc = t < 0.f ? 2u : 1u;
+  // its ticket is taken even when its loop ran no iteration (a numel-0 tensor).
+  const unsigned int inc = ticket_after(__float_as_uint(t));
   if (threadIdx.x == 0 && last_workgroup(ticket, inc)) {
     step[0] = t;
     __threadfence();

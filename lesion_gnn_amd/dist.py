@@ -42,6 +42,95 @@ def allreduce_grads(params: list[torch.nn.Parameter], local_count: int, global_c
         g.copy_(f)
 
 
+_SEGMENTS = None  # the SegmentedCapture in progress on this process, if any
+
+
+def sync_all_reduce(t: torch.Tensor, group) -> None:
+    """SUM all-reduce of the SyncBN sums over `group`. Eager: the collective runs here. Inside a
+    SegmentedCapture: the HIP graph being captured ends here, the collective is recorded to run
+    eagerly between that graph and the next one on replay, and capture resumes — so a step whose
+    forward and backward exchange statistics still replays as graphs (no collective is ever
+    captured)."""
+    seg = _SEGMENTS
+    if seg is not None and seg.capturing:
+        seg.split(lambda: dist.all_reduce(t, group=group))
+    else:
+        dist.all_reduce(t, group=group)
+
+
+class SegmentedCapture:
+    """A training step captured as a chain of HIP graphs split at its collectives:
+        replay() = graph_0, collective_0, graph_1, collective_1, ..., graph_n
+    Every graph shares one memory pool and is replayed in capture order (torch's rule for
+    graphs sharing a pool), so a tensor a collective reduces keeps its address from the graph
+    that writes it to the one that reads it. The split points come from sync_all_reduce (the
+    SyncBN exchanges of GIN, inside forward AND backward: the backward's split happens on the
+    autograd thread, which runs on the capture stream); `extra` collectives (the gradient
+    all-reduce) are added with add_collective between two capture() calls."""
+
+    def __init__(self, dev):
+        self.dev = torch.device(dev)
+        self.pool = torch.cuda.graph_pool_handle()
+        self.stream = torch.cuda.Stream(self.dev)
+        self.items: list = []  # ("graph", CUDAGraph) | ("collective", callable)
+        self.capturing = False
+        self._cur = None
+
+    def _begin(self) -> None:
+        self._cur = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(self.stream):
+            # relaxed: the backward's split points end and begin captures on the autograd thread
+            self._cur.capture_begin(pool=self.pool, capture_error_mode="relaxed")
+
+    def _end(self) -> None:
+        with torch.cuda.stream(self.stream):
+            self._cur.capture_end()
+        self.items.append(("graph", self._cur))
+        self._cur = None
+
+    def split(self, collective) -> None:
+        self._end()
+        self.items.append(("collective", collective))
+        self._begin()
+
+    def add_collective(self, collective) -> None:
+        self.items.append(("collective", collective))
+
+    def capture(self, fn) -> None:
+        """Capture fn() (on the capture stream) as one or more graphs."""
+        global _SEGMENTS
+        if _SEGMENTS is not None:
+            raise RuntimeError("nested SegmentedCapture")
+        cur = torch.cuda.current_stream(self.dev)
+        self.stream.wait_stream(cur)
+        torch.cuda.synchronize(self.dev)
+        _SEGMENTS = self
+        self.capturing = True
+        self._begin()
+        try:
+            with torch.cuda.stream(self.stream):
+                fn()
+        finally:
+            self._end()
+            self.capturing = False
+            _SEGMENTS = None
+        cur.wait_stream(self.stream)
+
+    @property
+    def num_graphs(self) -> int:
+        return sum(1 for k, _ in self.items if k == "graph")
+
+    def plan(self) -> tuple:
+        return tuple("graph" if k == "graph" else "rccl" for k, _ in self.items)
+
+    def replay(self) -> None:
+        for kind, obj in self.items:
+            if kind == "graph":
+                obj.replay()
+            else:
+                obj()
+
+
 def broadcast_params(module: torch.nn.Module, src: int = 0, group=None) -> None:
     """Start every replica from rank `src`'s weights."""
     for t in list(module.parameters()) + list(module.buffers()):

@@ -10,9 +10,12 @@ function of (seed, counter, stream, element) — see include/lgnn.h — so the C
 
 A model draws all masks of its forward in ONE launch from its generator state: a non-persistent
 buffer `_dropout_rng` (uint64 [seed, counter, ticket words...] x 8, stored as int64; not in state_dict, so
-checkpoint keys stay PyG's; moved by .to(device)). The seed comes from torch's default generator
-when the model is built (torch.manual_seed makes runs reproducible, as for the weights); the launch
-advances the counter on the device, so captured HIP graphs draw fresh masks per replay.
+checkpoint keys stay PyG's; moved by .to(device)). The seed is derived from the state of torch's default
+generator (set by torch.manual_seed, advanced by weight init) WITHOUT drawing from it — so building a model does not shift the random stream later
+draws (weight init of other modules, data shuffling, splits) see. The launch advances the counter
+on the device, so captured HIP graphs draw fresh masks per replay. A resumed run restarts the
+counter (the state is not checkpointed, to keep the reference's state_dict keys): masks differ
+from an uninterrupted run's, as torch's own dropout stream does after a resume.
 """
 from __future__ import annotations
 
@@ -28,10 +31,32 @@ MAX_MASKS = 16  # LGNN_MAX_MASKS
 STATE_WORDS = 8  # uint64: seed, counter, then the launch's ticket words (lgnn.h)
 
 
+_M64 = 2 ** 64 - 1
+
+
+def _splitmix64(z: int) -> int:
+    z = (z + 0x9E3779B97F4A7C15) & _M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return z ^ (z >> 31)
+
+
+def derived_seed() -> int:
+    """A seed derived from torch's default CPU generator WITHOUT advancing it: the splitmix64 of
+    a hash of its current state (read, not drawn from). Reproducible under torch.manual_seed, and
+    building a model leaves the generator's stream exactly where weight init left it. Two states
+    derived with no draw in between get the same seed (a model's weight init draws in between)."""
+    import hashlib
+
+    h = int.from_bytes(hashlib.sha256(torch.default_generator.get_state().numpy().tobytes())
+                       .digest()[:8], "little")
+    return _splitmix64(h) & (2 ** 62 - 1)
+
+
 def new_state(seed: int | None = None) -> torch.Tensor:
     """A generator state [seed, counter = 0, tickets = 0 ...] (CPU; register it as a buffer)."""
     if seed is None:
-        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        seed = derived_seed()
     return torch.tensor([int(seed)] + [0] * (STATE_WORDS - 1), dtype=torch.int64)
 
 

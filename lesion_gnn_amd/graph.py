@@ -16,6 +16,8 @@ import torch
 
 from . import _lib
 
+KEEP_BUILD_WS = os.environ.get("LGNN_GRAPH_DIAG", "0") == "1"
+
 KIND = {
     # kind: (loops mode, norm mode, self_scale of the aggregation)
     "gcn": (_lib.LGNN_LOOPS_REMAINING, _lib.LGNN_NORM_GCN),
@@ -55,6 +57,9 @@ class Graph:
         self._csr: dict[str, Csr] = {}
         self._aux: dict[str, torch.Tensor] = {}
         self.adj_values: torch.Tensor | None = None  # values of an adj_t input (as_graph)
+        # keep the last eager build's workspace for build_path() (tests / diagnostics only: it
+        # holds several (E + N)-sized arrays for the Graph's lifetime); LGNN_GRAPH_DIAG=1 sets it
+        self.keep_build_workspace = KEEP_BUILD_WS
         self.batch = None
         self._gptr = None
         self.num_graphs = None
@@ -137,15 +142,18 @@ class Graph:
             _lib.call("lgnn_graph_build_lazy" if kind == "gcn_lazy" else "lgnn_graph_build",
                       *args, _lib.stream(dev))
         self._csr[kind] = c
-        self._last_ws = (kind, ws)
+        if self.keep_build_workspace:
+            self._last_ws = (kind, ws)
         return c
 
     def build_path(self, kind: str) -> str:
         """Which launches the last eager build of `kind` took: "sorted" (the target-sorted fast
-        path: k-NN input grouped by target) or "general" (the counting sort). Synchronises."""
+        path: k-NN input grouped by target) or "general" (the counting sort). Synchronises.
+        Needs keep_build_workspace set before the build."""
         k, ws = getattr(self, "_last_ws", (None, None))
         if k != kind:
-            raise ValueError(f"no eager build of {kind!r} on this graph")
+            raise ValueError(f"no eager build of {kind!r} on this graph kept its workspace "
+                             "(set Graph.keep_build_workspace = True, or LGNN_GRAPH_DIAG=1)")
         r = _lib.load().lgnn_graph_build_path(_lib.ptr(ws), self.num_nodes, self.num_edges,
                                               _lib.stream(self.device))
         _lib.check(r if r < 0 else 0, "lgnn_graph_build_path")

@@ -578,18 +578,34 @@ def s3_weight_bundle(specs: list, bf16: bool) -> list:
     return list(flat.split(_s3_bundle_sizes([tuple(W.shape) for W in Ws], tr, bf16)))
 
 
+def _row_blocks(M: int, K: int, N: int, pad_rows: int = 64) -> list:
+    """Row ranges [r0, r1) of an M-row GEMM operand that the kernels' 32-bit buffer offsets
+    address: (rows + pad_rows) * K * 4 < 2^31 and rows * N * 4 < 2^30 (s3gemm.hip / bflin.hip
+    refuse bigger launches with LGNN_EINVAL). Blocks start on 64-row boundaries, so per-tile
+    outputs (column-sum rows) of consecutive blocks are contiguous. One block below the limits:
+    at the reference's d_in = 1025 a block holds ~520 k nodes."""
+    if M <= 0:
+        return [(0, max(M, 0))]
+    rows = min(((1 << 31) - 1) // (4 * max(K, 1)) - pad_rows, ((1 << 30) - 1) // (4 * max(N, 1)))
+    rows = max(64, rows // 64 * 64)
+    return [(r, min(r + rows, M)) for r in range(0, M, rows)]
+
+
 def dense_mm(a: torch.Tensor, Wp: torch.Tensor, N: int, bias, bf16: bool,
              want_colsum: bool = False) -> torch.Tensor:
     """Y = a B^T (+ bias) on the split-3 (fp32 accuracy) or bf16-operand MFMA kernel
-    (lgnn_s3_gemm); B's planes from dense_planes. a is fp32 (a bf16 copy is widened: exact)."""
+    (lgnn_s3_gemm); B's planes from dense_planes. a is fp32 (a bf16 copy is widened: exact).
+    Operands past the kernel's 32-bit offsets run as several row-block launches."""
     a = a.float().contiguous() if a.dtype != torch.float32 else a.contiguous()
     M, K = a.shape
     Y = torch.empty(M, N, dtype=torch.float32, device=a.device)
     cs = torch.empty((M + 63) // 64 * N, dtype=torch.float32, device=a.device) \
         if want_colsum and M > 0 else None
-    _lib.call("lgnn_s3_gemm", _lib.ptr(a), M, K, _lib.ptr(Wp), N, 1 if bf16 else 3,
-              _lib.ptr(_f32c(bias) if bias is not None else None), _lib.ptr(Y), _lib.ptr(cs),
-              _s(a.device))
+    bp = _lib.ptr(_f32c(bias) if bias is not None else None)
+    for r0, r1 in _row_blocks(M, K, N):
+        _lib.call("lgnn_s3_gemm", _lib.ptr(a) + r0 * K * 4, r1 - r0, K, _lib.ptr(Wp), N,
+                  1 if bf16 else 3, bp, _lib.ptr(Y) + r0 * N * 4,
+                  _lib.ptr(cs) + (r0 // 64) * N * 4 if cs is not None else None, _s(a.device))
     if cs is not None:
         _COLSUMS[id(Y)] = (weakref.ref(Y), Y._version, cs)
         weakref.finalize(Y, _COLSUMS.pop, id(Y), None)
@@ -609,11 +625,20 @@ def dense_wgrad(dy: torch.Tensor, x: torch.Tensor, bf16: bool, want_db: bool = F
     if N % 2:  # the kernel reads dY in column pairs: pad one zero column (exact)
         dy = torch.nn.functional.pad(dy, (0, 1))
     Ne = dy.size(1)
-    S = _lib.load().lgnn_s3_wgrad_partials(M, K, Ne)
+    lib = _lib.load()
+    # row blocks past the kernel's 32-bit offsets: each block's partial slabs follow the
+    # previous block's, so one fixed-order reduction sums them all
+    blocks = _row_blocks(M, max(K, Ne), 0, pad_rows=64)
+    Ss = [lib.lgnn_s3_wgrad_partials(r1 - r0, K, Ne) for r0, r1 in blocks]
+    S = sum(Ss)
     part = torch.empty(S * Ne * K, dtype=torch.float32, device=dev)
     dbp = torch.empty(S * Ne, dtype=torch.float32, device=dev) if want_db else None
-    _lib.call("lgnn_s3_wgrad", _lib.ptr(dy), Ne, _lib.ptr(x), M, K, 1 if bf16 else 3,
-              _lib.ptr(part), S, _lib.ptr(dbp), _s(dev))
+    so = 0
+    for (r0, r1), Sb in zip(blocks, Ss):
+        _lib.call("lgnn_s3_wgrad", _lib.ptr(dy) + r0 * Ne * 4, Ne, _lib.ptr(x) + r0 * K * 4,
+                  r1 - r0, K, 1 if bf16 else 3, _lib.ptr(part) + so * Ne * K * 4, Sb,
+                  _lib.ptr(dbp) + so * Ne * 4 if dbp is not None else None, _s(dev))
+        so += Sb
     dW = torch.empty(Ne, K, dtype=torch.float32, device=dev)
     db = torch.empty(Ne, dtype=torch.float32, device=dev) if want_db else None
     jobs = [(part, S, Ne * K, dW)] + ([(dbp, S, Ne, db)] if want_db else [])
@@ -626,8 +651,8 @@ def dense_wgrad(dy: torch.Tensor, x: torch.Tensor, bf16: bool, want_db: bool = F
     return dW, db
 
 
-# bf16 GEMMs on the hand-written MFMA kernels (csrc/bflin.hip); LGNN_BF16_MFMA=0 routes them to
-# the library GEMMs above instead (A/B and fallback for N > 128)
+# bf16 GEMMs on the hand-written MFMA kernels (csrc/bflin.hip); LGNN_BF16_MFMA=0 (A/B) and widths
+# N > 128 route them to the one-plane split GEMMs above (dense_mm / dense_wgrad with bf16=True)
 BF16_MFMA = os.environ.get("LGNN_BF16_MFMA", "1") != "0"
 
 
@@ -697,9 +722,13 @@ def bf16_gemm(A: torch.Tensor, Wb: torch.Tensor, bias, N: int, want_yb: bool = F
     Yb = torch.empty(M, N, dtype=torch.bfloat16, device=A.device) if want_yb else None
     cs = torch.empty((M + 63) // 64 * N, dtype=torch.float32, device=A.device) \
         if want_colsum and M > 0 else None
-    _lib.call("lgnn_bf16_gemm", _lib.ptr(A), int(A.dtype == torch.float32), M, K, _lib.ptr(Wb),
-              _lib.ptr(_f32c(bias) if bias is not None else None), N, _lib.ptr(Y), _lib.ptr(Yb),
-              _lib.ptr(cs), _s(A.device))
+    es = A.element_size()
+    bp = _lib.ptr(_f32c(bias) if bias is not None else None)
+    for r0, r1 in _row_blocks(M, K, N):  # row blocks past the kernel's 32-bit offsets
+        _lib.call("lgnn_bf16_gemm", _lib.ptr(A) + r0 * K * es, int(A.dtype == torch.float32),
+                  r1 - r0, K, _lib.ptr(Wb), bp, N, _lib.ptr(Y) + r0 * N * 4,
+                  _lib.ptr(Yb) + r0 * N * 2 if Yb is not None else None,
+                  _lib.ptr(cs) + (r0 // 64) * N * 4 if cs is not None else None, _s(A.device))
     if cs is not None:
         _COLSUMS[id(Y)] = (weakref.ref(Y), Y._version, cs)
         weakref.finalize(Y, _COLSUMS.pop, id(Y), None)
@@ -737,10 +766,18 @@ def bf16_wgrad(dYb: torch.Tensor, X: torch.Tensor, N: int, reducer: list = None)
     if X.dtype != torch.float32 and K % 2:  # bf16 X needs even rows; bf16 -> fp32 is exact
         X = X.float()
     dev = X.device
-    S = _lib.load().lgnn_bf16_wgrad_partials(M, K)
+    lib = _lib.load()
+    es = X.element_size()
+    blocks = _row_blocks(M, K, 0, pad_rows=32 * 64)  # past the kernel's 32-bit offsets
+    Ss = [lib.lgnn_bf16_wgrad_partials(r1 - r0, K) for r0, r1 in blocks]
+    S = sum(Ss)
     part = torch.empty(S * N * K, dtype=torch.float32, device=dev)
-    _lib.call("lgnn_bf16_wgrad", _lib.ptr(dYb), N, _lib.ptr(X), int(X.dtype == torch.float32), M,
-              K, _lib.ptr(part), S, _s(dev))
+    so = 0
+    for (r0, r1), Sb in zip(blocks, Ss):
+        _lib.call("lgnn_bf16_wgrad", _lib.ptr(dYb) + r0 * N * 2, N, _lib.ptr(X) + r0 * K * es,
+                  int(X.dtype == torch.float32), r1 - r0, K, _lib.ptr(part) + so * N * K * 4, Sb,
+                  _s(dev))
+        so += Sb
     dW = torch.empty(N, K, dtype=torch.float32, device=dev)
     if reducer is not None:
         reducer.append((part, S, N * K, dW))
@@ -836,8 +873,8 @@ def dense_path(W, bf16: bool) -> bool:
 
 
 def linear_auto(x, W, b=None, bf16: bool = False, wp=None):
-    """node_linear (tile kernels) where the shape allows and fp32 is asked for; else the library
-    GEMM (dense_linear)."""
+    """node_linear (tile kernels) where the shape allows and fp32 is asked for; else the
+    hand-written dense GEMMs (dense_linear: split-3 s3gemm.hip, or one bf16 plane in bf16 mode)."""
     if not bf16 and fast_shape(W.size(1), W.size(0)):
         return node_linear(x, W, b)
     return dense_linear(x, W, b, bf16, wp)
@@ -1175,9 +1212,9 @@ class _GINConv(torch.autograd.Function):
             if count <= 1:
                 raise ValueError("Expected more than 1 value per channel when training")
             if group is not None:
-                import torch.distributed as dist
+                from .dist import sync_all_reduce
 
-                dist.all_reduce(sums, group=group)
+                sync_all_reduce(sums, group)
         mean, invstd, scale, shift = bn_finalize(sums, count, bn, training, N1, x.device)
         A1 = bn_act(Z1, scale, shift, mask)
         H = linear_fwd(A1, W2, b2, act)
@@ -1224,11 +1261,11 @@ class _GINConv(torch.autograd.Function):
                 mean, invstd, scale, shift = bn_finalize(sums, count, bn, training, N1, dev,
                                                          part=(part, P))
             else:
-                import torch.distributed as dist
+                from .dist import sync_all_reduce
 
                 _lib.call("lgnn_bn_partials_reduce", _lib.ptr(part), P, N1, _lib.ptr(sums), None,
                           None, _s(dev))
-                dist.all_reduce(sums, group=group)
+                sync_all_reduce(sums, group)
                 mean, invstd, scale, shift = bn_finalize(sums, count, bn, training, N1, dev)
         else:
             if s3:
@@ -1319,10 +1356,10 @@ class _GINConv(torch.autograd.Function):
                   _lib.ptr(dg), _lib.ptr(dbt), _s(dev))
         sums = local
         if ctx.training and ctx.group is not None:
-            import torch.distributed as dist
+            from .dist import sync_all_reduce
 
             sums = local.clone()
-            dist.all_reduce(sums, group=ctx.group)
+            sync_all_reduce(sums, ctx.group)
         # Lin1 backward with the BN backward applied to dA1 as it is loaded
         want_dx = ctx.needs_input_grad[0]
         dxpre = torch.empty(M, K, dtype=torch.float32, device=dev) if want_dx else None
@@ -1355,10 +1392,10 @@ class _GINConv(torch.autograd.Function):
         local = bn_bwd_stats(dA1, Z1, mask, scale, shift, mean, invstd)
         sums = local
         if ctx.training and ctx.group is not None:
-            import torch.distributed as dist
+            from .dist import sync_all_reduce
 
             sums = local.clone()
-            dist.all_reduce(sums, group=ctx.group)
+            sync_all_reduce(sums, ctx.group)
         dZ1, dg, dbt = bn_bwd_apply(dA1, Z1, mask, scale, shift, mean, invstd, sums, ctx.count,
                                     ctx.training, local, ctx.affine)
         want_dx = ctx.needs_input_grad[0]

@@ -91,12 +91,12 @@ class LinearWarmupCosineAnnealingLR(torch.optim.lr_scheduler.LRScheduler):
     """pl_bolts.optimizers.lr_scheduler.LinearWarmupCosineAnnealingLR (pl_bolts 0.7.0), the
     scheduler the reference's configure_optimizers builds by name (models/base.py:174-175; pl_bolts
     is not installed here). A closed-form schedule per base lr b, epoch e (= last_epoch), warmup
-    w, max m, start s, minimum eta:
+    w, max m, start s, minimum eta, as pl_bolts' _get_closed_form_lr():
       e < w:  s + e (b - s) / max(1, w - 1)          (linear warmup from s to b)
       e >= w: eta + (b - eta) (1 + cos(pi (e - w) / (m - w))) / 2   (cosine to eta at e = m)
-    pl_bolts' get_lr() applies the same values recursively (each step from the group's current
-    lr); _get_closed_form_lr() is this formula. This scheduler computes it directly, so its
-    values match pl_bolts' closed form exactly and its recursive form to fp rounding."""
+    get_lr() is pl_bolts' recursive form (each step from the group's current lr), restated case
+    for case, so the schedule equals pl_bolts' for every warmup including w = 0 (where pl_bolts
+    starts at warmup_start_lr and decays from there, unlike the closed form)."""
 
     def __init__(self, optimizer, warmup_epochs: int, max_epochs: int,
                  warmup_start_lr: float = 0.0, eta_min: float = 0.0, last_epoch: int = -1):
@@ -114,10 +114,26 @@ class LinearWarmupCosineAnnealingLR(torch.optim.lr_scheduler.LRScheduler):
         return self.eta_min + 0.5 * (base_lr - self.eta_min) * (1 + math.cos(math.pi * (e - w)
                                                                                / span))
 
+    def _get_closed_form_lr(self):
+        return [self._closed_form(b) for b in self.base_lrs]
+
     def get_lr(self):
         if not getattr(self, "_get_lr_called_within_step", True):
             warnings.warn("To get the last learning rate computed by the scheduler, please use "
                           "`get_last_lr()`.", UserWarning)
-        return [self._closed_form(b) for b in self.base_lrs]
+        e, w, m, s, eta = (self.last_epoch, self.warmup_epochs, self.max_epochs,
+                           self.warmup_start_lr, self.eta_min)
+        span = max(1, m - w)
+        groups = self.optimizer.param_groups
+        if e == 0:
+            return [s] * len(self.base_lrs)
+        if e < w:
+            return [g["lr"] + (b - s) / max(1, w - 1) for b, g in zip(self.base_lrs, groups)]
+        if e == w:
+            return list(self.base_lrs)
+        if (e - 1 - m) % (2 * span) == 0:
+            return [g["lr"] + (b - eta) * (1 - math.cos(math.pi / span)) / 2
+                    for b, g in zip(self.base_lrs, groups)]
+        return [(1 + math.cos(math.pi * (e - w) / span)) / (1 + math.cos(math.pi * (e - w - 1) / span))
+                * (g["lr"] - eta) + eta for g in groups]
 
-    _get_closed_form_lr = get_lr

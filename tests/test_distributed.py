@@ -85,15 +85,17 @@ def test_shard_bounds_balance_edges():
 
 def test_bench_step_plan():
     """bench.py's step structure: a collective is never inside a captured graph — SyncBN (GIN,
-    C4) at N > 1 runs eagerly (its all-reduces sit inside forward and backward); otherwise the
-    flat-gradient RCCL all-reduce is the only eager part between two graphs."""
+    C4) at N > 1 is captured as graph segments split at its all-reduces (which sit inside
+    forward and backward); otherwise the flat-gradient RCCL all-reduce is the only eager part
+    between two graphs."""
     import bench
 
     assert bench.step_plan(1, True, False) == ("graph:step",)
     assert bench.step_plan(1, True, True) == ("graph:step",)  # one rank: SyncBN is local
     assert bench.step_plan(2, True, False) == ("graph:fwd_bwd+pack", "rccl", "graph:unpack+opt")
-    assert bench.step_plan(8, True, True) == ("eager",)
+    assert bench.step_plan(8, True, True) == ("graph:segments+pack", "rccl", "graph:unpack+opt")
     assert bench.step_plan(4, False, False) == ("eager",)
+    assert bench.step_plan(4, False, True) == ("eager",)
 
 
 class _SyncNormNet(torch.nn.Module):
@@ -138,7 +140,9 @@ def _plan_worker(rank, world, port, out):
     def fwd_bwd():
         torch.nn.functional.cross_entropy(m(x, world), y).backward()
 
-    plan = bench.step_plan(world, True, True)
+    # CPU: the eager form of the plan (--graph 0); the captured segments run on the GPU
+    # (tests/test_gpu_dist.py)
+    plan = bench.step_plan(world, False, True)
     step = bench.make_step(plan, fwd_bwd, bucket, opt, torch.device("cpu"))
     for _ in range(3):
         step()

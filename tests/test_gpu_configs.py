@@ -8,6 +8,9 @@ the logits, loss and every parameter gradient are compared.
   C3f32 the same in fp32
   C4   GIN + global_add_pool, 8192 graphs on one GPU (the 8-GPU global batch)
   C5   GCN, power-law N in [16, 512], k = 4 and k = 16, 1024 graphs
+  refcfg the reference experiment (configs/config.py:52-65): GAT [128]*4, heads 2, dropout 0.35,
+       torch.compile(dynamic=True), d_in 1025, MSE, 1024 graphs — the oracle replays the step's
+       dropout masks (oracle.pyg_ref.DropoutMasks)
 
 Bars (written per case): fp32 logits within 1e-4 absolute (× max(1, |logits|) for the add pool,
 whose logits sum 64 rows), gradients within 1e-4 × max|grad| per tensor (floor 1e-6); bf16 (C3)
@@ -22,11 +25,12 @@ import oracle.pyg_ref as ref
 pytestmark = pytest.mark.gpu
 
 CASES = [("c2", 1024), ("c3", 1024), ("c3f32", 1024), ("c4", 8192), ("c5k4", 1024),
-         ("c5k16", 1024)]
+         ("c5k16", 1024), ("refcfg", 1024)]
 
 
-def run_step(wl, model, b, dev, oracle):
-    logits = model(b.x.to(dev), b.edge_index.to(dev), b.batch.to(dev), b.num_graphs)
+def run_step(wl, model, b, dev, oracle, masks=None):
+    kw = {"masks": masks} if masks is not None else {}
+    logits = model(b.x.to(dev), b.edge_index.to(dev), b.batch.to(dev), b.num_graphs, **kw)
     loss = bench.loss_fn(wl, logits, b.y.to(dev), oracle=oracle)
     model.zero_grad(set_to_none=True)
     loss.backward()
@@ -42,8 +46,19 @@ def test_bench_config_step_vs_oracle(cuda, name, B):
     oref = bench.build_model(wl, oracle=True).train()
     oref.load_state_dict({k: v.cpu() for k, v in ours.state_dict().items()})
     tol = 1e-3 if wl.get("precision") == "bf16" else 1e-4
-    lo, losso, go = run_step(wl, ours, b, cuda, oracle=False)
-    lr_, lossr, gr = run_step(wl, oref, b, "cpu", oracle=True)
+    masks = None
+    run = ours
+    if wl.get("dropout"):  # the oracle applies the masks the device step draws
+        from lesion_gnn_amd import dropout
+
+        seed, ctr = dropout.get_state(ours._dropout_rng)
+        masks = ref.DropoutMasks(seed, ctr, wl["dropout"])
+    if wl.get("compile"):  # as bench.py runs it (reference gat.py:84)
+        torch._dynamo.reset()
+        run = torch.compile(ours, dynamic=True)
+    lo, losso, go = run_step(wl, run, b, cuda, oracle=False)
+    go = {k.replace("_orig_mod.", ""): v for k, v in go.items()}
+    lr_, lossr, gr = run_step(wl, oref, b, "cpu", oracle=True, masks=masks)
     scale = max(1.0, lr_.abs().max().item()) if wl["pool"] == "add" else 1.0
     torch.testing.assert_close(lo, lr_, rtol=0, atol=tol * scale)
     torch.testing.assert_close(losso, lossr, rtol=10 * tol, atol=1e-6)

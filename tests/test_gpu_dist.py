@@ -103,3 +103,78 @@ def test_two_ranks_match_full_batch(cuda, kind):
             if "running" in k:
                 torch.testing.assert_close(torch.from_numpy(res[0]["state"][k]), v.cpu(),
                                            rtol=1e-5, atol=1e-6)
+
+
+def plan_worker(rank, world, port, q):
+    """bench.py's N > 1 GIN + SyncBN plan, captured: graph segments split at the SyncBN
+    exchanges (forward and backward), the gradient bucket exchange, the optimizer graph."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from lesion_gnn_amd import dist as ldist
+    from lesion_gnn_amd import ops, synth
+
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    b = synth.make_batch(B, n=N, k=K, d_in=32, seed=17)
+    m = build("gin").to(dev).train()
+    m.set_sync_bn(dist.group.WORLD, global_count=B * N)
+    g0, g1 = rank * B // world, (rank + 1) * B // world
+    x, ei, bt, y = (t.to(dev) for t in shard(b, g0, g1))
+    params = list(m.parameters())
+    # SGD: Adam would normalise the analytically-zero gradient of the bias that feeds BatchNorm
+    # (round-off noise) into +-lr steps that differ between the replicas and the full batch
+    opt = torch.optim.SGD(params, lr=0.05)
+    bucket = ldist.GradBucket(params, g1 - g0, B)
+
+    def fwd_bwd():
+        ops.cross_entropy(m(x, ei, bt, g1 - g0), y).backward()
+
+    plan = bench.step_plan(world, True, True)
+    info = {}
+    step = bench.make_step(plan, fwd_bwd, bucket, opt, dev, info)
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize(dev)
+    q.put((rank, {"plan": plan, "segments": info.get("segments"),
+                  "state": {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_segmented_syncbn_plan_matches_full_batch(cuda):
+    """The captured N > 1 GIN + SyncBN step (bench.step_plan -> SegmentedCapture) on 2 ranks:
+    after the 3 warm-up eager steps make_step runs and 3 replays, every replica holds the weights
+    and BN running statistics of 6 full-batch single-process steps."""
+    from lesion_gnn_amd import ops, synth
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=plan_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert res[0]["plan"] == ("graph:segments+pack", "rccl", "graph:unpack+opt")
+    seg = res[0]["segments"].split(" | ")
+    # per GINConv: one exchange in the forward, one in the backward; then the gradient bucket
+    assert seg.count("rccl") == 2 * 2 + 1 and seg[-1] == "graph", seg
+    b = synth.make_batch(B, n=N, k=K, d_in=32, seed=17)
+    m = build("gin").to(cuda).train()
+    opt = torch.optim.SGD(list(m.parameters()), lr=0.05)
+    x, ei, bt, y = b.x.to(cuda), b.edge_index.to(cuda), b.batch.to(cuda), b.y.to(cuda)
+    for _ in range(6):
+        opt.zero_grad(set_to_none=True)
+        ops.cross_entropy(m(x, ei, bt, B), y).backward()
+        opt.step()
+    for k, v in m.state_dict().items():
+        for r in range(2):
+            got = torch.from_numpy(res[r]["state"][k])
+            if got.dtype.is_floating_point:
+                torch.testing.assert_close(got, v.cpu(), rtol=1e-4, atol=1e-5,
+                                           msg=lambda s: f"rank {r} {k}: {s}")
+            else:
+                assert torch.equal(got, v.cpu()), k

@@ -109,12 +109,16 @@ def test_reference_config_gat_dropout_training_step(cuda, compiled):
     oref = ref.GAT(1025, [128] * 4, 1, heads=2, dropout=0.35).train()
     oref.load_state_dict(_strip(module.model.state_dict()))
     rng = module.model._dropout_rng
+    seen = []  # the inner model's logits of the step (forward hook; compiled or not)
+    module.model.register_forward_hook(lambda m, a, out: seen.append(out.detach().cpu()))
     for step in range(2):  # the second step draws new masks (counter + 1)
         seed, ctr = dropout.get_state(rng)
         assert ctr == step
         module.zero_grad(set_to_none=True)
+        seen.clear()
         loss = module.training_step(b.to(cuda))
         loss.backward()
+        assert len(seen) == 1
         go = {k: p.grad.detach().cpu() for k, p in _strip(dict(module.model.named_parameters()))
               .items()}
         oref.zero_grad(set_to_none=True)
@@ -124,7 +128,10 @@ def test_reference_config_gat_dropout_training_step(cuda, compiled):
         want.backward()
         gr = {k: p.grad for k, p in oref.named_parameters()}
         torch.testing.assert_close(loss.detach().cpu(), want.detach(), rtol=1e-5, atol=1e-6)
-        _check(torch.zeros(1), go, torch.zeros(1), gr, 1e-4)
+        # the raw logits and the clamped predictions the criterion saw (gat.py:94-95)
+        _check(seen[0], go, logits.detach(), gr, 1e-4)
+        torch.testing.assert_close(seen[0].squeeze(1).clamp(0, 4),
+                                   logits.detach().squeeze(1).clamp(0, 4), rtol=0, atol=1e-4)
     # dropout changed the result: the same step without masks differs
     with torch.no_grad():
         plain = ref.criterion("MSE", oref.eval()(b.x, b.edge_index, b.batch, b.num_graphs),

@@ -426,6 +426,7 @@ def test_lazy_transpose_build(cuda, case):
     else:
         b = synth.make_batch(6, n=64, k=20, d_in=8, seed=53, sizes=[64, 64, 64, 64, 64, 64])
     g = Graph(b.edge_index.to(cuda), b.num_nodes)
+    g.keep_build_workspace = True  # build_path() below
     full, lazy = g.csr("gcn"), g.csr("gcn_lazy")
     nnz = int(full.rowptr[-1])  # arrays have capacity E + N; entries past nnz are unused
     for name in ("rowptr", "err"):

@@ -113,6 +113,7 @@ def test_sorted_build_bitexact(cuda, monkeypatch, case, kind):
     want = _build(ei, n, kind, False, cuda, monkeypatch)
     monkeypatch.setenv("LGNN_GRAPH_SORTED", "1")
     g = Graph(ei.to(cuda), n)
+    g.keep_build_workspace = True  # build_path() below
     got = _build(ei, n, kind, False, cuda, monkeypatch)
     assert set(got) == set(want)
     for f in want:

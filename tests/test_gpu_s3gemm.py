@@ -211,3 +211,45 @@ def test_s3_gemm_att_scores(cuda, heads, C, K):
     for got, want in ((a_s, r_s), (a_d, r_d)):
         scale = (Y.view(M, heads, C).abs() * att_s.view(heads, C).abs()).sum(-1).max().item()
         assert (got - want).abs().max().item() <= 2e-6 * scale
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_in_proj_past_32bit_offsets(cuda, bf16):
+    """the in_proj GEMMs take 32-bit buffer offsets, so a launch over more than
+    ~523 k rows of 1025 channels would be refused (LGNN_EINVAL). ops splits such operands into
+    row blocks (ops._row_blocks): here M is just above one block (two launches), the rows on
+    both sides of the block boundary and the last rows are checked against float64, and the
+    weight / bias gradients (partial slabs of both blocks in one fixed-order reduction) against
+    float64 over all rows."""
+    K, N = 1025, 128
+    blocks = ops._row_blocks(10 ** 7, K, N)
+    M = blocks[0][1] + 1000  # one block + 1000 rows
+    assert len(ops._row_blocks(M, K, N)) == 2
+    g = torch.Generator(device=cuda).manual_seed(7)
+    A = torch.randn(M, K, device=cuda, generator=g)
+    W = torch.randn(N, K, device=cuda, generator=g) / K ** 0.5
+    b = torch.randn(N, device=cuda, generator=g)
+    if bf16:
+        Wb, _ = ops.bf16_weight_operands(W, False)
+        Y = ops.bf16_gemm(A, Wb, b, N)[0]
+        Ar, Wr = A.bfloat16().double(), W.bfloat16().double()
+    else:
+        Y = ops.dense_mm(A, ops.dense_planes(W, False, False), N, b, False)
+        Ar, Wr = A.double(), W.double()
+    r0 = blocks[0][1]
+    for rows in (slice(0, 64), slice(r0 - 64, r0 + 64), slice(M - 64, M)):
+        want = Ar[rows] @ Wr.T + b.double()
+        err = (Y[rows].double() - want).abs().max().item()
+        assert err <= (2e-6 if bf16 else 2e-5) * max(1.0, want.abs().max().item()), (rows, err)
+    dy = torch.randn(M, N, device=cuda, generator=g) / M ** 0.5
+    if bf16:
+        dW = ops.bf16_wgrad(dy.bfloat16(), A, N)
+        want = dy.bfloat16().double().T @ Ar
+        tol = 2e-6
+    else:
+        dW, db = ops.dense_wgrad(dy, A, False, want_db=True)
+        want = dy.double().T @ A.double()
+        torch.testing.assert_close(db.double(), dy.double().sum(0), rtol=0, atol=1e-5)
+        tol = 2e-5
+    err = (dW.double() - want).abs().max().item()
+    assert err <= tol * max(1.0, want.abs().max().item()), err

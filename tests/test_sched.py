@@ -31,7 +31,8 @@ def pl_bolts_recursive(base, warmup, max_epochs, start, eta, epochs):
 
 
 @pytest.mark.parametrize("warmup,max_epochs,start,eta", [(10, 100, 0.0, 0.0), (5, 40, 1e-4, 1e-5),
-                                                        (3, 7, 0.0, 1e-6)])
+                                                        (3, 7, 0.0, 1e-6), (0, 20, 1e-4, 0.0),
+                                                        (1, 20, 1e-4, 0.0), (0, 9, 0.0, 1e-6)])
 def test_schedule_matches_pl_bolts(warmup, max_epochs, start, eta):
     base = 1e-3
     p = torch.nn.Parameter(torch.zeros(2))
@@ -46,7 +47,11 @@ def test_schedule_matches_pl_bolts(warmup, max_epochs, start, eta):
     want = pl_bolts_recursive(base, warmup, max_epochs, start, eta, max_epochs + 1)
     for e, (g, w) in enumerate(zip(got, want)):
         assert g == pytest.approx(w, rel=1e-9, abs=1e-15), e
-    assert got[warmup] == pytest.approx(base) and got[max_epochs] == pytest.approx(eta, abs=1e-15)
+    if warmup > 0:
+        assert got[warmup] == pytest.approx(base)
+        assert got[max_epochs] == pytest.approx(eta, abs=1e-15)
+    else:  # pl_bolts starts at warmup_start_lr and decays from it (never reaches base)
+        assert got[0] == start
 
 
 def test_configure_optimizers_builds_warmup_cosine():

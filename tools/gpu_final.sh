@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-3 final measurements: kernel-trace + HBM PMC passes for the bench workloads, then one bench
-# line per workload (with the CPU baseline leg). Usage: bash tools/gpu_r03_final.sh <tag>
+# Final measurements of a round: kernel-trace + HBM PMC passes for the bench workloads, then one bench
+# line per workload (with the CPU baseline leg). Usage: bash tools/gpu_final.sh <tag>
 set -uo pipefail
 TAG=$1
 OUT=gpurun_out/$TAG

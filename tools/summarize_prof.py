@@ -46,6 +46,8 @@ def pmc(run: str, counter: str):
 def main():
     run, prefix = sys.argv[1], sys.argv[2]
     steps = 25
+    # --workload W: traffic.json keys "W:<kernel>" (kernels shared by workloads of other sizes)
+    wl = sys.argv[sys.argv.index("--workload") + 1] if "--workload" in sys.argv else None
     if "--steps" in sys.argv:
         steps = int(sys.argv[sys.argv.index("--steps") + 1])
     ks = kernel_stats(run)
@@ -74,7 +76,7 @@ def main():
             w = write.get(k, 0.0)
             b = (2 * fetch[k] + w) * 1024
             tl.append(f"{k[:100]:100s} {fetch[k]:11.1f} {w:11.1f} {b / 1e6:9.2f}")
-            traffic[k] = {"bytes_per_launch": b, "source": os.path.basename(prefix) +
+            traffic[f"{wl}:{k}" if wl else k] = {"bytes_per_launch": b, "source": os.path.basename(prefix) +
                           "_pmc_traffic.txt"}
         open(prefix + "_pmc_traffic.txt", "w").write("\n".join(tl) + "\n")
         json.dump(traffic, open(traffic_path, "w"), indent=1, sort_keys=True)
