@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 31
+#define LGNN_ABI_VERSION 32
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -138,6 +138,32 @@ size_t lgnn_knn_workspace_bytes(int64_t num_graphs);
 int lgnn_knn_graph(const double* pos, int64_t num_nodes, int dims, const int64_t* batch,
                    const int32_t* ptr, int64_t num_graphs, int k, int loop, int64_t* edge_index,
                    int64_t num_edges, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Radius graph of a batch of point sets (ABI v32). Replaces: torch_cluster.radius_graph(pos, r,
+ * batch, loop, max_num_neighbors, flow='source_to_target') behind PyG's RadiusGraph transform,
+ * the reference sweep's alternative to KNNGraph (src/lesion_gnn/scripts/sweep.py:113-118,
+ * RadiusGraph(r=...) with PyG's defaults loop=False, max_num_neighbors=32; resolved by name in
+ * transforms.py:19-23). For every node q of graph g: walk the nodes c of g in index order, taking
+ * c when the fp64 squared distance |p_q - p_c|^2 < r * r, until limit = max_num_neighbors (loop)
+ * or max_num_neighbors + 1 (!loop) are taken; without loop the pair (q, q) is then dropped
+ * (torch_cluster 1.6.3's CUDA selection; its CPU kd-tree keeps a traversal-order subset when more
+ * than `limit` are in range). edge_index [2][E] int64 = (c, q), grouped by q in node order, c
+ * ascending. pos / batch / ptr as lgnn_knn_graph; workspace lgnn_radius_workspace_bytes(N).
+ *   lgnn_radius_count: per-node counts and their scan into the workspace; the edge count E is the
+ *                      int64 at byte offset N * 8 of the workspace (the caller reads it to size
+ *                      edge_index: the one host synchronisation).
+ *   lgnn_radius_graph: writes the edges (same workspace, untouched in between; num_edges = E).
+ * Deterministic, bit-exact vs the fp64 restatement (oracle/pyg_ref.py radius_graph).
+ * ------------------------------------------------------------------------------------------- */
+size_t lgnn_radius_workspace_bytes(int64_t num_nodes);
+int lgnn_radius_count(const double* pos, int64_t num_nodes, int dims, const int64_t* batch,
+                      const int32_t* ptr, int64_t num_graphs, double r, int max_num_neighbors,
+                      int loop, void* workspace, size_t workspace_bytes, void* stream);
+int lgnn_radius_graph(const double* pos, int64_t num_nodes, int dims, const int64_t* batch,
+                      const int32_t* ptr, int64_t num_graphs, double r, int max_num_neighbors,
+                      int loop, int64_t* edge_index, int64_t num_edges, const void* workspace,
+                      size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Gaussian edge weights. Replaces lesion_gnn.transforms.GaussianDistance.__call__ (reference

@@ -97,6 +97,9 @@ SIGNATURES: dict[str, tuple] = {
                                     P, P, P]),
     "lgnn_knn_workspace_bytes": (SZ, [I64]),
     "lgnn_knn_graph": (I32, [P, I64, I32, P, P, I64, I32, I32, P, I64, P, SZ, P]),
+    "lgnn_radius_workspace_bytes": (SZ, [I64]),
+    "lgnn_radius_count": (I32, [P, I64, I32, P, P, I64, F64, I32, I32, P, SZ, P]),
+    "lgnn_radius_graph": (I32, [P, I64, I32, P, P, I64, F64, I32, I32, P, I64, P, SZ, P]),
     "lgnn_gaussian_distance": (I32, [P, I32, I64, I32, P, I64, F64, P, I32, P, P]),
     "lgnn_tile_count": (I32, [I64]),
     "lgnn_tile_open": (I32, [P, P, I64, P, P]),
@@ -142,7 +145,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 31
+ABI_VERSION = 32
 
 _lib = None
 

@@ -1031,6 +1031,14 @@ extern "C" size_t lgnn_graph_workspace_bytes(int64_t num_nodes, int64_t num_edge
   return ws_total(num_nodes, num_edges);
 }
 
+// Ablation knob (timing only, never a product setting): LGNN_ABL_SKIP_GENERAL=1 drops the three
+// general-path launches of a target-sorted-path build (k_count / k_fill / k_finish), which is
+// correct only for input the sorted path accepts — it measures what those no-op launches cost.
+static bool abl_skip_general() {
+  const char* e = getenv("LGNN_ABL_SKIP_GENERAL");
+  return e && e[0] == '1';
+}
+
 static int graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loops, int norm,
                        int32_t* rowptr, int32_t* col, float* w, int32_t* tptr, int32_t* tidx,
                        float* tw, int32_t* tmap, int32_t* tile_open, const int64_t* batch,
@@ -1198,7 +1206,8 @@ static int graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loop
       return (int)hipGetLastError();
     return LGNN_OK;
   }
-  if (E > 0) {
+  const bool skip_general = try_sorted && abl_skip_general();
+  if (E > 0 && !skip_general) {
     if (small_edges(E))
       hipLaunchKernelGGL(k_count<4>, dim3((unsigned)((E + chunk_of(4) - 1) / chunk_of(4))),
                          dim3(kThreads), 0, s, edge_index, E, N, loops, ws.cnt,
@@ -1221,7 +1230,7 @@ static int graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loop
                        col, w, err_count, (int)nblk);
     LGNN_LAUNCH_CHECK();
   }
-  if (E > 0) {
+  if (E > 0 && !skip_general) {
     if (small_edges(E))
       hipLaunchKernelGGL(k_fill<4>, dim3((unsigned)((E + chunk_of(4) - 1) / chunk_of(4))),
                          dim3(kThreads), 0, s, edge_index, E, N, loops, rowptr, ws.fill, col,
@@ -1239,10 +1248,13 @@ static int graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loop
   const int64_t nfin = (N + kFinT - 1) / kFinT;
   dim3 fg((unsigned)((nfin + kFinWaves - 1) / kFinWaves), tptr ? 2u : 1u);
   // with tmap, the target side of k_finish also writes inv (edge id -> target-CSR position)
-  hipLaunchKernelGGL(k_finish, fg, dim3(kThreads), 0, s, N, E, add_loop, norm, rowptr, col,
-                     ws.eid, w, tptr, tidx, ws.teid, tw, ws.dis, ws.err, err_count, tile_open,
-                     lazy, tmap ? ws.inv : nullptr, try_sorted ? ws.verdict + kVerdictMax : nullptr);
-  LGNN_LAUNCH_CHECK();
+  if (!skip_general) {
+    hipLaunchKernelGGL(k_finish, fg, dim3(kThreads), 0, s, N, E, add_loop, norm, rowptr, col,
+                       ws.eid, w, tptr, tidx, ws.teid, tw, ws.dis, ws.err, err_count, tile_open,
+                       lazy, tmap ? ws.inv : nullptr,
+                       try_sorted ? ws.verdict + kVerdictMax : nullptr);
+    LGNN_LAUNCH_CHECK();
+  }
   if (tmap) {
     const int g = grid_for(E + N, 2048);
     hipLaunchKernelGGL(k_tmap, dim3(g), dim3(kThreads), 0, s, tptr, N, ws.teid, ws.inv, tmap);

@@ -99,9 +99,9 @@ class TransformConfig:
 def get_transform(config: TransformConfig):
     """Reference transforms.py:19-23: GaussianDistance by name, otherwise the
     torch_geometric.transforms class of that name. The graph-building transforms the reference
-    configs use run on the GPU here (KNNGraph, GaussianDistance); ToSparseTensor is accepted
-    (the models take either input form); any other PyG transform is outside the hot path and
-    raises."""
+    configs and sweep use run on the GPU here (KNNGraph, RadiusGraph — sweep.py:105-118 —,
+    GaussianDistance); ToSparseTensor is accepted (the models take either input form); any other
+    PyG transform is outside the hot path and raises."""
     kw = dict(config.kwargs)
     if config.name == "GaussianDistance":
         return GaussianDistance(**kw)
@@ -109,9 +109,13 @@ def get_transform(config: TransformConfig):
         from .knn import KNNGraph
 
         return KNNGraph(**kw)
+    if config.name == "RadiusGraph":
+        from .knn import RadiusGraph
+
+        return RadiusGraph(**kw)
     if config.name == "ToSparseTensor":
         from .datasets.datamodule import ToSparseTensor
 
         return ToSparseTensor()
     raise NotImplementedError(f"transform {config.name!r} is not part of this package (the "
-                              "reference configs use KNNGraph and GaussianDistance)")
+                              "reference configs use KNNGraph, RadiusGraph and GaussianDistance)")

@@ -138,6 +138,41 @@ def knn_graph(pos: Tensor, k: int, loop: bool = True) -> Tensor:
     return torch.tensor([rows, cols], dtype=torch.long).view(2, -1)
 
 
+def radius_graph(pos: Tensor, r: float, loop: bool = False, max_num_neighbors: int = 32) -> Tensor:
+    """torch_cluster.radius_graph for ONE graph, flow='source_to_target' (torch_cluster 1.6.3 —
+    not under /root/reference; the reference sweep builds it through PyG's RadiusGraph(r),
+    scripts/sweep.py:113-118, defaults loop=False, max_num_neighbors=32).
+
+    radius_graph calls radius(x, x, r, limit = max_num_neighbors (+ 1 without loop)); radius
+    walks each query's candidates in INDEX order and takes c when the squared distance < r * r
+    (strict), stopping at `limit` (the CUDA kernel radius_cuda.cu; the CPU path's nanoflann search
+    with sorted=False keeps a traversal-order subset when more than `limit` are in range — that
+    case is parity-unpinned and this restatement follows the CUDA rule); without loop the self
+    pair is dropped afterwards, so up to max_num_neighbors + 1 neighbours can remain. Returns
+    [2, E] = [neighbour (source), query (target)], grouped by query, neighbours ascending.
+    Squared distances: ((p_q - p_c) ** 2).sum(-1) in fp64."""
+    n = pos.size(0)
+    if n == 0:
+        return torch.empty(2, 0, dtype=torch.long)
+    pos = pos.to(torch.float64)
+    d = ((pos[:, None, :] - pos[None, :, :]) ** 2).sum(-1)  # [query, cand]
+    r2 = float(r) * float(r)
+    limit = max_num_neighbors if loop else max_num_neighbors + 1
+    inr = d < r2
+    taken = inr & (torch.cumsum(inr.to(torch.int64), 1) <= limit)  # first `limit` in index order
+    if not loop:
+        taken &= ~torch.eye(n, dtype=torch.bool)
+    q, c = torch.nonzero(taken, as_tuple=True)  # row-major: grouped by query, c ascending
+    return torch.stack([c, q]).to(torch.long)
+
+
+def radius_graph_batch(pos: Tensor, r: float, ptr: list[int], loop: bool = False,
+                       max_num_neighbors: int = 32) -> Tensor:
+    """radius_graph per graph of a collated batch (node offsets `ptr`), concatenated."""
+    parts = [radius_graph(pos[a:b], r, loop, max_num_neighbors) + a for a, b in pairwise(ptr)]
+    return torch.cat(parts, 1) if parts else torch.empty(2, 0, dtype=torch.long)
+
+
 def collate(graphs: list[dict]) -> dict:
     """PyG Batch.from_data_list for graphs {'x', 'edge_index', 'y'}: concat x, offset edges,
     build batch (graph id per node) and ptr."""

@@ -132,11 +132,11 @@ def test_reference_config_gat_dropout_training_step(cuda, compiled):
         _check(seen[0], go, logits.detach(), gr, 1e-4)
         torch.testing.assert_close(seen[0].squeeze(1).clamp(0, 4),
                                    logits.detach().squeeze(1).clamp(0, 4), rtol=0, atol=1e-4)
-    # dropout changed the result: the same step without masks differs
+    # dropout changed the result: the same forward without masks gives other logits (the
+    # clamped MSE itself can barely move when most predictions sit at a clamp bound)
     with torch.no_grad():
-        plain = ref.criterion("MSE", oref.eval()(b.x, b.edge_index, b.batch, b.num_graphs),
-                              b.y, 5)
-    assert abs(plain.item() - want.item()) > 1e-4
+        plain = oref.eval()(b.x, b.edge_index, b.batch, b.num_graphs)
+    assert (plain - logits.detach()).abs().max().item() > 1e-3
 
 
 @pytest.mark.parametrize("precision,heads,tol", [("fp32", 2, 1e-4), ("bf16", 4, 1e-3)])

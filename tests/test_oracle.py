@@ -169,3 +169,51 @@ def test_extract_features_by_cc_known_answer():
     mx = ref.extract_features_by_cc(cc, feats, 2, "max")
     assert torch.equal(mx, torch.tensor([[3., 7.], [2., 6.]]))
     assert torch.equal(ref.extract_features_by_cc(cc, feats, 1), feats.mean((2, 3)))
+
+
+def _radius_loop(pos, r, loop, max_nb):
+    """torch_cluster 1.6.3 radius_cuda.cu's per-query walk, literally (one graph): candidates in
+    index order, taken while the squared distance < r * r, at most `limit`; radius_graph then
+    swaps to (source, target) and drops the self pair without loop."""
+    n = pos.size(0)
+    limit = max_nb if loop else max_nb + 1
+    rows, cols = [], []
+    for q in range(n):
+        count = 0
+        for c in range(n):
+            d = float(((pos[q] - pos[c]) ** 2).sum())
+            if d < r * r:
+                if loop or c != q:
+                    rows.append(c)
+                    cols.append(q)
+                count += 1
+            if count >= limit:
+                break
+    return torch.tensor([rows, cols], dtype=torch.long).view(2, -1)
+
+
+@pytest.mark.parametrize("seed,n,r,loop,max_nb", [(0, 40, 0.3, False, 32), (1, 90, 0.5, False, 8),
+                                                 (2, 50, 0.2, True, 32), (3, 7, 10.0, True, 3),
+                                                 (4, 1, 1.0, False, 32), (5, 64, 0.0, False, 32)])
+def test_radius_graph_oracle_matches_literal_walk(seed, n, r, loop, max_nb):
+    g = torch.Generator().manual_seed(seed)
+    pos = torch.rand(n, 2, generator=g, dtype=torch.float64)
+    assert torch.equal(ref.radius_graph(pos, r, loop, max_nb), _radius_loop(pos, r, loop, max_nb))
+
+
+def test_radius_graph_known_answers():
+    """Points on a line at 0..9: r = 1.5 links neighbours at distance 1 only; r = 1 links nothing
+    (the comparison is strict); 40 coincident points with the default cap (32, no loop): the walk
+    takes the first 33 in index order, so nodes 0..32 keep 32 neighbours (their self pair was
+    among the 33 and is dropped) and nodes 33..39 keep 33 (torch_cluster's behaviour)."""
+    line = torch.stack([torch.arange(10, dtype=torch.float64), torch.zeros(10, dtype=torch.float64)], 1)
+    ei = ref.radius_graph(line, 1.5)
+    want = sorted([(q - 1, q) for q in range(1, 10)] + [(q + 1, q) for q in range(9)],
+                  key=lambda e: (e[1], e[0]))
+    assert ei.t().tolist() == [list(e) for e in want]
+    assert ref.radius_graph(line, 1.0).numel() == 0
+    same = torch.zeros(40, 2, dtype=torch.float64)
+    ei = ref.radius_graph(same, 1.0)
+    cnt = torch.bincount(ei[1], minlength=40)
+    assert cnt.tolist() == [32] * 33 + [33] * 7
+    assert ei[0][ei[1] == 35].tolist() == list(range(33))  # the first 33 in index order
