@@ -290,21 +290,32 @@ def time_dominant_kernels(model, b, dev):
                   csr.col.data_ptr(), csr.w.data_ptr(), L, planes_f.data_ptr(), bp,
                   (ctypes.c_int * (L + 1))(*widths[1:]), Hp, open_.data_ptr(), _lib.ptr(adjt), s)
 
-        # the step's launch: the _all entry with the logits gradient (dP = dlogits W_out formed
-        # in the kernel's prologue, the dZ_L product), as ops.stack_bwd runs it in the step
+        # the step's launch: the CE entry (the model + criterion node, ops.gcn_stack_ce): the
+        # logits gradient formed per graph in the prologue from the CE forward's values, then
+        # dP = dlogits W_out as the dZ_L product — as ops.stack_bwd runs it in the step
         W_out = model.out_proj.weight.detach()
-        dlog = torch.randn(b.num_graphs, W_out.size(0), device=dev)
+        C = W_out.size(0)
+        z = torch.randn(b.num_graphs, C, device=dev)
+        y = b.y.to(dev)
+        lse = torch.empty(b.num_graphs, device=dev)
+        ce_out = torch.empty(2, device=dev)
+        bad = torch.empty(1, dtype=torch.int32, device=dev)
+        gloss = torch.ones(1, device=dev)
+        _lib.call("lgnn_ce_fwd", z.data_ptr(), y.data_ptr(), None, b.num_graphs, C,
+                  lse.data_ptr(), ce_out.data_ptr(), ce_out.data_ptr() + 4, bad.data_ptr(), s)
+        ce = _lib.CeSrc(z.data_ptr(), lse.data_ptr(), y.data_ptr(), None, ce_out.data_ptr() + 4,
+                        gloss.data_ptr())
         dS_ws = torch.empty(2 * M * 128, dtype=torch.float32, device=dev)
         Sp = (ctypes.c_void_p * L)(*[x.data_ptr() for x in hs[1:]])  # open tiles only (none)
 
         def bwd_s3f():
-            _lib.call("lgnn_gcn_stack_bwd_s3f_all", None, g.batch.data_ptr(),
+            _lib.call("lgnn_gcn_stack_bwd_s3f_ce", g.batch.data_ptr(),
                       g.gptr.data_ptr(), 1, b.num_graphs, csr.rowptr.data_ptr(),
                       csr.col.data_ptr(), csr.w.data_ptr(), csr.tptr.data_ptr(),
                       csr.tidx.data_ptr(), csr.tw.data_ptr(), b.x.data_ptr(), M, L,
                       planes_t.data_ptr(), Wp, Hp, Sp, (ctypes.c_int * (L + 2))(*widths), dWp,
-                      dbp, P, dS_ws.data_ptr(), open_.data_ptr(), dlog.data_ptr(),
-                      W_out.data_ptr(), W_out.size(0), _lib.ptr(adjt), s)
+                      dbp, P, dS_ws.data_ptr(), open_.data_ptr(), ctypes.byref(ce),
+                      W_out.data_ptr(), C, _lib.ptr(adjt), s)
 
         out.append({"kernel": f"lgnn_s3::k_s3_fbwd<{L + 1}, {str(ops.ADJT).lower()}> (fused GCN "
                               "backward, all layers, "
@@ -907,8 +918,13 @@ def main():
 
     one = torch.ones((), device=dev)  # the loss gradient, allocated once (no fill per step)
 
+    fused_ce = wl["loss"] == "CE" and hasattr(run, "forward_loss") and not wl.get("compile")
+
     def fwd_bwd():
-        loss_fn(wl, run(b.x, b.edge_index, b.batch, B), b.y).backward(one)
+        if fused_ce:  # model + criterion as one node (GCN.forward_loss = training_step's pair)
+            run.forward_loss(b.x, b.edge_index, b.batch, b.y, None, B)[1].backward(one)
+        else:
+            loss_fn(wl, run(b.x, b.edge_index, b.batch, B), b.y).backward(one)
 
     # GIN under SyncBN all-reduces inside its forward and backward (RCCL collectives)
     plan = step_plan(2 if multi else 1, bool(args.graph), sync_bn)
@@ -942,6 +958,8 @@ def main():
         "data": "synthetic k-NN lesion graphs (pos~U[0,1)^2, x~N(0,1)), random-init weights",
         "config": {"workload": wl["desc"], "name": args.workload,
                    "step_launch": " | ".join(plan),
+                   "criterion": "CE fused with the model node (forward_loss)" if fused_ce else
+                   ("CE (ops.cross_entropy)" if wl["loss"] == "CE" else "clamp + MSE"),
                    "sync_bn": sync_bn, "process_group": multi,
                    "adam": args.opt, "graphs_per_gpu": B, "global_batch": B * world,
                    "nodes": b.num_nodes, "edges": b.num_edges, "k": wl["k"], "d_in": wl["d_in"],

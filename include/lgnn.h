@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 32
+#define LGNN_ABI_VERSION 33
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -531,6 +531,24 @@ int lgnn_ce_fwd(const float* logits, const int64_t* target, const float* weight,
 int lgnn_ce_bwd(const float* logits, const int64_t* target, const float* weight, int64_t B, int C,
                 const float* lse, const float* wsum, const float* grad_loss, float* dlogits,
                 void* stream);
+/* The CE logits gradient without materialising it (ABI v33): the consumers form
+ * lgnn_ce_bwd's dlogits[i][c] themselves, bit for bit, from the forward's saved values.
+ * lgnn_reduce_jobs_ce = lgnn_reduce_jobs where jobs with ce_job[j] != 0 take the [P][C] logits
+ * gradient (P = B) in place of partials[j] (which may be NULL): out_proj's db (len C) and
+ * dW = dlogits^T pooled (factor = pooled, len C * width). The same sums as lgnn_reduce_jobs on
+ * lgnn_ce_bwd's output, bitwise. */
+typedef struct lgnn_ce_src {
+  const float* logits;   /* [B][C] */
+  const float* lse;      /* [B] (lgnn_ce_fwd) */
+  const int64_t* target; /* [B] */
+  const float* weight;   /* [C] class weights or NULL */
+  const float* wsum;     /* [1] (lgnn_ce_fwd) */
+  const float* gloss;    /* [1] gradient of the loss */
+} lgnn_ce_src;
+int lgnn_reduce_jobs_ce(int n, const float* const* partials, const float* const* factor,
+                        const int* width, const int* num_partials, const int64_t* len,
+                        float* const* out, const int* ce_job, const lgnn_ce_src* ce,
+                        int num_classes, void* stream);
 /* Regression head + criterion (ABI v23): pred = clamp(z, lo, hi) (reference gat.py:94-95,
  * gin.py:66-67: logits.squeeze(1).clamp(0, C - 1)) and loss = mean l(pred - y) with
  * l = nn.MSELoss (smooth_l1 = 0) or nn.SmoothL1Loss(beta = 1) (models/base.py:95-96), one
@@ -646,6 +664,21 @@ int lgnn_gcn_stack_bwd_s3f_all(const float* dP, const int64_t* batch, const int3
                                float* dS_ws, int32_t* tile_open, const float* dlogits,
                                const float* Wout, int num_classes, const void* adjt,
                                void* stream);
+/* lgnn_gcn_stack_bwd_s3f_all with the logits gradient formed in the kernel from the CE forward
+ * (ABI v33: lgnn_ce_src, declared with lgnn_ce_fwd below): the model + criterion backward without
+ * a dlogits tensor or the lgnn_ce_bwd launch (reference models/base.py:93-94 + :196-201). The
+ * same arithmetic as lgnn_ce_bwd followed by lgnn_gcn_stack_bwd_s3f_all, bitwise. */
+struct lgnn_ce_src;
+int lgnn_gcn_stack_bwd_s3f_ce(const int64_t* batch, const int32_t* gptr, int pool_mean,
+                              int64_t num_graphs, const int32_t* rowptr, const int32_t* col,
+                              const float* w, const int32_t* tptr, const int32_t* tidx,
+                              const float* tw, const float* X, int64_t M, int L,
+                              const uint16_t* planes_t, const float* const* W,
+                              const float* const* H, const float* const* S, const int* widths,
+                              float* const* dWp, float* const* dbp, int num_partials,
+                              float* dS_ws, int32_t* tile_open, const struct lgnn_ce_src* ce,
+                              const float* Wout, int num_classes, const void* adjt,
+                              void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Dense GEMMs at fp32 accuracy on bf16 MFMA ("split-3"), any width. Replace: the plain

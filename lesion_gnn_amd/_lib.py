@@ -32,6 +32,13 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 SZ = ctypes.c_size_t
 
+
+class CeSrc(ctypes.Structure):
+    """lgnn_ce_src (include/lgnn.h): the CE forward's values its logits gradient is formed from."""
+    _fields_ = [("logits", P), ("lse", P), ("target", P), ("weight", P), ("wsum", P),
+                ("gloss", P)]
+
+
 # name -> (restype, argtypes); mirrors include/lgnn.h exactly
 SIGNATURES: dict[str, tuple] = {
     "lgnn_abi_version": (I32, []),
@@ -60,6 +67,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_spmm": (I32, [P, P, P, F32, P, I64, I32, P, P]),
     "lgnn_reduce_partials_multi": (I32, [I32, P, P, P, P, P]),
     "lgnn_reduce_jobs": (I32, [I32, P, P, P, P, P, P, P]),
+    "lgnn_reduce_jobs_ce": (I32, [I32, P, P, P, P, P, P, P, ctypes.POINTER(CeSrc), I32, P]),
     "lgnn_ce_fwd": (I32, [P, P, P, I64, I32, P, P, P, P, P]),
     "lgnn_ce_bwd": (I32, [P, P, P, I64, I32, P, P, P, P, P]),
     "lgnn_pool_head_fwd": (I32, [P, P, I64, I32, I32, P, P, I32, P, P, P]),
@@ -128,6 +136,8 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_gcn_stack_fwd_s3_all": (I32, [P, I64, I32, I32, P, P, P, I32, P, P, P, P, P, P, P, P, P]),
     "lgnn_gcn_stack_bwd_s3f_all": (I32, [P, P, P, I32, I64, P, P, P, P, P, P, P, I64, I32, P, P, P,
                                          P, P, P, P, I32, P, P, P, P, I32, P, P]),
+    "lgnn_gcn_stack_bwd_s3f_ce": (I32, [P, P, I32, I64, P, P, P, P, P, P, P, I64, I32, P, P, P, P,
+                                        P, P, P, I32, P, P, ctypes.POINTER(CeSrc), P, I32, P, P]),
     "lgnn_fused_grid_capacity": (I32, [I32]),
     "lgnn_dropout_masks": (I32, [I32, P, P, P, P, P, I32, P]),
     "lgnn_s3_weight_planes_numel": (SZ, [I32, I32, I32]),
@@ -145,7 +155,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 32
+ABI_VERSION = 33
 
 _lib = None
 

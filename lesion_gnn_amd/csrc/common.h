@@ -97,5 +97,24 @@ __device__ __forceinline__ unsigned int ticket_after(unsigned int dep) {
   return one;
 }
 
+// nn.CrossEntropyLoss(weight) (mean reduction) logits gradient formed where it is consumed, from
+// the forward's saved values (lgnn_ce_fwd: lse, wsum) — k_ce_bwd's expression, bit for bit:
+//   dz[i][c] = gloss * w[y_i] / wsum * (exp(z[i][c] - lse[i]) - [c == y_i])
+struct CeSrc {
+  const float* z;      // [B][C] logits
+  const float* lse;    // [B]
+  const int64_t* y;    // [B] targets
+  const float* w;      // [C] class weights or nullptr
+  const float* wsum;   // [1]
+  const float* gloss;  // [1]
+  int C;
+};
+__device__ __forceinline__ float ce_dlogit(const CeSrc& s, int64_t i, int c) {
+  const int64_t t = s.y[i];
+  const float wt = (t >= 0 && t < s.C) ? (s.w ? s.w[t] : 1.f) : 0.f;
+  const float p = expf(s.z[i * s.C + c] - s.lse[i]);
+  return s.gloss[0] * wt / s.wsum[0] * (p - (c == t ? 1.f : 0.f));
+}
+
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }

@@ -774,8 +774,8 @@ __device__ __forceinline__ void finish_body(int64_t N, int64_t E, int add_loop, 
                                             const int32_t* __restrict__ ws_err, int32_t* err_out,
                                             int32_t* tile_open, int lazy,
                                             int32_t* __restrict__ inv, int32_t* s_key,
-                                            int32_t* s_val, int64_t bx, int by, int tid,
-                                            Sync sync) {
+                                            int32_t* s_val, int32_t* s_ptr, int64_t bx, int by,
+                                            int tid, Sync sync) {
   if (lazy && by == 1 && tile_open[(N + 63) >> 6] == 0) return;  // no source CSR needed
   if (err_out && bx == 0 && by == 0 && tid == 0) *err_out = *ws_err;
   const bool tr = by == 1;
@@ -820,6 +820,39 @@ __device__ __forceinline__ void finish_body(int64_t N, int64_t E, int add_loop, 
     }
   } else if (inv && !tr && i < N) {
     for (int j = ptr[i]; j < ptr[i + 1]; ++j) inv[key[j]] = j;
+  }
+  if (staged) {
+    // entry-parallel passes (weights, tile marks): lane t takes entries eb + t, + kFinT, ... —
+    // coalesced stores and independent loads (a per-row walk chained 17 dependent gathers per
+    // lane at C5 k = 16); the row of an entry by binary search over the block's row starts
+    s_ptr[tid] = i < N ? ptr[i] : ee;
+    if (tid == 0) s_ptr[kFinT] = ee;
+    sync();
+    const int nrows = (int)(iend - i0);
+    // lazy builds took the tile marks in k_count (cross edges) and k_scan (capacity)
+    const bool marks = tile_open && !tr && !lazy;
+    const int64_t ntiles = (N + 63) >> 6;
+    for (int j = eb + tid; j < ee; j += kFinT) {
+      int lo = 0, hi = nrows - 1;  // largest r with s_ptr[r] <= j (empty rows share a start)
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_ptr[mid] <= j) lo = mid;
+        else hi = mid - 1;
+      }
+      const int64_t row = i0 + lo;
+      const int nb = s_val[j - eb];
+      if (wt) wt[j] = norm == LGNN_NORM_GCN ? (dis[nb] * 1.0f) * dis[row] : 1.0f;
+      if (marks && (nb >> 6) != (row >> 6)) {
+        if (tile_open[row >> 6] == 0) mark_open(tile_open, row >> 6, ntiles);
+        if (tile_open[nb >> 6] == 0) mark_open(tile_open, nb >> 6, ntiles);
+      }
+    }
+    if (marks && i < N && (i & 63) == 0) {
+      const int64_t iend64 = i + 64 < N ? i + 64 : N;
+      if (ptr[iend64] - ptr[i] > 1024) mark_open(tile_open, i >> 6, ntiles);
+    }
+    sync();  // the staging arrays are free for the next virtual block
+    return;
   }
   if (wt) {
     // row of each entry: binary search is avoided by a per-thread row walk (rows are short)
@@ -889,12 +922,13 @@ __global__ __launch_bounds__(kThreads) void k_finish(int64_t N, int64_t E, int a
                                                      const int32_t* summary) {
   __shared__ int32_t s_key[kFinWaves][kFinishCap];
   __shared__ int32_t s_val[kFinWaves][kFinishCap];
+  __shared__ int32_t s_ptr[kFinWaves][kFinT + 1];
   if (summary && __builtin_amdgcn_readfirstlane(*summary)) return;  // sorted path took it
   const int wave = threadIdx.x >> 6;
   const int64_t v = (int64_t)blockIdx.x * kFinWaves + wave;
   if (v * kFinT >= N) return;
   finish_body(N, E, add_loop, norm, rowptr, col, eid, w, tptr, tidx, teid, tw, dis, ws_err,
-              err_out, tile_open, lazy, inv, s_key[wave], s_val[wave], v, blockIdx.y,
+              err_out, tile_open, lazy, inv, s_key[wave], s_val[wave], s_ptr[wave], v, blockIdx.y,
               threadIdx.x & 63, WaveSync{});
 }
 
@@ -937,6 +971,7 @@ union BuildSmem {
   struct {
     int32_t key[kThreads / 64][kFinishCap];
     int32_t val[kThreads / 64][kFinishCap];
+    int32_t ptr[kThreads / 64][kFinT + 1];
   } fin;
 };
 
@@ -981,7 +1016,7 @@ __global__ __launch_bounds__(kThreads) void k_build(BuildArgs a, int32_t* sync) 
          v += (int64_t)G * (kThreads / 64))
       finish_body(N, E, a.add_loop, a.norm, a.rowptr, a.col, a.ws.eid, a.w, a.tptr, a.tidx,
                   a.ws.teid, a.tw, a.ws.dis, a.ws.err, a.err_count, a.tile_open, a.lazy,
-                  a.tmap ? a.ws.inv : nullptr, sm.fin.key[wave], sm.fin.val[wave], v % nfin,
+                  a.tmap ? a.ws.inv : nullptr, sm.fin.key[wave], sm.fin.val[wave], sm.fin.ptr[wave], v % nfin,
                   (int)(v / nfin), lane, WaveSync{});
   }
   if (a.tmap) {

@@ -73,10 +73,8 @@ __global__ __launch_bounds__(256) void k_ce_bwd(const float* __restrict__ z,
   if (idx >= B * C) return;
   const int64_t i = idx / C;
   const int c = (int)(idx % C);
-  const int64_t t = y[i];
-  const float wt = (t >= 0 && t < C) ? (weight ? weight[t] : 1.f) : 0.f;
-  const float p = expf(z[idx] - lse[i]);
-  dz[idx] = gloss[0] * wt / wsum[0] * (p - (c == t ? 1.f : 0.f));
+  const CeSrc ce{z, lse, y, weight, wsum, gloss, C};
+  dz[idx] = ce_dlogit(ce, i, c);
 }
 
 // Regression head + criterion (reference gat.py:94-95 / gin.py:66-67: logits.squeeze(1).clamp(0,
@@ -133,6 +131,8 @@ __global__ __launch_bounds__(256) void k_reg_bwd(const float* __restrict__ z,
 // with a factor (outer-product job): out_j[c * width_j + d] =
 //   sum_p part_j[p * (len_j / width_j) + c] * factor_j[p * width_j + d]
 struct ReduceJobs {
+  CeSrc ce;                    // ce_part jobs: part[p][c] = the CE logits gradient (ce_dlogit)
+  int ce_part[LGNN_MAX_REDUCE];
   const float* part[LGNN_MAX_REDUCE];
   const float* factor[LGNN_MAX_REDUCE];
   float* out[LGNN_MAX_REDUCE];
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(RT) void k_reduce_multi(ReduceJobs jobs) {
   const int64_t len = jobs.len[j];
   // long plain jobs (the dW slabs) take 16-B loads: 4 columns per lane, 256 per block, the same
   // slot order per column (bitwise the scalar path's sums)
-  const bool vec = !jobs.factor[j] && (len & 3) == 0 && len >= 4096;
+  const bool vec = !jobs.factor[j] && !jobs.ce_part[j] && (len & 3) == 0 && len >= 4096;
   if ((int64_t)blockIdx.x * (vec ? 256 : 64) >= len) return;
   const float* __restrict__ part = jobs.part[j];
   int P = jobs.P[j];
@@ -181,7 +181,36 @@ __global__ __launch_bounds__(RT) void k_reduce_multi(ReduceJobs jobs) {
   const int64_t ic = i < len ? i : len - 1;
   float s = 0.f;
   int p = wave;
-  if (const float* __restrict__ f = jobs.factor[j]) {  // sum_p part[p][c] * f[p][d]
+  if (jobs.ce_part[j]) {  // part = the CE logits gradient [P][C], formed here (no dlogits)
+    const CeSrc& ce = jobs.ce;
+    // the slot order of the materialised-part paths (p = wave, wave + 16, ...), 16 slots'
+    // gradients formed (their loads in flight) before they are summed in order
+    if (const float* __restrict__ f = jobs.factor[j]) {  // sum_p dz[p][c] * f[p][d]
+      const int width = jobs.width[j];
+      const int64_t c = ic / width, d = ic % width;
+      for (; p + 16 * 15 < P; p += 16 * 16) {
+        float av[16], fv[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          av[u] = ce_dlogit(ce, p + 16 * u, (int)c);
+          fv[u] = f[(int64_t)(p + 16 * u) * width + d];
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) s = fmaf(av[u], fv[u], s);
+      }
+      for (; p < P; p += 16) s = fmaf(ce_dlogit(ce, p, (int)c), f[(int64_t)p * width + d], s);
+    } else {
+      for (; p + 16 * 15 < P; p += 16 * 16) {
+        float av[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) av[u] = ce_dlogit(ce, p + 16 * u, (int)ic);
+#pragma unroll
+        for (int u = 0; u < 16; ++u) s += av[u];
+      }
+      for (; p < P; p += 16) s += ce_dlogit(ce, p, (int)ic);
+    }
+    P = 0;  // fall through to the fixed-order wave fold
+  } else if (const float* __restrict__ f = jobs.factor[j]) {  // sum_p part[p][c] * f[p][d]
     const int width = jobs.width[j];
     const int64_t rows = len / width, c = ic / width, d = ic % width;
     for (; p + 16 * 31 < P; p += 16 * 32) {  // 64 loads in flight per lane (latency bound:
@@ -298,15 +327,28 @@ extern "C" int lgnn_reduce_partials_multi(int n, const float* const* partials,
   return lgnn_reduce_jobs(n, partials, nullptr, nullptr, num_partials, len, out, stream);
 }
 
-extern "C" int lgnn_reduce_jobs(int n, const float* const* partials, const float* const* factor,
-                                const int* width, const int* num_partials, const int64_t* len,
-                                float* const* out, void* stream) {
+static int reduce_jobs(int n, const float* const* partials, const float* const* factor,
+                       const int* width, const int* num_partials, const int64_t* len,
+                       float* const* out, const int* ce_job, const lgnn_ce_src* ce, int C,
+                       void* stream) {
   if (n <= 0 || n > LGNN_MAX_REDUCE || !partials || !num_partials || !len || !out)
     return LGNN_EINVAL;
   ReduceJobs jobs = {};
+  if (ce_job) {
+    if (!ce || !ce->logits || !ce->lse || !ce->target || !ce->wsum || !ce->gloss || C < 1)
+      return LGNN_EINVAL;
+    jobs.ce = CeSrc{ce->logits, ce->lse, ce->target, ce->weight, ce->wsum, ce->gloss, C};
+  }
   int64_t maxlen = 0;
   for (int j = 0; j < n; ++j) {
-    if (!partials[j] || !out[j] || num_partials[j] <= 0 || len[j] < 0) return LGNN_EINVAL;
+    const bool cj = ce_job && ce_job[j];
+    if ((!partials[j] && !cj) || !out[j] || num_partials[j] <= 0 || len[j] < 0)
+      return LGNN_EINVAL;
+    if (cj) {  // the [P][C] logits gradient: len = C (db) or C * width (outer product)
+      const int64_t rows = factor && factor[j] && width ? len[j] / width[j] : len[j];
+      if (rows != C) return LGNN_EINVAL;
+      jobs.ce_part[j] = 1;
+    }
     if (factor && factor[j]) {
       if (!width || width[j] <= 0 || len[j] % width[j] != 0) return LGNN_EINVAL;
       jobs.factor[j] = factor[j];
@@ -323,4 +365,21 @@ extern "C" int lgnn_reduce_jobs(int n, const float* const* partials, const float
                      0, as_stream(stream), jobs);
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
+}
+
+extern "C" int lgnn_reduce_jobs(int n, const float* const* partials, const float* const* factor,
+                                const int* width, const int* num_partials, const int64_t* len,
+                                float* const* out, void* stream) {
+  return reduce_jobs(n, partials, factor, width, num_partials, len, out, nullptr, nullptr, 0,
+                     stream);
+}
+
+extern "C" int lgnn_reduce_jobs_ce(int n, const float* const* partials,
+                                   const float* const* factor, const int* width,
+                                   const int* num_partials, const int64_t* len,
+                                   float* const* out, const int* ce_job, const lgnn_ce_src* ce,
+                                   int num_classes, void* stream) {
+  if (!ce_job) return LGNN_EINVAL;
+  return reduce_jobs(n, partials, factor, width, num_partials, len, out, ce_job, ce, num_classes,
+                     stream);
 }

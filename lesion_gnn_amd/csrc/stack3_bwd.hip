@@ -498,6 +498,7 @@ namespace lgnn_s3 {
 struct FBwdArgs {
   const float* dP;                // [B][N_L] pooled-output gradient (or formed from dlog / Wout)
   const float* dlog;              // [B][C] logits gradient (nullable): dP = dlog Wout on the fly
+  CeSrc ce;                       // or (ce.z set) the CE logits gradient, formed on the fly
   const float* Wout;              // [C][N_L]
   int C;
   const unsigned char* adjt;      // Â^T planes per tile from the forward (AG), or nullptr
@@ -528,6 +529,12 @@ struct OpenBwdArgs {
 };
 
 constexpr int kMaxHeadC = 8;  // classes for which dP is formed in the kernel
+
+// the logits gradient row of graph g: given (dlog) or formed from the CE forward (ce)
+__device__ __forceinline__ bool has_head(const FBwdArgs& a) { return a.dlog || a.ce.z; }
+__device__ __forceinline__ float head_dl(const FBwdArgs& a, int64_t g, int c) {
+  return a.ce.z ? ce_dlogit(a.ce, g, c) : a.dlog[g * a.C + c];
+}
 
 struct FBwdSmem {
   unsigned char Img[3][TM * AROW];  // 48 KiB: H_{l-1} (or X) feature-major [k][perm16 m]
@@ -641,7 +648,7 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
   // out_proj's W as the B operand of the dZ_L product (lane: feature n; K: class 8h + e; classes
   // past C, features past N_L and the h = 1 half read 0 through the buffer range), split once
   u32x4 wob[3] = {};
-  if (a.dlog) {
+  if (has_head(a)) {
     const int tq = fresh_tid();
     const int h = (tq >> 5) & 1, n = 32 * (tq >> 6) + (tq & 31);
     const Buf bW = mkbuf(a.Wout, (int64_t)a.C * NLast * 4);
@@ -666,9 +673,9 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
       if (tq < TM && row < M) {
         pre_g = a.batch[row];
         pre_cnt = a.gptr[pre_g + 1] - a.gptr[pre_g];
-        if (a.dlog) {
+        if (has_head(a)) {
 #pragma unroll
-          for (int c = 0; c < kMaxHeadC; ++c) pre_dl[c] = c < a.C ? a.dlog[pre_g * a.C + c] : 0.f;
+          for (int c = 0; c < kMaxHeadC; ++c) pre_dl[c] = c < a.C ? head_dl(a, pre_g, c) : 0.f;
         }
       }
     }
@@ -699,7 +706,7 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
         const float ps = row >= M ? 0.f : (a.pool_mean && cnt > 1 ? 1.f / (float)cnt : 1.f);
         sm.pg[tq] = (int)g;
         sm.pscale[tq] = ps;
-        if (a.dlog) {  // zero-padded to kMaxHeadC: the dZ_L loop below runs without branches
+        if (has_head(a)) {  // zero-padded to kMaxHeadC: the dZ_L loop below runs without branches
           float v[kMaxHeadC];
 #pragma unroll
           for (int c = 0; c < kMaxHeadC; ++c) v[c] = pre_dl[c] * ps;
@@ -711,6 +718,7 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
     // this tile's H_L rows (and, AG, its Â) were issued during the previous tile: landed
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();  // ... in every wave; the staging above is visible
+    STAMP(stamp++);
     if constexpr (!AG) {
       adj_scatter<true>(scr, sm.rp, R, r0);
       if (has_next) idx_load_head(R, rowptr, M, tn * TM);
@@ -728,7 +736,7 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
           const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
           hv[q][r] = (n < NLast && r0 + m < M) ? sm.hl[m * NLast + n] : 0.f;
         }
-      if (a.dlog) {
+      if (has_head(a)) {
         // dP[g(m)][n] / |g(m)| = sum_c dl[m][c] Wout[c][n] as ONE split-3 product per node half
         // (K = the <= 8 classes, zero-padded to 16): A = the staged dl rows (node on the lane:
         // two 16-B LDS reads per half instead of 32 rows x 8 classes per lane), B = out_proj's
@@ -763,6 +771,7 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
           }
       }
     }
+    STAMP(stamp++);
     if constexpr (AG) {
       // (every wave's Â loads landed before the barrier above)
       // Â^T planes: row am = source, positions perm16 of targets 16 aq .. (a wave reads 64
@@ -1063,10 +1072,10 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
           }
         (void)K;
         pre_cnt = (has_next && tq < TM) ? a.gptr[pre_g + 1] - a.gptr[pre_g] : 0;
-        if (a.dlog) {
+        if (has_head(a)) {
 #pragma unroll
           for (int c = 0; c < kMaxHeadC; ++c)
-            pre_dl[c] = (has_next && tq < TM && c < a.C) ? a.dlog[pre_g * a.C + c] : 0.f;
+            pre_dl[c] = (has_next && tq < TM && c < a.C) ? head_dl(a, pre_g, c) : 0.f;
         }
       }
       lds_barrier();
@@ -1127,7 +1136,7 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
         bwd_tiles<LGNN_GRAD_POOL, LGNN_ACT_ELU, true>(
             lw.A, lw.C, lw.ti, a.dP, a.batch, a.gptr, a.pool_mean, nullptr, nullptr, nullptr, 0.f,
             a.H[l], Sx, M, K, o.W[l], N, o.dS[l & 1], a.dWp[l], a.dbp[l], tmask, 1, 1, a.dlog,
-            a.Wout, a.C);
+            a.Wout, a.C, BnFuse{}, a.ce.z ? &a.ce : nullptr);
       else if (l >= 1)
         bwd_tiles<LGNN_GRAD_TRANSPOSE, LGNN_ACT_ELU, true>(
             lw.A, lw.C, lw.ti, o.dS[(l + 1) & 1], a.batch, a.gptr, a.pool_mean, o.tptr, o.tidx,
@@ -1305,9 +1314,9 @@ __global__ __launch_bounds__(NT8, 1) void k_s3_fbwd8(int64_t M, FBwdArgs a,
     if (tq < TM && row < M) {
       pre_g = a.batch[row];
       pre_cnt = a.gptr[pre_g + 1] - a.gptr[pre_g];
-      if (a.dlog) {
+      if (has_head(a)) {
 #pragma unroll
-        for (int c = 0; c < kMaxHeadC; ++c) pre_dl[c] = c < a.C ? a.dlog[pre_g * a.C + c] : 0.f;
+        for (int c = 0; c < kMaxHeadC; ++c) pre_dl[c] = c < a.C ? head_dl(a, pre_g, c) : 0.f;
       }
     }
   }
@@ -1325,7 +1334,7 @@ __global__ __launch_bounds__(NT8, 1) void k_s3_fbwd8(int64_t M, FBwdArgs a,
             row >= M ? 0.f : (a.pool_mean && pre_cnt > 1 ? 1.f / (float)pre_cnt : 1.f);
         sm.pg[tq] = (int)pre_g;
         sm.pscale[tq] = ps;
-        if (a.dlog) {
+        if (has_head(a)) {
           st4(&sm.dl[tq][0], f32x4{pre_dl[0] * ps, pre_dl[1] * ps, pre_dl[2] * ps, pre_dl[3] * ps});
           st4(&sm.dl[tq][4], f32x4{pre_dl[4] * ps, pre_dl[5] * ps, pre_dl[6] * ps, pre_dl[7] * ps});
         }
@@ -1339,7 +1348,7 @@ __global__ __launch_bounds__(NT8, 1) void k_s3_fbwd8(int64_t M, FBwdArgs a,
       const int tq = fresh_tid();
       const int h = (tq >> 5) & 1, n = 32 * nb + (tq & 31);
       float wo[kMaxHeadC];
-      if (a.dlog) {
+      if (has_head(a)) {
 #pragma unroll
         for (int c = 0; c < kMaxHeadC; ++c)
           wo[c] = (c < a.C && n < NLast) ? a.Wout[c * NLast + n] : 0.f;
@@ -1350,7 +1359,7 @@ __global__ __launch_bounds__(NT8, 1) void k_s3_fbwd8(int64_t M, FBwdArgs a,
           const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
           const float hv = (n < NLast && r0 + m < M) ? hl[m * NLast + n] : 0.f;
           float gv;
-          if (a.dlog) {
+          if (has_head(a)) {
             const f32x4 d0 = ld4(&sm.dl[m][0]), d1 = ld4(&sm.dl[m][4]);
             gv = d0[0] * wo[0];
 #pragma unroll
@@ -1580,10 +1589,10 @@ __global__ __launch_bounds__(NT8, 1) void k_s3_fbwd8(int64_t M, FBwdArgs a,
           for (int p = 0; p < 3; ++p) sts8(sm.Img[p] + off, ov[p]);
         }
         pre_cnt = (has_next && tq < TM) ? a.gptr[pre_g + 1] - a.gptr[pre_g] : 0;
-        if (a.dlog) {
+        if (has_head(a)) {
 #pragma unroll
           for (int c = 0; c < kMaxHeadC; ++c)
-            pre_dl[c] = (has_next && tq < TM && c < a.C) ? a.dlog[pre_g * a.C + c] : 0.f;
+            pre_dl[c] = (has_next && tq < TM && c < a.C) ? head_dl(a, pre_g, c) : 0.f;
         }
       }
       lds_barrier();
@@ -1647,7 +1656,7 @@ __global__ __launch_bounds__(NT8, 1) void k_s3_fbwd8(int64_t M, FBwdArgs a,
         bwd_tiles<LGNN_GRAD_POOL, LGNN_ACT_ELU, true>(
             lw.A, lw.C, lw.ti, a.dP, a.batch, a.gptr, a.pool_mean, nullptr, nullptr, nullptr, 0.f,
             a.H[l], Sx, M, K, o.W[l], N, o.dS[l & 1], a.dWp[l], a.dbp[l], tmask, 1, 1, a.dlog,
-            a.Wout, a.C);
+            a.Wout, a.C, BnFuse{}, a.ce.z ? &a.ce : nullptr);
       else if (l >= 1)
         bwd_tiles<LGNN_GRAD_TRANSPOSE, LGNN_ACT_ELU, true>(
             lw.A, lw.C, lw.ti, o.dS[(l + 1) & 1], a.batch, a.gptr, a.pool_mean, o.tptr, o.tidx,
@@ -1690,7 +1699,8 @@ static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* g
                          float* const* dWp, float* const* dbp, int num_partials,
                          const int32_t* tile_open, const lgnn_s3::OpenBwdArgs& o, void* stream,
                          const float* dlogits = nullptr, const float* Wout = nullptr,
-                         int num_classes = 0, const void* adjt = nullptr);
+                         int num_classes = 0, const void* adjt = nullptr,
+                         const lgnn_ce_src* ce = nullptr);
 
 extern "C" int lgnn_gcn_stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* gptr,
                                       int pool_mean, int64_t num_graphs, const int32_t* rowptr,
@@ -1705,17 +1715,17 @@ extern "C" int lgnn_gcn_stack_bwd_s3f(const float* dP, const int64_t* batch, con
                        0, adjt);
 }
 
-extern "C" int lgnn_gcn_stack_bwd_s3f_all(
+static int stack_bwd_s3f_all(
     const float* dP, const int64_t* batch, const int32_t* gptr, int pool_mean,
     int64_t num_graphs, const int32_t* rowptr, const int32_t* col, const float* w,
     const int32_t* tptr, const int32_t* tidx, const float* tw, const float* X, int64_t M, int L,
     const uint16_t* planes_t, const float* const* W, const float* const* H,
     const float* const* S, const int* widths, float* const* dWp, float* const* dbp,
-    int num_partials, float* dS_ws, int32_t* tile_open, const float* dlogits, const float* Wout,
-    int num_classes, const void* adjt, void* stream) {
+    int num_partials, float* dS_ws, int32_t* tile_open, const float* dlogits,
+    const lgnn_ce_src* ce, const float* Wout, int num_classes, const void* adjt, void* stream) {
   if (M < 0 || L < 1 || L > 2 || !W || !S || !tptr || !tidx || !tw || !dS_ws || !tile_open)
     return LGNN_EINVAL;
-  if (dlogits && (!Wout || num_classes < 1 || num_classes > lgnn_s3::kMaxHeadC))
+  if ((dlogits || ce) && (!Wout || num_classes < 1 || num_classes > lgnn_s3::kMaxHeadC))
     return LGNN_EINVAL;
   lgnn_s3::OpenBwdArgs o = {};
   for (int l = 0; l <= L; ++l) {
@@ -1732,7 +1742,34 @@ extern "C" int lgnn_gcn_stack_bwd_s3f_all(
   o.sync = tile_open + ntiles + 4;
   return stack_bwd_s3f(dP, batch, gptr, pool_mean, num_graphs, rowptr, col, w, X, M, L, planes_t,
                        H, widths, dWp, dbp, num_partials, tile_open, o, stream, dlogits, Wout,
-                       num_classes, adjt);
+                       num_classes, adjt, ce);
+}
+
+extern "C" int lgnn_gcn_stack_bwd_s3f_all(
+    const float* dP, const int64_t* batch, const int32_t* gptr, int pool_mean,
+    int64_t num_graphs, const int32_t* rowptr, const int32_t* col, const float* w,
+    const int32_t* tptr, const int32_t* tidx, const float* tw, const float* X, int64_t M, int L,
+    const uint16_t* planes_t, const float* const* W, const float* const* H,
+    const float* const* S, const int* widths, float* const* dWp, float* const* dbp,
+    int num_partials, float* dS_ws, int32_t* tile_open, const float* dlogits, const float* Wout,
+    int num_classes, const void* adjt, void* stream) {
+  return stack_bwd_s3f_all(dP, batch, gptr, pool_mean, num_graphs, rowptr, col, w, tptr, tidx, tw,
+                           X, M, L, planes_t, W, H, S, widths, dWp, dbp, num_partials, dS_ws,
+                           tile_open, dlogits, nullptr, Wout, num_classes, adjt, stream);
+}
+
+extern "C" int lgnn_gcn_stack_bwd_s3f_ce(
+    const int64_t* batch, const int32_t* gptr, int pool_mean, int64_t num_graphs,
+    const int32_t* rowptr, const int32_t* col, const float* w, const int32_t* tptr,
+    const int32_t* tidx, const float* tw, const float* X, int64_t M, int L,
+    const uint16_t* planes_t, const float* const* W, const float* const* H,
+    const float* const* S, const int* widths, float* const* dWp, float* const* dbp,
+    int num_partials, float* dS_ws, int32_t* tile_open, const struct lgnn_ce_src* ce,
+    const float* Wout, int num_classes, const void* adjt, void* stream) {
+  if (!ce) return LGNN_EINVAL;
+  return stack_bwd_s3f_all(nullptr, batch, gptr, pool_mean, num_graphs, rowptr, col, w, tptr, tidx,
+                           tw, X, M, L, planes_t, W, H, S, widths, dWp, dbp, num_partials, dS_ws,
+                           tile_open, nullptr, ce, Wout, num_classes, adjt, stream);
 }
 
 static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* gptr,
@@ -1742,14 +1779,20 @@ static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* g
                          float* const* dWp, float* const* dbp, int num_partials,
                          const int32_t* tile_open, const lgnn_s3::OpenBwdArgs& o, void* stream,
                          const float* dlogits, const float* Wout, int num_classes,
-                         const void* adjt) {
-  if (M < 0 || L < 1 || L > 2 || !(dP || dlogits) || !batch || !gptr || !rowptr || !col || !X ||
+                         const void* adjt, const lgnn_ce_src* ce) {
+  if (M < 0 || L < 1 || L > 2 || !(dP || dlogits || ce) || !batch || !gptr || !rowptr || !col ||
+      !X ||
       !planes_t || !H || !widths || !dWp || !dbp || !tile_open || num_graphs < 0)
     return LGNN_EINVAL;
   if (num_partials != lgnn_gcn_stack_bwd_partials(M)) return LGNN_EINVAL;
   lgnn_s3::FBwdArgs a = {};
   a.dP = dP;
   a.dlog = dlogits;
+  if (ce) {
+    if (dlogits || !ce->logits || !ce->lse || !ce->target || !ce->wsum || !ce->gloss)
+      return LGNN_EINVAL;
+    a.ce = CeSrc{ce->logits, ce->lse, ce->target, ce->weight, ce->wsum, ce->gloss, num_classes};
+  }
   a.Wout = Wout;
   a.C = num_classes;
   a.adjt = static_cast<const unsigned char*>(adjt);

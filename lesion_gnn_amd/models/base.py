@@ -132,6 +132,16 @@ class BaseModule(nn.Module):
             # (the reference's y.float() happens in the kernel)
             return ops.regression_loss(self._model_logits(batch), batch.y, 0.0,
                                        float(self.num_classes - 1), self.criterion.kind)[1]
+        # model + criterion as one node where the model offers it (GCN; the eager model only:
+        # a compiled model keeps the reference's logits -> criterion sequence)
+        fused = None if hasattr(self.model, "_orig_mod") else getattr(self.model, "forward_loss",
+                                                                         None)
+        if fused is not None and isinstance(self.criterion, CrossEntropyLoss):
+            edge_index = getattr(batch, "adj_t", None)
+            if edge_index is None:
+                edge_index = batch.edge_index
+            return fused(batch.x, edge_index, batch.batch, batch.y, self.criterion.weight,
+                         getattr(batch, "num_graphs", None))[1]
         logits = self(batch)
         y = batch.y.float() if self.is_regression else batch.y
         return self.criterion(logits, y)

@@ -61,6 +61,21 @@ class GCN(nn.Module):
         return ops.pool_head(h, self.out_proj.weight, self.out_proj.bias, g, mean)
 
 
+    def forward_loss(self, x: torch.Tensor, edge_index, batch: torch.Tensor, y: torch.Tensor,
+                     weight: torch.Tensor | None = None, num_graphs: int | None = None):
+        """(logits, loss) of forward() followed by nn.CrossEntropyLoss(weight) (the reference's
+        criterion, base.py:93-94, as its training_step applies it, :196-201). Without dropout the
+        model and the criterion are one autograd node (ops.gcn_stack_ce): the backward forms the
+        logits gradient inside its own launches. Otherwise forward() then ops.cross_entropy."""
+        if self.dropout.p == 0.0 or not self.training:
+            if not torch.compiler.is_compiling():
+                g = as_graph(edge_index, x.size(0), batch, num_graphs)
+                return ops.gcn_stack_ce(x, g, self.flat_params(), len(self.convs), y, weight,
+                                        self.pool == "mean")
+        logits = self(x, edge_index, batch, num_graphs)
+        return logits, ops.cross_entropy(logits, y, weight)
+
+
 @dataclasses.dataclass(kw_only=True)
 class GCNConfig(BaseModelConfig):
     input_features: Placeholder[int] = dataclasses.field(default_factory=Placeholder, init=False)

@@ -280,18 +280,23 @@ def stack_bwd(dp: torch.Tensor | None, x: torch.Tensor, graph: Graph, mean: bool
     arr = ctypes.c_void_p * (L + 1)
     Sx = [x] + list(ss)
     dlog, W_out = head if head is not None else (None, None)
-    B = dp.size(0) if dp is not None else dlog.size(0)
+    ce = dlog if isinstance(dlog, _lib.CeSrc) else None  # CE-formed logits gradient
+    B = dp.size(0) if dp is not None else (graph.num_graphs if ce is not None else dlog.size(0))
     if s3f and _open_in_fused(OPEN_IN_FUSED_BWD, graph, "bwd"):  # one launch, open tiles last
         dS_ws = torch.empty(2 * M * 128, dtype=torch.float32, device=dev)
-        _lib.call("lgnn_gcn_stack_bwd_s3f_all", _lib.ptr(dp), _lib.ptr(graph.batch),
-                  _lib.ptr(graph.gptr), int(mean), B, _lib.ptr(csr.rowptr),
-                  _lib.ptr(csr.col), _lib.ptr(csr.w), _lib.ptr(csr.tptr), _lib.ptr(csr.tidx),
-                  _lib.ptr(csr.tw), _lib.ptr(x), M, L, _lib.ptr(planes_t),
+        common = (_lib.ptr(graph.batch), _lib.ptr(graph.gptr), int(mean), B,
+                  _lib.ptr(csr.rowptr), _lib.ptr(csr.col), _lib.ptr(csr.w), _lib.ptr(csr.tptr),
+                  _lib.ptr(csr.tidx), _lib.ptr(csr.tw), _lib.ptr(x), M, L, _lib.ptr(planes_t),
                   arr(*[W.data_ptr() for W in Ws]), arr(*[h.data_ptr() for h in hs]),
                   (ctypes.c_void_p * L)(*[t.data_ptr() for t in ss]),
                   (ctypes.c_int * (L + 2))(*widths), arr(*[t.data_ptr() for t in dWp]),
-                  arr(*[t.data_ptr() for t in dbp]), P, _lib.ptr(dS_ws), _lib.ptr(open_),
-                  _lib.ptr(dlog), _lib.ptr(W_out), W_out.size(0) if head else 0, adjt, _s(dev))
+                  arr(*[t.data_ptr() for t in dbp]), P, _lib.ptr(dS_ws), _lib.ptr(open_))
+        if ce is not None:
+            _lib.call("lgnn_gcn_stack_bwd_s3f_ce", *common, ctypes.byref(ce), _lib.ptr(W_out),
+                      W_out.size(0), adjt, _s(dev))
+        else:
+            _lib.call("lgnn_gcn_stack_bwd_s3f_all", _lib.ptr(dp), *common, _lib.ptr(dlog),
+                      _lib.ptr(W_out), W_out.size(0) if head else 0, adjt, _s(dev))
         return _stack_bwd_outputs(L, widths, dWp, dbp, P, dev, reducer)
     assert head is None, "dP from the logits gradient only in the single-launch split-3 path"
     if s3f:  # one fused split-3 launch, every layer of a tile in one pass (stack3_bwd.hip)
@@ -386,19 +391,32 @@ def linear_bwd(grad_mode: int, dY: torch.Tensor, *, H: torch.Tensor | None, act:
     return dX, dW, db
 
 
-def reduce_multi(jobs: list, dev) -> None:
+CE_PART = object()  # reduce_multi job part: the CE logits gradient, formed in the reduction
+
+
+def reduce_multi(jobs: list, dev, ce=None, num_classes: int = 0) -> None:
     """Deterministic slab reductions [(partials, P, len, out), ...] in one launch per 16; a job
-    (a, P, len, out, f, width) is the outer-product sum out[c, d] = sum_p a[p, c] f[p, d]."""
+    (a, P, len, out, f, width) is the outer-product sum out[c, d] = sum_p a[p, c] f[p, d]. A job
+    whose partials are CE_PART takes the [P][C] CE logits gradient formed from `ce`
+    (_lib.CeSrc, lgnn_reduce_jobs_ce) instead of a materialised dlogits tensor."""
     for i in range(0, len(jobs), 16):
         chunk = jobs[i:i + 16]
         n = len(chunk)
-        parts = (ctypes.c_void_p * n)(*[j[0].data_ptr() for j in chunk])
+        is_ce = [j[0] is CE_PART for j in chunk]
+        parts = (ctypes.c_void_p * n)(*[None if c else j[0].data_ptr()
+                                        for j, c in zip(chunk, is_ce)])
         nps = (ctypes.c_int * n)(*[j[1] for j in chunk])
         lens = (ctypes.c_int64 * n)(*[j[2] for j in chunk])
         outs = (ctypes.c_void_p * n)(*[j[3].data_ptr() for j in chunk])
-        if any(len(j) > 4 for j in chunk):
-            fac = (ctypes.c_void_p * n)(*[j[4].data_ptr() if len(j) > 4 else None for j in chunk])
-            wid = (ctypes.c_int * n)(*[j[5] if len(j) > 4 else 0 for j in chunk])
+        fac = (ctypes.c_void_p * n)(*[j[4].data_ptr() if len(j) > 4 else None for j in chunk])
+        wid = (ctypes.c_int * n)(*[j[5] if len(j) > 4 else 0 for j in chunk])
+        if any(is_ce):
+            if ce is None:
+                raise _lib.LgnnError("reduce_multi: a CE_PART job needs the CE source")
+            _lib.call("lgnn_reduce_jobs_ce", n, parts, fac, wid, nps, lens, outs,
+                      (ctypes.c_int * n)(*[int(c) for c in is_ce]), ctypes.byref(ce),
+                      int(num_classes), _s(dev))
+        elif any(len(j) > 4 for j in chunk):
             _lib.call("lgnn_reduce_jobs", n, parts, fac, wid, nps, lens, outs, _s(dev))
         else:
             _lib.call("lgnn_reduce_partials_multi", n, parts, nps, lens, outs, _s(dev))
@@ -950,6 +968,12 @@ class _GCNStack(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, graph, mean, L, *params):
+        logits, to_save = _GCNStack._fwd(ctx, x, graph, mean, L, params)
+        ctx.save_for_backward(*to_save)
+        return logits
+
+    @staticmethod
+    def _fwd(ctx, x, graph, mean, L, params):
         _lib.require_gpu(x, *params)
         x = _f32c(x)
         params = [_f32c(p) for p in params]
@@ -987,14 +1011,26 @@ class _GCNStack(torch.autograd.Function):
                 ctx.saved_s.append(fast)
         W_out, b_out = params[2 + 2 * L], params[3 + 2 * L]
         pooled, logits = pool_head_fwd(hs[-1], graph, mean, W_out, b_out)
-        ctx.save_for_backward(x, pooled, *hs, *ss, *params)
         ctx.graph, ctx.mean, ctx.L = graph, mean, L
-        return logits
+        ctx.n_saved = 2 + len(hs) + len(ss) + len(params)
+        return logits, (x, pooled, *hs, *ss, *params)
 
     @staticmethod
     def backward(ctx, dlogits):
+        return _GCNStack._bwd(ctx, dlogits, ctx.saved_tensors)
+
+    @staticmethod
+    def fused_head(ctx, W_out) -> bool:
+        """True when the backward forms dP = dlogits W_out inside the single split-3 launch."""
+        return (ctx.fused and (1 <= ctx.L <= 2 or ctx.planes_t is not None) and
+                not ctx.needs_input_grad[0] and FUSED_BWD and
+                head_in_stack_bwd(ctx.graph, ctx.L, W_out.size(0), ctx.planes_t is not None))
+
+    @staticmethod
+    def _bwd(ctx, dlogits, saved, ce=None):
+        """ce = (CeSrc, logits): the logits gradient is CE's, formed where it is consumed (the
+        fused backward's prologue, the out_proj reduction jobs) — dlogits is None then."""
         L = ctx.L
-        saved = ctx.saved_tensors
         x, pooled = saved[0], saved[1]
         hs = saved[2:3 + L]
         ss = saved[3 + L:3 + 2 * L]
@@ -1003,7 +1039,7 @@ class _GCNStack(torch.autograd.Function):
         kind = getattr(ctx, "kind", "gcn")
         csr = graph.csr(kind)
         W_out = params[2 + 2 * L]
-        dlogits = _f32c(dlogits)
+        dlogits = _f32c(dlogits) if dlogits is not None else None
         grads = [None] * len(params)
         red: list = []
         s3 = ctx.planes_t is not None
@@ -1013,12 +1049,13 @@ class _GCNStack(torch.autograd.Function):
                 # dP is formed inside the stack kernel; out_proj's gradients (dlogits^T pooled,
                 # column sums of dlogits) join the stack's slab reductions: no head launch
                 C, D = W_out.shape
+                B = pooled.size(0)
                 dWo = torch.empty_like(W_out)
                 dbo = torch.empty(C, dtype=torch.float32, device=x.device)
-                red += [(dlogits, dlogits.size(0), C * D, dWo, pooled, D),
-                        (dlogits, dlogits.size(0), C, dbo)]
+                part = CE_PART if ce is not None else dlogits
+                red += [(part, B, C * D, dWo, pooled, D), (part, B, C, dbo)]
                 outs = stack_bwd(None, x, graph, ctx.mean, Ws, hs, ss, red, ctx.planes_t,
-                                 head=(dlogits, W_out), kind=kind)
+                                 head=(ce[0] if ce is not None else dlogits, W_out), kind=kind)
             else:
                 dp, dWo, dbo = pool_head_bwd(dlogits, pooled, W_out)
                 outs = stack_bwd(dp, x, graph, ctx.mean, Ws, hs, ss, red, ctx.planes_t,
@@ -1026,8 +1063,10 @@ class _GCNStack(torch.autograd.Function):
             grads[2 + 2 * L], grads[3 + 2 * L] = dWo, dbo
             for l, (dW, db) in enumerate(outs):
                 grads[2 * l], grads[2 * l + 1] = dW, db
-            reduce_multi(red, x.device)
+            reduce_multi(red, x.device, ce=ce[0] if ce is not None else None,
+                         num_classes=W_out.size(0))
             return (None, None, None, None, *grads)
+        assert ce is None, "the CE-formed logits gradient only on the fused head path"
         dp, dWo, dbo = pool_head_bwd(dlogits, pooled, W_out)
         grads[2 + 2 * L], grads[3 + 2 * L] = dWo, dbo
         if ctx.fused:  # the fused forward saves no aggregated inputs: S_l = Â H_{l-1}
@@ -1057,6 +1096,71 @@ class _GCNStack(torch.autograd.Function):
         reduce_multi(red, x.device)
         grads[0], grads[1] = dW, db
         return (dx, None, None, None, *grads)
+
+
+class _GCNStackCE(torch.autograd.Function):
+    """The GCN model and its criterion nn.CrossEntropyLoss(weight) (mean reduction, reference
+    models/base.py:93-94, training_step :196-201) as ONE autograd node: outputs (logits, loss).
+    Forward: _GCNStack's launches + lgnn_ce_fwd. Backward with only the loss differentiated (the
+    training step): the logits gradient is never materialised — the fused split-3 backward forms
+    it per graph in its prologue and the out_proj reduction jobs form it per (graph, class), both
+    with lgnn_ce_bwd's expression (no lgnn_ce_bwd launch, bitwise the same gradients). Anything
+    else (logits also differentiated, shapes off the fused head path) forms dlogits with
+    lgnn_ce_bwd and takes _GCNStack's backward."""
+
+    @staticmethod
+    def forward(ctx, x, graph, mean, L, y, weight, *params):
+        ctx.set_materialize_grads(False)
+        logits, to_save = _GCNStack._fwd(ctx, x, graph, mean, L, params)
+        z = logits
+        yy = y.to(torch.int64).contiguous()
+        B, C = z.shape
+        dev = z.device
+        lse = torch.empty(B, dtype=torch.float32, device=dev)
+        out = torch.empty(2, dtype=torch.float32, device=dev)  # loss, sum of weights
+        bad = torch.empty(1, dtype=torch.int32, device=dev)
+        w = _f32c(weight) if weight is not None else None
+        _lib.call("lgnn_ce_fwd", _lib.ptr(z), _lib.ptr(yy), _lib.ptr(w), B, C, _lib.ptr(lse),
+                  _lib.ptr(out), _lib.ptr(out) + 4, _lib.ptr(bad), _s(dev))
+        ctx.has_w = w is not None
+        ctx.save_for_backward(*to_save, z, yy, lse, out, *((w,) if w is not None else ()))
+        return logits, out[0]
+
+    @staticmethod
+    def backward(ctx, dlogits, dloss):
+        saved = ctx.saved_tensors
+        n = ctx.n_saved
+        stack_saved = saved[:n]
+        z, yy, lse, out = saved[n:n + 4]
+        w = saved[n + 4] if ctx.has_w else None
+        params = stack_saved[3 + 2 * ctx.L:]
+        W_out = params[2 + 2 * ctx.L]
+
+        def grads(r):  # _GCNStack's (dx, -, -, -, *param grads) -> this node's inputs
+            return (r[0], None, None, None, None, None, *r[4:])
+
+        if dloss is None:
+            if dlogits is None:
+                return (None,) * (6 + len(params))
+            return grads(_GCNStack._bwd(ctx, dlogits, stack_saved))
+        g = _f32c(dloss.reshape(1))
+        if dlogits is None and _GCNStack.fused_head(ctx, W_out):
+            src = _lib.CeSrc(z.data_ptr(), lse.data_ptr(), yy.data_ptr(), _lib.ptr(w),
+                             out.data_ptr() + 4, g.data_ptr())
+            return grads(_GCNStack._bwd(ctx, None, stack_saved, ce=(src, z)))
+        B, C = z.shape
+        dz = torch.empty_like(z)
+        _lib.call("lgnn_ce_bwd", _lib.ptr(z), _lib.ptr(yy), _lib.ptr(w), B, C, _lib.ptr(lse),
+                  _lib.ptr(out) + 4, _lib.ptr(g), _lib.ptr(dz), _s(z.device))
+        if dlogits is not None:
+            dz = dz + dlogits
+        return grads(_GCNStack._bwd(ctx, dz, stack_saved))
+
+
+def gcn_stack_ce(x, graph: Graph, params: list[torch.Tensor], L: int, y: torch.Tensor,
+                 weight: torch.Tensor | None = None, mean: bool = True):
+    """(logits, loss): the GCN stack and its cross-entropy criterion in one node (_GCNStackCE)."""
+    return _GCNStackCE.apply(x, graph, mean, L, y, weight, *params)
 
 
 def gcn_stack(x, graph: Graph, params: list[torch.Tensor], L: int, mean: bool = True):

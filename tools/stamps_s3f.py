@@ -23,7 +23,7 @@ if os.environ.get("STAMPS_ABLATIONS"):
         VARIANTS[k] = [f"-DLGNN_ABLATE={v}"]
     VARIANTS["sb"] = ["-DLGNN_S3F_SB"]
     VARIANTS["sb_stamps"] = ["-DLGNN_S3F_SB", "-DLGNN_STAMPS"]
-NAMES = ["prologue (adj, dZ_L)", "l2 G, G image", "l2 H image", "l2 dW", "l2 dH+dZ", "l1 G, G image",
+NAMES = ["prologue: stage + load wait", "prologue: dZ_L", "prologue: Â planes", "l2 G, G image", "l2 H image", "l2 dW", "l2 dH+dZ", "l1 G, G image",
          "l1 H image", "l1 dW", "l1 dH+dZ", "l0 X + dW", "tile tail"]
 # k_s3_fbwd8 (LGNN_S3F_WAVES=8): the same libraries, copied so each has its own variant switch
 NAMES8 = ["prologue (adj, dZ_L)", "l2 G + images", "l2 dW", "l2 dH+dZ+exch", "l1 G + images",
@@ -60,6 +60,9 @@ def run():
     Ws = [torch.randn(D, D, device=dev, generator=gen) / 11.3 for _ in range(L + 1)]
     Hs = [torch.randn(M, D, device=dev, generator=gen) for _ in range(L + 1)]
     dP = torch.randn(b.num_graphs, D, device=dev, generator=gen)
+    W_out = torch.randn(5, D, device=dev, generator=gen) / 11.3
+    dlog = torch.randn(b.num_graphs, 5, device=dev, generator=gen)
+    dS_ws = torch.empty(2 * M * 128, device=dev)
     # the forward's Â^T planes handed to the backward (STAMPS_ADJT=0: rebuilt from the CSR)
     keep = {}
     ops.stack_fwd(b.x, g, Ws, [torch.zeros(D, device=dev)] * (L + 1), keep)
@@ -80,17 +83,22 @@ def run():
         slabs = [torch.empty(P * (D * D + D), device=dev) for _ in range(L + 1)]
         dWp = arr(*[t.data_ptr() for t in slabs])
         dbp = arr(*[t.data_ptr() + P * D * D * 4 for t in slabs])
-        args = (dP.data_ptr(), g.batch.data_ptr(), g.gptr.data_ptr(), 1, b.num_graphs,
-                csr.rowptr.data_ptr(), csr.col.data_ptr(), csr.w.data_ptr(), b.x.data_ptr(), M, L,
-                planes_t.data_ptr(), arr(*[h.data_ptr() for h in Hs]),
-                (ctypes.c_int * (L + 2))(D, D, D, D), dWp, dbp, P, open_.data_ptr(), adjt_ptr, s)
+        # the step's entry: the _all launch with the logits gradient (dZ_L = dlogits W_out
+        # formed in the prologue), as ops.stack_bwd runs it at C2
+        args = (None, g.batch.data_ptr(), g.gptr.data_ptr(), 1, b.num_graphs,
+                csr.rowptr.data_ptr(), csr.col.data_ptr(), csr.w.data_ptr(), csr.tptr.data_ptr(),
+                csr.tidx.data_ptr(), csr.tw.data_ptr(), b.x.data_ptr(), M, L,
+                planes_t.data_ptr(), arr(*[W.data_ptr() for W in Ws]),
+                arr(*[h.data_ptr() for h in Hs]), (ctypes.c_void_p * L)(*[h.data_ptr() for h in Hs[1:]]),
+                (ctypes.c_int * (L + 2))(D, D, D, D), dWp, dbp, P, dS_ws.data_ptr(),
+                open_.data_ptr(), dlog.data_ptr(), W_out.data_ptr(), W_out.size(0), adjt_ptr, s)
         for _ in range(3):
-            assert lib.lgnn_gcn_stack_bwd_s3f(*args) == 0
+            assert lib.lgnn_gcn_stack_bwd_s3f_all(*args) == 0
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(20):
-            lib.lgnn_gcn_stack_bwd_s3f(*args)
+            lib.lgnn_gcn_stack_bwd_s3f_all(*args)
         e1.record()
         torch.cuda.synchronize()
         print(f"{v:14s} {e0.elapsed_time(e1) / 20 * 1e3:8.1f} us per launch", flush=True)
