@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 33
+#define LGNN_ABI_VERSION 34
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -272,6 +272,19 @@ int lgnn_spmm(const int32_t* rowptr, const int32_t* col, const float* w, float s
 int lgnn_pool_head_fwd(const float* H, const int32_t* gptr, int64_t B, int D, int pool_mean,
                        const float* Wout, const float* bout, int C, float* pooled,
                        float* logits, void* stream);
+
+/* lgnn_pool_head_fwd (D % 4 == 0, 1 <= C <= 16) with the criterion's forward folded in (ABI v34):
+ * nn.CrossEntropyLoss(weight), mean reduction (reference models/base.py:93-94) — lgnn_ce_fwd's
+ * outputs and arithmetic, bitwise: lse [B], loss [1], wsum [1], bad [1] (1 if a target is outside
+ * [0, C); such graphs skipped). The last workgroup to finish sums the per-graph terms.
+ * ticket: uint32[10] zero before the first call, re-armed by every call (one stream at a time).
+ * workspace: lgnn_pool_head_ce_workspace_bytes(B) bytes. */
+size_t lgnn_pool_head_ce_workspace_bytes(int64_t num_graphs);
+int lgnn_pool_head_ce_fwd(const float* H, const int32_t* gptr, int64_t B, int D, int pool_mean,
+                          const float* Wout, const float* bout, int C, float* pooled,
+                          float* logits, const int64_t* target, const float* weight, float* lse,
+                          float* loss, float* wsum, int* bad, unsigned int* ticket,
+                          void* workspace, size_t workspace_bytes, void* stream);
 
 /* The same with each graph split over `splits` workgroups (few, large graphs: the GAT configs);
  * part: [B][splits][D] scratch; tickets: int32 [B], zero on entry, left zero. Each graph's

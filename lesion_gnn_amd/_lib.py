@@ -71,6 +71,9 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_ce_fwd": (I32, [P, P, P, I64, I32, P, P, P, P, P]),
     "lgnn_ce_bwd": (I32, [P, P, P, I64, I32, P, P, P, P, P]),
     "lgnn_pool_head_fwd": (I32, [P, P, I64, I32, I32, P, P, I32, P, P, P]),
+    "lgnn_pool_head_ce_workspace_bytes": (SZ, [I64]),
+    "lgnn_pool_head_ce_fwd": (I32, [P, P, I64, I32, I32, P, P, I32, P, P, P, P, P, P, P, P, P, P,
+                                    SZ, P]),
     "lgnn_pool_head_fwd_split": (I32, [P, P, I64, I32, I32, P, P, I32, I32, P, P, P, P, P]),
     "lgnn_pool_head_bwd": (I32, [P, P, I64, I32, P, I32, P, P, P, P]),
     "lgnn_pool_bwd": (I32, [P, P, P, I64, I32, I32, P, P]),
@@ -155,7 +158,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 33
+ABI_VERSION = 34
 
 _lib = None
 

@@ -37,8 +37,9 @@ constexpr int kSortedRows = 256;   // k_scan's sorted body: rows per workgroup (
 inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
 inline size_t scan_bsum_bytes(int64_t N) {
-  // 2 arrays x blocks of 1024 elements; the sorted path's scan: one word per 256 rows
-  return (size_t)4 * 4 * ((N + 1 + 1023) / 1024);
+  // 2 arrays x blocks of 1024 elements; the sorted path's scan: one word per 256 rows (4 per
+  // 1024), then the sorted-open mode's source scan (one per 1024 rows) after them
+  return (size_t)4 * 5 * ((N + 1 + 1023) / 1024);
 }
 
 struct GraphWs {
@@ -235,14 +236,15 @@ __global__ __launch_bounds__(kThreads) void k_prep_sorted(int32_t* __restrict__ 
       if (!in) continue;
       const int64_t sv = s[c], dv = d[c];
       if (!edge_ok(sv, dv, N) || dp > dv) {
-        bad = 1;
+        bad |= 1;
         continue;
       }
-      if (a.need_closed && (sv >> 6) != (dv >> 6)) bad = 1;
+      // an edge leaving its tile: the lazy build needs the source CSR (sorted-open mode)
+      if (a.need_closed && (sv >> 6) != (dv >> 6)) bad |= 2;
       if (dv != dp) {  // head of row dv: the rows since the previous target have no entries
         const int64_t r0 = dp < 0 ? 0 : dp + 1;
         if (dv - r0 > kGapCap) {
-          bad = 1;
+          bad |= 1;
         } else {
           for (int64_t q = r0; q < dv; ++q) sorted_empty_row(a, q, e);
         }
@@ -254,10 +256,10 @@ __global__ __launch_bounds__(kThreads) void k_prep_sorted(int32_t* __restrict__ 
           if (nl == 0 && cl) lpos = r.len + __ffsll((long long)(clm & cmask)) - 1;
           nl += cl;
           n += clen;
-          if (clen == 64) bad = 1;  // longer than any row the fast path takes
+          if (clen == 64) bad |= 1;  // longer than any row the fast path takes
         }
         const int deg = n - nl;
-        if (n > kSortedRowCap + 1 || nl > 1 || deg + a.add_loop > kSortedRowCap) bad = 1;
+        if (n > kSortedRowCap + 1 || nl > 1 || deg + a.add_loop > kSortedRowCap) bad |= 1;
         a.rs[dv] = (int32_t)e;
         a.scnt[dv] = deg;
         a.lp[dv] = nl ? lpos : -1;
@@ -266,7 +268,7 @@ __global__ __launch_bounds__(kThreads) void k_prep_sorted(int32_t* __restrict__ 
       }
       if (e == E - 1) {  // rows after the last target
         if (N - 1 - dv > kGapCap) {
-          bad = 1;
+          bad |= 1;
         } else {
           for (int64_t q = dv + 1; q < N; ++q) sorted_empty_row(a, q, E);
         }
@@ -275,17 +277,23 @@ __global__ __launch_bounds__(kThreads) void k_prep_sorted(int32_t* __restrict__ 
     }
   }
   if (!prepped) prep_body(zero, nzero, tile_open, ntiles, batch, M, B, gptr, blockIdx.x, gridDim.x);
-  bad = __syncthreads_or(bad);
-  if (threadIdx.x == 0) a.verdict[blockIdx.x] = bad;
+  const int b1 = __syncthreads_or(bad & 1), b2 = __syncthreads_or(bad & 2);
+  if (threadIdx.x == 0) a.verdict[blockIdx.x] = (b1 ? 1 : 0) | (b2 ? 2 : 0);
 }
 
-// true when k_prep_sorted found the input target-sorted (every workgroup's verdict clear);
-// block-uniform, every thread of the block must call it
-__device__ __forceinline__ bool sorted_ok(const int32_t* verdict, int nverdict) {
-  if (!verdict) return false;
+// The build mode from k_prep_sorted's verdict words (block-uniform, every thread must call it):
+//   kModeSorted: target-sorted, every tile closed -> k_scan's sorted body writes the CSR, the
+//                general launches return at once (no source CSR is needed);
+//   kModeSortedOpen: target-sorted but some edge leaves its tile (lazy build) -> the sorted body
+//                writes the target CSR, the general launches build only the source CSR;
+//   kModeGeneral: the counting sort for both.
+constexpr int kModeGeneral = 0, kModeSorted = 1, kModeSortedOpen = 2;
+__device__ __forceinline__ int sorted_mode(const int32_t* verdict, int nverdict) {
+  if (!verdict) return kModeGeneral;
   int v = 0;
   for (int i = threadIdx.x; i < nverdict; i += blockDim.x) v |= verdict[i];
-  return __syncthreads_or(v) == 0;
+  const int b1 = __syncthreads_or(v & 1), b2 = __syncthreads_or(v & 2);
+  return b1 ? kModeGeneral : (b2 ? kModeSortedOpen : kModeSorted);
 }
 
 // Edge passes. A block takes a chunk of kChunk consecutive edges, kPer per thread, so every
@@ -376,7 +384,7 @@ __device__ __forceinline__ void count_body(const int64_t* __restrict__ ei, int64
 #pragma unroll
   for (int it = 0; it < PER; ++it) {
     const Run r = wave_run(c.use[it] ? c.d[it] : -2 - lane);
-    if (c.use[it] && r.head) atomicAdd(&cnt[c.d[it]], r.len);
+    if (cnt && c.use[it] && r.head) atomicAdd(&cnt[c.d[it]], r.len);
   }
   if (tile_open) {  // lazy transpose: the tiles an edge leaves are known before the fill
     const int64_t ntiles = (N + 63) >> 6;
@@ -413,11 +421,12 @@ __global__ __launch_bounds__(kThreads) void k_count(const int64_t* __restrict__ 
                                                     int32_t* verdict, int nverdict) {
   __shared__ int hist[kBins];
   __shared__ int red[2 * kThreads / 64];
-  const bool fast = sorted_ok(verdict, nverdict);
+  const int mode = sorted_mode(verdict, nverdict);
   // the summary word for k_scan / k_fill / k_finish (one word to read instead of all of them)
-  if (verdict && blockIdx.x == 0 && threadIdx.x == 0) verdict[kVerdictMax] = fast;
-  if (fast) return;
-  count_body<PER>(ei, E, N, loops, cnt, tcnt, err, tile_open, hist, red, blockIdx.x);
+  if (verdict && blockIdx.x == 0 && threadIdx.x == 0) verdict[kVerdictMax] = mode;
+  if (mode == kModeSorted) return;
+  count_body<PER>(ei, E, N, loops, mode == kModeSortedOpen ? nullptr : cnt, tcnt, err, tile_open,
+                  hist, red, blockIdx.x);
 }
 
 // fill[d] / tfill[s] start at the row offsets (set by k_scan); slots come from atomics on them,
@@ -435,6 +444,7 @@ __device__ __forceinline__ void fill_body(const int64_t* __restrict__ ei, int64_
   load_chunk(c, ei, E, N, loops, c0, nullptr);
 #pragma unroll
   for (int it = 0; it < PER; ++it) {
+    if (!fill) break;  // sorted-open mode: the target CSR comes from k_scan's sorted body
     const int64_t e = c0 + (int64_t)it * kThreads + threadIdx.x;
     const Run r = wave_run(c.use[it] ? c.d[it] : -2 - lane);
     int slot0 = 0;
@@ -492,9 +502,10 @@ __global__ __launch_bounds__(kThreads) void k_fill(const int64_t* __restrict__ e
                                                    const int32_t* summary) {
   __shared__ int hist[kBins];
   __shared__ int red[2 * kThreads / 64];
-  if (summary && __builtin_amdgcn_readfirstlane(*summary)) return;  // sorted path took it
-  fill_body<PER>(ei, E, N, loops, rowptr, fill, col, eid, tptr, tfill, tidx, teid, lazy_open, hist,
-                 red, blockIdx.x);
+  const int mode = summary ? __builtin_amdgcn_readfirstlane(*summary) : kModeGeneral;
+  if (mode == kModeSorted) return;  // the sorted path took it
+  fill_body<PER>(ei, E, N, loops, rowptr, mode == kModeSortedOpen ? nullptr : fill, col, eid, tptr,
+                 tfill, tidx, teid, lazy_open, hist, red, blockIdx.x);
 }
 
 // Both degree scans (blockIdx.y = 0: rowptr from cnt, 1: tptr from tcnt) in ONE launch over
@@ -729,14 +740,22 @@ __global__ __launch_bounds__(kScanT) void k_scan(const int32_t* __restrict__ cnt
                                                  int32_t* err_out, int nblk) {
   __shared__ ScanSmem sm;
   __shared__ SortedSmem ss;
-  const bool fast = sa.summary_ready
-                        ? (sa.verdict && __builtin_amdgcn_readfirstlane(sa.verdict[kVerdictMax]))
-                        : sorted_ok(sa.verdict, sa.nverdict);
+  const int mode = sa.summary_ready
+                       ? (sa.verdict ? __builtin_amdgcn_readfirstlane(sa.verdict[kVerdictMax])
+                                     : kModeGeneral)
+                       : sorted_mode(sa.verdict, sa.nverdict);
   if (!sa.summary_ready && sa.verdict && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
-    sa.verdict[kVerdictMax] = fast;  // the summary word k_fill / k_finish read
-  if (fast) {
-    if (blockIdx.y == 0 && (int64_t)blockIdx.x * kSortedRows < N)
-      sorted_body(sa, N, stat, rowptr, col, w, tile_open, err_out, ss, blockIdx.x);
+    sa.verdict[kVerdictMax] = mode;  // the summary word k_fill / k_finish read
+  if (mode != kModeGeneral) {
+    if (blockIdx.y == 0) {
+      if ((int64_t)blockIdx.x * kSortedRows < N)
+        sorted_body(sa, N, stat, rowptr, col, w, tile_open, err_out, ss, blockIdx.x);
+      return;
+    }
+    // sorted-open: the source scan (y = 1), its flags past the sorted body's (stat + 4 nblk)
+    if (mode == kModeSorted || (int)blockIdx.x >= nblk) return;
+    scan_body(cnt, tcnt, N, add, stat + 3 * (int64_t)nblk, rowptr, tptr, fill, tfill, dis,
+              tile_open, sm, blockIdx.x, 1, nblk);
     return;
   }
   if ((int)blockIdx.x >= nblk) return;
@@ -923,7 +942,9 @@ __global__ __launch_bounds__(kThreads) void k_finish(int64_t N, int64_t E, int a
   __shared__ int32_t s_key[kFinWaves][kFinishCap];
   __shared__ int32_t s_val[kFinWaves][kFinishCap];
   __shared__ int32_t s_ptr[kFinWaves][kFinT + 1];
-  if (summary && __builtin_amdgcn_readfirstlane(*summary)) return;  // sorted path took it
+  const int mode = summary ? __builtin_amdgcn_readfirstlane(*summary) : kModeGeneral;
+  if (mode == kModeSorted) return;  // the sorted path took it
+  if (mode == kModeSortedOpen && blockIdx.y == 0) return;  // target CSR: k_scan's sorted body
   const int wave = threadIdx.x >> 6;
   const int64_t v = (int64_t)blockIdx.x * kFinWaves + wave;
   if (v * kFinT >= N) return;
@@ -1148,7 +1169,7 @@ extern "C" int lgnn_graph_build_path(const void* workspace, int64_t num_nodes, i
                      as_stream(stream)) != hipSuccess ||
       hipStreamSynchronize(as_stream(stream)) != hipSuccess)
     return LGNN_EINVAL;
-  return v ? 1 : 0;
+  return v;  // kModeGeneral 0, kModeSorted 1, kModeSortedOpen 2
 }
 
 // the target-sorted fast path is tried unless LGNN_GRAPH_SORTED=0 (a test / A-B knob)

@@ -61,16 +61,35 @@ __global__ __launch_bounds__(NT) void k_pool_head_fwd(const float* __restrict__ 
   }
 }
 
-// D % 4 == 0 (every hidden width of the reference): one 256-thread block per graph; the 8 half
-// waves stride the graph's rows (float4 per lane, 128-feature strips, 2 rows in flight each),
-// partial sums combined in half-wave order; then one wave per class for the logits.
+// The criterion's forward folded into the readout (CE = true): nn.CrossEntropyLoss(weight), mean
+// reduction (reference models/base.py:93-94) — k_ce_fwd's arithmetic, bit for bit:
+//   per graph (its block, once its logits are out): lse_g = m + log(sum exp(z - m)), the terms
+//     num_g = w[y_g] (lse_g - z_g[y_g]), den_g = w[y_g] (0 and *bad for a target outside [0, C));
+//   the last block to finish (two-level ticket) sums the terms in k_ce_fwd's order (1024 strided
+//     partials, then the 16-wave fixed tree) and writes loss = num / den and wsum = den.
+// Cross-block traffic without release fences (one per block would write back its XCD's L2, the
+// readout split's lesson): the terms are returning agent-scope atomic exchanges whose results
+// feed the ticket operand, and the last block reads them with agent-scope atomic loads.
+struct CeFwd {
+  const int64_t* y;
+  const float* w;
+  float* lse;
+  float* part;   // [B][2] num_g, den_g
+  unsigned int* ticket;  // [10] zero, re-armed: 9 ticket words + the blocks' bad-target OR
+  float* loss;
+  float* wsum;
+  int* bad;      // written by the last block
+  int64_t B;
+};
+
+template <bool CE>
 __global__ __launch_bounds__(NT) void k_pool_head_fwd4(const float* __restrict__ H,
                                                        const int32_t* __restrict__ gptr, int D,
                                                        int pool_mean,
                                                        const float* __restrict__ Wout,
                                                        const float* __restrict__ bout, int C,
                                                        float* __restrict__ pooled,
-                                                       float* __restrict__ logits) {
+                                                       float* __restrict__ logits, CeFwd ce) {
   __shared__ __attribute__((aligned(16))) float red[8][512];
   __shared__ float pl[512];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -124,12 +143,81 @@ __global__ __launch_bounds__(NT) void k_pool_head_fwd4(const float* __restrict__
   }
   if (!Wout) return;
   __syncthreads();
+  __shared__ float zl[16];  // this graph's logits (CE; C <= 16)
   for (int c = wave; c < C; c += NT / 64) {
     float acc = 0.f;
     for (int d = lane; d < D; d += 64) acc = fmaf(pl[d], Wout[(int64_t)c * D + d], acc);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-    if (lane == 0) logits[g * C + c] = acc + (bout ? bout[c] : 0.f);
+    const float z = acc + (bout ? bout[c] : 0.f);
+    if (lane == 0) logits[g * C + c] = z;
+    if (CE && lane == 0) zl[c] = z;
+  }
+  if constexpr (CE) {
+    __syncthreads();
+    __shared__ int last;
+    if (threadIdx.x == 0) {
+      float m = -INFINITY;
+      for (int c = 0; c < C; ++c) m = fmaxf(m, zl[c]);
+      float sx = 0.f;
+      for (int c = 0; c < C; ++c) sx += expf(zl[c] - m);
+      const float l = m + logf(sx);
+      ce.lse[g] = l;
+      const int64_t t = ce.y[g];
+      float num = 0.f, den = 0.f;
+      unsigned int badv = 0u;
+      if (t < 0 || t >= C) {
+        badv = 1u;
+      } else {
+        const float wt = ce.w ? ce.w[t] : 1.f;
+        num = wt * (l - zl[t]);
+        den = wt;
+      }
+      const unsigned int r0 = __float_as_uint(__hip_atomic_exchange(
+          ce.part + 2 * g, num, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      const unsigned int r1 = __float_as_uint(__hip_atomic_exchange(
+          ce.part + 2 * g + 1, den, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      const unsigned int rb = __hip_atomic_fetch_or(ce.ticket + 9, badv, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+      last = last_workgroup(ce.ticket, ticket_after(r0 ^ r1 ^ rb));
+    }
+    __syncthreads();
+    if (!last) return;
+    // k_ce_fwd's order: virtual thread v (of 1024) sums rows v, v + 1024, ...; each virtual wave
+    // (64 consecutive v) folds by the xor tree; the 16 wave sums add in order
+    __shared__ float rn[16], rd[16];
+    for (int j = 0; j < 4; ++j) {
+      const int v = 256 * j + threadIdx.x;
+      float n = 0.f, d = 0.f;
+      for (int64_t i = v; i < ce.B; i += 1024) {
+        const float pn = __hip_atomic_load(ce.part + 2 * i, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+        const float pd = __hip_atomic_load(ce.part + 2 * i + 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+        const int64_t t = ce.y[i];
+        if (t < 0 || t >= C) continue;  // k_ce_fwd skips such rows
+        n += pn;
+        d += pd;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+      if (lane == 0) {
+        rn[4 * j + wave] = n;
+        rd[4 * j + wave] = d;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float tn = 0.f, td = 0.f;
+      for (int q = 0; q < 16; ++q) tn += rn[q];
+      for (int q = 0; q < 16; ++q) td += rd[q];
+      ce.loss[0] = tn / td;
+      ce.wsum[0] = td;
+      ce.bad[0] = (int)__hip_atomic_load(ce.ticket + 9, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ce.ticket + 9, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -287,12 +375,34 @@ extern "C" int lgnn_pool_head_fwd(const float* H, const int32_t* gptr, int64_t B
   if (Wout && (C <= 0 || !logits)) return LGNN_EINVAL;
   if (B == 0) return LGNN_OK;
   if ((D & 3) == 0)
-    hipLaunchKernelGGL(k_pool_head_fwd4, dim3((unsigned)B), dim3(NT), 0, as_stream(stream), H,
-                       gptr, D, pool_mean, Wout, bout, C, pooled, logits);
+    hipLaunchKernelGGL(k_pool_head_fwd4<false>, dim3((unsigned)B), dim3(NT), 0, as_stream(stream),
+                       H, gptr, D, pool_mean, Wout, bout, C, pooled, logits, CeFwd{});
   else
     hipLaunchKernelGGL(k_pool_head_fwd, dim3((unsigned)((B + 3) / 4)), dim3(NT), 0,
                        as_stream(stream), H, gptr, B, D, pool_mean, Wout, bout, C, pooled,
                        logits);
+  LGNN_LAUNCH_CHECK();
+  return LGNN_OK;
+}
+
+extern "C" size_t lgnn_pool_head_ce_workspace_bytes(int64_t B) {
+  return B < 0 ? 0 : (size_t)B * 2 * sizeof(float);
+}
+
+extern "C" int lgnn_pool_head_ce_fwd(const float* H, const int32_t* gptr, int64_t B, int D,
+                                     int pool_mean, const float* Wout, const float* bout, int C,
+                                     float* pooled, float* logits, const int64_t* target,
+                                     const float* weight, float* lse, float* loss, float* wsum,
+                                     int* bad, unsigned int* ticket, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
+  if (B < 1 || D <= 0 || D > 512 || (D & 3) != 0 || !gptr || !pooled || !Wout || !logits ||
+      C < 1 || C > 16 || !target || !lse || !loss || !wsum || !bad || !ticket || !workspace)
+    return LGNN_EINVAL;
+  if (workspace_bytes < lgnn_pool_head_ce_workspace_bytes(B)) return LGNN_ENOSPC;
+  hipStream_t s = as_stream(stream);
+  const CeFwd ce{target, weight, lse, static_cast<float*>(workspace), ticket, loss, wsum, bad, B};
+  hipLaunchKernelGGL(k_pool_head_fwd4<true>, dim3((unsigned)B), dim3(NT), 0, s, H, gptr, D,
+                     pool_mean, Wout, bout, C, pooled, logits, ce);
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
 }

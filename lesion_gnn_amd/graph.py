@@ -148,7 +148,9 @@ class Graph:
 
     def build_path(self, kind: str) -> str:
         """Which launches the last eager build of `kind` took: "sorted" (the target-sorted fast
-        path: k-NN input grouped by target) or "general" (the counting sort). Synchronises.
+        path: k-NN input grouped by target), "sorted_open" (target-sorted, but an edge leaves its
+        64-row tile: the sorted path writes the target CSR, the counting sort only the source
+        CSR) or "general" (the counting sort for both). Synchronises.
         Needs keep_build_workspace set before the build."""
         k, ws = getattr(self, "_last_ws", (None, None))
         if k != kind:
@@ -157,7 +159,7 @@ class Graph:
         r = _lib.load().lgnn_graph_build_path(_lib.ptr(ws), self.num_nodes, self.num_edges,
                                               _lib.stream(self.device))
         _lib.check(r if r < 0 else 0, "lgnn_graph_build_path")
-        return "sorted" if r == 1 else "general"
+        return {1: "sorted", 2: "sorted_open"}.get(r, "general")
 
     def weighted(self, edge_weight: torch.Tensor) -> str:
         """Register the CSR pair carrying per-edge weights `edge_weight` [E] (edge order, e.g.

@@ -473,6 +473,36 @@ def pool_head_fwd(H: torch.Tensor, graph: Graph, mean: bool, Wout=None, bout=Non
     return pooled, logits
 
 
+_CE_TICKETS: dict = {}
+
+
+def pool_head_ce_fwd(H: torch.Tensor, graph: Graph, mean: bool, Wout, bout, y, weight):
+    """pool_head_fwd + the CE criterion's forward in one launch (lgnn_pool_head_ce_fwd), or None
+    when the shape is off that kernel (then the caller runs the two launches). Returns
+    (pooled, logits, lse, out[loss, wsum], bad)."""
+    B, D = graph.num_graphs, H.size(1)
+    C = Wout.size(0)
+    if B < 1 or D % 4 or D > 512 or not 1 <= C <= 16 or pool_splits(B, H.size(0), D) > 1:
+        return None
+    dev = H.device
+    key = torch.device(dev).index
+    tk = _CE_TICKETS.get(key)
+    if tk is None:  # zeroed once, re-armed by every launch
+        tk = _CE_TICKETS[key] = torch.zeros(10, dtype=torch.int32, device=dev)
+    pooled = torch.empty(B, D, dtype=torch.float32, device=dev)
+    logits = torch.empty(B, C, dtype=torch.float32, device=dev)
+    lse = torch.empty(B, dtype=torch.float32, device=dev)
+    out = torch.empty(2, dtype=torch.float32, device=dev)
+    bad = torch.empty(1, dtype=torch.int32, device=dev)
+    ws = torch.empty(_lib.load().lgnn_pool_head_ce_workspace_bytes(B), dtype=torch.uint8,
+                     device=dev)
+    _lib.call("lgnn_pool_head_ce_fwd", _lib.ptr(H), _lib.ptr(graph.gptr), B, D, int(mean),
+              _lib.ptr(Wout), _lib.ptr(bout), C, _lib.ptr(pooled), _lib.ptr(logits), _lib.ptr(y),
+              _lib.ptr(weight), _lib.ptr(lse), _lib.ptr(out), _lib.ptr(out) + 4, _lib.ptr(bad),
+              _lib.ptr(tk), _lib.ptr(ws), ws.numel(), _s(dev))
+    return pooled, logits, lse, out, bad
+
+
 def pool_head_bwd(dlogits: torch.Tensor, pooled: torch.Tensor, Wout: torch.Tensor):
     B, D = pooled.shape
     C = Wout.size(0)
@@ -973,7 +1003,9 @@ class _GCNStack(torch.autograd.Function):
         return logits
 
     @staticmethod
-    def _fwd(ctx, x, graph, mean, L, params):
+    def _fwd(ctx, x, graph, mean, L, params, ce=None):
+        """ce = (y int64, weight | None): the readout also runs the CE forward where the kernel
+        takes the shape (ctx.ce_fwd = (lse, out) then; None otherwise)."""
         _lib.require_gpu(x, *params)
         x = _f32c(x)
         params = [_f32c(p) for p in params]
@@ -1010,7 +1042,13 @@ class _GCNStack(torch.autograd.Function):
                 ss.append(s_)
                 ctx.saved_s.append(fast)
         W_out, b_out = params[2 + 2 * L], params[3 + 2 * L]
-        pooled, logits = pool_head_fwd(hs[-1], graph, mean, W_out, b_out)
+        ctx.ce_fwd = None
+        r = pool_head_ce_fwd(hs[-1], graph, mean, W_out, b_out, *ce) if ce is not None else None
+        if r is not None:
+            pooled, logits, lse, out, _ = r
+            ctx.ce_fwd = (lse, out)
+        else:
+            pooled, logits = pool_head_fwd(hs[-1], graph, mean, W_out, b_out)
         ctx.graph, ctx.mean, ctx.L = graph, mean, L
         ctx.n_saved = 2 + len(hs) + len(ss) + len(params)
         return logits, (x, pooled, *hs, *ss, *params)
@@ -1111,17 +1149,22 @@ class _GCNStackCE(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, graph, mean, L, y, weight, *params):
         ctx.set_materialize_grads(False)
-        logits, to_save = _GCNStack._fwd(ctx, x, graph, mean, L, params)
-        z = logits
         yy = y.to(torch.int64).contiguous()
-        B, C = z.shape
-        dev = z.device
-        lse = torch.empty(B, dtype=torch.float32, device=dev)
-        out = torch.empty(2, dtype=torch.float32, device=dev)  # loss, sum of weights
-        bad = torch.empty(1, dtype=torch.int32, device=dev)
         w = _f32c(weight) if weight is not None else None
-        _lib.call("lgnn_ce_fwd", _lib.ptr(z), _lib.ptr(yy), _lib.ptr(w), B, C, _lib.ptr(lse),
-                  _lib.ptr(out), _lib.ptr(out) + 4, _lib.ptr(bad), _s(dev))
+        # the readout runs the CE forward too (one launch) where its kernel takes the shape
+        logits, to_save = _GCNStack._fwd(ctx, x, graph, mean, L, params, ce=(yy, w))
+        z = logits
+        if ctx.ce_fwd is not None:
+            lse, out = ctx.ce_fwd
+        else:
+            B, C = z.shape
+            dev = z.device
+            lse = torch.empty(B, dtype=torch.float32, device=dev)
+            out = torch.empty(2, dtype=torch.float32, device=dev)  # loss, sum of weights
+            bad = torch.empty(1, dtype=torch.int32, device=dev)
+            _lib.call("lgnn_ce_fwd", _lib.ptr(z), _lib.ptr(yy), _lib.ptr(w), B, C,
+                      _lib.ptr(lse), _lib.ptr(out), _lib.ptr(out) + 4, _lib.ptr(bad), _s(dev))
+        ctx.ce_fwd = None
         ctx.has_w = w is not None
         ctx.save_for_backward(*to_save, z, yy, lse, out, *((w,) if w is not None else ()))
         return logits, out[0]

@@ -438,7 +438,8 @@ def test_lazy_transpose_build(cuda, case):
     nt = (b.num_nodes + 63) // 64
     n_open = int(to_lazy[nt])
     assert (n_open == 0) == (case == "aligned")
-    assert g.build_path("gcn_lazy") == ("sorted" if case == "aligned" else "general")
+    assert g.build_path("gcn_lazy") == {"aligned": "sorted", "ragged": "sorted_open",
+                                        "capacity": "general"}[case]
     if n_open:
         assert int(full.tptr[-1]) == nnz
         assert torch.equal(full.tptr, lazy.tptr)

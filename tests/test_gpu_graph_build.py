@@ -92,9 +92,18 @@ def _sorted_cases():
         "k17": ((k17.edge_index, k17.num_nodes), "general"),
         "two_loops": ((two, n), "general"),
         "trailing_gap": ((ei, n + 200), "general"),
+        # ragged graphs: target-sorted, but edges leave their 64-row tiles (the lazy build then
+        # needs the source CSR): the sorted body writes the target CSR, the counting sort the
+        # source CSR only ("sorted_open", the C5 / reference-config case)
         "lognormal": ((synth.make_batch(100, k=6, seed=9, sizes="lognormal").edge_index,
                        synth.make_batch(100, k=6, seed=9, sizes="lognormal").num_nodes),
-                      "general"),
+                      "sorted_open"),
+        "powerlaw_k4": ((synth.make_batch(40, k=4, seed=10, sizes="powerlaw").edge_index,
+                         synth.make_batch(40, k=4, seed=10, sizes="powerlaw").num_nodes),
+                        "sorted_open"),
+        "powerlaw_k16": ((synth.make_batch(24, k=16, seed=11, sizes="powerlaw").edge_index,
+                          synth.make_batch(24, k=16, seed=11, sizes="powerlaw").num_nodes),
+                         "sorted_open"),
         "unsorted": ((ei[:, torch.randperm(ei.size(1),
                                            generator=torch.Generator().manual_seed(1))], n),
                      "general"),
