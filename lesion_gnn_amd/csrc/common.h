@@ -110,6 +110,8 @@ struct CeSrc {
   int C;
 };
 __device__ __forceinline__ float ce_dlogit(const CeSrc& s, int64_t i, int c) {
+  // rounded as a stored dlogits value is: no FMA contraction into the consumer's sum
+#pragma clang fp contract(off)
   const int64_t t = s.y[i];
   const float wt = (t >= 0 && t < s.C) ? (s.w ? s.w[t] : 1.f) : 0.f;
   const float p = expf(s.z[i * s.C + c] - s.lse[i]);
