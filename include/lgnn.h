@@ -617,6 +617,19 @@ int lgnn_adam_step(int n, float* const* params, const float* const* grads, float
                    unsigned int* ticket, float lr, float beta1, float beta2, float eps,
                    float weight_decay, int decoupled, int maximize, int advance,
                    void* stream);
+/* lgnn_adam_step that also writes the split-3 weight planes of updated weights (ABI v34): for
+ * every tensor i with planes[i] != NULL (a [rows[i]][cols[i]] weight, both <= 128) the new
+ * values' three bf16 planes go to planes[i] (lgnn_weight_planes' layout of that layer: 3 planes
+ * of 128 x 128, fragment order, feature order perm16) and, when planes_t[i] != NULL, the
+ * transposed planes to planes_t[i] — bitwise what lgnn_weight_planes writes from the new
+ * weights (padding positions are left as they are: the caller's planes hold zeros there). The
+ * next forward then needs no weight-plane launch. */
+int lgnn_adam_step_planes(int n, float* const* params, const float* const* grads,
+                          float* const* exp_avg, float* const* exp_avg_sq, const int64_t* numels,
+                          float* step, unsigned int* ticket, float lr, float beta1, float beta2,
+                          float eps, float weight_decay, int decoupled, int maximize, int advance,
+                          uint16_t* const* planes, uint16_t* const* planes_t, const int* rows,
+                          const int* cols, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Fused GCN stack backward on split-3 bf16 MFMA (fp32 accuracy), every layer of a tile in one

@@ -63,6 +63,8 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_s3f_set_waves": (I32, [I32]),
     "lgnn_adam_step": (I32, [I32, P, P, P, P, P, P, P, F32, F32, F32, F32, F32, I32, I32, I32,
                              P]),
+    "lgnn_adam_step_planes": (I32, [I32, P, P, P, P, P, P, P, F32, F32, F32, F32, F32, I32, I32,
+                                    I32, P, P, P, P, P]),
     "lgnn_gcn_stack_bwd": (I32, [P, P, P, I32, P, P, P, P, I64, I32, P, P, P, P, P, I32, P, P]),
     "lgnn_spmm": (I32, [P, P, P, F32, P, I64, I32, P, P]),
     "lgnn_reduce_partials_multi": (I32, [I32, P, P, P, P, P]),

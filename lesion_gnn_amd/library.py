@@ -795,10 +795,11 @@ def _gcn_layout(params, L):
 def gcn_stack(x: Tensor, g: list[Tensor], mean: bool, L: int,
               params: list[Tensor]) -> list[Tensor]:
     """[logits, pooled, H_0..H_L, S_1..S_L, planes_t or none] (the eager _GCNStack forward)."""
-    from .ops import _GCNStack
+    from .ops import _GCNStack, no_plane_cache
 
     ctx = _Ctx()
-    logits = _GCNStack.forward(ctx, x, TGraph(g, "gcn"), mean, L, *params)
+    with no_plane_cache():  # the op's planes output is a fresh buffer (planes + Â^T room)
+        logits = _GCNStack.forward(ctx, x, TGraph(g, "gcn"), mean, L, *params)
     sv = ctx.saved_tensors
     hs = list(sv[2:3 + L])
     ss = [s if s.data_ptr() != x.data_ptr() and all(s.data_ptr() != h.data_ptr() for h in hs)

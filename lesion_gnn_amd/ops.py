@@ -162,6 +162,93 @@ def weight_planes(Ws: list, d_in: int, transposed: bool = False, extra: int = 0)
     return planes, planes_t
 
 
+# Split-3 weight planes kept across steps (LGNN_PLANE_CACHE=0: made afresh by every forward).
+# An entry holds the planes of one weight list, valid while every weight keeps the version it had
+# when the planes were made. lesion_gnn_amd.optim.Adam rewrites the planes of the weights it
+# updates in the same launch (lgnn_adam_step_planes) and, writing the weights through their
+# pointers, leaves their versions alone: the next forward then runs no weight-plane launch. Any
+# other in-place update (torch's optimizers, load_state_dict, copy_) bumps a version and the next
+# forward makes the planes afresh. Writes through `.data` bypass version counters: call
+# invalidate_weight_planes() after such a write.
+PLANE_CACHE = os.environ.get("LGNN_PLANE_CACHE", "1") != "0"
+_PLANES: dict = {}     # (weight pointers, d_in, transposed) -> _PlaneEntry
+_PLANE_REG: dict = {}  # weight data_ptr -> (_PlaneEntry, layer index)
+
+
+class _PlaneEntry:
+    __slots__ = ("planes", "planes_t", "refs", "versions", "shapes")
+
+    def __init__(self, Ws, planes, planes_t):
+        self.planes, self.planes_t = planes, planes_t
+        self.refs = [weakref.ref(W) for W in Ws]
+        self.versions = [W._version for W in Ws]
+        self.shapes = [tuple(W.shape) for W in Ws]
+
+    def valid(self, Ws) -> bool:
+        return len(Ws) == len(self.refs) and all(
+            r() is W and W._version == v and tuple(W.shape) == sh
+            for r, W, v, sh in zip(self.refs, Ws, self.versions, self.shapes))
+
+
+_NO_CACHE = [0]  # > 0 inside no_plane_cache()
+
+
+class no_plane_cache:
+    """Context: stack forwards make fresh planes (with the Â^T room after them) — the compiled
+    lgnn::gcn_stack op returns that buffer as an output of its own."""
+
+    def __enter__(self):
+        _NO_CACHE[0] += 1
+
+    def __exit__(self, *exc):
+        _NO_CACHE[0] -= 1
+
+
+def invalidate_weight_planes() -> None:
+    """Drop every cached weight-plane entry (after writing weights through `.data`)."""
+    _PLANES.clear()
+    _PLANE_REG.clear()
+
+
+def cached_weight_planes(Ws: list, d_in: int, transposed: bool):
+    """weight_planes(Ws, d_in, transposed) kept across steps (PLANE_CACHE): one lgnn_weight_planes
+    launch when the weights changed other than through lesion_gnn_amd.optim.Adam, none
+    otherwise. The returned tensors are shared with the cache (the optimizer rewrites them)."""
+    if not PLANE_CACHE or torch.compiler.is_compiling():
+        return weight_planes(Ws, d_in, transposed)
+    key = (tuple(W.data_ptr() for W in Ws), int(d_in), bool(transposed))
+    e = _PLANES.get(key)
+    if e is not None and e.valid(Ws):
+        return e.planes, e.planes_t
+    planes, planes_t = weight_planes(Ws, d_in, transposed)
+    e = _PlaneEntry(Ws, planes, planes_t)
+    if len(_PLANES) >= 16:  # a few weight sets per process; drop the oldest
+        old = _PLANES.pop(next(iter(_PLANES)))
+        for k in [k for k, (ent, _) in _PLANE_REG.items() if ent is old]:
+            del _PLANE_REG[k]
+    _PLANES[key] = e
+    for l, W in enumerate(Ws):
+        _PLANE_REG[W.data_ptr()] = (e, l)
+    return planes, planes_t
+
+
+def plane_targets(p: torch.Tensor):
+    """(planes ptr, planes_t ptr or None) of parameter p's layer in a valid cache entry, or None:
+    where lesion_gnn_amd.optim.Adam writes p's new planes."""
+    if not PLANE_CACHE:
+        return None
+    hit = _PLANE_REG.get(p.data_ptr())
+    if hit is None:
+        return None
+    e, l = hit
+    r = e.refs[l]()
+    if r is not p or p._version != e.versions[l] or tuple(p.shape) != e.shapes[l]:
+        return None
+    per = 3 * 128 * 128 * 2  # bytes of one layer's three planes
+    return (e.planes.data_ptr() + l * per,
+            e.planes_t.data_ptr() + l * per if e.planes_t is not None else None)
+
+
 def adjt_numel(M) -> int:
     """int16 elements of the Â^T planes the split-3 forward hands to the fused backward."""
     return (M + 63) // 64 * (_lib.LGNN_S3_ADJT_TILE_BYTES // 2)
@@ -210,11 +297,20 @@ def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list, keep: dict | No
     if MFMA_MODE == "s3" and L >= 1:
         # the transposed planes (the split-3 backward's dH = G W_l operand) come from the same
         # launch when the caller keeps them
-        extra = adjt_numel(M) if keep is not None and _s3f(L) and ADJT else 0
-        planes, planes_t = weight_planes(Ws, x.size(1), transposed=keep is not None, extra=extra)
-        adjt = _adjt_ptr(planes_t, L) if extra else None
+        want_adjt = keep is not None and _s3f(L) and ADJT
+        if PLANE_CACHE and not _NO_CACHE[0]:  # cached planes; the Â^T tiles in their own buffer
+            planes, planes_t = cached_weight_planes(Ws, x.size(1), transposed=keep is not None)
+            adjt_t = torch.empty(adjt_numel(M), dtype=torch.int16, device=dev) \
+                if want_adjt else None
+            adjt = _lib.ptr(adjt_t)
+        else:  # fresh planes with the Â^T tiles after them (the compiled op's one output)
+            extra = adjt_numel(M) if want_adjt else 0
+            planes, planes_t = weight_planes(Ws, x.size(1), transposed=keep is not None,
+                                             extra=extra)
+            adjt_t, adjt = None, (_adjt_ptr(planes_t, L) if extra else None)
         if keep is not None:
             keep["planes_t"] = planes_t
+            keep["adjt"] = adjt_t
         if _open_in_fused(OPEN_IN_FUSED, graph, "fwd"):  # open tiles in the same launch
             _lib.call("lgnn_gcn_stack_fwd_s3_all", _lib.ptr(x), M, x.size(1), 1,
                       _lib.ptr(csr.rowptr), _lib.ptr(csr.col), _lib.ptr(csr.w), L,
@@ -250,7 +346,7 @@ def head_in_stack_bwd(graph: Graph, L: int, C: int, s3: bool) -> bool:
 
 def stack_bwd(dp: torch.Tensor | None, x: torch.Tensor, graph: Graph, mean: bool, Ws: list,
               hs: list, ss: list, reducer: list, planes_t: torch.Tensor | None = None,
-              head: tuple | None = None, kind: str = "gcn"):
+              head: tuple | None = None, kind: str = "gcn", adjt_t: torch.Tensor | None = None):
     """Backward of stack_fwd from the pooled-output gradient dp down to in_proj, L = 1 or 2
     convs, no input gradient. Closed tiles run fused (lgnn_gcn_stack_bwd, one launch); open
     tiles layer by layer (lgnn_node_linear_bwd_tiles, want_open = 1, accumulate = 1) into the
@@ -264,7 +360,9 @@ def stack_bwd(dp: torch.Tensor | None, x: torch.Tensor, graph: Graph, mean: bool
     lib = _lib.load()
     s3 = planes_t is not None
     s3f = s3 and _s3f(L)
-    adjt = _adjt_ptr(planes_t, L) if s3f else None
+    # the forward's Â^T tiles: their own buffer (adjt_t), or room after the planes (weight_planes'
+    # `extra`); none -> the backward rebuilds them from the CSR
+    adjt = (_lib.ptr(adjt_t) if adjt_t is not None else _adjt_ptr(planes_t, L)) if s3f else None
     P = lib.lgnn_gcn_stack_bwd_s3_partials(M) if s3 and not s3f else \
         lib.lgnn_gcn_stack_bwd_partials(M)
     _lib.check(0 if P > 0 else P, "lgnn_gcn_stack_bwd_partials")
@@ -1022,10 +1120,12 @@ class _GCNStack(torch.autograd.Function):
         csr = graph.csr(kind)
         ctx.fused = fused
         ctx.planes_t = None
+        ctx.adjt = None
         if fused:
             hs, ss = stack_fwd(x, graph, Ws, [params[2 * l + 1] for l in range(L + 1)], keep,
                                kind)
             ctx.planes_t = keep.get("planes_t") if keep else None
+            ctx.adjt = keep.get("adjt") if keep else None
             ctx.saved_s = [True] * L
         else:
             hs = [linear_fwd(x, W_in, b_in, _lib.LGNN_ACT_NONE)]
@@ -1093,11 +1193,12 @@ class _GCNStack(torch.autograd.Function):
                 part = CE_PART if ce is not None else dlogits
                 red += [(part, B, C * D, dWo, pooled, D), (part, B, C, dbo)]
                 outs = stack_bwd(None, x, graph, ctx.mean, Ws, hs, ss, red, ctx.planes_t,
-                                 head=(ce[0] if ce is not None else dlogits, W_out), kind=kind)
+                                 head=(ce[0] if ce is not None else dlogits, W_out), kind=kind,
+                                 adjt_t=getattr(ctx, "adjt", None))
             else:
                 dp, dWo, dbo = pool_head_bwd(dlogits, pooled, W_out)
                 outs = stack_bwd(dp, x, graph, ctx.mean, Ws, hs, ss, red, ctx.planes_t,
-                                 kind=kind)
+                                 kind=kind, adjt_t=getattr(ctx, "adjt", None))
             grads[2 + 2 * L], grads[3 + 2 * L] = dWo, dbo
             for l, (dW, db) in enumerate(outs):
                 grads[2 * l], grads[2 * l + 1] = dW, db

@@ -77,8 +77,9 @@ def run():
         os.environ["LGNN_S3F_WAVES"] = "8" if v in WAVES8 else "4"
         lib = ctypes.CDLL(LIB % v)
         for name, (res, args) in _lib.SIGNATURES.items():
-            f = getattr(lib, name)
-            f.restype, f.argtypes = res, args
+            f = getattr(lib, name, None)  # a variant built from an older source may lack some
+            if f is not None:
+                f.restype, f.argtypes = res, args
         P = lib.lgnn_gcn_stack_bwd_partials(M)
         slabs = [torch.empty(P * (D * D + D), device=dev) for _ in range(L + 1)]
         dWp = arr(*[t.data_ptr() for t in slabs])
