@@ -614,6 +614,52 @@ __device__ __forceinline__ u32x2 quad_transpose_bf16(uint32_t w0, uint32_t w1, i
   return u32x2{b1 ? r : a, b1 ? b : r};
 }
 
+// Â^T planes of a tile from the fp32 scratch the forward handed over (AG): each thread reads its
+// 16 targets of one source row (a wave reads 64 different banks) and splits them into the three
+// planes; adj_write (after a barrier: the planes overwrite the scratch) stores them
+struct AdjPlanes {
+  uint32_t q[3][8];
+};
+__device__ __forceinline__ AdjPlanes adj_split(FBwdSmem& sm) {
+  const float* scr = reinterpret_cast<const float*>(sm.Adj[0]);
+  const int tq = fresh_tid();
+  const int am = tq & 63, aq = tq >> 6;
+  float f[16];
+#pragma unroll
+  for (int y = 0; y < 16; ++y) f[y] = scr[(16 * aq + perm16(y)) * TM + am];
+  AdjPlanes o;
+  uint32_t inexact = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const Split2 s2 = split2(f[2 * i], f[2 * i + 1]);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) o.q[p][i] = s2.p[p];
+    inexact |= s2.p[1] | s2.p[2];
+  }
+  // sm.flag: set when some Â weight of the tile is inexact in bf16 (cleared before)
+  if (__any(inexact != 0) && (tq & 63) == 0) sm.flag = 1;
+  return o;
+}
+__device__ __forceinline__ void adj_write(FBwdSmem& sm, const AdjPlanes& o) {
+  const int tq = fresh_tid();
+  const int am = tq & 63, aq = tq >> 6;
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    unsigned char* dst = sm.Adj[p] + am * ADJ_LD * 2 + 32 * aq;
+    *reinterpret_cast<u32x4*>(dst) = u32x4{o.q[p][0], o.q[p][1], o.q[p][2], o.q[p][3]};
+    *reinterpret_cast<u32x4*>(dst + 16) = u32x4{o.q[p][4], o.q[p][5], o.q[p][6], o.q[p][7]};
+  }
+}
+
+// AG: the next tile's Â^T planes are split during this tile's in_proj phase (VALU and LDS work
+// beside the dW_0 MFMAs) instead of in the next tile's prologue; -DLGNN_S3F_NOPIPE: in the
+// prologue (the round-3 order; A/B builds only)
+#ifdef LGNN_S3F_NOPIPE
+constexpr bool kAdjPipe = false;
+#else
+constexpr bool kAdjPipe = true;
+#endif
+
 template <int NL, bool AG>
 __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ rowptr,
                                                    const int32_t* __restrict__ col,
@@ -686,6 +732,16 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
       idx_load_body(R, col, w);
     }
   }
+  if constexpr (AG && kAdjPipe) {  // the first tile's Â^T planes (later tiles': in_proj phase)
+    if (t < ntiles) {
+      if (fresh_tid() == 0) sm.flag = 0;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_barrier();
+      const AdjPlanes ap = adj_split(sm);
+      lds_barrier();
+      adj_write(sm, ap);
+    }
+  }
   for (; t < ntiles;) {
     STAMP(stamp++);
     const int64_t r0 = t * TM;
@@ -698,7 +754,9 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
         for (int i = 0; i < TM * TM / 4 / NT; ++i) st4(scr + 4 * (tq + i * NT), zero4());
         if (tq <= TM) sm.rp[tq] = R.rp;
       }
-      if (tq == 0) sm.flag = 0;  // set below when some Â weight of the tile is inexact in bf16
+      // set below when some Â weight of the tile is inexact in bf16 (pipelined: set while the
+      // previous tile split this one's planes)
+      if (!(AG && kAdjPipe) && tq == 0) sm.flag = 0;
       if (tq < TM) {
         const int64_t row = r0 + tq;
         const int64_t g = pre_g;
@@ -774,31 +832,12 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
     STAMP(stamp++);
     if constexpr (AG) {
       // (every wave's Â loads landed before the barrier above)
-      // Â^T planes: row am = source, positions perm16 of targets 16 aq .. (a wave reads 64
-      // different banks)
-      const int tq = fresh_tid();
-      const int am = tq & 63, aq = tq >> 6;
-      float f[16];
-#pragma unroll
-      for (int y = 0; y < 16; ++y) f[y] = scr[(16 * aq + perm16(y)) * TM + am];
-      uint32_t q[3][8];
-      uint32_t inexact = 0;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const Split2 s2 = split2(f[2 * i], f[2 * i + 1]);
-#pragma unroll
-        for (int p = 0; p < 3; ++p) q[p][i] = s2.p[p];
-        inexact |= s2.p[1] | s2.p[2];
+      if constexpr (!kAdjPipe) {
+        const AdjPlanes ap = adj_split(sm);
+        lds_barrier();  // every scratch read done (the planes overwrite it)
+        adj_write(sm, ap);
+        lds_barrier();
       }
-      if (__any(inexact != 0) && (tq & 63) == 0) sm.flag = 1;
-      lds_barrier();  // every scratch read done (the planes overwrite it)
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        unsigned char* dst = sm.Adj[p] + am * ADJ_LD * 2 + 32 * aq;
-        *reinterpret_cast<u32x4*>(dst) = u32x4{q[p][0], q[p][1], q[p][2], q[p][3]};
-        *reinterpret_cast<u32x4*>(dst + 16) = u32x4{q[p][4], q[p][5], q[p][6], q[p][7]};
-      }
-      lds_barrier();
     } else {
     lds_barrier();  // Â^T summed
     {
@@ -1049,6 +1088,14 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
     // in_proj: db_0, dW_0 += dZ_0^T X
     {
       const int K = a.width[0];
+      // (pipelined Â: unconditional — a branch around these barriers and stores made the
+      // register allocator spill ~116 VGPRs; past the last tile the planes written are unused)
+      if constexpr (AG && kAdjPipe) {
+        // the next tile's Â (issued at the last conv, long landed) and H_L rows: complete before
+        // the barrier below, so every wave can split the Â planes beside the dW_0 products
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (fresh_tid() == 0) sm.flag = 0;
+      }
       {
         const int tq = fresh_tid();
         const int h = (tq >> 5) & 1, li = tq & 31, k = 32 * (tq >> 6) + li;
@@ -1079,6 +1126,7 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
         }
       }
       lds_barrier();
+      AdjPlanes nap;  // the next tile's Â^T planes (pipe)
       {
         u32x4 gp[4][3];
         split_p(dz, gp);
@@ -1094,10 +1142,20 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
             for (int p = 0; p < 3; ++p) hb[p] = lds16(sm.Img[p] + off);
             if constexpr (!(ABL & 1)) dw[0][kb] = mfma_s3(gp[s], hb, dw[0][kb]);
           }
+          // the next tile's Â split beside the products (independent VALU / LDS work)
+          if constexpr (AG && kAdjPipe) {
+            // (unconditional: without a next tile the planes are not written, and its flag
+            // word is never read)
+            if (s == 1) nap = adj_split(sm);
+          }
           S3F_SB();
         }
       }
-      lds_barrier();  // X image read; the next tile may overwrite LDS
+      lds_barrier();  // X image read (and the Â scratch); the next tile may overwrite LDS
+      if constexpr (AG && kAdjPipe) {
+        adj_write(sm, nap);
+        lds_barrier();  // the next tile's Â^T planes are in place
+      }
       STAMP(stamp++);
     }
     t = tn;
