@@ -297,14 +297,12 @@ def time_dominant_kernels(model, b, dev):
         C = W_out.size(0)
         z = torch.randn(b.num_graphs, C, device=dev)
         y = b.y.to(dev)
-        lse = torch.empty(b.num_graphs, device=dev)
-        ce_out = torch.empty(2, device=dev)
-        bad = torch.empty(1, dtype=torch.int32, device=dev)
+        # the readout's CE factors (lgnn_pool_head_ce_fwd): pm = softmax(z) - onehot(y), wt = 1
+        pm = (torch.softmax(z, 1) - torch.nn.functional.one_hot(y.long(), C).float()).contiguous()
+        wt = torch.ones(b.num_graphs, device=dev)
+        ce_out = torch.full((2,), float(b.num_graphs), device=dev)
         gloss = torch.ones(1, device=dev)
-        _lib.call("lgnn_ce_fwd", z.data_ptr(), y.data_ptr(), None, b.num_graphs, C,
-                  lse.data_ptr(), ce_out.data_ptr(), ce_out.data_ptr() + 4, bad.data_ptr(), s)
-        ce = _lib.CeSrc(z.data_ptr(), lse.data_ptr(), y.data_ptr(), None, ce_out.data_ptr() + 4,
-                        gloss.data_ptr())
+        ce = _lib.CeSrc(pm.data_ptr(), wt.data_ptr(), ce_out.data_ptr() + 4, gloss.data_ptr())
         dS_ws = torch.empty(2 * M * 128, dtype=torch.float32, device=dev)
         Sp = (ctypes.c_void_p * L)(*[x.data_ptr() for x in hs[1:]])  # open tiles only (none)
 

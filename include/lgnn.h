@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 34
+#define LGNN_ABI_VERSION 35
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -255,6 +255,23 @@ int lgnn_reduce_jobs(int n, const float* const* partials, const float* const* fa
                      float* const* out, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * Windowed dense aggregation (ABI v35), the layer-wise GCN path's open tiles:
+ *   out[r] = sum_{e in row r} w_e in[col_e]   for the rows of the 64-row tiles t with
+ *   (tile_mask[t] != 0) == (want != 0) (tile_mask NULL: every tile); other rows untouched.
+ * Replaces the per-entry row gather of GCNConv's propagate (reference gin.py / PyG
+ * MessagePassing.propagate, aggr='add' over gcn_norm weights) for graphs that straddle tiles:
+ * each tile multiplies the dense 64 x 64 blocks of its entries per 64-row source chunk by that
+ * chunk's rows (split-3 bf16 MFMA, fp32 accuracy; the per-row sum is not in CSR order). Chunks
+ * whose tile is not selected are never read (an edge between two tiles marks both open). Tiles
+ * whose sources span more than max_chunks chunks, or with more than 2048 entries, take the
+ * per-row gather (CSR order). width must be 128 (row stride of in / out). w NULL: weight 1.
+ * Called with the transpose CSR (tptr, tidx, tw) it is the aggregation's backward, A_hat^T dY.
+ * ------------------------------------------------------------------------------------------- */
+int lgnn_window_aggregate(const int32_t* rowptr, const int32_t* col, const float* w, int64_t M,
+                          const float* in, int width, float* out, const int32_t* tile_mask,
+                          int want, int max_chunks, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
  * Sparse aggregation alone (no linear): Y_i = self_scale*X_i + sum_{e in row i} w_e X[col_e].
  * Replaces: torch_sparse spmm(adj_t, x, 'sum') / PyG propagate(aggr='add') (GINConv, and the
  * transposed pass of every conv backward when called with the transpose CSR).
@@ -277,14 +294,18 @@ int lgnn_pool_head_fwd(const float* H, const int32_t* gptr, int64_t B, int D, in
  * nn.CrossEntropyLoss(weight), mean reduction (reference models/base.py:93-94) — lgnn_ce_fwd's
  * outputs and arithmetic, bitwise: lse [B], loss [1], wsum [1], bad [1] (1 if a target is outside
  * [0, C); such graphs skipped). The last workgroup to finish sums the per-graph terms.
+ * ABI v35: also the per-graph factors of the logits gradient, pm [B][C] = exp(z - lse) - [c == y]
+ * and wt [B] = weight[y] (1 unweighted, 0 for a target outside [0, C)), so that a consumer forms
+ * lgnn_ce_bwd's dlogits[i][c] = grad_loss * wt[i] / wsum * pm[i][c] from plain loads (lgnn_ce_src).
  * ticket: uint32[10] zero before the first call, re-armed by every call (one stream at a time).
  * workspace: lgnn_pool_head_ce_workspace_bytes(B) bytes. */
 size_t lgnn_pool_head_ce_workspace_bytes(int64_t num_graphs);
 int lgnn_pool_head_ce_fwd(const float* H, const int32_t* gptr, int64_t B, int D, int pool_mean,
                           const float* Wout, const float* bout, int C, float* pooled,
                           float* logits, const int64_t* target, const float* weight, float* lse,
-                          float* loss, float* wsum, int* bad, unsigned int* ticket,
-                          void* workspace, size_t workspace_bytes, void* stream);
+                          float* loss, float* wsum, int* bad, float* pm, float* wt,
+                          unsigned int* ticket, void* workspace, size_t workspace_bytes,
+                          void* stream);
 
 /* The same with each graph split over `splits` workgroups (few, large graphs: the GAT configs);
  * part: [B][splits][D] scratch; tickets: int32 [B], zero on entry, left zero. Each graph's
@@ -544,19 +565,18 @@ int lgnn_ce_fwd(const float* logits, const int64_t* target, const float* weight,
 int lgnn_ce_bwd(const float* logits, const int64_t* target, const float* weight, int64_t B, int C,
                 const float* lse, const float* wsum, const float* grad_loss, float* dlogits,
                 void* stream);
-/* The CE logits gradient without materialising it (ABI v33): the consumers form
- * lgnn_ce_bwd's dlogits[i][c] themselves, bit for bit, from the forward's saved values.
+/* The CE logits gradient without materialising it (ABI v33; v35: from the readout's pm / wt): the
+ * consumers form lgnn_ce_bwd's dlogits[i][c] = gloss * wt[i] / wsum * pm[i][c] themselves, bit
+ * for bit (lgnn_pool_head_ce_fwd writes pm and wt with lgnn_ce_bwd's expressions).
  * lgnn_reduce_jobs_ce = lgnn_reduce_jobs where jobs with ce_job[j] != 0 take the [P][C] logits
  * gradient (P = B) in place of partials[j] (which may be NULL): out_proj's db (len C) and
  * dW = dlogits^T pooled (factor = pooled, len C * width). The same sums as lgnn_reduce_jobs on
  * lgnn_ce_bwd's output, bitwise. */
 typedef struct lgnn_ce_src {
-  const float* logits;   /* [B][C] */
-  const float* lse;      /* [B] (lgnn_ce_fwd) */
-  const int64_t* target; /* [B] */
-  const float* weight;   /* [C] class weights or NULL */
-  const float* wsum;     /* [1] (lgnn_ce_fwd) */
-  const float* gloss;    /* [1] gradient of the loss */
+  const float* pm;     /* [B][C] exp(z - lse) - [c == y] (lgnn_pool_head_ce_fwd) */
+  const float* wt;     /* [B] weight[y] (lgnn_pool_head_ce_fwd) */
+  const float* wsum;   /* [1] */
+  const float* gloss;  /* [1] gradient of the loss */
 } lgnn_ce_src;
 int lgnn_reduce_jobs_ce(int n, const float* const* partials, const float* const* factor,
                         const int* width, const int* num_partials, const int64_t* len,

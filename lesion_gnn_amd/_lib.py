@@ -34,9 +34,9 @@ SZ = ctypes.c_size_t
 
 
 class CeSrc(ctypes.Structure):
-    """lgnn_ce_src (include/lgnn.h): the CE forward's values its logits gradient is formed from."""
-    _fields_ = [("logits", P), ("lse", P), ("target", P), ("weight", P), ("wsum", P),
-                ("gloss", P)]
+    """lgnn_ce_src (include/lgnn.h): the readout's CE factors the logits gradient is formed from,
+    dlogits[i][c] = gloss * wt[i] / wsum * pm[i][c]."""
+    _fields_ = [("pm", P), ("wt", P), ("wsum", P), ("gloss", P)]
 
 
 # name -> (restype, argtypes); mirrors include/lgnn.h exactly
@@ -71,11 +71,12 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_reduce_jobs": (I32, [I32, P, P, P, P, P, P, P]),
     "lgnn_reduce_jobs_ce": (I32, [I32, P, P, P, P, P, P, P, ctypes.POINTER(CeSrc), I32, P]),
     "lgnn_ce_fwd": (I32, [P, P, P, I64, I32, P, P, P, P, P]),
+    "lgnn_window_aggregate": (I32, [P, P, P, I64, P, I32, P, P, I32, I32, P]),
     "lgnn_ce_bwd": (I32, [P, P, P, I64, I32, P, P, P, P, P]),
     "lgnn_pool_head_fwd": (I32, [P, P, I64, I32, I32, P, P, I32, P, P, P]),
     "lgnn_pool_head_ce_workspace_bytes": (SZ, [I64]),
     "lgnn_pool_head_ce_fwd": (I32, [P, P, I64, I32, I32, P, P, I32, P, P, P, P, P, P, P, P, P, P,
-                                    SZ, P]),
+                                    P, P, SZ, P]),
     "lgnn_pool_head_fwd_split": (I32, [P, P, I64, I32, I32, P, P, I32, I32, P, P, P, P, P]),
     "lgnn_pool_head_bwd": (I32, [P, P, I64, I32, P, I32, P, P, P, P]),
     "lgnn_pool_bwd": (I32, [P, P, P, I64, I32, I32, P, P]),
@@ -160,7 +161,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 34
+ABI_VERSION = 35
 
 _lib = None
 

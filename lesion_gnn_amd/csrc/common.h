@@ -97,25 +97,32 @@ __device__ __forceinline__ unsigned int ticket_after(unsigned int dep) {
   return one;
 }
 
-// nn.CrossEntropyLoss(weight) (mean reduction) logits gradient formed where it is consumed, from
-// the forward's saved values (lgnn_ce_fwd: lse, wsum) — k_ce_bwd's expression, bit for bit:
-//   dz[i][c] = gloss * w[y_i] / wsum * (exp(z[i][c] - lse[i]) - [c == y_i])
+// nn.CrossEntropyLoss(weight) (mean reduction) logits gradient, k_ce_bwd's expression:
+//   dz[i][c] = gloss * wt_i / wsum * pm_ic,  wt_i = w[y_i] (0 if y_i is outside [0, C)),
+//   pm_ic = exp(z[i][c] - lse[i]) - [c == y_i]
+// ce_pm / ce_wt are the per-graph factors (the readout's CE forward stores them); ce_dlogit forms
+// the gradient where it is consumed from plain loads of them, bit for bit k_ce_bwd's value.
+__device__ __forceinline__ float ce_wt(const int64_t* y, const float* w, int C, int64_t i) {
+  const int64_t t = y[i];
+  return (t >= 0 && t < C) ? (w ? w[t] : 1.f) : 0.f;
+}
+__device__ __forceinline__ float ce_pm(float z, float lse, int64_t t, int c) {
+  return expf(z - lse) - (c == t ? 1.f : 0.f);
+}
+__device__ __forceinline__ float ce_grad(float gloss, float wt, float wsum, float pm) {
+  // rounded as a stored dlogits value is: no FMA contraction into the consumer's sum
+#pragma clang fp contract(off)
+  return gloss * wt / wsum * pm;
+}
 struct CeSrc {
-  const float* z;      // [B][C] logits
-  const float* lse;    // [B]
-  const int64_t* y;    // [B] targets
-  const float* w;      // [C] class weights or nullptr
+  const float* pm;     // [B][C]
+  const float* wt;     // [B]
   const float* wsum;   // [1]
   const float* gloss;  // [1]
   int C;
 };
 __device__ __forceinline__ float ce_dlogit(const CeSrc& s, int64_t i, int c) {
-  // rounded as a stored dlogits value is: no FMA contraction into the consumer's sum
-#pragma clang fp contract(off)
-  const int64_t t = s.y[i];
-  const float wt = (t >= 0 && t < s.C) ? (s.w ? s.w[t] : 1.f) : 0.f;
-  const float p = expf(s.z[i * s.C + c] - s.lse[i]);
-  return s.gloss[0] * wt / s.wsum[0] * (p - (c == t ? 1.f : 0.f));
+  return ce_grad(s.gloss[0], s.wt[i], s.wsum[0], s.pm[i * s.C + c]);
 }
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }

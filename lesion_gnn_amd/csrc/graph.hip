@@ -22,6 +22,7 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kFinT = 64;          // k_finish: rows (threads) per block
 constexpr int kFinishCap = 1536;   // staged CSR entries per k_finish block
+constexpr int kLongRow = 24;       // k_finish: longer staged rows are sorted by the whole wave
 // k_build's barrier bound (~4 s): a row longer than kFinishCap is sorted by one thread in global
 // memory (seconds for thousands of entries) while the other workgroups wait at the next barrier
 constexpr int kBuildSpins = 1 << 24;
@@ -373,10 +374,16 @@ __device__ __forceinline__ void mark_open(int32_t* tile_open, int64_t t, int64_t
   if (atomicCAS(&tile_open[t], 0, 1) == 0) atomicAdd(&tile_open[ntiles], 1);
 }
 
+// count_body's tile marks are first collected per workgroup in LDS (kMarkWin tiles around the
+// chunk's first target): many edges of a chunk leave the same few tiles (C5: graphs straddling
+// tiles), and their racing first-marker atomics on one word serialised (~50 us at k = 16)
+constexpr int kMarkWin = 64;
+
 template <int PER = kPer>
 __device__ __forceinline__ void count_body(const int64_t* __restrict__ ei, int64_t E, int64_t N,
                                            int loops, int32_t* cnt, int32_t* tcnt, int32_t* err,
-                                           int32_t* tile_open, int* hist, int* red, int64_t bx) {
+                                           int32_t* tile_open, int* hist, int* red, int64_t bx,
+                                           int* tmk = nullptr) {
   const int lane = threadIdx.x & 63;
   const int64_t c0 = bx * chunk_of(PER);
   EdgeChunk<PER> c;
@@ -388,12 +395,29 @@ __device__ __forceinline__ void count_body(const int64_t* __restrict__ ei, int64
   }
   if (tile_open) {  // lazy transpose: the tiles an edge leaves are known before the fill
     const int64_t ntiles = (N + 63) >> 6;
+    int64_t tb = 0;
+    if (tmk) {
+      const int64_t d0 = E > 0 ? ei[E + (c0 < E ? c0 : E - 1)] : 0;
+      tb = (d0 >> 6) - kMarkWin / 2;
+      for (int q = threadIdx.x; q < kMarkWin; q += kThreads) tmk[q] = 0;
+      __syncthreads();
+    }
+    auto mk = [&](int64_t t) {
+      const int64_t rel = t - tb;
+      if (tmk && rel >= 0 && rel < kMarkWin) tmk[rel] = 1;  // idempotent plain store
+      else if (tile_open[t] == 0) mark_open(tile_open, t, ntiles);
+    };
 #pragma unroll
     for (int it = 0; it < PER; ++it)
       if (c.use[it] && (c.s[it] >> 6) != (c.d[it] >> 6)) {
-        if (tile_open[c.d[it] >> 6] == 0) mark_open(tile_open, c.d[it] >> 6, ntiles);
-        if (tile_open[c.s[it] >> 6] == 0) mark_open(tile_open, c.s[it] >> 6, ntiles);
+        mk(c.d[it] >> 6);
+        mk(c.s[it] >> 6);
       }
+    if (tmk) {
+      __syncthreads();
+      for (int q = threadIdx.x; q < kMarkWin; q += kThreads)
+        if (tmk[q] && tile_open[tb + q] == 0) mark_open(tile_open, tb + q, ntiles);
+    }
   }
   if (!tcnt) return;
   int64_t smin;
@@ -421,12 +445,13 @@ __global__ __launch_bounds__(kThreads) void k_count(const int64_t* __restrict__ 
                                                     int32_t* verdict, int nverdict) {
   __shared__ int hist[kBins];
   __shared__ int red[2 * kThreads / 64];
+  __shared__ int tmk[kMarkWin];
   const int mode = sorted_mode(verdict, nverdict);
   // the summary word for k_scan / k_fill / k_finish (one word to read instead of all of them)
   if (verdict && blockIdx.x == 0 && threadIdx.x == 0) verdict[kVerdictMax] = mode;
   if (mode == kModeSorted) return;
   count_body<PER>(ei, E, N, loops, mode == kModeSortedOpen ? nullptr : cnt, tcnt, err, tile_open,
-                  hist, red, blockIdx.x);
+                  hist, red, blockIdx.x, tmk);
 }
 
 // fill[d] / tfill[s] start at the row offsets (set by k_scan); slots come from atomics on them,
@@ -814,6 +839,10 @@ __device__ __forceinline__ void finish_body(int64_t N, int64_t E, int add_loop, 
     }
   }
   sync();
+  // staged rows longer than kLongRow (source CSR rows of hub nodes: insertion sort is quadratic
+  // and one lane's long row held the whole launch, ~60 us at C5 k = 16) are sorted afterwards by
+  // the whole wave: each entry's rank among its row's (unique) edge ids, at most 4 per lane
+  bool long_row = false;
   if (i < N) {
     const int r0 = ptr[i], r1 = ptr[i + 1];
     if (staged) {
@@ -821,7 +850,8 @@ __device__ __forceinline__ void finish_body(int64_t N, int64_t E, int add_loop, 
         s_val[r1 - 1 - eb] = (int32_t)i;
         s_key[r1 - 1 - eb] = (int32_t)(E + i);
       }
-      sort_row(s_key + (r0 - eb), s_val + (r0 - eb), r1 - r0);
+      long_row = r1 - r0 > kLongRow && r1 - r0 <= 4 * kFinT;
+      if (!long_row) sort_row(s_key + (r0 - eb), s_val + (r0 - eb), r1 - r0);
     } else {
       if (add_loop) {
         idx[r1 - 1] = (int32_t)i;
@@ -832,6 +862,34 @@ __device__ __forceinline__ void finish_body(int64_t N, int64_t E, int add_loop, 
   }
   sync();
   if (staged) {
+    unsigned long long lm = __ballot(long_row);
+    while (lm) {
+      const int L = __ffsll((long long)lm) - 1;
+      lm &= lm - 1;
+      const int64_t ri = i0 + L;
+      const int q0 = ptr[ri] - eb, n = ptr[ri + 1] - ptr[ri];
+      int kk[4], vv[4], rk[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int j = tid + u * kFinT;
+        kk[u] = j < n ? s_key[q0 + j] : 0;
+        vv[u] = j < n ? s_val[q0 + j] : 0;
+        rk[u] = 0;
+      }
+      for (int m = 0; m < n; ++m) {
+        const int km = s_key[q0 + m];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) rk[u] += km < kk[u];
+      }
+      sync();
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (tid + u * kFinT < n) {
+          s_key[q0 + rk[u]] = kk[u];
+          s_val[q0 + rk[u]] = vv[u];
+        }
+      sync();
+    }
     for (int j = eb + tid; j < ee; j += kFinT) {
       idx[j] = s_val[j - eb];
       key[j] = s_key[j - eb];

@@ -73,8 +73,7 @@ __global__ __launch_bounds__(256) void k_ce_bwd(const float* __restrict__ z,
   if (idx >= B * C) return;
   const int64_t i = idx / C;
   const int c = (int)(idx % C);
-  const CeSrc ce{z, lse, y, weight, wsum, gloss, C};
-  dz[idx] = ce_dlogit(ce, i, c);
+  dz[idx] = ce_grad(gloss[0], ce_wt(y, weight, C, i), wsum[0], ce_pm(z[idx], lse[i], y[i], c));
 }
 
 // Regression head + criterion (reference gat.py:94-95 / gin.py:66-67: logits.squeeze(1).clamp(0,
@@ -335,9 +334,9 @@ static int reduce_jobs(int n, const float* const* partials, const float* const* 
     return LGNN_EINVAL;
   ReduceJobs jobs = {};
   if (ce_job) {
-    if (!ce || !ce->logits || !ce->lse || !ce->target || !ce->wsum || !ce->gloss || C < 1)
+    if (!ce || !ce->pm || !ce->wt || !ce->wsum || !ce->gloss || C < 1)
       return LGNN_EINVAL;
-    jobs.ce = CeSrc{ce->logits, ce->lse, ce->target, ce->weight, ce->wsum, ce->gloss, C};
+    jobs.ce = CeSrc{ce->pm, ce->wt, ce->wsum, ce->gloss, C};
   }
   int64_t maxlen = 0;
   for (int j = 0; j < n; ++j) {

@@ -74,6 +74,8 @@ struct CeFwd {
   const int64_t* y;
   const float* w;
   float* lse;
+  float* pm;     // [B][C] the logits gradient's factors (lgnn_ce_src)
+  float* wt;     // [B]
   float* part;   // [B][2] num_g, den_g
   unsigned int* ticket;  // [10] zero, re-armed: 9 ticket words + the blocks' bad-target OR
   float* loss;
@@ -164,12 +166,14 @@ __global__ __launch_bounds__(NT) void k_pool_head_fwd4(const float* __restrict__
       const float l = m + logf(sx);
       ce.lse[g] = l;
       const int64_t t = ce.y[g];
+      const float wt = ce_wt(ce.y, ce.w, C, g);
+      for (int c = 0; c < C; ++c) ce.pm[g * C + c] = ce_pm(zl[c], l, t, c);
+      ce.wt[g] = wt;
       float num = 0.f, den = 0.f;
       unsigned int badv = 0u;
       if (t < 0 || t >= C) {
         badv = 1u;
       } else {
-        const float wt = ce.w ? ce.w[t] : 1.f;
         num = wt * (l - zl[t]);
         den = wt;
       }
@@ -177,8 +181,11 @@ __global__ __launch_bounds__(NT) void k_pool_head_fwd4(const float* __restrict__
           ce.part + 2 * g, num, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
       const unsigned int r1 = __float_as_uint(__hip_atomic_exchange(
           ce.part + 2 * g + 1, den, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      const unsigned int rb = __hip_atomic_fetch_or(ce.ticket + 9, badv, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
+      // the bad-target OR only from the blocks that have one: 1024 same-address atomics
+      // serialise (~30 us)
+      const unsigned int rb = badv ? __hip_atomic_fetch_or(ce.ticket + 9, badv, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT)
+                                   : 0u;
       last = last_workgroup(ce.ticket, ticket_after(r0 ^ r1 ^ rb));
     }
     __syncthreads();
@@ -393,14 +400,16 @@ extern "C" int lgnn_pool_head_ce_fwd(const float* H, const int32_t* gptr, int64_
                                      int pool_mean, const float* Wout, const float* bout, int C,
                                      float* pooled, float* logits, const int64_t* target,
                                      const float* weight, float* lse, float* loss, float* wsum,
-                                     int* bad, unsigned int* ticket, void* workspace,
-                                     size_t workspace_bytes, void* stream) {
+                                     int* bad, float* pm, float* wt, unsigned int* ticket,
+                                     void* workspace, size_t workspace_bytes, void* stream) {
   if (B < 1 || D <= 0 || D > 512 || (D & 3) != 0 || !gptr || !pooled || !Wout || !logits ||
-      C < 1 || C > 16 || !target || !lse || !loss || !wsum || !bad || !ticket || !workspace)
+      C < 1 || C > 16 || !target || !lse || !loss || !wsum || !bad || !pm || !wt || !ticket ||
+      !workspace)
     return LGNN_EINVAL;
   if (workspace_bytes < lgnn_pool_head_ce_workspace_bytes(B)) return LGNN_ENOSPC;
   hipStream_t s = as_stream(stream);
-  const CeFwd ce{target, weight, lse, static_cast<float*>(workspace), ticket, loss, wsum, bad, B};
+  const CeFwd ce{target, weight, lse, pm, wt, static_cast<float*>(workspace), ticket, loss, wsum,
+                 bad, B};
   hipLaunchKernelGGL(k_pool_head_fwd4<true>, dim3((unsigned)B), dim3(NT), 0, s, H, gptr, D,
                      pool_mean, Wout, bout, C, pooled, logits, ce);
   LGNN_LAUNCH_CHECK();

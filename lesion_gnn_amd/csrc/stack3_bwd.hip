@@ -498,7 +498,7 @@ namespace lgnn_s3 {
 struct FBwdArgs {
   const float* dP;                // [B][N_L] pooled-output gradient (or formed from dlog / Wout)
   const float* dlog;              // [B][C] logits gradient (nullable): dP = dlog Wout on the fly
-  CeSrc ce;                       // or (ce.z set) the CE logits gradient, formed on the fly
+  CeSrc ce;                       // or (ce.pm set) the CE logits gradient, formed on the fly
   const float* Wout;              // [C][N_L]
   int C;
   const unsigned char* adjt;      // Â^T planes per tile from the forward (AG), or nullptr
@@ -531,9 +531,16 @@ struct OpenBwdArgs {
 constexpr int kMaxHeadC = 8;  // classes for which dP is formed in the kernel
 
 // the logits gradient row of graph g: given (dlog) or formed from the CE forward (ce)
-__device__ __forceinline__ bool has_head(const FBwdArgs& a) { return a.dlog || a.ce.z; }
-__device__ __forceinline__ float head_dl(const FBwdArgs& a, int64_t g, int c) {
-  return a.ce.z ? ce_dlogit(a.ce, g, c) : a.dlog[g * a.C + c];
+__device__ __forceinline__ bool has_head(const FBwdArgs& a) { return a.dlog || a.ce.pm; }
+// the raw per-graph value loaded a tile ahead: dlog, or CE's pm (the factor gloss * wt / wsum is
+// applied where the row is used, so that the prefetch stays a plain load nothing waits on)
+__device__ __forceinline__ float head_raw(const FBwdArgs& a, int64_t g, int c) {
+  return a.ce.pm ? a.ce.pm[g * a.C + c] : a.dlog[g * a.C + c];
+}
+// the logits gradient from the raw value: ce_dlogit's expression, bit for bit
+__device__ __forceinline__ float head_dl(const FBwdArgs& a, float raw, float wt, float gl,
+                                         float ws) {
+  return a.ce.pm ? ce_grad(gl, wt, ws, raw) : raw;
 }
 
 struct FBwdSmem {
@@ -688,7 +695,9 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
   // graph of row tq of the tile and its size (tq < TM), loaded a tile ahead
   int64_t pre_g = 0;
   int pre_cnt = 0;
-  float pre_dl[kMaxHeadC];  // dlog row of pre_g (tq < TM), loaded a tile ahead
+  float pre_dl[kMaxHeadC];  // dlog (or CE pm) row of pre_g (tq < TM), loaded a tile ahead
+  float pre_wt = 0.f;       // CE: wt[pre_g]
+  const float ce_gl = a.ce.pm ? a.ce.gloss[0] : 0.f, ce_ws = a.ce.pm ? a.ce.wsum[0] : 1.f;
 #pragma unroll
   for (int c = 0; c < kMaxHeadC; ++c) pre_dl[c] = 0.f;
   // out_proj's W as the B operand of the dZ_L product (lane: feature n; K: class 8h + e; classes
@@ -721,7 +730,8 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
         pre_cnt = a.gptr[pre_g + 1] - a.gptr[pre_g];
         if (has_head(a)) {
 #pragma unroll
-          for (int c = 0; c < kMaxHeadC; ++c) pre_dl[c] = c < a.C ? head_dl(a, pre_g, c) : 0.f;
+          for (int c = 0; c < kMaxHeadC; ++c) pre_dl[c] = c < a.C ? head_raw(a, pre_g, c) : 0.f;
+          if (a.ce.pm) pre_wt = a.ce.wt[pre_g];
         }
       }
     }
@@ -767,7 +777,7 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
         if (has_head(a)) {  // zero-padded to kMaxHeadC: the dZ_L loop below runs without branches
           float v[kMaxHeadC];
 #pragma unroll
-          for (int c = 0; c < kMaxHeadC; ++c) v[c] = pre_dl[c] * ps;
+          for (int c = 0; c < kMaxHeadC; ++c) v[c] = head_dl(a, pre_dl[c], pre_wt, ce_gl, ce_ws) * ps;
           st4(&sm.dl[tq][0], f32x4{v[0], v[1], v[2], v[3]});
           st4(&sm.dl[tq][4], f32x4{v[4], v[5], v[6], v[7]});
         }
@@ -1122,7 +1132,8 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
         if (has_head(a)) {
 #pragma unroll
           for (int c = 0; c < kMaxHeadC; ++c)
-            pre_dl[c] = (has_next && tq < TM && c < a.C) ? head_dl(a, pre_g, c) : 0.f;
+            pre_dl[c] = (has_next && tq < TM && c < a.C) ? head_raw(a, pre_g, c) : 0.f;
+          if (a.ce.pm) pre_wt = (has_next && tq < TM) ? a.ce.wt[pre_g] : 0.f;
         }
       }
       lds_barrier();
@@ -1194,7 +1205,7 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
         bwd_tiles<LGNN_GRAD_POOL, LGNN_ACT_ELU, true>(
             lw.A, lw.C, lw.ti, a.dP, a.batch, a.gptr, a.pool_mean, nullptr, nullptr, nullptr, 0.f,
             a.H[l], Sx, M, K, o.W[l], N, o.dS[l & 1], a.dWp[l], a.dbp[l], tmask, 1, 1, a.dlog,
-            a.Wout, a.C, BnFuse{}, a.ce.z ? &a.ce : nullptr);
+            a.Wout, a.C, BnFuse{}, a.ce);
       else if (l >= 1)
         bwd_tiles<LGNN_GRAD_TRANSPOSE, LGNN_ACT_ELU, true>(
             lw.A, lw.C, lw.ti, o.dS[(l + 1) & 1], a.batch, a.gptr, a.pool_mean, o.tptr, o.tidx,
@@ -1343,6 +1354,8 @@ __global__ __launch_bounds__(NT8, 1) void k_s3_fbwd8(int64_t M, FBwdArgs a,
   int64_t pre_g = 0;
   int pre_cnt = 0;
   float pre_dl[kMaxHeadC];
+  float pre_wt = 0.f;
+  const float ce_gl = a.ce.pm ? a.ce.gloss[0] : 0.f, ce_ws = a.ce.pm ? a.ce.wsum[0] : 1.f;
 #pragma unroll
   for (int c = 0; c < kMaxHeadC; ++c) pre_dl[c] = 0.f;
   auto hl_issue8 = [&](int64_t tt) {  // tile tt's H_L rows -> the G image region (1 KiB loads)
@@ -1374,7 +1387,8 @@ __global__ __launch_bounds__(NT8, 1) void k_s3_fbwd8(int64_t M, FBwdArgs a,
       pre_cnt = a.gptr[pre_g + 1] - a.gptr[pre_g];
       if (has_head(a)) {
 #pragma unroll
-        for (int c = 0; c < kMaxHeadC; ++c) pre_dl[c] = c < a.C ? head_dl(a, pre_g, c) : 0.f;
+        for (int c = 0; c < kMaxHeadC; ++c) pre_dl[c] = c < a.C ? head_raw(a, pre_g, c) : 0.f;
+        if (a.ce.pm) pre_wt = a.ce.wt[pre_g];
       }
     }
   }
@@ -1393,8 +1407,11 @@ __global__ __launch_bounds__(NT8, 1) void k_s3_fbwd8(int64_t M, FBwdArgs a,
         sm.pg[tq] = (int)pre_g;
         sm.pscale[tq] = ps;
         if (has_head(a)) {
-          st4(&sm.dl[tq][0], f32x4{pre_dl[0] * ps, pre_dl[1] * ps, pre_dl[2] * ps, pre_dl[3] * ps});
-          st4(&sm.dl[tq][4], f32x4{pre_dl[4] * ps, pre_dl[5] * ps, pre_dl[6] * ps, pre_dl[7] * ps});
+          float v[kMaxHeadC];
+#pragma unroll
+          for (int c = 0; c < kMaxHeadC; ++c) v[c] = head_dl(a, pre_dl[c], pre_wt, ce_gl, ce_ws) * ps;
+          st4(&sm.dl[tq][0], f32x4{v[0], v[1], v[2], v[3]});
+          st4(&sm.dl[tq][4], f32x4{v[4], v[5], v[6], v[7]});
         }
       }
     }
@@ -1650,7 +1667,8 @@ __global__ __launch_bounds__(NT8, 1) void k_s3_fbwd8(int64_t M, FBwdArgs a,
         if (has_head(a)) {
 #pragma unroll
           for (int c = 0; c < kMaxHeadC; ++c)
-            pre_dl[c] = (has_next && tq < TM && c < a.C) ? head_dl(a, pre_g, c) : 0.f;
+            pre_dl[c] = (has_next && tq < TM && c < a.C) ? head_raw(a, pre_g, c) : 0.f;
+          if (a.ce.pm) pre_wt = (has_next && tq < TM) ? a.ce.wt[pre_g] : 0.f;
         }
       }
       lds_barrier();
@@ -1714,7 +1732,7 @@ __global__ __launch_bounds__(NT8, 1) void k_s3_fbwd8(int64_t M, FBwdArgs a,
         bwd_tiles<LGNN_GRAD_POOL, LGNN_ACT_ELU, true>(
             lw.A, lw.C, lw.ti, a.dP, a.batch, a.gptr, a.pool_mean, nullptr, nullptr, nullptr, 0.f,
             a.H[l], Sx, M, K, o.W[l], N, o.dS[l & 1], a.dWp[l], a.dbp[l], tmask, 1, 1, a.dlog,
-            a.Wout, a.C, BnFuse{}, a.ce.z ? &a.ce : nullptr);
+            a.Wout, a.C, BnFuse{}, a.ce);
       else if (l >= 1)
         bwd_tiles<LGNN_GRAD_TRANSPOSE, LGNN_ACT_ELU, true>(
             lw.A, lw.C, lw.ti, o.dS[(l + 1) & 1], a.batch, a.gptr, a.pool_mean, o.tptr, o.tidx,
@@ -1847,9 +1865,9 @@ static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* g
   a.dP = dP;
   a.dlog = dlogits;
   if (ce) {
-    if (dlogits || !ce->logits || !ce->lse || !ce->target || !ce->wsum || !ce->gloss)
+    if (dlogits || !ce->pm || !ce->wt || !ce->wsum || !ce->gloss)
       return LGNN_EINVAL;
-    a.ce = CeSrc{ce->logits, ce->lse, ce->target, ce->weight, ce->wsum, ce->gloss, num_classes};
+    a.ce = CeSrc{ce->pm, ce->wt, ce->wsum, ce->gloss, num_classes};
   }
   a.Wout = Wout;
   a.C = num_classes;

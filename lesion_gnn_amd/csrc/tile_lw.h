@@ -244,7 +244,7 @@ __device__ __forceinline__ void bwd_tiles(
     const float* __restrict__ W, int N, float* __restrict__ dXpre, float* __restrict__ dWp,
     float* __restrict__ dbp, const int32_t* __restrict__ tmask, int want, int accumulate,
     const float* __restrict__ dlog = nullptr, const float* __restrict__ Wout = nullptr,
-    int nclass = 0, const BnFuse& bn = BnFuse{}, const CeSrc* ce = nullptr) {
+    int nclass = 0, const BnFuse& bn = BnFuse{}, const CeSrc ce = CeSrc{}) {
   static_assert(BNM == BN_NONE || (BNM == BN_GSTATS && DX) ||
                     (BNM == BN_GIN && GMODE == LGNN_GRAD_DIRECT && ACT == LGNN_ACT_NONE), "");
   // GRAD_POOL with dlog: the pooled-output gradient is formed on the fly from the logits'
@@ -368,11 +368,11 @@ __device__ __forceinline__ void bwd_tiles(
           if constexpr (BNM == BN_GIN) hv[it] = ld4(bn.Z + rc * N + oc);  // BN input rows
         } else {
           const int64_t gi = batch[rc];
-          if (dlog || ce) {  // k_head_bwd's arithmetic: an fmaf chain over the classes in order
+          if (dlog || ce.pm) {  // k_head_bwd's arithmetic: an fmaf chain over the classes in order
             f32x4 acc = zero4();
             for (int c = 0; c < nclass; ++c) {
               // the logits gradient as given, or formed from the CE forward (bitwise the same)
-              const float d = ce ? ce_dlogit(*ce, gi, c) : dlog[gi * nclass + c];
+              const float d = ce.pm ? ce_dlogit(ce, gi, c) : dlog[gi * nclass + c];
               const f32x4 wv = ld4(Wout + (int64_t)c * N + oc);
 #pragma unroll
               for (int j = 0; j < 4; ++j) acc[j] = fmaf(d, wv[j], acc[j]);

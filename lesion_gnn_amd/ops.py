@@ -100,6 +100,19 @@ OPEN_IN_FUSED_BWD = OPEN_IN_FUSED
 # dP = dlogits W_out formed inside the single-launch split-3 backward (LGNN_HEAD_FOLD=0: by
 # lgnn_pool_head_bwd before it)
 HEAD_FOLD = os.environ.get("LGNN_HEAD_FOLD", "1") != "0"
+# the open tiles' aggregations (forward Â H, backward Â^T dY) of 128-wide layers by windowed dense
+# blocks (lgnn_window_aggregate) ahead of the layer kernel, instead of the layer kernel's per-entry
+# row gather; LGNN_WINDOW=0: the gather. WINDOW_CHUNKS: widest window (64-row chunks) per tile.
+WINDOW = os.environ.get("LGNN_WINDOW", "1") != "0"
+WINDOW_CHUNKS = int(os.environ.get("LGNN_WINDOW_CHUNKS", "20"))
+
+
+def window_aggregate(csr_ptr, csr_idx, csr_w, M: int, inp: torch.Tensor, out: torch.Tensor,
+                     open_: torch.Tensor | None, want: int = 1):
+    """out[rows of the selected tiles] = A_hat inp (lgnn_window_aggregate; 128-wide rows)."""
+    _lib.call("lgnn_window_aggregate", _lib.ptr(csr_ptr), _lib.ptr(csr_idx), _lib.ptr(csr_w), M,
+              _lib.ptr(inp), inp.size(1), _lib.ptr(out), _lib.ptr(open_), int(want),
+              WINDOW_CHUNKS, _s(inp.device))
 
 
 _CAPACITY: dict = {}
@@ -328,12 +341,16 @@ def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list, keep: dict | No
     for l in range(L + 1):
         inp = x if l == 0 else hs[l - 1]
         c = csr if l > 0 else None
+        s_out = ss[l - 1] if l > 0 else None
+        if c is not None and WINDOW and inp.size(1) == 128:
+            # S_l = Â H_{l-1} of the open tiles by windowed dense blocks, then the layer on S_l
+            window_aggregate(c.rowptr, c.col, c.w, M, inp, s_out, open_)
+            inp, c, s_out = s_out, None, None
         _lib.call("lgnn_node_linear_fwd_tiles", _lib.ptr(inp), M, inp.size(1),
                   _lib.ptr(c.rowptr) if c else None, _lib.ptr(c.col) if c else None,
                   _lib.ptr(c.w) if c else None, 0.0, _lib.ptr(Ws[l]), _lib.ptr(bs[l]),
                   Ws[l].size(0), _lib.LGNN_ACT_ELU if l > 0 else _lib.LGNN_ACT_NONE,
-                  _lib.ptr(hs[l]), _lib.ptr(ss[l - 1]) if l > 0 else None, _lib.ptr(open_), 1,
-                  _s(dev))
+                  _lib.ptr(hs[l]), _lib.ptr(s_out), _lib.ptr(open_), 1, _s(dev))
     return hs, ss
 
 
@@ -424,6 +441,12 @@ def stack_bwd(dp: torch.Tensor | None, x: torch.Tensor, graph: Graph, mean: bool
         K, N = widths[l], widths[l + 1]
         if l == L:
             mode, dY, tc = _lib.LGNN_GRAD_POOL, dp, None
+        elif WINDOW and N == 128:
+            # the conv's aggregation gradient Â^T dS of the open tiles by windowed dense blocks
+            # (transpose CSR), then the layer in direct mode
+            dY = torch.empty(M, N, dtype=torch.float32, device=dev)
+            window_aggregate(csr.tptr, csr.tidx, csr.tw, M, dS, dY, open_)
+            mode, tc = _lib.LGNN_GRAD_DIRECT, None
         else:
             mode, dY, tc = _lib.LGNN_GRAD_TRANSPOSE, dS, csr
         dX = torch.empty(M, K, dtype=torch.float32, device=dev) if l > 0 else None
@@ -577,7 +600,8 @@ _CE_TICKETS: dict = {}
 def pool_head_ce_fwd(H: torch.Tensor, graph: Graph, mean: bool, Wout, bout, y, weight):
     """pool_head_fwd + the CE criterion's forward in one launch (lgnn_pool_head_ce_fwd), or None
     when the shape is off that kernel (then the caller runs the two launches). Returns
-    (pooled, logits, lse, out[loss, wsum], bad)."""
+    (pooled, logits, lse, out[loss, wsum], bad, pm, wt): pm [B, C] and wt [B] are the factors of
+    the logits gradient, dlogits = gloss * wt / wsum * pm (lgnn_ce_src)."""
     B, D = graph.num_graphs, H.size(1)
     C = Wout.size(0)
     if B < 1 or D % 4 or D > 512 or not 1 <= C <= 16 or pool_splits(B, H.size(0), D) > 1:
@@ -592,13 +616,15 @@ def pool_head_ce_fwd(H: torch.Tensor, graph: Graph, mean: bool, Wout, bout, y, w
     lse = torch.empty(B, dtype=torch.float32, device=dev)
     out = torch.empty(2, dtype=torch.float32, device=dev)
     bad = torch.empty(1, dtype=torch.int32, device=dev)
+    pm = torch.empty(B, C, dtype=torch.float32, device=dev)
+    wt = torch.empty(B, dtype=torch.float32, device=dev)
     ws = torch.empty(_lib.load().lgnn_pool_head_ce_workspace_bytes(B), dtype=torch.uint8,
                      device=dev)
     _lib.call("lgnn_pool_head_ce_fwd", _lib.ptr(H), _lib.ptr(graph.gptr), B, D, int(mean),
               _lib.ptr(Wout), _lib.ptr(bout), C, _lib.ptr(pooled), _lib.ptr(logits), _lib.ptr(y),
               _lib.ptr(weight), _lib.ptr(lse), _lib.ptr(out), _lib.ptr(out) + 4, _lib.ptr(bad),
-              _lib.ptr(tk), _lib.ptr(ws), ws.numel(), _s(dev))
-    return pooled, logits, lse, out, bad
+              _lib.ptr(pm), _lib.ptr(wt), _lib.ptr(tk), _lib.ptr(ws), ws.numel(), _s(dev))
+    return pooled, logits, lse, out, bad, pm, wt
 
 
 def pool_head_bwd(dlogits: torch.Tensor, pooled: torch.Tensor, Wout: torch.Tensor):
@@ -1145,8 +1171,8 @@ class _GCNStack(torch.autograd.Function):
         ctx.ce_fwd = None
         r = pool_head_ce_fwd(hs[-1], graph, mean, W_out, b_out, *ce) if ce is not None else None
         if r is not None:
-            pooled, logits, lse, out, _ = r
-            ctx.ce_fwd = (lse, out)
+            pooled, logits, lse, out, _, pm, wt = r
+            ctx.ce_fwd = (lse, out, pm, wt)
         else:
             pooled, logits = pool_head_fwd(hs[-1], graph, mean, W_out, b_out)
         ctx.graph, ctx.mean, ctx.L = graph, mean, L
@@ -1255,8 +1281,9 @@ class _GCNStackCE(torch.autograd.Function):
         # the readout runs the CE forward too (one launch) where its kernel takes the shape
         logits, to_save = _GCNStack._fwd(ctx, x, graph, mean, L, params, ce=(yy, w))
         z = logits
+        pm = wt = None  # the logits gradient's factors, when the readout ran the CE forward
         if ctx.ce_fwd is not None:
-            lse, out = ctx.ce_fwd
+            lse, out, pm, wt = ctx.ce_fwd
         else:
             B, C = z.shape
             dev = z.device
@@ -1267,7 +1294,9 @@ class _GCNStackCE(torch.autograd.Function):
                       _lib.ptr(lse), _lib.ptr(out), _lib.ptr(out) + 4, _lib.ptr(bad), _s(dev))
         ctx.ce_fwd = None
         ctx.has_w = w is not None
-        ctx.save_for_backward(*to_save, z, yy, lse, out, *((w,) if w is not None else ()))
+        ctx.has_pm = pm is not None
+        ctx.save_for_backward(*to_save, z, yy, lse, out, *((w,) if w is not None else ()),
+                              *((pm, wt) if pm is not None else ()))
         return logits, out[0]
 
     @staticmethod
@@ -1277,6 +1306,7 @@ class _GCNStackCE(torch.autograd.Function):
         stack_saved = saved[:n]
         z, yy, lse, out = saved[n:n + 4]
         w = saved[n + 4] if ctx.has_w else None
+        pm, wt = saved[-2:] if ctx.has_pm else (None, None)
         params = stack_saved[3 + 2 * ctx.L:]
         W_out = params[2 + 2 * ctx.L]
 
@@ -1288,9 +1318,8 @@ class _GCNStackCE(torch.autograd.Function):
                 return (None,) * (6 + len(params))
             return grads(_GCNStack._bwd(ctx, dlogits, stack_saved))
         g = _f32c(dloss.reshape(1))
-        if dlogits is None and _GCNStack.fused_head(ctx, W_out):
-            src = _lib.CeSrc(z.data_ptr(), lse.data_ptr(), yy.data_ptr(), _lib.ptr(w),
-                             out.data_ptr() + 4, g.data_ptr())
+        if dlogits is None and pm is not None and _GCNStack.fused_head(ctx, W_out):
+            src = _lib.CeSrc(pm.data_ptr(), wt.data_ptr(), out.data_ptr() + 4, g.data_ptr())
             return grads(_GCNStack._bwd(ctx, None, stack_saved, ce=(src, z)))
         B, C = z.shape
         dz = torch.empty_like(z)
