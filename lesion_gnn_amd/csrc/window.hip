@@ -221,7 +221,9 @@ __global__ __launch_bounds__(NT, 2) void k_win_agg(const int32_t* __restrict__ r
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, s[q][r]), bO,
+        // (__float_as_uint, not __builtin_bit_cast on the vector-element lvalue: this clang
+        // bit-casts from the vector's first element there)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s[q][r]), bO,
                                               (int)(((r0 + m) * WP + n) * 4), 0, 0);
       }
     __syncthreads();  // sm.rp / scr / Adj are rewritten by the next tile
