@@ -565,6 +565,12 @@ int lgnn_ce_fwd(const float* logits, const int64_t* target, const float* weight,
 int lgnn_ce_bwd(const float* logits, const int64_t* target, const float* weight, int64_t B, int C,
                 const float* lse, const float* wsum, const float* grad_loss, float* dlogits,
                 void* stream);
+/* lgnn_ce_fwd that also writes the logits gradient's per-row factors (ABI v35):
+ * pm [B][C] = exp(z - lse) - [c == y], wt [B] = weight[y] (1 unweighted, 0 for a target outside
+ * [0, C)) — lgnn_ce_src's inputs, so a consumer forms lgnn_ce_bwd's dlogits from plain loads. */
+int lgnn_ce_fwd_factors(const float* logits, const int64_t* target, const float* weight,
+                        int64_t B, int C, float* lse, float* loss, float* wsum, int* bad,
+                        float* pm, float* wt, void* stream);
 /* The CE logits gradient without materialising it (ABI v33; v35: from the readout's pm / wt): the
  * consumers form lgnn_ce_bwd's dlogits[i][c] = gloss * wt[i] / wsum * pm[i][c] themselves, bit
  * for bit (lgnn_pool_head_ce_fwd writes pm and wt with lgnn_ce_bwd's expressions).

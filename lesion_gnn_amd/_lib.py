@@ -71,6 +71,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_reduce_jobs": (I32, [I32, P, P, P, P, P, P, P]),
     "lgnn_reduce_jobs_ce": (I32, [I32, P, P, P, P, P, P, P, ctypes.POINTER(CeSrc), I32, P]),
     "lgnn_ce_fwd": (I32, [P, P, P, I64, I32, P, P, P, P, P]),
+    "lgnn_ce_fwd_factors": (I32, [P, P, P, I64, I32, P, P, P, P, P, P, P]),
     "lgnn_window_aggregate": (I32, [P, P, P, I64, P, I32, P, P, I32, I32, P]),
     "lgnn_ce_bwd": (I32, [P, P, P, I64, I32, P, P, P, P, P]),
     "lgnn_pool_head_fwd": (I32, [P, P, I64, I32, I32, P, P, I32, P, P, P]),

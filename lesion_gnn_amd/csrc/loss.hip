@@ -26,12 +26,15 @@ __device__ __forceinline__ float block_sum_fixed(float v, float* red) {
   return red[CT / 64];
 }
 
-// lse[i] = logsumexp(z_i) (saved for the backward); loss[0] = weighted mean NLL; wsum[0]
+// lse[i] = logsumexp(z_i) (saved for the backward); loss[0] = weighted mean NLL; wsum[0];
+// FACTORS: also the logits gradient's per-row factors pm [B][C], wt [B] (lgnn_ce_src)
+template <bool FACTORS>
 __global__ __launch_bounds__(CT) void k_ce_fwd(const float* __restrict__ z,
                                                const int64_t* __restrict__ y,
                                                const float* __restrict__ weight, int64_t B, int C,
                                                float* __restrict__ lse, float* __restrict__ loss,
-                                               float* __restrict__ wsum, int* __restrict__ bad) {
+                                               float* __restrict__ wsum, int* __restrict__ bad,
+                                               float* __restrict__ pm, float* __restrict__ wtf) {
   __shared__ float red[CT / 64 + 1];
   if (threadIdx.x == 0) *bad = 0;
   __syncthreads();
@@ -45,6 +48,10 @@ __global__ __launch_bounds__(CT) void k_ce_fwd(const float* __restrict__ z,
     const float l = m + logf(s);
     lse[i] = l;
     const int64_t t = y[i];
+    if constexpr (FACTORS) {
+      for (int c = 0; c < C; ++c) pm[i * C + c] = ce_pm(zi[c], l, t, c);
+      wtf[i] = ce_wt(y, weight, C, i);
+    }
     if (t < 0 || t >= C) {
       atomicOr(bad, 1);
       continue;
@@ -270,8 +277,19 @@ extern "C" int lgnn_ce_fwd(const float* logits, const int64_t* target, const flo
                            void* stream) {
   if (B <= 0 || C <= 0 || !logits || !target || !lse || !loss || !wsum || !bad)
     return LGNN_EINVAL;
-  hipLaunchKernelGGL(k_ce_fwd, dim3(1), dim3(CT), 0, as_stream(stream), logits, target, weight, B,
-                     C, lse, loss, wsum, bad);
+  hipLaunchKernelGGL(k_ce_fwd<false>, dim3(1), dim3(CT), 0, as_stream(stream), logits, target,
+                     weight, B, C, lse, loss, wsum, bad, nullptr, nullptr);
+  LGNN_LAUNCH_CHECK();
+  return LGNN_OK;
+}
+
+extern "C" int lgnn_ce_fwd_factors(const float* logits, const int64_t* target,
+                                   const float* weight, int64_t B, int C, float* lse, float* loss,
+                                   float* wsum, int* bad, float* pm, float* wt, void* stream) {
+  if (B <= 0 || C <= 0 || !logits || !target || !lse || !loss || !wsum || !bad || !pm || !wt)
+    return LGNN_EINVAL;
+  hipLaunchKernelGGL(k_ce_fwd<true>, dim3(1), dim3(CT), 0, as_stream(stream), logits, target,
+                     weight, B, C, lse, loss, wsum, bad, pm, wt);
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
 }

@@ -102,8 +102,10 @@ OPEN_IN_FUSED_BWD = OPEN_IN_FUSED
 HEAD_FOLD = os.environ.get("LGNN_HEAD_FOLD", "1") != "0"
 # the open tiles' aggregations (forward Â H, backward Â^T dY) of 128-wide layers by windowed dense
 # blocks (lgnn_window_aggregate) ahead of the layer kernel, instead of the layer kernel's per-entry
-# row gather; LGNN_WINDOW=0: the gather. WINDOW_CHUNKS: widest window (64-row chunks) per tile.
-WINDOW = os.environ.get("LGNN_WINDOW", "1") != "0"
+# row gather: opt-in (LGNN_WINDOW=1) — correct, but slower than the gather at C5 (62 us per call
+# against the 40-65 us of gather it replaces). WINDOW_CHUNKS: widest window
+# (64-row chunks) per tile.
+WINDOW = os.environ.get("LGNN_WINDOW", "0") == "1"
 WINDOW_CHUNKS = int(os.environ.get("LGNN_WINDOW_CHUNKS", "20"))
 
 
@@ -595,6 +597,10 @@ def pool_head_fwd(H: torch.Tensor, graph: Graph, mean: bool, Wout=None, bout=Non
 
 
 _CE_TICKETS: dict = {}
+# the CE forward inside the readout kernel (lgnn_pool_head_ce_fwd, last-workgroup sum) instead of
+# a separate single-workgroup launch: opt-in — 1024 workgroups' tickets on a few words cost more
+# (C2: readout 8.5 -> 25 us) than the launch saved (4.9 us)
+CE_IN_POOL = os.environ.get("LGNN_CE_IN_POOL", "0") == "1"
 
 
 def pool_head_ce_fwd(H: torch.Tensor, graph: Graph, mean: bool, Wout, bout, y, weight):
@@ -1169,7 +1175,8 @@ class _GCNStack(torch.autograd.Function):
                 ctx.saved_s.append(fast)
         W_out, b_out = params[2 + 2 * L], params[3 + 2 * L]
         ctx.ce_fwd = None
-        r = pool_head_ce_fwd(hs[-1], graph, mean, W_out, b_out, *ce) if ce is not None else None
+        r = pool_head_ce_fwd(hs[-1], graph, mean, W_out, b_out, *ce) \
+            if ce is not None and CE_IN_POOL else None
         if r is not None:
             pooled, logits, lse, out, _, pm, wt = r
             ctx.ce_fwd = (lse, out, pm, wt)
@@ -1281,17 +1288,19 @@ class _GCNStackCE(torch.autograd.Function):
         # the readout runs the CE forward too (one launch) where its kernel takes the shape
         logits, to_save = _GCNStack._fwd(ctx, x, graph, mean, L, params, ce=(yy, w))
         z = logits
-        pm = wt = None  # the logits gradient's factors, when the readout ran the CE forward
-        if ctx.ce_fwd is not None:
+        if ctx.ce_fwd is not None:  # the readout ran the CE forward (CE_IN_POOL)
             lse, out, pm, wt = ctx.ce_fwd
-        else:
+        else:  # one single-workgroup launch: loss, lse and the gradient's factors pm / wt
             B, C = z.shape
             dev = z.device
             lse = torch.empty(B, dtype=torch.float32, device=dev)
             out = torch.empty(2, dtype=torch.float32, device=dev)  # loss, sum of weights
             bad = torch.empty(1, dtype=torch.int32, device=dev)
-            _lib.call("lgnn_ce_fwd", _lib.ptr(z), _lib.ptr(yy), _lib.ptr(w), B, C,
-                      _lib.ptr(lse), _lib.ptr(out), _lib.ptr(out) + 4, _lib.ptr(bad), _s(dev))
+            pm = torch.empty(B, C, dtype=torch.float32, device=dev)
+            wt = torch.empty(B, dtype=torch.float32, device=dev)
+            _lib.call("lgnn_ce_fwd_factors", _lib.ptr(z), _lib.ptr(yy), _lib.ptr(w), B, C,
+                      _lib.ptr(lse), _lib.ptr(out), _lib.ptr(out) + 4, _lib.ptr(bad),
+                      _lib.ptr(pm), _lib.ptr(wt), _s(dev))
         ctx.ce_fwd = None
         ctx.has_w = w is not None
         ctx.has_pm = pm is not None
