@@ -901,22 +901,21 @@ __device__ __forceinline__ void finish_body(int64_t N, int64_t E, int add_loop, 
   if (staged) {
     // entry-parallel passes (weights, tile marks): lane t takes entries eb + t, + kFinT, ... —
     // coalesced stores and independent loads (a per-row walk chained 17 dependent gathers per
-    // lane at C5 k = 16); the row of an entry by binary search over the block's row starts
-    s_ptr[tid] = i < N ? ptr[i] : ee;
-    if (tid == 0) s_ptr[kFinT] = ee;
+    // lane at C5 k = 16). The row of each entry comes from a table in the (now free) key
+    // staging array, written by each lane for its own row (a per-entry binary search chained
+    // six dependent LDS reads: C5 k = 16's source CSR finish 62 -> 46 us with it)
+    sync();  // every lane's write-back reads of s_key are done
+    if (i < N) {
+      const int r1 = ptr[i + 1];
+      for (int j = ptr[i]; j < r1; ++j) s_key[j - eb] = tid;
+    }
     sync();
-    const int nrows = (int)(iend - i0);
     // lazy builds took the tile marks in k_count (cross edges) and k_scan (capacity)
     const bool marks = tile_open && !tr && !lazy;
     const int64_t ntiles = (N + 63) >> 6;
+#pragma unroll 4
     for (int j = eb + tid; j < ee; j += kFinT) {
-      int lo = 0, hi = nrows - 1;  // largest r with s_ptr[r] <= j (empty rows share a start)
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (s_ptr[mid] <= j) lo = mid;
-        else hi = mid - 1;
-      }
-      const int64_t row = i0 + lo;
+      const int64_t row = i0 + s_key[j - eb];
       const int nb = s_val[j - eb];
       if (wt) wt[j] = norm == LGNN_NORM_GCN ? (dis[nb] * 1.0f) * dis[row] : 1.0f;
       if (marks && (nb >> 6) != (row >> 6)) {
