@@ -975,7 +975,7 @@ def main():
         rows = []
         for kt in time_dominant_kernels(model, b, dev):
             achieved = kt["flops"] / (kt["ms"] * 1e-3) / 1e12
-            traffic, tsrc = pmc_traffic(kt["trace_name"])
+            traffic, tsrc = pmc_traffic(kt["trace_name"], args.workload)
             peak = kt.get("peak", MFMA_F32_PEAK_TF)
             rows.append({"bound": "mfma", "achieved": round(achieved, 2),
                          "peak": peak, "unit": "TFLOP/s",
@@ -997,7 +997,7 @@ def main():
             tf = kt["flops"] / sec / 1e12
             gbs = kt["bytes"] / sec / 1e9
             f_mfma, f_hbm = tf / kt["peak"], gbs / HBM_PEAK_GBS
-            traffic, tsrc = pmc_traffic(kt["trace_name"])
+            traffic, tsrc = pmc_traffic(kt["trace_name"], args.workload)
             mfma_bound = f_mfma >= f_hbm  # the roof the kernel is closer to
             rows.append({"bound": "mfma" if mfma_bound else "hbm",
                          "achieved": round(tf if mfma_bound else gbs, 2),
