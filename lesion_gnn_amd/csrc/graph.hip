@@ -236,6 +236,7 @@ __global__ __launch_bounds__(kThreads) void k_prep_sorted(int32_t* __restrict__ 
       const unsigned long long cmask = clen >= 64 ? ~0ull : (1ull << clen) - 1;
       if (!in) continue;
       const int64_t sv = s[c], dv = d[c];
+      if (drop_loops && sv == dv) bad |= 4;  // a dropped input self loop (k_scan: scan needed)
       if (!edge_ok(sv, dv, N) || dp > dv) {
         bad |= 1;
         continue;
@@ -248,6 +249,7 @@ __global__ __launch_bounds__(kThreads) void k_prep_sorted(int32_t* __restrict__ 
           bad |= 1;
         } else {
           for (int64_t q = r0; q < dv; ++q) sorted_empty_row(a, q, e);
+          if (r0 < dv) bad |= 8;  // a row without a (dropped) self loop
         }
         const unsigned long long run = (r.len >= 64 ? ~0ull : ((1ull << r.len) - 1)) << lane;
         int n = r.len, nl = __popcll(lm & run);
@@ -260,6 +262,7 @@ __global__ __launch_bounds__(kThreads) void k_prep_sorted(int32_t* __restrict__ 
           if (clen == 64) bad |= 1;  // longer than any row the fast path takes
         }
         const int deg = n - nl;
+        if (nl == 0) bad |= 8;
         if (n > kSortedRowCap + 1 || nl > 1 || deg + a.add_loop > kSortedRowCap) bad |= 1;
         a.rs[dv] = (int32_t)e;
         a.scnt[dv] = deg;
@@ -272,6 +275,7 @@ __global__ __launch_bounds__(kThreads) void k_prep_sorted(int32_t* __restrict__ 
           bad |= 1;
         } else {
           for (int64_t q = dv + 1; q < N; ++q) sorted_empty_row(a, q, E);
+          if (dv + 1 < N) bad |= 8;
         }
         a.rs[N] = (int32_t)E;
       }
@@ -279,7 +283,9 @@ __global__ __launch_bounds__(kThreads) void k_prep_sorted(int32_t* __restrict__ 
   }
   if (!prepped) prep_body(zero, nzero, tile_open, ntiles, batch, M, B, gptr, blockIdx.x, gridDim.x);
   const int b1 = __syncthreads_or(bad & 1), b2 = __syncthreads_or(bad & 2);
-  if (threadIdx.x == 0) a.verdict[blockIdx.x] = (b1 ? 1 : 0) | (b2 ? 2 : 0);
+  const int b4 = __syncthreads_or(bad & 4), b8 = __syncthreads_or(bad & 8);
+  if (threadIdx.x == 0)
+    a.verdict[blockIdx.x] = (b1 ? 1 : 0) | (b2 ? 2 : 0) | (b4 ? 4 : 0) | (b8 ? 8 : 0);
 }
 
 // The build mode from k_prep_sorted's verdict words (block-uniform, every thread must call it):
@@ -288,13 +294,21 @@ __global__ __launch_bounds__(kThreads) void k_prep_sorted(int32_t* __restrict__ 
 //   kModeSortedOpen: target-sorted but some edge leaves its tile (lazy build) -> the sorted body
 //                writes the target CSR, the general launches build only the source CSR;
 //   kModeGeneral: the counting sort for both.
+// The summary word (verdict[kVerdictMax]) is the mode | kNoDrop when no input self loop is dropped
+// (graphs built with loop = False, or loops kept) | kAllDrop when every row drops exactly one
+// (k-NN with loop = True: each node is its own nearest neighbour, configs/config.py:47): the
+// sorted body's rowptr is then rs[d] + d * add_loop (- d) directly, with no scan across
+// workgroups. Readers mask with kModeMask.
 constexpr int kModeGeneral = 0, kModeSorted = 1, kModeSortedOpen = 2;
+constexpr int kModeMask = 3, kNoDrop = 4, kAllDrop = 8;
 __device__ __forceinline__ int sorted_mode(const int32_t* verdict, int nverdict) {
   if (!verdict) return kModeGeneral;
   int v = 0;
   for (int i = threadIdx.x; i < nverdict; i += blockDim.x) v |= verdict[i];
   const int b1 = __syncthreads_or(v & 1), b2 = __syncthreads_or(v & 2);
-  return b1 ? kModeGeneral : (b2 ? kModeSortedOpen : kModeSorted);
+  const int b4 = __syncthreads_or(v & 4), b8 = __syncthreads_or(v & 8);
+  const int flags = !b4 ? kNoDrop : (!b8 ? kAllDrop : 0);
+  return b1 ? kModeGeneral : ((b2 ? kModeSortedOpen : kModeSorted) | flags);
 }
 
 // Edge passes. A block takes a chunk of kChunk consecutive edges, kPer per thread, so every
@@ -446,9 +460,9 @@ __global__ __launch_bounds__(kThreads) void k_count(const int64_t* __restrict__ 
   __shared__ int hist[kBins];
   __shared__ int red[2 * kThreads / 64];
   __shared__ int tmk[kMarkWin];
-  const int mode = sorted_mode(verdict, nverdict);
+  const int summary = sorted_mode(verdict, nverdict), mode = summary & kModeMask;
   // the summary word for k_scan / k_fill / k_finish (one word to read instead of all of them)
-  if (verdict && blockIdx.x == 0 && threadIdx.x == 0) verdict[kVerdictMax] = mode;
+  if (verdict && blockIdx.x == 0 && threadIdx.x == 0) verdict[kVerdictMax] = summary;
   if (mode == kModeSorted) return;
   count_body<PER>(ei, E, N, loops, mode == kModeSortedOpen ? nullptr : cnt, tcnt, err, tile_open,
                   hist, red, blockIdx.x, tmk);
@@ -527,7 +541,7 @@ __global__ __launch_bounds__(kThreads) void k_fill(const int64_t* __restrict__ e
                                                    const int32_t* summary) {
   __shared__ int hist[kBins];
   __shared__ int red[2 * kThreads / 64];
-  const int mode = summary ? __builtin_amdgcn_readfirstlane(*summary) : kModeGeneral;
+  const int mode = summary ? __builtin_amdgcn_readfirstlane(*summary) & kModeMask : kModeGeneral;
   if (mode == kModeSorted) return;  // the sorted path took it
   fill_body<PER>(ei, E, N, loops, rowptr, mode == kModeSortedOpen ? nullptr : fill, col, eid, tptr,
                  tfill, tidx, teid, lazy_open, hist, red, blockIdx.x);
@@ -646,7 +660,7 @@ __device__ __forceinline__ void sorted_body(const SortedArgs& a, int64_t N, int3
                                             int32_t* __restrict__ rowptr,
                                             int32_t* __restrict__ col, float* __restrict__ w,
                                             int32_t* tile_open, int32_t* err_out, SortedSmem& ss,
-                                            int bx) {
+                                            int bx, int scanless) {
   constexpr int PASS = 8;  // entries per thread per copy pass
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t r0 = (int64_t)bx * kSortedRows;
@@ -680,39 +694,48 @@ __device__ __forceinline__ void sorted_body(const SortedArgs& a, int64_t N, int3
     ss.dis[tid] = a.dis[row];
   }
   if (tid == 0) ss.rs[nrow] = in1;
-  int x = v;  // inclusive scan in the wave
+  int excl;
+  if (scanless) {
+    // no input self loop dropped (kNoDrop) or exactly one per row (kAllDrop), by every
+    // workgroup's verdict: the entries before row d are the input edges before its head, rs[d],
+    // less d dropped loops (kAllDrop), plus one appended loop per earlier row — the integers the
+    // scan would yield, without the scan's look-back across workgroups
+    excl = (tid < nrow ? ss.rs[tid] : 0) + (int)row * (a.add_loop - (scanless == kAllDrop));
+  } else {
+    int x = v;  // inclusive scan in the wave
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) ss.wsum[wave] = x;
-  __syncthreads();
-  int tot = 0, before = 0;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) ss.wsum[wave] = x;
+    __syncthreads();
+    int tot = 0, before = 0;
 #pragma unroll
-  for (int q = 0; q < kSortedRows / 64; ++q) {
-    tot += ss.wsum[q];
-    before += q < wave ? ss.wsum[q] : 0;
-  }
-  // the flag word carries its own payload (the sum), so relaxed agent-scope atomics suffice: no
-  // release / acquire fence (an agent-scope release writes back the XCD's whole L2)
-  if (tid == 0)
-    __hip_atomic_store(&stat[bx], tot | kScanFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  int pre = 0;  // the preceding workgroups' sums, thread-strided, combined in a fixed order
-  for (int j = tid; j < bx; j += kSortedRows) {
-    int f;
-    while (((f = __hip_atomic_load(&stat[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) &
-            kScanFlag) == 0)
-      __builtin_amdgcn_s_sleep(1);
-    pre += f & (kScanFlag - 1);
-  }
-  for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
-  if (lane == 0) ss.wpre[wave] = pre;
-  __syncthreads();
-  int base = 0;
+    for (int q = 0; q < kSortedRows / 64; ++q) {
+      tot += ss.wsum[q];
+      before += q < wave ? ss.wsum[q] : 0;
+    }
+    // the flag word carries its own payload (the sum), so relaxed agent-scope atomics suffice: no
+    // release / acquire fence (an agent-scope release writes back the XCD's whole L2)
+    if (tid == 0)
+      __hip_atomic_store(&stat[bx], tot | kScanFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int pre = 0;  // the preceding workgroups' sums, thread-strided, combined in a fixed order
+    for (int j = tid; j < bx; j += kSortedRows) {
+      int f;
+      while (((f = __hip_atomic_load(&stat[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) &
+              kScanFlag) == 0)
+        __builtin_amdgcn_s_sleep(1);
+      pre += f & (kScanFlag - 1);
+    }
+    for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
+    if (lane == 0) ss.wpre[wave] = pre;
+    __syncthreads();
+    int base = 0;
 #pragma unroll
-  for (int q = 0; q < kSortedRows / 64; ++q) base += ss.wpre[q];
-  const int excl = base + before + x - v;
+    for (int q = 0; q < kSortedRows / 64; ++q) base += ss.wpre[q];
+    excl = base + before + x - v;
+  }
   if (tid < nrow) {
     rowptr[row] = excl;
     ss.rp[tid] = excl;
@@ -765,16 +788,18 @@ __global__ __launch_bounds__(kScanT) void k_scan(const int32_t* __restrict__ cnt
                                                  int32_t* err_out, int nblk) {
   __shared__ ScanSmem sm;
   __shared__ SortedSmem ss;
-  const int mode = sa.summary_ready
-                       ? (sa.verdict ? __builtin_amdgcn_readfirstlane(sa.verdict[kVerdictMax])
-                                     : kModeGeneral)
-                       : sorted_mode(sa.verdict, sa.nverdict);
+  const int summary = sa.summary_ready
+                          ? (sa.verdict ? __builtin_amdgcn_readfirstlane(sa.verdict[kVerdictMax])
+                                        : kModeGeneral)
+                          : sorted_mode(sa.verdict, sa.nverdict);
+  const int mode = summary & kModeMask;
   if (!sa.summary_ready && sa.verdict && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
-    sa.verdict[kVerdictMax] = mode;  // the summary word k_fill / k_finish read
+    sa.verdict[kVerdictMax] = summary;  // the summary word k_fill / k_finish read
   if (mode != kModeGeneral) {
     if (blockIdx.y == 0) {
       if ((int64_t)blockIdx.x * kSortedRows < N)
-        sorted_body(sa, N, stat, rowptr, col, w, tile_open, err_out, ss, blockIdx.x);
+        sorted_body(sa, N, stat, rowptr, col, w, tile_open, err_out, ss, blockIdx.x,
+                    summary & (kNoDrop | kAllDrop));
       return;
     }
     // sorted-open: the source scan (y = 1), its flags past the sorted body's (stat + 4 nblk)
@@ -999,7 +1024,7 @@ __global__ __launch_bounds__(kThreads) void k_finish(int64_t N, int64_t E, int a
   __shared__ int32_t s_key[kFinWaves][kFinishCap];
   __shared__ int32_t s_val[kFinWaves][kFinishCap];
   __shared__ int32_t s_ptr[kFinWaves][kFinT + 1];
-  const int mode = summary ? __builtin_amdgcn_readfirstlane(*summary) : kModeGeneral;
+  const int mode = summary ? __builtin_amdgcn_readfirstlane(*summary) & kModeMask : kModeGeneral;
   if (mode == kModeSorted) return;  // the sorted path took it
   if (mode == kModeSortedOpen && blockIdx.y == 0) return;  // target CSR: k_scan's sorted body
   const int wave = threadIdx.x >> 6;
@@ -1226,7 +1251,7 @@ extern "C" int lgnn_graph_build_path(const void* workspace, int64_t num_nodes, i
                      as_stream(stream)) != hipSuccess ||
       hipStreamSynchronize(as_stream(stream)) != hipSuccess)
     return LGNN_EINVAL;
-  return v;  // kModeGeneral 0, kModeSorted 1, kModeSortedOpen 2
+  return v & kModeMask;  // kModeGeneral 0, kModeSorted 1, kModeSortedOpen 2
 }
 
 // the target-sorted fast path is tried unless LGNN_GRAPH_SORTED=0 (a test / A-B knob)

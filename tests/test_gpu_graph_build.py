@@ -85,6 +85,14 @@ def _sorted_cases():
     return {
         "knn_c2": ((ei, n), "sorted"),
         "knn_noloop": ((noloop.edge_index, noloop.num_nodes), "sorted"),
+        # no input self loop (k_scan's sorted body without its scan) with an empty row and
+        # trailing isolated nodes; every row with exactly one loop is knn_c2 / k16 / dup_edge
+        "noloop_gap_row": ((noloop.edge_index[:, noloop.edge_index[1] != 7],
+                            noloop.num_nodes + 3), "sorted"),
+        "powerlaw_noloop": ((synth.make_batch(40, k=4, seed=12, sizes="powerlaw",
+                                              loop=False).edge_index,
+                             synth.make_batch(40, k=4, seed=12, sizes="powerlaw",
+                                              loop=False).num_nodes), "sorted_open"),
         "k16": ((k16.edge_index, k16.num_nodes), "sorted"),
         "gap_row": ((ei[:, keep], n), "sorted"),
         "trailing_isolated": ((ei, n + 20), "sorted"),
