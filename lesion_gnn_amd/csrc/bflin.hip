@@ -152,6 +152,7 @@ __global__ __launch_bounds__(NT) void k_bf_gemm(const void* __restrict__ A, int6
                                                 AttOut att = AttOut{}) {
   __shared__ __attribute__((aligned(16))) unsigned char img[2][TM * ROWB];
   __shared__ __attribute__((aligned(16))) float ytile[ATT ? TM * YLD : 1];
+  __shared__ float attv[ATT ? 256 : 1];  // att_src / att_dst (the chains read LDS only)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, li = lane & 31;
   const int64_t r0 = xcd_block() * TM;
@@ -267,6 +268,10 @@ __global__ __launch_bounds__(NT) void k_bf_gemm(const void* __restrict__ A, int6
           ytile[m * YLD + n] = (q ? acc1[r] : acc0[r]) + bv;
         }
     }
+    if (tid < N) {  // N = H C <= 128 (lgnn_bf16_gemm_att)
+      attv[tid] = att.src[tid];
+      attv[128 + tid] = att.dst[tid];
+    }
     __syncthreads();
     const int H = att.H, C = att.C;
     const int64_t rows = M - r0 < TM ? M - r0 : TM;
@@ -274,9 +279,10 @@ __global__ __launch_bounds__(NT) void k_bf_gemm(const void* __restrict__ A, int6
       const int m = p / H, hd = p % H;
       if (m >= rows) continue;
       const float* yr = ytile + m * YLD + hd * C;
-      const float* ws = att.src + hd * C;
-      const float* wd = att.dst + hd * C;
+      const float* ws = attv + hd * C;
+      const float* wd = attv + 128 + hd * C;
       float ps = 0.f, pd = 0.f;
+#pragma unroll 8
       for (int c = 0; c < C; ++c) {
         ps = fmaf(yr[c], ws[c], ps);
         pd = fmaf(yr[c], wd[c], pd);

@@ -256,8 +256,12 @@ __device__ __forceinline__ void gemm_tile(unsigned char (&img)[2][PLANES * IMG],
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), bY, (m * N + ncol) * 4, 0, 0);
     }
   if constexpr (ATT) {
-    static_assert(TM * YLD * 4 <= 2 * PLANES * IMG, "the Y tile fits in the A images");
+    static_assert((TM * YLD + 256) * 4 <= 2 * PLANES * IMG, "the Y tile fits in the A images");
     float* ytile = reinterpret_cast<float*>(&img[0][0]);
+    // att_src / att_dst staged beside the tile: the chains below then read LDS only (from global
+    // memory every step of a chain waited on an L1/L2 round trip: 19.2 vs 14.4 us per launch at
+    // the reference lins, K = 128)
+    float* attv = ytile + TM * YLD;
     lds_barrier();  // every wave's last image reads are done
     if (nok) {
 #pragma unroll
@@ -268,6 +272,10 @@ __device__ __forceinline__ void gemm_tile(unsigned char (&img)[2][PLANES * IMG],
           ytile[m * YLD + n] = acc[q][r] + bv;
         }
     }
+    if (tid < N) {  // N = H C <= 128 (lgnn_s3_gemm_att)
+      attv[tid] = att.src[tid];
+      attv[128 + tid] = att.dst[tid];
+    }
     lds_barrier();
     const int H = att.H, C = att.C;
     const int64_t rows = M - r0 < 32 * MT ? M - r0 : 32 * MT;
@@ -275,9 +283,10 @@ __device__ __forceinline__ void gemm_tile(unsigned char (&img)[2][PLANES * IMG],
       const int m = p / H, hd = p % H;
       if (m >= rows) continue;
       const float* yr = ytile + m * YLD + hd * C;
-      const float* ws = att.src + hd * C;
-      const float* wd = att.dst + hd * C;
+      const float* ws = attv + hd * C;
+      const float* wd = attv + 128 + hd * C;
       float ps = 0.f, pd = 0.f;
+#pragma unroll 8
       for (int c = 0; c < C; ++c) {
         ps = fmaf(yr[c], ws[c], ps);
         pd = fmaf(yr[c], wd[c], pd);
