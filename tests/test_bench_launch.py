@@ -48,3 +48,28 @@ def test_world_size_mismatch_refused():
                   env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode != 0
     assert "WORLD_SIZE=2" in (p.stderr + p.stdout)
+
+
+def test_pmc_traffic_prefers_the_workloads_own_pass():
+    """bench.pmc_traffic: a "<workload>:<kernel>" key (the PMC pass recorded for that workload)
+    wins over the bare kernel name, which stays the fallback; unknown kernels give (None, None).
+    Every kernel the committed traffic table names resolves with its source file present."""
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import bench
+
+    table = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
+    for key, v in table.items():
+        assert v["bytes_per_launch"] > 0
+        fname = v["source"].split(" ")[0]  # a note may follow the file name
+        assert os.path.exists(os.path.join(ROOT, "profiles", fname)), v["source"]
+    bare = [k for k in table if ":" not in k.split("(")[0]]
+    wl = [k for k in table if ":" in k.split("(")[0]]
+    assert bare and wl
+    k = wl[0]
+    w, kern = k.split(":", 1)
+    b, src = bench.pmc_traffic(kern, w)
+    assert (b, src) == (table[k]["bytes_per_launch"], table[k]["source"])
+    b0, src0 = bench.pmc_traffic(bare[0])
+    assert (b0, src0) == (table[bare[0]]["bytes_per_launch"], table[bare[0]]["source"])
+    assert bench.pmc_traffic("no_such_kernel", "c2") == (None, None)
