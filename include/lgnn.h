@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 35
+#define LGNN_ABI_VERSION 36
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -34,9 +34,14 @@ extern "C" {
 #define LGNN_EBUSY (-16) /* a grid-barrier launch cannot have all its workgroups resident */
 
 /* tile flag arrays (tile_open) hold ceil(N/64) + LGNN_TILE_OPEN_EXTRA int32: one flag per 64-node
- * tile, the number of flagged tiles, then six words the fused GCN stack kernels use as grid-barrier
- * counters for their open-tile phase (zeroed by whoever writes the flags, re-armed by the kernels) */
-#define LGNN_TILE_OPEN_EXTRA 7
+ * tile, the number of flagged tiles, six words the fused GCN stack kernels use as grid-barrier
+ * counters for their open-tile phase (zeroed by whoever writes the flags, re-armed by the kernels),
+ * then LGNN_SLOT_FLAGS partial-slot skip words at [ceil(N/64) + LGNN_SLOT_FLAG0 + b]: set by
+ * lgnn_gcn_stack_bwd_s3f for a workgroup b that processed no closed tile and so wrote no partial
+ * slot, read by lgnn_node_linear_bwd_tiles(..., accumulate = 2) (see there) */
+#define LGNN_SLOT_FLAG0 7
+#define LGNN_SLOT_FLAGS 256
+#define LGNN_TILE_OPEN_EXTRA (LGNN_SLOT_FLAG0 + LGNN_SLOT_FLAGS)
 
 /* self-loop handling of the graph build (which PyG utility the conv applies to edge_index) */
 #define LGNN_LOOPS_KEEP 0      /* GINConv: edges used as given (KNN loop=True self pairs kept) */
@@ -102,15 +107,25 @@ int lgnn_graph_build_lazy(const int64_t* edge_index, int64_t E, int64_t N, int l
                           float* tw, int32_t* tmap, int32_t* tile_open, const int64_t* batch,
                           int64_t num_graphs, int32_t* gptr, int32_t* err_count, void* workspace,
                           size_t workspace_bytes, void* stream);
-/* lgnn_graph_build_sync: the same build (lazy != 0: as lgnn_graph_build_lazy) in ONE persistent
- * launch — the five phases behind grid barriers, every workgroup resident at once (grid sized from
- * the occupancy query). sync: 4 int32 owned by the caller, zero before the first call and re-armed
- * by every launch (one sync triple per stream: two builds that may run concurrently need two). */
-int lgnn_graph_build_sync(const int64_t* edge_index, int64_t E, int64_t N, int loops, int norm,
-                          int32_t* rowptr, int32_t* col, float* w, int32_t* tptr, int32_t* tidx,
-                          float* tw, int32_t* tmap, int32_t* tile_open, const int64_t* batch,
-                          int64_t num_graphs, int32_t* gptr, int32_t* err_count, void* workspace,
-                          size_t workspace_bytes, int lazy, int32_t* sync, void* stream);
+/* lgnn_graph_build[_lazy] (lazy != 0: the lazy variant) whose first launch also writes the split-3
+ * weight planes of `job` (what lgnn_weight_planes(job->nl, job->W, job->widths, job->planes,
+ * job->planes_t) writes, bitwise) as extra workgroups: the planes a fused GCN stack forward reads
+ * are made from the live weights by every forward that builds its graph, with no launch of their
+ * own (a captured step replays the split, so weights written between replays are seen). */
+#define LGNN_PLANE_JOB_MAX 8
+typedef struct lgnn_plane_job {
+  int nl;                                /* layers, 1..LGNN_PLANE_JOB_MAX */
+  int widths[LGNN_PLANE_JOB_MAX + 1];    /* W[l] is [widths[l+1]][widths[l]] */
+  const float* W[LGNN_PLANE_JOB_MAX];
+  uint16_t* planes;                      /* lgnn_weight_planes_bytes(nl) */
+  uint16_t* planes_t;                    /* nullable: the transposed planes */
+} lgnn_plane_job;
+int lgnn_graph_build_planes(const int64_t* edge_index, int64_t E, int64_t N, int loops, int norm,
+                            int32_t* rowptr, int32_t* col, float* w, int32_t* tptr,
+                            int32_t* tidx, float* tw, int32_t* tmap, int32_t* tile_open,
+                            const int64_t* batch, int64_t num_graphs, int32_t* gptr,
+                            int32_t* err_count, void* workspace, size_t workspace_bytes, int lazy,
+                            const lgnn_plane_job* job, void* stream);
 
 /* Diagnostic (synchronises `stream`): 1 when the last lgnn_graph_build[_lazy] on `workspace`
  * took the target-sorted fast path, 0 when it ran the general launches. Meaningful only after a
@@ -230,7 +245,10 @@ int lgnn_node_linear_bwd(int grad_mode, const float* dY, const int64_t* batch, c
 /* Same, restricted to the 64-node tiles t with (tile_open[t] != 0) == want_open; with
  * accumulate = 1 a workgroup that processed a tile adds its dW/db into partial slot blockIdx.x
  * (num_partials = lgnn_gcn_stack_bwd_partials, slots written by lgnn_gcn_stack_bwd) instead of
- * overwriting it, and a workgroup that processed none leaves its slot alone. Fast path only. */
+ * overwriting it, and a workgroup that processed none leaves its slot alone. accumulate = 2 (after
+ * lgnn_gcn_stack_bwd_s3f, num_partials <= LGNN_SLOT_FLAGS): the same, except for slots whose skip
+ * word in tile_open is set (the fused kernel wrote nothing there): those are written, with zeros
+ * by a workgroup that processed no tile. Fast path only. */
 int lgnn_node_linear_bwd_tiles(int grad_mode, const float* dY, const int64_t* batch,
                                const int32_t* gptr, int pool_mean, const int32_t* tptr,
                                const int32_t* tidx, const float* tw, float tself, const float* H,
@@ -255,23 +273,6 @@ int lgnn_reduce_jobs(int n, const float* const* partials, const float* const* fa
                      float* const* out, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
- * Windowed dense aggregation (ABI v35), the layer-wise GCN path's open tiles:
- *   out[r] = sum_{e in row r} w_e in[col_e]   for the rows of the 64-row tiles t with
- *   (tile_mask[t] != 0) == (want != 0) (tile_mask NULL: every tile); other rows untouched.
- * Replaces the per-entry row gather of GCNConv's propagate (reference gin.py / PyG
- * MessagePassing.propagate, aggr='add' over gcn_norm weights) for graphs that straddle tiles:
- * each tile multiplies the dense 64 x 64 blocks of its entries per 64-row source chunk by that
- * chunk's rows (split-3 bf16 MFMA, fp32 accuracy; the per-row sum is not in CSR order). Chunks
- * whose tile is not selected are never read (an edge between two tiles marks both open). Tiles
- * whose sources span more than max_chunks chunks, or with more than 2048 entries, take the
- * per-row gather (CSR order). width must be 128 (row stride of in / out). w NULL: weight 1.
- * Called with the transpose CSR (tptr, tidx, tw) it is the aggregation's backward, A_hat^T dY.
- * ------------------------------------------------------------------------------------------- */
-int lgnn_window_aggregate(const int32_t* rowptr, const int32_t* col, const float* w, int64_t M,
-                          const float* in, int width, float* out, const int32_t* tile_mask,
-                          int want, int max_chunks, void* stream);
-
-/* ---------------------------------------------------------------------------------------------
  * Sparse aggregation alone (no linear): Y_i = self_scale*X_i + sum_{e in row i} w_e X[col_e].
  * Replaces: torch_sparse spmm(adj_t, x, 'sum') / PyG propagate(aggr='add') (GINConv, and the
  * transposed pass of every conv backward when called with the transpose CSR).
@@ -289,30 +290,6 @@ int lgnn_spmm(const int32_t* rowptr, const int32_t* col, const float* w, float s
 int lgnn_pool_head_fwd(const float* H, const int32_t* gptr, int64_t B, int D, int pool_mean,
                        const float* Wout, const float* bout, int C, float* pooled,
                        float* logits, void* stream);
-
-/* lgnn_pool_head_fwd (D % 4 == 0, 1 <= C <= 16) with the criterion's forward folded in (ABI v34):
- * nn.CrossEntropyLoss(weight), mean reduction (reference models/base.py:93-94) — lgnn_ce_fwd's
- * outputs and arithmetic, bitwise: lse [B], loss [1], wsum [1], bad [1] (1 if a target is outside
- * [0, C); such graphs skipped). The last workgroup to finish sums the per-graph terms.
- * ABI v35: also the per-graph factors of the logits gradient, pm [B][C] = exp(z - lse) - [c == y]
- * and wt [B] = weight[y] (1 unweighted, 0 for a target outside [0, C)), so that a consumer forms
- * lgnn_ce_bwd's dlogits[i][c] = grad_loss * wt[i] / wsum * pm[i][c] from plain loads (lgnn_ce_src).
- * ticket: uint32[10] zero before the first call, re-armed by every call (one stream at a time).
- * workspace: lgnn_pool_head_ce_workspace_bytes(B) bytes. */
-size_t lgnn_pool_head_ce_workspace_bytes(int64_t num_graphs);
-int lgnn_pool_head_ce_fwd(const float* H, const int32_t* gptr, int64_t B, int D, int pool_mean,
-                          const float* Wout, const float* bout, int C, float* pooled,
-                          float* logits, const int64_t* target, const float* weight, float* lse,
-                          float* loss, float* wsum, int* bad, float* pm, float* wt,
-                          unsigned int* ticket, void* workspace, size_t workspace_bytes,
-                          void* stream);
-
-/* The same with each graph split over `splits` workgroups (few, large graphs: the GAT configs);
- * part: [B][splits][D] scratch; tickets: int32 [B], zero on entry, left zero. Each graph's
- * column sums are its splits' fixed-order partial sums added in split order. */
-int lgnn_pool_head_fwd_split(const float* H, const int32_t* gptr, int64_t B, int D, int pool_mean,
-                             const float* Wout, const float* bout, int C, int splits, float* part,
-                             int32_t* tickets, float* pooled, float* logits, void* stream);
 
 /* Backward of lgnn_pool_head_fwd's Linear part:
  *   dpooled = dlogits Wout;  dWout = dlogits^T pooled;  dbout = colsum(dlogits). */
@@ -418,23 +395,6 @@ int lgnn_node_linear_bwd_bn_gather(const float* dS, const int32_t* tptr, const i
                                    const float* bn_scale, const float* bn_shift,
                                    const float* bn_mean, const float* bn_invstd,
                                    double* gstats_part, void* stream);
-/* Split-3 variants (bf16 MFMA at fp32 accuracy, liblgnn lin3.hip) of the two calls below: the
- * same arguments with `planes` / `planes_t` (lgnn_weight_planes of W: the weight and, for dX, the
- * transposed planes of this one layer) in place of W; either BN option (or none: stats_part and
- * bn_scale NULL, bn_mode 0) as lgnn_node_linear_fwd_bn / _bwd_bn. */
-int lgnn_node_linear_fwd_s3(const float* X, int64_t M, int K, const int32_t* rowptr,
-                            const int32_t* col, const float* w, float self_scale,
-                            const uint16_t* planes, const float* b, int N, int act, float* Y,
-                            float* S_out, double* stats_part, const float* bn_scale,
-                            const float* bn_shift, const float* bn_mask, float* bn_out,
-                            void* stream);
-int lgnn_node_linear_bwd_s3(int bn_mode, const float* dY, const float* H, int act,
-                            const float* X, int64_t M, int K, const uint16_t* planes_t, int N,
-                            float* dXpre, float* dW_partial, float* db_partial, int num_partials,
-                            const float* bn_Z, const float* bn_mask, const float* bn_scale,
-                            const float* bn_shift, const float* bn_mean, const float* bn_invstd,
-                            double* gstats_part, const double* bn_sums, double count,
-                            int training, void* stream);
 int lgnn_bn_fused_partials(int64_t num_rows);
 int lgnn_node_linear_fwd_bn(const float* X, int64_t M, int K, const int32_t* rowptr,
                             const int32_t* col, const float* w, float self_scale, const float* W,
@@ -573,14 +533,14 @@ int lgnn_ce_fwd_factors(const float* logits, const int64_t* target, const float*
                         float* pm, float* wt, void* stream);
 /* The CE logits gradient without materialising it (ABI v33; v35: from the readout's pm / wt): the
  * consumers form lgnn_ce_bwd's dlogits[i][c] = gloss * wt[i] / wsum * pm[i][c] themselves, bit
- * for bit (lgnn_pool_head_ce_fwd writes pm and wt with lgnn_ce_bwd's expressions).
+ * for bit (lgnn_ce_fwd_factors writes pm and wt with lgnn_ce_bwd's expressions).
  * lgnn_reduce_jobs_ce = lgnn_reduce_jobs where jobs with ce_job[j] != 0 take the [P][C] logits
  * gradient (P = B) in place of partials[j] (which may be NULL): out_proj's db (len C) and
  * dW = dlogits^T pooled (factor = pooled, len C * width). The same sums as lgnn_reduce_jobs on
  * lgnn_ce_bwd's output, bitwise. */
 typedef struct lgnn_ce_src {
-  const float* pm;     /* [B][C] exp(z - lse) - [c == y] (lgnn_pool_head_ce_fwd) */
-  const float* wt;     /* [B] weight[y] (lgnn_pool_head_ce_fwd) */
+  const float* pm;     /* [B][C] exp(z - lse) - [c == y] (lgnn_ce_fwd_factors) */
+  const float* wt;     /* [B] weight[y] (lgnn_ce_fwd_factors) */
   const float* wsum;   /* [1] */
   const float* gloss;  /* [1] gradient of the loss */
 } lgnn_ce_src;
@@ -617,11 +577,6 @@ int lgnn_regression_bwd(const float* z, const void* target, int target_is_i64, i
  * ------------------------------------------------------------------------------------------- */
 int lgnn_gcn_stack_bwd_partials(int64_t num_nodes);
 
-/* Variant of the fused split-3 backward (lgnn_gcn_stack_bwd_s3f[_all] with the forward's Â^T
- * hand-over): 4 = one wave per SIMD (the default), 8 = two waves per SIMD (k_s3_fbwd8, opt-in;
- * same results to the parity bar, slower at C2). Returns the previous value, LGNN_EINVAL for any
- * other argument. Process-wide; not synchronised with launches in flight on other threads. */
-int lgnn_s3f_set_waves(int waves);
 int lgnn_gcn_stack_bwd(const float* dP, const int64_t* batch, const int32_t* gptr, int pool_mean,
                        const int32_t* rowptr, const int32_t* col, const float* w, const float* X,
                        int64_t M, int L, const float* const* W, const float* const* H,
@@ -643,19 +598,6 @@ int lgnn_adam_step(int n, float* const* params, const float* const* grads, float
                    unsigned int* ticket, float lr, float beta1, float beta2, float eps,
                    float weight_decay, int decoupled, int maximize, int advance,
                    void* stream);
-/* lgnn_adam_step that also writes the split-3 weight planes of updated weights (ABI v34): for
- * every tensor i with planes[i] != NULL (a [rows[i]][cols[i]] weight, both <= 128) the new
- * values' three bf16 planes go to planes[i] (lgnn_weight_planes' layout of that layer: 3 planes
- * of 128 x 128, fragment order, feature order perm16) and, when planes_t[i] != NULL, the
- * transposed planes to planes_t[i] — bitwise what lgnn_weight_planes writes from the new
- * weights (padding positions are left as they are: the caller's planes hold zeros there). The
- * next forward then needs no weight-plane launch. */
-int lgnn_adam_step_planes(int n, float* const* params, const float* const* grads,
-                          float* const* exp_avg, float* const* exp_avg_sq, const int64_t* numels,
-                          float* step, unsigned int* ticket, float lr, float beta1, float beta2,
-                          float eps, float weight_decay, int decoupled, int maximize, int advance,
-                          uint16_t* const* planes, uint16_t* const* planes_t, const int* rows,
-                          const int* cols, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Fused GCN stack backward on split-3 bf16 MFMA (fp32 accuracy), every layer of a tile in one

@@ -22,7 +22,9 @@ LGNN_NORM_NONE, LGNN_NORM_GCN = 0, 1
 LGNN_ACT_NONE, LGNN_ACT_ELU = 0, 1
 LGNN_BN_GSTATS, LGNN_BN_GIN = 3, 4
 LGNN_GRAD_DIRECT, LGNN_GRAD_POOL, LGNN_GRAD_TRANSPOSE = 0, 1, 2
-LGNN_TILE_OPEN_EXTRA = 7  # tile_open words after the per-tile flags (count + barrier words)
+LGNN_SLOT_FLAG0 = 7  # tile_open: count + six barrier words, then the partial-slot skip words
+LGNN_SLOT_FLAGS = 256
+LGNN_TILE_OPEN_EXTRA = LGNN_SLOT_FLAG0 + LGNN_SLOT_FLAGS  # words after the per-tile flags
 LGNN_S3_ADJT_TILE_BYTES = 16384  # lgnn.h: fp32 Â per tile, split-3 forward -> fused backward
 
 P = ctypes.c_void_p
@@ -39,6 +41,16 @@ class CeSrc(ctypes.Structure):
     _fields_ = [("pm", P), ("wt", P), ("wsum", P), ("gloss", P)]
 
 
+LGNN_PLANE_JOB_MAX = 8
+
+
+class PlaneJob(ctypes.Structure):
+    """lgnn_plane_job (include/lgnn.h): the split-3 weight planes lgnn_graph_build_planes writes
+    beside the build (lgnn_weight_planes' arguments)."""
+    _fields_ = [("nl", I32), ("widths", I32 * (LGNN_PLANE_JOB_MAX + 1)),
+                ("W", P * LGNN_PLANE_JOB_MAX), ("planes", P), ("planes_t", P)]
+
+
 # name -> (restype, argtypes); mirrors include/lgnn.h exactly
 SIGNATURES: dict[str, tuple] = {
     "lgnn_abi_version": (I32, []),
@@ -49,8 +61,8 @@ SIGNATURES: dict[str, tuple] = {
                                     P, SZ, P]),
     "lgnn_graph_build": (I32, [P, I64, I64, I32, I32, P, P, P, P, P, P, P, P, P, I64, P, P, P,
                                SZ, P]),
-    "lgnn_graph_build_sync": (I32, [P, I64, I64, I32, I32, P, P, P, P, P, P, P, P, P, I64, P, P,
-                                    P, SZ, I32, P, P]),
+    "lgnn_graph_build_planes": (I32, [P, I64, I64, I32, I32, P, P, P, P, P, P, P, P, P, I64, P,
+                                      P, P, SZ, I32, P, P]),
     "lgnn_batch_ptr": (I32, [P, I64, I64, P, P]),
     "lgnn_node_linear_fwd": (I32, [P, I64, I32, P, P, P, F32, P, P, I32, I32, P, P, P]),
     "lgnn_bwd_num_partials": (I32, [I64, I32, I32, I32]),
@@ -60,11 +72,8 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_node_linear_bwd_tiles": (I32, [I32, P, P, P, I32, P, P, P, F32, P, I32, P, I64, I32,
                                          P, P, P, F32, P, I32, P, P, P, I32, P, I32, I32, P]),
     "lgnn_gcn_stack_bwd_partials": (I32, [I64]),
-    "lgnn_s3f_set_waves": (I32, [I32]),
     "lgnn_adam_step": (I32, [I32, P, P, P, P, P, P, P, F32, F32, F32, F32, F32, I32, I32, I32,
                              P]),
-    "lgnn_adam_step_planes": (I32, [I32, P, P, P, P, P, P, P, F32, F32, F32, F32, F32, I32, I32,
-                                    I32, P, P, P, P, P]),
     "lgnn_gcn_stack_bwd": (I32, [P, P, P, I32, P, P, P, P, I64, I32, P, P, P, P, P, I32, P, P]),
     "lgnn_spmm": (I32, [P, P, P, F32, P, I64, I32, P, P]),
     "lgnn_reduce_partials_multi": (I32, [I32, P, P, P, P, P]),
@@ -72,13 +81,8 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_reduce_jobs_ce": (I32, [I32, P, P, P, P, P, P, P, ctypes.POINTER(CeSrc), I32, P]),
     "lgnn_ce_fwd": (I32, [P, P, P, I64, I32, P, P, P, P, P]),
     "lgnn_ce_fwd_factors": (I32, [P, P, P, I64, I32, P, P, P, P, P, P, P]),
-    "lgnn_window_aggregate": (I32, [P, P, P, I64, P, I32, P, P, I32, I32, P]),
     "lgnn_ce_bwd": (I32, [P, P, P, I64, I32, P, P, P, P, P]),
     "lgnn_pool_head_fwd": (I32, [P, P, I64, I32, I32, P, P, I32, P, P, P]),
-    "lgnn_pool_head_ce_workspace_bytes": (SZ, [I64]),
-    "lgnn_pool_head_ce_fwd": (I32, [P, P, I64, I32, I32, P, P, I32, P, P, P, P, P, P, P, P, P, P,
-                                    P, P, SZ, P]),
-    "lgnn_pool_head_fwd_split": (I32, [P, P, I64, I32, I32, P, P, I32, I32, P, P, P, P, P]),
     "lgnn_pool_head_bwd": (I32, [P, P, I64, I32, P, I32, P, P, P, P]),
     "lgnn_pool_bwd": (I32, [P, P, P, I64, I32, I32, P, P]),
     "lgnn_bn_workspace_bytes": (SZ, [I64, I32]),
@@ -134,10 +138,6 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_node_linear_bwd_bn_pool": (I32, [I32, P, P, I32, P, I64, I32, P, I32, P, P, P, I32, P,
                                            P, P, P, P, P, P, P, F64, I32, P, P, I32, P, P, I32,
                                            P]),
-    "lgnn_node_linear_fwd_s3": (I32, [P, I64, I32, P, P, P, F32, P, P, I32, I32, P, P, P, P, P, P,
-                                      P, P]),
-    "lgnn_node_linear_bwd_s3": (I32, [I32, P, P, I32, P, I64, I32, P, I32, P, P, P, I32, P, P, P,
-                                      P, P, P, P, P, F64, I32, P]),
     "lgnn_gcn_stack_bwd_s3f": (I32, [P, P, P, I32, I64, P, P, P, P, I64, I32, P, P, P, P, P,
                                      I32, P, P, P]),
     "lgnn_gcn_stack_fwd_s3_all": (I32, [P, I64, I32, I32, P, P, P, I32, P, P, P, P, P, P, P, P, P]),
@@ -162,7 +162,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 35
+ABI_VERSION = 36
 
 _lib = None
 

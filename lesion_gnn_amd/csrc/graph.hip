@@ -16,6 +16,7 @@
 // The result is identical run to run.
 #include "common.h"
 #include "tile_util.h"
+#include "s3_util.h"
 
 namespace {
 
@@ -23,9 +24,6 @@ constexpr int kThreads = 256;
 constexpr int kFinT = 64;          // k_finish: rows (threads) per block
 constexpr int kFinishCap = 1536;   // staged CSR entries per k_finish block
 constexpr int kLongRow = 24;       // k_finish: longer staged rows are sorted by the whole wave
-// k_build's barrier bound (~4 s): a row longer than kFinishCap is sorted by one thread in global
-// memory (seconds for thousands of entries) while the other workgroups wait at the next barrier
-constexpr int kBuildSpins = 1 << 24;
 // Target-sorted fast path (k_prep_sorted + the sorted body of k_scan): rows of at most
 // kSortedRowCap CSR entries (a 64-row tile then stays within the fused kernels' 1024 staged
 // entries), runs of at most kGapCap rows without entries, at most one self loop per row
@@ -144,12 +142,21 @@ __device__ __forceinline__ void prep_body(int32_t* __restrict__ zero, int64_t nz
   }
 }
 
+// workgroups past the build's own grid (gx) run the weight-plane side job (lgnn_graph_build_planes)
+__device__ __forceinline__ bool plane_side_job(const lgnn_s3::PlaneArgs& pj, int gx) {
+  if ((int)blockIdx.x < gx) return false;
+  lgnn_s3::wplanes_item(pj, ((int)blockIdx.x - gx) * kThreads + threadIdx.x);
+  return true;
+}
+
 __global__ __launch_bounds__(kThreads) void k_prep(int32_t* __restrict__ zero, int64_t nzero,
                                                    int32_t* __restrict__ tile_open,
                                                    int64_t ntiles,
                                                    const int64_t* __restrict__ batch, int64_t M,
-                                                   int64_t B, int32_t* __restrict__ gptr) {
-  prep_body(zero, nzero, tile_open, ntiles, batch, M, B, gptr, blockIdx.x, gridDim.x);
+                                                   int64_t B, int32_t* __restrict__ gptr,
+                                                   lgnn_s3::PlaneArgs pj, int gx) {
+  if (plane_side_job(pj, gx)) return;
+  prep_body(zero, nzero, tile_open, ntiles, batch, M, B, gptr, blockIdx.x, gx);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -191,7 +198,9 @@ __global__ __launch_bounds__(kThreads) void k_prep_sorted(int32_t* __restrict__ 
                                                           const int64_t* __restrict__ batch,
                                                           int64_t M, int64_t B,
                                                           int32_t* __restrict__ gptr,
-                                                          SortedArgs a) {
+                                                          SortedArgs a, lgnn_s3::PlaneArgs pj,
+                                                          int gx) {
+  if (plane_side_job(pj, gx)) return;  // (block-uniform: before any barrier)
   constexpr int CH = kSortedChunks;
   const int64_t E = a.E, N = M;
   const int64_t* __restrict__ src = a.ei;
@@ -199,7 +208,7 @@ __global__ __launch_bounds__(kThreads) void k_prep_sorted(int32_t* __restrict__ 
   const bool drop_loops = a.loops != LGNN_LOOPS_KEEP;
   const int lane = threadIdx.x & 63;
   const int64_t wv = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
-  const int64_t nwv = ((int64_t)gridDim.x * kThreads) >> 6;
+  const int64_t nwv = ((int64_t)gx * kThreads) >> 6;
   int bad = 0;
   bool prepped = false;
   // a wave takes CH chunks of 64 consecutive edges (+ one chunk of look-ahead for the row that
@@ -215,7 +224,7 @@ __global__ __launch_bounds__(kThreads) void k_prep_sorted(int32_t* __restrict__ 
     }
     const int64_t before = base > 0 ? dst[base - 1] : -1;
     if (!prepped) {
-      prep_body(zero, nzero, tile_open, ntiles, batch, M, B, gptr, blockIdx.x, gridDim.x);
+      prep_body(zero, nzero, tile_open, ntiles, batch, M, B, gptr, blockIdx.x, gx);
       prepped = true;
     }
 #pragma unroll
@@ -281,7 +290,7 @@ __global__ __launch_bounds__(kThreads) void k_prep_sorted(int32_t* __restrict__ 
       }
     }
   }
-  if (!prepped) prep_body(zero, nzero, tile_open, ntiles, batch, M, B, gptr, blockIdx.x, gridDim.x);
+  if (!prepped) prep_body(zero, nzero, tile_open, ntiles, batch, M, B, gptr, blockIdx.x, gx);
   const int b1 = __syncthreads_or(bad & 1), b2 = __syncthreads_or(bad & 2);
   const int b4 = __syncthreads_or(bad & 4), b8 = __syncthreads_or(bad & 8);
   if (threadIdx.x == 0)
@@ -1047,90 +1056,6 @@ __global__ __launch_bounds__(kThreads) void k_tmap(const int32_t* __restrict__ t
     tmap[q] = inv[teid[q]];
 }
 
-// ---------------------------------------------------------------------------------------------
-// The whole build in ONE persistent launch (k_build): the phases of the launches above (prep,
-// count, scan, fill, finish, tmap) run back to back, separated by grid barriers (tile_util.h
-// grid_sync on a caller-owned, self-re-arming word triple), each workgroup striding over the
-// phase's virtual blocks. Every workgroup must be resident at once: the grid is sized from the
-// occupancy query. The finish phase runs its 64-row virtual blocks one per wave. Saves the
-// launch gaps and the fill / drain of five dependent launches (C2: 36 -> see DESIGN §4.1).
-struct BuildArgs {
-  const int64_t* ei;
-  int64_t E, N;
-  int loops, norm, add_loop, lazy;
-  int32_t *rowptr, *col, *tptr, *tidx, *tmap, *tile_open, *gptr, *err_count;
-  float *w, *tw;
-  const int64_t* batch;
-  int64_t num_graphs;
-  GraphWs ws;
-};
-
-union BuildSmem {
-  struct {
-    int hist[kBins];
-    int red[2 * kThreads / 64];
-  } e;
-  ScanSmem scan;
-  struct {
-    int32_t key[kThreads / 64][kFinishCap];
-    int32_t val[kThreads / 64][kFinishCap];
-    int32_t ptr[kThreads / 64][kFinT + 1];
-  } fin;
-};
-
-__global__ __launch_bounds__(kThreads) void k_build(BuildArgs a, int32_t* sync) {
-  __shared__ BuildSmem sm;
-  const int G = gridDim.x, b = blockIdx.x;
-  const int64_t N = a.N, E = a.E, ntiles = (N + 63) / 64;
-  {
-    const int64_t nzero = (int64_t)(a.ws.zero_bytes / 4);
-    prep_body(a.ws.err, nzero, a.tile_open, ntiles, a.batch, N, a.num_graphs, a.gptr, b, G);
-  }
-  lgnn_tile::grid_sync(sync, 1, kBuildSpins);
-  const int64_t nch = (E + kChunk - 1) / kChunk;
-  for (int64_t c = b; c < nch; c += G) {
-    __syncthreads();  // the previous chunk's LDS reads are done
-    count_body(a.ei, E, N, a.loops, a.ws.cnt, a.tptr ? a.ws.tcnt : nullptr, a.ws.err,
-               a.lazy ? a.tile_open : nullptr, sm.e.hist, sm.e.red, c);
-  }
-  lgnn_tile::grid_sync(sync, 2, kBuildSpins);
-  {
-    const int nblk = (int)((N + 1 + kScanBlk - 1) / kScanBlk), ny = a.tptr ? 2 : 1;
-    for (int v = b; v < nblk * ny; v += G) {
-      __syncthreads();
-      scan_body(a.ws.cnt, a.ws.tcnt, N, a.add_loop, a.ws.stat, a.rowptr, a.tptr, a.ws.fill,
-                a.ws.tfill, a.ws.dis, a.lazy ? a.tile_open : nullptr, sm.scan, v % nblk,
-                v / nblk, nblk);
-    }
-  }
-  lgnn_tile::grid_sync(sync, 3, kBuildSpins);
-  for (int64_t c = b; c < nch; c += G) {
-    __syncthreads();
-    fill_body(a.ei, E, N, a.loops, a.rowptr, a.ws.fill, a.col, a.ws.eid, a.tptr, a.ws.tfill,
-              a.tidx, a.ws.teid, a.lazy ? a.tile_open + ntiles : nullptr, sm.e.hist, sm.e.red, c);
-  }
-  lgnn_tile::grid_sync(sync, 4, kBuildSpins);
-  {
-    __syncthreads();  // the union's finish arrays overlay the fill bins
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t nfin = (N + kFinT - 1) / kFinT;
-    const int ny = a.tptr ? 2 : 1;
-    for (int64_t v = (int64_t)b * (kThreads / 64) + wave; v < nfin * ny;
-         v += (int64_t)G * (kThreads / 64))
-      finish_body(N, E, a.add_loop, a.norm, a.rowptr, a.col, a.ws.eid, a.w, a.tptr, a.tidx,
-                  a.ws.teid, a.tw, a.ws.dis, a.ws.err, a.err_count, a.tile_open, a.lazy,
-                  a.tmap ? a.ws.inv : nullptr, sm.fin.key[wave], sm.fin.val[wave], sm.fin.ptr[wave], v % nfin,
-                  (int)(v / nfin), lane, WaveSync{});
-  }
-  if (a.tmap) {
-    lgnn_tile::grid_sync(sync, 5, kBuildSpins);
-    const int nnz = a.tptr[N];
-    for (int q = b * kThreads + threadIdx.x; q < nnz; q += G * kThreads)
-      a.tmap[q] = a.ws.inv[a.ws.teid[q]];
-  }
-  lgnn_tile::grid_exit(sync);
-}
-
 __global__ void k_batch_ptr(const int64_t* __restrict__ batch, int64_t M, int64_t B,
                             int32_t* ptr) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= M;
@@ -1173,43 +1098,20 @@ extern "C" size_t lgnn_graph_workspace_bytes(int64_t num_nodes, int64_t num_edge
 // general-path launches of a target-sorted-path build (k_count / k_fill / k_finish), which is
 // correct only for input the sorted path accepts — it measures what those no-op launches cost.
 static bool abl_skip_general() {
+#ifdef LGNN_ABLATION_BUILD  // timing-only libraries (never the product): the knob is compiled out
   const char* e = getenv("LGNN_ABL_SKIP_GENERAL");
   return e && e[0] == '1';
+#else
+  return false;
+#endif
 }
 
 static int graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loops, int norm,
                        int32_t* rowptr, int32_t* col, float* w, int32_t* tptr, int32_t* tidx,
                        float* tw, int32_t* tmap, int32_t* tile_open, const int64_t* batch,
                        int64_t num_graphs, int32_t* gptr, int32_t* err_count, void* workspace,
-                       size_t workspace_bytes, void* stream, int lazy, int32_t* sync = nullptr);
-
-// workgroups of k_build resident at once on this device (occupancy x CUs), cached per device
-static int build_capacity() {
-  static int cache[16];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 0;
-  if (cache[dev] > 0) return cache[dev];
-  int cus = 0, per = 0;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_build, kThreads, 0) != hipSuccess)
-    return 0;
-  cache[dev] = cus * per;
-  return cache[dev];
-}
-
-extern "C" int lgnn_graph_build_sync(const int64_t* edge_index, int64_t E, int64_t N, int loops,
-                                     int norm, int32_t* rowptr, int32_t* col, float* w,
-                                     int32_t* tptr, int32_t* tidx, float* tw, int32_t* tmap,
-                                     int32_t* tile_open, const int64_t* batch,
-                                     int64_t num_graphs, int32_t* gptr, int32_t* err_count,
-                                     void* workspace, size_t workspace_bytes, int lazy,
-                                     int32_t* sync, void* stream) {
-  if (!sync) return LGNN_EINVAL;
-  if (lazy && (!tile_open || !tptr || tmap)) return LGNN_EINVAL;
-  return graph_build(edge_index, E, N, loops, norm, rowptr, col, w, tptr, tidx, tw, tmap,
-                     tile_open, batch, num_graphs, gptr, err_count, workspace, workspace_bytes,
-                     stream, lazy ? 1 : 0, sync);
-}
+                       size_t workspace_bytes, void* stream, int lazy,
+                       const lgnn_s3::PlaneArgs* planes = nullptr);
 
 extern "C" int lgnn_graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loops,
                                 int norm, int32_t* rowptr, int32_t* col, float* w, int32_t* tptr,
@@ -1220,6 +1122,23 @@ extern "C" int lgnn_graph_build(const int64_t* edge_index, int64_t E, int64_t N,
   return graph_build(edge_index, E, N, loops, norm, rowptr, col, w, tptr, tidx, tw, tmap,
                      tile_open, batch, num_graphs, gptr, err_count, workspace, workspace_bytes,
                      stream, 0);
+}
+
+extern "C" int lgnn_graph_build_planes(const int64_t* edge_index, int64_t E, int64_t N,
+                                       int loops, int norm, int32_t* rowptr, int32_t* col,
+                                       float* w, int32_t* tptr, int32_t* tidx, float* tw,
+                                       int32_t* tmap, int32_t* tile_open, const int64_t* batch,
+                                       int64_t num_graphs, int32_t* gptr, int32_t* err_count,
+                                       void* workspace, size_t workspace_bytes, int lazy,
+                                       const lgnn_plane_job* job, void* stream) {
+  if (lazy && (!tile_open || !tptr || tmap)) return LGNN_EINVAL;
+  if (!job || job->nl > LGNN_PLANE_JOB_MAX) return LGNN_EINVAL;
+  lgnn_s3::PlaneArgs pj;
+  const int r = lgnn_s3::plane_args(job->nl, job->W, job->widths, job->planes, job->planes_t, pj);
+  if (r != LGNN_OK) return r;
+  return graph_build(edge_index, E, N, loops, norm, rowptr, col, w, tptr, tidx, tw, tmap,
+                     tile_open, batch, num_graphs, gptr, err_count, workspace, workspace_bytes,
+                     stream, lazy ? 1 : 0, &pj);
 }
 
 extern "C" int lgnn_graph_build_lazy(const int64_t* edge_index, int64_t E, int64_t N, int loops,
@@ -1264,7 +1183,8 @@ static int graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loop
                        int32_t* rowptr, int32_t* col, float* w, int32_t* tptr, int32_t* tidx,
                        float* tw, int32_t* tmap, int32_t* tile_open, const int64_t* batch,
                        int64_t num_graphs, int32_t* gptr, int32_t* err_count, void* workspace,
-                       size_t workspace_bytes, void* stream, int lazy, int32_t* sync) {
+                       size_t workspace_bytes, void* stream, int lazy,
+                       const lgnn_s3::PlaneArgs* planes) {
   if (N < 0 || E < 0 || loops < 0 || loops > 2 || norm < 0 || norm > 1) return LGNN_EINVAL;
   if (!rowptr || !col || (E > 0 && !edge_index)) return LGNN_EINVAL;
   if (N + E >= (int64_t)1 << 30) return LGNN_EINVAL;
@@ -1275,39 +1195,10 @@ static int graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loop
   hipStream_t s = as_stream(stream);
   const int add_loop = loops == LGNN_LOOPS_KEEP ? 0 : 1;
   GraphWs ws = carve(workspace, N, E);
-  const int cap = (sync && N > 0) ? build_capacity() : 0;
-  if (cap > 0) {  // one persistent launch (k_build)
-    BuildArgs a{};
-    a.ei = edge_index;
-    a.E = E;
-    a.N = N;
-    a.loops = loops;
-    a.norm = norm;
-    a.add_loop = add_loop;
-    a.lazy = lazy;
-    a.rowptr = rowptr;
-    a.col = col;
-    a.tptr = tptr;
-    a.tidx = tidx;
-    a.tmap = tmap;
-    a.tile_open = tile_open;
-    a.gptr = gptr;
-    a.err_count = err_count;
-    a.w = w;
-    a.tw = tw;
-    a.batch = batch;
-    a.num_graphs = num_graphs;
-    a.ws = ws;
-    const int64_t nch = (E + kChunk - 1) / kChunk;
-    const int64_t nfin = (N + kFinT - 1) / kFinT * (tptr ? 2 : 1);
-    int64_t g = nch;
-    if ((nfin + 3) / 4 > g) g = (nfin + 3) / 4;
-    if (g < 1) g = 1;
-    if (g > cap) g = cap;
-    hipLaunchKernelGGL(k_build, dim3((unsigned)g), dim3(kThreads), 0, s, a, sync);
-    LGNN_LAUNCH_CHECK();
-    return LGNN_OK;
-  }
+  // the weight-plane side job rides the first launch as extra workgroups
+  lgnn_s3::PlaneArgs pj{};
+  if (planes) pj = *planes;
+  const int pblocks = planes ? (pj.nl * lgnn_s3::PLANE_ITEMS + kThreads - 1) / kThreads : 0;
   // target-sorted fast path: only for builds without the source CSR (or lazily with it) and
   // without tmap
   SortedArgs sa{};
@@ -1328,12 +1219,13 @@ static int graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loop
       sa.dis = ws.dis;
       sa.verdict = ws.verdict;
       sa.nverdict = sorted_grid(N, E);
-      hipLaunchKernelGGL(k_prep_sorted, dim3(sa.nverdict), dim3(kThreads), 0, s, ws.err, nzero,
-                         tile_open, ntiles, batch, N, num_graphs, gptr, sa);
+      hipLaunchKernelGGL(k_prep_sorted, dim3(sa.nverdict + pblocks), dim3(kThreads), 0, s,
+                         ws.err, nzero, tile_open, ntiles, batch, N, num_graphs, gptr, sa, pj,
+                         sa.nverdict);
     } else {
-      hipLaunchKernelGGL(k_prep, dim3(grid_for(nzero > N + 1 ? nzero : N + 1, 1024)),
-                         dim3(kThreads), 0, s, ws.err, nzero, tile_open, ntiles, batch, N,
-                         num_graphs, gptr);
+      const int g = grid_for(nzero > N + 1 ? nzero : N + 1, 1024);
+      hipLaunchKernelGGL(k_prep, dim3(g + pblocks), dim3(kThreads), 0, s, ws.err, nzero,
+                         tile_open, ntiles, batch, N, num_graphs, gptr, pj, g);
     }
     LGNN_LAUNCH_CHECK();
   }

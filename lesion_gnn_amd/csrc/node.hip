@@ -712,6 +712,9 @@ extern "C" int lgnn_node_linear_bwd_tiles(int grad_mode, const float* dY, const 
                                           int num_partials, const int32_t* tile_open,
                                           int want_open, int accumulate, void* stream) {
   if (M < 0 || K <= 0 || N <= 0 || (N & 3) || !W || !dW_partial) return LGNN_EINVAL;
+  if (accumulate < 0 || accumulate > 2 ||
+      (accumulate == 2 && (!tile_open || num_partials > LGNN_SLOT_FLAGS)))
+    return LGNN_EINVAL;
   const bool fast = bwd_fast(M, N, K, rowptr != nullptr);
   if (tile_open && !fast) return LGNN_EINVAL;  // tile selection only on the fast path
   if (!tile_open && num_partials != (fast ? lgnn_tile_partials(M) : grid_partials(M, N, K)))

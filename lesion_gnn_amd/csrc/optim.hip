@@ -11,7 +11,6 @@
 // to finish (ticket counter) increments it and re-arms the ticket (advance = 1; a group of
 // more than LGNN_MAX_ADAM (16) tensors is stepped in several launches, the last one advancing).
 #include "common.h"
-#include "s3_util.h"
 
 namespace {
 
@@ -24,12 +23,6 @@ struct AdamJobs {
   float* v[LGNN_MAX_ADAM];
   int64_t off[LGNN_MAX_ADAM + 1];  // prefix of the element counts
   int boff[LGNN_MAX_ADAM + 1];     // prefix of the workgroups per tensor
-  // split-3 weight planes of the updated tensor (lgnn_adam_step_planes; wp nullptr = none): a
-  // [N][K] weight's three bf16 planes in the fragment order lgnn_weight_planes writes (the next
-  // forward's and backward's operands), so no weight-plane launch runs before the next forward
-  uint16_t* wp[LGNN_MAX_ADAM];
-  uint16_t* wpt[LGNN_MAX_ADAM];
-  int wk[LGNN_MAX_ADAM];
   int n;
 };
 
@@ -66,19 +59,6 @@ __global__ __launch_bounds__(kT) void k_adam(AdamJobs J, float* __restrict__ ste
     Vv[k] = v;
     p -= step_size * m / (sqrtf(v) / bc2s + eps);
     P[k] = p;
-    if (uint16_t* __restrict__ wp = J.wp[j]) {  // k_wplanes' split of the new value, element-wise
-      const int K = J.wk[j];
-      const int r = (int)(k / K), c = (int)(k - (int64_t)r * K);
-      const lgnn_s3::Split2 sp = lgnn_s3::split2(p, 0.f);
-      const int fi = lgnn_s3::frag_index(r, lgnn_s3::perm16(c));
-      const int ft = lgnn_s3::frag_index(c, lgnn_s3::perm16(r));
-      uint16_t* __restrict__ wt = J.wpt[j];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        wp[q * lgnn_s3::PLANE + fi] = (uint16_t)(sp.p[q] & 0xffffu);
-        if (wt) wt[q * lgnn_s3::PLANE + ft] = (uint16_t)(sp.p[q] & 0xffffu);
-      }
-    }
   }
   if (!advance) return;
   __syncthreads();
@@ -102,8 +82,7 @@ static int adam_step(int n, float* const* params, const float* const* grads,
                      float* const* exp_avg, float* const* exp_avg_sq, const int64_t* numels,
                      float* step, unsigned int* ticket, float lr, float beta1, float beta2,
                      float eps, float weight_decay, int decoupled, int maximize, int advance,
-                     uint16_t* const* planes, uint16_t* const* planes_t, const int* rows,
-                     const int* cols, void* stream) {
+                     void* stream) {
   if (n < 0 || n > LGNN_MAX_ADAM || !step || !ticket || (n > 0 && (!params || !grads ||
       !exp_avg || !exp_avg_sq || !numels)))
     return LGNN_EINVAL;
@@ -129,14 +108,6 @@ static int adam_step(int n, float* const* params, const float* const* grads,
     J.m[i] = exp_avg[i];
     J.v[i] = exp_avg_sq[i];
     J.off[i + 1] = J.off[i] + numels[i];
-    if (planes && planes[i]) {  // a [rows][cols] weight (<= 128 x 128) with split-3 planes
-      if (!rows || !cols || rows[i] < 1 || cols[i] < 1 || rows[i] > lgnn_s3::WP ||
-          cols[i] > lgnn_s3::WP || (int64_t)rows[i] * cols[i] != numels[i])
-        return LGNN_EINVAL;
-      J.wp[i] = planes[i];
-      J.wpt[i] = planes_t ? planes_t[i] : nullptr;
-      J.wk[i] = cols[i];
-    }
     const int64_t nb = (numels[i] + per - 1) / per;
     J.boff[i + 1] = J.boff[i] + (int)(nb > 0 ? nb : 1);
   }
@@ -154,19 +125,5 @@ extern "C" int lgnn_adam_step(int n, float* const* params, const float* const* g
                               float beta1, float beta2, float eps, float weight_decay,
                               int decoupled, int maximize, int advance, void* stream) {
   return adam_step(n, params, grads, exp_avg, exp_avg_sq, numels, step, ticket, lr, beta1, beta2,
-                   eps, weight_decay, decoupled, maximize, advance, nullptr, nullptr, nullptr,
-                   nullptr, stream);
-}
-
-extern "C" int lgnn_adam_step_planes(int n, float* const* params, const float* const* grads,
-                                     float* const* exp_avg, float* const* exp_avg_sq,
-                                     const int64_t* numels, float* step, unsigned int* ticket,
-                                     float lr, float beta1, float beta2, float eps,
-                                     float weight_decay, int decoupled, int maximize, int advance,
-                                     uint16_t* const* planes, uint16_t* const* planes_t,
-                                     const int* rows, const int* cols, void* stream) {
-  if (!planes) return LGNN_EINVAL;
-  return adam_step(n, params, grads, exp_avg, exp_avg_sq, numels, step, ticket, lr, beta1, beta2,
-                   eps, weight_decay, decoupled, maximize, advance, planes, planes_t, rows, cols,
-                   stream);
+                   eps, weight_decay, decoupled, maximize, advance, stream);
 }

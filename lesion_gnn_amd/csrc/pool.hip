@@ -61,37 +61,13 @@ __global__ __launch_bounds__(NT) void k_pool_head_fwd(const float* __restrict__ 
   }
 }
 
-// The criterion's forward folded into the readout (CE = true): nn.CrossEntropyLoss(weight), mean
-// reduction (reference models/base.py:93-94) — k_ce_fwd's arithmetic, bit for bit:
-//   per graph (its block, once its logits are out): lse_g = m + log(sum exp(z - m)), the terms
-//     num_g = w[y_g] (lse_g - z_g[y_g]), den_g = w[y_g] (0 and *bad for a target outside [0, C));
-//   the last block to finish (two-level ticket) sums the terms in k_ce_fwd's order (1024 strided
-//     partials, then the 16-wave fixed tree) and writes loss = num / den and wsum = den.
-// Cross-block traffic without release fences (one per block would write back its XCD's L2, the
-// readout split's lesson): the terms are returning agent-scope atomic exchanges whose results
-// feed the ticket operand, and the last block reads them with agent-scope atomic loads.
-struct CeFwd {
-  const int64_t* y;
-  const float* w;
-  float* lse;
-  float* pm;     // [B][C] the logits gradient's factors (lgnn_ce_src)
-  float* wt;     // [B]
-  float* part;   // [B][2] num_g, den_g
-  unsigned int* ticket;  // [10] zero, re-armed: 9 ticket words + the blocks' bad-target OR
-  float* loss;
-  float* wsum;
-  int* bad;      // written by the last block
-  int64_t B;
-};
-
-template <bool CE>
 __global__ __launch_bounds__(NT) void k_pool_head_fwd4(const float* __restrict__ H,
                                                        const int32_t* __restrict__ gptr, int D,
                                                        int pool_mean,
                                                        const float* __restrict__ Wout,
                                                        const float* __restrict__ bout, int C,
                                                        float* __restrict__ pooled,
-                                                       float* __restrict__ logits, CeFwd ce) {
+                                                       float* __restrict__ logits) {
   __shared__ __attribute__((aligned(16))) float red[8][512];
   __shared__ float pl[512];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -143,158 +119,6 @@ __global__ __launch_bounds__(NT) void k_pool_head_fwd4(const float* __restrict__
     pooled[g * D + d] = t;
     pl[d] = t;
   }
-  if (!Wout) return;
-  __syncthreads();
-  __shared__ float zl[16];  // this graph's logits (CE; C <= 16)
-  for (int c = wave; c < C; c += NT / 64) {
-    float acc = 0.f;
-    for (int d = lane; d < D; d += 64) acc = fmaf(pl[d], Wout[(int64_t)c * D + d], acc);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-    const float z = acc + (bout ? bout[c] : 0.f);
-    if (lane == 0) logits[g * C + c] = z;
-    if (CE && lane == 0) zl[c] = z;
-  }
-  if constexpr (CE) {
-    __syncthreads();
-    __shared__ int last;
-    if (threadIdx.x == 0) {
-      float m = -INFINITY;
-      for (int c = 0; c < C; ++c) m = fmaxf(m, zl[c]);
-      float sx = 0.f;
-      for (int c = 0; c < C; ++c) sx += expf(zl[c] - m);
-      const float l = m + logf(sx);
-      ce.lse[g] = l;
-      const int64_t t = ce.y[g];
-      const float wt = ce_wt(ce.y, ce.w, C, g);
-      for (int c = 0; c < C; ++c) ce.pm[g * C + c] = ce_pm(zl[c], l, t, c);
-      ce.wt[g] = wt;
-      float num = 0.f, den = 0.f;
-      unsigned int badv = 0u;
-      if (t < 0 || t >= C) {
-        badv = 1u;
-      } else {
-        num = wt * (l - zl[t]);
-        den = wt;
-      }
-      const unsigned int r0 = __float_as_uint(__hip_atomic_exchange(
-          ce.part + 2 * g, num, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      const unsigned int r1 = __float_as_uint(__hip_atomic_exchange(
-          ce.part + 2 * g + 1, den, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      // the bad-target OR only from the blocks that have one: 1024 same-address atomics
-      // serialise (~30 us)
-      const unsigned int rb = badv ? __hip_atomic_fetch_or(ce.ticket + 9, badv, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT)
-                                   : 0u;
-      last = last_workgroup(ce.ticket, ticket_after(r0 ^ r1 ^ rb));
-    }
-    __syncthreads();
-    if (!last) return;
-    // k_ce_fwd's order: virtual thread v (of 1024) sums rows v, v + 1024, ...; each virtual wave
-    // (64 consecutive v) folds by the xor tree; the 16 wave sums add in order
-    __shared__ float rn[16], rd[16];
-    for (int j = 0; j < 4; ++j) {
-      const int v = 256 * j + threadIdx.x;
-      float n = 0.f, d = 0.f;
-      for (int64_t i = v; i < ce.B; i += 1024) {
-        const float pn = __hip_atomic_load(ce.part + 2 * i, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-        const float pd = __hip_atomic_load(ce.part + 2 * i + 1, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-        const int64_t t = ce.y[i];
-        if (t < 0 || t >= C) continue;  // k_ce_fwd skips such rows
-        n += pn;
-        d += pd;
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
-      if (lane == 0) {
-        rn[4 * j + wave] = n;
-        rd[4 * j + wave] = d;
-      }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      float tn = 0.f, td = 0.f;
-      for (int q = 0; q < 16; ++q) tn += rn[q];
-      for (int q = 0; q < 16; ++q) td += rd[q];
-      ce.loss[0] = tn / td;
-      ce.wsum[0] = td;
-      ce.bad[0] = (int)__hip_atomic_load(ce.ticket + 9, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ce.ticket + 9, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-// Few, large graphs (the GAT configs: 64 graphs of ~660 rows) leave most CUs idle with one
-// workgroup per graph, each walking its rows latency-bound. Here graph g is split over S
-// workgroups (rows [n0 + s chunk, ..), chunk = ceil(|g| / S)); each writes its column sums (the
-// fwd4 half-wave order) to part[g][s], and the last of the S to arrive — a per-graph ticket taken
-// with agent-scope acquire-release after the partial's release — sums the S partials in split
-// order, scales, writes pooled and the logits, and re-arms the ticket (zero on entry and exit).
-__global__ __launch_bounds__(NT) void k_pool_head_split(const float* __restrict__ H,
-                                                        const int32_t* __restrict__ gptr, int D,
-                                                        int pool_mean,
-                                                        const float* __restrict__ Wout,
-                                                        const float* __restrict__ bout, int C,
-                                                        int S, float* __restrict__ part,
-                                                        int32_t* __restrict__ tickets,
-                                                        float* __restrict__ pooled,
-                                                        float* __restrict__ logits) {
-  __shared__ __attribute__((aligned(16))) float red[8][512];
-  __shared__ float pl[512];
-  __shared__ int is_last;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int li = lane & 31, hw = wave * 2 + (lane >> 5);
-  const int64_t g = blockIdx.x / S;
-  const int sp = blockIdx.x % S;
-  const int n0 = gptr[g], n1 = gptr[g + 1];
-  const int cnt = n1 - n0, chunk = (cnt + S - 1) / S;
-  const int r0 = n0 + sp * chunk, r1 = r0 + chunk < n1 ? r0 + chunk : n1;
-  for (int s0 = 0; s0 < D; s0 += 128) {
-    const int f = s0 + 4 * li;
-    const int fc = f < D ? f : D - 4;
-    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-    int i = r0 + hw;
-    for (; i + 8 < r1; i += 16) {
-      const f32x4 v0 = ld4(H + (int64_t)i * D + fc);
-      const f32x4 v1 = ld4(H + (int64_t)(i + 8) * D + fc);
-      a0 += v0;
-      a1 += v1;
-    }
-    if (i < r1) a0 += ld4(H + (int64_t)i * D + fc);
-    if (f < D) st4(&red[hw][f], a0 + a1);
-  }
-  __syncthreads();
-  float* mine = part + ((int64_t)g * S + sp) * D;
-  for (int d = threadIdx.x; d < D; d += NT) {
-    float t = red[0][d];
-#pragma unroll
-    for (int r = 1; r < 8; ++r) t += red[r][d];
-    mine[d] = t;
-  }
-  __threadfence();  // this partial, at agent scope, before the ticket
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int prev =
-        __hip_atomic_fetch_add(tickets + g, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    is_last = prev == S - 1;
-  }
-  __syncthreads();
-  if (!is_last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the other S - 1 partials
-  const float denom = (float)(cnt > 0 ? cnt : 1);
-  const float* pg = part + (int64_t)g * S * D;
-  for (int d = threadIdx.x; d < D; d += NT) {
-    float t = pg[d];
-    for (int q = 1; q < S; ++q) t += pg[(int64_t)q * D + d];
-    if (pool_mean) t = t / denom;
-    pooled[g * D + d] = t;
-    pl[d] = t;
-  }
-  if (threadIdx.x == 0) tickets[g] = 0;  // re-armed for the next launch (stream order)
   if (!Wout) return;
   __syncthreads();
   for (int c = wave; c < C; c += NT / 64) {
@@ -382,53 +206,12 @@ extern "C" int lgnn_pool_head_fwd(const float* H, const int32_t* gptr, int64_t B
   if (Wout && (C <= 0 || !logits)) return LGNN_EINVAL;
   if (B == 0) return LGNN_OK;
   if ((D & 3) == 0)
-    hipLaunchKernelGGL(k_pool_head_fwd4<false>, dim3((unsigned)B), dim3(NT), 0, as_stream(stream),
-                       H, gptr, D, pool_mean, Wout, bout, C, pooled, logits, CeFwd{});
+    hipLaunchKernelGGL(k_pool_head_fwd4, dim3((unsigned)B), dim3(NT), 0, as_stream(stream), H,
+                       gptr, D, pool_mean, Wout, bout, C, pooled, logits);
   else
     hipLaunchKernelGGL(k_pool_head_fwd, dim3((unsigned)((B + 3) / 4)), dim3(NT), 0,
                        as_stream(stream), H, gptr, B, D, pool_mean, Wout, bout, C, pooled,
                        logits);
-  LGNN_LAUNCH_CHECK();
-  return LGNN_OK;
-}
-
-extern "C" size_t lgnn_pool_head_ce_workspace_bytes(int64_t B) {
-  return B < 0 ? 0 : (size_t)B * 2 * sizeof(float);
-}
-
-extern "C" int lgnn_pool_head_ce_fwd(const float* H, const int32_t* gptr, int64_t B, int D,
-                                     int pool_mean, const float* Wout, const float* bout, int C,
-                                     float* pooled, float* logits, const int64_t* target,
-                                     const float* weight, float* lse, float* loss, float* wsum,
-                                     int* bad, float* pm, float* wt, unsigned int* ticket,
-                                     void* workspace, size_t workspace_bytes, void* stream) {
-  if (B < 1 || D <= 0 || D > 512 || (D & 3) != 0 || !gptr || !pooled || !Wout || !logits ||
-      C < 1 || C > 16 || !target || !lse || !loss || !wsum || !bad || !pm || !wt || !ticket ||
-      !workspace)
-    return LGNN_EINVAL;
-  if (workspace_bytes < lgnn_pool_head_ce_workspace_bytes(B)) return LGNN_ENOSPC;
-  hipStream_t s = as_stream(stream);
-  const CeFwd ce{target, weight, lse, pm, wt, static_cast<float*>(workspace), ticket, loss, wsum,
-                 bad, B};
-  hipLaunchKernelGGL(k_pool_head_fwd4<true>, dim3((unsigned)B), dim3(NT), 0, s, H, gptr, D,
-                     pool_mean, Wout, bout, C, pooled, logits, ce);
-  LGNN_LAUNCH_CHECK();
-  return LGNN_OK;
-}
-
-extern "C" int lgnn_pool_head_fwd_split(const float* H, const int32_t* gptr, int64_t B, int D,
-                                        int pool_mean, const float* Wout, const float* bout,
-                                        int C, int splits, float* part, int32_t* tickets,
-                                        float* pooled, float* logits, void* stream) {
-  if (B < 0 || D <= 0 || D > 512 || (D & 3) || !gptr || !pooled || splits < 1 || splits > 64 ||
-      !part || !tickets)
-    return LGNN_EINVAL;
-  if (Wout && (C <= 0 || !logits)) return LGNN_EINVAL;
-  if (B == 0) return LGNN_OK;
-  if (B * splits > (int64_t)1 << 30) return LGNN_EINVAL;
-  hipLaunchKernelGGL(k_pool_head_split, dim3((unsigned)(B * splits)), dim3(NT), 0,
-                     as_stream(stream), H, gptr, D, pool_mean, Wout, bout, C, splits, part,
-                     tickets, pooled, logits);
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
 }

@@ -70,7 +70,9 @@ __global__ __launch_bounds__(QT) void k_radius(const double* __restrict__ pos, i
   const int64_t base = WRITE && active ? off[q] : 0;
   for (int64_t c0 = cbeg; c0 < cend; c0 += CHUNK) {
     const int64_t c1 = c0 + CHUNK < cend ? c0 + CHUNK : cend;
-    __syncthreads();
+    // every query of the block has taken `limit` candidates, or its graph ends before this
+    // chunk: the rest of the range cannot add an edge (block-uniform, so the barriers stay so)
+    if (!__syncthreads_or(active && taken < limit && ge > c0)) break;
     for (int64_t i = c0 * D + threadIdx.x; i < c1 * D; i += QT) cp[i - c0 * D] = pos[i];
     __syncthreads();
     if (!active || taken >= limit) continue;
@@ -139,6 +141,7 @@ int radius_args_ok(const double* pos, int64_t N, int dims, const int64_t* batch,
   if (N < 0 || B < 0 || (dims != 2 && dims != 3) || !(r >= 0.0) || max_num_neighbors < 1)
     return 0;
   if (N > 0 && (!pos || !batch || !ptr)) return 0;
+  if (N > 0 && B == 0) return 0;  // nodes but no graphs: batch cannot index ptr
   if (N > INT32_MAX) return 0;
   return 1;
 }
@@ -158,7 +161,7 @@ extern "C" int lgnn_radius_count(const double* pos, int64_t N, int dims, const i
   if (!workspace || workspace_bytes < lgnn_radius_workspace_bytes(N)) return LGNN_ENOSPC;
   hipStream_t s = as_stream(stream);
   const RadiusWs w = radius_ws(workspace, N);
-  if (N == 0 || B == 0) {
+  if (N == 0) {
     if (hipMemsetAsync(w.off, 0, sizeof(int64_t), s) != hipSuccess) return (int)hipGetLastError();
     return LGNN_OK;
   }
@@ -184,7 +187,7 @@ extern "C" int lgnn_radius_graph(const double* pos, int64_t N, int dims, const i
   if (!radius_args_ok(pos, N, dims, batch, ptr, B, r, max_num_neighbors)) return LGNN_EINVAL;
   if (num_edges < 0 || (num_edges > 0 && !edge_index)) return LGNN_EINVAL;
   if (!workspace || workspace_bytes < lgnn_radius_workspace_bytes(N)) return LGNN_ENOSPC;
-  if (N == 0 || B == 0 || num_edges == 0) return LGNN_OK;
+  if (N == 0 || num_edges == 0) return LGNN_OK;
   hipStream_t s = as_stream(stream);
   const RadiusWs w = radius_ws(const_cast<void*>(workspace), N);
   const double r2 = r * r;

@@ -104,6 +104,67 @@ __device__ __forceinline__ int frag_index(int row, int phys) {
          (phys & 7);
 }
 
+// Weight planes: W_l [N][K] fp32 -> bf16 planes of W_l[n][perm16(k)], zero-padded to 128 x 128,
+// stored in MFMA fragment order so that one wave's load of a k-step fragment is 1 KiB contiguous:
+//   Wp[l][plane][n / 32][s][h][n % 32][8]  holds  phys positions 16 s + 8 h .. + 7 of row n
+// (lane h * 32 + n % 32 of wave n / 32 loads k-step s with one 16-B load). With WpT also the
+// transposed planes (rows k, positions perm16(n)) in the same order: the backward's dH = G W_l
+// operand. Item i = one (layer, n, 4 consecutive k); nl * PLANE_ITEMS items in all. Run by
+// k_wplanes (stack3.hip) or as side work of the graph build's first launch (graph.hip).
+struct PlaneArgs {
+  const float* W[LGNN_MAX_STACK];
+  int N[LGNN_MAX_STACK];
+  int K[LGNN_MAX_STACK];
+  int nl;
+  uint16_t* Wp;
+  uint16_t* WpT;  // nullable
+};
+constexpr int PLANE_ITEMS = WP * WP / 4;  // items per layer
+static_assert(LGNN_PLANE_JOB_MAX == LGNN_MAX_STACK, "plane job layers");
+
+__device__ __forceinline__ void wplanes_item(const PlaneArgs& a, int i) {
+  const int l = i / PLANE_ITEMS;
+  if (l >= a.nl) return;
+  const int n = (i / (WP / 4)) % WP, k = 4 * (i % (WP / 4));
+  const int N = a.N[l], K = a.K[l];
+  const f32x4 v = (n < N && k < K) ? ld4(a.W[l] + (int64_t)n * K + k) : zero4();
+  u32x2 o[3];
+  split4(v, o);
+  uint16_t* base = a.Wp + (size_t)l * 3 * PLANE;
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+    *reinterpret_cast<u32x2*>(base + p * PLANE + frag_index(n, perm16(k))) = o[p];
+  if (a.WpT) {
+    uint16_t* bt = a.WpT + (size_t)l * 3 * PLANE;
+    const int pn = perm16(n);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      bt[p * PLANE + frag_index(k + 0, pn)] = (uint16_t)(o[p][0] & 0xffffu);
+      bt[p * PLANE + frag_index(k + 1, pn)] = (uint16_t)(o[p][0] >> 16);
+      bt[p * PLANE + frag_index(k + 2, pn)] = (uint16_t)(o[p][1] & 0xffffu);
+      bt[p * PLANE + frag_index(k + 3, pn)] = (uint16_t)(o[p][1] >> 16);
+    }
+  }
+}
+
+// host: the plane job of lgnn_weight_planes' arguments (LGNN_EINVAL on a bad shape)
+inline int plane_args(int nl, const float* const* W, const int* widths, uint16_t* planes,
+                      uint16_t* planes_t, PlaneArgs& a) {
+  if (nl < 1 || nl > LGNN_MAX_STACK || !W || !widths || !planes) return LGNN_EINVAL;
+  a = PlaneArgs{};
+  for (int l = 0; l < nl; ++l) {
+    const int K = widths[l], N = widths[l + 1];
+    if (!W[l] || K < 4 || N < 4 || K > WP || N > WP || K % 4 || N % 4) return LGNN_EINVAL;
+    a.W[l] = W[l];
+    a.N[l] = N;
+    a.K[l] = K;
+  }
+  a.nl = nl;
+  a.Wp = planes;
+  a.WpT = planes_t;
+  return LGNN_OK;
+}
+
 // threadIdx.x through an empty asm: addresses derived from it cannot be hoisted out of the tile
 // loop or merged across phases (held over the whole loop they cost ~60 registers); each phase
 // recomputes its own in a few VALU ops.

@@ -57,45 +57,9 @@ namespace lgnn_s3 {
 using namespace lgnn_tile;
 constexpr int S3ABL = LGNN_S3_ABLATE;
 
-// ------------------------------------------------------------------------------------------
-// Weight planes: W_l [N][K] fp32 -> bf16 planes of W_l[n][perm16(k)], zero-padded to 128 x 128,
-// stored in MFMA fragment order so that one wave's load of a k-step fragment is 1 KiB contiguous:
-//   Wp[l][plane][n / 32][s][h][n % 32][8]  holds  phys positions 16 s + 8 h .. + 7 of row n
-// (lane h * 32 + n % 32 of wave n / 32 loads k-step s with one 16-B load). With WpT also the
-// transposed planes (rows k, positions perm16(n)) in the same order: the backward's dH = G W_l
-// operand. One thread per (layer, n, 4 consecutive k).
-// ------------------------------------------------------------------------------------------
-struct PlaneArgs {
-  const float* W[LGNN_MAX_STACK];
-  int N[LGNN_MAX_STACK];
-  int K[LGNN_MAX_STACK];
-};
-
-__global__ __launch_bounds__(256) void k_wplanes(PlaneArgs a, int nl, uint16_t* __restrict__ Wp,
-                                                 uint16_t* __restrict__ WpT) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  const int l = i / (WP * WP / 4);
-  if (l >= nl) return;
-  const int n = (i / (WP / 4)) % WP, k = 4 * (i % (WP / 4));
-  const int N = a.N[l], K = a.K[l];
-  const f32x4 v = (n < N && k < K) ? ld4(a.W[l] + (int64_t)n * K + k) : zero4();
-  u32x2 o[3];
-  split4(v, o);
-  uint16_t* base = Wp + (size_t)l * 3 * PLANE;
-#pragma unroll
-  for (int p = 0; p < 3; ++p)
-    *reinterpret_cast<u32x2*>(base + p * PLANE + frag_index(n, perm16(k))) = o[p];
-  if (WpT) {
-    uint16_t* bt = WpT + (size_t)l * 3 * PLANE;
-    const int pn = perm16(n);
-#pragma unroll
-    for (int p = 0; p < 3; ++p) {
-      bt[p * PLANE + frag_index(k + 0, pn)] = (uint16_t)(o[p][0] & 0xffffu);
-      bt[p * PLANE + frag_index(k + 1, pn)] = (uint16_t)(o[p][0] >> 16);
-      bt[p * PLANE + frag_index(k + 2, pn)] = (uint16_t)(o[p][1] & 0xffffu);
-      bt[p * PLANE + frag_index(k + 3, pn)] = (uint16_t)(o[p][1] >> 16);
-    }
-  }
+// Weight planes (s3_util.h wplanes_item): one thread per (layer, n, 4 consecutive k).
+__global__ __launch_bounds__(256) void k_wplanes(PlaneArgs a) {
+  wplanes_item(a, blockIdx.x * 256 + threadIdx.x);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -477,19 +441,12 @@ extern "C" size_t lgnn_weight_planes_bytes(int nl) {
 
 extern "C" int lgnn_weight_planes(int nl, const float* const* W, const int* widths,
                                   uint16_t* planes, uint16_t* planes_t, void* stream) {
-  if (nl < 1 || nl > LGNN_MAX_STACK || !W || !widths || !planes) return LGNN_EINVAL;
-  lgnn_s3::PlaneArgs a = {};
-  for (int l = 0; l < nl; ++l) {
-    const int K = widths[l], N = widths[l + 1];
-    if (!W[l] || K < 4 || N < 4 || K > lgnn_s3::WP || N > lgnn_s3::WP || K % 4 || N % 4)
-      return LGNN_EINVAL;
-    a.W[l] = W[l];
-    a.N[l] = N;
-    a.K[l] = K;
-  }
-  const int threads = nl * lgnn_s3::WP * lgnn_s3::WP / 4;
+  lgnn_s3::PlaneArgs a;
+  const int r = lgnn_s3::plane_args(nl, W, widths, planes, planes_t, a);
+  if (r != LGNN_OK) return r;
+  const int threads = nl * lgnn_s3::PLANE_ITEMS;
   hipLaunchKernelGGL(lgnn_s3::k_wplanes, dim3((threads + 255) / 256), dim3(256), 0,
-                     as_stream(stream), a, nl, planes, planes_t);
+                     as_stream(stream), a);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? LGNN_OK : (int)e;
 }

@@ -692,6 +692,12 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
   IdxRegs R;
   [[maybe_unused]] int stamp = 0;
   int64_t t = seek_tile(blockIdx.x, ntiles, tmask, 0);
+  // a workgroup with no closed tile writes no partial slot when separate open-tile launches
+  // follow (no o.sync): it sets its skip word instead, and those launches write the slot (C5:
+  // nearly every tile open, 49.5 MB of zero slabs no longer written)
+  const bool write_slots = t < ntiles || o.sync != nullptr || blockIdx.x >= LGNN_SLOT_FLAGS;
+  if (!o.sync && blockIdx.x < LGNN_SLOT_FLAGS && threadIdx.x == 0)
+    const_cast<int32_t*>(tmask)[ntiles + LGNN_SLOT_FLAG0 + blockIdx.x] = write_slots ? 0 : 1;
   // graph of row tq of the tile and its size (tq < TM), loaded a tile ahead
   int64_t pre_g = 0;
   int pre_cnt = 0;
@@ -796,14 +802,19 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
     {
       const int tq = fresh_tid();
       const int h = (tq >> 5) & 1, n = 32 * (tq >> 6) + (tq & 31);
-      f32x16 hv[2];  // H_L from the LDS copy (rows past M and features past N_L read 0)
+      f32x16 hv[2];  // H_L from the LDS copy
+      {
+        // unconditional reads, no masks: rows past M hold zeros (hl_issue's out-of-range DMA
+        // lanes write 0), and lanes past N_L read column 0 (finite), which every use below
+        // multiplies by an exact 0 (W_out / dP columns past N_L read 0); conditional reads
+        // compiled to exec-masked blocks with a v_mul_lo each (the phase took 6.8 k ticks)
+        const int nl = __builtin_amdgcn_readfirstlane(NLast);
+        const float* hb = sm.hl + 4 * h * nl + (n < nl ? n : 0);
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
+        for (int q = 0; q < 2; ++q)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
-          hv[q][r] = (n < NLast && r0 + m < M) ? sm.hl[m * NLast + n] : 0.f;
-        }
+          for (int r = 0; r < 16; ++r) hv[q][r] = hb[(32 * q + (r & 3) + 8 * (r >> 2)) * nl];
+      }
       if (has_head(a)) {
         // dP[g(m)][n] / |g(m)| = sum_c dl[m][c] Wout[c][n] as ONE split-3 product per node half
         // (K = the <= 8 classes, zero-padded to 16): A = the staged dl rows (node on the lane:
@@ -1173,7 +1184,7 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
   }
   // partial slot blockIdx.x of every layer: dW rows n = 32 wave + (r & 3) + 8 (r >> 2) + 4h,
   // columns k = 32 kb + li; db from the h = 0 lanes
-  {
+  if (write_slots) {
     const int tq = threadIdx.x;
     const int h = (tq >> 5) & 1, li = tq & 31, wv = tq >> 6;
 #pragma unroll
@@ -1220,553 +1231,7 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
   }
 }
 
-// ==============================================================================================
-// Fused split-3 backward, two waves per SIMD (k_s3_fbwd8; AG only: the forward hands over Â).
-//
-// k_s3_fbwd keeps every layer's dW (three 128 x 128 blocks) in the AGPRs of 4 waves: 192
-// accumulator registers per lane, one wave per SIMD, and nothing hides a phase's latency. Here 8
-// waves share the work without redundant products: wave (nb, hq) = (wv & 3, wv >> 2) owns
-// features [32 nb, +32) and node half hq of a tile, and the dW blocks (nb, kb) with kb = 2 hq,
-// 2 hq + 1 (96 accumulator registers: two waves fit one SIMD). Per conv layer:
-//   G half  = Â^T dZ over its node half (24 products); written (a) to the node-major G image by
-//             the DPP quad transpose and (b) fp32 to the exchange buffer, from which the partner
-//             wave (wv ^ 4) takes it: each wave then holds G[all m][nb] for its dW blocks;
-//   dW_l   += G^T H_{l-1} for its two k blocks (48 products, H image as in k_s3_fbwd);
-//   dH half = G W_l for its node half and feature block nb (48 products, G image rows);
-//   dZ_{l-1} half = dH * ELU'(H_{l-1}) (the H rows it loaded for the image), exchanged through the
-//             same buffer, so the next layer's G sees all 64 target nodes.
-// Products per wave per tile: 2 x 120 + 48 (in_proj), the same total as k_s3_fbwd without G^T.
-// A wave contracts its own node half first: node steps run in the order (2 hq, 2 hq + 1,
-// 2 (1 - hq), 2 (1 - hq) + 1), so its sums are ordered per wave, deterministic run to run.
-// LDS (158 KiB): H image 48, G image 48 (also the next tile's H_L rows between its last dH and its
-// first G), Â planes 27, exchange buffer 32. Open tiles: waves 4..7 leave after the slab write and
-// waves 0..3 run k_s3_fbwd's open-tile phase (a barrier no longer counts a finished wave).
-// ==============================================================================================
-
-constexpr int NT8 = 512;
-
-struct FBwd8Smem {
-  unsigned char Img[3][TM * AROW];  // 48 KiB: H_{l-1} (or X) feature-major [k][perm16 m]
-  unsigned char Gt[3][TM * AROW];   // 48 KiB: G node-major [m][perm16 n]; H_L rows in between
-  unsigned char Adj[3][ADJ_PLANE];  // 27 KiB: Â^T planes; first 16 KiB fp32 while summed
-  f32x4 xb[8][4][64];               // 32 KiB: per-wave exchange of a 64 x 32 node-half block
-  float pscale[TM];
-  int pg[TM];
-  int flag;
-  __attribute__((aligned(16))) float dl[TM][kMaxHeadC];
-};
-static_assert(sizeof(FBwd8Smem) <= 160 * 1024, "fbwd8 LDS exceeds the CU's 160 KiB");
-
-// one node half (q) of a P-layout tile: rows m = 32 q + (r & 3) + 8 (r >> 2) + 4 h
-__device__ __forceinline__ void load_pt_half(f32x16& v, const float* base, int64_t M, int64_t r0,
-                                             int ld, int colv, int ncols, int h, int q) {
-  const int64_t rem = M - r0;
-  const Buf b = mkbuf(base + r0 * ld, rem > 0 ? rem * ld * 4 : 0);
-  const int vb = colv < ncols ? ((32 * q + 4 * h) * ld + colv) * 4 : 0x7fff0000;
-  const int rs = __builtin_amdgcn_readfirstlane(ld * 4);
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int mc = (r & 3) + 8 * (r >> 2);
-    v[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(b, vb + mc * rs, 0, 0));
-  }
-}
-
-__device__ __forceinline__ void xb_put(FBwd8Smem& sm, int wv, int lane, const f32x16& v) {
-#pragma unroll
-  for (int r4 = 0; r4 < 4; ++r4)
-    sm.xb[wv][r4][lane] = f32x4{v[4 * r4], v[4 * r4 + 1], v[4 * r4 + 2], v[4 * r4 + 3]};
-}
-__device__ __forceinline__ void xb_get(const FBwd8Smem& sm, int wv, int lane, f32x16& v) {
-#pragma unroll
-  for (int r4 = 0; r4 < 4; ++r4) {
-    const f32x4 x = sm.xb[wv][r4][lane];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v[4 * r4 + i] = x[i];
-  }
-}
-
-// one P-layout accumulator (a node half) -> the operand planes of its two node steps
-__device__ __forceinline__ void split_half(const f32x16& v, u32x4 (&o)[4][3]) {
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const int rb = 8 * s;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const Split2 s2 = split2(v[rb + 2 * i], v[rb + 2 * i + 1]);
-#pragma unroll
-      for (int p = 0; p < 3; ++p) o[s][p][i] = s2.p[p];
-    }
-  }
-}
-
-// The partner's G half (node half q) as dW's A operand planes o[2], o[3], read back from the
-// node-major G image (the same bf16 planes the partner split): lane (li, h) of node step
-// s = 2 q + j takes G[m][n] for n = 32 nb + li and m = 16 s + 8 (e >> 2) + 4 h + (e & 3),
-// elements e = 0..7 packed in pairs (the k order split_p gives an accumulator's rows)
-__device__ __forceinline__ void gt_frag(const FBwd8Smem& sm, int q, int nb, int li, int h,
-                                        u32x4 (&o)[4][3]) {
-  const int n = 32 * nb + li;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int s = 2 * q + j;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = 2 * i;
-      const int m0 = 16 * s + 8 * (e >> 2) + 4 * h + (e & 3);
-      const int off0 = ap_off(m0, n & ~3) + 2 * (n & 3);
-      const int off1 = ap_off(m0 + 1, n & ~3) + 2 * (n & 3);
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        const uint32_t lo = *reinterpret_cast<const uint16_t*>(sm.Gt[p] + off0);
-        const uint32_t hi = *reinterpret_cast<const uint16_t*>(sm.Gt[p] + off1);
-        o[2 + j][p][i] = lo | (hi << 16);
-      }
-    }
-  }
-}
-
-// global node step of local step s (0, 1: own half hq; 2, 3: the partner's)
-__device__ __forceinline__ int node_step(int s, int hq) { return s < 2 ? 2 * hq + s : 2 * (1 - hq) + s - 2; }
-
-template <int NL>
-__global__ __launch_bounds__(NT8, 1) void k_s3_fbwd8(int64_t M, FBwdArgs a,
-                                                     const int32_t* __restrict__ tmask,
-                                                     OpenBwdArgs o) {
-  constexpr int L = NL - 1;
-  __shared__ __attribute__((aligned(16))) FBwd8Smem sm;
-  const int64_t ntiles = (M + TM - 1) / TM;
-  float* const scr = reinterpret_cast<float*>(sm.Adj[0]);  // fp32 Â [target][source]
-  float* const hl = reinterpret_cast<float*>(sm.Gt[0]);    // H_L rows [row][N_L]
-  const int NLast = a.width[L + 1];
-  const Buf bP = mkbuf(a.dP, a.num_graphs * NLast * 4);
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nb = wv & 3, hq = wv >> 2;
-
-  f32x16 dw[NL][2];
-#pragma unroll
-  for (int l = 0; l < NL; ++l) dw[l][0] = dw[l][1] = f32x16{};
-  float dbacc[NL];
-#pragma unroll
-  for (int l = 0; l < NL; ++l) dbacc[l] = 0.f;
-
-  [[maybe_unused]] int stamp = 0;
-  int64_t t = seek_tile(blockIdx.x, ntiles, tmask, 0);
-  int64_t pre_g = 0;
-  int pre_cnt = 0;
-  float pre_dl[kMaxHeadC];
-  float pre_wt = 0.f;
-  const float ce_gl = a.ce.pm ? a.ce.gloss[0] : 0.f, ce_ws = a.ce.pm ? a.ce.wsum[0] : 1.f;
-#pragma unroll
-  for (int c = 0; c < kMaxHeadC; ++c) pre_dl[c] = 0.f;
-  auto hl_issue8 = [&](int64_t tt) {  // tile tt's H_L rows -> the G image region (1 KiB loads)
-    const int lane = threadIdx.x & 63;
-    const int64_t rr = tt * TM;
-    const int64_t rows = M - rr < TM ? M - rr : TM;
-    const Buf rs = mkbuf(a.H[L] + rr * NLast, rows * NLast * 4);
-    const int nch = (TM * NLast * 4 + 1023) >> 10;
-    for (int c = wv; c < nch; c += NT8 / 64)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rs, (__attribute__((address_space(3))) void*)(&sm.Gt[0][0] + c * 1024), 16,
-          c * 1024 + lane * 16, 0, 0, 0);
-  };
-  auto adj_issue8 = [&](int64_t tt) {
-    const int lane = threadIdx.x & 63;
-    const Buf rs = mkbuf(a.adjt + tt * ADJT_TILE_BYTES, ADJT_TILE_BYTES);
-    for (int c = wv; c < ADJT_TILE_BYTES / 1024; c += NT8 / 64)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rs, (__attribute__((address_space(3))) void*)(&sm.Adj[0][0] + c * 1024), 16,
-          c * 1024 + lane * 16, 0, 0, 0);
-  };
-  if (t < ntiles) {
-    hl_issue8(t);
-    adj_issue8(t);
-    const int tq = fresh_tid();
-    const int64_t row = t * TM + tq;
-    if (tq < TM && row < M) {
-      pre_g = a.batch[row];
-      pre_cnt = a.gptr[pre_g + 1] - a.gptr[pre_g];
-      if (has_head(a)) {
-#pragma unroll
-        for (int c = 0; c < kMaxHeadC; ++c) pre_dl[c] = c < a.C ? head_raw(a, pre_g, c) : 0.f;
-        if (a.ce.pm) pre_wt = a.ce.wt[pre_g];
-      }
-    }
-  }
-  for (; t < ntiles;) {
-    STAMP(stamp++);
-    const int64_t r0 = t * TM;
-    const int64_t tn = seek_tile(t + gridDim.x, ntiles, tmask, 0);
-    const bool has_next = tn < ntiles;
-    {
-      const int tq = fresh_tid();
-      if (tq == 0) sm.flag = 0;
-      if (tq < TM) {
-        const int64_t row = r0 + tq;
-        const float ps =
-            row >= M ? 0.f : (a.pool_mean && pre_cnt > 1 ? 1.f / (float)pre_cnt : 1.f);
-        sm.pg[tq] = (int)pre_g;
-        sm.pscale[tq] = ps;
-        if (has_head(a)) {
-          float v[kMaxHeadC];
-#pragma unroll
-          for (int c = 0; c < kMaxHeadC; ++c) v[c] = head_dl(a, pre_dl[c], pre_wt, ce_gl, ce_ws) * ps;
-          st4(&sm.dl[tq][0], f32x4{v[0], v[1], v[2], v[3]});
-          st4(&sm.dl[tq][4], f32x4{v[4], v[5], v[6], v[7]});
-        }
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's H_L rows and Â landed
-    lds_barrier();
-    // dZ_L for features nb, both node halves: dz0 = half hq, dz1 = the other
-    f32x16 dz0, dz1;
-    {
-      const int tq = fresh_tid();
-      const int h = (tq >> 5) & 1, n = 32 * nb + (tq & 31);
-      float wo[kMaxHeadC];
-      if (has_head(a)) {
-#pragma unroll
-        for (int c = 0; c < kMaxHeadC; ++c)
-          wo[c] = (c < a.C && n < NLast) ? a.Wout[c * NLast + n] : 0.f;
-      }
-      auto half = [&](f32x16& d, int q) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
-          const float hv = (n < NLast && r0 + m < M) ? hl[m * NLast + n] : 0.f;
-          float gv;
-          if (has_head(a)) {
-            const f32x4 d0 = ld4(&sm.dl[m][0]), d1 = ld4(&sm.dl[m][4]);
-            gv = d0[0] * wo[0];
-#pragma unroll
-            for (int c = 1; c < 4; ++c) gv = fmaf(d0[c], wo[c], gv);
-#pragma unroll
-            for (int c = 0; c < 4; ++c) gv = fmaf(d1[c], wo[4 + c], gv);
-          } else {
-            const int off = n < NLast ? (sm.pg[m] * NLast + n) * 4 : INT32_MAX - 3;
-            gv = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(bP, off, 0, 0)) *
-                 sm.pscale[m];
-          }
-          d[r] = gv * elu_grad_from_out(hv);
-        }
-      };
-      half(dz0, hq);
-      half(dz1, 1 - hq);
-    }
-    {  // Â^T planes: row am = source, 8 targets per thread
-      const int tq = fresh_tid();
-      const int am = tq & 63, a8 = tq >> 6;
-      float f[8];
-#pragma unroll
-      for (int y = 0; y < 8; ++y) f[y] = scr[(16 * (a8 >> 1) + perm16(8 * (a8 & 1) + y)) * TM + am];
-      uint32_t qv[3][4];
-      uint32_t inexact = 0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const Split2 s2 = split2(f[2 * i], f[2 * i + 1]);
-#pragma unroll
-        for (int p = 0; p < 3; ++p) qv[p][i] = s2.p[p];
-        inexact |= s2.p[1] | s2.p[2];
-      }
-      if (__any(inexact != 0) && (tq & 63) == 0) sm.flag = 1;
-      lds_barrier();  // every scratch read done (the planes overwrite it)
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-        *reinterpret_cast<u32x4*>(sm.Adj[p] + am * ADJ_LD * 2 + 32 * (a8 >> 1) + 16 * (a8 & 1)) =
-            u32x4{qv[p][0], qv[p][1], qv[p][2], qv[p][3]};
-      lds_barrier();
-    }
-    const bool aexact = __builtin_amdgcn_readfirstlane(sm.flag) == 0;
-    STAMP(stamp++);
-
-    f32x16 xp;  // X rows (features nb, node half hq) of the in_proj phase
-#pragma unroll
-    for (int l = L; l >= 1; --l) {
-      const int K = a.width[l];
-      const bool elu_prev = l >= 2;
-      f32x16 hp;  // H_{l-1}: features nb, node half hq (image part + ELU' of this wave's dZ half)
-      {
-        const int tq = fresh_tid();
-        const int h = (tq >> 5) & 1, k = 32 * nb + (tq & 31);
-        load_pt_half(hp, a.H[l - 1], M, r0, K, k, K, h, hq);
-      }
-      if (hq == 0) {  // db_l (the partner wave holds the same dZ)
-        float sacc = 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sacc += dz0[r] + dz1[r];
-        sacc += __shfl_xor(sacc, 32, 64);
-        dbacc[l] += sacc;
-      }
-      u32x4 dzp[4][3];
-      {
-        const f32x16 dzv[2] = {dz0, dz1};
-        split_p(dzv, dzp);
-      }
-      // G (node half hq) = Â^T dZ over the 64 target nodes
-      f32x16 g0 = f32x16{};
-      {
-        const int tq = fresh_tid();
-        const int h = (tq >> 5) & 1, li = tq & 31;
-        const int arow = (32 * hq + li) * ADJ_LD * 2;
-        if (aexact) {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            const u32x4 a0 = lds16(sm.Adj[0] + arow + 16 * (2 * node_step(s, hq) + h));
-            g0 = mfma_s3_aexact(a0, dzp[s], g0);
-          }
-        } else {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            u32x4 at[3];
-#pragma unroll
-            for (int p = 0; p < 3; ++p)
-              at[p] = lds16(sm.Adj[p] + arow + 16 * (2 * node_step(s, hq) + h));
-            g0 = mfma_s3(at, dzp[s], g0);
-          }
-        }
-      }
-      {  // G half -> node-major image (DPP quad transpose) and -> the exchange buffer
-        const int tq = fresh_tid();
-        const int lane = tq & 63, h = (lane >> 5) & 1, li = lane & 31, qi = li & 3;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float v[4] = {g0[4 * j], g0[4 * j + 1], g0[4 * j + 2], g0[4 * j + 3]};
-          quad_transpose(v, qi);
-          u32x2 ov[3];
-          split4(f32x4{v[0], v[1], v[2], v[3]}, ov);
-          const int off = ap_off(32 * hq + 8 * j + 4 * h + qi, 32 * nb + (li & ~3));
-#pragma unroll
-          for (int p = 0; p < 3; ++p) sts8(sm.Gt[p] + off, ov[p]);
-        }
-      }
-      {  // H_{l-1} part -> feature-major image
-        const int tq = fresh_tid();
-        const int h = (tq >> 5) & 1, k = 32 * nb + (tq & 31);
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          u32x2 ov[3];
-          split4(f32x4{hp[4 * gq], hp[4 * gq + 1], hp[4 * gq + 2], hp[4 * gq + 3]}, ov);
-          const int off = hf_off(k, 32 * hq + 8 * gq + 4 * h);
-#pragma unroll
-          for (int p = 0; p < 3; ++p) sts8(sm.Img[p] + off, ov[p]);
-        }
-      }
-      const uint16_t* wbase;
-      {
-        const int tq = fresh_tid();
-        wbase = a.WpT + (size_t)l * 3 * PLANE + nb * 8 * 512 + (tq & 63) * 8;
-      }
-      // W_l^T planes of feature block nb, one pair of k-steps at a time (two pairs in flight)
-      auto load_w2 = [&](u32x4 (&wf)[3][2], int pair) {
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2)
-            wf[p][s2] = *reinterpret_cast<const u32x4*>(wbase + p * PLANE + 512 * (2 * pair + s2));
-      };
-      lds_barrier();  // both images complete
-      if (l == 1 && has_next) adj_issue8(tn);  // the Â^T reads of this tile are done
-      if (l == 1) {
-        const int tq = fresh_tid();
-        const int64_t row = tn * TM + tq;
-        pre_g = (has_next && tq < TM && row < M) ? a.batch[row] : 0;
-        const int h = (tq >> 5) & 1, k = 32 * nb + (tq & 31);
-        load_pt_half(xp, a.X, M, r0, a.width[0], k, a.width[0], h, hq);
-      }
-      STAMP(stamp++);
-      // dW_l += G^T H for k blocks 2 hq, 2 hq + 1: A = G (own half, then the partner's)
-      {
-        const int tq = fresh_tid();
-        const int lane = tq & 63, h = (lane >> 5) & 1, li = lane & 31;
-        (void)lane;
-        u32x4 gp[4][3];
-        split_half(g0, gp);  // steps 0, 1: this wave's half
-        gt_frag(sm, 1 - hq, nb, li, h, gp);  // steps 2, 3: the partner's, from the G image
-#pragma unroll
-        for (int kb2 = 0; kb2 < 2; ++kb2) {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            u32x4 hb[3];
-            const int off = hf_chunk(32 * (2 * hq + kb2) + li, 2 * node_step(s, hq) + h);
-#pragma unroll
-            for (int p = 0; p < 3; ++p) hb[p] = lds16(sm.Img[p] + off);
-            dw[l][kb2] = mfma_s3(gp[s], hb, dw[l][kb2]);
-          }
-        }
-      }
-      STAMP(stamp++);
-      // dH (node half hq, features nb) = G W_l: A = G image rows, B = W_l^T planes
-      f32x16 dh = f32x16{};
-      {
-        const int tq = fresh_tid();
-        const int h = (tq >> 5) & 1, li = tq & 31;
-        auto dh_pair = [&](const u32x4 (&wf)[3][2], int pair) {
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            u32x4 f[3];
-            const int off = ap_chunk(32 * hq + li, 2 * (2 * pair + s2) + h);
-#pragma unroll
-            for (int p = 0; p < 3; ++p) f[p] = lds16(sm.Gt[p] + off);
-            u32x4 bw[3];
-#pragma unroll
-            for (int p = 0; p < 3; ++p) bw[p] = wf[p][s2];
-            dh = mfma_s3(f, bw, dh);
-          }
-        };
-        u32x4 wa[3][2], wb[3][2];
-        load_w2(wa, 0);
-        load_w2(wb, 1);
-        dh_pair(wa, 0);
-        load_w2(wa, 2);
-        dh_pair(wb, 1);
-        load_w2(wb, 3);
-        dh_pair(wa, 2);
-        dh_pair(wb, 3);
-      }
-      // dZ_{l-1} (node half hq) = dH * ELU'(H_{l-1}); rows past M, features past K are zero
-      {
-        const int tq = fresh_tid();
-        const int h = (tq >> 5) & 1, k = 32 * nb + (tq & 31);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = 32 * hq + (r & 3) + 8 * (r >> 2) + 4 * h;
-          const float v = elu_prev ? dh[r] * elu_grad_from_out(hp[r]) : dh[r];
-          dz0[r] = (k < K && r0 + m < M) ? v : 0.f;
-        }
-      }
-      lds_barrier();  // every read of both images and of the G halves done
-      if (l == 1 && has_next) hl_issue8(tn);  // the next tile's H_L rows into the G image
-      {
-        const int lane = threadIdx.x & 63;
-        xb_put(sm, wv, lane, dz0);
-        lds_barrier();
-        xb_get(sm, wv ^ 4, lane, dz1);
-      }
-      STAMP(stamp++);
-    }
-    // in_proj: db_0, dW_0 += dZ_0^T X for k blocks 2 hq, 2 hq + 1
-    {
-      {
-        const int tq = fresh_tid();
-        const int h = (tq >> 5) & 1, k = 32 * nb + (tq & 31);
-        if (hq == 0) {
-          float sacc = 0.f;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) sacc += dz0[r] + dz1[r];
-          sacc += __shfl_xor(sacc, 32, 64);
-          dbacc[0] += sacc;
-        }
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          u32x2 ov[3];
-          split4(f32x4{xp[4 * gq], xp[4 * gq + 1], xp[4 * gq + 2], xp[4 * gq + 3]}, ov);
-          const int off = hf_off(k, 32 * hq + 8 * gq + 4 * h);
-#pragma unroll
-          for (int p = 0; p < 3; ++p) sts8(sm.Img[p] + off, ov[p]);
-        }
-        pre_cnt = (has_next && tq < TM) ? a.gptr[pre_g + 1] - a.gptr[pre_g] : 0;
-        if (has_head(a)) {
-#pragma unroll
-          for (int c = 0; c < kMaxHeadC; ++c)
-            pre_dl[c] = (has_next && tq < TM && c < a.C) ? head_raw(a, pre_g, c) : 0.f;
-          if (a.ce.pm) pre_wt = (has_next && tq < TM) ? a.ce.wt[pre_g] : 0.f;
-        }
-      }
-      lds_barrier();
-      {
-        u32x4 gp[4][3];
-        {
-          const f32x16 dzv[2] = {dz0, dz1};
-          split_p(dzv, gp);
-        }
-        const int tq = fresh_tid();
-        const int h = (tq >> 5) & 1, li = tq & 31;
-#pragma unroll
-        for (int kb2 = 0; kb2 < 2; ++kb2) {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            u32x4 hb[3];
-            const int off = hf_chunk(32 * (2 * hq + kb2) + li, 2 * node_step(s, hq) + h);
-#pragma unroll
-            for (int p = 0; p < 3; ++p) hb[p] = lds16(sm.Img[p] + off);
-            dw[0][kb2] = mfma_s3(gp[s], hb, dw[0][kb2]);
-          }
-        }
-      }
-      lds_barrier();  // X image read; the next tile may overwrite LDS
-      STAMP(stamp++);
-    }
-    t = tn;
-  }
-  // partial slot blockIdx.x: dW rows n = 32 nb + (r & 3) + 8 (r >> 2) + 4h, columns
-  // k = 32 (2 hq + kb2) + li; db from the hq = 0 waves' h = 0 lanes
-  {
-    const int tq = threadIdx.x;
-    const int h = (tq >> 5) & 1, li = tq & 31;
-#pragma unroll
-    for (int l = 0; l < NL; ++l) {
-      const int N = a.width[l + 1], K = a.width[l];
-      float* slab = a.dWp[l] + (int64_t)blockIdx.x * N * K;
-#pragma unroll
-      for (int kb2 = 0; kb2 < 2; ++kb2) {
-        const int k = 32 * (2 * hq + kb2) + li;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int n = 32 * nb + (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (n < N && k < K) slab[(int64_t)n * K + k] = dw[l][kb2][r];
-        }
-      }
-      const int n = 32 * nb + li;
-      if (hq == 0 && h == 0 && n < N) a.dbp[l][(int64_t)blockIdx.x * N + n] = dbacc[l];
-    }
-  }
-  if (o.sync && tmask[ntiles] > 0) {
-    if (wv >= 4) return;  // the open-tile phase runs on k_s3_fbwd's 4-wave bodies
-    static_assert(sizeof(LwSmem) <= sizeof(FBwd8Smem), "open-tile LDS aliases the fused LDS");
-    __syncthreads();
-    LwSmem& lw = *reinterpret_cast<LwSmem*>(&sm);
-    for (int l = L; l >= 0; --l) {
-      if (l < L) grid_sync(o.sync, L - l);
-      const int K = a.width[l], N = a.width[l + 1];
-      const float* Sx = l == 0 ? a.X : o.S[l - 1];
-      if (l == L)
-        bwd_tiles<LGNN_GRAD_POOL, LGNN_ACT_ELU, true>(
-            lw.A, lw.C, lw.ti, a.dP, a.batch, a.gptr, a.pool_mean, nullptr, nullptr, nullptr, 0.f,
-            a.H[l], Sx, M, K, o.W[l], N, o.dS[l & 1], a.dWp[l], a.dbp[l], tmask, 1, 1, a.dlog,
-            a.Wout, a.C, BnFuse{}, a.ce);
-      else if (l >= 1)
-        bwd_tiles<LGNN_GRAD_TRANSPOSE, LGNN_ACT_ELU, true>(
-            lw.A, lw.C, lw.ti, o.dS[(l + 1) & 1], a.batch, a.gptr, a.pool_mean, o.tptr, o.tidx,
-            o.tw, 0.f, a.H[l], Sx, M, K, o.W[l], N, o.dS[l & 1], a.dWp[l], a.dbp[l], tmask, 1,
-            1);
-      else
-        bwd_tiles<LGNN_GRAD_TRANSPOSE, LGNN_ACT_NONE, false>(
-            lw.A, lw.C, lw.ti, o.dS[1], a.batch, a.gptr, a.pool_mean, o.tptr, o.tidx, o.tw, 0.f,
-            nullptr, Sx, M, K, o.W[0], N, nullptr, a.dWp[0], a.dbp[0], tmask, 1, 1);
-    }
-    grid_exit(o.sync);
-  }
-}
-
 }  // namespace lgnn_s3
-
-// Fused backward variant (the Â hand-over case): 4 = k_s3_fbwd (the default), 8 = k_s3_fbwd8
-// (two waves per SIMD: parity-tested, slower at C2 — DESIGN §4.3); LGNN_S3F_WAVES=8 or
-// lgnn_s3f_set_waves selects it
-static int g_s3f_waves = -1;
-static int s3f_waves() {
-  if (g_s3f_waves < 0) {
-    const char* e = getenv("LGNN_S3F_WAVES");
-    g_s3f_waves = (e && atoi(e) == 8) ? 8 : 4;
-  }
-  return g_s3f_waves;
-}
-
-extern "C" int lgnn_s3f_set_waves(int waves) {
-  if (waves != 4 && waves != 8) return LGNN_EINVAL;
-  const int prev = s3f_waves();
-  g_s3f_waves = waves;
-  return prev;
-}
 
 static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* gptr,
                          int pool_mean, int64_t num_graphs, const int32_t* rowptr,
@@ -1899,14 +1364,7 @@ static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* g
     const int cap = lgnn_fused_grid_capacity(1);
     if (cap < (int)grid.x) return cap == LGNN_EINVAL ? cap : cap < 0 ? -cap : LGNN_EBUSY;
   }
-  if (adjt && s3f_waves() == 8) {
-    if (L == 1)
-      hipLaunchKernelGGL((lgnn_s3::k_s3_fbwd8<2>), grid, dim3(lgnn_s3::NT8), 0, s, M, a,
-                         tile_open, o);
-    else
-      hipLaunchKernelGGL((lgnn_s3::k_s3_fbwd8<3>), grid, dim3(lgnn_s3::NT8), 0, s, M, a,
-                         tile_open, o);
-  } else if (L == 1 && adjt)
+  if (L == 1 && adjt)
     hipLaunchKernelGGL((lgnn_s3::k_s3_fbwd<2, true>), grid, blk, 0, s, rowptr, col, w, M, a,
                        tile_open, o);
   else if (L == 1)
@@ -1923,16 +1381,10 @@ static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* g
 }
 
 // workgroups per CU of the fused backward (the open-tile phase's grid barrier needs them all
-// resident): the smaller of the two variants', so the answer holds for either
+// resident)
 hipError_t lgnn_s3_fbwd_occupancy(int* per_cu) {
-  int a = 0, b = 0;
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, lgnn_s3::k_s3_fbwd<3, true>,
-                                                              lgnn_tile::NT, 0);
-  if (e != hipSuccess) return e;
-  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, lgnn_s3::k_s3_fbwd8<3>, lgnn_s3::NT8, 0);
-  if (e != hipSuccess) return e;
-  *per_cu = a < b ? a : b;
-  return hipSuccess;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, lgnn_s3::k_s3_fbwd<3, true>,
+                                                      lgnn_tile::NT, 0);
 }
 
 #ifdef LGNN_STAMPS

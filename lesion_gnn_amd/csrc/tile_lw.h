@@ -507,8 +507,13 @@ __device__ __forceinline__ void bwd_tiles(
   }
   if constexpr (BNM == BN_GSTATS) bn_part_write(reinterpret_cast<double*>(A), s0, s1, bn.part, K);
   // accumulate: add into slot blockIdx.x (written by the fused stack backward) if this
-  // workgroup processed any tile; otherwise leave the slot untouched
-  if (accumulate && tfirst >= ntiles) return;
+  // workgroup processed any tile; otherwise leave the slot untouched. accumulate = 2: a slot
+  // whose skip word is set was not written by the fused kernel: write it (zeros when this
+  // workgroup processed no tile)
+  const bool skipped = accumulate == 2 && blockIdx.x < LGNN_SLOT_FLAGS &&
+                       tmask[ntiles + LGNN_SLOT_FLAG0 + blockIdx.x] != 0;
+  if (accumulate && tfirst >= ntiles && !skipped) return;
+  const bool add = accumulate && !skipped;
   float* slab = dWp + (int64_t)blockIdx.x * N * K;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -518,13 +523,13 @@ __device__ __forceinline__ void bwd_tiles(
       const int o = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * h;
       if (o < N && k < K) {
         float* p = slab + (int64_t)o * K + k;
-        *p = accumulate ? *p + dw[j][r] : dw[j][r];
+        *p = add ? *p + dw[j][r] : dw[j][r];
       }
     }
   }
   if (dbp && tid < N) {
     float* p = dbp + (int64_t)blockIdx.x * N + tid;
-    *p = accumulate ? *p + dbacc : dbacc;
+    *p = add ? *p + dbacc : dbacc;
   }
 }
 

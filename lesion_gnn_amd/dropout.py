@@ -41,15 +41,22 @@ def _splitmix64(z: int) -> int:
     return z ^ (z >> 31)
 
 
+_CONSTRUCTIONS = [0]  # seeds derived so far in this process
+
+
 def derived_seed() -> int:
     """A seed derived from torch's default CPU generator WITHOUT advancing it: the splitmix64 of
-    a hash of its current state (read, not drawn from). Reproducible under torch.manual_seed, and
-    building a model leaves the generator's stream exactly where weight init left it. Two states
-    derived with no draw in between get the same seed (a model's weight init draws in between)."""
+    a hash of its current state (read, not drawn from) and of a per-process construction counter.
+    Reproducible under torch.manual_seed (the counter restarts with the process), building a
+    model leaves the generator's stream exactly where weight init left it, and two constructions
+    never share a seed even with no CPU draw between them (models initialised on the GPU, meta
+    device or skip_init, or loaded from a checkpoint without re-init)."""
     import hashlib
 
-    h = int.from_bytes(hashlib.sha256(torch.default_generator.get_state().numpy().tobytes())
-                       .digest()[:8], "little")
+    n = _CONSTRUCTIONS[0]
+    _CONSTRUCTIONS[0] += 1
+    state = torch.default_generator.get_state().numpy().tobytes()
+    h = int.from_bytes(hashlib.sha256(state + n.to_bytes(8, "little")).digest()[:8], "little")
     return _splitmix64(h) & (2 ** 62 - 1)
 
 

@@ -10,6 +10,7 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import ctypes
 import os
 
 import torch
@@ -93,8 +94,15 @@ class Graph:
         return self._gptr
 
     def csr(self, kind: str) -> Csr:
+        return self.csr_planes(kind)[0]
+
+    def csr_planes(self, kind: str, planes: "_lib.PlaneJob | None" = None) -> tuple[Csr, bool]:
+        """csr(kind), with the split-3 weight planes of `planes` written by the build's first
+        launch when this call builds the CSR (lgnn_graph_build_planes). Returns (csr, True) when
+        the planes were written, (csr, False) when the CSR was already built (or is traced):
+        the caller then makes them itself (lgnn_weight_planes)."""
         if kind in self._csr:
-            return self._csr[kind]
+            return self._csr[kind], False
         if torch.compiler.is_compiling():  # traced: the graph build is one opaque lgnn op
             if self._gptr is None and self.batch is not None:  # Batch.ptr rides along
                 rp, col, w, tp, ti, tw, tmap, topen, err, self._gptr = \
@@ -107,7 +115,7 @@ class Graph:
                     tmap=tmap if kind == "gat" else None,
                     tile_open=topen if kind == "gcn" else None, err=err)
             self._csr[kind] = c
-            return c
+            return c, False
         loops, norm = KIND[kind]
         n, e = self.num_nodes, self.num_edges
         cap = e + n
@@ -135,16 +143,16 @@ class Graph:
                 _lib.ptr(self.batch) if gptr is not None else None,
                 self.num_graphs if gptr is not None else 0, _lib.ptr(gptr), _lib.ptr(c.err),
                 _lib.ptr(ws), ws_bytes)
-        if FUSED_BUILD:  # one persistent launch (lgnn_graph_build_sync)
-            _lib.call("lgnn_graph_build_sync", *args, int(kind == "gcn_lazy"),
-                      _lib.ptr(_build_sync(dev)), _lib.stream(dev))
+        if planes is not None:
+            _lib.call("lgnn_graph_build_planes", *args, int(kind == "gcn_lazy"),
+                      ctypes.byref(planes), _lib.stream(dev))
         else:
             _lib.call("lgnn_graph_build_lazy" if kind == "gcn_lazy" else "lgnn_graph_build",
                       *args, _lib.stream(dev))
         self._csr[kind] = c
         if self.keep_build_workspace:
             self._last_ws = (kind, ws)
-        return c
+        return c, planes is not None
 
     def build_path(self, kind: str) -> str:
         """Which launches the last eager build of `kind` took: "sorted" (the target-sorted fast
@@ -231,25 +239,6 @@ class Graph:
     def dropped_edges(self, kind: str) -> int:
         """Number of edges with an out-of-range index (synchronises)."""
         return int(self.csr(kind).err.item())
-
-
-# the graph build as one persistent launch (LGNN_FUSED_BUILD=1); off by default: measured on
-# MI355X at C2 it takes 242 us against 36 us for the five launches — every grid barrier's
-# agent-scope release writes back the workgroup's XCD L2 and the acquire invalidates it, so the
-# CSR data each phase produces crosses the XCDs through memory instead of the kernel boundary's
-# single write-back (profiles/r03f_c2_per_step.txt)
-FUSED_BUILD = os.environ.get("LGNN_FUSED_BUILD", "0") == "1"
-_SYNC: dict = {}
-
-
-def _build_sync(dev) -> torch.Tensor:
-    """The fused build's grid-barrier words for this device (zeroed once, re-armed by every
-    launch). One per device: this package issues its builds on one stream per device."""
-    key = torch.device(dev).index
-    t = _SYNC.get(key)
-    if t is None:
-        t = _SYNC[key] = torch.zeros(4, dtype=torch.int32, device=dev)
-    return t
 
 
 def adj_t_to_edge_index(adj_t, with_values: bool = False):

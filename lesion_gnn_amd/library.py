@@ -795,10 +795,10 @@ def _gcn_layout(params, L):
 def gcn_stack(x: Tensor, g: list[Tensor], mean: bool, L: int,
               params: list[Tensor]) -> list[Tensor]:
     """[logits, pooled, H_0..H_L, S_1..S_L, planes_t or none] (the eager _GCNStack forward)."""
-    from .ops import _GCNStack, no_plane_cache
+    from .ops import _GCNStack, adjt_in_planes
 
     ctx = _Ctx()
-    with no_plane_cache():  # the op's planes output is a fresh buffer (planes + Â^T room)
+    with adjt_in_planes():  # the op's planes output is a fresh buffer (planes + Â^T room)
         logits = _GCNStack.forward(ctx, x, TGraph(g, "gcn"), mean, L, *params)
     sv = ctx.saved_tensors
     hs = list(sv[2:3 + L])

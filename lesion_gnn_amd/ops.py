@@ -100,23 +100,6 @@ OPEN_IN_FUSED_BWD = OPEN_IN_FUSED
 # dP = dlogits W_out formed inside the single-launch split-3 backward (LGNN_HEAD_FOLD=0: by
 # lgnn_pool_head_bwd before it)
 HEAD_FOLD = os.environ.get("LGNN_HEAD_FOLD", "1") != "0"
-# the open tiles' aggregations (forward Â H, backward Â^T dY) of 128-wide layers by windowed dense
-# blocks (lgnn_window_aggregate) ahead of the layer kernel, instead of the layer kernel's per-entry
-# row gather: opt-in (LGNN_WINDOW=1) — correct, but slower than the gather at C5 (62 us per call
-# against the 40-65 us of gather it replaces). WINDOW_CHUNKS: widest window
-# (64-row chunks) per tile.
-WINDOW = os.environ.get("LGNN_WINDOW", "0") == "1"
-WINDOW_CHUNKS = int(os.environ.get("LGNN_WINDOW_CHUNKS", "20"))
-
-
-def window_aggregate(csr_ptr, csr_idx, csr_w, M: int, inp: torch.Tensor, out: torch.Tensor,
-                     open_: torch.Tensor | None, want: int = 1):
-    """out[rows of the selected tiles] = A_hat inp (lgnn_window_aggregate; 128-wide rows)."""
-    _lib.call("lgnn_window_aggregate", _lib.ptr(csr_ptr), _lib.ptr(csr_idx), _lib.ptr(csr_w), M,
-              _lib.ptr(inp), inp.size(1), _lib.ptr(out), _lib.ptr(open_), int(want),
-              WINDOW_CHUNKS, _s(inp.device))
-
-
 _CAPACITY: dict = {}
 
 
@@ -161,107 +144,70 @@ def _mode_open_in_fused(mode, graph: Graph, direction: str) -> bool:
     return n > 0 and (64 % n == 0 or n % 64 == 0)
 
 
-def weight_planes(Ws: list, d_in: int, transposed: bool = False, extra: int = 0):
-    """bf16 three-plane images of the stack weights for the split-3 kernels (one launch):
-    returns (planes [L+1, 3, 128, 128] int16, planes_t or None). planes_t is flat: the
+def plane_buffers(Ws: list, transposed: bool = False, extra: int = 0):
+    """Uninitialised buffers for the bf16 three-plane images of the stack weights (split-3
+    kernels): (planes [L+1, 3, 128, 128] int16, planes_t or None). planes_t is flat: the
     transposed planes, then `extra` int16 of room (the forward's Â^T planes, bwd_planes_numel)."""
     nl = len(Ws)
     dev = Ws[0].device
     planes = torch.empty(nl, 3, 128, 128, dtype=torch.int16, device=dev)
     planes_t = torch.empty(nl * 3 * 128 * 128 + extra, dtype=torch.int16, device=dev) \
         if transposed else None
-    widths = (ctypes.c_int * (nl + 1))(*([d_in] + [W.size(0) for W in Ws]))
-    arr = ctypes.c_void_p * nl
-    _lib.call("lgnn_weight_planes", nl, arr(*[W.data_ptr() for W in Ws]), widths,
-              _lib.ptr(planes), _lib.ptr(planes_t), _s(dev))
     return planes, planes_t
 
 
-# Split-3 weight planes kept across steps (LGNN_PLANE_CACHE=0: made afresh by every forward).
-# An entry holds the planes of one weight list, valid while every weight keeps the version it had
-# when the planes were made. lesion_gnn_amd.optim.Adam rewrites the planes of the weights it
-# updates in the same launch (lgnn_adam_step_planes) and, writing the weights through their
-# pointers, leaves their versions alone: the next forward then runs no weight-plane launch. Any
-# other in-place update (torch's optimizers, load_state_dict, copy_) bumps a version and the next
-# forward makes the planes afresh. Writes through `.data` bypass version counters: call
-# invalidate_weight_planes() after such a write.
-PLANE_CACHE = os.environ.get("LGNN_PLANE_CACHE", "1") != "0"
-_PLANES: dict = {}     # (weight pointers, d_in, transposed) -> _PlaneEntry
-_PLANE_REG: dict = {}  # weight data_ptr -> (_PlaneEntry, layer index)
+def plane_job(Ws: list, d_in: int, planes, planes_t) -> _lib.PlaneJob:
+    """lgnn_plane_job: the split of Ws into `planes` / `planes_t` (lgnn_weight_planes' arguments),
+    run by the graph build's first launch (Graph.csr_planes) or by lgnn_weight_planes."""
+    nl = len(Ws)
+    if nl > _lib.LGNN_PLANE_JOB_MAX:
+        raise _lib.LgnnError("plane job: too many layers")
+    job = _lib.PlaneJob()
+    job.nl = nl
+    widths = [d_in] + [W.size(0) for W in Ws]
+    for i, v in enumerate(widths):
+        job.widths[i] = v
+    for i, W in enumerate(Ws):
+        job.W[i] = W.data_ptr()
+    job.planes = planes.data_ptr()
+    job.planes_t = planes_t.data_ptr() if planes_t is not None else None
+    job._keep = (Ws, planes, planes_t)  # the pointers' owners live as long as the job
+    return job
 
 
-class _PlaneEntry:
-    __slots__ = ("planes", "planes_t", "refs", "versions", "shapes")
-
-    def __init__(self, Ws, planes, planes_t):
-        self.planes, self.planes_t = planes, planes_t
-        self.refs = [weakref.ref(W) for W in Ws]
-        self.versions = [W._version for W in Ws]
-        self.shapes = [tuple(W.shape) for W in Ws]
-
-    def valid(self, Ws) -> bool:
-        return len(Ws) == len(self.refs) and all(
-            r() is W and W._version == v and tuple(W.shape) == sh
-            for r, W, v, sh in zip(self.refs, Ws, self.versions, self.shapes))
+def run_plane_job(job: _lib.PlaneJob, dev) -> None:
+    """The split of `job` as its own launch (lgnn_weight_planes)."""
+    arr = ctypes.c_void_p * job.nl
+    _lib.call("lgnn_weight_planes", job.nl, arr(*[job.W[i] for i in range(job.nl)]),
+              (ctypes.c_int * (job.nl + 1))(*[job.widths[i] for i in range(job.nl + 1)]),
+              job.planes, job.planes_t, _s(dev))
 
 
-_NO_CACHE = [0]  # > 0 inside no_plane_cache()
+def weight_planes(Ws: list, d_in: int, transposed: bool = False, extra: int = 0):
+    """bf16 three-plane images of the stack weights for the split-3 kernels (one launch):
+    returns (planes [L+1, 3, 128, 128] int16, planes_t or None); see plane_buffers."""
+    planes, planes_t = plane_buffers(Ws, transposed, extra)
+    run_plane_job(plane_job(Ws, d_in, planes, planes_t), Ws[0].device)
+    return planes, planes_t
 
 
-class no_plane_cache:
-    """Context: stack forwards make fresh planes (with the Â^T room after them) — the compiled
-    lgnn::gcn_stack op returns that buffer as an output of its own."""
+# The split-3 weight planes are made afresh by every forward, from the live weights: when the
+# forward builds its graph the split runs as extra workgroups of the build's first launch
+# (lgnn_graph_build_planes), otherwise as its own launch. Nothing is cached across steps, so a
+# captured step replays the split and sees any write to the weights between replays
+# (load_state_dict, EMA, clipping), eager or captured alike.
+_ADJT_IN_PLANES = [0]  # > 0 inside adjt_in_planes()
+
+
+class adjt_in_planes:
+    """Context: stack forwards put the Â^T room after the transposed planes (one buffer) — the
+    compiled lgnn::gcn_stack op returns that buffer as an output of its own."""
 
     def __enter__(self):
-        _NO_CACHE[0] += 1
+        _ADJT_IN_PLANES[0] += 1
 
     def __exit__(self, *exc):
-        _NO_CACHE[0] -= 1
-
-
-def invalidate_weight_planes() -> None:
-    """Drop every cached weight-plane entry (after writing weights through `.data`)."""
-    _PLANES.clear()
-    _PLANE_REG.clear()
-
-
-def cached_weight_planes(Ws: list, d_in: int, transposed: bool):
-    """weight_planes(Ws, d_in, transposed) kept across steps (PLANE_CACHE): one lgnn_weight_planes
-    launch when the weights changed other than through lesion_gnn_amd.optim.Adam, none
-    otherwise. The returned tensors are shared with the cache (the optimizer rewrites them)."""
-    if not PLANE_CACHE or torch.compiler.is_compiling():
-        return weight_planes(Ws, d_in, transposed)
-    key = (tuple(W.data_ptr() for W in Ws), int(d_in), bool(transposed))
-    e = _PLANES.get(key)
-    if e is not None and e.valid(Ws):
-        return e.planes, e.planes_t
-    planes, planes_t = weight_planes(Ws, d_in, transposed)
-    e = _PlaneEntry(Ws, planes, planes_t)
-    if len(_PLANES) >= 16:  # a few weight sets per process; drop the oldest
-        old = _PLANES.pop(next(iter(_PLANES)))
-        for k in [k for k, (ent, _) in _PLANE_REG.items() if ent is old]:
-            del _PLANE_REG[k]
-    _PLANES[key] = e
-    for l, W in enumerate(Ws):
-        _PLANE_REG[W.data_ptr()] = (e, l)
-    return planes, planes_t
-
-
-def plane_targets(p: torch.Tensor):
-    """(planes ptr, planes_t ptr or None) of parameter p's layer in a valid cache entry, or None:
-    where lesion_gnn_amd.optim.Adam writes p's new planes."""
-    if not PLANE_CACHE:
-        return None
-    hit = _PLANE_REG.get(p.data_ptr())
-    if hit is None:
-        return None
-    e, l = hit
-    r = e.refs[l]()
-    if r is not p or p._version != e.versions[l] or tuple(p.shape) != e.shapes[l]:
-        return None
-    per = 3 * 128 * 128 * 2  # bytes of one layer's three planes
-    return (e.planes.data_ptr() + l * per,
-            e.planes_t.data_ptr() + l * per if e.planes_t is not None else None)
+        _ADJT_IN_PLANES[0] -= 1
 
 
 def adjt_numel(M) -> int:
@@ -297,11 +243,33 @@ def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list, keep: dict | No
     rest (graphs straddling 64-node tiles) layer by layer (lgnn_node_linear_fwd_tiles), into the
     same buffers. With graphs aligned to tiles (C2: N = 64) the second group is empty.
     kind: the graph build ("gcn", or "gcn_lazy" when only the fused backward follows)."""
-    csr = graph.csr(kind)
-    open_ = graph.tile_open(kind)
     M = x.size(0)
     L = len(Ws) - 1
     dev = x.device
+    s3 = MFMA_MODE == "s3" and L >= 1
+    if s3:
+        # the transposed planes (the split-3 backward's dH = G W_l operand) come from the same
+        # split when the caller keeps them; the split rides the graph build when this forward
+        # builds the graph
+        want_adjt = keep is not None and _s3f(L) and ADJT
+        extra = adjt_numel(M) if want_adjt and _ADJT_IN_PLANES[0] else 0
+        planes, planes_t = plane_buffers(Ws, transposed=keep is not None, extra=extra)
+        job = plane_job(Ws, x.size(1), planes, planes_t)
+        csr, split_done = graph.csr_planes(kind, job)
+        if not split_done:
+            run_plane_job(job, dev)
+        if extra:  # the Â^T tiles in the room after the planes (the compiled op's one output)
+            adjt_t, adjt = None, _adjt_ptr(planes_t, L)
+        else:
+            adjt_t = torch.empty(adjt_numel(M), dtype=torch.int16, device=dev) \
+                if want_adjt else None
+            adjt = _lib.ptr(adjt_t)
+        if keep is not None:
+            keep["planes_t"] = planes_t
+            keep["adjt"] = adjt_t
+    else:
+        csr = graph.csr(kind)
+    open_ = graph.tile_open(kind)
     hs = [torch.empty(M, W.size(0), dtype=torch.float32, device=dev) for W in Ws]
     ss = [torch.empty(M, Ws[l].size(1), dtype=torch.float32, device=dev) for l in range(1, L + 1)]
     arr = ctypes.c_void_p * (L + 1)
@@ -309,23 +277,7 @@ def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list, keep: dict | No
     bp = arr(*[b.data_ptr() for b in bs])
     Hp = arr(*[h.data_ptr() for h in hs])
     widths = (ctypes.c_int * (L + 1))(*[W.size(0) for W in Ws])
-    if MFMA_MODE == "s3" and L >= 1:
-        # the transposed planes (the split-3 backward's dH = G W_l operand) come from the same
-        # launch when the caller keeps them
-        want_adjt = keep is not None and _s3f(L) and ADJT
-        if PLANE_CACHE and not _NO_CACHE[0]:  # cached planes; the Â^T tiles in their own buffer
-            planes, planes_t = cached_weight_planes(Ws, x.size(1), transposed=keep is not None)
-            adjt_t = torch.empty(adjt_numel(M), dtype=torch.int16, device=dev) \
-                if want_adjt else None
-            adjt = _lib.ptr(adjt_t)
-        else:  # fresh planes with the Â^T tiles after them (the compiled op's one output)
-            extra = adjt_numel(M) if want_adjt else 0
-            planes, planes_t = weight_planes(Ws, x.size(1), transposed=keep is not None,
-                                             extra=extra)
-            adjt_t, adjt = None, (_adjt_ptr(planes_t, L) if extra else None)
-        if keep is not None:
-            keep["planes_t"] = planes_t
-            keep["adjt"] = adjt_t
+    if s3:
         if _open_in_fused(OPEN_IN_FUSED, graph, "fwd"):  # open tiles in the same launch
             _lib.call("lgnn_gcn_stack_fwd_s3_all", _lib.ptr(x), M, x.size(1), 1,
                       _lib.ptr(csr.rowptr), _lib.ptr(csr.col), _lib.ptr(csr.w), L,
@@ -344,10 +296,6 @@ def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list, keep: dict | No
         inp = x if l == 0 else hs[l - 1]
         c = csr if l > 0 else None
         s_out = ss[l - 1] if l > 0 else None
-        if c is not None and WINDOW and inp.size(1) == 128:
-            # S_l = Â H_{l-1} of the open tiles by windowed dense blocks, then the layer on S_l
-            window_aggregate(c.rowptr, c.col, c.w, M, inp, s_out, open_)
-            inp, c, s_out = s_out, None, None
         _lib.call("lgnn_node_linear_fwd_tiles", _lib.ptr(inp), M, inp.size(1),
                   _lib.ptr(c.rowptr) if c else None, _lib.ptr(c.col) if c else None,
                   _lib.ptr(c.w) if c else None, 0.0, _lib.ptr(Ws[l]), _lib.ptr(bs[l]),
@@ -443,12 +391,6 @@ def stack_bwd(dp: torch.Tensor | None, x: torch.Tensor, graph: Graph, mean: bool
         K, N = widths[l], widths[l + 1]
         if l == L:
             mode, dY, tc = _lib.LGNN_GRAD_POOL, dp, None
-        elif WINDOW and N == 128:
-            # the conv's aggregation gradient Â^T dS of the open tiles by windowed dense blocks
-            # (transpose CSR), then the layer in direct mode
-            dY = torch.empty(M, N, dtype=torch.float32, device=dev)
-            window_aggregate(csr.tptr, csr.tidx, csr.tw, M, dS, dY, open_)
-            mode, tc = _lib.LGNN_GRAD_DIRECT, None
         else:
             mode, dY, tc = _lib.LGNN_GRAD_TRANSPOSE, dS, csr
         dX = torch.empty(M, K, dtype=torch.float32, device=dev) if l > 0 else None
@@ -458,7 +400,7 @@ def stack_bwd(dp: torch.Tensor | None, x: torch.Tensor, graph: Graph, mean: bool
                   _lib.ptr(hs[l]) if l > 0 else None,
                   _lib.LGNN_ACT_ELU if l > 0 else _lib.LGNN_ACT_NONE, _lib.ptr(Sx[l]), M, K,
                   None, None, None, 0.0, _lib.ptr(Ws[l]), N, _lib.ptr(dX), _lib.ptr(dWp[l]),
-                  _lib.ptr(dbp[l]), P, _lib.ptr(open_), 1, 1, _s(dev))
+                  _lib.ptr(dbp[l]), P, _lib.ptr(open_), 1, 2 if s3f else 1, _s(dev))
         dS = dX
     return _stack_bwd_outputs(L, widths, dWp, dbp, P, dev, reducer)
 
@@ -553,84 +495,15 @@ def spmm_raw(rowptr, col, w, self_scale: float, x: torch.Tensor) -> torch.Tensor
     return y
 
 
-_POOL_TICKETS: dict = {}
-
-
-def pool_tickets(dev, B: int) -> torch.Tensor:
-    """lgnn_pool_head_fwd_split's per-graph tickets for this device: zeroed once, grown as needed,
-    left zero by every launch (one stream per device issues them)."""
-    key = torch.device(dev).index
-    t = _POOL_TICKETS.get(key)
-    if t is None or t.numel() < B:
-        t = _POOL_TICKETS[key] = torch.zeros(max(B, 1024), dtype=torch.int32, device=dev)
-    return t
-
-
-def pool_splits(B: int, M: int, D: int) -> int:
-    """Workgroups per graph of the readout: 1 (one workgroup per graph) unless LGNN_POOL_SPLITS
-    asks for the split kernel. Measured: the split kernel's per-workgroup agent-scope release
-    (before its ticket) writes back the XCD's dirty L2 — the activations the forward just wrote —
-    so it lost everywhere (refcfg 0.642 -> 1.010 ms at 4 splits, C2 0.247 -> 0.450 at 2)."""
-    if D % 4 or D > 512 or B == 0:
-        return 1
-    env = os.environ.get("LGNN_POOL_SPLITS")
-    return max(1, min(64, int(env))) if env else 1
-
-
 def pool_head_fwd(H: torch.Tensor, graph: Graph, mean: bool, Wout=None, bout=None):
     B, D = graph.num_graphs, H.size(1)
     pooled = torch.empty(B, D, dtype=torch.float32, device=H.device)
     C = Wout.size(0) if Wout is not None else 0
     logits = torch.empty(B, C, dtype=torch.float32, device=H.device) if Wout is not None else None
-    S = pool_splits(B, H.size(0), D)
-    if S > 1:
-        part = torch.empty(B * S * D, dtype=torch.float32, device=H.device)
-        _lib.call("lgnn_pool_head_fwd_split", _lib.ptr(H), _lib.ptr(graph.gptr), B, D,
-                  int(mean), _lib.ptr(Wout), _lib.ptr(bout), C, S, _lib.ptr(part),
-                  _lib.ptr(pool_tickets(H.device, B)), _lib.ptr(pooled), _lib.ptr(logits),
-                  _s(H.device))
-        return pooled, logits
     _lib.call("lgnn_pool_head_fwd", _lib.ptr(H), _lib.ptr(graph.gptr), B, D, int(mean),
               _lib.ptr(Wout), _lib.ptr(bout), C, _lib.ptr(pooled), _lib.ptr(logits),
               _s(H.device))
     return pooled, logits
-
-
-_CE_TICKETS: dict = {}
-# the CE forward inside the readout kernel (lgnn_pool_head_ce_fwd, last-workgroup sum) instead of
-# a separate single-workgroup launch: opt-in — 1024 workgroups' tickets on a few words cost more
-# (C2: readout 8.5 -> 25 us) than the launch saved (4.9 us)
-CE_IN_POOL = os.environ.get("LGNN_CE_IN_POOL", "0") == "1"
-
-
-def pool_head_ce_fwd(H: torch.Tensor, graph: Graph, mean: bool, Wout, bout, y, weight):
-    """pool_head_fwd + the CE criterion's forward in one launch (lgnn_pool_head_ce_fwd), or None
-    when the shape is off that kernel (then the caller runs the two launches). Returns
-    (pooled, logits, lse, out[loss, wsum], bad, pm, wt): pm [B, C] and wt [B] are the factors of
-    the logits gradient, dlogits = gloss * wt / wsum * pm (lgnn_ce_src)."""
-    B, D = graph.num_graphs, H.size(1)
-    C = Wout.size(0)
-    if B < 1 or D % 4 or D > 512 or not 1 <= C <= 16 or pool_splits(B, H.size(0), D) > 1:
-        return None
-    dev = H.device
-    key = torch.device(dev).index
-    tk = _CE_TICKETS.get(key)
-    if tk is None:  # zeroed once, re-armed by every launch
-        tk = _CE_TICKETS[key] = torch.zeros(10, dtype=torch.int32, device=dev)
-    pooled = torch.empty(B, D, dtype=torch.float32, device=dev)
-    logits = torch.empty(B, C, dtype=torch.float32, device=dev)
-    lse = torch.empty(B, dtype=torch.float32, device=dev)
-    out = torch.empty(2, dtype=torch.float32, device=dev)
-    bad = torch.empty(1, dtype=torch.int32, device=dev)
-    pm = torch.empty(B, C, dtype=torch.float32, device=dev)
-    wt = torch.empty(B, dtype=torch.float32, device=dev)
-    ws = torch.empty(_lib.load().lgnn_pool_head_ce_workspace_bytes(B), dtype=torch.uint8,
-                     device=dev)
-    _lib.call("lgnn_pool_head_ce_fwd", _lib.ptr(H), _lib.ptr(graph.gptr), B, D, int(mean),
-              _lib.ptr(Wout), _lib.ptr(bout), C, _lib.ptr(pooled), _lib.ptr(logits), _lib.ptr(y),
-              _lib.ptr(weight), _lib.ptr(lse), _lib.ptr(out), _lib.ptr(out) + 4, _lib.ptr(bad),
-              _lib.ptr(pm), _lib.ptr(wt), _lib.ptr(tk), _lib.ptr(ws), ws.numel(), _s(dev))
-    return pooled, logits, lse, out, bad, pm, wt
 
 
 def pool_head_bwd(dlogits: torch.Tensor, pooled: torch.Tensor, Wout: torch.Tensor):
@@ -1133,9 +1006,7 @@ class _GCNStack(torch.autograd.Function):
         return logits
 
     @staticmethod
-    def _fwd(ctx, x, graph, mean, L, params, ce=None):
-        """ce = (y int64, weight | None): the readout also runs the CE forward where the kernel
-        takes the shape (ctx.ce_fwd = (lse, out) then; None otherwise)."""
+    def _fwd(ctx, x, graph, mean, L, params):
         _lib.require_gpu(x, *params)
         x = _f32c(x)
         params = [_f32c(p) for p in params]
@@ -1149,7 +1020,8 @@ class _GCNStack(torch.autograd.Function):
             (1 <= L <= 2 or keep is not None) and not ctx.needs_input_grad[0]
         kind = "gcn_lazy" if lazy else "gcn"
         ctx.kind = kind
-        csr = graph.csr(kind)
+        # the fused forward builds the graph itself (with the weight-plane split riding along)
+        csr = None if fused else graph.csr(kind)
         ctx.fused = fused
         ctx.planes_t = None
         ctx.adjt = None
@@ -1174,14 +1046,7 @@ class _GCNStack(torch.autograd.Function):
                 ss.append(s_)
                 ctx.saved_s.append(fast)
         W_out, b_out = params[2 + 2 * L], params[3 + 2 * L]
-        ctx.ce_fwd = None
-        r = pool_head_ce_fwd(hs[-1], graph, mean, W_out, b_out, *ce) \
-            if ce is not None and CE_IN_POOL else None
-        if r is not None:
-            pooled, logits, lse, out, _, pm, wt = r
-            ctx.ce_fwd = (lse, out, pm, wt)
-        else:
-            pooled, logits = pool_head_fwd(hs[-1], graph, mean, W_out, b_out)
+        pooled, logits = pool_head_fwd(hs[-1], graph, mean, W_out, b_out)
         ctx.graph, ctx.mean, ctx.L = graph, mean, L
         ctx.n_saved = 2 + len(hs) + len(ss) + len(params)
         return logits, (x, pooled, *hs, *ss, *params)
@@ -1286,11 +1151,9 @@ class _GCNStackCE(torch.autograd.Function):
         yy = y.to(torch.int64).contiguous()
         w = _f32c(weight) if weight is not None else None
         # the readout runs the CE forward too (one launch) where its kernel takes the shape
-        logits, to_save = _GCNStack._fwd(ctx, x, graph, mean, L, params, ce=(yy, w))
+        logits, to_save = _GCNStack._fwd(ctx, x, graph, mean, L, params)
         z = logits
-        if ctx.ce_fwd is not None:  # the readout ran the CE forward (CE_IN_POOL)
-            lse, out, pm, wt = ctx.ce_fwd
-        else:  # one single-workgroup launch: loss, lse and the gradient's factors pm / wt
+        if True:  # one single-workgroup launch: loss, lse and the gradient's factors pm / wt
             B, C = z.shape
             dev = z.device
             lse = torch.empty(B, dtype=torch.float32, device=dev)
@@ -1440,12 +1303,6 @@ def bn_bwd_apply(dA, Z, mask, scale, shift, mean, invstd, sums, count, training,
 BN_FUSED = os.environ.get("LGNN_BN_FUSED", "1") != "0"
 
 
-# GEMM arithmetic of the BN-fused GIN MLP kernels: "f32" = fp32 MFMA (tile_lw.h, the default),
-# "s3" = split-3 bf16 MFMA (lin3.hip, fp32 accuracy). The layer-wise kernels are bound by the
-# per-tile load latency, not by the MFMA pipe: at C4 the split-3 pair measured 0.735 ms per step
-# against 0.703 for fp32 (same box), so split-3 stays opt-in (LGNN_GIN_MFMA=s3).
-GIN_MFMA = os.environ.get("LGNN_GIN_MFMA", "f32")
-
 
 def gin_bn_fused(K: int, N1: int, N2: int) -> bool:
     """True when _GINConv runs its BatchNorm inside the linear kernels (fast-path shapes)."""
@@ -1525,14 +1382,8 @@ class _GINConv(torch.autograd.Function):
         S = torch.empty_like(x)
         count = float(M)
         sums = None
-        s3 = GIN_MFMA == "s3"  # split-3 kernels: both layers' weight planes in one launch
-        fname = "lgnn_node_linear_fwd_s3" if s3 else "lgnn_node_linear_fwd_bn"
-        if s3:
-            planes, planes_t = weight_planes([W1, W2], x.size(1), transposed=True)
-            w1, w2 = planes[0].data_ptr(), planes[1].data_ptr()
-            ctx.gin_planes_t = planes_t
-        else:
-            w1, w2 = W1.data_ptr(), W2.data_ptr()
+        fname = "lgnn_node_linear_fwd_bn"
+        w1, w2 = W1.data_ptr(), W2.data_ptr()
         if training:
             part = torch.empty(P * 2 * N1, dtype=torch.float64, device=dev)
             _lib.call(fname, _lib.ptr(x), M, x.size(1), _lib.ptr(csr.rowptr),
@@ -1554,13 +1405,7 @@ class _GINConv(torch.autograd.Function):
                 sync_all_reduce(sums, group)
                 mean, invstd, scale, shift = bn_finalize(sums, count, bn, training, N1, dev)
         else:
-            if s3:
-                _lib.call(fname, _lib.ptr(x), M, x.size(1), _lib.ptr(csr.rowptr),
-                          _lib.ptr(csr.col), _lib.ptr(csr.w), float(self_scale), w1,
-                          _lib.ptr(b1), N1, _lib.LGNN_ACT_NONE, _lib.ptr(Z1), _lib.ptr(S),
-                          None, None, None, None, None, _s(dev))
-            else:
-                Z1, S = linear_fwd(x, W1, b1, _lib.LGNN_ACT_NONE, csr, self_scale, save_s=True)
+            Z1, S = linear_fwd(x, W1, b1, _lib.LGNN_ACT_NONE, csr, self_scale, save_s=True)
             mean, invstd, scale, shift = bn_finalize(sums, count, bn, training, N1, dev)
         A1 = torch.empty_like(Z1)
         N2 = W2.size(0)
@@ -1593,16 +1438,8 @@ class _GINConv(torch.autograd.Function):
         dev = Z1.device
         P = _lib.load().lgnn_bn_fused_partials(M)
         red: list = []
-        s3 = GIN_MFMA == "s3"
-        fname = "lgnn_node_linear_bwd_s3" if s3 else "lgnn_node_linear_bwd_bn"
-        if s3:  # the forward's transposed planes (rebuilt when the ctx does not carry them)
-            planes_t = getattr(ctx, "gin_planes_t", None)
-            if planes_t is None:
-                planes_t = weight_planes([W1, W2], K, transposed=True)[1]
-            w1 = planes_t.data_ptr()
-            w2 = w1 + 2 * 3 * 128 * 128
-        else:
-            w1, w2 = W1.data_ptr(), W2.data_ptr()
+        fname = "lgnn_node_linear_bwd_bn"
+        w1, w2 = W1.data_ptr(), W2.data_ptr()
         # Lin2 backward; its dX (= dA1) epilogue also sums the BN backward's (g, g xhat)
         dA1 = torch.empty_like(Z1)
         slab2 = torch.empty(P * (N2 * N1 + N2), dtype=torch.float32, device=dev)
@@ -1833,7 +1670,7 @@ class _GINStack(torch.autograd.Function):
 def gin_stack_eligible(x, W_in, convs_W) -> bool:
     """Whether the GIN model runs as one _GINStack node (eager, BN-fused fp32 kernels, every
     layer on the fast-path shapes)."""
-    return (not _compiling() and GIN_MFMA == "f32" and fast_shape(x.size(1), W_in.size(0)) and
+    return (not _compiling() and fast_shape(x.size(1), W_in.size(0)) and
             all(gin_bn_fused(W1.size(1), W1.size(0), W2.size(0)) for W1, W2 in convs_W))
 
 
@@ -1852,7 +1689,7 @@ def gin_stack(x, W_in, b_in, convs: list, W_out, b_out, graph: Graph, mean: bool
 
 def gin_conv_head_eligible(x, W1, W2) -> bool:
     """Whether gin_conv_head runs fused (eager, BN-fused fp32 kernels, fast-path shapes)."""
-    return (not _compiling() and GIN_MFMA == "f32" and
+    return (not _compiling() and
             gin_bn_fused(x.size(1), W1.size(0), W2.size(0)))
 
 

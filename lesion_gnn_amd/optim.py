@@ -65,7 +65,6 @@ class Adam(torch.optim.Optimizer):
                 # lgnn_adam_step's two-level ticket: 9 words, zeroed once, left zero
                 ticket = self._tickets[gi] = torch.zeros(9, dtype=torch.int32, device=dev)
             b1, b2 = group["betas"]
-            from .ops import plane_targets
 
             for c in range(0, len(ps), MAX_TENSORS):
                 chunk = ps[c:c + MAX_TENSORS]
@@ -80,20 +79,7 @@ class Adam(torch.optim.Optimizer):
                         float(b2), float(group["eps"]), float(group["weight_decay"]),
                         int(self._decoupled), int(group["maximize"]),
                         int(c + MAX_TENSORS >= len(ps)))
-                # weights with cached split-3 planes (ops.cached_weight_planes): the same launch
-                # writes their new planes, so the next forward runs no weight-plane launch
-                tg = [plane_targets(p) if p.dim() == 2 else None for p in chunk]
-                if any(t is not None for t in tg):
-                    _lib.call("lgnn_adam_step_planes", *args,
-                              arr(*[t[0] if t else None for t in tg]),
-                              arr(*[t[1] if t else None for t in tg]),
-                              (ctypes.c_int * n)(*[p.size(0) if p.dim() == 2 else 0
-                                                   for p in chunk]),
-                              (ctypes.c_int * n)(*[p.size(1) if p.dim() == 2 else 0
-                                                   for p in chunk]),
-                              _lib.stream(dev))
-                else:
-                    _lib.call("lgnn_adam_step", *args, _lib.stream(dev))
+                _lib.call("lgnn_adam_step", *args, _lib.stream(dev))
         return loss
 
 

@@ -29,11 +29,7 @@ def _grads(m):
 
 
 @pytest.mark.parametrize("case", ["c2", "ragged", "weighted"])
-@pytest.mark.parametrize("in_pool", [False, True])
-def test_fused_ce_bitwise_equals_unfused(cuda, case, in_pool, monkeypatch):
-    # in_pool: the CE forward inside the readout kernel (lgnn_pool_head_ce_fwd, opt-in) instead
-    # of lgnn_ce_fwd_factors; both hand the backward the same pm / wt factors
-    monkeypatch.setattr(ops, "CE_IN_POOL", in_pool)
+def test_fused_ce_bitwise_equals_unfused(cuda, case):
     if case == "ragged":
         b = synth.make_batch(96, k=8, d_in=128, seed=5, sizes="powerlaw")
     else:

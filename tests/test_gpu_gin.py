@@ -38,14 +38,12 @@ def assert_grads(go, gr):
                                    msg=lambda m: f"{k}: {m}")
 
 
-@pytest.mark.parametrize("bn_fused,mfma", [(True, "f32"), (True, "s3"), (False, "f32")])
+@pytest.mark.parametrize("bn_fused", [True, False])
 @pytest.mark.parametrize("B,pool", [(1024, "add"), (32, "mean")])
-def test_gin_c4_shape(cuda, B, pool, bn_fused, mfma, monkeypatch):
+def test_gin_c4_shape(cuda, B, pool, bn_fused, monkeypatch):
     """bn_fused: BatchNorm inside the MLP's linear kernels (lgnn_node_linear_fwd_bn / _bwd_bn,
-    the default; mfma "s3": their split-3 variants lgnn_node_linear_fwd_s3 / _bwd_s3) or the
-    separate lgnn_bn_* passes."""
+    the default) or the separate lgnn_bn_* passes."""
     monkeypatch.setattr(ops, "BN_FUSED", bn_fused)
-    monkeypatch.setattr(ops, "GIN_MFMA", mfma)
     b = synth.make_batch(B, n=64, k=8, d_in=128, seed=4)
     ours, oref = make_pair(128, [128, 128, 128], pool=pool)
     lo, losso, go, so = step(ours.to(cuda).train(), b, cuda)
@@ -107,7 +105,7 @@ def test_gin_dropout_runs(cuda):
 
 
 def test_gin_bn_fused_matches_unfused_with_dropout(cuda, monkeypatch):
-    """The BN-fused kernels (fp32 and split-3 MFMA) against the separate BN passes on the same
+    """The BN-fused kernels against the separate BN passes on the same
     dropout masks (MLP and
     between convs), training mode, ragged graphs: the same arithmetic up to the order of the fp64
     statistic sums, so within 1e-5 of each tensor's scale; running statistics too."""
@@ -118,14 +116,13 @@ def test_gin_bn_fused_matches_unfused_with_dropout(cuda, monkeypatch):
     sd = {k: v.clone() for k, v in m.state_dict().items()}
     rng = m._dropout_rng.clone()  # every run draws the same device dropout masks
     res = []
-    for fused, mfma in ((True, "f32"), (False, "f32"), (True, "s3")):
+    for fused in (True, False):
         monkeypatch.setattr(ops, "BN_FUSED", fused)
-        monkeypatch.setattr(ops, "GIN_MFMA", mfma)
         m.load_state_dict(sd)
         m._dropout_rng.copy_(rng)
         res.append(step(m, b, cuda))
-    _, (l2, _, g2, s2), _ = res
-    for l1, _, g1, s1 in (res[0], res[2]):
+    _, (l2, _, g2, s2) = res
+    for l1, _, g1, s1 in (res[0],):
         torch.testing.assert_close(l1, l2, rtol=0, atol=1e-5 * max(1.0, l2.abs().max().item()))
         for k in g2:
             torch.testing.assert_close(g1[k], g2[k], rtol=0,

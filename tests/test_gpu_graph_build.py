@@ -1,13 +1,10 @@
-"""GPU: the graph build as ONE persistent launch (lgnn_graph_build_sync, k_build: prep / count /
-scan / fill / finish / tmap behind grid barriers) is bit-identical to the five-launch pipeline
-(lgnn_graph_build / _lazy) for every CSR kind the models use — GCN (gcn_norm weights), its lazy
-variant with the tile flags, GAT (remove + add self loops, with tmap), GIN (loops kept) — on
-k-NN, irregular, shuffled-with-duplicates, invalid-edge and empty inputs; built twice in a row
-(the barrier words re-arm: all zero afterwards, no barrier timed out)."""
+"""GPU: the graph build's target-sorted fast path (k_prep_sorted + k_scan's sorted body) is
+bit-identical to the general launches (count / scan / fill / finish) on the inputs it takes, and
+hands the near misses to them; the weight-plane side job of the first launch
+(lgnn_graph_build_planes) writes what lgnn_weight_planes writes."""
 import pytest
 import torch
 
-from lesion_gnn_amd import graph as graph_mod
 from lesion_gnn_amd import synth
 from lesion_gnn_amd.graph import Graph
 
@@ -33,8 +30,7 @@ def _cases():
 FIELDS = ("rowptr", "col", "w", "tptr", "tidx", "tw", "tmap", "tile_open", "err")
 
 
-def _build(ei, n, kind, fused, cuda, monkeypatch):
-    monkeypatch.setattr(graph_mod, "FUSED_BUILD", fused)
+def _build(ei, n, kind, cuda):
     g = Graph(ei.to(cuda), n)
     c = g.csr(kind)
     nnz = int(c.rowptr[-1].item())
@@ -49,22 +45,6 @@ def _build(ei, n, kind, fused, cuda, monkeypatch):
             continue  # the lazy build leaves the source CSR unwritten when no tile is open
         out[f] = t.cpu()
     return out
-
-
-@pytest.mark.parametrize("case", ["knn_c2", "irregular", "lognormal", "invalid", "no_edges",
-                                  "big_rows"])
-@pytest.mark.parametrize("kind", ["gcn", "gcn_lazy", "gat", "gin"])
-def test_fused_build_bitexact(cuda, monkeypatch, case, kind):
-    graph_mod._build_sync(cuda).zero_()  # a failed case must not leave its give-up count here
-    ei, n = _cases()[case]
-    want = _build(ei, n, kind, False, cuda, monkeypatch)
-    for _ in range(2):
-        got = _build(ei, n, kind, True, cuda, monkeypatch)
-        assert set(got) == set(want)
-        for f in want:
-            assert torch.equal(got[f], want[f]), (case, kind, f)
-    sync = graph_mod._build_sync(cuda).cpu().tolist()
-    assert sync == [0, 0, 0, 0], sync  # re-armed, no barrier gave up
 
 
 def _sorted_cases():
@@ -127,14 +107,43 @@ def test_sorted_build_bitexact(cuda, monkeypatch, case, kind):
     is taken exactly for the inputs it covers (lazy GCN builds; the others never try it)."""
     (ei, n), path = _sorted_cases()[case]
     monkeypatch.setenv("LGNN_GRAPH_SORTED", "0")
-    want = _build(ei, n, kind, False, cuda, monkeypatch)
+    want = _build(ei, n, kind, cuda)
     monkeypatch.setenv("LGNN_GRAPH_SORTED", "1")
     g = Graph(ei.to(cuda), n)
     g.keep_build_workspace = True  # build_path() below
-    got = _build(ei, n, kind, False, cuda, monkeypatch)
+    got = _build(ei, n, kind, cuda)
     assert set(got) == set(want)
     for f in want:
         assert torch.equal(got[f], want[f]), (case, kind, f)
     if kind == "gcn_lazy":
         g.csr(kind)
         assert g.build_path(kind) == path, case
+
+
+@pytest.mark.parametrize("kind", ["gcn_lazy", "gcn", "gin"])
+@pytest.mark.parametrize("case", ["knn_c2", "irregular", "no_edges"])
+def test_build_plane_side_job(cuda, kind, case):
+    """lgnn_graph_build_planes: the first launch's extra workgroups write bitwise the planes
+    (and transposed planes) lgnn_weight_planes writes, on both first launches (the sorted path's
+    k_prep_sorted and the general k_prep), and the CSR is the plain build's."""
+    from lesion_gnn_amd import ops
+
+    ei, n = _cases()[case]
+    gen = torch.Generator().manual_seed(3)
+    widths = [128, 96, 128, 64]
+    Ws = [torch.randn(widths[l + 1], widths[l], generator=gen).to(cuda) for l in range(3)]
+    want_p, want_t = ops.weight_planes(Ws, widths[0], transposed=True)
+    planes, planes_t = ops.plane_buffers(Ws, transposed=True)
+    planes.fill_(-1)
+    planes_t.fill_(-1)
+    g = Graph(ei.to(cuda), n)
+    c, done = g.csr_planes(kind, ops.plane_job(Ws, widths[0], planes, planes_t))
+    assert done
+    assert torch.equal(planes, want_p) and torch.equal(planes_t, want_t)
+    c2, done2 = g.csr_planes(kind, ops.plane_job(Ws, widths[0], planes, planes_t))
+    assert c2 is c and not done2  # already built: the caller splits on its own
+    want = _build(ei, n, kind, cuda)
+    for f in ("rowptr", "col", "w"):
+        nnz = int(c.rowptr[-1].item())
+        t = getattr(c, f)
+        assert torch.equal(t[:nnz].cpu() if f != "rowptr" else t.cpu(), want[f]), f

@@ -74,6 +74,13 @@ def test_radius_graph_edge_cases(cuda):
     # flow='target_to_source' swaps the rows
     got = radius_graph(big.to(cuda), 0.03, flow="target_to_source").cpu()
     assert torch.equal(got, want.flip(0))
+    # nodes but num_graphs = 0: rejected (the batch vector cannot index an empty ptr)
+    from lesion_gnn_amd._lib import LgnnError
+    with pytest.raises(LgnnError):
+        radius_graph(big.to(cuda), 0.03, torch.zeros(1500, dtype=torch.int64, device=cuda),
+                     num_graphs=0)
+    # no nodes: no edges
+    assert radius_graph(big[:0].to(cuda), 0.03).numel() == 0
 
 
 def test_radius_transform_by_name(cuda):

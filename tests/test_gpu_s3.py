@@ -176,57 +176,3 @@ def test_stack_fwd_s3_deterministic(cuda):
     h2, _ = ops.stack_fwd(x, g, Ws, bs)
     for a, c in zip(h1, h2):
         assert torch.equal(a, c)
-
-
-@pytest.mark.parametrize("M,K,N,act,gather", [(1000, 128, 128, 1, False), (130, 96, 64, 0, True),
-                                              (4096, 128, 100, 1, True), (70, 64, 128, 0, False)])
-def test_layerwise_linear_s3(cuda, M, K, N, act, gather):
-    """lgnn_node_linear_fwd_s3 / _bwd_s3 (lin3.hip, no BatchNorm): Y = act(P(X) W^T + b) and
-    its DIRECT backward (dW, db slabs, dX) against float64 torch, at fp32-class error (1e-5 of
-    each result's scale); P(X) the GIN aggregation (1 + eps) x + sum of neighbours with eps =
-    0.25 when gather."""
-    gen = torch.Generator().manual_seed(M + K + N)
-    x = torch.randn(M, K, generator=gen)
-    W = torch.randn(N, K, generator=gen) / K ** 0.5
-    b = torch.randn(N, generator=gen)
-    dy = torch.randn(M, N, generator=gen)
-    xd = x.double()
-    g = None
-    if gather:
-        bt = synth.make_batch((M + 39) // 40, k=6, seed=3, sizes="lognormal")
-        ei = bt.edge_index[:, bt.edge_index.max(0).values < M]
-        g = Graph(ei.to(cuda), M)
-        s = 1.25 * xd + torch.zeros_like(xd).index_add_(0, ei[1], xd[ei[0]])
-    else:
-        s = xd
-    z = s @ W.double().T + b.double()
-    y = torch.nn.functional.elu(z) if act else z
-    dz = dy.double() * (torch.where(y > 0, 1.0, y + 1.0) if act else 1.0)
-    dW_ref, db_ref, dX_ref = dz.T @ s, dz.sum(0), dz @ W.double()
-
-    dev = cuda
-    planes, planes_t = ops.weight_planes([W.to(dev)], K, transposed=True)
-    xg = x.to(dev)
-    Y = torch.empty(M, N, device=dev)
-    S = torch.empty(M, K, device=dev) if gather else None
-    csr = g.csr("gin") if gather else None
-    _lib.call("lgnn_node_linear_fwd_s3", _lib.ptr(xg), M, K,
-              _lib.ptr(csr.rowptr) if gather else None, _lib.ptr(csr.col) if gather else None,
-              _lib.ptr(csr.w) if gather else None, 1.25 if gather else 0.0, _lib.ptr(planes),
-              _lib.ptr(b.to(dev)), N, act, _lib.ptr(Y), _lib.ptr(S), None, None, None, None,
-              None, _lib.stream(dev))
-    torch.testing.assert_close(Y.cpu().double(), y, rtol=0, atol=1e-5 * y.abs().max().item())
-    if gather:
-        torch.testing.assert_close(S.cpu().double(), s, rtol=0, atol=1e-5 * s.abs().max().item())
-    P = _lib.load().lgnn_bn_fused_partials(M)
-    slab = torch.empty(P * (N * K + N), device=dev)
-    dX = torch.empty(M, K, device=dev)
-    Xs = S if gather else xg
-    _lib.call("lgnn_node_linear_bwd_s3", 0, _lib.ptr(dy.to(dev)), _lib.ptr(Y), act, _lib.ptr(Xs),
-              M, K, _lib.ptr(planes_t), N, _lib.ptr(dX), _lib.ptr(slab),
-              _lib.ptr(slab[P * N * K:]), P, None, None, None, None, None, None, None, None, 0.0,
-              0, _lib.stream(dev))
-    dW = slab[:P * N * K].view(P, N, K).sum(0).cpu().double()
-    db = slab[P * N * K:].view(P, N).sum(0).cpu().double()
-    for got, want in ((dW, dW_ref), (db, db_ref), (dX.cpu().double(), dX_ref)):
-        torch.testing.assert_close(got, want, rtol=0, atol=1e-5 * want.abs().max().item())

@@ -87,3 +87,19 @@ def test_stack_fwd_validation_without_gpu():
     assert lib.lgnn_gcn_stack_fwd(None, 10, 128, 1, 1, 1, None, 1, arr, arr, widths, arr,
                                   None, None) == -22
     assert lib.lgnn_tile_count(65) == 2 and lib.lgnn_tile_count(64) == 1
+
+
+def test_dropout_seeds_distinct_without_cpu_draws():
+    """Two models built with no CPU generator draw in between (GPU / meta init, checkpoint
+    loads) get different dropout seeds: derived_seed mixes a per-process construction counter
+    into the hash of the generator state, and leaves the generator untouched."""
+    import torch
+
+    from lesion_gnn_amd import dropout
+
+    torch.manual_seed(0)
+    before = torch.default_generator.get_state().clone()
+    a, b = dropout.derived_seed(), dropout.derived_seed()
+    assert a != b
+    assert torch.equal(torch.default_generator.get_state(), before)
+    assert 0 <= a < 2 ** 62 and 0 <= b < 2 ** 62

@@ -23,15 +23,14 @@ if os.environ.get("STAMPS_ABLATIONS"):
         VARIANTS[k] = [f"-DLGNN_ABLATE={v}"]
     VARIANTS["sb"] = ["-DLGNN_S3F_SB"]
     VARIANTS["sb_stamps"] = ["-DLGNN_S3F_SB", "-DLGNN_STAMPS"]
-NAMES = ["prologue: stage + load wait", "prologue: dZ_L", "prologue: Â planes", "l2 G, G image", "l2 H image", "l2 dW", "l2 dH+dZ", "l1 G, G image",
-         "l1 H image", "l1 dW", "l1 dH+dZ", "l0 X + dW", "tile tail"]
-# k_s3_fbwd8 (LGNN_S3F_WAVES=8): the same libraries, copied so each has its own variant switch
-NAMES8 = ["prologue (adj, dZ_L)", "l2 G + images", "l2 dW", "l2 dH+dZ+exch", "l1 G + images",
-          "l1 dW", "l1 dH+dZ+exch", "l0 X + dW", "tile tail"]
-WAVES8 = {"w8": "default", "w8_stamps": "stamps"}
+NAMES = ["prologue: stage + load wait", "prologue: dZ_L", "prologue: Â planes", "l2 G, G image",
+         "l2 H image", "l2 dW", "l2 dH+dZ", "l1 G, G image", "l1 H image", "l1 dW", "l1 dH+dZ",
+         "l0 X + dW", "tile tail"]
 
 
-PREBUILT = ["v2"]  # variant libraries built by hand from an earlier source (not rebuilt here)
+# variant libraries built from another source tree (tools/build_base_lib.sh: git HEAD's sources
+# as tools/_abl/liblgnn_s3f_base.so, an A/B baseline on the same box); not rebuilt here
+PREBUILT = ["base", "base_stamps"]
 
 
 def build():
@@ -70,11 +69,7 @@ def run():
     adjt_ptr = ops._adjt_ptr(planes_t, L) if os.environ.get("STAMPS_ADJT", "1") != "0" else None
     s = torch.cuda.current_stream().cuda_stream
     arr = ctypes.c_void_p * (L + 1)
-    import shutil
-    for v8, v in WAVES8.items():
-        shutil.copy(LIB % v, LIB % v8)
-    for v in [*VARIANTS, *WAVES8, *[p for p in PREBUILT if os.path.exists(LIB % p)]]:
-        os.environ["LGNN_S3F_WAVES"] = "8" if v in WAVES8 else "4"
+    for v in [*VARIANTS, *[p for p in PREBUILT if os.path.exists(LIB % p)]]:
         lib = ctypes.CDLL(LIB % v)
         for name, (res, args) in _lib.SIGNATURES.items():
             f = getattr(lib, name, None)  # a variant built from an older source may lack some
@@ -111,7 +106,7 @@ def run():
             n = int((a[0, :62] > 0).sum())
             d = np.diff(a[:, :n], axis=1)
             print(f"stamps per block: {n}; mean span {(a[:, n - 1] - a[:, 0]).mean():.0f} ticks")
-            names = NAMES8 if v in WAVES8 else NAMES
+            names = NAMES
             per = len(names)
             for i in range(per):  # phases of the 2nd and later tiles, averaged
                 cols = [j for j in range(i, n - 1, per) if j >= per]
