@@ -65,6 +65,18 @@ WORKLOADS = {
     "c5k16": dict(model="gcn", sizes="powerlaw", n=64, k=16, d_in=128, hidden=[128, 128, 128],
                   classes=5, loss="CE", pool="mean",
                   desc="C5: GCN, power-law N in [16,512], k=16"),
+    # the reference sweep's space off the fused fast paths (scripts/sweep.py:126-141: widths
+    # {32..512}, 1-8 layers, heads {1, 2, 4, 8}): timed as lines of their own, not the metric
+    "sweep_gcn3": dict(model="gcn", sizes="fixed", n=64, k=8, d_in=128, hidden=[128] * 4,
+                       classes=5, loss="CE", pool="mean",
+                       desc="sweep: GCN with 3 convs (layer-major split-3 backward)"),
+    "sweep_gat256h8": dict(model="gat", sizes="lognormal", n=64, k=6, d_in=1025,
+                           hidden=[256] * 4, heads=8, classes=5, loss="MSE", pool="mean",
+                           last_channel_class=True, dropout=0.35,
+                           desc="sweep: GAT [256]*4, heads 8, dropout 0.35, d_in 1025, fp32"),
+    "sweep_gin512": dict(model="gin", sizes="fixed", n=64, k=8, d_in=128, hidden=[512] * 4,
+                         classes=5, loss="CE", pool="add",
+                         desc="sweep: GIN [512]*4 + global_add_pool (generic-shape kernels)"),
 }
 
 

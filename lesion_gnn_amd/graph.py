@@ -39,7 +39,7 @@ class Csr:
     tidx: torch.Tensor    # int32 [cap] target of each entry, grouped by source
     tw: torch.Tensor      # fp32 [cap]
     tmap: torch.Tensor | None  # int32 [cap] target-CSR position of each transpose entry (GAT)
-    tile_open: torch.Tensor | None  # int32 [ceil(N/64) + 7] tiles an edge leaves, their count,
+    tile_open: torch.Tensor | None  # int32 [ceil(N/64) + LGNN_TILE_OPEN_EXTRA] tiles an edge leaves, their count,
     # and the fused stack kernels' grid-barrier words (LGNN_TILE_OPEN_EXTRA)
     err: torch.Tensor     # int32 [1] count of dropped out-of-range edges
 
@@ -209,7 +209,7 @@ class Graph:
         return key
 
     def tile_open(self, kind: str) -> torch.Tensor:
-        """int32 [ceil(N/64) + 7]: 1 for the 64-node tiles an edge leaves or that exceed the
+        """int32 [ceil(N/64) + LGNN_TILE_OPEN_EXTRA]: 1 for the 64-node tiles an edge leaves or that exceed the
         on-chip CSR capacity, then the number of such tiles (from the graph build for kind
         "gcn"; lgnn_tile_open otherwise)."""
         c = self.csr(kind)

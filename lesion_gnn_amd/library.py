@@ -26,6 +26,7 @@ import torch
 from torch import Tensor
 from torch.library import custom_op
 
+from . import _lib
 from .graph import Csr
 
 GPARTS = ("rowptr", "col", "w", "tptr", "tidx", "tw", "tmap", "tile_open", "err", "batch", "gptr")
@@ -84,6 +85,9 @@ class TGraph:
         if self._csr is None:
             raise RuntimeError(f"graph bundle carries no CSR (asked for {kind!r})")
         return self._csr
+
+    def csr_planes(self, kind: str, planes=None) -> tuple[Csr, bool]:
+        return self.csr(kind), False  # built by its own op: the caller splits the planes
 
     def tile_open(self, kind: str) -> Tensor:
         return self.csr(kind).tile_open
@@ -150,7 +154,7 @@ def _graph_build_fake(edge_index, num_nodes, kind):
             e.new_empty(n + 1, **i32), e.new_empty(cap, **i32), e.new_empty(cap, **f32),
             e.new_empty(cap if kind == "gat" else 0, **(i32 if kind == "gat" else
                                                        dict(dtype=torch.uint8))),
-            e.new_empty((n + 63) // 64 + 7 if kind == "gcn" else 0,
+            e.new_empty((n + 63) // 64 + _lib.LGNN_TILE_OPEN_EXTRA if kind == "gcn" else 0,
                         **(i32 if kind == "gcn" else dict(dtype=torch.uint8))),
             e.new_empty(1, **i32)]
 
