@@ -247,11 +247,15 @@ def _time_launches(launch, dev, reps=20):
 
 def time_dominant_kernels(model, b, dev):
     """The two largest kernels of the C2 step, each launched alone with the step's arguments:
-    * lgnn_tile::k_stack_bwd<3> — the fused backward of in_proj + 2 GCN convs (closed tiles),
-      useful FLOP per launch 2*M*(d_in*h + L*h*h) (dW) + 2*M*L*h*h (dH = G W) + 2*nnz*h*L (the
-      transposed aggregation);
-    * lgnn_tile::k_stack_fwd<true> — the fused forward, 2*M*(d_in*h + L*h*h) + 2*nnz*h*L.
-    The tile aggregation runs as a dense 64 x 64 MFMA product; its zeros are not counted."""
+    * lgnn_s3::k_s3_fbwd<L + 1, true> (`lgnn_gcn_stack_bwd_s3f_ce`, stack3_bwd.hip) — the fused
+      split-3 backward of in_proj + L GCN convs with the CE logits gradient and out_proj's dP
+      formed in its prologue; useful FLOP per launch 2*M*(d_in*h + L*h*h) (dW) + 2*M*L*h*h
+      (dH = G W) + 2*nnz*h*L (the transposed aggregation);
+    * lgnn_s3::k_s3_fwd<true> (`lgnn_gcn_stack_fwd_s3`, stack3.hip) — the fused split-3 forward,
+      2*M*(d_in*h + L*h*h) + 2*nnz*h*L.
+    The tile aggregation runs as a dense 64 x 64 MFMA product; its zeros are not counted. (The fp32
+    kernels lgnn_tile::k_stack_fwd / k_stack_bwd are timed instead when MFMA_MODE / BWD_MODE
+    select them.)"""
     import ctypes
 
     from lesion_gnn_amd import _lib, ops
