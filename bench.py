@@ -117,6 +117,9 @@ def parse():
                     help="run the N > 1 step plan (process group, gradient bucket + all-reduce, "
                          "SyncBN for GIN) even at --gpus 1, over a one-rank group: times the plan "
                          "a multi-GPU run executes on one GPU")
+    ap.add_argument("--rccl-eager", action="store_true",
+                    help="N > 1: run the collectives eagerly between captured graph segments "
+                         "instead of capturing them into the step's graph")
     ap.add_argument("--sync-bn", choices=["auto", "on", "off"], default="auto",
                     help="GIN with a process group: auto/on = SyncBN (full-batch statistics, "
                          "all-reduces inside forward and backward), off = per-replica statistics "
@@ -809,10 +812,17 @@ def dry_run(args, wl, world, rank):
         raise SystemExit("bench.py --dry-run: all-reduce result wrong")
 
 
-def step_plan(world: int, capture: bool, collectives_in_fwd: bool) -> tuple:
-    """How one training step runs (no collective is ever inside a captured HIP graph):
+def step_plan(world: int, capture: bool, collectives_in_fwd: bool,
+              rccl_capture: bool = False) -> tuple:
+    """How one training step runs:
       ("eager",)                                   --graph 0
       ("graph:step",)                              N = 1: forward + backward + Adam, one graph
+      ("graph:step+rccl",)                         N > 1 over RCCL (the default): the same one
+                                                   graph with the collectives captured in it —
+                                                   the SyncBN exchanges where forward and backward
+                                                   issue them, then the gradient bucket (pack,
+                                                   all-reduce, unpack) before Adam
+    With rccl_capture False (gloo, or --rccl-eager) no collective is captured:
       ("graph:fwd_bwd+pack", "rccl", "graph:unpack+opt")   N > 1: the gradient bucket is packed
                                                    (and scaled) at the end of the first graph and
                                                    unpacked at the head of the second; only the
@@ -827,6 +837,8 @@ def step_plan(world: int, capture: bool, collectives_in_fwd: bool) -> tuple:
         return ("eager",)
     if world == 1:
         return ("graph:step",)
+    if rccl_capture:
+        return ("graph:step+rccl",)
     if collectives_in_fwd:
         return ("graph:segments+pack", "rccl", "graph:unpack+opt")
     return ("graph:fwd_bwd+pack", "rccl", "graph:unpack+opt")
@@ -865,6 +877,17 @@ def make_step(plan: tuple, fwd_bwd, bucket, opt, dev, info: dict | None = None):
             fwd_bwd()
             opt.step()
         return g_step.replay
+    if plan == ("graph:step+rccl",):
+        # N > 1 over RCCL: the collectives (the SyncBN exchanges inside forward and backward,
+        # the gradient bucket) are captured into the step's one graph with everything else
+        g_all = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_all):
+            fwd_bwd()
+            bucket.pack()
+            bucket.reduce()
+            bucket.unpack()
+            opt.step()
+        return g_all.replay
     if plan[0] == "graph:segments+pack":
         from lesion_gnn_amd.dist import SegmentedCapture
 
@@ -941,7 +964,8 @@ def main():
             loss_fn(wl, run(b.x, b.edge_index, b.batch, B), b.y).backward(one)
 
     # GIN under SyncBN all-reduces inside its forward and backward (RCCL collectives)
-    plan = step_plan(2 if multi else 1, bool(args.graph), sync_bn)
+    plan = step_plan(2 if multi else 1, bool(args.graph), sync_bn,
+                     rccl_capture=multi and args.backend == "nccl" and not args.rccl_eager)
     bucket = ldist.GradBucket(params, B, B * world) if multi else None
     plan_info: dict = {}
     step = make_step(plan, fwd_bwd, bucket, opt, dev, plan_info)

@@ -84,10 +84,11 @@ def test_shard_bounds_balance_edges():
 
 
 def test_bench_step_plan():
-    """bench.py's step structure: a collective is never inside a captured graph — SyncBN (GIN,
-    C4) at N > 1 is captured as graph segments split at its all-reduces (which sit inside
-    forward and backward); otherwise the flat-gradient RCCL all-reduce is the only eager part
-    between two graphs."""
+    """bench.py's step structure: over RCCL the N > 1 step is one graph with its collectives
+    captured in it; with collectives that cannot be captured (gloo, --rccl-eager) SyncBN (GIN,
+    C4) is captured as graph segments split at its all-reduces (which sit inside forward and
+    backward), and otherwise the flat-gradient all-reduce is the only eager part between two
+    graphs."""
     import bench
 
     assert bench.step_plan(1, True, False) == ("graph:step",)
@@ -96,6 +97,11 @@ def test_bench_step_plan():
     assert bench.step_plan(8, True, True) == ("graph:segments+pack", "rccl", "graph:unpack+opt")
     assert bench.step_plan(4, False, False) == ("eager",)
     assert bench.step_plan(4, False, True) == ("eager",)
+    # over RCCL (the default backend) the collectives are captured into the step's graph
+    assert bench.step_plan(8, True, True, rccl_capture=True) == ("graph:step+rccl",)
+    assert bench.step_plan(2, True, False, rccl_capture=True) == ("graph:step+rccl",)
+    assert bench.step_plan(1, True, True, rccl_capture=True) == ("graph:step",)
+    assert bench.step_plan(4, False, True, rccl_capture=True) == ("eager",)
 
 
 class _SyncNormNet(torch.nn.Module):

@@ -105,11 +105,14 @@ def test_two_ranks_match_full_batch(cuda, kind):
                                            rtol=1e-5, atol=1e-6)
 
 
-def plan_worker(rank, world, port, q):
+def plan_worker(rank, world, port, q, backend="gloo"):
     """bench.py's N > 1 GIN + SyncBN plan, captured: graph segments split at the SyncBN
     exchanges (forward and backward), the gradient bucket exchange, the optimizer graph."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    kw = {"device_id": dev} if backend == "nccl" else {}
+    dist.init_process_group(backend, rank=rank, world_size=world, **kw)
     import bench
     from lesion_gnn_amd import dist as ldist
     from lesion_gnn_amd import ops, synth
@@ -130,7 +133,7 @@ def plan_worker(rank, world, port, q):
     def fwd_bwd():
         ops.cross_entropy(m(x, ei, bt, g1 - g0), y).backward()
 
-    plan = bench.step_plan(world, True, True)
+    plan = bench.step_plan(max(world, 2), True, True, rccl_capture=backend == "nccl")
     info = {}
     step = bench.make_step(plan, fwd_bwd, bucket, opt, dev, info)
     for _ in range(3):
@@ -178,3 +181,34 @@ def test_segmented_syncbn_plan_matches_full_batch(cuda):
                                            msg=lambda s: f"rank {r} {k}: {s}")
             else:
                 assert torch.equal(got, v.cpu()), k
+
+
+def test_rccl_captured_plan_one_rank(cuda):
+    """bench.py's default N > 1 plan over RCCL (step_plan -> "graph:step+rccl": the SyncBN
+    exchanges and the gradient all-reduce captured into the step's one HIP graph), run on a
+    one-rank RCCL group (RCCL needs one GPU per rank): 3 replays after make_step's 3 eager steps
+    hold the weights and BN statistics of 6 single-process steps."""
+    from lesion_gnn_amd import ops, synth
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=plan_worker, args=(0, 1, free_port(), q, "nccl"))
+    p.start()
+    rank, res = q.get(timeout=300)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    assert res["plan"] == ("graph:step+rccl",)
+    b = synth.make_batch(B, n=N, k=K, d_in=32, seed=17)
+    m = build("gin").to(cuda).train()
+    opt = torch.optim.SGD(list(m.parameters()), lr=0.05)
+    x, ei, bt, y = b.x.to(cuda), b.edge_index.to(cuda), b.batch.to(cuda), b.y.to(cuda)
+    for _ in range(6):
+        opt.zero_grad(set_to_none=True)
+        ops.cross_entropy(m(x, ei, bt, B), y).backward()
+        opt.step()
+    for k, v in m.state_dict().items():
+        got = torch.from_numpy(res["state"][k])
+        if got.dtype.is_floating_point:
+            torch.testing.assert_close(got, v.cpu(), rtol=1e-4, atol=1e-5, msg=lambda s: f"{k}: {s}")
+        else:
+            assert torch.equal(got, v.cpu()), k
