@@ -744,7 +744,7 @@ def cpu_share() -> int:
     return n
 
 
-def cpu_baseline(wl, B, seconds):
+def cpu_baseline(wl, B, seconds, c1: bool = False):
     """Oracle (plain-torch CPU restatement of the PyG path) on the host cores:
     same model, same step (fwd + loss + bwd + Adam), same per-graph shapes. Two legs, each 3
     warmup steps then the median of up to 10 timed steps (fewer if a leg passes `seconds`):
@@ -753,11 +753,15 @@ def cpu_baseline(wl, B, seconds):
       * 1 thread, on a B/8-graph sample of the same workload (a 1024-graph step takes seconds
         on one core; the per-graph cost does not depend on the batch size at these sizes).
     `value` / `cores` are the all-cores leg; the host's os.cpu_count() and OMP_NUM_THREADS are
-    reported beside them."""
+    reported beside them. c1 (the C2 workload): two more legs at SURVEY §8d's C1 shape — the same
+    GCN step on 32 graphs (the reference's CPU plumbing config), all cores and 1 thread."""
     host = os.cpu_count() or 1
     avail = cpu_share()
     legs = []
-    for threads, nb in ((avail, B), (1, max(1, B // 8))):
+    plan = [(avail, B), (1, max(1, B // 8))]
+    if c1:
+        plan += [(avail, 32), (1, 32)]
+    for threads, nb in plan:
         torch.set_num_threads(threads)
         b = make_batch(wl, nb, seed=11)
         m = build_model(wl, oracle=True)
@@ -780,14 +784,20 @@ def cpu_baseline(wl, B, seconds):
         legs.append({"threads": threads, "graphs_per_step": nb, "steps": len(times),
                      "median_ms": round(med * 1e3, 2), "value": round(nb / med, 2)})
     main_leg = legs[0]
-    return {"value": main_leg["value"], "unit": "graphs/s", "cores": main_leg["threads"],
+    extra = {}
+    if c1:
+        extra["c1"] = {"graphs_per_step": 32, "value": legs[2]["value"], "cores": legs[2]["threads"],
+                       "one_thread_value": legs[3]["value"]}
+    return {**{"value": main_leg["value"], "unit": "graphs/s", "cores": main_leg["threads"]},
+            **extra,
             "kind": "port", "host_cpu_count": host, "cpu_share": avail,
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
             "one_thread_value": legs[1]["value"], "legs": legs,
             "sample": f"{wl['desc']}; all-cores leg {main_leg['steps']} steps x "
                       f"{main_leg['graphs_per_step']} graphs, 1-thread leg {legs[1]['steps']} "
-                      f"steps x {legs[1]['graphs_per_step']} graphs; median step time after 3 "
-                      f"warmups; torch CPU fp32"}
+                      f"steps x {legs[1]['graphs_per_step']} graphs"
+                      + ("; C1 legs (32 graphs, all cores / 1 thread)" if c1 else "")
+                      + "; median step time after 3 warmups; torch CPU fp32"}
 
 
 def dry_run(args, wl, world, rank):
@@ -1064,7 +1074,7 @@ def main():
     if rank == 0 and not args.no_kernel_timing:
         out["knn_graph"] = time_knn(b, wl, dev)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        out["cpu_baseline"] = cpu_baseline(wl, B, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(wl, B, args.cpu_seconds, c1=args.workload == "c2")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if multi:
