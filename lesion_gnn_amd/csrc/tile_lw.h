@@ -36,7 +36,33 @@ __device__ __forceinline__ f32x4 agg_row_local(const TileIdx& ti, int rr, const 
   return acc;
 }
 
-// Global path (graphs straddling tiles, or more than CAPE entries): CSR and source rows read
+// Staged-index global path (AGG_GROWS: sources outside the tile, the block within CAPE_LW): the
+// entries from LDS as the local path reads them, the source rows gathered from global memory —
+// one dependent round trip per EB batch instead of two; same order and arithmetic.
+template <int UB = EB>
+__device__ __forceinline__ f32x4 agg_row_grows(const TileIdx& ti, int rr,
+                                               const float* __restrict__ X, int K, int kc) {
+  static_assert(UB <= EB, "row batches read at most EB padding entries");
+  const int eb = ti.rp[0];
+  const int e0 = ti.rp[rr] - eb, e1 = ti.rp[rr + 1] - eb;
+  f32x4 acc = zero4();
+  for (int e = e0; e < e1; e += UB) {
+    int2 p[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) p[u] = ti.ow[e + u];
+    f32x4 v[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) v[u] = ld4(X + (int64_t)p[u].x * K + kc);
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const float wv = e + u < e1 ? __int_as_float(p[u].y) : 0.f;
+      acc += wv * v[u];
+    }
+  }
+  return acc;
+}
+
+// Global path (graphs straddling tiles with more than CAPE_LW entries): CSR and source rows read
 // from global memory, same order and arithmetic as the local path (bitwise-identical sums).
 __device__ __forceinline__ f32x4 agg_row_global(const TileIdx& ti, int rr,
                                                 const float* __restrict__ X, int K, int kc,
@@ -119,7 +145,7 @@ __device__ __forceinline__ void fwd_tiles(float* A, float* S, TileIdx& ti,
   }
   // pipeline prologue: the first tile's rows and index block
   f32x4 xr[8];
-  IdxRegs R;
+  IdxRegsLw R;
   if constexpr (!(ABL & 16)) load_rows(xr, bX, K, (int)(t * TM));
   if constexpr (GATHER && !(ABL & 2)) {
     idx_load_head(R, rowptr, M, t * TM);
@@ -129,7 +155,7 @@ __device__ __forceinline__ void fwd_tiles(float* A, float* S, TileIdx& ti,
     const int64_t r0 = t * TM;
     const int64_t tn = seek_tile(t + gridDim.x, ntiles, tmask, want);
     const bool has_next = tn < ntiles;
-    bool staged = true;
+    int agg = AGG_LOCAL;
     if constexpr (ABL & 16) {
 #pragma unroll
       for (int it = 0; it < 8; ++it) xr[it] = zero4();
@@ -151,7 +177,7 @@ __device__ __forceinline__ void fwd_tiles(float* A, float* S, TileIdx& ti,
     } else {
       store_rows_lds(A, xr, M, K, r0);
     }
-    if constexpr (GATHER && !(ABL & 2)) idx_store(ti, staged, R, r0);
+    if constexpr (GATHER && !(ABL & 2)) agg = idx_store(ti, R, r0);
     __syncthreads();
     // prefetch: next tile's rows and index head fly during this tile's aggregation and MFMAs
     if (has_next) {
@@ -159,14 +185,15 @@ __device__ __forceinline__ void fwd_tiles(float* A, float* S, TileIdx& ti,
       if constexpr (GATHER && !(ABL & 2)) idx_load_head(R, rowptr, M, tn * TM);
     }
     if constexpr (GATHER) {
-      auto agg_tile = [&](auto staged_tag) {
-        constexpr bool STG = decltype(staged_tag)::value;
+      auto agg_tile = [&](auto mode_tag) {
+        constexpr int MODE = decltype(mode_tag)::value;
 #pragma unroll 1
         for (int it = 0; it < 8; ++it) {
           const int rr = hw + 8 * it;
           f32x4 a;
           if constexpr (ABL & 2) a = ld4(A + rr * LDS + 4 * li);
-          else if constexpr (STG) a = agg_row_local(ti, rr, A);
+          else if constexpr (MODE == AGG_LOCAL) a = agg_row_local(ti, rr, A);
+          else if constexpr (MODE == AGG_GROWS) a = agg_row_grows(ti, rr, X, K, kc);
           else a = agg_row_global(ti, rr, X, K, kc, col, w);
           if (self_scale != 0.f) a += self_scale * ld4(A + rr * LDS + 4 * li);
           a = sel4(4 * li < K && r0 + rr < M, a);
@@ -175,8 +202,9 @@ __device__ __forceinline__ void fwd_tiles(float* A, float* S, TileIdx& ti,
             bst4(bS, (int)((r0 + rr) * K + 4 * li) * 4, a);
         }
       };
-      if (staged) agg_tile(std::true_type{});
-      else agg_tile(std::false_type{});
+      if (agg == AGG_LOCAL) agg_tile(std::integral_constant<int, AGG_LOCAL>{});
+      else if (agg == AGG_GROWS) agg_tile(std::integral_constant<int, AGG_GROWS>{});
+      else agg_tile(std::integral_constant<int, AGG_GLOBAL>{});
       if constexpr (!(ABL & 2)) {
         if (has_next) idx_load_body(R, col, w);
       }
@@ -291,7 +319,7 @@ __device__ __forceinline__ void bwd_tiles(
   constexpr bool PREF =
       !(GMODE == LGNN_GRAD_TRANSPOSE && (BNM == BN_GSTATS || LGNN_TPREF_ALL));
   f32x4 dr[8];
-  IdxRegs R;
+  IdxRegsLw R;
   const int64_t tfirst = seek_tile(xcd_block(), ntiles, tmask, want);  // XCD-contiguous tiles
   if constexpr (GMODE == LGNN_GRAD_TRANSPOSE) {
     const int64_t t0 = tfirst;
@@ -310,7 +338,7 @@ __device__ __forceinline__ void bwd_tiles(
     const bool has_next = tn < ntiles;
     // ---- dZ tile -> C
     if constexpr (GMODE == LGNN_GRAD_TRANSPOSE) {
-      bool staged = true;
+      int agg = AGG_LOCAL;
       if constexpr (ABL & 16) {
 #pragma unroll
         for (int it = 0; it < 8; ++it) dr[it] = zero4();
@@ -318,7 +346,7 @@ __device__ __forceinline__ void bwd_tiles(
         load_rows(dr, bdY, N, (int)r0);
       }
       store_rows_lds(A, dr, M, N, r0);
-      if constexpr (!(ABL & 2)) idx_store(ti, staged, R, r0);
+      if constexpr (!(ABL & 2)) agg = idx_store(ti, R, r0);
       // this tile's H rows (ELU') are issued before the barrier so they land during it
       f32x4 hv[8];
       if constexpr (ACT == LGNN_ACT_ELU) {
@@ -334,15 +362,16 @@ __device__ __forceinline__ void bwd_tiles(
         if constexpr (!(ABL & 16) && PREF) load_rows(dr, bdY, N, (int)(tn * TM));
         if constexpr (!(ABL & 2)) idx_load_head(R, tptr, M, tn * TM);
       }
-      auto agg_tile = [&](auto staged_tag) {
-        constexpr bool STG = decltype(staged_tag)::value;
+      auto agg_tile = [&](auto mode_tag) {
+        constexpr int MODE = decltype(mode_tag)::value;
 #pragma unroll 1
         for (int it = 0; it < 8; ++it) {
           const int rr = hw + 8 * it;
           const int64_t row = r0 + rr;
           f32x4 g;
           if constexpr (ABL & 2) g = ld4(A + rr * LDS + 4 * li);
-          else if constexpr (STG) g = agg_row_local(ti, rr, A);
+          else if constexpr (MODE == AGG_LOCAL) g = agg_row_local(ti, rr, A);
+          else if constexpr (MODE == AGG_GROWS) g = agg_row_grows(ti, rr, dY, N, oc);
           else g = agg_row_global(ti, rr, dY, N, oc, tidx, tw);
           if (tself != 0.f) g += tself * ld4(A + rr * LDS + 4 * li);
           if constexpr (ACT == LGNN_ACT_ELU) {
@@ -352,8 +381,9 @@ __device__ __forceinline__ void bwd_tiles(
           st4(C + rr * LDS + 4 * li, sel4(oin && row < M, g));
         }
       };
-      if (staged) agg_tile(std::true_type{});
-      else agg_tile(std::false_type{});
+      if (agg == AGG_LOCAL) agg_tile(std::integral_constant<int, AGG_LOCAL>{});
+      else if (agg == AGG_GROWS) agg_tile(std::integral_constant<int, AGG_GROWS>{});
+      else agg_tile(std::integral_constant<int, AGG_GLOBAL>{});
       if constexpr (!(ABL & 2)) {
         if (has_next) idx_load_body(R, tidx, tw);
       }

@@ -41,17 +41,22 @@ constexpr int TM = 64;
 constexpr int KC = 128;
 constexpr int LDS = KC + 4;
 constexpr int NT = 256;
-constexpr int CAPE = 1024;
+constexpr int CAPE = 1024;     // CSR entries of a closed tile (the fused stack kernels)
+constexpr int CAPE_LW = 1280;  // CSR entries staged by the layer-wise tile bodies (64 x (16 + 1)
+                               // at k = 16 fits; 5 per thread)
 constexpr int EB = 8;
 
-// A tile's CSR block in LDS. `local` (every entry's source row is in this tile — the k-NN
-// case with graphs aligned to tiles): ow[j] = (float offset of the source row in the A image,
-// weight bits), padded with EB zero-weight entries so a row's batch reads need no bounds logic.
-// Otherwise only rp is used and the rows are aggregated from global memory.
+// How a tile's rows are aggregated (idx_store):
+enum { AGG_GLOBAL = 0,   // index block too large: CSR entries and source rows from global memory
+       AGG_LOCAL = 1,    // every source row is in this tile: ow[j] = (float offset of the source
+                         // row in the A image, weight bits), rows read from LDS
+       AGG_GROWS = 2 };  // sources leave the tile: ow[j] = (global source row, weight bits),
+                         // rows gathered from global memory, no index round trip
+// A tile's CSR block in LDS, padded with EB zero-weight entries (source offset / row 0) so a
+// row's batch reads need no bounds logic.
 struct TileIdx {
   int rp[TM + 1];
-  int local;
-  int2 ow[CAPE + EB];
+  int2 ow[CAPE_LW + EB];
 };
 
 // Tile selection by a per-tile mask (nullable = every tile): with `want` = 1 only tiles whose
@@ -113,17 +118,19 @@ __device__ __forceinline__ void store_rows_lds(float* A, const f32x4 (&v)[RPT], 
 // tile's block is in flight while the current tile aggregates and runs its MFMAs).
 //   head: rowptr[r0 .. r0+64] (one per thread, tid <= 64) + the uniform entry range (eb, ne)
 //   body: the ne <= CAPE entries (col, w), CAPE/NT per thread; issued once the head has landed
-template <int NTH>
+template <int NTH, int CAP = CAPE>
 struct IdxRegsT {
+  static constexpr int cap = CAP;
   int rp;
   int eb, ne;
-  int c[CAPE / NTH];
-  float w[CAPE / NTH];
+  int c[CAP / NTH];
+  float w[CAP / NTH];
 };
 using IdxRegs = IdxRegsT<NT>;
+using IdxRegsLw = IdxRegsT<NT, CAPE_LW>;  // the layer-wise tile bodies (tile_lw.h)
 
-template <int NTH>
-__device__ __forceinline__ void idx_load_head(IdxRegsT<NTH>& R, const int32_t* __restrict__ rowptr,
+template <int NTH, int CAP>
+__device__ __forceinline__ void idx_load_head(IdxRegsT<NTH, CAP>& R, const int32_t* __restrict__ rowptr,
                                               int64_t M, int64_t r0, int tid_ = -1) {
   const int tid = tid_ < 0 ? (int)threadIdx.x : tid_;
   const int64_t r = r0 + (tid <= TM ? tid : 0);
@@ -133,13 +140,13 @@ __device__ __forceinline__ void idx_load_head(IdxRegsT<NTH>& R, const int32_t* _
   R.ne = rowptr[rl] - R.eb;
 }
 
-template <int NTH>
-__device__ __forceinline__ void idx_load_body(IdxRegsT<NTH>& R, const int32_t* __restrict__ col,
+template <int NTH, int CAP>
+__device__ __forceinline__ void idx_load_body(IdxRegsT<NTH, CAP>& R, const int32_t* __restrict__ col,
                                               const float* __restrict__ w, int tid_ = -1) {
-  if (R.ne > CAPE) return;
+  if (R.ne > CAP) return;
   const int tid = tid_ < 0 ? (int)threadIdx.x : tid_;
 #pragma unroll
-  for (int u = 0; u < CAPE / NTH; ++u) {
+  for (int u = 0; u < CAP / NTH; ++u) {
     const int j = tid + u * NTH;
     const int jc = j < R.ne ? j : 0;
     R.c[u] = col[R.eb + jc];
@@ -147,33 +154,33 @@ __device__ __forceinline__ void idx_load_body(IdxRegsT<NTH>& R, const int32_t* _
   }
 }
 
-// Writes the prefetched block to LDS. Ends with a barrier (block-wide OR of "an entry leaves
-// the tile"); `staged` = the tile takes the local path.
-template <int NTH>
-__device__ __forceinline__ void idx_store(TileIdx& ti, bool& staged, const IdxRegsT<NTH>& R,
-                                          int64_t r0) {
+// Writes the prefetched block to LDS and returns how the tile aggregates (AGG_*, block-uniform).
+// Ends with a barrier (block-wide OR of "an entry leaves the tile").
+template <int NTH, int CAP>
+__device__ __forceinline__ int idx_store(TileIdx& ti, const IdxRegsT<NTH, CAP>& R, int64_t r0) {
+  static_assert(CAP <= CAPE_LW, "TileIdx holds CAPE_LW entries");
   const int tid = threadIdx.x;
   if (tid <= TM) ti.rp[tid] = R.rp;
-  bool fits = R.ne <= CAPE;
+  const bool fits = R.ne <= CAP;
   int out = 0;
   if (fits) {
 #pragma unroll
-    for (int u = 0; u < CAPE / NTH; ++u) {
+    for (int u = 0; u < CAP / NTH; ++u) {
       const int j = tid + u * NTH;
       const int rel = R.c[u] - (int)r0;
       if (j < R.ne && (unsigned)rel >= (unsigned)TM) out = 1;
     }
   }
   const bool any_out = __syncthreads_or(out);
-  staged = fits && !any_out;
-  if (staged) {
+  if (!fits) return AGG_GLOBAL;
 #pragma unroll
-    for (int u = 0; u < CAPE / NTH; ++u) {
-      const int j = tid + u * NTH;
-      if (j < R.ne) ti.ow[j] = make_int2((R.c[u] - (int)r0) * LDS, __float_as_int(R.w[u]));
-    }
-    if (tid < EB) ti.ow[R.ne + tid] = make_int2(0, 0);
+  for (int u = 0; u < CAP / NTH; ++u) {
+    const int j = tid + u * NTH;
+    if (j < R.ne)
+      ti.ow[j] = make_int2(any_out ? R.c[u] : (R.c[u] - (int)r0) * LDS, __float_as_int(R.w[u]));
   }
+  if (tid < EB) ti.ow[R.ne + tid] = make_int2(0, 0);
+  return any_out ? AGG_GROWS : AGG_LOCAL;
 }
 
 // Dense Â_tile from the tile's row-CSR block (entry j of R: source R.c, weight R.w; its target
