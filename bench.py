@@ -810,12 +810,11 @@ def dry_run(args, wl, world, rank):
         dist.barrier()
     ok = bool(torch.all(flat == world * (world + 1) / 2))
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": None, "unit": "graphs/s", "n_gpus": world,
-                          "dry_run": True, "allreduce_ok": ok,
-                          "dist": {"backend": args.backend if world > 1 else None,
-                                   "world_size": world},
-                          "config": {"workload": wl["desc"], "name": args.workload,
-                                     "parallelism": f"dp{world}"}}), flush=True)
+        emit({"metric": METRIC, "value": None, "unit": "graphs/s", "n_gpus": world,
+              "dry_run": True, "allreduce_ok": ok,
+              "dist": {"backend": args.backend if world > 1 else None, "world_size": world},
+              "config": {"workload": wl["desc"], "name": args.workload,
+                         "parallelism": f"dp{world}"}})
     if world > 1:
         dist.destroy_process_group()
     if not ok:
@@ -931,11 +930,30 @@ def make_step(plan: tuple, fwd_bwd, bucket, opt, dev, info: dict | None = None):
     return step
 
 
+_JSON_OUT = None  # the process's original stdout: the one JSON line goes there
+
+
+def emit(obj) -> None:
+    """Print the bench's JSON line on the real stdout (library banners went to stderr)."""
+    line = json.dumps(obj) + "\n"
+    if _JSON_OUT is None:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    else:
+        os.write(_JSON_OUT, line.encode())
+
+
 def main():
+    global _JSON_OUT
     args = parse()
     wl = WORKLOADS[args.workload]
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
+    # everything the libraries print on stdout (RCCL's version banner at communicator creation,
+    # ...) goes to stderr, so stdout holds exactly the one JSON line
+    sys.stdout.flush()
+    _JSON_OUT = os.dup(1)
+    os.dup2(2, 1)
     world, rank, dev = setup_dist(args)
     if args.dry_run:
         return dry_run(args, wl, world, rank)
@@ -1076,7 +1094,7 @@ def main():
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(wl, B, args.cpu_seconds, c1=args.workload == "c2")
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     if multi:
         dist.destroy_process_group()
 
