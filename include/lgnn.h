@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 36
+#define LGNN_ABI_VERSION 37
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -716,6 +716,11 @@ int lgnn_s3_gemm_att(const float* A, int64_t M, int K, const uint16_t* Wp, int N
 int lgnn_s3_wgrad_partials(int64_t M, int K, int N);
 int lgnn_s3_wgrad(const float* dY, int N, const float* X, int64_t M, int K, int planes,
                   float* partials, int num_partials, float* db_partials, void* stream);
+/* lgnn_s3_gemm_act (ABI v37): lgnn_s3_gemm (planes = 3, no column sums) with the activation in
+ * the epilogue, Y = act(A B^T + b) (LGNN_ACT_ELU = torch's F.elu, reference gin.py:31) — the wide
+ * (K or N > 128) GIN / GCN linears of the reference sweep (scripts/sweep.py:126) */
+int lgnn_s3_gemm_act(const float* A, int64_t M, int K, const uint16_t* Wp, int N,
+                     const float* bias, int act, float* Y, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Dropout. Replaces: the Bernoulli draws of torch's dropout on the hot path — nn.Dropout between
@@ -739,6 +744,10 @@ int lgnn_dropout_masks(int num_masks, float* const* out, const int64_t* numel,
                        const uint32_t* thr, const float* scale, uint64_t* state, int advance,
                        void* stream);
 int lgnn_mask_mul(const float* x, const float* mask, float* y, int64_t n, void* stream);
+/* lgnn_act_bwd (ABI v37): dZ = dY * act'(H) elementwise from the activation's saved output H
+ * (act = LGNN_ACT_ELU: 1 where H > 0, H + 1 elsewhere — F.elu's autograd, reference gin.py:31);
+ * n floats, 16-B aligned; dZ may alias dY */
+int lgnn_act_bwd(const float* dY, const float* H, float* dZ, int64_t n, int act, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Sort pooling (DGCNN). Replaces: PyG 2.5.1 SortAggregation(k) as DRGNet applies it to the

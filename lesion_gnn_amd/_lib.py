@@ -151,10 +151,12 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_s3_weight_planes": (I32, [P, I32, I32, I32, I32, P, P]),
     "lgnn_s3_weight_planes_multi": (I32, [I32, P, P, P, P, I32, P, P]),
     "lgnn_s3_gemm_att": (I32, [P, I64, I32, P, I32, I32, P, P, P, I32, I32, P, P, P]),
+    "lgnn_s3_gemm_act": (I32, [P, I64, I32, P, I32, P, I32, P, P]),
     "lgnn_s3_gemm": (I32, [P, I64, I32, P, I32, I32, P, P, P, P]),
     "lgnn_s3_wgrad_partials": (I32, [I64, I32, I32]),
     "lgnn_s3_wgrad": (I32, [P, I32, P, I64, I32, I32, P, I32, P, P]),
     "lgnn_mask_mul": (I32, [P, P, P, I64, P]),
+    "lgnn_act_bwd": (I32, [P, P, P, I64, I32, P]),
     "lgnn_sort_pool_workspace_bytes": (SZ, []),
     "lgnn_sort_pool_fwd": (I32, [P, I64, I32, P, I64, I32, P, P, P, P, SZ, P]),
     "lgnn_sort_pool_bwd": (I32, [P, P, P, P, P, I64, I32, I32, P, P]),
@@ -162,7 +164,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 36
+ABI_VERSION = 37
 
 _lib = None
 

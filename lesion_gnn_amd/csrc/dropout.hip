@@ -95,7 +95,37 @@ __global__ __launch_bounds__(kT) void k_mask_mul(const float* __restrict__ x,
   }
 }
 
+// dZ = dY * act'(H) from the activation's saved output (ELU: 1 above 0, H + 1 below)
+__global__ __launch_bounds__(kT) void k_act_bwd(const float* __restrict__ dy,
+                                                const float* __restrict__ h,
+                                                float* __restrict__ dz, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * kT * 4;
+  for (int64_t i = ((int64_t)blockIdx.x * kT + threadIdx.x) * 4; i < n; i += stride) {
+    if (i + 4 <= n) {
+      const f32x4 g = ld4(dy + i), hv = ld4(h + i);
+      f32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = g[j] * elu_grad_from_out(hv[j]);
+      st4(dz + i, o);
+    } else {
+      for (int64_t k = i; k < n; ++k) dz[k] = dy[k] * elu_grad_from_out(h[k]);
+    }
+  }
+}
+
 }  // namespace
+
+extern "C" int lgnn_act_bwd(const float* dy, const float* h, float* dz, int64_t n, int act,
+                            void* stream) {
+  if (n < 0 || act != LGNN_ACT_ELU || (n > 0 && (!dy || !h || !dz))) return LGNN_EINVAL;
+  if (((uintptr_t)dy | (uintptr_t)h | (uintptr_t)dz) % 16) return LGNN_EINVAL;
+  if (n == 0) return LGNN_OK;
+  int64_t nb = (n + 4 * kT - 1) / (4 * kT);
+  if (nb > 4096) nb = 4096;
+  hipLaunchKernelGGL(k_act_bwd, dim3((unsigned)nb), dim3(kT), 0, as_stream(stream), dy, h, dz, n);
+  LGNN_LAUNCH_CHECK();
+  return LGNN_OK;
+}
 
 extern "C" int lgnn_dropout_masks(int num_masks, float* const* out, const int64_t* numel,
                                   const uint32_t* thr, const float* scale, uint64_t* state,

@@ -155,7 +155,7 @@ constexpr int YLD = 128 + 4;  // LDS row stride of the staged Y tile (floats)
 
 // One tile of 32 MT rows (MT = 2: the 64-row tile; MT = 1: the 32-row tiles that finish a grid
 // whose 64-row tiles would leave a mostly idle last round)
-template <int PLANES, bool VEC, int NCK, bool ATT, int MT>
+template <int PLANES, bool VEC, int NCK, bool ATT, int MT, int ACT = LGNN_ACT_NONE>
 __device__ __forceinline__ void gemm_tile(unsigned char (&img)[2][PLANES * IMG], int64_t r0,
                                           const float* __restrict__ A, int64_t M, int K,
                                           const uint16_t* __restrict__ Wp, int Kp,
@@ -252,7 +252,8 @@ __device__ __forceinline__ void gemm_tile(unsigned char (&img)[2][PLANES * IMG],
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int m = 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float v = acc[q][r] + bv;
+      float v = acc[q][r] + bv;
+      if constexpr (ACT == LGNN_ACT_ELU) v = elu_f(v);
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), bY, (m * N + ncol) * 4, 0, 0);
     }
   if constexpr (ATT) {
@@ -302,7 +303,7 @@ __device__ __forceinline__ void gemm_tile(unsigned char (&img)[2][PLANES * IMG],
 // launch's last round would hold a few of them on an otherwise idle chip; the host keeps whole
 // rounds of 64-row tiles and cuts the rest in halves (lgnn_s3_gemm: the reference in_proj at
 // 42,279 rows is 661 tiles over 512 slots).
-template <int PLANES, bool VEC, int NCK, bool ATT = false>
+template <int PLANES, bool VEC, int NCK, bool ATT = false, int ACT = LGNN_ACT_NONE>
 __global__ __launch_bounds__(NT, 2) void k_s3_gemm(const float* __restrict__ A, int64_t M, int K,
                                                    const uint16_t* __restrict__ Wp, int Kp,
                                                    const float* __restrict__ bias, int N,
@@ -314,10 +315,11 @@ __global__ __launch_bounds__(NT, 2) void k_s3_gemm(const float* __restrict__ A, 
   if (b < n64) {
     const int64_t q = n64 / 8, r = n64 % 8, xcd = b % 8;
     const int64_t t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
-    gemm_tile<PLANES, VEC, NCK, ATT, 2>(img, t * TM, A, M, K, Wp, Kp, bias, N, Y, colsum, att);
+    gemm_tile<PLANES, VEC, NCK, ATT, 2, ACT>(img, t * TM, A, M, K, Wp, Kp, bias, N, Y, colsum,
+                                             att);
   } else {
-    gemm_tile<PLANES, VEC, NCK, ATT, 1>(img, (int64_t)n64 * TM + (b - n64) * 32, A, M, K, Wp, Kp,
-                                        bias, N, Y, nullptr, att);
+    gemm_tile<PLANES, VEC, NCK, ATT, 1, ACT>(img, (int64_t)n64 * TM + (b - n64) * 32, A, M, K, Wp,
+                                             Kp, bias, N, Y, nullptr, att);
   }
 }
 
@@ -646,6 +648,39 @@ extern "C" int lgnn_s3_gemm(const float* A, int64_t M, int K, const uint16_t* Wp
   }
 #undef LGNN_S3G_N
 #undef LGNN_S3G
+  LGNN_LAUNCH_CHECK();
+  return LGNN_OK;
+}
+
+// Y = act(A B^T + b) (act = LGNN_ACT_ELU: torch's ELU in the epilogue, as the tile kernels)
+extern "C" int lgnn_s3_gemm_act(const float* A, int64_t M, int K, const uint16_t* Wp, int N,
+                                const float* bias, int act, float* Y, void* stream) {
+  if (act == LGNN_ACT_NONE) return lgnn_s3_gemm(A, M, K, Wp, N, 3, bias, Y, nullptr, stream);
+  if (act != LGNN_ACT_ELU || M < 0 || K < 1 || N < 1 || !Wp || !Y) return LGNN_EINVAL;
+  if (M > 0 && !A) return LGNN_EINVAL;
+  const int Kp = (K + BK - 1) / BK * BK;
+  if ((M + TM) * (int64_t)K * 4 >= ((int64_t)1 << 31) || M * (int64_t)N * 4 >= ((int64_t)1 << 30) ||
+      (int64_t)3 * 128 * Kp * 2 >= ((int64_t)1 << 31))
+    return LGNN_EINVAL;
+  if (M == 0) return LGNN_OK;
+  int n64 = 0;
+  const unsigned gx = s3g_grid(M, K, (N + 127) / 128, false, &n64);
+  const dim3 grid(gx, (unsigned)((N + 127) / 128)), block(NT);
+  hipStream_t s = as_stream(stream);
+  const bool v = K % 4 == 0;
+  const int nck = Kp / BK;
+#define LGNN_S3E(V, NC)                                                                          \
+  hipLaunchKernelGGL((k_s3_gemm<3, V, NC, false, LGNN_ACT_ELU>), grid, block, 0, s, A, M, K, Wp, \
+                     Kp, bias, N, Y, nullptr, n64)
+#define LGNN_S3E_N(V)                  \
+  switch (nck) {                       \
+    case 2: LGNN_S3E(V, 2); break;     \
+    case 8: LGNN_S3E(V, 8); break;     \
+    default: LGNN_S3E(V, 0); break;    \
+  }
+  if (v) { LGNN_S3E_N(true) } else { LGNN_S3E_N(false) }
+#undef LGNN_S3E_N
+#undef LGNN_S3E
   LGNN_LAUNCH_CHECK();
   return LGNN_OK;
 }

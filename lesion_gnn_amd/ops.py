@@ -52,11 +52,31 @@ def fast_shape(K: int, N: int) -> bool:
     return K <= 128 and N <= 128 and K % 4 == 0 and N % 4 == 0
 
 
+# Wide linears (K or N > 128: the reference sweep's widths 256 / 512, scripts/sweep.py:126) run as
+# the aggregation (lgnn_spmm) + the split-3 dense GEMMs (s3gemm.hip) instead of the fp32 generic
+# node kernels, which stream the weight per 128-wide block and re-derive dZ per output block
+# (GIN [512]*4: dX 1.4 ms per launch). LGNN_WIDE=f32 keeps the generic kernels (A/B).
+WIDE = os.environ.get("LGNN_WIDE", "s3")
+
+
+def wide_shape(K: int, N: int) -> bool:
+    return WIDE == "s3" and (K > 128 or N > 128) and K % 4 == 0 and N % 4 == 0
+
+
 def linear_fwd(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None, act: int,
                csr: Csr | None = None, self_scale: float = 0.0, save_s: bool = False):
-    """Y = act(P(x) W^T + b). With save_s (aggregating fast-path shapes) also returns S = P(x)."""
+    """Y = act(P(x) W^T + b). With save_s (aggregating fast-path and wide shapes) also returns
+    S = P(x)."""
     M, K = x.shape
     N = W.size(0)
+    if wide_shape(K, N):
+        S = spmm_raw(csr.rowptr, csr.col, csr.w, self_scale, x) if csr is not None else x
+        Wp = dense_planes(W, False, False)
+        y = torch.empty(M, N, dtype=torch.float32, device=x.device)
+        for r0, r1 in _row_blocks(M, K, N):
+            _lib.call("lgnn_s3_gemm_act", _lib.ptr(S) + r0 * K * 4, r1 - r0, K, _lib.ptr(Wp), N,
+                      _lib.ptr(b), act, _lib.ptr(y) + r0 * N * 4, _s(x.device))
+        return (y, S) if save_s else y
     y = torch.empty(M, N, dtype=torch.float32, device=x.device)
     s_out = torch.empty(M, K, dtype=torch.float32, device=x.device) if save_s else None
     _lib.call("lgnn_node_linear_fwd", _lib.ptr(x), M, K,
@@ -432,6 +452,25 @@ def linear_bwd(grad_mode: int, dY: torch.Tensor, *, H: torch.Tensor | None, act:
     M, K = X.shape
     N = W.size(0)
     dev = X.device
+    if wide_shape(K, N):
+        # the output gradient as given, from the pooled gradient, or gathered through the
+        # transpose CSR; dZ = g * act'(H); then dXpre = dZ W and (dW, db) = (dZ^T S, sum dZ)
+        if grad_mode == _lib.LGNN_GRAD_POOL:
+            g = pool_bwd(_f32c(dY), graph, pool_mean, M)
+        elif grad_mode == _lib.LGNN_GRAD_TRANSPOSE:
+            g = spmm_raw(tcsr.tptr, tcsr.tidx, tcsr.tw, tself, dY)
+        else:
+            g = _f32c(dY)
+        if act == _lib.LGNN_ACT_ELU:
+            dZ = torch.empty_like(g)
+            _lib.call("lgnn_act_bwd", _lib.ptr(g), _lib.ptr(H), _lib.ptr(dZ), g.numel(), act,
+                      _s(dev))
+        else:
+            dZ = g
+        S = spmm_raw(csr.rowptr, csr.col, csr.w, self_scale, X) if csr is not None else X
+        dX = dense_mm(dZ, dense_planes(W, True, False), K, None, False) if want_dx else None
+        dW, db = dense_wgrad(dZ, S, False, want_db=want_db, reducer=reducer)
+        return dX, dW, db
     P = num_partials(M, N, K, csr is not None)
     slab = torch.empty(P * N * K + (P * N if want_db else 0), dtype=torch.float32, device=dev)
     dWp = slab[: P * N * K]
@@ -1037,7 +1076,7 @@ class _GCNStack(torch.autograd.Function):
             ctx.saved_s = []
             for l in range(L):
                 W, b = params[2 + 2 * l], params[3 + 2 * l]
-                fast = fast_shape(W.size(1), W.size(0))
+                fast = fast_shape(W.size(1), W.size(0)) or wide_shape(W.size(1), W.size(0))
                 if fast:
                     h, s_ = linear_fwd(hs[-1], W, b, _lib.LGNN_ACT_ELU, csr, save_s=True)
                 else:
@@ -1343,7 +1382,7 @@ class _GINConv(torch.autograd.Function):
                                                training, mask, act, group, sync_count, gamma)
             ctx.save_for_backward(*saved)
             return H
-        if fast:
+        if fast or wide_shape(W1.size(1), N1):
             Z1, S = linear_fwd(x, W1, b1, _lib.LGNN_ACT_NONE, csr, self_scale, save_s=True)
         else:
             Z1, S = linear_fwd(x, W1, b1, _lib.LGNN_ACT_NONE, csr, self_scale), None
