@@ -585,16 +585,13 @@ extern "C" int lgnn_s3_weight_planes(const float* W, int rows, int cols, int tra
 // Row tiling of k_s3_gemm: whole rounds of 64-row tiles over the resident slots (2 workgroups per
 // CU, divided among the column blocks), the rest as 32-row tiles — for long K only (the in_proj,
 // K = 1025: 75.3 -> 73.5 us; at K = 128 the halves lost more per tile than the round saved);
-// only 64-row tiles when the caller wants per-64-row column sums or LGNN_S3G_HALF=0. Returns
-// grid.x, sets *n64.
+// only 64-row tiles when the caller wants per-64-row column sums. Returns grid.x, sets *n64.
 static unsigned s3g_grid(int64_t M, int K, int nblk, bool colsum, int* n64) {
   const int64_t t64 = (M + TM - 1) / TM;
   static int slots = -1;
   if (slots < 0) {
     int dev = 0, cus = 0;
-    const char* e = getenv("LGNN_S3G_HALF");
-    if (e && e[0] == '0') slots = 0;
-    else if (hipGetDevice(&dev) == hipSuccess &&
+    if (hipGetDevice(&dev) == hipSuccess &&
              hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
       slots = 2 * cus;
     else slots = 0;
@@ -626,8 +623,7 @@ extern "C" int lgnn_s3_gemm(const float* A, int64_t M, int K, const uint16_t* Wp
   const dim3 grid(gx, (unsigned)((N + 127) / 128)), block(NT);
   hipStream_t s = as_stream(stream);
   const bool v = K % 4 == 0;
-  const char* loop = getenv("LGNN_S3G_LOOP");  // tuning knob: 1 = the pair loop at every K
-  const int nck = loop && loop[0] == '1' ? -1 : Kp / BK;
+  const int nck = Kp / BK;
 #define LGNN_S3G(P, V, NC) \
   hipLaunchKernelGGL((k_s3_gemm<P, V, NC>), grid, block, 0, s, A, M, K, Wp, Kp, bias, N, Y, \
                      colsum_part, n64)
@@ -720,18 +716,12 @@ extern "C" int lgnn_s3_gemm_att(const float* A, int64_t M, int K, const uint16_t
 
 // k_s3_wgrad2: 32-row chunks per split, so that the grid (128-wide k-blocks x splits x n-blocks)
 // holds about two workgroups per CU (512), at least 4 chunks per split
-// (tuning knobs: LGNN_S3_WG_TARGET workgroups, LGNN_S3_WG_MINCPS chunks per split)
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  const int v = e ? atoi(e) : 0;
-  return v > 0 ? v : dflt;
-}
 static int s3_wg_cps(int64_t M, int K, int N) {
   const int64_t nch = std::max<int64_t>((M + W2M - 1) / W2M, 1);
   const int64_t work = (int64_t)((K + 127) / 128) * ((N + 127) / 128);
-  int64_t splits = std::max<int64_t>(env_int("LGNN_S3_WG_TARGET", 512) / work, 1);
+  int64_t splits = std::max<int64_t>(512 / work, 1);
   int64_t cps = (nch + splits - 1) / splits;
-  const int mincps = env_int("LGNN_S3_WG_MINCPS", 4);
+  const int mincps = 4;
   if (cps < mincps) cps = mincps;
   return (int)cps;
 }

@@ -662,14 +662,9 @@ bool lgnn_tile_fits(int64_t M, int K, int N) {
          (M + TM) * (int64_t)(K > N ? K : N) * 4 < (int64_t)INT32_MAX;
 }
 
-// Workgroups of the backward kernels = dW partial slots (persistent over the tiles). Tuning knob
-// LGNN_BWD_WGS (read once; default 512 = 2 per CU).
+// Workgroups of the backward kernels = dW partial slots (persistent over the tiles): 512 = 2 per CU.
 int lgnn_tile_partials(int64_t M) {
-  static const int64_t cap = [] {
-    const char* e = getenv("LGNN_BWD_WGS");
-    const long v = e ? atol(e) : 0;
-    return (int64_t)(v > 0 ? v : 512);
-  }();
+  const int64_t cap = 512;
   const int64_t ntiles = (M + TM - 1) / TM;
   const int64_t p = ntiles < cap ? ntiles : cap;
   return (int)(p < 1 ? 1 : p);
