@@ -198,7 +198,13 @@ __device__ __forceinline__ void gemm_tile(unsigned char (&img)[2][PLANES * IMG],
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int t = 0; t < MT; ++t) acc[t] = mma<PLANES>(a[s & 1][t], bc[s], acc[t]);
+      for (int t = 0; t < MT; ++t) {
+#if defined(LGNN_ABL_S3G) && (LGNN_ABL_S3G & 1)  // timing ablation: no MFMA (operands kept live)
+        acc[t][0] += __uint_as_float(a[s & 1][t][0][0] ^ bc[s][0][0]);
+#else
+        acc[t] = mma<PLANES>(a[s & 1][t], bc[s], acc[t]);
+#endif
+      }
       if (store_next && s < RA) store_a_row<PLANES>(imn, Rn, rq, kq, s);
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -217,7 +223,9 @@ __device__ __forceinline__ void gemm_tile(unsigned char (&img)[2][PLANES * IMG],
   auto step = [&](int c, ARegs<MT>& Rn, u32x4 (&bc)[4][PLANES], bool store_next) {
     chunk(img[c & 1], bc, img[(c + 1) & 1], Rn, store_next);
     load_a<VEC>(Rn, bA, K, c + 3, rq, kq);
+#if !(defined(LGNN_ABL_S3G) && (LGNN_ABL_S3G & 2))  // timing ablation: no B loads in the loop
     load_b<PLANES>(bc, bW, pstride, wlane, c + 2);
+#endif
     lds_barrier();  // image c + 1 complete, image c's reads done
   };
   if constexpr (NCK > 0) {
@@ -331,7 +339,9 @@ __global__ __launch_bounds__(NT, 2) void k_s3_gemm(const float* __restrict__ A, 
 // rows: the transposed images dY^T [128 n][32 m] and X^T [128 k][32 m] x 3 planes are 48 KiB
 // (single buffer, two workgroups per CU), the next chunk's rows in registers during the MFMAs.
 // Image rows are 64 B (4 chunks of 16 B), chunk-swizzled by (row >> 2) & 3: a 16-lane b128 read
-// group of consecutive rows touches 64 distinct banks.
+// group of consecutive rows touches 64 distinct banks. (The transposed ds_write_b64 groups are
+// 2-way: rows j and j + 4 share a 16-bank quarter. 64 B of padding per 4 rows removes that, and
+// measured no faster: 229 vs 232 us at 65,536 x 512 x 512, equal at the in_proj.)
 // ------------------------------------------------------------------------------------------
 constexpr int W2M = 32;               // rows per chunk
 constexpr int W2ROW = W2M * 2;        // bytes per image row (bf16)
@@ -350,13 +360,11 @@ struct W2Regs {
 };
 
 __device__ __forceinline__ u32x4 ld16(Buf b, int off, int col, int ncol) {
-  // a 4-column group inside the columns [0, ncol): one 16-B load; at or past it: 0 (OOB offset);
-  // straddling it (ncol % 4 != 0): the columns past it zeroed after the load
-  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(b, opaque(col < ncol ? off : OOB), 0, 0);
-  u32x4 r;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) r[j] = col + j < ncol ? v[j] : 0u;
-  return r;
+  // a 4-column group inside the columns [0, ncol): one 16-B load; at or past it: 0 (OOB offset).
+  // Straddling it (ncol % 4 != 0) the columns past it are zeroed by w2_mask when the registers
+  // are consumed, not here: a select right after the load makes the compiler wait for the load
+  // in the middle of the MFMA phase it is meant to overlap
+  return __builtin_amdgcn_raw_buffer_load_b128(b, opaque(col < ncol ? off : OOB), 0, 0);
 }
 
 __device__ __forceinline__ void w2_load(W2Regs& R, Buf bY, Buf bX, int N, int K, int m0, int n0,
@@ -369,6 +377,18 @@ __device__ __forceinline__ void w2_load(W2Regs& R, Buf bY, Buf bX, int N, int K,
     R.y[i] = ld16(bY, (m * N + n) * 4, n, N);
     R.x[i] = ld16(bX, (m * K + k) * 4, k, K);
   }
+}
+
+// the straddling group's columns >= N (dY) / >= K (X) -> 0 (no-op unless N or K % 4 != 0)
+__device__ __forceinline__ void w2_mask(W2Regs& R, int N, int K, int n0, int k0, int tid) {
+  const int cq = tid >> 3, n = n0 + 4 * cq, k = k0 + 4 * cq;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      R.y[i][j] = n + j < N ? R.y[i][j] : 0u;
+      R.x[i][j] = k + j < K ? R.x[i][j] : 0u;
+    }
 }
 
 // transposed write of one operand: column c (4 cq + j) gets rows 4 rq .. + 3 as 8 B per plane
@@ -420,13 +440,16 @@ __global__ __launch_bounds__(NT, 2) void k_s3_wgrad2(const float* __restrict__ d
   w2_load(R, bY, bX, N, K, (int)(c0 * W2M), n0, k0, tid);
   for (int64_t c = c0; c < cend; ++c) {
     lds_barrier();  // the previous chunk's image reads are done
+    if ((N | K) & 3) w2_mask(R, N, K, n0, k0, tid);  // uniform: only a width % 4 != 0 straddles
     w2_store1<PLANES>(iy, R.y, tid);
     w2_store1<PLANES>(ix, R.x, tid);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) cs[j] += __uint_as_float(R.y[i][j]);
+#if !(defined(LGNN_ABL_S3G) && (LGNN_ABL_S3G & 2))  // timing ablation: no global loads in the loop
     w2_load(R, bY, bX, N, K, (int)((c + 1) * W2M), n0, k0, tid);
+#endif
     lds_barrier();  // images complete (the next chunk's loads stay in flight)
 #pragma unroll
     for (int st = 0; st < 2; ++st) {  // two k-steps of 16 rows
@@ -441,7 +464,13 @@ __global__ __launch_bounds__(NT, 2) void k_s3_wgrad2(const float* __restrict__ d
 #pragma unroll
       for (int qa = 0; qa < 2; ++qa)
 #pragma unroll
-        for (int qb = 0; qb < 2; ++qb) acc[qa][qb] = mma<PLANES>(a[qa], b[qb], acc[qa][qb]);
+        for (int qb = 0; qb < 2; ++qb) {
+#if defined(LGNN_ABL_S3G) && (LGNN_ABL_S3G & 1)
+          acc[qa][qb][0] += __uint_as_float(a[qa][0][0] ^ b[qb][0][0]);
+#else
+          acc[qa][qb] = mma<PLANES>(a[qa], b[qb], acc[qa][qb]);
+#endif
+        }
     }
   }
   // slab s: rows n = n0 + 64 wn + 32 qa + (r & 3) + 8 (r >> 2) + 4 h, columns k0 + 64 wk + 32 qb + li

@@ -73,17 +73,7 @@ __global__ __launch_bounds__(NT, 2) void k_bwd(
 __device__ __forceinline__ void load_bfrag(float (&bf)[64], const float* __restrict__ W, int N,
                                            int K) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int h = lane >> 5, li = lane & 31;
-  const int n = wave * 32 + li;
-  const int ncl = n < N ? n : N - 1;
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int k = 64 * h + 4 * q;
-    const f32x4 v = ld4(W + (int64_t)ncl * K + (k < K ? k : K - 4));
-    const bool ok = n < N && k < K;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bf[4 * q + j] = ok ? v[j] : 0.f;
-  }
+  load_wfrag(bf, W, N, K, wave * 32 + (lane & 31), lane >> 5);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -124,14 +124,7 @@ __device__ __forceinline__ void fwd_tiles(float* A, float* S, TileIdx& ti,
     bsh = ld4(bn.shift + kq);
   }
   float bf[64];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int k = 64 * h + 4 * q;
-    const f32x4 v = ld4(W + (int64_t)ncl * K + (k < K ? k : K - 4));
-    const bool ok = n < N && k < K;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bf[4 * q + j] = ok ? v[j] : 0.f;
-  }
+  load_wfrag(bf, W, N, K, n, h);
   const float bias = b ? b[ncl] : 0.f;
   const int kc = 4 * li < K ? 4 * li : K - 4;
   const Buf bX = mkbuf(X, M * K * 4), bY = mkbuf(Y, M * N * 4);

@@ -87,6 +87,22 @@ __device__ __forceinline__ void bst4(Buf r, int off, f32x4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
 }
 
+// A wave's weight fragment for the fp32 MFMA (lane (h, li) of wave w: row n = 32 w + li of W
+// [N][K], columns 64 h .. + 63): rows past N and columns past K read 0 through an out-of-range
+// buffer offset (K % 4 == 0), so no select consumes the loaded values here — a select right after
+// the loads made the compiler wait for them on the spot instead of at the first MFMA
+__device__ __forceinline__ void load_wfrag(float (&bf)[64], const float* __restrict__ W, int N,
+                                           int K, int n, int h) {
+  const Buf bW = mkbuf(W, (int64_t)N * K * 4);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int k = 64 * h + 4 * q;
+    const f32x4 v = bld4(bW, (n < N && k < K) ? (n * K + k) * 4 : 0x7ff00000);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[4 * q + j] = v[j];
+  }
+}
+
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 __device__ __forceinline__ f32x4 sel4(bool c, f32x4 v) { return c ? v : zero4(); }
 
