@@ -6,6 +6,6 @@ mkdir -p gpurun_out/micro
 for v in intree $(cd tools/_abl && ls liblgnn_v_*.so 2>/dev/null); do
   if [ $v = intree ]; then LP=""; else LP=$GRAFT_REPO_ROOT/tools/_abl/$v; fi
   echo "== $v"
-  PYTHONPATH=$GRAFT_REPO_ROOT LGNN_LIB_PATH=$LP timeout -k 10 120 python tools/s3_micro.py --wide 2>&1 | grep -v amdgpu.ids
+  PYTHONPATH=$GRAFT_REPO_ROOT LGNN_LIB_PATH=$LP timeout -k 10 120 python tools/s3_micro.py ${MICRO_ARGS:---wide} 2>&1 | grep -v amdgpu.ids
 done > gpurun_out/micro/$1.txt 2>&1
 cat gpurun_out/micro/$1.txt

@@ -25,6 +25,8 @@ dev = torch.device("cuda:0")
 SHAPES = [(42279, 1025, 128)] if "--inproj" in sys.argv else [(42279, 1025, 128), (42279, 128, 128)]
 if "--kalign" in sys.argv:  # the in_proj at 16-B aligned row strides (1024, 1028) vs 1025
     SHAPES = [(42279, 1024, 128), (42279, 1025, 128), (42279, 1028, 128)]
+if "--lin" in sys.argv:  # the reference GATConv.lin shape alone (42,279 x 128 -> 128)
+    SHAPES = [(42279, 128, 128)]
 if "--wide" in sys.argv:  # the sweep's GIN [512]*4 linears (scripts/sweep.py:126)
     SHAPES += [(65536, 512, 512), (65536, 128, 512)]
 for M, K, N in SHAPES:
