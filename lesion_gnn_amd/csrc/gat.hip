@@ -119,6 +119,7 @@ struct Pass {
   int fc[NS];    // clamped feature (loads stay in bounds)
   int head, G;
   bool leader;
+  Pass() = default;
   __device__ __forceinline__ Pass(int p, int li, int HC, int C) {
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
@@ -991,17 +992,424 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_node_p(
   }
 }
 
+// Two-strip form (k_gat_fwd_ps<…, 2>, 128 < H*C <= 256): NST strips of 128 features per row
+// (H*C <= 128 NST, C <= 128; with NST > 1, C >= 32, so a
+// strip's heads, 128 / C of them, fit the 4 head slots of the edge lanes). Every row's loads of
+// all strips are issued together; each strip's softmax and messages are then those of the
+// single-strip kernel for the strip's heads (bitwise k_gat_fwd's per-head values). The
+// one-strip shapes keep k_gat_fwd_p: this form at NST = 1 compiled 1.5 us slower per launch.
+template <int ACT, int NST>
+__global__ __launch_bounds__(NT) void k_gat_fwd_ps(const int32_t* __restrict__ rowptr,
+                                                  const int32_t* __restrict__ col,
+                                                  const float* __restrict__ XP,
+                                                  const float* __restrict__ a_s,
+                                                  const float* __restrict__ a_d, int64_t M, int H,
+                                                  int C, float slope,
+                                                  const float* __restrict__ mask,
+                                                  const float* __restrict__ bias,
+                                                  float* __restrict__ alpha, float* __restrict__ Y,
+                                                  uint16_t* __restrict__ Yb) {
+  const EdgeLane L(H);
+  const int HC = H * C;
+  const int hps = 128 / C < H ? 128 / C : H;  // heads per strip
+  RowWalk W = row_walk(M);
+  if (W.r >= W.rend) return;
+  // per strip: the feature lane's pass, its head's edge lanes, and this edge lane's head
+  Pass<1> P[NST];
+  int hbase[NST], hq[NST];
+  bool hv[NST];
+#pragma unroll
+  for (int st = 0; st < NST; ++st) {
+    P[st] = Pass<1>(st, L.li, HC, C);
+    hbase[st] = L.hwb + 8 * (P[st].head - st * hps);
+    const int he = st * hps + L.hh;
+    hv[st] = L.hh < hps && he < H;
+    hq[st] = hv[st] ? he : 0;
+  }
+  const int64_t cap = rowptr[M];
+  const Buf bR = mkbuf(rowptr, (M + 1) * 4), bC = mkbuf(col, cap * 4);
+  const Buf bX = mkbuf(XP, M * HC * 4), bA = mkbuf(a_s, M * H * 4), bD = mkbuf(a_d, M * H * 4);
+  const Buf bAl = mkbuf(alpha, alpha ? cap * H * 4 : 0), bM = mkbuf(mask, mask ? cap * H * 4 : 0);
+  int64_t r = W.r;
+  int e0 = bldi(bR, (uint32_t)r * 4u), e1 = bldi(bR, (uint32_t)r * 4u + 4u);
+  int cu = bldi(bC, (uint32_t)L.pos(e0, e1) * 4u);
+  int64_t rn = r + W.step;
+  uint32_t ro = rn < W.rend ? (uint32_t)rn * 4u : OOB;
+  int e0n = bldi(bR, ro), e1n = bldi(bR, ro + 4u);
+  for (;;) {
+    const int deg = e1 - e0;
+    // row r: edge lanes load the logit inputs, feature lanes gather the first batch's rows
+    const int eu = L.pos(e0, e1);
+    float a[NST], ad[NST], mk[NST];
+    f32x4 xv[NST][EB];
+#pragma unroll
+    for (int st = 0; st < NST; ++st) {
+      a[st] = bld1(bA, (uint32_t)(cu * H + hq[st]) * 4u);
+      ad[st] = bld1(bD, (uint32_t)(r * H + hq[st]) * 4u);
+      mk[st] = mask ? bld1(bM, (uint32_t)(eu * H + hq[st]) * 4u) : 1.f;
+#pragma unroll
+      for (int k = 0; k < EB; ++k)
+        xv[st][k] = bld4(bX, ((uint32_t)bperm_i(cu, L.hwb + k) * HC + P[st].fc[0]) * 4u);
+    }
+    // row r + step: its first batch's columns; row r + 2 step: its extent
+    const int64_t rnn = rn + W.step;
+    const int cun = bldi(bC, rn < W.rend ? (uint32_t)L.pos(e0n, e1n) * 4u : OOB);
+    const uint32_t ron = rnn < W.rend ? (uint32_t)rnn * 4u : OOB;
+    const int e0nn = bldi(bR, ron), e1nn = bldi(bR, ron + 4u);
+#pragma unroll
+    for (int st = 0; st < NST; ++st) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      if (deg <= EB) {
+        const bool ev = L.u < deg && hv[st];
+        const float lg = leaky(a[st] + ad[st], slope);
+        const float m = max8(ev ? lg : -INFINITY);
+        const float ex = ev ? expf(lg - m) : 0.f;
+        float sum = 0.f;  // in CSR order (the zeros of absent edges add exactly nothing)
+#pragma unroll
+        for (int k = 0; k < EB; ++k) sum += bperm_f(ex, L.hwb + 8 * L.hh + k);
+        sum += EPS16;
+        const float al = ex / sum;
+        if (alpha && ev) bst1(bAl, (uint32_t)(eu * H + hq[st]) * 4u, al);
+        const float alm = mask ? al * mk[st] : al;
+#pragma unroll
+        for (int k = 0; k < EB; ++k) {
+          const float w = bperm_f(alm, hbase[st] + k);
+          if (k < deg) acc += w * xv[st][k];
+        }
+      } else {  // long row: max, denominator, messages, each a walk over batches of EB entries
+        float m = -INFINITY;
+        for (int b = e0; b < e1; b += EB) {
+          const int c = bldi(bC, (uint32_t)L.pos(b, e1) * 4u);
+          const float lg = leaky(bld1(bA, (uint32_t)(c * H + hq[st]) * 4u) + ad[st], slope);
+          if (b + L.u < e1 && hv[st]) m = fmaxf(m, lg);
+        }
+        m = max8(m);
+        float sum = 0.f;
+        for (int b = e0; b < e1; b += EB) {
+          const int c = bldi(bC, (uint32_t)L.pos(b, e1) * 4u);
+          const float lg = leaky(bld1(bA, (uint32_t)(c * H + hq[st]) * 4u) + ad[st], slope);
+          const float ex = b + L.u < e1 && hv[st] ? expf(lg - m) : 0.f;
+#pragma unroll
+          for (int k = 0; k < EB; ++k) sum += bperm_f(ex, L.hwb + 8 * L.hh + k);
+        }
+        sum += EPS16;
+        for (int b = e0; b < e1; b += EB) {
+          const int eb = L.pos(b, e1);
+          const bool ev = b + L.u < e1 && hv[st];
+          const int c = bldi(bC, (uint32_t)eb * 4u);
+          const float lg = leaky(bld1(bA, (uint32_t)(c * H + hq[st]) * 4u) + ad[st], slope);
+          const float mb = mask ? bld1(bM, (uint32_t)(eb * H + hq[st]) * 4u) : 1.f;
+          f32x4 xb[EB];
+#pragma unroll
+          for (int k = 0; k < EB; ++k)
+            xb[k] = bld4(bX, ((uint32_t)bperm_i(c, L.hwb + k) * HC + P[st].fc[0]) * 4u);
+          const float al = (ev ? expf(lg - m) : 0.f) / sum;
+          if (alpha && ev) bst1(bAl, (uint32_t)(eb * H + hq[st]) * 4u, al);
+          const float alm = mask ? al * mb : al;
+#pragma unroll
+          for (int k = 0; k < EB; ++k) {
+            const float w = bperm_f(alm, hbase[st] + k);
+            if (b + k < e1) acc += w * xb[k];
+          }
+        }
+      }
+      const f32x4 out[1] = {acc};
+      gat_out<ACT, 1>(P[st], out, bias, Y, Yb, r * HC);
+    }
+    if (rn >= W.rend) break;
+    r = rn;
+    rn = rnn;
+    e0 = e0n;
+    e1 = e1n;
+    cu = cun;
+    e0n = e0nn;
+    e1n = e1nn;
+  }
+}
+
+// NST strips as in k_gat_fwd_ps (two-strip shapes only, as there): the row's loads of every strip issued together, then each
+// strip's logit gradients for its heads.
+template <int ACT, bool POOL, int NST>
+__global__ __launch_bounds__(NT) void k_gat_bwd_edge_ps(
+    const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+    const float* __restrict__ XP, const float* __restrict__ a_s, const float* __restrict__ a_d,
+    const float* __restrict__ alpha, const float* __restrict__ mask, const float* __restrict__ dY,
+    const float* __restrict__ Y, int64_t M, int H, int C, float slope, float* __restrict__ dZ,
+    float* __restrict__ da_e, float* __restrict__ da_d, PoolGrad pg) {
+  const EdgeLane L(H);
+  const int HC = H * C;
+  const int hps = 128 / C < H ? 128 / C : H;  // heads per strip
+  Pass<1> P[NST];
+  int hbase[NST], hlead[NST], hq[NST];
+  bool hv[NST];
+#pragma unroll
+  for (int st = 0; st < NST; ++st) {
+    P[st] = Pass<1>(st, L.li, HC, C);
+    hbase[st] = L.hwb + 8 * (P[st].head - st * hps);
+    const int he = st * hps + L.hh;
+    hv[st] = L.hh < hps && he < H;
+    hq[st] = hv[st] ? he : st * hps;
+    hlead[st] = L.hwb + (hq[st] - st * hps) * P[st].G;  // the first feature lane of that head
+  }
+  RowWalk W = row_walk(M);
+  if (W.r >= W.rend) return;
+  const int64_t cap = rowptr[M];
+  const Buf bR = mkbuf(rowptr, (M + 1) * 4), bC = mkbuf(col, cap * 4);
+  const Buf bX = mkbuf(XP, M * HC * 4), bA = mkbuf(a_s, M * H * 4), bD = mkbuf(a_d, M * H * 4);
+  const Buf bAl = mkbuf(alpha, cap * H * 4), bM = mkbuf(mask, mask ? cap * H * 4 : 0);
+  const Buf bDa = mkbuf(da_e, cap * H * 4);
+  int64_t r = W.r;
+  int e0 = bldi(bR, (uint32_t)r * 4u), e1 = bldi(bR, (uint32_t)r * 4u + 4u);
+  int cu = bldi(bC, (uint32_t)L.pos(e0, e1) * 4u);
+  int64_t rn = r + W.step;
+  uint32_t ro = rn < W.rend ? (uint32_t)rn * 4u : OOB;
+  int e0n = bldi(bR, ro), e1n = bldi(bR, ro + 4u);
+  for (;;) {
+    const int deg = e1 - e0;
+    const int eu = L.pos(e0, e1);
+    float al[NST], mk[NST], pre[NST];
+    f32x4 xv[NST][EB], dz[NST];
+#pragma unroll
+    for (int st = 0; st < NST; ++st) {
+      al[st] = bld1(bAl, (uint32_t)(eu * H + hq[st]) * 4u);
+      mk[st] = mask ? bld1(bM, (uint32_t)(eu * H + hq[st]) * 4u) : 1.f;
+      pre[st] = bld1(bA, (uint32_t)(cu * H + hq[st]) * 4u) +
+                bld1(bD, (uint32_t)(r * H + hq[st]) * 4u);
+#pragma unroll
+      for (int k = 0; k < EB; ++k)
+        xv[st][k] = bld4(bX, ((uint32_t)bperm_i(cu, L.hwb + k) * HC + P[st].fc[0]) * 4u);
+      dz[st] = dz_row<ACT, POOL>(r, HC, P[st].fc[0], dY, Y, pg);
+    }
+    const int64_t rnn = rn + W.step;
+    const int cun = bldi(bC, rn < W.rend ? (uint32_t)L.pos(e0n, e1n) * 4u : OOB);
+    const uint32_t ron = rnn < W.rend ? (uint32_t)rnn * 4u : OOB;
+    const int e0nn = bldi(bR, ron), e1nn = bldi(bR, ron + 4u);
+#pragma unroll
+    for (int st = 0; st < NST; ++st) {
+      const Pass<1>& Ps = P[st];
+      if (!Ps.act[0]) dz[st] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (Ps.act[0]) st4(dZ + r * HC + Ps.f[0], dz[st]);
+      float dad = 0.f;
+      if (deg <= EB) {
+        float d[EB], alk[EB];
+        float s_i = 0.f;
+#pragma unroll
+        for (int k = 0; k < EB; ++k) {
+          d[k] = group_sum(dot4(dz[st], xv[st][k]), Ps.G);
+          if (mask) d[k] *= bperm_f(mk[st], hbase[st] + k);
+          alk[k] = bperm_f(al[st], hbase[st] + k);
+          if (k < deg) s_i += alk[k] * d[k];
+        }
+        float mine = 0.f;  // edge lane (u, h): the logit gradient of its edge and head
+#pragma unroll
+        for (int k = 0; k < EB; ++k) {
+          const float fk = bperm_f(pre[st] > 0.f ? 1.f : slope, hbase[st] + k);
+          const float da = alk[k] * (d[k] - s_i) * fk;
+          if (k < deg) dad += da;
+          const float t = bperm_f(da, hlead[st]);
+          mine = L.u == k ? t : mine;
+        }
+        if (L.u < deg && hv[st]) bst1(bDa, (uint32_t)(eu * H + hq[st]) * 4u, mine);
+      } else {  // long row: two walks over batches of EB entries (s_i, then the gradients)
+        float s_i = 0.f;
+#pragma unroll 1
+        for (int sweep = 0; sweep < 2; ++sweep) {
+          for (int b = e0; b < e1; b += EB) {
+            const int eb = L.pos(b, e1);
+            const int c = bldi(bC, (uint32_t)eb * 4u);
+            const float alb = bld1(bAl, (uint32_t)(eb * H + hq[st]) * 4u);
+            const float mb = mask ? bld1(bM, (uint32_t)(eb * H + hq[st]) * 4u) : 1.f;
+            const float preb = bld1(bA, (uint32_t)(c * H + hq[st]) * 4u) +
+                               bld1(bD, (uint32_t)(r * H + hq[st]) * 4u);
+            f32x4 xb[EB];
+#pragma unroll
+            for (int k = 0; k < EB; ++k)
+              xb[k] = bld4(bX, ((uint32_t)bperm_i(c, L.hwb + k) * HC + Ps.fc[0]) * 4u);
+            float mine = 0.f;
+#pragma unroll
+            for (int k = 0; k < EB; ++k) {
+              float dk = group_sum(dot4(dz[st], xb[k]), Ps.G);
+              if (mask) dk *= bperm_f(mb, hbase[st] + k);
+              const float ak = bperm_f(alb, hbase[st] + k);
+              const float fk = bperm_f(preb > 0.f ? 1.f : slope, hbase[st] + k);
+              if (sweep == 0) {
+                if (b + k < e1) s_i += ak * dk;
+              } else {
+                const float da = ak * (dk - s_i) * fk;
+                if (b + k < e1) dad += da;
+                const float t = bperm_f(da, hlead[st]);
+                mine = L.u == k ? t : mine;
+              }
+            }
+            if (sweep == 1 && b + L.u < e1 && hv[st])
+              bst1(bDa, (uint32_t)(eb * H + hq[st]) * 4u, mine);
+          }
+        }
+      }
+      if (Ps.leader) da_d[r * H + Ps.head] = dad;
+    }
+    if (rn >= W.rend) break;
+    r = rn;
+    rn = rnn;
+    e0 = e0n;
+    e1 = e1n;
+    cu = cun;
+    e0n = e0nn;
+    e1n = e1nn;
+  }
+}
+
+// source-row pass, NST strips (two-strip shapes only, as k_gat_fwd_ps)
+template <int NST>
+__global__ __launch_bounds__(NT) void k_gat_bwd_node_ps(
+    const int32_t* __restrict__ tptr, const int32_t* __restrict__ tidx,
+    const int32_t* __restrict__ tmap, const float* __restrict__ alpha,
+    const float* __restrict__ mask, const float* __restrict__ da_e,
+    const float* __restrict__ da_d, const float* __restrict__ dZ, const float* __restrict__ XP,
+    const float* __restrict__ att_src, const float* __restrict__ att_dst, int64_t M, int H,
+    int C, float* __restrict__ dXP, float* __restrict__ part, uint16_t* __restrict__ dXPb) {
+  constexpr int SW = 128 * NST;  // features of the partial rows in LDS
+  __shared__ __attribute__((aligned(16))) float red[RB][3 * SW];
+  const EdgeLane L(H);
+  const int HC = H * C;
+  const int hps = 128 / C < H ? 128 / C : H;  // heads per strip
+  Pass<1> P[NST];
+  int hbase[NST], hq[NST];
+#pragma unroll
+  for (int st = 0; st < NST; ++st) {
+    P[st] = Pass<1>(st, L.li, HC, C);
+    hbase[st] = L.hwb + 8 * (P[st].head - st * hps);
+    const int he = st * hps + L.hh;
+    hq[st] = L.hh < hps && he < H ? he : st * hps;
+  }
+  const int hw = (threadIdx.x >> 6) * 2 + ((threadIdx.x & 63) >> 5);
+  f32x4 ps[NST], pd[NST], pb[NST];
+#pragma unroll
+  for (int st = 0; st < NST; ++st) ps[st] = pd[st] = pb[st] = f32x4{0.f, 0.f, 0.f, 0.f};
+  RowWalk W = row_walk(M);
+  if (W.r < W.rend) {
+    const int64_t cap = tptr[M];
+    const Buf bR = mkbuf(tptr, (M + 1) * 4), bT = mkbuf(tidx, cap * 4), bP = mkbuf(tmap, cap * 4);
+    const Buf bZ = mkbuf(dZ, M * HC * 4), bAl = mkbuf(alpha, cap * H * 4);
+    const Buf bM = mkbuf(mask, mask ? cap * H * 4 : 0), bDa = mkbuf(da_e, cap * H * 4);
+    f32x4 as[NST], adv[NST];
+#pragma unroll
+    for (int st = 0; st < NST; ++st) {
+      as[st] = ld4(att_src + P[st].fc[0]);
+      adv[st] = ld4(att_dst + P[st].fc[0]);
+    }
+    int64_t r = W.r;
+    int q0 = bldi(bR, (uint32_t)r * 4u), q1 = bldi(bR, (uint32_t)r * 4u + 4u);
+    int tu = bldi(bT, (uint32_t)L.pos(q0, q1) * 4u), pu = bldi(bP, (uint32_t)L.pos(q0, q1) * 4u);
+    int64_t rn = r + W.step;
+    uint32_t ro = rn < W.rend ? (uint32_t)rn * 4u : OOB;
+    int q0n = bldi(bR, ro), q1n = bldi(bR, ro + 4u);
+    for (;;) {
+      const int deg = q1 - q0;
+      float alu[NST], mk[NST], dau[NST], dd[NST];
+      f32x4 dv[NST][EB], xp[NST], zr[NST];
+#pragma unroll
+      for (int st = 0; st < NST; ++st) {
+        alu[st] = bld1(bAl, (uint32_t)(pu * H + hq[st]) * 4u);
+        mk[st] = mask ? bld1(bM, (uint32_t)(pu * H + hq[st]) * 4u) : 1.f;
+        dau[st] = bld1(bDa, (uint32_t)(pu * H + hq[st]) * 4u);
+#pragma unroll
+        for (int k = 0; k < EB; ++k)
+          dv[st][k] = bld4(bZ, ((uint32_t)bperm_i(tu, L.hwb + k) * HC + P[st].fc[0]) * 4u);
+        dd[st] = da_d[r * H + P[st].head];
+        xp[st] = ld4(XP + r * HC + P[st].fc[0]);
+        zr[st] = ld4(dZ + r * HC + P[st].fc[0]);
+      }
+      const int64_t rnn = rn + W.step;
+      const uint32_t qn = rn < W.rend ? (uint32_t)L.pos(q0n, q1n) * 4u : OOB;
+      const int tun = bldi(bT, qn), pun = bldi(bP, qn);
+      const uint32_t ron = rnn < W.rend ? (uint32_t)rnn * 4u : OOB;
+      const int q0nn = bldi(bR, ron), q1nn = bldi(bR, ron + 4u);
+#pragma unroll
+      for (int st = 0; st < NST; ++st) {
+        if (mask) alu[st] *= mk[st];
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        float sda = 0.f;
+#pragma unroll
+        for (int k = 0; k < EB; ++k) {
+          const float ak = bperm_f(alu[st], hbase[st] + k), dk = bperm_f(dau[st], hbase[st] + k);
+          if (k < deg) {
+            acc += ak * dv[st][k];
+            sda += dk;
+          }
+        }
+        for (int b = q0 + EB; b < q1; b += EB) {  // entries past the first batch
+          const int qb = L.pos(b, q1);
+          const int tb = bldi(bT, (uint32_t)qb * 4u), pb_ = bldi(bP, (uint32_t)qb * 4u);
+          float alb = bld1(bAl, (uint32_t)(pb_ * H + hq[st]) * 4u);
+          if (mask) alb *= bld1(bM, (uint32_t)(pb_ * H + hq[st]) * 4u);
+          const float dab = bld1(bDa, (uint32_t)(pb_ * H + hq[st]) * 4u);
+          f32x4 db[EB];
+#pragma unroll
+          for (int k = 0; k < EB; ++k)
+            db[k] = bld4(bZ, ((uint32_t)bperm_i(tb, L.hwb + k) * HC + P[st].fc[0]) * 4u);
+#pragma unroll
+          for (int k = 0; k < EB; ++k) {
+            const float ak = bperm_f(alb, hbase[st] + k), dk = bperm_f(dab, hbase[st] + k);
+            if (b + k < q1) {
+              acc += ak * db[k];
+              sda += dk;
+            }
+          }
+        }
+        const f32x4 o = acc + sda * as[st] + dd[st] * adv[st];
+        if (P[st].act[0]) {
+          st4(dXP + r * HC + P[st].f[0], o);
+          if (dXPb) st4_bf16(dXPb + r * HC + P[st].f[0], o);
+          ps[st] += sda * xp[st];
+          pd[st] += dd[st] * xp[st];
+          pb[st] += zr[st];
+        }
+      }
+      if (rn >= W.rend) break;
+      r = rn;
+      rn = rnn;
+      q0 = q0n;
+      q1 = q1n;
+      tu = tun;
+      pu = pun;
+      q0n = q0nn;
+      q1n = q1nn;
+    }
+  }
+#pragma unroll
+  for (int st = 0; st < NST; ++st) {
+    st4(&red[hw][0 * SW + 128 * st + 4 * L.li], ps[st]);
+    st4(&red[hw][1 * SW + 128 * st + 4 * L.li], pd[st]);
+    st4(&red[hw][2 * SW + 128 * st + 4 * L.li], pb[st]);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 3 * HC; i += NT) {
+    const int kind = i / HC, f = i % HC;
+    const int idx = kind * SW + f;
+    float t = red[0][idx];
+#pragma unroll
+    for (int q = 1; q < RB; ++q) t += red[q][idx];
+    part[(int64_t)blockIdx.x * 3 * HC + i] = t;
+  }
+}
+
 // the pipelined kernels' shapes, and whether they are enabled (LGNN_GAT_PIPE=0: the kernels above)
 inline bool pipe_ok(int H, int C) {
   const char* e = getenv("LGNN_GAT_PIPE");
   return H <= 4 && H * C <= 128 && !(e && e[0] == '0');
+}
+// the two-strip forms: 128 < H*C <= 256, 32 <= C <= 128 (the sweep's GAT [256]*L, 2..8 heads)
+inline bool pipe2_ok(int H, int C) {
+  const char* e = getenv("LGNN_GAT_PIPE");
+  return H * C > 128 && H * C <= 256 && C >= 32 && C <= 128 && !(e && e[0] == '0');
 }
 
 // persistent grid of a row-pipelined kernel: the workgroups one launch keeps resident (occupancy
 // API, cached per device and kernel), LGNN_GAT_BPC per CU if set
 template <typename K>
 inline unsigned pipe_grid(K kernel, int slot, int64_t M) {
-  static int cap[16][8];
+  static int cap[16][16];
   int dev = 0;
   (void)hipGetDevice(&dev);
   dev &= 15;
@@ -1067,6 +1475,17 @@ extern "C" int lgnn_gat_fwd(const int32_t* rowptr, const int32_t* col, const flo
   if (M > 0 && (!rowptr || !col || !XP || !a_s || !a_d || !Y)) return LGNN_EINVAL;
   if (!bytes_ok(M, H, C)) return LGNN_EINVAL;
   if (M == 0) return LGNN_OK;
+  if (pipe2_ok(H, C)) {
+#define LGNN_GFS(A_, SLOT_)                                                                     \
+  hipLaunchKernelGGL((k_gat_fwd_ps<A_, 2>), dim3(pipe_grid(k_gat_fwd_ps<A_, 2>, SLOT_, M)),        \
+                     dim3(NT), 0, as_stream(stream), rowptr, col, XP, a_s, a_d, M, H, C,           \
+                     negative_slope, edge_mask, bias, alpha, Y, Y_bf16)
+    if (act == LGNN_ACT_ELU) LGNN_GFS(LGNN_ACT_ELU, 6);
+    else LGNN_GFS(LGNN_ACT_NONE, 7);
+#undef LGNN_GFS
+    LGNN_LAUNCH_CHECK();
+    return LGNN_OK;
+  }
   if (pipe_ok(H, C)) {
     if (act == LGNN_ACT_ELU)
       hipLaunchKernelGGL(k_gat_fwd_p<LGNN_ACT_ELU>,
@@ -1117,6 +1536,21 @@ int gat_bwd_edge_launch(const int32_t* rowptr, const int32_t* col, const float* 
   if (!bytes_ok(M, H, C)) return LGNN_EINVAL;
   if (M == 0) return LGNN_OK;
   const PoolGrad p = pg ? *pg : PoolGrad{};
+  if (pipe2_ok(H, C)) {
+#define LGNN_GBS(A_, POOL_, SLOT_)                                                             \
+  hipLaunchKernelGGL((k_gat_bwd_edge_ps<A_, POOL_, 2>),                                         \
+                     dim3(pipe_grid(k_gat_bwd_edge_ps<A_, POOL_, 2>, SLOT_, M)), dim3(NT), 0,    \
+                     as_stream(stream), rowptr, col, XP, a_s, a_d, alpha, edge_mask, dY, Y, M, H, \
+                     C, slope, dZ, da_e, da_d, p)
+    if (act == LGNN_ACT_ELU) {
+      if (pg) LGNN_GBS(LGNN_ACT_ELU, true, 8); else LGNN_GBS(LGNN_ACT_ELU, false, 9);
+    } else {
+      if (pg) LGNN_GBS(LGNN_ACT_NONE, true, 10); else LGNN_GBS(LGNN_ACT_NONE, false, 11);
+    }
+#undef LGNN_GBS
+    LGNN_LAUNCH_CHECK();
+    return LGNN_OK;
+  }
   if (pipe_ok(H, C)) {
 #define LGNN_GBP(A_, POOL_, SLOT_)                                                             \
   hipLaunchKernelGGL((k_gat_bwd_edge_p<A_, POOL_>),                                             \
@@ -1204,6 +1638,13 @@ extern "C" int lgnn_gat_bwd_node(const int32_t* tptr, const int32_t* tidx, const
   if (M > 0 && (!tptr || !tidx || !tmap || !alpha || !da_e || !da_d || !dZ || !XP || !dXP))
     return LGNN_EINVAL;
   if (!bytes_ok(M, H, C)) return LGNN_EINVAL;
+  if (pipe2_ok(H, C) && M > 0) {
+    hipLaunchKernelGGL(k_gat_bwd_node_ps<2>, dim3(num_partials), dim3(NT), 0, as_stream(stream),
+                       tptr, tidx, tmap, alpha, edge_mask, da_e, da_d, dZ, XP, att_src, att_dst, M,
+                       H, C, dXP, partials, dXP_bf16);
+    LGNN_LAUNCH_CHECK();
+    return LGNN_OK;
+  }
   if (pipe_ok(H, C) && M > 0) {
     hipLaunchKernelGGL(k_gat_bwd_node_p, dim3(num_partials), dim3(NT), 0, as_stream(stream), tptr,
                        tidx, tmap, alpha, edge_mask, da_e, da_d, dZ, XP, att_src, att_dst, M, H, C,
