@@ -74,6 +74,10 @@ WORKLOADS = {
                            hidden=[256] * 4, heads=8, classes=5, loss="MSE", pool="mean",
                            last_channel_class=True, dropout=0.35,
                            desc="sweep: GAT [256]*4, heads 8, dropout 0.35, d_in 1025, fp32"),
+    "sweep_gat512h4": dict(model="gat", sizes="lognormal", n=64, k=6, d_in=1025,
+                           hidden=[512] * 3, heads=4, classes=5, loss="MSE", pool="mean",
+                           last_channel_class=True, dropout=0.35,
+                           desc="sweep: GAT [512]*3, heads 4, dropout 0.35, d_in 1025, fp32"),
     "sweep_gin512": dict(model="gin", sizes="fixed", n=64, k=8, d_in=128, hidden=[512] * 4,
                          classes=5, loss="CE", pool="add",
                          desc="sweep: GIN [512]*4 + global_add_pool (generic-shape kernels)"),

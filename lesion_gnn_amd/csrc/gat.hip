@@ -1004,7 +1004,7 @@ __global__ __launch_bounds__(NT) void k_gat_fwd_ps(const int32_t* __restrict__ r
                                                   const float* __restrict__ XP,
                                                   const float* __restrict__ a_s,
                                                   const float* __restrict__ a_d, int64_t M, int H,
-                                                  int C, float slope,
+                                                  int C, int s0, float slope,
                                                   const float* __restrict__ mask,
                                                   const float* __restrict__ bias,
                                                   float* __restrict__ alpha, float* __restrict__ Y,
@@ -1020,9 +1020,9 @@ __global__ __launch_bounds__(NT) void k_gat_fwd_ps(const int32_t* __restrict__ r
   bool hv[NST];
 #pragma unroll
   for (int st = 0; st < NST; ++st) {
-    P[st] = Pass<1>(st, L.li, HC, C);
-    hbase[st] = L.hwb + 8 * (P[st].head - st * hps);
-    const int he = st * hps + L.hh;
+    P[st] = Pass<1>(s0 + st, L.li, HC, C);
+    hbase[st] = L.hwb + 8 * (P[st].head - (s0 + st) * hps);
+    const int he = (s0 + st) * hps + L.hh;
     hv[st] = L.hh < hps && he < H;
     hq[st] = hv[st] ? he : 0;
   }
@@ -1134,8 +1134,8 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_edge_ps(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const float* __restrict__ XP, const float* __restrict__ a_s, const float* __restrict__ a_d,
     const float* __restrict__ alpha, const float* __restrict__ mask, const float* __restrict__ dY,
-    const float* __restrict__ Y, int64_t M, int H, int C, float slope, float* __restrict__ dZ,
-    float* __restrict__ da_e, float* __restrict__ da_d, PoolGrad pg) {
+    const float* __restrict__ Y, int64_t M, int H, int C, int s0, float slope,
+    float* __restrict__ dZ, float* __restrict__ da_e, float* __restrict__ da_d, PoolGrad pg) {
   const EdgeLane L(H);
   const int HC = H * C;
   const int hps = 128 / C < H ? 128 / C : H;  // heads per strip
@@ -1144,12 +1144,12 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_edge_ps(
   bool hv[NST];
 #pragma unroll
   for (int st = 0; st < NST; ++st) {
-    P[st] = Pass<1>(st, L.li, HC, C);
-    hbase[st] = L.hwb + 8 * (P[st].head - st * hps);
-    const int he = st * hps + L.hh;
+    P[st] = Pass<1>(s0 + st, L.li, HC, C);
+    hbase[st] = L.hwb + 8 * (P[st].head - (s0 + st) * hps);
+    const int he = (s0 + st) * hps + L.hh;
     hv[st] = L.hh < hps && he < H;
-    hq[st] = hv[st] ? he : st * hps;
-    hlead[st] = L.hwb + (hq[st] - st * hps) * P[st].G;  // the first feature lane of that head
+    hq[st] = hv[st] ? he : (s0 + st) * hps;
+    hlead[st] = L.hwb + (hq[st] - (s0 + st) * hps) * P[st].G;  // the first feature lane of that head
   }
   RowWalk W = row_walk(M);
   if (W.r >= W.rend) return;
@@ -1267,7 +1267,8 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_node_ps(
     const float* __restrict__ mask, const float* __restrict__ da_e,
     const float* __restrict__ da_d, const float* __restrict__ dZ, const float* __restrict__ XP,
     const float* __restrict__ att_src, const float* __restrict__ att_dst, int64_t M, int H,
-    int C, float* __restrict__ dXP, float* __restrict__ part, uint16_t* __restrict__ dXPb) {
+    int C, int s0, float* __restrict__ dXP, float* __restrict__ part,
+    uint16_t* __restrict__ dXPb) {
   constexpr int SW = 128 * NST;  // features of the partial rows in LDS
   __shared__ __attribute__((aligned(16))) float red[RB][3 * SW];
   const EdgeLane L(H);
@@ -1277,10 +1278,10 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_node_ps(
   int hbase[NST], hq[NST];
 #pragma unroll
   for (int st = 0; st < NST; ++st) {
-    P[st] = Pass<1>(st, L.li, HC, C);
-    hbase[st] = L.hwb + 8 * (P[st].head - st * hps);
-    const int he = st * hps + L.hh;
-    hq[st] = L.hh < hps && he < H ? he : st * hps;
+    P[st] = Pass<1>(s0 + st, L.li, HC, C);
+    hbase[st] = L.hwb + 8 * (P[st].head - (s0 + st) * hps);
+    const int he = (s0 + st) * hps + L.hh;
+    hq[st] = L.hh < hps && he < H ? he : (s0 + st) * hps;
   }
   const int hw = (threadIdx.x >> 6) * 2 + ((threadIdx.x & 63) >> 5);
   f32x4 ps[NST], pd[NST], pb[NST];
@@ -1384,13 +1385,14 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_node_ps(
     st4(&red[hw][2 * SW + 128 * st + 4 * L.li], pb[st]);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 3 * HC; i += NT) {
-    const int kind = i / HC, f = i % HC;
-    const int idx = kind * SW + f;
-    float t = red[0][idx];
+  // this launch's features [128 s0, 128 s0 + SW) of each partial row
+  for (int i = threadIdx.x; i < 3 * SW; i += NT) {
+    const int kind = i / SW, fl = i % SW, f = 128 * s0 + fl;
+    if (f >= HC) continue;
+    float t = red[0][i];
 #pragma unroll
-    for (int q = 1; q < RB; ++q) t += red[q][idx];
-    part[(int64_t)blockIdx.x * 3 * HC + i] = t;
+    for (int q = 1; q < RB; ++q) t += red[q][i];
+    part[(int64_t)blockIdx.x * 3 * HC + kind * HC + f] = t;
   }
 }
 
@@ -1399,10 +1401,11 @@ inline bool pipe_ok(int H, int C) {
   const char* e = getenv("LGNN_GAT_PIPE");
   return H <= 4 && H * C <= 128 && !(e && e[0] == '0');
 }
-// the two-strip forms: 128 < H*C <= 256, 32 <= C <= 128 (the sweep's GAT [256]*L, 2..8 heads)
+// the two-strip forms: 128 < H*C <= 512, 32 <= C <= 128 (the sweep's GAT widths 256 and 512 at
+// 2..8 heads), one launch per 256 features (a pass's heads are independent of the others')
 inline bool pipe2_ok(int H, int C) {
   const char* e = getenv("LGNN_GAT_PIPE");
-  return H * C > 128 && H * C <= 256 && C >= 32 && C <= 128 && !(e && e[0] == '0');
+  return H * C > 128 && H * C <= 512 && C >= 32 && C <= 128 && !(e && e[0] == '0');
 }
 
 // persistent grid of a row-pipelined kernel: the workgroups one launch keeps resident (occupancy
@@ -1478,10 +1481,12 @@ extern "C" int lgnn_gat_fwd(const int32_t* rowptr, const int32_t* col, const flo
   if (pipe2_ok(H, C)) {
 #define LGNN_GFS(A_, SLOT_)                                                                     \
   hipLaunchKernelGGL((k_gat_fwd_ps<A_, 2>), dim3(pipe_grid(k_gat_fwd_ps<A_, 2>, SLOT_, M)),        \
-                     dim3(NT), 0, as_stream(stream), rowptr, col, XP, a_s, a_d, M, H, C,           \
+                     dim3(NT), 0, as_stream(stream), rowptr, col, XP, a_s, a_d, M, H, C, s0,       \
                      negative_slope, edge_mask, bias, alpha, Y, Y_bf16)
-    if (act == LGNN_ACT_ELU) LGNN_GFS(LGNN_ACT_ELU, 6);
-    else LGNN_GFS(LGNN_ACT_NONE, 7);
+    for (int s0 = 0; 128 * s0 < H * C; s0 += 2) {
+      if (act == LGNN_ACT_ELU) LGNN_GFS(LGNN_ACT_ELU, 6);
+      else LGNN_GFS(LGNN_ACT_NONE, 7);
+    }
 #undef LGNN_GFS
     LGNN_LAUNCH_CHECK();
     return LGNN_OK;
@@ -1541,11 +1546,13 @@ int gat_bwd_edge_launch(const int32_t* rowptr, const int32_t* col, const float* 
   hipLaunchKernelGGL((k_gat_bwd_edge_ps<A_, POOL_, 2>),                                         \
                      dim3(pipe_grid(k_gat_bwd_edge_ps<A_, POOL_, 2>, SLOT_, M)), dim3(NT), 0,    \
                      as_stream(stream), rowptr, col, XP, a_s, a_d, alpha, edge_mask, dY, Y, M, H, \
-                     C, slope, dZ, da_e, da_d, p)
-    if (act == LGNN_ACT_ELU) {
-      if (pg) LGNN_GBS(LGNN_ACT_ELU, true, 8); else LGNN_GBS(LGNN_ACT_ELU, false, 9);
-    } else {
-      if (pg) LGNN_GBS(LGNN_ACT_NONE, true, 10); else LGNN_GBS(LGNN_ACT_NONE, false, 11);
+                     C, s0, slope, dZ, da_e, da_d, p)
+    for (int s0 = 0; 128 * s0 < H * C; s0 += 2) {
+      if (act == LGNN_ACT_ELU) {
+        if (pg) LGNN_GBS(LGNN_ACT_ELU, true, 8); else LGNN_GBS(LGNN_ACT_ELU, false, 9);
+      } else {
+        if (pg) LGNN_GBS(LGNN_ACT_NONE, true, 10); else LGNN_GBS(LGNN_ACT_NONE, false, 11);
+      }
     }
 #undef LGNN_GBS
     LGNN_LAUNCH_CHECK();
@@ -1639,9 +1646,10 @@ extern "C" int lgnn_gat_bwd_node(const int32_t* tptr, const int32_t* tidx, const
     return LGNN_EINVAL;
   if (!bytes_ok(M, H, C)) return LGNN_EINVAL;
   if (pipe2_ok(H, C) && M > 0) {
-    hipLaunchKernelGGL(k_gat_bwd_node_ps<2>, dim3(num_partials), dim3(NT), 0, as_stream(stream),
-                       tptr, tidx, tmap, alpha, edge_mask, da_e, da_d, dZ, XP, att_src, att_dst, M,
-                       H, C, dXP, partials, dXP_bf16);
+    for (int s0 = 0; 128 * s0 < H * C; s0 += 2)
+      hipLaunchKernelGGL(k_gat_bwd_node_ps<2>, dim3(num_partials), dim3(NT), 0,
+                         as_stream(stream), tptr, tidx, tmap, alpha, edge_mask, da_e, da_d, dZ, XP,
+                         att_src, att_dst, M, H, C, s0, dXP, partials, dXP_bf16);
     LGNN_LAUNCH_CHECK();
     return LGNN_OK;
   }

@@ -2,7 +2,7 @@
 k_gat_bwd_node_p: a half wave walks many rows with the next rows' indices in flight, per-edge
 scalars loaded edge-parallel and handed over by ds_bpermute; taken when H*C <= 128 and H <= 4,
 i.e. the reference config's GAT (heads 2, C 64; gat.py:31, configs/config.py:59-64) and C3's,
-and also when 128 < H*C <= 256 with C >= 32: two 128-feature strips per row)
+and also when 128 < H*C <= 512 with C >= 32: two 128-feature strips per row and launch)
 are bit-identical to the per-row kernels they replace (LGNN_GAT_PIPE=0): forward outputs and
 every parameter gradient, with dropout masks, with the readout folded into the last layer's edge
 kernel and without, on rows longer than one 8-entry batch (k = 10, hub nodes: the batched walk),
@@ -53,11 +53,15 @@ def _run(m, b, cuda, rng):
     ("hubs", 2, [128, 128], 0.3, True),
     ("hubs", 4, [64, 128], 0.0, False),
     ("tiny", 2, [128, 128], 0.0, True),
-    # H*C = 256 (the sweep's width 256): the two-strip forms, 2..8 heads
+    # H*C = 256 (the sweep's width 256): the two-strip form, 2..8 heads
     ("refcfg", 8, [256, 256], 0.35, True),
     ("k10", 2, [256, 256], 0.0, False),
     ("hubs", 4, [256, 128], 0.3, True),
     ("tiny", 8, [256, 256], 0.0, True),
+    # H*C = 512: two launches of the two-strip form per kernel
+    ("refcfg", 4, [512, 512], 0.35, True),
+    ("hubs", 8, [512, 256], 0.3, False),
+    ("k10", 8, [512, 512], 0.0, True),
 ])
 def test_pipelined_kernels_bitwise(cuda, monkeypatch, kind, heads, hidden, dropout, fold):
     b = _batch(kind)
