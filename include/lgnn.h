@@ -607,8 +607,11 @@ int lgnn_adam_step(int n, float* const* params, const float* const* grads, float
  *   planes_t: the transposed weight planes of lgnn_weight_planes (all L + 1 layers);
  *   H[0..L]: layer outputs (H[0] = in_proj output); X: model input; widths[0..L+1];
  *   dWp / dbp: per-layer partial slabs with num_partials = lgnn_gcn_stack_bwd_partials(M)
- *   slots, every slot written (zeros for a workgroup without tiles), so open tiles can be
- *   accumulated afterwards by lgnn_node_linear_bwd_tiles(..., accumulate = 1).
+ *   slots. A workgroup that processed no closed tile writes NO slot: it sets its skip word
+ *   tile_open[ceil(M/64) + LGNN_SLOT_FLAG0 + b] instead (so tile_open is written by this call,
+ *   beside the barrier words), and the open tiles must then be accumulated by
+ *   lgnn_node_linear_bwd_tiles(..., accumulate = 2), which writes the skipped slots (zeros where
+ *   it has no tile either). accumulate = 1 after this call would add to uninitialised slots.
  *   adjt (nullable): the tile adjacencies the split-3 forward wrote for this graph (its adjt);
  *   each tile's goes straight into LDS (prefetched during the previous tile) instead of being
  *   rebuilt from the CSR.

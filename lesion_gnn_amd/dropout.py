@@ -41,29 +41,49 @@ def _splitmix64(z: int) -> int:
     return z ^ (z >> 31)
 
 
-_CONSTRUCTIONS = [0]  # seeds derived so far in this process
+_UNSALTED = [0]  # unsalted seeds derived so far in this process
 
 
-def derived_seed() -> int:
-    """A seed derived from torch's default CPU generator WITHOUT advancing it: the splitmix64 of
-    a hash of its current state (read, not drawn from) and of a per-process construction counter.
-    Reproducible under torch.manual_seed (the counter restarts with the process), building a
-    model leaves the generator's stream exactly where weight init left it, and two constructions
-    never share a seed even with no CPU draw between them (models initialised on the GPU, meta
-    device or skip_init, or loaded from a checkpoint without re-init)."""
+def param_salt(module) -> bytes | None:
+    """The digest of a freshly built module's initial parameters (None when any parameter has no
+    data: meta device, lazy modules)."""
     import hashlib
 
-    n = _CONSTRUCTIONS[0]
-    _CONSTRUCTIONS[0] += 1
+    h = hashlib.sha256()
+    for p in module.parameters():
+        if p.is_meta or isinstance(p, torch.nn.parameter.UninitializedParameter):
+            return None
+        h.update(p.detach().to("cpu", torch.float32).contiguous().numpy().tobytes())
+    return h.digest()
+
+
+def derived_seed(salt: bytes | None = None) -> int:
+    """A seed derived from torch's default CPU generator WITHOUT advancing it: the splitmix64 of a
+    hash of its current state (read, not drawn from) and of a salt.
+
+    Models pass the digest of their initial parameters (`param_salt`), so the seed is a function
+    of the generator state and the model's own initial weights only: `torch.manual_seed(s);
+    m1 = Model(); torch.manual_seed(s); m2 = Model()` gives m1 and m2 the same dropout stream (as
+    torch's own dropout would), whatever was built earlier in the process, and two models whose
+    weights differ (CPU or GPU init) get different streams. Without a salt (a lone conv, meta
+    parameters) a per-process counter is mixed in instead, so two such constructions with no
+    generator draw between them still differ. Building a model leaves the generator's stream
+    exactly where weight init left it."""
+    import hashlib
+
+    if salt is None:
+        n = _UNSALTED[0]
+        _UNSALTED[0] += 1
+        salt = b"unsalted" + n.to_bytes(8, "little")
     state = torch.default_generator.get_state().numpy().tobytes()
-    h = int.from_bytes(hashlib.sha256(state + n.to_bytes(8, "little")).digest()[:8], "little")
+    h = int.from_bytes(hashlib.sha256(state + salt).digest()[:8], "little")
     return _splitmix64(h) & (2 ** 62 - 1)
 
 
-def new_state(seed: int | None = None) -> torch.Tensor:
+def new_state(seed: int | None = None, salt: bytes | None = None) -> torch.Tensor:
     """A generator state [seed, counter = 0, tickets = 0 ...] (CPU; register it as a buffer)."""
     if seed is None:
-        seed = derived_seed()
+        seed = derived_seed(salt)
     return torch.tensor([int(seed)] + [0] * (STATE_WORDS - 1), dtype=torch.int64)
 
 

@@ -717,10 +717,11 @@ def _(running_mean, running_var, nbt, sums, count, bn_eps, momentum):
 @gin_conv.register_fake
 def _(x, W1, b1, gamma, beta, W2, b2, running_mean, running_var, g, training, eps, bn_eps,
       mask, act):
-    from .ops import fast_shape
+    from .ops import fast_shape, wide_shape
 
     M, N1 = x.shape[0], W1.shape[0]
-    gathered = not fast_shape(W1.shape[1], N1)
+    # the eager rule (_GINConv.forward): S is saved for the tile fast path and the wide path
+    gathered = not (fast_shape(W1.shape[1], N1) or wide_shape(W1.shape[1], N1))
     S = _none(x.device) if gathered else torch.empty_like(x)
     sums = x.new_empty(2 * N1, dtype=torch.float64) if training else _none(x.device)
     return [x.new_empty(M, W2.shape[0]), S, x.new_empty(M, N1), x.new_empty(M, N1)] + \
@@ -786,12 +787,14 @@ gin_conv.register_autograd(_gin_backward, setup_context=_gin_setup)
 
 
 def _gcn_layout(params, L):
-    from .ops import STACK_MAX, fast_shape
+    from .ops import STACK_MAX, fast_shape, wide_shape
 
     Ws = [params[2 * l] for l in range(L + 1)]
     fused = L + 1 <= STACK_MAX and all(fast_shape(W.shape[1], W.shape[0]) for W in Ws)
-    saved_s = [True] * L if fused else [fast_shape(params[2 + 2 * l].shape[1],
-                                                   params[2 + 2 * l].shape[0]) for l in range(L)]
+    # the eager rule (_GCNStack._fwd): S_l is saved for fast-path and wide layers
+    saved_s = [True] * L if fused else [
+        fast_shape(params[2 + 2 * l].shape[1], params[2 + 2 * l].shape[0]) or
+        wide_shape(params[2 + 2 * l].shape[1], params[2 + 2 * l].shape[0]) for l in range(L)]
     return fused, saved_s
 
 
@@ -833,7 +836,12 @@ def _(x, g, mean, L, params):
 def gcn_stack_bwd(dlogits: Tensor, x: Tensor, pooled: Tensor, hs: list[Tensor],
                   ss: list[Tensor], params: list[Tensor], planes_t: Tensor, g: list[Tensor],
                   mean: bool, L: int, want_dx: bool) -> list[Tensor]:
-    """[dx or none, dparams...]"""
+    """[dx or none, dparams...]
+
+    The graph's tile_open (in g) is written here although the op declares no mutation: the fused
+    backward's barrier words and partial-slot skip words (include/lgnn.h LGNN_SLOT_FLAG0) are
+    scratch set and consumed inside this one call, and the next graph build zeroes them; the tile
+    flags proper, the only part of tile_open other ops read, are left unchanged."""
     from .ops import _GCNStack
 
     fused, saved_s = _gcn_layout(params, L)

@@ -55,7 +55,10 @@ class GAT(nn.Module):
         self.dropout_p = float(dropout)
         self._dropout_key = repr(self.dropout_p)
         # the attention-dropout generator (lesion_gnn_amd.dropout; not in state_dict)
-        self.register_buffer("_dropout_rng", lgnn_dropout.new_state(), persistent=False)
+        # (seeded by the generator state and this model's initial weights)
+        self.register_buffer("_dropout_rng",
+                             lgnn_dropout.new_state(salt=lgnn_dropout.param_salt(self)),
+                             persistent=False)
 
     def dropout_masks(self, g) -> list | None:
         """Every conv's attention-dropout mask of this forward, in one launch (mask l -> conv l);

@@ -37,7 +37,10 @@ class GCN(nn.Module):
         self.pool = pool
         self._dropout_key = repr(float(dropout))
         # the dropout generator (lesion_gnn_amd.dropout; not in state_dict)
-        self.register_buffer("_dropout_rng", lgnn_dropout.new_state(), persistent=False)
+        # (seeded by the generator state and this model's initial weights)
+        self.register_buffer("_dropout_rng",
+                             lgnn_dropout.new_state(salt=lgnn_dropout.param_salt(self)),
+                             persistent=False)
 
     def flat_params(self) -> list[torch.Tensor]:
         ps = [self.in_proj.weight, self.in_proj.bias]

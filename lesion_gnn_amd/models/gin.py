@@ -42,7 +42,10 @@ class GIN(nn.Module):
         self.pool = pool
         self._dropout_key = repr(float(dropout))
         # the dropout generator (lesion_gnn_amd.dropout; not in state_dict)
-        self.register_buffer("_dropout_rng", lgnn_dropout.new_state(), persistent=False)
+        # (seeded by the generator state and this model's initial weights)
+        self.register_buffer("_dropout_rng",
+                             lgnn_dropout.new_state(salt=lgnn_dropout.param_salt(self)),
+                             persistent=False)
 
     def dropout_masks(self, x: torch.Tensor) -> list | None:
         """This forward's masks in one launch: conv l's MLP dropout (mask 2l, reference gin.py:23)

@@ -1189,20 +1189,19 @@ class _GCNStackCE(torch.autograd.Function):
         ctx.set_materialize_grads(False)
         yy = y.to(torch.int64).contiguous()
         w = _f32c(weight) if weight is not None else None
-        # the readout runs the CE forward too (one launch) where its kernel takes the shape
         logits, to_save = _GCNStack._fwd(ctx, x, graph, mean, L, params)
         z = logits
-        if True:  # one single-workgroup launch: loss, lse and the gradient's factors pm / wt
-            B, C = z.shape
-            dev = z.device
-            lse = torch.empty(B, dtype=torch.float32, device=dev)
-            out = torch.empty(2, dtype=torch.float32, device=dev)  # loss, sum of weights
-            bad = torch.empty(1, dtype=torch.int32, device=dev)
-            pm = torch.empty(B, C, dtype=torch.float32, device=dev)
-            wt = torch.empty(B, dtype=torch.float32, device=dev)
-            _lib.call("lgnn_ce_fwd_factors", _lib.ptr(z), _lib.ptr(yy), _lib.ptr(w), B, C,
-                      _lib.ptr(lse), _lib.ptr(out), _lib.ptr(out) + 4, _lib.ptr(bad),
-                      _lib.ptr(pm), _lib.ptr(wt), _s(dev))
+        # one single-workgroup launch: loss, lse and the gradient's factors pm / wt
+        B, C = z.shape
+        dev = z.device
+        lse = torch.empty(B, dtype=torch.float32, device=dev)
+        out = torch.empty(2, dtype=torch.float32, device=dev)  # loss, sum of weights
+        bad = torch.empty(1, dtype=torch.int32, device=dev)
+        pm = torch.empty(B, C, dtype=torch.float32, device=dev)
+        wt = torch.empty(B, dtype=torch.float32, device=dev)
+        _lib.call("lgnn_ce_fwd_factors", _lib.ptr(z), _lib.ptr(yy), _lib.ptr(w), B, C,
+                  _lib.ptr(lse), _lib.ptr(out), _lib.ptr(out) + 4, _lib.ptr(bad),
+                  _lib.ptr(pm), _lib.ptr(wt), _s(dev))
         ctx.ce_fwd = None
         ctx.has_w = w is not None
         ctx.has_pm = pm is not None

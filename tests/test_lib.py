@@ -90,9 +90,9 @@ def test_stack_fwd_validation_without_gpu():
 
 
 def test_dropout_seeds_distinct_without_cpu_draws():
-    """Two models built with no CPU generator draw in between (GPU / meta init, checkpoint
-    loads) get different dropout seeds: derived_seed mixes a per-process construction counter
-    into the hash of the generator state, and leaves the generator untouched."""
+    """Two unsalted constructions with no CPU generator draw in between (a lone conv, meta
+    parameters) get different dropout seeds: derived_seed mixes a per-process counter into the
+    hash of the generator state, and leaves the generator untouched."""
     import torch
 
     from lesion_gnn_amd import dropout
@@ -103,3 +103,29 @@ def test_dropout_seeds_distinct_without_cpu_draws():
     assert a != b
     assert torch.equal(torch.default_generator.get_state(), before)
     assert 0 <= a < 2 ** 62 and 0 <= b < 2 ** 62
+
+
+def test_dropout_seed_reproducible_under_manual_seed():
+    """Re-seeding and rebuilding reproduces a model's dropout seed, whatever was built in
+    between (the seed is salted with the model's initial weights, not a process counter); two
+    models with different weights get different seeds, and building leaves the generator where
+    weight init left it."""
+    import torch
+
+    from lesion_gnn_amd.models.gat import GAT
+    from lesion_gnn_amd.models.gcn import GCN
+    from lesion_gnn_amd.models.gin import GIN
+
+    builders = {"GCN": lambda: GCN(16, [32, 32], 3, 0.35), "GIN": lambda: GIN(16, [32, 32], 3, 0.35),
+                "GAT": lambda: GAT(16, [32, 32], 3, 2, 0.35)}
+    for name, build in builders.items():
+        torch.manual_seed(7)
+        m1 = build()
+        after = torch.default_generator.get_state().clone()
+        build()  # a construction in between
+        torch.manual_seed(7)
+        m2 = build()
+        assert torch.equal(torch.default_generator.get_state(), after)
+        m3 = build()
+        s1, s2, s3 = (int(m._dropout_rng[0]) for m in (m1, m2, m3))
+        assert s1 == s2 and s3 != s1, name
