@@ -78,6 +78,19 @@ WORKLOADS = {
                            hidden=[512] * 3, heads=4, classes=5, loss="MSE", pool="mean",
                            last_channel_class=True, dropout=0.35,
                            desc="sweep: GAT [512]*3, heads 4, dropout 0.35, d_in 1025, fp32"),
+    "sweep_gat128h8": dict(model="gat", sizes="lognormal", n=64, k=6, d_in=1025,
+                           hidden=[128] * 4, heads=8, classes=5, loss="MSE", pool="mean",
+                           last_channel_class=True, dropout=0.35,
+                           desc="sweep: GAT [128]*4, heads 8 (16 channels per head), dropout 0.35, "
+                                "d_in 1025, fp32"),
+    "sweep_gcn_k16": dict(model="gcn", sizes="fixed", n=64, k=16, d_in=128, hidden=[128] * 3,
+                          classes=5, loss="CE", pool="mean",
+                          desc="sweep: 2-layer GCN, N = 64, k = 16 (closed 64-row tiles of 1024 "
+                               "CSR entries)"),
+    "sweep_gcn_k32": dict(model="gcn", sizes="fixed", n=64, k=32, d_in=128, hidden=[128] * 3,
+                          classes=5, loss="CE", pool="mean",
+                          desc="sweep: 2-layer GCN, N = 64, k = 32 (the sweep's largest k, "
+                               "scripts/sweep.py:110)"),
     "sweep_gin512": dict(model="gin", sizes="fixed", n=64, k=8, d_in=128, hidden=[512] * 4,
                          classes=5, loss="CE", pool="add",
                          desc="sweep: GIN [512]*4 + global_add_pool (generic-shape kernels)"),
@@ -522,7 +535,46 @@ def _entry_model(name, a, gs):
             by += 8.0 * gs.nnz + 4 * M
             fl += 2.0 * gs.nnz * N
         return by, fl
+    # split-3 dense GEMMs (s3gemm.hip: the wide GIN / GCN linears, the GAT lins / in_proj)
+    if name in ("lgnn_s3_gemm", "lgnn_s3_gemm_act"):  # A, M, K, Wp, N, ...: Y = A W^T (+ b)
+        M, K, N = a[1], a[2], a[4]
+        return f4 * M * (K + N) + 6.0 * N * K, 2.0 * M * K * N
+    if name == "lgnn_s3_wgrad":  # dY, N, X, M, K, ...: dW = dY^T X (the slab written once)
+        N, M, K = a[1], a[3], a[4]
+        return f4 * M * (K + N) + f4 * N * K, 2.0 * M * K * N
+    if name == "lgnn_spmm":  # rowptr, col, w, self_scale, X, M, D, Y: Y = (s I + A) X
+        M, D = a[5], a[6]
+        return 2 * f4 * M * D + 8.0 * gs.nnz + 4 * M, 2.0 * (gs.nnz + M) * D
+    if name in ("lgnn_gcn_stack_fwd_s3_all", "lgnn_gcn_stack_bwd_s3"):
+        if name.endswith("_all"):  # X, M, d_in, has_in_proj, rowptr, col, w, L, planes, W, b, widths
+            M, L, wd = a[1], a[7], list(a[11])
+            wd = [a[2]] + wd  # widths of lgnn_gcn_stack_fwd_s3_all: the layers' outputs
+        else:  # dP, batch, gptr, mean, B, rowptr, col, w, X, M, L, planes_t, H, widths
+            M, L, wd = a[9], a[10], list(a[13])
+        R, nz = gs.rows(1, 0) if gs.open_rows else (M, gs.nnz)
+        conv = sum(2.0 * R * wd[l] * wd[l + 1] + 2.0 * nz * wd[l] for l in range(1, L + 1))
+        if name.endswith("_all"):  # reads X, writes H_0..H_L, walks the CSR once per conv
+            by = f4 * M * (wd[0] + sum(wd[1:L + 2])) + 8.0 * nz * L
+            return by, 2.0 * R * wd[0] * wd[1] + conv
+        # layer-major backward: H_{l-1} and dZ_l read, dZ_{l-1} written per conv, X and dZ_0 for
+        # in_proj, H_L for the top ELU', the CSR once per conv
+        by = f4 * M * (wd[L + 1] + sum(wd[l] + wd[l + 1] + wd[l] for l in range(1, L + 1))
+                       + wd[0] + wd[1]) + 8.0 * nz * L
+        return by, 2.0 * R * wd[0] * wd[1] + 2 * conv
     return None
+
+
+# the MFMA roof of a modelled entry (useful fp32 FLOP): split-3 bf16 entries against dense bf16 / 6,
+# the fp32-MFMA tile kernels against the fp32 peak
+_S3_ENTRIES = ("lgnn_s3_gemm", "lgnn_s3_gemm_act", "lgnn_s3_wgrad", "lgnn_gcn_stack_fwd_s3_all",
+               "lgnn_gcn_stack_bwd_s3")
+
+
+# kernel-name fragments of the modelled entries without a _entry_kernel mapping (PMC lookups)
+_ENTRY_TRACE = {"lgnn_s3_gemm": "lgnn_s3::k_s3_gemm", "lgnn_s3_gemm_act": "lgnn_s3::k_s3_gemm",
+                "lgnn_s3_wgrad": "lgnn_s3::k_s3_wgrad2", "lgnn_spmm": "::k_spmm",
+                "lgnn_gcn_stack_fwd_s3_all": "lgnn_s3::k_s3_fwd",
+                "lgnn_gcn_stack_bwd_s3": "lgnn_s3::k_s3_bwd"}
 
 
 def _entry_kernel(name, a):
@@ -650,18 +702,22 @@ def layer_roofline(rows, workload):
     for r in cand[:3]:
         sec = r["avg_launch_ms"] * 1e-3
         gbs, tf = r["bytes_per_launch"] / sec / 1e9, r["flops_per_launch"] / sec / 1e12
-        f_hbm, f_mfma = gbs / HBM_PEAK_GBS, tf / MFMA_F32_PEAK_TF
-        traffic, tsrc = pmc_traffic(r["kernel"], workload) if r["kernel"] else (None, None)
+        mpeak = MFMA_S3_PEAK_TF if r["entry"] in _S3_ENTRIES else MFMA_F32_PEAK_TF
+        f_hbm, f_mfma = gbs / HBM_PEAK_GBS, tf / mpeak
+        traffic, tsrc = pmc_traffic(r["kernel"] or _ENTRY_TRACE.get(r["entry"], r["entry"]),
+                                    workload)
         hbm = f_hbm >= f_mfma
+        what = ("split-3 bf16 MFMA at fp32 accuracy" if r["entry"] in _S3_ENTRIES else
+                "fp32 MFMA + CSR gather, tile.hip" if r["kernel"] else "CSR gather")
         row = {"bound": "hbm" if hbm else "mfma", "achieved": round(gbs if hbm else tf, 2),
-               "peak": HBM_PEAK_GBS if hbm else MFMA_F32_PEAK_TF,
+               "peak": HBM_PEAK_GBS if hbm else mpeak,
                "unit": "GB/s" if hbm else "TFLOP/s", "frac": round(max(f_hbm, f_mfma), 4),
                "frac_hbm": round(f_hbm, 4), "frac_mfma": round(f_mfma, 4),
                "achieved_GBps": round(gbs, 1), "achieved_TFLOPs": round(tf, 2),
                "traffic": round(traffic) if traffic else None, "traffic_source": tsrc,
                "pmc_GBps": round(traffic / sec / 1e9, 1) if traffic else None,
                "frac_pmc_hbm": round(traffic / sec / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
-               "kernel": f"{r['entry']} -> {r['kernel']} (fp32 MFMA + CSR gather, tile.hip)",
+               "kernel": f"{r['entry']} -> {r['kernel'] or 'its kernels'} ({what})",
                "trace_name": r["kernel"], "calls_per_step": r["calls_per_step"],
                "avg_launch_ms": r["avg_launch_ms"],
                "bytes_per_launch": r["bytes_per_launch"],
@@ -723,6 +779,10 @@ def pmc_traffic(trace_name: str, workload: str | None = None):
     for pre in prefixes:
         for k, v in data.items():
             if k.startswith(pre):
+                return v["bytes_per_launch"], v["source"]
+    if workload and "::" in trace_name and "(" not in trace_name:  # a bare kernel name
+        for k, v in data.items():
+            if k.startswith(f"{workload}:") and trace_name in k:
                 return v["bytes_per_launch"], v["source"]
     return None, None
 
@@ -1091,7 +1151,7 @@ def main():
                                     GraphStats(b, kind))
         out["entries"] = rows[:16]
         out["entries_total"] = tot
-        if args.workload in ("c4", "c5k4", "c5k16"):
+        if args.workload in ("c4", "c5k4", "c5k16") or "roofline" not in out:
             out["roofline"], out["roofline_next"] = layer_roofline(rows, args.workload)
     if rank == 0 and not args.no_kernel_timing:
         out["knn_graph"] = time_knn(b, wl, dev)

@@ -464,7 +464,7 @@ int lgnn_gat_bwd_node(const int32_t* tptr, const int32_t* tidx, const int32_t* t
  *   L+1 device pointers; widths[l] = output width of layer l. All widths and d_in <= 128,
  *   multiples of 4; L + 1 <= 8.
  *   tile_open (required when L >= 1): only tiles with tile_open[t] == 0 are computed — their
- *   CSR entries stay inside the tile and number at most 1024 (lgnn_graph_build /
+ *   CSR entries stay inside the tile and number at most 2048 (lgnn_graph_build /
  *   lgnn_tile_open flags); run the others with lgnn_node_linear_fwd_tiles(..., tile_open, 1).
  * ------------------------------------------------------------------------------------------- */
 int lgnn_gcn_stack_fwd(const float* X, int64_t M, int d_in, int has_in_proj,
@@ -505,7 +505,7 @@ int lgnn_gcn_stack_bwd_s3(const float* dP, const int64_t* batch, const int32_t* 
                           float* const* dWp, float* const* dbp, int num_partials, float* dz_ws,
                           const int32_t* tile_open, void* stream);
 /* Tiles: 64 consecutive node rows. open[t] = 1 when an edge joins tile t to another tile (its
- * layers then depend on other tiles) or when the tile holds more than 1024 CSR entries; the
+ * layers then depend on other tiles) or when the tile holds more than 2048 CSR entries; the
  * fused stacks skip open tiles. open has lgnn_tile_count(N) + 1 entries: the last one counts the
  * open tiles (the *_tiles kernels with want_open = 1 return at once when it is 0). */
 int lgnn_tile_count(int64_t num_nodes);
@@ -625,7 +625,7 @@ int lgnn_gcn_stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t*
 
 /* ---------------------------------------------------------------------------------------------
  * The fused GCN stack with its open-tile phase in the same launch (no separate layer-by-layer
- * launches). Tiles flagged open (an edge leaves them, or > 1024 CSR entries) share no edge with
+ * launches). Tiles flagged open (an edge leaves them, or > 2048 CSR entries) share no edge with
  * closed tiles, so after the closed tiles the kernel runs them layer by layer in fp32 (the bodies
  * of lgnn_node_linear_fwd_tiles / _bwd_tiles) with a grid barrier between layers; with no open
  * tile (the count word of tile_open is 0) that phase is skipped. tile_open: the graph build's

@@ -25,9 +25,11 @@ constexpr int kFinT = 64;          // k_finish: rows (threads) per block
 constexpr int kFinishCap = 1536;   // staged CSR entries per k_finish block
 constexpr int kLongRow = 24;       // k_finish: longer staged rows are sorted by the whole wave
 // Target-sorted fast path (k_prep_sorted + the sorted body of k_scan): rows of at most
-// kSortedRowCap CSR entries (a 64-row tile then stays within the fused kernels' 1024 staged
-// entries), runs of at most kGapCap rows without entries, at most one self loop per row
-constexpr int kSortedRowCap = 16;
+// kSortedRowCap CSR entries (a 64-row tile then stays within the fused kernels' CAPE_TILE
+// entries: k <= 32, the reference sweep's range), runs of at most kGapCap rows without entries,
+// at most one self loop per row
+constexpr int kSortedRowCap = 32;
+static_assert(kSortedRowCap * 64 <= lgnn_tile::CAPE_TILE, "a sorted tile fits the closed cap");
 constexpr int kGapCap = 64;
 constexpr int kVerdictMax = 1024;  // k_prep_sorted workgroups (one verdict word each)
 constexpr int kSortedChunks = 2;   // k_prep_sorted: 64-edge chunks per wave pass (more waves in flight)
@@ -632,7 +634,7 @@ __device__ __forceinline__ void scan_body(const int32_t* __restrict__ cnt,
     int ts = s;            // (a 64-row tile = 16 threads' elements; tiles never straddle blocks)
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) ts += __shfl_xor(ts, o, 64);
-    if ((tid & 15) == 0 && i0 < N && ts > 1024) {
+    if ((tid & 15) == 0 && i0 < N && ts > lgnn_tile::CAPE_TILE) {
       const int64_t t = i0 >> 6;
       if (tile_open[t] == 0) mark_open(tile_open, t, (N + 63) >> 6);
     }
@@ -959,7 +961,7 @@ __device__ __forceinline__ void finish_body(int64_t N, int64_t E, int add_loop, 
     }
     if (marks && i < N && (i & 63) == 0) {
       const int64_t iend64 = i + 64 < N ? i + 64 : N;
-      if (ptr[iend64] - ptr[i] > 1024) mark_open(tile_open, i >> 6, ntiles);
+      if (ptr[iend64] - ptr[i] > lgnn_tile::CAPE_TILE) mark_open(tile_open, i >> 6, ntiles);
     }
     sync();  // the staging arrays are free for the next virtual block
     return;
@@ -976,12 +978,12 @@ __device__ __forceinline__ void finish_body(int64_t N, int64_t E, int add_loop, 
     }
   }
   // 64-node tiles an edge leaves (source CSR pass) are open: the fused layer stacks skip them.
-  // So are tiles with more CSR entries than a tile stages in LDS (lgnn_tile CAPE = 1024).
+  // So are tiles with more CSR entries than a closed tile takes (lgnn_tile::CAPE_TILE).
   // flag setter: the first writer of a tile also counts it (tile_open[ntiles])
   auto mark = [&](int64_t t) { mark_open(tile_open, t, (N + 63) >> 6); };
   if (tile_open && !tr && i < N && (i & 63) == 0) {
     const int64_t iend64 = i + 64 < N ? i + 64 : N;
-    if (ptr[iend64] - ptr[i] > 1024) mark(i >> 6);
+    if (ptr[iend64] - ptr[i] > lgnn_tile::CAPE_TILE) mark(i >> 6);
   }
   if (tile_open && !tr && i < N) {
     const int r0 = ptr[i], r1 = ptr[i + 1];

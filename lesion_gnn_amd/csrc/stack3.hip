@@ -239,7 +239,7 @@ __global__ __launch_bounds__(NT, 2) void k_s3_fwd(const float* __restrict__ X, i
     }
     lds_barrier();
     S3STAMP();  // 1: prologue (X planes) + B1
-    adj_scatter<false>(scr, sm.rp, R, r0);
+    adj_scatter<false>(scr, sm.rp, R, r0, col, w);
     if (has_next) idx_load_head(R, rowptr, M, tn * TM);
     f32x16 z0 = {}, z1 = {};
     if (FIRST) {

@@ -164,7 +164,7 @@ __global__ __launch_bounds__(NT, 2) void k_s3_bwd(const int32_t* __restrict__ ro
     }
     lds_barrier();
     if (AGG) {
-      adj_scatter<true>(scr, sm.rp, R, r0);
+      adj_scatter<true>(scr, sm.rp, R, r0, col, w);
       if (has_next) idx_load_head(R, rowptr, M, tn * TM);
     }
     // dZ_l in P layout (feature n = 32 wave + li on the lane)
@@ -794,7 +794,7 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
     lds_barrier();  // ... in every wave; the staging above is visible
     STAMP(stamp++);
     if constexpr (!AG) {
-      adj_scatter<true>(scr, sm.rp, R, r0);
+      adj_scatter<true>(scr, sm.rp, R, r0, col, w);
       if (has_next) idx_load_head(R, rowptr, M, tn * TM);
     }
     // dZ_L = pool broadcast of dP (/ |graph|) * ELU'(H_L), P layout (feature n on the lane)

@@ -145,7 +145,7 @@ __global__ __launch_bounds__(NT, 2) void k_stack_fwd(const float* __restrict__ X
     }
     __syncthreads();
     STAMP(stamp++);
-    if (any_conv && !(ABL & 64)) adj_scatter<true>(AdjT, sm.rp, R, r0);
+    if (any_conv && !(ABL & 64)) adj_scatter<true>(AdjT, sm.rp, R, r0, col, w);
     if (has_next) {
       load_rows(xr, bX, K0, (int)(tn * TM));
       if (any_conv) idx_load_head(R, rowptr, M, tn * TM);
@@ -427,7 +427,7 @@ __global__ __launch_bounds__(NTB, 1) void k_stack_bwd(const float* __restrict__ 
     const bool has_next = tn < ntiles;
     if (tid <= TM) sm.rp[tid] = R.rp;
     __syncthreads();  // rp visible, Adj zero
-    adj_scatter<false>(Adj, sm.rp, R, r0);
+    adj_scatter<false>(Adj, sm.rp, R, r0, col, w);
     {
       const int N = a.width[L + 1];
       f32x4 dsum = zero4();
@@ -617,7 +617,7 @@ __global__ __launch_bounds__(NTB, 1) void k_stack_bwd(const float* __restrict__ 
 }
 
 // open[t] = 1 if an edge joins a node of tile t with a node of another tile (target CSR), or
-// if the tile holds more than CAPE CSR entries.
+// if the tile holds more than CAPE_TILE CSR entries.
 __global__ __launch_bounds__(NT) void k_tile_open(const int32_t* __restrict__ rowptr,
                                                   const int32_t* __restrict__ col, int64_t M,
                                                   int32_t* __restrict__ open) {
@@ -629,7 +629,7 @@ __global__ __launch_bounds__(NT) void k_tile_open(const int32_t* __restrict__ ro
     };
     if (i % TM == 0) {
       const int64_t ie = i + TM < M ? i + TM : M;
-      if (rowptr[ie] - rowptr[i] > CAPE) mark(ti);
+      if (rowptr[ie] - rowptr[i] > CAPE_TILE) mark(ti);
     }
     const int e0 = rowptr[i], e1 = rowptr[i + 1];
     for (int e = e0; e < e1; ++e) {

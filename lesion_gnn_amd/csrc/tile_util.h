@@ -41,7 +41,11 @@ constexpr int TM = 64;
 constexpr int KC = 128;
 constexpr int LDS = KC + 4;
 constexpr int NT = 256;
-constexpr int CAPE = 1024;     // CSR entries of a closed tile (the fused stack kernels)
+constexpr int CAPE = 1024;     // CSR entries of a closed tile staged in registers (the fused
+                               // stack kernels; a closed tile's entries past them are read from
+                               // global memory as its Â is built: adj_scatter)
+constexpr int CAPE_TILE = 2048;  // CSR entries of a closed tile (64 x 32: the reference sweep's
+                                 // largest k, scripts/sweep.py:110); more -> the tile is open
 constexpr int CAPE_LW = 1280;  // CSR entries staged by the layer-wise tile bodies (64 x (16 + 1)
                                // at k = 16 fits; 5 per thread)
 constexpr int EB = 8;
@@ -159,7 +163,8 @@ __device__ __forceinline__ void idx_load_head(IdxRegsT<NTH, CAP>& R, const int32
 template <int NTH, int CAP>
 __device__ __forceinline__ void idx_load_body(IdxRegsT<NTH, CAP>& R, const int32_t* __restrict__ col,
                                               const float* __restrict__ w, int tid_ = -1) {
-  if (R.ne > CAP) return;
+  // (a closed tile of up to CAPE_TILE entries stages its first CAPE; adj_scatter reads the rest)
+  if (R.ne > CAP && !(CAP == CAPE && R.ne <= CAPE_TILE)) return;
   const int tid = tid_ < 0 ? (int)threadIdx.x : tid_;
 #pragma unroll
   for (int u = 0; u < CAP / NTH; ++u) {
@@ -202,25 +207,40 @@ __device__ __forceinline__ int idx_store(TileIdx& ti, const IdxRegsT<NTH, CAP>& 
 // Dense Â_tile from the tile's row-CSR block (entry j of R: source R.c, weight R.w; its target
 // row found by binary search over rp): Adj[target][source] (TRANS = false) or Adj[source][target]
 // (TRANS = true), row stride TM. Adj must be zero and rp visible. Duplicate (target, source)
-// pairs carry equal weights, so the LDS float adds are order independent.
+// pairs carry equal weights, so the LDS float adds are order independent. A closed tile with
+// more than CAPE entries (k > 16 neighbours at 64 nodes, up to CAPE_TILE) adds the rest straight
+// from the CSR (col / w, the tile's entries past the staged ones) — before R is reloaded for the
+// next tile.
+__device__ __forceinline__ int adj_row(const int* rp, int e) {
+  int lo = 0, hi = TM;
+#pragma unroll
+  for (int it = 0; it < 6; ++it) {
+    const int mid = (lo + hi) >> 1;
+    if (rp[mid] <= e) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
 template <bool TRANS, int NTH>
 __device__ __forceinline__ void adj_scatter(float* Adj, const int* rp, const IdxRegsT<NTH>& R,
-                                            int64_t r0, int tid_ = -1) {
+                                            int64_t r0, const int32_t* __restrict__ col,
+                                            const float* __restrict__ w, int tid_ = -1) {
   const int tid = tid_ < 0 ? (int)threadIdx.x : tid_;
 #pragma unroll
   for (int u = 0; u < CAPE / NTH; ++u) {
     const int j = tid + u * NTH;
     if (j < R.ne) {
-      const int e = R.eb + j;
-      int lo = 0, hi = TM;
-#pragma unroll
-      for (int it = 0; it < 6; ++it) {
-        const int mid = (lo + hi) >> 1;
-        if (rp[mid] <= e) lo = mid;
-        else hi = mid;
-      }
+      const int lo = adj_row(rp, R.eb + j);
       const int c = R.c[u] - (int)r0;
       atomicAdd(&Adj[TRANS ? c * TM + lo : lo * TM + c], R.w[u]);
+    }
+  }
+  if (R.ne > CAPE) {  // block-uniform
+    for (int j = CAPE + tid; j < R.ne; j += NTH) {
+      const int e = R.eb + j;
+      const int lo = adj_row(rp, e);
+      const int c = col[e] - (int)r0;
+      atomicAdd(&Adj[TRANS ? c * TM + lo : lo * TM + c], w ? w[e] : 1.f);
     }
   }
 }

@@ -33,7 +33,8 @@ def test_fused_ce_bitwise_equals_unfused(cuda, case):
     if case == "ragged":
         b = synth.make_batch(96, k=8, d_in=128, seed=5, sizes="powerlaw")
     else:
-        b = synth.make_batch(256, n=64, k=8, d_in=128, seed=4)
+        # the bench's C2 batch size (BASELINE configs[1]: 1024 graphs)
+        b = synth.make_batch(1024, n=64, k=8, d_in=128, seed=4)
     w = torch.tensor([0.5, 2.0, 1.0, 3.0, 0.25], device=cuda) if case == "weighted" else None
     m = _model(cuda)
     x, ei, bt, y = (t.to(cuda) for t in (b.x, b.edge_index, b.batch, b.y))

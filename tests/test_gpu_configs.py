@@ -27,8 +27,8 @@ import oracle.pyg_ref as ref
 pytestmark = pytest.mark.gpu
 
 CASES = [("c2", 1024), ("c3", 1024), ("c3f32", 1024), ("c4", 8192), ("c5k4", 1024),
-         ("c5k16", 1024), ("refcfg", 1024), ("sweep_gcn3", 1024), ("sweep_gat256h8", 256),
-         ("sweep_gin512", 256)]
+         ("c5k16", 1024), ("refcfg", 1024), ("sweep_gcn3", 1024), ("sweep_gat256h8", 1024),
+         ("sweep_gin512", 1024)]
 
 
 def run_step(wl, model, b, dev, oracle, masks=None):

@@ -297,11 +297,13 @@ def test_tile_open_flags(cuda):
 
 @pytest.mark.parametrize("bwd", ["f32", "s3", "s3f"])
 @pytest.mark.parametrize("case", ["c2_L2", "irregular_L2", "irregular_L1_add", "dense_tiles",
-                                  "c2_L3"])
+                                  "wide_tiles", "c2_L3"])
 def test_gcn_fused_backward(cuda, case, bwd, monkeypatch):
     """lgnn_gcn_stack_bwd (closed tiles, fused) + masked accumulating layer-wise backward (open
-    tiles) vs the layer-wise backward and the oracle. dense_tiles: 64-node graphs with k = 20
-    (1344 CSR entries per tile > the 1024 a tile stages) are flagged open by the graph build.
+    tiles) vs the layer-wise backward and the oracle. dense_tiles: 64-node graphs with k = 40
+    (2560 CSR entries per tile > the 2048 a closed tile takes) are flagged open by the graph
+    build. wide_tiles: k = 20 and k = 32 (1280 and 2048 entries: closed tiles whose entries past
+    the 1024 staged in registers are read from the CSR as the tile's Â is built).
     c2_L3: three convs (fp32: layer-wise backward on recomputed aggregates; split-3: fused).
     bwd: the fp32 fused kernel (lgnn_gcn_stack_bwd), the split-3 layer-major kernels
     (lgnn_gcn_stack_bwd_s3) or the fused split-3 kernel (lgnn_gcn_stack_bwd_s3f; L <= 2, so c2_L3
@@ -311,16 +313,24 @@ def test_gcn_fused_backward(cuda, case, bwd, monkeypatch):
     if case.startswith("c2"):
         b = synth.make_batch(300, n=64, k=8, d_in=128, seed=31)
     elif case == "dense_tiles":
-        b = synth.make_batch(6, n=64, k=20, d_in=128, seed=32, sizes=[64, 64, 30, 34, 64, 64])
+        b = synth.make_batch(6, n=64, k=40, d_in=128, seed=32, sizes=[64, 64, 30, 34, 64, 64])
+    elif case == "wide_tiles":
+        b1 = synth.make_batch(3, n=64, k=20, d_in=128, seed=34)
+        b2 = synth.make_batch(3, n=64, k=32, d_in=128, seed=35)
+        b = synth.Batch(torch.cat([b1.x, b2.x]),
+                        torch.cat([b1.edge_index, b2.edge_index + b1.num_nodes], 1),
+                        torch.cat([b1.batch, b2.batch + 3]), None, torch.cat([b1.y, b2.y]),
+                        None, 6)
     else:
         b = synth.make_batch(9, k=6, d_in=128, seed=33, sizes=[1, 5, 64, 200, 2, 33, 512, 17, 64])
     ours, oref = make_pair(hidden, pool=pool)
     ours = ours.to(cuda)
     monkeypatch.setattr(ops, "BWD_MODE", bwd)
     monkeypatch.setattr(ops, "BWD_S3", bwd != "f32")
-    if case == "dense_tiles":
+    if case in ("dense_tiles", "wide_tiles"):
         g = Graph(b.edge_index.to(cuda), b.num_nodes)
-        assert g.tile_open("gcn").cpu().tolist()[:6] == [1, 1, 1, 1, 1, 5]
+        want = [1, 1, 1, 1, 1, 5] if case == "dense_tiles" else [0, 0, 0, 0, 0, 0]
+        assert g.tile_open("gcn").cpu().tolist()[:6] == want
     monkeypatch.setattr(ops, "FUSED_BWD", True)
     lf, _, gf = run_step(ours, b, cuda)
     monkeypatch.setattr(ops, "FUSED_BWD", False)
@@ -408,7 +418,7 @@ def test_head_backward_folded_into_stack(cuda, classes, pool, monkeypatch):
 @pytest.mark.parametrize("case", ["aligned", "ragged", "capacity"])
 def test_lazy_transpose_build(cuda, case):
     """lgnn_graph_build_lazy (the fused GCN stack's build): the target CSR and the tile flags
-    (cross edges marked in the count pass, the > 1024-entry capacity rule in the scan) equal the
+    (cross edges marked in the count pass, the > 2048-entry capacity rule in the scan) equal the
     full build's bit for bit; the source CSR (tptr / tidx / tw) is built exactly when some tile
     is open (ragged graphs, dense tiles) and then equals the full build's (aligned k-NN input
     takes the target-sorted path, which leaves it unwritten)."""
@@ -417,7 +427,7 @@ def test_lazy_transpose_build(cuda, case):
     elif case == "ragged":
         b = synth.make_batch(9, k=6, d_in=8, seed=52, sizes=[1, 5, 64, 200, 2, 33, 512, 17, 64])
     else:
-        b = synth.make_batch(6, n=64, k=20, d_in=8, seed=53, sizes=[64, 64, 64, 64, 64, 64])
+        b = synth.make_batch(6, n=64, k=40, d_in=8, seed=53, sizes=[64, 64, 64, 64, 64, 64])
     g = Graph(b.edge_index.to(cuda), b.num_nodes)
     g.keep_build_workspace = True  # build_path() below
     full, lazy = g.csr("gcn"), g.csr("gcn_lazy")

@@ -56,6 +56,8 @@ def _sorted_cases():
     noloop = synth.make_batch(40, n=64, k=8, seed=6, loop=False)
     k16 = synth.make_batch(16, n=64, k=16, seed=7)
     k17 = synth.make_batch(16, n=64, k=17, seed=8)
+    k32 = synth.make_batch(16, n=64, k=32, seed=13)
+    k33 = synth.make_batch(16, n=64, k=33, seed=14)
     keep = ei[1] != 5  # node 5 receives nothing: a one-row gap
     # a duplicated non-loop edge inside row 9 (kept, in order) and a second self loop in row 12
     r9 = int((ei[1] == 9).nonzero()[1])
@@ -77,7 +79,9 @@ def _sorted_cases():
         "gap_row": ((ei[:, keep], n), "sorted"),
         "trailing_isolated": ((ei, n + 20), "sorted"),
         "dup_edge": ((dup, n), "sorted"),
-        "k17": ((k17.edge_index, k17.num_nodes), "general"),
+        "k17": ((k17.edge_index, k17.num_nodes), "sorted"),
+        "k32": ((k32.edge_index, k32.num_nodes), "sorted"),  # 2048 entries per tile: closed
+        "k33": ((k33.edge_index, k33.num_nodes), "general"),  # rows past kSortedRowCap
         "two_loops": ((two, n), "general"),
         "trailing_gap": ((ei, n + 200), "general"),
         # ragged graphs: target-sorted, but edges leave their 64-row tiles (the lazy build then
