@@ -64,6 +64,10 @@ def _sorted_cases():
     dup = torch.cat([ei[:, :r9 + 1], ei[:, r9:]], 1)
     r12 = int((ei[1] == 12).nonzero()[0])
     two = torch.cat([ei[:, :r12], torch.tensor([[12], [12]]), ei[:, r12:]], 1)
+    # every one of 1024 target rows takes 31 sources from the first 64-row tile: source rows of
+    # ~500 entries (the source CSR's long-row sort)
+    d = torch.arange(1024).repeat_interleave(31)
+    hub = torch.stack([(d * 7 + torch.arange(31).repeat(1024)) % 64, d])
     return {
         "knn_c2": ((ei, n), "sorted"),
         "knn_noloop": ((noloop.edge_index, noloop.num_nodes), "sorted"),
@@ -82,6 +86,7 @@ def _sorted_cases():
         "k17": ((k17.edge_index, k17.num_nodes), "sorted"),
         "k32": ((k32.edge_index, k32.num_nodes), "sorted"),  # 2048 entries per tile: closed
         "k33": ((k33.edge_index, k33.num_nodes), "general"),  # rows past kSortedRowCap
+        "hub_rows": ((hub, 1024), "sorted_open"),
         "two_loops": ((two, n), "general"),
         "trailing_gap": ((ei, n + 200), "general"),
         # ragged graphs: target-sorted, but edges leave their 64-row tiles (the lazy build then

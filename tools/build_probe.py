@@ -1,0 +1,28 @@
+"""Graph-build timing probe: builds the CSR of one bench workload's batch `reps` times (eager,
+no model), so rocprofv3 can time the build kernels alone. Usage (GPU box):
+  rocprofv3 --kernel-trace --stats -d <dir> -- python3 tools/build_probe.py <workload> <kind> [reps]
+kind: gcn_lazy | gcn | gin | gat"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from lesion_gnn_amd.graph import Graph  # noqa: E402
+
+
+def main():
+    wl, kind = sys.argv[1], sys.argv[2]
+    reps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+    dev = torch.device("cuda", 0)
+    b = bench.make_batch(bench.WORKLOADS[wl], 1024, seed=100).to(dev)
+    for _ in range(reps):
+        g = Graph(b.edge_index, b.num_nodes, b.batch, b.num_graphs)
+        g.csr(kind)
+    torch.cuda.synchronize(dev)
+    print(wl, kind, "nodes", b.num_nodes, "edges", b.num_edges)
+
+
+if __name__ == "__main__":
+    main()
