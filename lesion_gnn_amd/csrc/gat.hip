@@ -38,6 +38,12 @@ constexpr float EPS16 = 1e-16f;
 #endif
 
 __device__ __forceinline__ float leaky(float v, float slope) { return v > 0.f ? v : v * slope; }
+// a value the compiler cannot see into: a sum of such terms is never fused with their products,
+// so kernels whose instruction selection differs still round it alike (the bitwise pairs)
+__device__ __forceinline__ float opaque(float v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
 
 // Raw buffer access (SGPR descriptor + 32-bit byte offset): one VGPR per gathered address instead
 // of two, which is what bounds these gather kernels' registers (8 source rows in flight). Every
@@ -415,7 +421,7 @@ __global__ __launch_bounds__(NT) GAT_OCC void k_gat_bwd_edge(
         if (e0 + u < e1) {
           const float pre = bld1(bA, (uint32_t)(c[u] * H + head) * 4u) + ad;
           const float da = al[u] * (d[u] - s_i) * (pre > 0.f ? 1.f : slope);
-          dad += da;
+          dad += opaque(da);  // (never contracted with da's product: every form alike)
           if (P.leader) bst1(bDa, (uint32_t)((e0 + u) * H + head) * 4u, da);
         }
       }
@@ -450,7 +456,7 @@ __global__ __launch_bounds__(NT) GAT_OCC void k_gat_bwd_edge(
             const float pre = bld1(bA, (uint32_t)(c[u] * H + head) * 4u) + ad;
             const float da = al * (d - s_i) * (pre > 0.f ? 1.f : slope);
             if (e + u < e1) {
-              dad += da;
+              dad += opaque(da);  // (never contracted with da's product: every form alike)
               if (P.leader) bst1(bDa, eo, da);
             }
           }
@@ -615,6 +621,8 @@ __device__ __forceinline__ RowWalk row_walk(int64_t M) {
 struct EdgeLane {
   int li, hwb, u, hh, hq;  // lane in the half wave, half-wave base lane, edge slot, head slot
   bool hv;                  // hh < H
+  int hh2, hq2;             // 8 heads (HS = 2): the lane's second head, hh + 4
+  bool hv2;
   __device__ __forceinline__ EdgeLane(int H) {
     const int lane = threadIdx.x & 63;
     li = lane & 31;
@@ -623,12 +631,32 @@ struct EdgeLane {
     hh = li >> 3;
     hv = hh < H;
     hq = hv ? hh : 0;
+    hh2 = hh + 4;
+    hv2 = hh2 < H;
+    hq2 = hv2 ? hh2 : 0;
   }
   // CSR position of edge slot u of the batch starting at b (clamped into the row)
   __device__ __forceinline__ int pos(int b, int e1) const { return b + (b + u < e1 ? u : 0); }
 };
 
-template <int ACT>
+// Head slots per edge lane: HS = 1 for H <= 4 (lane u + 8 h: edge u, head h), HS = 2 for
+// 5..8 heads (the same lane also holds head h + 4 in a second register: 8 heads of C <= 16, the
+// sweep's heads 8 at widths <= 128). A feature lane of head h reads its head's per-edge value
+// from lane 8 (h & 3) + k of its half wave, in register (h >> 2).
+template <int HS>
+__device__ __forceinline__ float head_perm(float v1, float v2, int base, int k, int head) {
+  const float x1 = bperm_f(v1, base + k);
+  if constexpr (HS == 1) {
+    (void)v2;
+    (void)head;
+    return x1;
+  } else {
+    const float x2 = bperm_f(v2, base + k);
+    return head >= 4 ? x2 : x1;
+  }
+}
+
+template <int ACT, int HS>
 __global__ __launch_bounds__(NT) void k_gat_fwd_p(const int32_t* __restrict__ rowptr,
                                                   const int32_t* __restrict__ col,
                                                   const float* __restrict__ XP,
@@ -642,13 +670,14 @@ __global__ __launch_bounds__(NT) void k_gat_fwd_p(const int32_t* __restrict__ ro
   const EdgeLane L(H);
   const int HC = H * C;
   const Pass<1> P(0, L.li, HC, C);
-  const int hbase = L.hwb + 8 * P.head;  // this feature lane's head: its edge lanes
+  const int hbase = L.hwb + 8 * (P.head & 3);  // this feature lane's head: its edge lanes
   RowWalk W = row_walk(M);
   if (W.r >= W.rend) return;
   const int64_t cap = rowptr[M];
   const Buf bR = mkbuf(rowptr, (M + 1) * 4), bC = mkbuf(col, cap * 4);
   const Buf bX = mkbuf(XP, M * HC * 4), bA = mkbuf(a_s, M * H * 4), bD = mkbuf(a_d, M * H * 4);
   const Buf bAl = mkbuf(alpha, alpha ? cap * H * 4 : 0), bM = mkbuf(mask, mask ? cap * H * 4 : 0);
+  const bool two = HS == 2;
   int64_t r = W.r;
   int e0 = bldi(bR, (uint32_t)r * 4u), e1 = bldi(bR, (uint32_t)r * 4u + 4u);
   int cu = bldi(bC, (uint32_t)L.pos(e0, e1) * 4u);
@@ -662,6 +691,12 @@ __global__ __launch_bounds__(NT) void k_gat_fwd_p(const int32_t* __restrict__ ro
     const float a = bld1(bA, (uint32_t)(cu * H + L.hq) * 4u);
     const float ad = bld1(bD, (uint32_t)(r * H + L.hq) * 4u);
     const float mk = mask ? bld1(bM, (uint32_t)(eu * H + L.hq) * 4u) : 1.f;
+    float a2 = 0.f, ad2 = 0.f, mk2 = 1.f;
+    if (two) {
+      a2 = bld1(bA, (uint32_t)(cu * H + L.hq2) * 4u);
+      ad2 = bld1(bD, (uint32_t)(r * H + L.hq2) * 4u);
+      mk2 = mask ? bld1(bM, (uint32_t)(eu * H + L.hq2) * 4u) : 1.f;
+    }
     f32x4 xv[EB];
 #pragma unroll
     for (int k = 0; k < EB; ++k)
@@ -673,7 +708,7 @@ __global__ __launch_bounds__(NT) void k_gat_fwd_p(const int32_t* __restrict__ ro
     const int e0nn = bldi(bR, ron), e1nn = bldi(bR, ron + 4u);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     if (deg <= EB) {
-      const bool ev = L.u < deg && L.hv;
+      const bool ev = L.u < deg && L.hv, ev2 = L.u < deg && L.hv2;
       const float lg = leaky(a + ad, slope);
       const float m = max8(ev ? lg : -INFINITY);
       const float ex = ev ? expf(lg - m) : 0.f;
@@ -684,28 +719,53 @@ __global__ __launch_bounds__(NT) void k_gat_fwd_p(const int32_t* __restrict__ ro
       const float al = ex / sum;
       if (alpha && ev) bst1(bAl, (uint32_t)(eu * H + L.hh) * 4u, al);
       const float alm = mask ? al * mk : al;
+      float alm2 = 0.f;
+      if (two) {  // the second head slot: the same operations
+        const float lg2 = leaky(a2 + ad2, slope);
+        const float m2 = max8(ev2 ? lg2 : -INFINITY);
+        const float ex2 = ev2 ? expf(lg2 - m2) : 0.f;
+        float sum2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < EB; ++k) sum2 += bperm_f(ex2, L.hwb + 8 * L.hh + k);
+        sum2 += EPS16;
+        const float al2 = ex2 / sum2;
+        if (alpha && ev2) bst1(bAl, (uint32_t)(eu * H + L.hh2) * 4u, al2);
+        alm2 = mask ? al2 * mk2 : al2;
+      }
 #pragma unroll
       for (int k = 0; k < EB; ++k) {
-        const float w = bperm_f(alm, hbase + k);
+        const float w = head_perm<HS>(alm, alm2, hbase, k, P.head);
         if (k < deg) acc += w * xv[k];
       }
     } else {  // long row: max, denominator, messages, each a walk over batches of EB entries
-      float m = -INFINITY;
+      float m = -INFINITY, m2 = -INFINITY;
       for (int b = e0; b < e1; b += EB) {
         const int c = bldi(bC, (uint32_t)L.pos(b, e1) * 4u);
         const float lg = leaky(bld1(bA, (uint32_t)(c * H + L.hq) * 4u) + ad, slope);
         if (b + L.u < e1 && L.hv) m = fmaxf(m, lg);
+        if (two) {
+          const float lg2 = leaky(bld1(bA, (uint32_t)(c * H + L.hq2) * 4u) + ad2, slope);
+          if (b + L.u < e1 && L.hv2) m2 = fmaxf(m2, lg2);
+        }
       }
       m = max8(m);
-      float sum = 0.f;
+      if (two) m2 = max8(m2);
+      float sum = 0.f, sum2 = 0.f;
       for (int b = e0; b < e1; b += EB) {
         const int c = bldi(bC, (uint32_t)L.pos(b, e1) * 4u);
         const float lg = leaky(bld1(bA, (uint32_t)(c * H + L.hq) * 4u) + ad, slope);
         const float ex = b + L.u < e1 && L.hv ? expf(lg - m) : 0.f;
 #pragma unroll
         for (int k = 0; k < EB; ++k) sum += bperm_f(ex, L.hwb + 8 * L.hh + k);
+        if (two) {
+          const float lg2 = leaky(bld1(bA, (uint32_t)(c * H + L.hq2) * 4u) + ad2, slope);
+          const float ex2 = b + L.u < e1 && L.hv2 ? expf(lg2 - m2) : 0.f;
+#pragma unroll
+          for (int k = 0; k < EB; ++k) sum2 += bperm_f(ex2, L.hwb + 8 * L.hh + k);
+        }
       }
       sum += EPS16;
+      sum2 += EPS16;
       for (int b = e0; b < e1; b += EB) {
         const int eb = L.pos(b, e1);
         const bool ev = b + L.u < e1 && L.hv;
@@ -719,9 +779,18 @@ __global__ __launch_bounds__(NT) void k_gat_fwd_p(const int32_t* __restrict__ ro
         const float al = (ev ? expf(lg - m) : 0.f) / sum;
         if (alpha && ev) bst1(bAl, (uint32_t)(eb * H + L.hh) * 4u, al);
         const float alm = mask ? al * mb : al;
+        float alm2 = 0.f;
+        if (two) {
+          const bool ev2 = b + L.u < e1 && L.hv2;
+          const float lg2 = leaky(bld1(bA, (uint32_t)(c * H + L.hq2) * 4u) + ad2, slope);
+          const float mb2 = mask ? bld1(bM, (uint32_t)(eb * H + L.hq2) * 4u) : 1.f;
+          const float al2 = (ev2 ? expf(lg2 - m2) : 0.f) / sum2;
+          if (alpha && ev2) bst1(bAl, (uint32_t)(eb * H + L.hh2) * 4u, al2);
+          alm2 = mask ? al2 * mb2 : al2;
+        }
 #pragma unroll
         for (int k = 0; k < EB; ++k) {
-          const float w = bperm_f(alm, hbase + k);
+          const float w = head_perm<HS>(alm, alm2, hbase, k, P.head);
           if (b + k < e1) acc += w * xb[k];
         }
       }
@@ -770,7 +839,7 @@ __device__ __forceinline__ f32x4 dz_row(int64_t r, int HC, int fc, const float* 
   return dz;
 }
 
-template <int ACT, bool POOL>
+template <int ACT, bool POOL, int HS>
 __global__ __launch_bounds__(NT) void k_gat_bwd_edge_p(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const float* __restrict__ XP, const float* __restrict__ a_s, const float* __restrict__ a_d,
@@ -780,8 +849,10 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_edge_p(
   const EdgeLane L(H);
   const int HC = H * C;
   const Pass<1> P(0, L.li, HC, C);
-  const int hbase = L.hwb + 8 * P.head;
-  const int hlead = L.hwb + L.hq * P.G;  // the first feature lane of edge lane's head
+  const int hbase = L.hwb + 8 * (P.head & 3);
+  const int hlead = L.hwb + L.hq * P.G;    // the first feature lane of edge lane's head
+  const int hlead2 = L.hwb + L.hq2 * P.G;  // ... of its second head (HS = 2)
+  const bool two = HS == 2;
   RowWalk W = row_walk(M);
   if (W.r >= W.rend) return;
   const int64_t cap = rowptr[M];
@@ -802,6 +873,12 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_edge_p(
     const float mk = mask ? bld1(bM, (uint32_t)(eu * H + L.hq) * 4u) : 1.f;
     const float pre = bld1(bA, (uint32_t)(cu * H + L.hq) * 4u) +
                       bld1(bD, (uint32_t)(r * H + L.hq) * 4u);
+    float al2 = 0.f, mk2 = 1.f, pre2 = 0.f;
+    if (two) {
+      al2 = bld1(bAl, (uint32_t)(eu * H + L.hq2) * 4u);
+      mk2 = mask ? bld1(bM, (uint32_t)(eu * H + L.hq2) * 4u) : 1.f;
+      pre2 = bld1(bA, (uint32_t)(cu * H + L.hq2) * 4u) + bld1(bD, (uint32_t)(r * H + L.hq2) * 4u);
+    }
     f32x4 xv[EB];
 #pragma unroll
     for (int k = 0; k < EB; ++k)
@@ -820,20 +897,26 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_edge_p(
 #pragma unroll
       for (int k = 0; k < EB; ++k) {
         d[k] = group_sum(dot4(dz, xv[k]), P.G);
-        if (mask) d[k] *= bperm_f(mk, hbase + k);
-        alk[k] = bperm_f(al, hbase + k);
+        if (mask) d[k] *= head_perm<HS>(mk, mk2, hbase, k, P.head);
+        alk[k] = head_perm<HS>(al, al2, hbase, k, P.head);
         if (k < deg) s_i += alk[k] * d[k];
       }
-      float mine = 0.f;  // edge lane (u, h): the logit gradient of its edge and head
+      float mine = 0.f, mine2 = 0.f;  // edge lane (u, h): the logit gradient of its edge and head
 #pragma unroll
       for (int k = 0; k < EB; ++k) {
-        const float fk = bperm_f(pre > 0.f ? 1.f : slope, hbase + k);
+        const float fk = head_perm<HS>(pre > 0.f ? 1.f : slope, pre2 > 0.f ? 1.f : slope, hbase,
+                                       k, P.head);
         const float da = alk[k] * (d[k] - s_i) * fk;
-        if (k < deg) dad += da;
+        if (k < deg) dad += opaque(da);  // (never contracted with da's product: every form alike)
         const float t = bperm_f(da, hlead);
         mine = L.u == k ? t : mine;
+        if (two) {
+          const float t2 = bperm_f(da, hlead2);
+          mine2 = L.u == k ? t2 : mine2;
+        }
       }
       if (L.u < deg && L.hv) bst1(bDa, (uint32_t)(eu * H + L.hh) * 4u, mine);
+      if (two && L.u < deg && L.hv2) bst1(bDa, (uint32_t)(eu * H + L.hh2) * 4u, mine2);
     } else {  // long row: two walks over batches of EB entries (s_i, then the gradients)
       float s_i = 0.f;
 #pragma unroll 1
@@ -845,28 +928,42 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_edge_p(
           const float mb = mask ? bld1(bM, (uint32_t)(eb * H + L.hq) * 4u) : 1.f;
           const float preb = bld1(bA, (uint32_t)(c * H + L.hq) * 4u) +
                              bld1(bD, (uint32_t)(r * H + L.hq) * 4u);
+          float alb2 = 0.f, mb2 = 1.f, preb2 = 0.f;
+          if (two) {
+            alb2 = bld1(bAl, (uint32_t)(eb * H + L.hq2) * 4u);
+            mb2 = mask ? bld1(bM, (uint32_t)(eb * H + L.hq2) * 4u) : 1.f;
+            preb2 = bld1(bA, (uint32_t)(c * H + L.hq2) * 4u) +
+                    bld1(bD, (uint32_t)(r * H + L.hq2) * 4u);
+          }
           f32x4 xb[EB];
 #pragma unroll
           for (int k = 0; k < EB; ++k)
             xb[k] = bld4(bX, ((uint32_t)bperm_i(c, L.hwb + k) * HC + P.fc[0]) * 4u);
-          float mine = 0.f;
+          float mine = 0.f, mine2 = 0.f;
 #pragma unroll
           for (int k = 0; k < EB; ++k) {
             float dk = group_sum(dot4(dz, xb[k]), P.G);
-            if (mask) dk *= bperm_f(mb, hbase + k);
-            const float ak = bperm_f(alb, hbase + k);
-            const float fk = bperm_f(preb > 0.f ? 1.f : slope, hbase + k);
+            if (mask) dk *= head_perm<HS>(mb, mb2, hbase, k, P.head);
+            const float ak = head_perm<HS>(alb, alb2, hbase, k, P.head);
+            const float fk = head_perm<HS>(preb > 0.f ? 1.f : slope, preb2 > 0.f ? 1.f : slope,
+                                           hbase, k, P.head);
             if (sweep == 0) {
               if (b + k < e1) s_i += ak * dk;
             } else {
               const float da = ak * (dk - s_i) * fk;
-              if (b + k < e1) dad += da;
+              if (b + k < e1) dad += opaque(da);  // (never contracted with da's product: every form alike)
               const float t = bperm_f(da, hlead);
               mine = L.u == k ? t : mine;
+              if (two) {
+                const float t2 = bperm_f(da, hlead2);
+                mine2 = L.u == k ? t2 : mine2;
+              }
             }
           }
           if (sweep == 1 && b + L.u < e1 && L.hv)
             bst1(bDa, (uint32_t)(eb * H + L.hh) * 4u, mine);
+          if (two && sweep == 1 && b + L.u < e1 && L.hv2)
+            bst1(bDa, (uint32_t)(eb * H + L.hh2) * 4u, mine2);
         }
       }
     }
@@ -885,6 +982,7 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_edge_p(
 // source-row pass (see k_gat_bwd_node), one 128-feature strip, pipelined: the next row's first
 // batch of transpose entries (target row, target-CSR position) is in flight during this row's
 // gathers. Same per-workgroup partials (grid = lgnn_gat_bwd_num_partials).
+template <int HS>
 __global__ __launch_bounds__(NT) void k_gat_bwd_node_p(
     const int32_t* __restrict__ tptr, const int32_t* __restrict__ tidx,
     const int32_t* __restrict__ tmap, const float* __restrict__ alpha,
@@ -896,7 +994,8 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_node_p(
   const EdgeLane L(H);
   const int HC = H * C;
   const Pass<1> P(0, L.li, HC, C);
-  const int hbase = L.hwb + 8 * P.head;
+  const int hbase = L.hwb + 8 * (P.head & 3);
+  const bool two = HS == 2;
   const int hw = (threadIdx.x >> 6) * 2 + ((threadIdx.x & 63) >> 5);
   f32x4 ps = {0.f, 0.f, 0.f, 0.f}, pd = ps, pb = ps;
   RowWalk W = row_walk(M);
@@ -917,6 +1016,12 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_node_p(
       float alu = bld1(bAl, (uint32_t)(pu * H + L.hq) * 4u);
       const float mk = mask ? bld1(bM, (uint32_t)(pu * H + L.hq) * 4u) : 1.f;
       const float dau = bld1(bDa, (uint32_t)(pu * H + L.hq) * 4u);
+      float alu2 = 0.f, mk2 = 1.f, dau2 = 0.f;
+      if (two) {
+        alu2 = bld1(bAl, (uint32_t)(pu * H + L.hq2) * 4u);
+        mk2 = mask ? bld1(bM, (uint32_t)(pu * H + L.hq2) * 4u) : 1.f;
+        dau2 = bld1(bDa, (uint32_t)(pu * H + L.hq2) * 4u);
+      }
       f32x4 dv[EB];
 #pragma unroll
       for (int k = 0; k < EB; ++k)
@@ -930,11 +1035,13 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_node_p(
       const uint32_t ron = rnn < W.rend ? (uint32_t)rnn * 4u : OOB;
       const int q0nn = bldi(bR, ron), q1nn = bldi(bR, ron + 4u);
       if (mask) alu *= mk;
+      if (mask) alu2 *= mk2;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       float sda = 0.f;
 #pragma unroll
       for (int k = 0; k < EB; ++k) {
-        const float ak = bperm_f(alu, hbase + k), dk = bperm_f(dau, hbase + k);
+        const float ak = head_perm<HS>(alu, alu2, hbase, k, P.head);
+        const float dk = head_perm<HS>(dau, dau2, hbase, k, P.head);
         if (k < deg) {
           acc += ak * dv[k];
           sda += dk;
@@ -946,13 +1053,20 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_node_p(
         float alb = bld1(bAl, (uint32_t)(pb_ * H + L.hq) * 4u);
         if (mask) alb *= bld1(bM, (uint32_t)(pb_ * H + L.hq) * 4u);
         const float dab = bld1(bDa, (uint32_t)(pb_ * H + L.hq) * 4u);
+        float alb2 = 0.f, dab2 = 0.f;
+        if (two) {
+          alb2 = bld1(bAl, (uint32_t)(pb_ * H + L.hq2) * 4u);
+          if (mask) alb2 *= bld1(bM, (uint32_t)(pb_ * H + L.hq2) * 4u);
+          dab2 = bld1(bDa, (uint32_t)(pb_ * H + L.hq2) * 4u);
+        }
         f32x4 db[EB];
 #pragma unroll
         for (int k = 0; k < EB; ++k)
           db[k] = bld4(bZ, ((uint32_t)bperm_i(tb, L.hwb + k) * HC + P.fc[0]) * 4u);
 #pragma unroll
         for (int k = 0; k < EB; ++k) {
-          const float ak = bperm_f(alb, hbase + k), dk = bperm_f(dab, hbase + k);
+          const float ak = head_perm<HS>(alb, alb2, hbase, k, P.head);
+          const float dk = head_perm<HS>(dab, dab2, hbase, k, P.head);
           if (b + k < q1) {
             acc += ak * db[k];
             sda += dk;
@@ -1205,7 +1319,7 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_edge_ps(
         for (int k = 0; k < EB; ++k) {
           const float fk = bperm_f(pre[st] > 0.f ? 1.f : slope, hbase[st] + k);
           const float da = alk[k] * (d[k] - s_i) * fk;
-          if (k < deg) dad += da;
+          if (k < deg) dad += opaque(da);  // (never contracted with da's product: every form alike)
           const float t = bperm_f(da, hlead[st]);
           mine = L.u == k ? t : mine;
         }
@@ -1236,7 +1350,7 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_edge_ps(
                 if (b + k < e1) s_i += ak * dk;
               } else {
                 const float da = ak * (dk - s_i) * fk;
-                if (b + k < e1) dad += da;
+                if (b + k < e1) dad += opaque(da);  // (never contracted with da's product: every form alike)
                 const float t = bperm_f(da, hlead[st]);
                 mine = L.u == k ? t : mine;
               }
@@ -1399,7 +1513,7 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_node_ps(
 // the pipelined kernels' shapes, and whether they are enabled (LGNN_GAT_PIPE=0: the kernels above)
 inline bool pipe_ok(int H, int C) {
   const char* e = getenv("LGNN_GAT_PIPE");
-  return H <= 4 && H * C <= 128 && !(e && e[0] == '0');
+  return H <= 8 && H * C <= 128 && !(e && e[0] == '0');
 }
 // the two-strip forms: 128 < H*C <= 512, 32 <= C <= 128 (the sweep's GAT widths 256 and 512 at
 // 2..8 heads), one launch per 256 features (a pass's heads are independent of the others')
@@ -1412,7 +1526,7 @@ inline bool pipe2_ok(int H, int C) {
 // API, cached per device and kernel), LGNN_GAT_BPC per CU if set
 template <typename K>
 inline unsigned pipe_grid(K kernel, int slot, int64_t M) {
-  static int cap[16][16];
+  static int cap[16][24];  // [device][kernel slot]
   int dev = 0;
   (void)hipGetDevice(&dev);
   dev &= 15;
@@ -1492,16 +1606,16 @@ extern "C" int lgnn_gat_fwd(const int32_t* rowptr, const int32_t* col, const flo
     return LGNN_OK;
   }
   if (pipe_ok(H, C)) {
-    if (act == LGNN_ACT_ELU)
-      hipLaunchKernelGGL(k_gat_fwd_p<LGNN_ACT_ELU>,
-                         dim3(pipe_grid(k_gat_fwd_p<LGNN_ACT_ELU>, 0, M)), dim3(NT), 0,
-                         as_stream(stream), rowptr, col, XP, a_s, a_d, M, H, C, negative_slope,
-                         edge_mask, bias, alpha, Y, Y_bf16);
-    else
-      hipLaunchKernelGGL(k_gat_fwd_p<LGNN_ACT_NONE>,
-                         dim3(pipe_grid(k_gat_fwd_p<LGNN_ACT_NONE>, 1, M)), dim3(NT), 0,
-                         as_stream(stream), rowptr, col, XP, a_s, a_d, M, H, C, negative_slope,
-                         edge_mask, bias, alpha, Y, Y_bf16);
+#define LGNN_GFP(A_, HS_, SLOT_)                                                                \
+  hipLaunchKernelGGL((k_gat_fwd_p<A_, HS_>), dim3(pipe_grid(k_gat_fwd_p<A_, HS_>, SLOT_, M)),      \
+                     dim3(NT), 0, as_stream(stream), rowptr, col, XP, a_s, a_d, M, H, C,            \
+                     negative_slope, edge_mask, bias, alpha, Y, Y_bf16)
+    if (H <= 4) {
+      if (act == LGNN_ACT_ELU) LGNN_GFP(LGNN_ACT_ELU, 1, 0); else LGNN_GFP(LGNN_ACT_NONE, 1, 1);
+    } else {
+      if (act == LGNN_ACT_ELU) LGNN_GFP(LGNN_ACT_ELU, 2, 12); else LGNN_GFP(LGNN_ACT_NONE, 2, 13);
+    }
+#undef LGNN_GFP
     LGNN_LAUNCH_CHECK();
     return LGNN_OK;
   }
@@ -1559,15 +1673,23 @@ int gat_bwd_edge_launch(const int32_t* rowptr, const int32_t* col, const float* 
     return LGNN_OK;
   }
   if (pipe_ok(H, C)) {
-#define LGNN_GBP(A_, POOL_, SLOT_)                                                             \
-  hipLaunchKernelGGL((k_gat_bwd_edge_p<A_, POOL_>),                                             \
-                     dim3(pipe_grid(k_gat_bwd_edge_p<A_, POOL_>, SLOT_, M)), dim3(NT), 0,        \
+#define LGNN_GBP(A_, POOL_, HS_, SLOT_)                                                        \
+  hipLaunchKernelGGL((k_gat_bwd_edge_p<A_, POOL_, HS_>),                                        \
+                     dim3(pipe_grid(k_gat_bwd_edge_p<A_, POOL_, HS_>, SLOT_, M)), dim3(NT), 0,   \
                      as_stream(stream), rowptr, col, XP, a_s, a_d, alpha, edge_mask, dY, Y, M, H, \
                      C, slope, dZ, da_e, da_d, p)
-    if (act == LGNN_ACT_ELU) {
-      if (pg) LGNN_GBP(LGNN_ACT_ELU, true, 2); else LGNN_GBP(LGNN_ACT_ELU, false, 3);
+    if (H <= 4) {
+      if (act == LGNN_ACT_ELU) {
+        if (pg) LGNN_GBP(LGNN_ACT_ELU, true, 1, 2); else LGNN_GBP(LGNN_ACT_ELU, false, 1, 3);
+      } else {
+        if (pg) LGNN_GBP(LGNN_ACT_NONE, true, 1, 4); else LGNN_GBP(LGNN_ACT_NONE, false, 1, 5);
+      }
     } else {
-      if (pg) LGNN_GBP(LGNN_ACT_NONE, true, 4); else LGNN_GBP(LGNN_ACT_NONE, false, 5);
+      if (act == LGNN_ACT_ELU) {
+        if (pg) LGNN_GBP(LGNN_ACT_ELU, true, 2, 14); else LGNN_GBP(LGNN_ACT_ELU, false, 2, 15);
+      } else {
+        if (pg) LGNN_GBP(LGNN_ACT_NONE, true, 2, 16); else LGNN_GBP(LGNN_ACT_NONE, false, 2, 17);
+      }
     }
 #undef LGNN_GBP
     LGNN_LAUNCH_CHECK();
@@ -1654,9 +1776,14 @@ extern "C" int lgnn_gat_bwd_node(const int32_t* tptr, const int32_t* tidx, const
     return LGNN_OK;
   }
   if (pipe_ok(H, C) && M > 0) {
-    hipLaunchKernelGGL(k_gat_bwd_node_p, dim3(num_partials), dim3(NT), 0, as_stream(stream), tptr,
-                       tidx, tmap, alpha, edge_mask, da_e, da_d, dZ, XP, att_src, att_dst, M, H, C,
-                       dXP, partials, dXP_bf16);
+    if (H <= 4)
+      hipLaunchKernelGGL(k_gat_bwd_node_p<1>, dim3(num_partials), dim3(NT), 0, as_stream(stream),
+                         tptr, tidx, tmap, alpha, edge_mask, da_e, da_d, dZ, XP, att_src, att_dst,
+                         M, H, C, dXP, partials, dXP_bf16);
+    else
+      hipLaunchKernelGGL(k_gat_bwd_node_p<2>, dim3(num_partials), dim3(NT), 0, as_stream(stream),
+                         tptr, tidx, tmap, alpha, edge_mask, da_e, da_d, dZ, XP, att_src, att_dst,
+                         M, H, C, dXP, partials, dXP_bf16);
     LGNN_LAUNCH_CHECK();
     return LGNN_OK;
   }

@@ -1,6 +1,7 @@
 """GPU: the row-pipelined GATConv kernels (gat.hip k_gat_fwd_p / k_gat_bwd_edge_p /
 k_gat_bwd_node_p: a half wave walks many rows with the next rows' indices in flight, per-edge
-scalars loaded edge-parallel and handed over by ds_bpermute; taken when H*C <= 128 and H <= 4,
+scalars loaded edge-parallel and handed over by ds_bpermute; taken when H*C <= 128 (5..8 heads:
+each edge lane holds a second head),
 i.e. the reference config's GAT (heads 2, C 64; gat.py:31, configs/config.py:59-64) and C3's,
 and also when 128 < H*C <= 512 with C >= 32: two 128-feature strips per row and launch)
 are bit-identical to the per-row kernels they replace (LGNN_GAT_PIPE=0): forward outputs and
@@ -53,6 +54,12 @@ def _run(m, b, cuda, rng):
     ("hubs", 2, [128, 128], 0.3, True),
     ("hubs", 4, [64, 128], 0.0, False),
     ("tiny", 2, [128, 128], 0.0, True),
+    # 8 heads at H*C <= 128 (C = 16, 8): two head slots per edge lane
+    ("refcfg", 8, [128] * 4, 0.35, True),
+    ("k10", 8, [128, 64, 128], 0.35, False),
+    ("hubs", 8, [64, 128], 0.3, True),
+    ("tiny", 8, [128, 128], 0.0, False),
+    ("refcfg", 6, [96, 96], 0.2, True),
     # H*C = 256 (the sweep's width 256): the two-strip form, 2..8 heads
     ("refcfg", 8, [256, 256], 0.35, True),
     ("k10", 2, [256, 256], 0.0, False),
