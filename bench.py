@@ -144,6 +144,9 @@ def parse():
     ap.add_argument("--entries", type=int, default=1,
                     help="1: per-entry HIP-event profile of an eager step (rank 0, after the "
                          "timed region)")
+    ap.add_argument("--path-option", action="append", default=[], metavar="NAME=VALUE",
+                    help="A/B only: set an lgnn_set_option path option before the run "
+                         "(gat_pipe, gat_bpc, graph_sorted; include/lgnn.h LGNN_OPT_*)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher/rank plumbing only: set up the process group, all-reduce a "
                          "gradient-sized buffer once, print the JSON line with value null; "
@@ -1023,6 +1026,10 @@ def main():
         return dry_run(args, wl, world, rank)
     from lesion_gnn_amd import dist as ldist
 
+    for opt in args.path_option:
+        from lesion_gnn_amd import _lib as llib
+        name, val = opt.split("=")
+        llib.load().lgnn_set_option(getattr(llib, "LGNN_OPT_" + name.upper()), int(val))
     B = args.graphs_per_gpu
     b = make_batch(wl, B, seed=100 + rank).to(dev)
     model = build_model(wl).to(dev)

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 37
+#define LGNN_ABI_VERSION 38
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -63,6 +63,24 @@ extern "C" {
 
 int lgnn_abi_version(void);
 const char* lgnn_status_string(int status);
+
+/* Process-wide path options (ABI v38; they replace round-5's LGNN_* environment reads): the
+ * alternative kernels the default path was measured against, kept selectable for the tests that
+ * check the pair bit for bit. lgnn_set_option returns the previous value (LGNN_EINVAL for an
+ * unknown option); lgnn_get_option the current one. Not meant to change while launches that read
+ * them are being recorded into a graph.
+ *   LGNN_OPT_GAT_PIPE      1 (default): the row-pipelined GATConv kernels where the shape allows;
+ *                          0: the per-row kernels
+ *   LGNN_OPT_GAT_BPC       0 (default): the pipelined grids are occupancy-sized; n > 0: n
+ *                          workgroups per CU
+ *   LGNN_OPT_GRAPH_SORTED  1 (default): the graph build tries its target-sorted path; 0: the
+ *                          general counting sort always */
+#define LGNN_OPT_GAT_PIPE 0
+#define LGNN_OPT_GAT_BPC 1
+#define LGNN_OPT_GRAPH_SORTED 2
+#define LGNN_OPT_COUNT 3
+int lgnn_set_option(int option, int value);
+int lgnn_get_option(int option);
 
 /* ---------------------------------------------------------------------------------------------
  * Graph structure.

@@ -7,6 +7,7 @@ product op raises. torch is imported first so that the HIP runtime torch ships
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 
@@ -26,6 +27,7 @@ LGNN_SLOT_FLAG0 = 7  # tile_open: count + six barrier words, then the partial-sl
 LGNN_SLOT_FLAGS = 256
 LGNN_TILE_OPEN_EXTRA = LGNN_SLOT_FLAG0 + LGNN_SLOT_FLAGS  # words after the per-tile flags
 LGNN_S3_ADJT_TILE_BYTES = 16384  # lgnn.h: fp32 Â per tile, split-3 forward -> fused backward
+LGNN_OPT_GAT_PIPE, LGNN_OPT_GAT_BPC, LGNN_OPT_GRAPH_SORTED = 0, 1, 2  # lgnn_set_option
 
 P = ctypes.c_void_p
 I32 = ctypes.c_int
@@ -55,6 +57,8 @@ class PlaneJob(ctypes.Structure):
 SIGNATURES: dict[str, tuple] = {
     "lgnn_abi_version": (I32, []),
     "lgnn_status_string": (ctypes.c_char_p, [I32]),
+    "lgnn_set_option": (I32, [I32, I32]),
+    "lgnn_get_option": (I32, [I32]),
     "lgnn_graph_workspace_bytes": (SZ, [I64, I64]),
     "lgnn_graph_build_path": (I32, [P, I64, I64, P]),
     "lgnn_graph_build_lazy": (I32, [P, I64, I64, I32, I32, P, P, P, P, P, P, P, P, P, I64, P, P,
@@ -164,7 +168,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 37
+ABI_VERSION = 38
 
 _lib = None
 
@@ -195,6 +199,20 @@ def check(status: int, what: str) -> None:
     if status != 0:
         msg = load().lgnn_status_string(status)
         raise LgnnError(f"{what} failed: {status} ({msg.decode() if msg else '?'})")
+
+
+@contextlib.contextmanager
+def path_option(option: int, value: int):
+    """Set one of the library's process-wide path options (lgnn_set_option: the alternative kernel
+    a test checks the default against) for the duration of a with-block."""
+    lib = load()
+    old = lib.lgnn_set_option(option, int(value))
+    if old < 0:
+        raise LgnnError(f"lgnn_set_option({option}, {value}) failed: {old}")
+    try:
+        yield
+    finally:
+        lib.lgnn_set_option(option, old)
 
 
 def ptr(t: torch.Tensor | None) -> int | None:

@@ -20,6 +20,9 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// the process-wide path options of lgnn_set_option (include/lgnn.h; defined in graph.hip)
+int lgnn_option(int option);
+
 __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }

@@ -1510,20 +1510,20 @@ __global__ __launch_bounds__(NT) void k_gat_bwd_node_ps(
   }
 }
 
-// the pipelined kernels' shapes, and whether they are enabled (LGNN_GAT_PIPE=0: the kernels above)
+// the pipelined kernels' shapes, and whether they are enabled (LGNN_OPT_GAT_PIPE = 0: the
+// kernels above)
 inline bool pipe_ok(int H, int C) {
-  const char* e = getenv("LGNN_GAT_PIPE");
-  return H <= 8 && H * C <= 128 && !(e && e[0] == '0');
+  return H <= 8 && H * C <= 128 && lgnn_option(LGNN_OPT_GAT_PIPE) != 0;
 }
 // the two-strip forms: 128 < H*C <= 512, 32 <= C <= 128 (the sweep's GAT widths 256 and 512 at
 // 2..8 heads), one launch per 256 features (a pass's heads are independent of the others')
 inline bool pipe2_ok(int H, int C) {
-  const char* e = getenv("LGNN_GAT_PIPE");
-  return H * C > 128 && H * C <= 512 && C >= 32 && C <= 128 && !(e && e[0] == '0');
+  return H * C > 128 && H * C <= 512 && C >= 32 && C <= 128 &&
+         lgnn_option(LGNN_OPT_GAT_PIPE) != 0;
 }
 
 // persistent grid of a row-pipelined kernel: the workgroups one launch keeps resident (occupancy
-// API, cached per device and kernel), LGNN_GAT_BPC per CU if set
+// API, cached per device and kernel), LGNN_OPT_GAT_BPC per CU if set
 template <typename K>
 inline unsigned pipe_grid(K kernel, int slot, int64_t M) {
   static int cap[16][24];  // [device][kernel slot]
@@ -1540,11 +1540,10 @@ inline unsigned pipe_grid(K kernel, int slot, int64_t M) {
     cap[dev][slot] = cus * per;
   }
   int64_t c = cap[dev][slot];
-  if (const char* e = getenv("LGNN_GAT_BPC")) {
+  if (const int bpc = lgnn_option(LGNN_OPT_GAT_BPC)) {
     int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        atoi(e) > 0)
-      c = (int64_t)cus * atoi(e);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      c = (int64_t)cus * bpc;
   }
   int64_t g = (M + RB - 1) / RB;
   if (g > c) g = c;

@@ -1082,6 +1082,24 @@ inline int grid_for(int64_t n, int64_t cap = 4096) {
 
 extern "C" int lgnn_abi_version(void) { return LGNN_ABI_VERSION; }
 
+// path options (lgnn_set_option): plain ints read on the host when a launch is configured
+static int g_options[LGNN_OPT_COUNT] = {1, 0, 1};
+
+int lgnn_option(int option) {
+  return option >= 0 && option < LGNN_OPT_COUNT ? __atomic_load_n(&g_options[option], __ATOMIC_RELAXED)
+                                                : 0;
+}
+
+extern "C" int lgnn_set_option(int option, int value) {
+  if (option < 0 || option >= LGNN_OPT_COUNT || value < 0) return LGNN_EINVAL;
+  return __atomic_exchange_n(&g_options[option], value, __ATOMIC_RELAXED);
+}
+
+extern "C" int lgnn_get_option(int option) {
+  if (option < 0 || option >= LGNN_OPT_COUNT) return LGNN_EINVAL;
+  return lgnn_option(option);
+}
+
 extern "C" const char* lgnn_status_string(int status) {
   switch (status) {
     case LGNN_OK: return "ok";
@@ -1175,11 +1193,8 @@ extern "C" int lgnn_graph_build_path(const void* workspace, int64_t num_nodes, i
   return v & kModeMask;  // kModeGeneral 0, kModeSorted 1, kModeSortedOpen 2
 }
 
-// the target-sorted fast path is tried unless LGNN_GRAPH_SORTED=0 (a test / A-B knob)
-static bool sorted_path_enabled() {
-  const char* e = getenv("LGNN_GRAPH_SORTED");
-  return !(e && e[0] == '0');
-}
+// the target-sorted fast path is tried unless LGNN_OPT_GRAPH_SORTED is 0 (a test / A-B option)
+static bool sorted_path_enabled() { return lgnn_option(LGNN_OPT_GRAPH_SORTED) != 0; }
 
 static int graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loops, int norm,
                        int32_t* rowptr, int32_t* col, float* w, int32_t* tptr, int32_t* tidx,

@@ -11,13 +11,12 @@ from __future__ import annotations
 from dataclasses import dataclass
 
 import ctypes
-import os
 
 import torch
 
 from . import _lib
 
-KEEP_BUILD_WS = os.environ.get("LGNN_GRAPH_DIAG", "0") == "1"
+KEEP_BUILD_WS = False
 
 KIND = {
     # kind: (loops mode, norm mode, self_scale of the aggregation)
@@ -59,7 +58,7 @@ class Graph:
         self._aux: dict[str, torch.Tensor] = {}
         self.adj_values: torch.Tensor | None = None  # values of an adj_t input (as_graph)
         # keep the last eager build's workspace for build_path() (tests / diagnostics only: it
-        # holds several (E + N)-sized arrays for the Graph's lifetime); LGNN_GRAPH_DIAG=1 sets it
+        # holds several (E + N)-sized arrays for the Graph's lifetime); KEEP_BUILD_WS = True sets it
         self.keep_build_workspace = KEEP_BUILD_WS
         self.batch = None
         self._gptr = None
@@ -163,7 +162,7 @@ class Graph:
         k, ws = getattr(self, "_last_ws", (None, None))
         if k != kind:
             raise ValueError(f"no eager build of {kind!r} on this graph kept its workspace "
-                             "(set Graph.keep_build_workspace = True, or LGNN_GRAPH_DIAG=1)")
+                             "(set Graph.keep_build_workspace = True, or KEEP_BUILD_WS = True)")
         r = _lib.load().lgnn_graph_build_path(_lib.ptr(ws), self.num_nodes, self.num_edges,
                                               _lib.stream(self.device))
         _lib.check(r if r < 0 else 0, "lgnn_graph_build_path")

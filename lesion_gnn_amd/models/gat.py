@@ -10,7 +10,6 @@ every conv one HIP autograd node (ops.gat_conv) with the ELU fused.
 from __future__ import annotations
 
 import dataclasses
-import os
 from itertools import pairwise
 
 import torch
@@ -24,10 +23,10 @@ from ..utils.placeholder import Placeholder
 from .base import BaseModelConfig, BaseModule
 
 
-# the last GATConv + readout as one autograd node (ops.gat_conv_head); LGNN_GAT_HEAD=0: separate
-HEAD_FOLD = os.environ.get("LGNN_GAT_HEAD", "1") != "0"
+# the last GATConv + readout as one autograd node (ops.gat_conv_head); HEAD_FOLD = False: separate
+HEAD_FOLD = True
 # fp32: every split-3 weight operand of a step in one launch (GAT.weight_planes); 0: per GEMM
-WEIGHT_BUNDLE = os.environ.get("LGNN_WEIGHT_BUNDLE", "1") != "0"
+WEIGHT_BUNDLE = True
 
 
 class GAT(nn.Module):

@@ -9,7 +9,6 @@ plus the model's F.elu (gin.py:31) runs as one HIP autograd node (ops.gin_conv).
 from __future__ import annotations
 
 import dataclasses
-import os
 from itertools import pairwise
 
 import torch
@@ -23,8 +22,8 @@ from ..utils.placeholder import Placeholder
 from .base import BaseModelConfig, BaseModule
 
 
-# the GIN model as one autograd node (ops.gin_stack) when eligible; LGNN_GIN_STACK=0: per-conv
-STACK = os.environ.get("LGNN_GIN_STACK", "1") != "0"
+# the GIN model as one autograd node (ops.gin_stack) when eligible; STACK = False: per-conv
+STACK = True
 
 
 class GIN(nn.Module):

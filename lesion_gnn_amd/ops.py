@@ -11,7 +11,6 @@
 from __future__ import annotations
 
 import ctypes
-import os
 import weakref
 
 import torch
@@ -55,8 +54,8 @@ def fast_shape(K: int, N: int) -> bool:
 # Wide linears (K or N > 128: the reference sweep's widths 256 / 512, scripts/sweep.py:126) run as
 # the aggregation (lgnn_spmm) + the split-3 dense GEMMs (s3gemm.hip) instead of the fp32 generic
 # node kernels, which stream the weight per 128-wide block and re-derive dZ per output block
-# (GIN [512]*4: dX 1.4 ms per launch). LGNN_WIDE=f32 keeps the generic kernels (A/B).
-WIDE = os.environ.get("LGNN_WIDE", "s3")
+# (GIN [512]*4: dX 1.4 ms per launch). WIDE = "f32" keeps the generic kernels (A/B).
+WIDE = "s3"
 
 
 def wide_shape(K: int, N: int) -> bool:
@@ -89,37 +88,37 @@ def linear_fwd(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None, act: in
 STACK_MAX = 8  # LGNN_MAX_STACK
 
 
-# fused stack backward on/off (LGNN_FUSED_BWD=0 selects the layer-wise backward; diagnostics)
-FUSED_BWD = os.environ.get("LGNN_FUSED_BWD", "1") != "0"
+# fused stack backward on/off (FUSED_BWD = False selects the layer-wise backward; diagnostics)
+FUSED_BWD = True
 # the fused stack's graph build skips the transpose CSR when no tile is open
-# (LGNN_LAZY_TRANSPOSE=0: always built)
-LAZY_TRANSPOSE = os.environ.get("LGNN_LAZY_TRANSPOSE", "1") != "0"
+# (LAZY_TRANSPOSE = False: always built)
+LAZY_TRANSPOSE = True
 
 
 # GEMM arithmetic of the fused GCN stack: "s3" = bf16 MFMA on three-plane split operands (fp32
-# accuracy, stack3.hip), "f32" = fp32 MFMA (tile.hip). LGNN_MFMA=f32 selects the latter.
-MFMA_MODE = os.environ.get("LGNN_MFMA", "s3")
-# Backward of the fused stack (LGNN_BWD): "f32" = the fp32 fused kernel (tile.hip k_stack_bwd, one
+# accuracy, stack3.hip), "f32" = fp32 MFMA (tile.hip). MFMA_MODE = "f32" selects the latter.
+MFMA_MODE = "s3"
+# Backward of the fused stack (BWD_MODE): "f32" = the fp32 fused kernel (tile.hip k_stack_bwd, one
 # launch); "s3" = the split-3 layer-major kernels (stack3_bwd.hip k_s3_bwd: one launch per layer,
 # dZ through HBM, 512 partial slots); "s3f" = the fused split-3 kernel (stack3_bwd.hip
 # k_s3_fbwd: every layer of a tile in one pass, one launch, 256 slots; the default: 121 us vs
 # 154 us for f32 at C2 on MI355X). s3 / s3f need the split-3 forward (their transposed weight
 # planes come out of its weight-plane launch); otherwise the f32 kernel runs.
-BWD_MODE = os.environ.get("LGNN_BWD", "s3f")
+BWD_MODE = "s3f"
 BWD_S3 = BWD_MODE in ("s3", "s3f")
 # open tiles (an edge leaves them) inside the fused split-3 launches, layer by layer behind grid
-# barriers, instead of three layer-wise launches per direction (LGNN_OPEN_IN_FUSED=0: separate)
+# barriers, instead of three layer-wise launches per direction (OPEN_IN_FUSED = "0": separate)
 # The fused kernels' open phase saves the six layer-wise launches (~4.5 us each), but runs the
 # open tiles ~1.5x slower than the standalone layer-wise kernels (measured C5, r02j). So it is
 # taken when open tiles are expected to be rare: "auto" (default) = when every graph could sit
 # whole in 64-node tiles (all graphs of one size that divides or is a multiple of 64: the
 # batch's node count is B * n with 64 % n == 0 or n % 64 == 0). Either choice is exact; "1" /
 # "0" force it (also "fwd" / "bwd" for one direction).
-OPEN_IN_FUSED = os.environ.get("LGNN_OPEN_IN_FUSED", "auto")
+OPEN_IN_FUSED = "auto"
 OPEN_IN_FUSED_BWD = OPEN_IN_FUSED
-# dP = dlogits W_out formed inside the single-launch split-3 backward (LGNN_HEAD_FOLD=0: by
+# dP = dlogits W_out formed inside the single-launch split-3 backward (HEAD_FOLD = False: by
 # lgnn_pool_head_bwd before it)
-HEAD_FOLD = os.environ.get("LGNN_HEAD_FOLD", "1") != "0"
+HEAD_FOLD = True
 _CAPACITY: dict = {}
 
 
@@ -245,9 +244,9 @@ def _s3f(L: int) -> bool:
     return BWD_MODE == "s3f" and L <= 2
 
 
-# the split-3 forward hands each closed tile's Â^T planes to the fused backward (LGNN_ADJT=0: the
+# the split-3 forward hands each closed tile's Â^T planes to the fused backward (ADJT = False: the
 # backward rebuilds them from the CSR)
-ADJT = os.environ.get("LGNN_ADJT", "1") != "0"
+ADJT = True
 
 
 def _adjt_ptr(planes_t: torch.Tensor, L: int):
@@ -741,9 +740,9 @@ def dense_wgrad(dy: torch.Tensor, x: torch.Tensor, bf16: bool, want_db: bool = F
     return dW, db
 
 
-# bf16 GEMMs on the hand-written MFMA kernels (csrc/bflin.hip); LGNN_BF16_MFMA=0 (A/B) and widths
+# bf16 GEMMs on the hand-written MFMA kernels (csrc/bflin.hip); BF16_MFMA = False (A/B) and widths
 # N > 128 route them to the one-plane split GEMMs above (dense_mm / dense_wgrad with bf16=True)
-BF16_MFMA = os.environ.get("LGNN_BF16_MFMA", "1") != "0"
+BF16_MFMA = True
 
 
 def bf16_mfma_fits(N: int) -> bool:
@@ -1336,9 +1335,9 @@ def bn_bwd_apply(dA, Z, mask, scale, shift, mean, invstd, sums, count, training,
     return dZ, dg, db
 
 
-# GIN: BatchNorm folded into the MLP's two linear launches (LGNN_BN_FUSED=0: the separate
+# GIN: BatchNorm folded into the MLP's two linear launches (BN_FUSED = False: the separate
 # lgnn_bn_* passes)
-BN_FUSED = os.environ.get("LGNN_BN_FUSED", "1") != "0"
+BN_FUSED = True
 
 
 
@@ -1612,8 +1611,8 @@ class _GINConvHead(torch.autograd.Function):
 
 
 # out_proj's dW / db as outer-product jobs of a layer's slab reduction (GIN / GAT model nodes);
-# LGNN_HEAD_JOBS=0: the separate lgnn_pool_head_bwd launch
-HEAD_JOBS = os.environ.get("LGNN_HEAD_JOBS", "1") != "0"
+# HEAD_JOBS = False: the separate lgnn_pool_head_bwd launch
+HEAD_JOBS = True
 
 
 class _SubCtx:
@@ -1792,7 +1791,7 @@ class _GATConv(torch.autograd.Function):
         C = HC // heads
         dev = x.device
         # fp32: the lin on the split-3 MFMA GEMMs (s3gemm.hip) at every width — they beat the
-        # fp32-MFMA tile kernels (2.7x the MFMA rate at fp32 accuracy); LGNN_GAT_S3=0: tiles
+        # fp32-MFMA tile kernels (2.7x the MFMA rate at fp32 accuracy); GAT_S3 = False: tiles
         dense = bf16 or not fast_shape(W.size(1), HC) or GAT_S3
         mfma = bf16 and bf16_mfma_fits(HC)
         ctx.wt = None
@@ -1934,12 +1933,12 @@ class _GATConv(torch.autograd.Function):
         return dx, dW, datt_s, datt_d, dbias, None, None, None, None, None, None, None, None
 
 
-GAT_S3 = os.environ.get("LGNN_GAT_S3", "1") != "0"
+GAT_S3 = True
 # bf16 GAT: the attention kernels write their fp32 outputs' bf16 copies for the following bf16
-# GEMMs (LGNN_BF16_OUT=0: torch casts instead; the values are identical, RNE both ways)
-BF16_OUT = os.environ.get("LGNN_BF16_OUT", "1") != "0"
+# GEMMs (BF16_OUT = False: torch casts instead; the values are identical, RNE both ways)
+BF16_OUT = True
 # bf16 GATConv.lin forward with the attention scores in its epilogue (lgnn_bf16_gemm_att)
-GAT_GEMM_ATT = os.environ.get("LGNN_GAT_GEMM_ATT", "1") != "0"
+GAT_GEMM_ATT = True
 _BF16_COPIES: dict = {}
 
 

@@ -4,7 +4,8 @@ scalars loaded edge-parallel and handed over by ds_bpermute; taken when H*C <= 1
 each edge lane holds a second head),
 i.e. the reference config's GAT (heads 2, C 64; gat.py:31, configs/config.py:59-64) and C3's,
 and also when 128 < H*C <= 512 with C >= 32: two 128-feature strips per row and launch)
-are bit-identical to the per-row kernels they replace (LGNN_GAT_PIPE=0): forward outputs and
+are bit-identical to the per-row kernels they replace (path option LGNN_OPT_GAT_PIPE = 0): forward
+outputs and
 every parameter gradient, with dropout masks, with the readout folded into the last layer's edge
 kernel and without, on rows longer than one 8-entry batch (k = 10, hub nodes: the batched walk),
 1-node graphs and launches with fewer rows than workgroups. Plus the oracle at the reference
@@ -13,7 +14,7 @@ import pytest
 import torch
 
 import oracle.pyg_ref as ref
-from lesion_gnn_amd import synth
+from lesion_gnn_amd import _lib, synth
 from lesion_gnn_amd.models import gat as gat_mod
 from lesion_gnn_amd.models.gat import GAT
 
@@ -77,18 +78,18 @@ def test_pipelined_kernels_bitwise(cuda, monkeypatch, kind, heads, hidden, dropo
     monkeypatch.setattr(gat_mod, "HEAD_FOLD", fold)
     rng = m._dropout_rng.clone()
     res = []
-    for pipe in ("1", "0"):
-        monkeypatch.setenv("LGNN_GAT_PIPE", pipe)
-        res.append(_run(m, b, cuda, rng))
+    for pipe in (1, 0):
+        with _lib.path_option(_lib.LGNN_OPT_GAT_PIPE, pipe):
+            res.append(_run(m, b, cuda, rng))
     assert torch.equal(res[0][0], res[1][0])
     for n in res[1][1]:
         assert torch.equal(res[0][1][n], res[1][1][n]), n
 
 
-def test_pipelined_reference_config_vs_oracle(cuda, monkeypatch):
-    """The reference model (GAT [128]*4, heads 2) through the pipelined kernels vs the oracle,
-    tests/test_gpu_gat.py's fp32 bar."""
-    monkeypatch.setenv("LGNN_GAT_PIPE", "1")
+def test_pipelined_reference_config_vs_oracle(cuda):
+    """The reference model (GAT [128]*4, heads 2) through the pipelined kernels (the default
+    path option) vs the oracle, tests/test_gpu_gat.py's fp32 bar."""
+    assert _lib.load().lgnn_get_option(_lib.LGNN_OPT_GAT_PIPE) == 1
     b = _batch("hubs")
     torch.manual_seed(5)
     ours = GAT(64, [128] * 4, 1, heads=2, dropout=0.0)
@@ -108,17 +109,17 @@ def test_pipelined_reference_config_vs_oracle(cuda, monkeypatch):
                                    msg=lambda s: f"{n}: {s}")
 
 
-@pytest.mark.parametrize("bpc", ["1", "3"])
-def test_pipelined_grid_override(cuda, monkeypatch, bpc):
-    """LGNN_GAT_BPC (workgroups per CU of the persistent grid, a tuning knob) changes only which
-    half wave walks which rows, never the results."""
+@pytest.mark.parametrize("bpc", [1, 3])
+def test_pipelined_grid_override(cuda, bpc):
+    """LGNN_OPT_GAT_BPC (workgroups per CU of the persistent grid, a tuning option) changes only
+    which half wave walks which rows, never the results."""
     b = _batch("refcfg")
     torch.manual_seed(3)
     m = GAT(64, [128] * 3, 1, heads=2, dropout=0.35).to(cuda).train()
     rng = m._dropout_rng.clone()
     base = _run(m, b, cuda, rng)
-    monkeypatch.setenv("LGNN_GAT_BPC", bpc)
-    got = _run(m, b, cuda, rng)
+    with _lib.path_option(_lib.LGNN_OPT_GAT_BPC, bpc):
+        got = _run(m, b, cuda, rng)
     assert torch.equal(base[0], got[0])
     for n in base[1]:
         assert torch.equal(base[1][n], got[1][n]), n

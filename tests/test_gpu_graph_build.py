@@ -5,7 +5,7 @@ hands the near misses to them; the weight-plane side job of the first launch
 import pytest
 import torch
 
-from lesion_gnn_amd import synth
+from lesion_gnn_amd import _lib, synth
 from lesion_gnn_amd.graph import Graph
 
 pytestmark = pytest.mark.gpu
@@ -110,14 +110,14 @@ def _sorted_cases():
 
 @pytest.mark.parametrize("case", list(_sorted_cases()))
 @pytest.mark.parametrize("kind", ["gcn_lazy", "gcn", "gin"])
-def test_sorted_build_bitexact(cuda, monkeypatch, case, kind):
+def test_sorted_build_bitexact(cuda, case, kind):
     """The target-sorted fast path (k_prep_sorted + k_scan's sorted body) writes the same CSR,
-    weights, tile flags and error count as the general counting sort (LGNN_GRAPH_SORTED=0), and
-    is taken exactly for the inputs it covers (lazy GCN builds; the others never try it)."""
+    weights, tile flags and error count as the general counting sort (path option
+    LGNN_OPT_GRAPH_SORTED = 0), and is taken exactly for the inputs it covers (lazy GCN builds;
+    the others never try it)."""
     (ei, n), path = _sorted_cases()[case]
-    monkeypatch.setenv("LGNN_GRAPH_SORTED", "0")
-    want = _build(ei, n, kind, cuda)
-    monkeypatch.setenv("LGNN_GRAPH_SORTED", "1")
+    with _lib.path_option(_lib.LGNN_OPT_GRAPH_SORTED, 0):
+        want = _build(ei, n, kind, cuda)
     g = Graph(ei.to(cuda), n)
     g.keep_build_workspace = True  # build_path() below
     got = _build(ei, n, kind, cuda)

@@ -1,12 +1,12 @@
 """Gradient differences between the row-pipelined GAT kernels and the per-row ones
-(LGNN_GAT_PIPE=1 / 0) for one shape. Usage (GPU box): python tools/gat_pipe_debug.py heads hidden fold"""
+(path option LGNN_OPT_GAT_PIPE 1 / 0) for one shape. Usage (GPU box): python tools/gat_pipe_debug.py heads hidden fold"""
 import os
 import sys
 
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from lesion_gnn_amd import synth  # noqa: E402
+from lesion_gnn_amd import _lib, synth  # noqa: E402
 from lesion_gnn_amd.models import gat as gat_mod  # noqa: E402
 from lesion_gnn_amd.models.gat import GAT  # noqa: E402
 
@@ -21,7 +21,7 @@ def main():
     m = GAT(64, hidden, 1, heads=heads, dropout=0.0, pool="mean").to(dev).train()
     res = {}
     for pipe in ("1", "0"):
-        os.environ["LGNN_GAT_PIPE"] = pipe
+        _lib.load().lgnn_set_option(_lib.LGNN_OPT_GAT_PIPE, int(pipe))
         out = m(b.x.to(dev), b.edge_index.to(dev), b.batch.to(dev), b.num_graphs)
         m.zero_grad(set_to_none=True)
         out.square().sum().backward()

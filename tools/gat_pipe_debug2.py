@@ -1,5 +1,5 @@
 """lgnn_gat_fwd / lgnn_gat_bwd_edge / lgnn_gat_bwd_node called directly with the row-pipelined
-kernels and the per-row ones (LGNN_GAT_PIPE=1 / 0) on the same inputs; prints which outputs differ.
+kernels and the per-row ones (path option LGNN_OPT_GAT_PIPE 1 / 0) on the same inputs; prints which outputs differ.
 Usage (GPU box): python tools/gat_pipe_debug2.py heads C"""
 import os
 import sys
@@ -33,7 +33,7 @@ def main():
     dY = torch.randn(M, HC, generator=gen).to(dev)
     res = {}
     for pipe in ("1", "0"):
-        os.environ["LGNN_GAT_PIPE"] = pipe
+        _lib.load().lgnn_set_option(_lib.LGNN_OPT_GAT_PIPE, int(pipe))
         alpha = torch.zeros(cap, H, device=dev)
         Y = torch.empty(M, HC, device=dev)
         _lib.call("lgnn_gat_fwd", P(csr.rowptr), P(csr.col), P(XP), P(a_s), P(a_d), M, H, C,

@@ -1,6 +1,6 @@
 #!/bin/bash
-# A/B of one environment knob on one box: bench.py --workload W with VAR=A, then VAR=B, twice
-# each, interleaved. Usage: VAR=LGNN_GRAPH_SORTED A=0 B=1 W="c2" bash tools/gpu_ab.sh <tag>
+# A/B of one library path option on one box: bench.py --workload W with OPT=A, then OPT=B, twice
+# each, interleaved. Usage: OPT=graph_sorted A=0 B=1 W="c2" bash tools/gpu_ab.sh <tag>
 set -uo pipefail
 TAG=$1
 OUT=gpurun_out/$TAG
@@ -8,12 +8,12 @@ mkdir -p "$OUT"
 for w in $W; do
   for rep in 1 2; do
     for val in $A $B; do
-      env "$VAR=$val" timeout -k 10 300 python bench.py --workload $w --steps ${STEPS:-200} \
+      timeout -k 10 300 python bench.py --workload $w --steps ${STEPS:-200} --path-option "$OPT=$val" \
         --warmup 30 --cpu-seconds 0 > "$OUT/ab_${w}_${val}_$rep.json" 2> "$OUT/ab_${w}_${val}_$rep.err" \
         || { tail -20 "$OUT/ab_${w}_${val}_$rep.err"; exit 1; }
       python -c "
 import json; d=json.load(open('$OUT/ab_${w}_${val}_$rep.json'))
-print('$w $VAR=$val rep $rep', d['value'], d['ms_per_step'])"
+print('$w $OPT=$val rep $rep', d['value'], d['ms_per_step'])"
     done
   done
 done
