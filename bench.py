@@ -1152,7 +1152,9 @@ def main():
         rows.sort(key=lambda r: -r["avg_launch_ms"])
         out["roofline"] = rows[0]
         out["roofline_next"] = rows[1:]
-    if rank == 0 and args.entries and not args.no_kernel_timing:
+    # one rank only: the eager step's gradient all-reduce (and GIN's SyncBN) would wait on ranks
+    # that have left for destroy_process_group
+    if rank == 0 and world == 1 and args.entries and not args.no_kernel_timing:
         kind = {"gcn": "gcn", "gin": "gin", "gat": "gat"}[wl["model"]]
         rows, tot = profile_entries(eager_step_fn(fwd_bwd, bucket, opt), dev,
                                     GraphStats(b, kind))

@@ -21,9 +21,9 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kFinT = 64;          // k_finish: rows (threads) per block
-constexpr int kFinishCap = 1536;   // staged CSR entries per k_finish block
-constexpr int kLongRow = 24;       // k_finish: longer staged rows are sorted by the whole wave
+constexpr int kFinR = 16;          // k_finish: rows per wave (virtual block)
+constexpr int kFinishCap = 1024;   // staged CSR entries per k_finish virtual block
+constexpr int kFinGrid = 1024;     // k_finish: workgroup cap (grid-stride over virtual blocks)
 // Target-sorted fast path (k_prep_sorted + the sorted body of k_scan): rows of at most
 // kSortedRowCap CSR entries (a 64-row tile then stays within the fused kernels' CAPE_TILE
 // entries: k <= 32, the reference sweep's range), runs of at most kGapCap rows without entries,
@@ -841,9 +841,16 @@ __device__ __forceinline__ void sort_row(KP key, VP val, int n) {
 }
 
 // by = 0: target CSR (rowptr/col/eid/w); 1: source CSR (tptr/tidx/teid/tw). One virtual block
-// = kFinT rows, run by one wave (tid = lane 0..63) with its own staging arrays and `sync` its
-// wave-scope ordering (k_finish and the fused build's finish phase alike).
-// Weight of entry (row i, neighbour j): GCN (dis(src) * 1) * dis(dst) = dis(j) * dis(i).
+// = kFinR rows, run by one wave (tid = lane 0..63) with its own staging arrays and `sync` its
+// wave-scope ordering. Weight of entry (row i, neighbour j): GCN (dis(src) * 1) * dis(dst) =
+// dis(j) * dis(i).
+// Staged blocks (<= kFinishCap entries) are finished entry-parallel: every lane takes entries
+// eb + t, + 64, ...; an entry's place in its row is its rank among the row's (distinct) edge
+// ids, counted over the staged row (lanes of one row read the same LDS words), and the entry,
+// its weight, the inverse map and the tile marks are written from there in one pass. Round 5
+// sorted each row by one lane (insertion sort, 64 rows per wave, 1536 entries): C5 k = 16's
+// source CSR finish took 40 us at under one wave per SIMD. Blocks past the cap (hub rows of
+// general graphs) sort each row in place in global memory, one lane per row.
 template <typename Sync>
 __device__ __forceinline__ void finish_body(int64_t N, int64_t E, int add_loop, int norm,
                                             const int32_t* __restrict__ rowptr, int32_t* col,
@@ -851,163 +858,98 @@ __device__ __forceinline__ void finish_body(int64_t N, int64_t E, int add_loop, 
                                             const int32_t* __restrict__ tptr, int32_t* tidx,
                                             int32_t* teid, float* tw,
                                             const float* __restrict__ dis,
-                                            const int32_t* __restrict__ ws_err, int32_t* err_out,
                                             int32_t* tile_open, int lazy,
                                             int32_t* __restrict__ inv, int32_t* s_key,
-                                            int32_t* s_val, int32_t* s_ptr, int64_t bx, int by,
-                                            int tid, Sync sync) {
-  if (lazy && by == 1 && tile_open[(N + 63) >> 6] == 0) return;  // no source CSR needed
-  if (err_out && bx == 0 && by == 0 && tid == 0) *err_out = *ws_err;
+                                            int32_t* s_val, uint8_t* s_row, int32_t* s_ptr,
+                                            int64_t bx, int by, int tid, Sync sync) {
   const bool tr = by == 1;
   const int32_t* __restrict__ ptr = tr ? tptr : rowptr;
   int32_t* idx = tr ? tidx : col;
   int32_t* key = tr ? teid : eid;
   float* wt = tr ? tw : w;
-  const int64_t i0 = bx * kFinT;
+  const int64_t i0 = bx * kFinR;
   const int64_t i = i0 + tid;
-  const int64_t iend = i0 + kFinT < N ? i0 + kFinT : N;
+  const int64_t iend = i0 + kFinR < N ? i0 + kFinR : N;
+  const bool own = tid < kFinR && i < N;  // lane tid < kFinR: row i of the block
   const int eb = ptr[i0], ee = ptr[iend];
-  const bool staged = ee - eb <= kFinishCap;
-  if (staged) {
-    for (int j = eb + tid; j < ee; j += kFinT) {
-      s_key[j - eb] = key[j];
-      s_val[j - eb] = idx[j];
-    }
+  const int n = ee - eb;
+  // lazy builds took the tile marks in k_count (cross edges) and k_scan (capacity)
+  const bool marks = tile_open && !tr && !lazy;
+  const int64_t ntiles = (N + 63) >> 6;
+  if (marks && own && (i & 63) == 0) {  // more CSR entries than a closed tile takes
+    const int64_t iend64 = i + 64 < N ? i + 64 : N;
+    if (ptr[iend64] - ptr[i] > lgnn_tile::CAPE_TILE) mark_open(tile_open, i >> 6, ntiles);
   }
-  sync();
-  // staged rows longer than kLongRow (source CSR rows of hub nodes: insertion sort is quadratic
-  // and one lane's long row held the whole launch, ~60 us at C5 k = 16) are sorted afterwards by
-  // the whole wave: each entry's rank among its row's (unique) edge ids, at most 4 per lane
-  bool long_row = false;
-  if (i < N) {
-    const int r0 = ptr[i], r1 = ptr[i + 1];
-    if (staged) {
+  if (n <= kFinishCap) {
+    for (int j = tid; j < n; j += 64) {
+      s_key[j] = key[eb + j];
+      s_val[j] = idx[eb + j];
+    }
+    if (tid <= kFinR) s_ptr[tid] = ptr[i0 + tid < iend ? i0 + tid : iend] - eb;
+    sync();
+    if (own) {  // the row table, and the appended self loop (the row's last slot)
+      const int r0 = s_ptr[tid], r1 = s_ptr[tid + 1];
+      for (int j = r0; j < r1; ++j) s_row[j] = (uint8_t)tid;
       if (add_loop) {
-        s_val[r1 - 1 - eb] = (int32_t)i;
-        s_key[r1 - 1 - eb] = (int32_t)(E + i);
+        s_val[r1 - 1] = (int32_t)i;
+        s_key[r1 - 1] = (int32_t)(E + i);
       }
-      long_row = r1 - r0 > kLongRow && r1 - r0 <= 4 * kFinT;
-      if (!long_row) sort_row(s_key + (r0 - eb), s_val + (r0 - eb), r1 - r0);
-    } else {
-      if (add_loop) {
-        idx[r1 - 1] = (int32_t)i;
-        key[r1 - 1] = (int32_t)(E + i);
-      }
-      sort_row(key + r0, idx + r0, r1 - r0);
-    }
-  }
-  sync();
-  if (staged) {
-    unsigned long long lm = __ballot(long_row);
-    while (lm) {
-      const int L = __ffsll((long long)lm) - 1;
-      lm &= lm - 1;
-      const int64_t ri = i0 + L;
-      const int q0 = ptr[ri] - eb, n = ptr[ri + 1] - ptr[ri];
-      int kk[4], vv[4], rk[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int j = tid + u * kFinT;
-        kk[u] = j < n ? s_key[q0 + j] : 0;
-        vv[u] = j < n ? s_val[q0 + j] : 0;
-        rk[u] = 0;
-      }
-      for (int m = 0; m < n; ++m) {
-        const int km = s_key[q0 + m];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) rk[u] += km < kk[u];
-      }
-      sync();
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (tid + u * kFinT < n) {
-          s_key[q0 + rk[u]] = kk[u];
-          s_val[q0 + rk[u]] = vv[u];
-        }
-      sync();
-    }
-    for (int j = eb + tid; j < ee; j += kFinT) {
-      idx[j] = s_val[j - eb];
-      key[j] = s_key[j - eb];
-      if (inv && !tr) inv[s_key[j - eb]] = j;  // k_tmap_inv's map, while the keys are at hand
-    }
-  } else if (inv && !tr && i < N) {
-    for (int j = ptr[i]; j < ptr[i + 1]; ++j) inv[key[j]] = j;
-  }
-  if (staged) {
-    // entry-parallel passes (weights, tile marks): lane t takes entries eb + t, + kFinT, ... —
-    // coalesced stores and independent loads (a per-row walk chained 17 dependent gathers per
-    // lane at C5 k = 16). The row of each entry comes from a table in the (now free) key
-    // staging array, written by each lane for its own row (a per-entry binary search chained
-    // six dependent LDS reads: C5 k = 16's source CSR finish 62 -> 46 us with it)
-    sync();  // every lane's write-back reads of s_key are done
-    if (i < N) {
-      const int r1 = ptr[i + 1];
-      for (int j = ptr[i]; j < r1; ++j) s_key[j - eb] = tid;
     }
     sync();
-    // lazy builds took the tile marks in k_count (cross edges) and k_scan (capacity)
-    const bool marks = tile_open && !tr && !lazy;
-    const int64_t ntiles = (N + 63) >> 6;
-#pragma unroll 4
-    for (int j = eb + tid; j < ee; j += kFinT) {
-      const int64_t row = i0 + s_key[j - eb];
-      const int nb = s_val[j - eb];
-      if (wt) wt[j] = norm == LGNN_NORM_GCN ? (dis[nb] * 1.0f) * dis[row] : 1.0f;
+    for (int j = tid; j < n; j += 64) {
+      const int r = s_row[j];
+      const int r0 = s_ptr[r], r1 = s_ptr[r + 1];
+      const int kj = s_key[j], nb = s_val[j];
+      int rank = 0;
+      for (int m = r0; m < r1; ++m) rank += s_key[m] < kj;
+      const int dst = eb + r0 + rank;
+      const int64_t row = i0 + r;
+      idx[dst] = nb;
+      key[dst] = kj;
+      if (wt) wt[dst] = norm == LGNN_NORM_GCN ? (dis[nb] * 1.0f) * dis[row] : 1.0f;
+      if (inv && !tr) inv[kj] = dst;  // k_tmap's map, while the keys are at hand
+      // 64-node tiles an edge leaves are open: the fused layer stacks skip them
       if (marks && (nb >> 6) != (row >> 6)) {
         if (tile_open[row >> 6] == 0) mark_open(tile_open, row >> 6, ntiles);
         if (tile_open[nb >> 6] == 0) mark_open(tile_open, nb >> 6, ntiles);
       }
     }
-    if (marks && i < N && (i & 63) == 0) {
-      const int64_t iend64 = i + 64 < N ? i + 64 : N;
-      if (ptr[iend64] - ptr[i] > lgnn_tile::CAPE_TILE) mark_open(tile_open, i >> 6, ntiles);
-    }
-    sync();  // the staging arrays are free for the next virtual block
+    sync();  // the staging arrays are free for the wave's next virtual block
     return;
   }
+  if (!own) return;
+  const int r0 = ptr[i], r1 = ptr[i + 1];
+  if (add_loop) {
+    idx[r1 - 1] = (int32_t)i;
+    key[r1 - 1] = (int32_t)(E + i);
+  }
+  sort_row(key + r0, idx + r0, r1 - r0);
+  if (inv && !tr)
+    for (int j = r0; j < r1; ++j) inv[key[j]] = j;
   if (wt) {
-    // row of each entry: binary search is avoided by a per-thread row walk (rows are short)
-    if (i < N) {
-      const int r0 = ptr[i], r1 = ptr[i + 1];
-      const float di = norm == LGNN_NORM_GCN ? dis[i] : 1.f;
-      for (int j = r0; j < r1; ++j) {
-        const int nb = staged ? s_val[j - eb] : idx[j];
-        wt[j] = norm == LGNN_NORM_GCN ? (dis[nb] * 1.0f) * di : 1.0f;
-      }
-    }
+    const float di = norm == LGNN_NORM_GCN ? dis[i] : 1.f;
+    for (int j = r0; j < r1; ++j) wt[j] = norm == LGNN_NORM_GCN ? (dis[idx[j]] * 1.0f) * di : 1.0f;
   }
-  // 64-node tiles an edge leaves (source CSR pass) are open: the fused layer stacks skip them.
-  // So are tiles with more CSR entries than a closed tile takes (lgnn_tile::CAPE_TILE).
-  // flag setter: the first writer of a tile also counts it (tile_open[ntiles])
-  auto mark = [&](int64_t t) { mark_open(tile_open, t, (N + 63) >> 6); };
-  if (tile_open && !tr && i < N && (i & 63) == 0) {
-    const int64_t iend64 = i + 64 < N ? i + 64 : N;
-    if (ptr[iend64] - ptr[i] > lgnn_tile::CAPE_TILE) mark(i >> 6);
-  }
-  if (tile_open && !tr && i < N) {
-    const int r0 = ptr[i], r1 = ptr[i + 1];
-    const int64_t ti = i >> 6;
+  if (marks) {
     // a row's neighbours sit in one or two tiles: each tile is looked up (and marked) once per
     // run of equal neighbour tiles, this row's own tile once per row (marks are idempotent)
+    const int64_t ti = i >> 6;
     bool self_done = false;
     int64_t last = -1;
     for (int j = r0; j < r1; ++j) {
-      const int nb = staged ? s_val[j - eb] : idx[j];
-      const int64_t nt = nb >> 6;
+      const int64_t nt = idx[j] >> 6;
       if (nt != ti) {
         if (!self_done) {
-          if (tile_open[ti] == 0) mark(ti);
+          if (tile_open[ti] == 0) mark_open(tile_open, ti, ntiles);
           self_done = true;
         }
         if (nt != last) {
-          if (tile_open[nt] == 0) mark(nt);
+          if (tile_open[nt] == 0) mark_open(tile_open, nt, ntiles);
           last = nt;
         }
       }
     }
   }
-  sync();  // the staging arrays are free for the next virtual block
 }
 
 // one wave: its LDS accesses are ordered by a wave-scope fence (no cross-wave barrier)
@@ -1019,8 +961,8 @@ struct WaveSync {
   }
 };
 
-// four 64-row virtual blocks per workgroup, one per wave (each wave its own staging arrays and
-// wave-scope ordering, as k_build's finish phase): a quarter of the workgroups to dispatch
+// one wave per virtual block, four per workgroup (each wave its own staging arrays and
+// wave-scope ordering), grid-stride over the blocks past kFinGrid workgroups
 constexpr int kFinWaves = kThreads / 64;
 __global__ __launch_bounds__(kThreads) void k_finish(int64_t N, int64_t E, int add_loop, int norm,
                                                      const int32_t* __restrict__ rowptr,
@@ -1034,16 +976,21 @@ __global__ __launch_bounds__(kThreads) void k_finish(int64_t N, int64_t E, int a
                                                      const int32_t* summary) {
   __shared__ int32_t s_key[kFinWaves][kFinishCap];
   __shared__ int32_t s_val[kFinWaves][kFinishCap];
-  __shared__ int32_t s_ptr[kFinWaves][kFinT + 1];
+  __shared__ uint8_t s_row[kFinWaves][kFinishCap];
+  __shared__ int32_t s_ptr[kFinWaves][kFinR + 1];
   const int mode = summary ? __builtin_amdgcn_readfirstlane(*summary) & kModeMask : kModeGeneral;
   if (mode == kModeSorted) return;  // the sorted path took it
   if (mode == kModeSortedOpen && blockIdx.y == 0) return;  // target CSR: k_scan's sorted body
+  const int by = blockIdx.y;
+  if (err_out && blockIdx.x == 0 && by == 0 && threadIdx.x == 0) *err_out = *ws_err;
+  if (lazy && by == 1 && tile_open[(N + 63) >> 6] == 0) return;  // no source CSR needed
   const int wave = threadIdx.x >> 6;
-  const int64_t v = (int64_t)blockIdx.x * kFinWaves + wave;
-  if (v * kFinT >= N) return;
-  finish_body(N, E, add_loop, norm, rowptr, col, eid, w, tptr, tidx, teid, tw, dis, ws_err,
-              err_out, tile_open, lazy, inv, s_key[wave], s_val[wave], s_ptr[wave], v, blockIdx.y,
-              threadIdx.x & 63, WaveSync{});
+  const int64_t nblk = (N + kFinR - 1) / kFinR;
+  for (int64_t v = (int64_t)blockIdx.x * kFinWaves + wave; v < nblk;
+       v += (int64_t)gridDim.x * kFinWaves)
+    finish_body(N, E, add_loop, norm, rowptr, col, eid, w, tptr, tidx, teid, tw, dis, tile_open,
+                lazy, inv, s_key[wave], s_val[wave], s_row[wave], s_ptr[wave], v, by,
+                threadIdx.x & 63, WaveSync{});
 }
 
 // tmap[q] = position in the target CSR of the edge at source-CSR position q (both CSRs hold the
@@ -1292,8 +1239,9 @@ static int graph_build(const int64_t* edge_index, int64_t E, int64_t N, int loop
                          try_sorted ? ws.verdict + kVerdictMax : nullptr);
     LGNN_LAUNCH_CHECK();
   }
-  const int64_t nfin = (N + kFinT - 1) / kFinT;
-  dim3 fg((unsigned)((nfin + kFinWaves - 1) / kFinWaves), tptr ? 2u : 1u);
+  const int64_t nfin = (N + kFinR - 1) / kFinR;
+  const int64_t fgx = (nfin + kFinWaves - 1) / kFinWaves;
+  dim3 fg((unsigned)(fgx < kFinGrid ? fgx : kFinGrid), tptr ? 2u : 1u);
   // with tmap, the target side of k_finish also writes inv (edge id -> target-CSR position)
   if (!skip_general) {
     hipLaunchKernelGGL(k_finish, fg, dim3(kThreads), 0, s, N, E, add_loop, norm, rowptr, col,
