@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LGNN_ABI_VERSION 38
+#define LGNN_ABI_VERSION 39
 
 #define LGNN_OK 0
 #define LGNN_EINVAL (-22)
@@ -652,7 +652,10 @@ int lgnn_gcn_stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t*
  *   device pointers) + S (host array of L pointers: S[l - 1] [M][K_l] receives Â H_{l-1} of the
  *   open tiles, read by the backward's open phase).
  * lgnn_gcn_stack_bwd_s3f_all = lgnn_gcn_stack_bwd_s3f + the transpose CSR (tptr / tidx / tw),
- *   W, S (as above) and dS_ws (2 * M * 128 floats of workspace); with dlogits [B][C] and Wout
+ *   W, S (as above) and dS_ws (2 * M * 128 floats of workspace). L = 3 (ABI v39; this entry and
+ *   _ce only): dS_ws holds 3 * M * 128 floats, its last block receives dZ_0 [M][widths[1]] (the
+ *   in_proj output gradient, every row) and dWp[0] / dbp[0] are not written — the caller forms
+ *   dW_0 = dZ_0^T X and db_0 = colsum dZ_0 (lgnn_s3_wgrad). With dlogits [B][C] and Wout
  *   [C][N_L] (C <= 8) the pooled-output gradient dP = dlogits Wout (out_proj backward) is formed
  *   inside the kernel and dP may be NULL (lgnn_pool_head_bwd then only needs dWout / dbout, and
  *   can run concurrently).

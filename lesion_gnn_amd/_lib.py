@@ -168,7 +168,7 @@ SIGNATURES: dict[str, tuple] = {
     "lgnn_cc_pool": (I32, [P, I32, I64, P, I32, I32, P, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 38
+ABI_VERSION = 39
 
 _lib = None
 

@@ -512,6 +512,7 @@ struct FBwdArgs {
   float* dWp[LGNN_MAX_STACK];     // [P][N_l][K_l]
   float* dbp[LGNN_MAX_STACK];     // [P][N_l]
   int width[LGNN_MAX_STACK + 1];
+  float* dZ0;                     // XIN: [M][N_0] in_proj output gradient (dWp[0] / dbp[0] unused)
 };
 
 // Open-tile phase of the fused backward (optional): after this workgroup wrote its partial
@@ -667,22 +668,59 @@ constexpr bool kAdjPipe = false;
 constexpr bool kAdjPipe = true;
 #endif
 
-template <int NL, bool AG>
+// The open-tile gather of the in_proj gradient for XIN launches: dZ_0 rows of the open tiles
+// = Â^T dS_1 through the transposed CSR (one wave per row, two features per lane)
+__device__ __forceinline__ void open_dz0(float* __restrict__ dZ0, const float* __restrict__ dS,
+                                         const int32_t* __restrict__ tptr,
+                                         const int32_t* __restrict__ tidx,
+                                         const float* __restrict__ tw, int64_t M, int N,
+                                         const int32_t* __restrict__ tmask) {
+  const int64_t ntiles = (M + TM - 1) / TM;
+  const int c = 2 * (threadIdx.x & 63), wave = threadIdx.x >> 6;
+  for (int64_t t = seek_tile(xcd_block(), ntiles, tmask, 1); t < ntiles;
+       t = seek_tile(t + gridDim.x, ntiles, tmask, 1)) {
+    for (int rr = wave; rr < TM; rr += NT / 64) {
+      const int64_t row = t * TM + rr;
+      if (row >= M) break;
+      float a0 = 0.f, a1 = 0.f;
+      const int j1 = tptr[row + 1];
+      for (int j = tptr[row]; j < j1; ++j) {
+        const float wgt = tw[j];
+        const int64_t src = tidx[j];
+        if (c < N) {
+          a0 += wgt * dS[src * N + c];
+          a1 += wgt * dS[src * N + c + 1];
+        }
+      }
+      if (c < N) {
+        dZ0[row * N + c] = a0;
+        dZ0[row * N + c + 1] = a1;
+      }
+    }
+  }
+}
+
+// XIN (NL = 4: in_proj + 3 convs): the in_proj weight gradient is not accumulated here — three
+// layers of dW fill the accumulator registers (192 of 512 per lane at one wave per SIMD), a fourth
+// would spill — the kernel writes dZ_0 (the in_proj output gradient) instead and the caller forms
+// dW_0 = dZ_0^T X, db_0 = colsum dZ_0 with one split-3 weight-gradient GEMM (lgnn_s3_wgrad)
+template <int NL, bool AG, bool XIN = false>
 __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ rowptr,
                                                    const int32_t* __restrict__ col,
                                                    const float* __restrict__ w, int64_t M,
                                                    FBwdArgs a, const int32_t* __restrict__ tmask,
                                                    OpenBwdArgs o) {
   constexpr int L = NL - 1;
+  constexpr int ND = XIN ? NL - 1 : NL;  // layers whose dW is accumulated here
   __shared__ __attribute__((aligned(16))) FBwdSmem sm;
   const int64_t ntiles = (M + TM - 1) / TM;
   float* const scr = reinterpret_cast<float*>(sm.Adj[0]);  // fp32 Â^T [source][target]
   const int NLast = a.width[L + 1];
   const Buf bP = mkbuf(a.dP, a.num_graphs * NLast * 4);
 
-  f32x16 dw[NL][4];
+  f32x16 dw[ND][4];
 #pragma unroll
-  for (int l = 0; l < NL; ++l)
+  for (int l = 0; l < ND; ++l)
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) dw[l][kb] = f32x16{};
   float dbacc[NL];
@@ -1032,7 +1070,7 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
       }
       // this tile's X rows for the in_proj phase, in flight from the first conv's dW on (issued
       // at the last conv they crowded that phase's load queue: in-step 107.6 -> 106.0 us)
-      if (l == L) {
+      if (!XIN && l == L) {
         const int tq = fresh_tid();
         const int h = (tq >> 5) & 1, k = 32 * (tq >> 6) + (tq & 31);
         load_pt(xp, a.X, (ABL & 16) ? 0 : M, r0, a.width[0], k, a.width[0], h);
@@ -1053,7 +1091,8 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
             const int off = hf_chunk(32 * kb + li, 2 * s + h);
 #pragma unroll
             for (int p = 0; p < 3; ++p) hb[p] = lds16(sm.Img[p] + off);
-            if constexpr (!(ABL & 1)) dw[l][kb] = mfma_s3(gp[s], hb, dw[l][kb]);
+            if constexpr (!(ABL & 1))
+              dw[XIN ? l - 1 : l][kb] = mfma_s3(gp[s], hb, dw[XIN ? l - 1 : l][kb]);
           }
           if (s == 1) load_w2(wb, 1);
           S3F_SB();
@@ -1106,6 +1145,42 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
       lds_barrier();  // every read of both images done
       STAMP(stamp++);
     }
+    if constexpr (XIN) {
+      // in_proj outside: this tile's dZ_0 rows to HBM (feature k on the lane: 128-B row pieces)
+      if constexpr (AG && kAdjPipe) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (fresh_tid() == 0) sm.flag = 0;
+      }
+      {
+        const int tq = fresh_tid();
+        const int h = (tq >> 5) & 1, k = 32 * (tq >> 6) + (tq & 31);
+        const int N0 = a.width[1];
+        if (k < N0) {
+#pragma unroll
+          for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int64_t row = r0 + 32 * q + (r & 3) + 8 * (r >> 2) + 4 * h;
+              if (row < M) a.dZ0[row * N0 + k] = dz[q][r];
+            }
+        }
+        pre_cnt = (has_next && tq < TM) ? a.gptr[pre_g + 1] - a.gptr[pre_g] : 0;
+        if (has_head(a)) {
+#pragma unroll
+          for (int c = 0; c < kMaxHeadC; ++c)
+            pre_dl[c] = (has_next && tq < TM && c < a.C) ? head_raw(a, pre_g, c) : 0.f;
+          if (a.ce.pm) pre_wt = (has_next && tq < TM) ? a.ce.wt[pre_g] : 0.f;
+        }
+      }
+      lds_barrier();  // every wave's next-tile Â landed
+      if constexpr (AG && kAdjPipe) {
+        const AdjPlanes nap = adj_split(sm);
+        lds_barrier();  // every scratch read done (the planes overwrite it)
+        adj_write(sm, nap);
+        lds_barrier();  // the next tile's Â^T planes are in place
+      }
+      STAMP(stamp++);
+    } else {
     // in_proj: db_0, dW_0 += dZ_0^T X
     {
       const int K = a.width[0];
@@ -1162,7 +1237,7 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
             const int off = hf_chunk(32 * kb + li, 2 * s + h);
 #pragma unroll
             for (int p = 0; p < 3; ++p) hb[p] = lds16(sm.Img[p] + off);
-            if constexpr (!(ABL & 1)) dw[0][kb] = mfma_s3(gp[s], hb, dw[0][kb]);
+            if constexpr (!(ABL & 1) && !XIN) dw[0][kb] = mfma_s3(gp[s], hb, dw[0][kb]);
           }
           // the next tile's Â split beside the products (independent VALU / LDS work)
           if constexpr (AG && kAdjPipe) {
@@ -1180,6 +1255,7 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
       }
       STAMP(stamp++);
     }
+    }
     t = tn;
   }
   // partial slot blockIdx.x of every layer: dW rows n = 32 wave + (r & 3) + 8 (r >> 2) + 4h,
@@ -1188,7 +1264,7 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
     const int tq = threadIdx.x;
     const int h = (tq >> 5) & 1, li = tq & 31, wv = tq >> 6;
 #pragma unroll
-    for (int l = 0; l < NL; ++l) {
+    for (int l = XIN ? 1 : 0; l < NL; ++l) {
       const int N = a.width[l + 1], K = a.width[l];
       float* slab = a.dWp[l] + (int64_t)blockIdx.x * N * K;
 #pragma unroll
@@ -1200,7 +1276,7 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
           if (n < N && k < K) {
             // write-through (sc1): the slab lines leave this XCD's L2 as they are written
             // instead of at the kernel-end write-back (one-box A/B: step 0.2306 -> 0.2294 ms)
-            st_wt(slab + (int64_t)n * K + k, dw[l][kb][r]);
+            st_wt(slab + (int64_t)n * K + k, dw[XIN ? l - 1 : l][kb][r]);
           }
         }
       }
@@ -1226,6 +1302,8 @@ __global__ __launch_bounds__(NT, 1) void k_s3_fbwd(const int32_t* __restrict__ r
             lw.A, lw.C, lw.ti, o.dS[(l + 1) & 1], a.batch, a.gptr, a.pool_mean, o.tptr, o.tidx,
             o.tw, 0.f, a.H[l], Sx, M, K, o.W[l], N, o.dS[l & 1], a.dWp[l], a.dbp[l], tmask, 1,
             1);
+      else if constexpr (XIN)
+        open_dz0(a.dZ0, o.dS[1], o.tptr, o.tidx, o.tw, M, N, tmask);
       else
         bwd_tiles<LGNN_GRAD_TRANSPOSE, LGNN_ACT_NONE, false>(
             lw.A, lw.C, lw.ti, o.dS[1], a.batch, a.gptr, a.pool_mean, o.tptr, o.tidx, o.tw, 0.f,
@@ -1245,7 +1323,7 @@ static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* g
                          const int32_t* tile_open, const lgnn_s3::OpenBwdArgs& o, void* stream,
                          const float* dlogits = nullptr, const float* Wout = nullptr,
                          int num_classes = 0, const void* adjt = nullptr,
-                         const lgnn_ce_src* ce = nullptr);
+                         const lgnn_ce_src* ce = nullptr, float* dz0 = nullptr);
 
 extern "C" int lgnn_gcn_stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* gptr,
                                       int pool_mean, int64_t num_graphs, const int32_t* rowptr,
@@ -1268,7 +1346,7 @@ static int stack_bwd_s3f_all(
     const float* const* S, const int* widths, float* const* dWp, float* const* dbp,
     int num_partials, float* dS_ws, int32_t* tile_open, const float* dlogits,
     const lgnn_ce_src* ce, const float* Wout, int num_classes, const void* adjt, void* stream) {
-  if (M < 0 || L < 1 || L > 2 || !W || !S || !tptr || !tidx || !tw || !dS_ws || !tile_open)
+  if (M < 0 || L < 1 || L > 3 || !W || !S || !tptr || !tidx || !tw || !dS_ws || !tile_open)
     return LGNN_EINVAL;
   if ((dlogits || ce) && (!Wout || num_classes < 1 || num_classes > lgnn_s3::kMaxHeadC))
     return LGNN_EINVAL;
@@ -1285,9 +1363,10 @@ static int stack_bwd_s3f_all(
   o.tw = tw;
   const int64_t ntiles = (M + lgnn_tile::TM - 1) / lgnn_tile::TM;
   o.sync = tile_open + ntiles + 4;
+  // L = 3: the third [M][128] block of dS_ws receives dZ_0 (the in_proj gradient is the caller's)
   return stack_bwd_s3f(dP, batch, gptr, pool_mean, num_graphs, rowptr, col, w, X, M, L, planes_t,
                        H, widths, dWp, dbp, num_partials, tile_open, o, stream, dlogits, Wout,
-                       num_classes, adjt, ce);
+                       num_classes, adjt, ce, L == 3 ? dS_ws + 2 * M * lgnn_s3::WP : nullptr);
 }
 
 extern "C" int lgnn_gcn_stack_bwd_s3f_all(
@@ -1324,8 +1403,9 @@ static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* g
                          float* const* dWp, float* const* dbp, int num_partials,
                          const int32_t* tile_open, const lgnn_s3::OpenBwdArgs& o, void* stream,
                          const float* dlogits, const float* Wout, int num_classes,
-                         const void* adjt, const lgnn_ce_src* ce) {
-  if (M < 0 || L < 1 || L > 2 || !(dP || dlogits || ce) || !batch || !gptr || !rowptr || !col ||
+                         const void* adjt, const lgnn_ce_src* ce, float* dz0) {
+  // L = 3 (XIN) only with the open-tile phase in the launch: it gathers the open tiles' dZ_0 rows
+  if (M < 0 || L < 1 || L > 3 || (L == 3 && (!dz0 || !o.sync)) || !(dP || dlogits || ce) || !batch || !gptr || !rowptr || !col ||
       !X ||
       !planes_t || !H || !widths || !dWp || !dbp || !tile_open || num_graphs < 0)
     return LGNN_EINVAL;
@@ -1347,6 +1427,7 @@ static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* g
   a.num_graphs = num_graphs;
   a.X = X;
   a.WpT = planes_t;
+  a.dZ0 = dz0;
   for (int l = 0; l <= L + 1; ++l) a.width[l] = widths[l];
   for (int l = 0; l <= L; ++l) {
     if (!lgnn_tile_fits(M, widths[l], widths[l + 1]) || !H[l] || !dWp[l] || !dbp[l])
@@ -1368,7 +1449,13 @@ static int stack_bwd_s3f(const float* dP, const int64_t* batch, const int32_t* g
     const int cap = lgnn_fused_grid_capacity(1);
     if (cap < (int)grid.x) return cap == LGNN_EINVAL ? cap : cap < 0 ? -cap : LGNN_EBUSY;
   }
-  if (L == 1 && adjt)
+  if (L == 3 && adjt)
+    hipLaunchKernelGGL((lgnn_s3::k_s3_fbwd<4, true, true>), grid, blk, 0, s, rowptr, col, w, M, a,
+                       tile_open, o);
+  else if (L == 3)
+    hipLaunchKernelGGL((lgnn_s3::k_s3_fbwd<4, false, true>), grid, blk, 0, s, rowptr, col, w, M,
+                       a, tile_open, o);
+  else if (L == 1 && adjt)
     hipLaunchKernelGGL((lgnn_s3::k_s3_fbwd<2, true>), grid, blk, 0, s, rowptr, col, w, M, a,
                        tile_open, o);
   else if (L == 1)

@@ -241,7 +241,10 @@ def bwd_planes_numel(L: int, M) -> int:
 
 
 def _s3f(L: int) -> bool:
-    return BWD_MODE == "s3f" and L <= 2
+    """The fused split-3 backward takes L <= 2 convs in one launch, and L = 3 with the in_proj
+    weight gradient outside it (the kernel writes dZ_0; stack_bwd runs the GEMM) when its
+    open-tile phase runs in the same launch (stack_bwd checks that; otherwise layer-major s3)."""
+    return BWD_MODE == "s3f" and L <= 3
 
 
 # the split-3 forward hands each closed tile's Â^T planes to the fused backward (ADJT = False: the
@@ -326,7 +329,7 @@ def stack_fwd(x: torch.Tensor, graph: Graph, Ws: list, bs: list, keep: dict | No
 def head_in_stack_bwd(graph: Graph, L: int, C: int, s3: bool) -> bool:
     """True when stack_bwd's single split-3 launch forms dP = dlogits W_out itself (out_proj
     backward folded into the kernel's pool prologue, <= 8 classes)."""
-    return (HEAD_FOLD and s3 and BWD_MODE == "s3f" and L <= 2 and C <= 8 and
+    return (HEAD_FOLD and s3 and BWD_MODE == "s3f" and L <= 3 and C <= 8 and
             _open_in_fused(OPEN_IN_FUSED_BWD, graph, "bwd"))
 
 
@@ -345,7 +348,7 @@ def stack_bwd(dp: torch.Tensor | None, x: torch.Tensor, graph: Graph, mean: bool
     dev = x.device
     lib = _lib.load()
     s3 = planes_t is not None
-    s3f = s3 and _s3f(L)
+    s3f = s3 and _s3f(L) and (L <= 2 or _open_in_fused(OPEN_IN_FUSED_BWD, graph, "bwd"))
     # the forward's Â^T tiles: their own buffer (adjt_t), or room after the planes (weight_planes'
     # `extra`); none -> the backward rebuilds them from the CSR
     adjt = (_lib.ptr(adjt_t) if adjt_t is not None else _adjt_ptr(planes_t, L)) if s3f else None
@@ -367,7 +370,8 @@ def stack_bwd(dp: torch.Tensor | None, x: torch.Tensor, graph: Graph, mean: bool
     ce = dlog if isinstance(dlog, _lib.CeSrc) else None  # CE-formed logits gradient
     B = dp.size(0) if dp is not None else (graph.num_graphs if ce is not None else dlog.size(0))
     if s3f and _open_in_fused(OPEN_IN_FUSED_BWD, graph, "bwd"):  # one launch, open tiles last
-        dS_ws = torch.empty(2 * M * 128, dtype=torch.float32, device=dev)
+        # L = 3: the third [M][128] block receives dZ_0, the in_proj output gradient
+        dS_ws = torch.empty((3 if L == 3 else 2) * M * 128, dtype=torch.float32, device=dev)
         common = (_lib.ptr(graph.batch), _lib.ptr(graph.gptr), int(mean), B,
                   _lib.ptr(csr.rowptr), _lib.ptr(csr.col), _lib.ptr(csr.w), _lib.ptr(csr.tptr),
                   _lib.ptr(csr.tidx), _lib.ptr(csr.tw), _lib.ptr(x), M, L, _lib.ptr(planes_t),
@@ -381,6 +385,10 @@ def stack_bwd(dp: torch.Tensor | None, x: torch.Tensor, graph: Graph, mean: bool
         else:
             _lib.call("lgnn_gcn_stack_bwd_s3f_all", _lib.ptr(dp), *common, _lib.ptr(dlog),
                       _lib.ptr(W_out), W_out.size(0) if head else 0, adjt, _s(dev))
+        if L == 3:  # in_proj: (dW_0, db_0) = (dZ_0^T X, colsum dZ_0), one split-3 GEMM
+            dz0 = dS_ws[2 * M * 128:2 * M * 128 + M * widths[1]].view(M, widths[1])
+            first = dense_wgrad(dz0, x, False, want_db=True, reducer=reducer)
+            return [first] + _stack_bwd_outputs(L, widths, dWp, dbp, P, dev, reducer, l0=1)
         return _stack_bwd_outputs(L, widths, dWp, dbp, P, dev, reducer)
     assert head is None, "dP from the logits gradient only in the single-launch split-3 path"
     if s3f:  # one fused split-3 launch, every layer of a tile in one pass (stack3_bwd.hip)
@@ -424,9 +432,9 @@ def stack_bwd(dp: torch.Tensor | None, x: torch.Tensor, graph: Graph, mean: bool
     return _stack_bwd_outputs(L, widths, dWp, dbp, P, dev, reducer)
 
 
-def _stack_bwd_outputs(L, widths, dWp, dbp, P, dev, reducer):
+def _stack_bwd_outputs(L, widths, dWp, dbp, P, dev, reducer, l0=0):
     out = []
-    for l in range(L + 1):
+    for l in range(l0, L + 1):
         dW = torch.empty(widths[l + 1], widths[l], dtype=torch.float32, device=dev)
         db = torch.empty(widths[l + 1], dtype=torch.float32, device=dev)
         reducer.extend([(dWp[l], P, dW.numel(), dW), (dbp[l], P, db.numel(), db)])

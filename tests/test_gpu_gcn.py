@@ -306,8 +306,9 @@ def test_gcn_fused_backward(cuda, case, bwd, monkeypatch):
     the 1024 staged in registers are read from the CSR as the tile's Â is built).
     c2_L3: three convs (fp32: layer-wise backward on recomputed aggregates; split-3: fused).
     bwd: the fp32 fused kernel (lgnn_gcn_stack_bwd), the split-3 layer-major kernels
-    (lgnn_gcn_stack_bwd_s3) or the fused split-3 kernel (lgnn_gcn_stack_bwd_s3f; L <= 2, so c2_L3
-    takes the layer-major one)."""
+    (lgnn_gcn_stack_bwd_s3) or the fused split-3 kernel (lgnn_gcn_stack_bwd_s3f; c2_L3: the
+    single-launch entry with three conv layers' dW in the kernel and the in_proj weight gradient
+    as a split-3 GEMM on the dZ_0 it writes)."""
     pool = "add" if case.endswith("add") else "mean"
     hidden = [128, 128] if "L1" in case else [128] * 4 if "L3" in case else [128, 128, 128]
     if case.startswith("c2"):
@@ -347,19 +348,21 @@ def test_gcn_fused_backward(cuda, case, bwd, monkeypatch):
         assert torch.equal(gf[k], gf2[k]), k
 
 
+@pytest.mark.parametrize("convs", [2, 3])
 @pytest.mark.parametrize("open_in_fused", [True, False])
-def test_open_tiles_in_fused_launch(cuda, open_in_fused, monkeypatch):
+def test_open_tiles_in_fused_launch(cuda, open_in_fused, convs, monkeypatch):
     """Open tiles (graphs straddling 64-node tiles, an over-capacity tile) processed inside the
     fused split-3 launches (layer by layer behind grid barriers) == the separate layer-wise
     launches == the oracle; the same Graph reused for a second step (the barrier words re-arm
-    themselves: every word back to 0, no barrier gave up)."""
+    themselves: every word back to 0, no barrier gave up). convs = 3: the open phase gathers the
+    open tiles' dZ_0 rows for the in_proj GEMM (layer-major s3 backward without open_in_fused)."""
     from lesion_gnn_amd.graph import Graph
 
     monkeypatch.setattr(ops, "OPEN_IN_FUSED", open_in_fused)
     monkeypatch.setattr(ops, "OPEN_IN_FUSED_BWD", open_in_fused)
     sizes = [1, 5, 64, 200, 2, 33, 512, 17, 64, 64, 30, 34]
     b = synth.make_batch(len(sizes), k=6, d_in=128, seed=41, sizes=sizes)
-    ours, oref = make_pair([128, 128, 128])
+    ours, oref = make_pair([128] * (convs + 1))
     ours = ours.to(cuda)
     g = Graph(b.edge_index.to(cuda), b.num_nodes, b.batch.to(cuda), b.num_graphs)
     nt = (b.num_nodes + 63) // 64
