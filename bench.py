@@ -564,20 +564,34 @@ def _entry_model(name, a, gs):
         by = f4 * M * (wd[L + 1] + sum(wd[l] + wd[l + 1] + wd[l] for l in range(1, L + 1))
                        + wd[0] + wd[1]) + 8.0 * nz * L
         return by, 2.0 * R * wd[0] * wd[1] + 2 * conv
+    if name in ("lgnn_gcn_stack_bwd_s3f_ce", "lgnn_gcn_stack_bwd_s3f_all"):
+        # fused split-3 backward (closed tiles; the open ones add their layer-wise bodies): per
+        # conv dW_l and dH (2 M K N each) and G = Â^T dZ (2 nnz N); in_proj's dW in the kernel for
+        # L <= 2, outside it (dZ_0 written, the lgnn_s3_wgrad entry) for L = 3. Reads H_0..H_L,
+        # X (L <= 2), the forward's Â tiles (64 x 64 fp32 per 64 rows); dW written once
+        i = 11 if name.endswith("_ce") else 12
+        M, L, wd = a[i], a[i + 1], list(a[i + 6])
+        conv = sum(4.0 * M * wd[l] * wd[l + 1] + 2.0 * gs.nnz * wd[l + 1] for l in range(1, L + 1))
+        inproj = L <= 2
+        by = f4 * M * (sum(wd[1:L + 2]) + (wd[0] if inproj else wd[1]) + 64) \
+            + f4 * sum(wd[l] * wd[l + 1] for l in range(0 if inproj else 1, L + 1))
+        return by, conv + (2.0 * M * wd[0] * wd[1] if inproj else 0.0)
     return None
 
 
 # the MFMA roof of a modelled entry (useful fp32 FLOP): split-3 bf16 entries against dense bf16 / 6,
 # the fp32-MFMA tile kernels against the fp32 peak
 _S3_ENTRIES = ("lgnn_s3_gemm", "lgnn_s3_gemm_act", "lgnn_s3_wgrad", "lgnn_gcn_stack_fwd_s3_all",
-               "lgnn_gcn_stack_bwd_s3")
+               "lgnn_gcn_stack_bwd_s3", "lgnn_gcn_stack_bwd_s3f_ce", "lgnn_gcn_stack_bwd_s3f_all")
 
 
 # kernel-name fragments of the modelled entries without a _entry_kernel mapping (PMC lookups)
 _ENTRY_TRACE = {"lgnn_s3_gemm": "lgnn_s3::k_s3_gemm", "lgnn_s3_gemm_act": "lgnn_s3::k_s3_gemm",
                 "lgnn_s3_wgrad": "lgnn_s3::k_s3_wgrad2", "lgnn_spmm": "::k_spmm",
                 "lgnn_gcn_stack_fwd_s3_all": "lgnn_s3::k_s3_fwd",
-                "lgnn_gcn_stack_bwd_s3": "lgnn_s3::k_s3_bwd"}
+                "lgnn_gcn_stack_bwd_s3": "lgnn_s3::k_s3_bwd",
+                "lgnn_gcn_stack_bwd_s3f_ce": "lgnn_s3::k_s3_fbwd",
+                "lgnn_gcn_stack_bwd_s3f_all": "lgnn_s3::k_s3_fbwd"}
 
 
 def _entry_kernel(name, a):
