@@ -270,7 +270,7 @@ def _time_launches(launch, dev, reps=20):
 
 def time_dominant_kernels(model, b, dev):
     """The two largest kernels of the C2 step, each launched alone with the step's arguments:
-    * lgnn_s3::k_s3_fbwd<L + 1, true> (`lgnn_gcn_stack_bwd_s3f_ce`, stack3_bwd.hip) — the fused
+    * lgnn_s3::k_s3_fbwd<L + 1, true, false> (`lgnn_gcn_stack_bwd_s3f_ce`, stack3_bwd.hip) — the fused
       split-3 backward of in_proj + L GCN convs with the CE logits gradient and out_proj's dP
       formed in its prologue; useful FLOP per launch 2*M*(d_in*h + L*h*h) (dW) + 2*M*L*h*h
       (dH = G W) + 2*nnz*h*L (the transposed aggregation);
@@ -354,12 +354,14 @@ def time_dominant_kernels(model, b, dev):
                       dbp, P, dS_ws.data_ptr(), open_.data_ptr(), ctypes.byref(ce),
                       W_out.data_ptr(), C, _lib.ptr(adjt), s)
 
-        out.append({"kernel": f"lgnn_s3::k_s3_fbwd<{L + 1}, {str(ops.ADJT).lower()}> (fused GCN "
+        out.append({"kernel": f"lgnn_s3::k_s3_fbwd<{L + 1}, {str(ops.ADJT).lower()}, false> "
+                              "(fused GCN "
                               "backward, all layers, "
                               "split-3 bf16 MFMA)",
                     "ms": _time_launches(bwd_s3f, dev), "flops": bwd_flops,
                     "peak": MFMA_S3_PEAK_TF,
-                    "trace_name": f"void lgnn_s3::k_s3_fbwd<{L + 1}, {str(ops.ADJT).lower()}>"})
+                    "trace_name": f"void lgnn_s3::k_s3_fbwd<{L + 1}, "
+                                  f"{str(ops.ADJT).lower()}, false>"})
     else:
         out.append({"kernel": f"lgnn_tile::k_stack_bwd<{L + 1}> (fused GCN backward, all "
                               "layers)",
