@@ -20,6 +20,7 @@ from an uninterrupted run's, as torch's own dropout stream does after a resume.
 from __future__ import annotations
 
 import ctypes
+import math
 
 import torch
 
@@ -101,10 +102,13 @@ def get_state(state: torch.Tensor) -> tuple[int, int]:
 
 def threshold_scale(p: float) -> tuple[int, float]:
     """(thr, scale): keep element i when its 24 random bits are >= thr = floor(p * 2^24); kept
-    values are multiplied by scale = fp32(1 / (1 - p))."""
+    values are multiplied by scale = fp32(1 / (1 - p)), rounded to fp32 (nearest, ties to even)
+    in plain Python arithmetic: a torch scalar here was a `Tensor.item()` graph break under
+    torch.compile (the reference experiment compiles its model with dropout 0.35)."""
     if not 0.0 <= p < 1.0:
         raise ValueError(f"dropout probability must be in [0, 1), got {p}")
-    return int(p * 16777216.0), float(torch.tensor(1.0 / (1.0 - p), dtype=torch.float32))
+    m, e = math.frexp(1.0 / (1.0 - p))  # 1 / (1 - p) >= 1: a normal fp32 number
+    return int(p * 16777216.0), math.ldexp(round(m * 16777216.0), e - 24)
 
 
 def key(module, p: float) -> str:

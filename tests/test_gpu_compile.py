@@ -109,6 +109,26 @@ def test_compiled_model_matches_eager_and_oracle(cuda, name):
     assert torch._dynamo.utils.counters["stats"]["unique_graphs"] <= 2  # no per-size recompile
 
 
+def test_compiled_dropout_model_is_one_graph(cuda):
+    """The reference experiment trains the compiled GAT with dropout 0.35 (configs/config.py:
+    52-65): with fullgraph=True a graph break (round 5: the mask scale's fp32 rounding went
+    through a torch scalar and `.item()` on the GPU box) fails the compile; the compiled step then
+    draws the same masks as the eager one (same generator state) and matches it bit for bit."""
+    torch.manual_seed(1234)
+    m = GAT(1025, [128] * 4, 1, heads=2, dropout=0.35).train()
+    eager, comp = clone_to(m, cuda), clone_to(m, cuda)
+    torch._dynamo.reset()
+    compiled = torch.compile(comp, dynamic=True, fullgraph=True)
+    b = synth.make_batch(64, n=64, k=6, d_in=1025, seed=44, sizes="lognormal",
+                         last_channel_class=True)
+    lc, gc = step(compiled, b, cuda, "MSE")
+    le, ge = step(eager, b, cuda, "MSE")
+    gc = strip(gc)
+    assert torch.equal(lc, le), (lc - le).abs().max()
+    for k in ge:
+        assert torch.equal(gc[k], ge[k]), k
+
+
 def test_compiled_drgnet(cuda):
     """DRGNet (drgnet.py:103 compiles it): lgnn ops for the GraphConv stack, the weighted CSR and
     SortAggregation; the head's torch ops go through Inductor, so the compiled model matches
