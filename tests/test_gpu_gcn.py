@@ -387,8 +387,9 @@ def test_open_tiles_in_fused_launch(cuda, open_in_fused, convs, monkeypatch):
     assert torch.equal(results[0][0], results[1][0])
 
 
-@pytest.mark.parametrize("classes,pool", [(5, "mean"), (8, "add"), (12, "mean")])
-def test_head_backward_folded_into_stack(cuda, classes, pool, monkeypatch):
+@pytest.mark.parametrize("classes,pool,convs", [(5, "mean", 2), (8, "add", 2), (12, "mean", 2),
+                                                (8, "add", 3), (12, "mean", 3)])
+def test_head_backward_folded_into_stack(cuda, classes, pool, convs, monkeypatch):
     """out_proj backward folded into the single split-3 backward launch (dP = dlogits W_out
     formed in the pool prologue of closed tiles and in the open-tile phase, dW_out / db_out as
     jobs of the slab reduction; <= 8 classes, 12 falls back to lgnn_pool_head_bwd) and the same
@@ -400,11 +401,11 @@ def test_head_backward_folded_into_stack(cuda, classes, pool, monkeypatch):
     sizes = [1, 5, 64, 200, 2, 33, 512, 17, 64, 64, 30, 34] * 3
     b = synth.make_batch(len(sizes), k=6, d_in=128, seed=43, sizes=sizes)
     b.y = b.y % classes
-    ours, oref = make_pair([128, 128, 128], classes=classes, pool=pool)
+    ours, oref = make_pair([128] * (convs + 1), classes=classes, pool=pool)
     ours = ours.to(cuda)
     if ops.BWD_S3:
         g = Graph(b.edge_index.to(cuda), b.num_nodes, b.batch.to(cuda), b.num_graphs)
-        assert ops.head_in_stack_bwd(g, 2, classes, True) == (classes <= 8)
+        assert ops.head_in_stack_bwd(g, convs, classes, True) == (classes <= 8)
     results = []
     for fold in (True, False):
         monkeypatch.setattr(ops, "HEAD_FOLD", fold)
