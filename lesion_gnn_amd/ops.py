@@ -146,7 +146,16 @@ def _open_in_fused(mode, graph: Graph, direction: str) -> bool:
     ntiles = (M + 63) // 64
     grid = min(ntiles, 512) if direction == "fwd" else \
         _lib.load().lgnn_gcn_stack_bwd_partials(M)
-    return grid <= fused_grid_capacity(direction, graph.edge_index.device)
+    return grid <= fused_grid_capacity(direction, _graph_device(graph))
+
+
+def _graph_device(graph):
+    """The device of a Graph, or of the graph bundle a compiled op body rebuilds (TGraph: no
+    edge_index, its CSR / batch tensors instead)."""
+    ei = getattr(graph, "edge_index", None)
+    if ei is not None:
+        return ei.device
+    return (graph.gptr if graph.gptr is not None else graph.batch).device
 
 
 def _mode_open_in_fused(mode, graph: Graph, direction: str) -> bool:

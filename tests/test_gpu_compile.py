@@ -63,6 +63,10 @@ CASES = {
     "gat_fp32": dict(d_in=128, sizes="lognormal", k=6, B=(64, 33), loss="MSE", tol=1e-4),
     "gin_add_train": dict(d_in=128, sizes="fixed", k=8, B=(256, 100), loss="CE", tol=1e-4),
     "gcn": dict(d_in=128, sizes="powerlaw", k=8, B=(128, 57), loss="CE", tol=1e-4),
+    # graphs aligned to tiles (C2's shape): the single-launch backward with its open-tile phase
+    "gcn_c2": dict(d_in=128, sizes="fixed", k=8, B=(128, 64), loss="CE", tol=1e-4),
+    # three convs on graphs aligned to tiles: the fused backward with in_proj's GEMM outside it
+    "gcn3": dict(d_in=128, sizes="fixed", k=8, B=(128, 64), loss="CE", tol=1e-4),
 }
 
 
@@ -77,8 +81,9 @@ def build(name):
         ours = GIN(128, [128, 128, 128], 5, 0.0, pool="add")
         oref = ref.GIN(128, [128, 128, 128], 5, 0.0, pool="add")
     else:
-        ours = GCN(128, [128, 128, 128], 5, 0.0)
-        oref = ref.GCN(128, [128, 128, 128], 5, 0.0)
+        hidden = [128] * (4 if name == "gcn3" else 3)
+        ours = GCN(128, hidden, 5, 0.0)
+        oref = ref.GCN(128, hidden, 5, 0.0)
     oref.load_state_dict(ours.state_dict())
     return ours.train(), oref.train()
 
