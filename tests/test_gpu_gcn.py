@@ -297,7 +297,7 @@ def test_tile_open_flags(cuda):
 
 @pytest.mark.parametrize("bwd", ["f32", "s3", "s3f"])
 @pytest.mark.parametrize("case", ["c2_L2", "irregular_L2", "irregular_L1_add", "dense_tiles",
-                                  "wide_tiles", "c2_L3"])
+                                  "wide_tiles", "c2_L3", "irregular_L3"])
 def test_gcn_fused_backward(cuda, case, bwd, monkeypatch):
     """lgnn_gcn_stack_bwd (closed tiles, fused) + masked accumulating layer-wise backward (open
     tiles) vs the layer-wise backward and the oracle. dense_tiles: 64-node graphs with k = 40
@@ -305,6 +305,8 @@ def test_gcn_fused_backward(cuda, case, bwd, monkeypatch):
     build. wide_tiles: k = 20 and k = 32 (1280 and 2048 entries: closed tiles whose entries past
     the 1024 staged in registers are read from the CSR as the tile's Â is built).
     c2_L3: three convs (fp32: layer-wise backward on recomputed aggregates; split-3: fused).
+    irregular_L3: three convs on graphs that straddle tiles (split-3: the layer-major kernels,
+    the open tiles then run in separate launches).
     bwd: the fp32 fused kernel (lgnn_gcn_stack_bwd), the split-3 layer-major kernels
     (lgnn_gcn_stack_bwd_s3) or the fused split-3 kernel (lgnn_gcn_stack_bwd_s3f; c2_L3: the
     single-launch entry with three conv layers' dW in the kernel and the in_proj weight gradient
