@@ -1,0 +1,77 @@
+"""GPU parity over the reference sweep's model space (src/lesion_gnn/scripts/sweep.py:122-143):
+GAT with layer_size in {32, 64, 128, 256, 512}, num_layers in [1, 8], heads in {1, 2, 4, 8}; GIN
+with the same widths and depths. Every model of a grid point is checked against the CPU oracle
+(fp32, dropout 0 so the two runs draw nothing) for one training step: logits, loss and every
+parameter gradient, tolerances as tests/test_gpu_gat.py. The points cover each kernel family a
+configuration can select: zero convs (num_layers = 1), the tile kernels (widths <= 128), the
+wide split-3 GEMMs (256, 512), per-row and row-pipelined GAT kernels (all head counts, C from 4
+to 512) and deep stacks (8 layers). d_in = 1025 and lognormal graph sizes as the reference
+experiment (configs/config.py:47-65)."""
+import pytest
+import torch
+
+import oracle.pyg_ref as ref
+from lesion_gnn_amd import synth
+from lesion_gnn_amd.models.gat import GAT
+from lesion_gnn_amd.models.gin import GIN
+
+pytestmark = pytest.mark.gpu
+
+D_IN = 1025
+
+
+def batch(seed):
+    return synth.make_batch(24, k=6, d_in=D_IN, seed=seed, sizes="lognormal",
+                            last_channel_class=True)
+
+
+def step(model, b, device):
+    logits = model(b.x.to(device), b.edge_index.to(device), b.batch.to(device), b.num_graphs)
+    loss = torch.nn.functional.cross_entropy(logits, b.y.to(device))
+    model.zero_grad(set_to_none=True)
+    loss.backward()
+    return (logits.detach().cpu(), loss.detach().cpu(),
+            {k: p.grad.detach().cpu() for k, p in model.named_parameters()})
+
+
+def check(ours, oref, b, cuda, tol=1e-4):
+    lo, losso, go = step(ours.to(cuda).train(), b, cuda)
+    lr_, lossr, gr = step(oref.train(), b, "cpu")
+    scale = max(1.0, lr_.abs().max().item())
+    torch.testing.assert_close(lo, lr_, rtol=0, atol=tol * scale)
+    torch.testing.assert_close(losso, lossr, rtol=10 * tol, atol=1e-6)
+    assert set(go) == set(gr)
+    for k in gr:
+        s = gr[k].abs().max().item()
+        torch.testing.assert_close(go[k], gr[k], rtol=0, atol=max(tol * s, 1e-6),
+                                   msg=lambda m: f"{k}: {m}")
+
+
+GAT_POINTS = [(w, n, h) for w, n, h in [
+    (32, 1, 1), (32, 2, 8), (32, 3, 2), (32, 8, 4), (64, 2, 4), (64, 3, 2), (64, 5, 8),
+    (64, 8, 1), (128, 2, 1), (128, 4, 2), (128, 4, 4), (128, 8, 8), (256, 2, 4), (256, 3, 8),
+    (256, 4, 2), (256, 6, 1), (512, 2, 2), (512, 3, 4), (512, 4, 8), (512, 2, 1), (512, 1, 4)]]
+
+
+@pytest.mark.parametrize("width,num_layers,heads", GAT_POINTS)
+def test_gat_sweep_point(cuda, width, num_layers, heads):
+    torch.manual_seed(1234)
+    hidden = [width] * num_layers
+    ours = GAT(D_IN, hidden, 5, heads=heads, dropout=0.0)
+    oref = ref.GAT(D_IN, hidden, 5, heads=heads, dropout=0.0)
+    oref.load_state_dict(ours.state_dict())
+    check(ours, oref, batch(60 + num_layers), cuda)
+
+
+GIN_POINTS = [(32, 1), (32, 3), (32, 8), (64, 2), (64, 5), (128, 1), (128, 2), (128, 4),
+              (128, 8), (256, 2), (256, 3), (256, 8), (512, 2), (512, 4)]
+
+
+@pytest.mark.parametrize("width,num_layers", GIN_POINTS)
+def test_gin_sweep_point(cuda, width, num_layers):
+    torch.manual_seed(1234)
+    hidden = [width] * num_layers
+    ours = GIN(D_IN, hidden, 5, dropout=0.0)
+    oref = ref.GIN(D_IN, hidden, 5, dropout=0.0)
+    oref.load_state_dict(ours.state_dict())
+    check(ours, oref, batch(80 + num_layers), cuda)
