@@ -75,3 +75,28 @@ def test_gin_sweep_point(cuda, width, num_layers):
     oref = ref.GIN(D_IN, hidden, 5, dropout=0.0)
     oref.load_state_dict(ours.state_dict())
     check(ours, oref, batch(80 + num_layers), cuda)
+
+
+@pytest.mark.parametrize("arch,width,num_layers,heads,p", [
+    ("gat", 64, 5, 8, 0.7), ("gat", 256, 3, 2, 0.1), ("gat", 32, 2, 1, 0.9),
+    ("gin", 256, 3, 0, 0.5), ("gin", 128, 8, 0, 0.3), ("gin", 512, 2, 0, 0.8)])
+def test_sweep_point_compiled_with_dropout(cuda, arch, width, num_layers, heads, p):
+    """The sweep compiles its models (COMPILE, sweep.py:133,142) and draws dropout in
+    [0.1, 0.9]: the compiled model (one graph, fullgraph=True) matches the eager one bit for bit
+    from the same generator state."""
+    import copy
+
+    torch.manual_seed(1234)
+    hidden = [width] * num_layers
+    m = GAT(D_IN, hidden, 5, heads=heads, dropout=p) if arch == "gat" else \
+        GIN(D_IN, hidden, 5, dropout=p)
+    eager, comp = copy.deepcopy(m).to(cuda), copy.deepcopy(m).to(cuda)
+    torch._dynamo.reset()
+    compiled = torch.compile(comp, dynamic=True, fullgraph=True)
+    b = batch(90 + num_layers)
+    lc, _, gc = step(compiled.train(), b, cuda)
+    le, _, ge = step(eager.train(), b, cuda)
+    assert torch.equal(lc, le), (lc - le).abs().max()
+    gc = {k.replace("_orig_mod.", ""): v for k, v in gc.items()}
+    for k in ge:
+        assert torch.equal(gc[k], ge[k]), k
