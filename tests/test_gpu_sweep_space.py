@@ -100,3 +100,25 @@ def test_sweep_point_compiled_with_dropout(cuda, arch, width, num_layers, heads,
     gc = {k.replace("_orig_mod.", ""): v for k, v in gc.items()}
     for k in ge:
         assert torch.equal(gc[k], ge[k]), k
+
+
+GCN_POINTS = [(32, 1, "fixed"), (64, 2, "fixed"), (128, 3, "fixed"), (128, 4, "fixed"),
+              (128, 5, "fixed"), (128, 8, "fixed"), (256, 3, "fixed"), (128, 3, "lognormal"),
+              (128, 4, "lognormal"), (64, 6, "lognormal"), (512, 2, "lognormal")]
+
+
+@pytest.mark.parametrize("width,num_layers,sizes", GCN_POINTS)
+def test_gcn_depth_width_point(cuda, width, num_layers, sizes):
+    """The GCN model (the benchmark's, on the GIN skeleton) over the same widths and depths:
+    tile-aligned graphs take the fused stacks (one to three convs, the in_proj GEMM outside the
+    fused backward at three), deeper stacks the layer-major split-3 backward, wide layers the
+    split-3 dense GEMMs; log-normal graphs the open-tile paths."""
+    from lesion_gnn_amd.models.gcn import GCN
+
+    torch.manual_seed(1234)
+    hidden = [width] * num_layers
+    ours = GCN(128, hidden, 5, 0.0)
+    oref = ref.GCN(128, hidden, 5, 0.0)
+    oref.load_state_dict(ours.state_dict())
+    b = synth.make_batch(32, n=64, k=8, d_in=128, seed=100 + num_layers, sizes=sizes)
+    check(ours, oref, b, cuda)
