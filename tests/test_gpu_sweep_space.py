@@ -122,3 +122,37 @@ def test_gcn_depth_width_point(cuda, width, num_layers, sizes):
     oref.load_state_dict(ours.state_dict())
     b = synth.make_batch(32, n=64, k=8, d_in=128, seed=100 + num_layers, sizes=sizes)
     check(ours, oref, b, cuda)
+
+
+@pytest.mark.parametrize("arch,hidden,classes,sizes", [
+    ("gcn", [128] * 3, 5, "fixed"), ("gcn", [128] * 4, 5, "fixed"), ("gcn", [64] * 3, 5, "lognormal"),
+    ("gin", [128] * 3, 5, "fixed"), ("gin", [256] * 2, 1, "lognormal"),
+    ("gat", [128] * 4, 1, "lognormal"), ("gat", [64] * 3, 5, "fixed")])
+def test_inference_under_no_grad(cuda, arch, hidden, classes, sizes):
+    """validation_step / test_step run the model in eval mode under no_grad (models/base.py):
+    the forward-only paths (no saved activations, no backward planes) against the oracle, after
+    one training step moved GIN's BatchNorm running statistics."""
+    from lesion_gnn_amd.models.gcn import GCN
+
+    torch.manual_seed(1234)
+    d_in = 128 if arch == "gcn" else D_IN
+    if arch == "gcn":
+        ours, oref = GCN(d_in, hidden, classes, 0.0), ref.GCN(d_in, hidden, classes, 0.0)
+    elif arch == "gin":
+        ours, oref = GIN(d_in, hidden, classes, 0.0), ref.GIN(d_in, hidden, classes, 0.0)
+    else:
+        ours = GAT(d_in, hidden, classes, heads=4, dropout=0.0)
+        oref = ref.GAT(d_in, hidden, classes, heads=4, dropout=0.0)
+    oref.load_state_dict(ours.state_dict())
+    ours = ours.to(cuda)
+    b = synth.make_batch(32, n=64, k=8, d_in=d_in, seed=120, sizes=sizes,
+                         last_channel_class=d_in > 128)
+    if arch == "gin":  # move the running statistics first (train mode, one step each side)
+        for m, dev in ((ours, cuda), (oref, "cpu")):
+            out = m.train()(b.x.to(dev), b.edge_index.to(dev), b.batch.to(dev), b.num_graphs)
+            out.sum().backward()
+    with torch.no_grad():
+        lo = ours.eval()(b.x.to(cuda), b.edge_index.to(cuda), b.batch.to(cuda), b.num_graphs)
+        lr_ = oref.eval()(b.x, b.edge_index, b.batch, b.num_graphs)
+    scale = max(1.0, lr_.abs().max().item())
+    torch.testing.assert_close(lo.cpu(), lr_, rtol=0, atol=1e-4 * scale)
