@@ -11,8 +11,9 @@ the logits, loss and every parameter gradient are compared.
   refcfg the reference experiment (configs/config.py:52-65): GAT [128]*4, heads 2, dropout 0.35,
        torch.compile(dynamic=True), d_in 1025, MSE, 1024 graphs — the oracle replays the step's
        dropout masks (oracle.pyg_ref.DropoutMasks)
-  sweep_* the reference sweep's space off the fused paths (scripts/sweep.py:126-141): GCN with 3
-       convs, GAT [256]*4 heads 8 (dropout 0.35), GIN [512]*4, 1024 graphs each
+  sweep_* the reference sweep's space (scripts/sweep.py:105-141): GCN with 3 convs, GCN at
+       k = 16 and k = 32 (closed tiles up to 2048 CSR entries), GAT [256]*4 heads 8 (dropout
+       0.35), GAT [128]*3 heads 8 (C = 16), GAT [512]*3 heads 4, GIN [512]*4, 1024 graphs each
 
 Bars (written per case): fp32 logits within 1e-4 absolute (× max(1, |logits|) for the add pool,
 whose logits sum 64 rows), gradients within 1e-4 × max|grad| per tensor (floor 1e-6); bf16 (C3)
@@ -28,7 +29,8 @@ pytestmark = pytest.mark.gpu
 
 CASES = [("c2", 1024), ("c3", 1024), ("c3f32", 1024), ("c4", 8192), ("c5k4", 1024),
          ("c5k16", 1024), ("refcfg", 1024), ("sweep_gcn3", 1024), ("sweep_gat256h8", 1024),
-         ("sweep_gin512", 1024)]
+         ("sweep_gin512", 1024), ("sweep_gcn_k16", 1024), ("sweep_gcn_k32", 1024),
+         ("sweep_gat128h8", 1024), ("sweep_gat512h4", 1024)]
 
 
 def run_step(wl, model, b, dev, oracle, masks=None):
