@@ -86,3 +86,31 @@ def test_wide_linear_elu_and_act_bwd(cuda, M, K, N):
               _lib.stream(cuda))
     want_dz = dy * torch.where(y > 0, torch.ones_like(y), y + 1)
     assert torch.equal(dz.cpu(), want_dz)
+
+
+@pytest.mark.parametrize("D", [4, 64, 128, 200, 512])
+def test_spmm_tiles_closed_open_and_partial(cuda, D):
+    """lgnn_spmm stages a 64-row tile in LDS when none of its CSR entries leaves it and gathers
+    from global memory otherwise: a CSR whose tiles are closed (graphs of 64 and 32 nodes), open
+    (a 100-node graph straddles two tiles, one edge reaches the previous tile) and a partial last
+    tile, with weights and a self term, in several feature widths (chunks of 128, a 72-wide tail),
+    against a float64 dense restatement."""
+    from lesion_gnn_amd.graph import Graph
+
+    b = synth.make_batch(7, k=6, d_in=D, seed=17, sizes=[64, 32, 32, 100, 64, 64, 37])
+    ei = b.edge_index.clone()
+    # an edge from node 10 (tile 0) into graph 1 (tile 1): both tiles open; the 100-node graph
+    # straddles tiles 2 and 3
+    assert 64 <= int(ei[1, 400]) < 96
+    ei[0, 400] = 10
+    g = Graph(ei.to(cuda), b.num_nodes)
+    csr = g.csr("gcn")
+    x = torch.randn(b.num_nodes, D, generator=torch.Generator().manual_seed(3))
+    y = ops.spmm_raw(csr.rowptr, csr.col, csr.w, 0.75, x.to(cuda)).cpu().double()
+    rp, cl, w = csr.rowptr.cpu(), csr.col.cpu(), csr.w.cpu().double()
+    A = torch.zeros(b.num_nodes, b.num_nodes, dtype=torch.float64)
+    for i in range(b.num_nodes):
+        for e in range(int(rp[i]), int(rp[i + 1])):
+            A[i, int(cl[e])] += w[e]
+    want = A @ x.double() + 0.75 * x.double()
+    torch.testing.assert_close(y, want, rtol=0, atol=1e-5 * max(1.0, want.abs().max().item()))
