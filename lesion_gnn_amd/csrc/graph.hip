@@ -10,9 +10,10 @@
 //   k_scan_*  rowptr / tptr = exclusive scans of (degree + appended loop), both arrays per
 //             launch; dis = deg^-1/2 for the GCN weights
 //   k_fill    claim slots (same run folding), write (source, edge id)
-//   k_finish  per 256-row block: stage the rows in LDS, append the self loop, sort each row by
-//             edge id (restores edge_index order: the order PyG's scatter_add_ visits a target's
-//             messages in), compute GCN weights, write back coalesced. Run for both CSRs.
+//   k_finish  per 16-row block (one wave): stage the entries in LDS, append the self loop, place
+//             each entry at its rank by edge id within its row (restores edge_index order: the
+//             order PyG's scatter_add_ visits a target's messages in), compute GCN weights,
+//             write back. Run for both CSRs.
 // The result is identical run to run.
 #include "common.h"
 #include "tile_util.h"
@@ -824,7 +825,7 @@ __global__ __launch_bounds__(kScanT) void k_scan(const int32_t* __restrict__ cnt
             blockIdx.y, nblk);
 }
 
-// insertion sort of n (key, val) pairs by key (keys distinct)
+// insertion sort of n (key, val) pairs by key (keys distinct): k_finish's unstaged blocks
 template <typename KP, typename VP>
 __device__ __forceinline__ void sort_row(KP key, VP val, int n) {
   for (int a = 1; a < n; ++a) {
