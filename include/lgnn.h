@@ -621,7 +621,8 @@ int lgnn_adam_step(int n, float* const* params, const float* const* grads, float
  * Fused GCN stack backward on split-3 bf16 MFMA (fp32 accuracy), every layer of a tile in one
  * pass, one launch. Replaces the same autograd chain as lgnn_gcn_stack_bwd (reference path:
  * global_mean/add_pool backward, per conv G = Â^T dZ, dW += G^T H, dH = G W, ELU', and in_proj
- * dW) for tiles with tile_open[t] == 0, L = 1 or 2 convs, every width <= 128 and % 4 == 0.
+ * dW) for tiles with tile_open[t] == 0, L = 1 or 2 convs (3 through the _all / _ce entries
+ * below), every width <= 128 and % 4 == 0.
  *   planes_t: the transposed weight planes of lgnn_weight_planes (all L + 1 layers);
  *   H[0..L]: layer outputs (H[0] = in_proj output); X: model input; widths[0..L+1];
  *   dWp / dbp: per-layer partial slabs with num_partials = lgnn_gcn_stack_bwd_partials(M)

@@ -345,10 +345,11 @@ def head_in_stack_bwd(graph: Graph, L: int, C: int, s3: bool) -> bool:
 def stack_bwd(dp: torch.Tensor | None, x: torch.Tensor, graph: Graph, mean: bool, Ws: list,
               hs: list, ss: list, reducer: list, planes_t: torch.Tensor | None = None,
               head: tuple | None = None, kind: str = "gcn", adjt_t: torch.Tensor | None = None):
-    """Backward of stack_fwd from the pooled-output gradient dp down to in_proj, L = 1 or 2
-    convs, no input gradient. Closed tiles run fused (lgnn_gcn_stack_bwd, one launch); open
-    tiles layer by layer (lgnn_node_linear_bwd_tiles, want_open = 1, accumulate = 1) into the
-    same partial slots. Returns [(dW_l, db_l)] for l = 0..L; the slab reductions are appended
+    """Backward of stack_fwd from the pooled-output gradient dp down to in_proj, L >= 1 convs,
+    no input gradient. Closed tiles run fused (one launch; L = 3 with in_proj's weight gradient
+    as a split-3 GEMM after it, the layer-major split-3 kernels past that); open tiles inside the
+    same launch behind grid barriers, or layer by layer (lgnn_node_linear_bwd_tiles,
+    want_open = 1) into the same partial slots. Returns [(dW_l, db_l)] for l = 0..L; the slab reductions are appended
     to `reducer`. head = (dlogits, W_out) replaces dp where head_in_stack_bwd() allows."""
     csr = graph.csr(kind)
     open_ = graph.tile_open(kind)
