@@ -129,3 +129,20 @@ def test_dropout_seed_reproducible_under_manual_seed():
         m3 = build()
         s1, s2, s3 = (int(m._dropout_rng[0]) for m in (m1, m2, m3))
         assert s1 == s2 and s3 != s1, name
+
+
+def test_dropout_scale_is_fp32_rounding_without_torch_scalars():
+    """dropout.threshold_scale rounds 1 / (1 - p) to fp32 in plain Python (a torch scalar there
+    was a Tensor.item() graph break under torch.compile): equal to numpy's float32 rounding."""
+    import random
+
+    import numpy as np
+
+    from lesion_gnn_amd import dropout
+
+    rnd = random.Random(7)
+    ps = [0.0, 0.1, 0.25, 0.35, 0.5, 0.9, 1 / 3] + [rnd.random() * 0.999 for _ in range(20000)]
+    for p in ps:
+        thr, scale = dropout.threshold_scale(p)
+        assert scale == float(np.float32(1.0 / (1.0 - p))), p
+        assert thr == int(p * 16777216.0)
